@@ -1,0 +1,250 @@
+// a2/a3/a4 — fp32 MFMA GEMM with the SAGE epilogue fused in.
+//
+// Replaces (reference src/model.py):
+//   fc_self(h_self) + fc_neigh(h_neigh), relu, zero-guarded row L2 norm   :98-99,226-235
+//   relu(fc_preagg(h_neigh))                                              :102,151,158,185,198
+//   NodeEmbedding (Linear + bias)                                         :19-24
+//   PredictingLayer hidden_1 (bias)                                       :258
+//   HeteroGraphConv(aggregate='sum'|'mean'|'max') across relations [DGL]  :384-406
+//
+// One launch computes, for a block of BM=128 rows and the full (padded) output
+// width BN, acc = A1·W1ᵀ + T(A2)·W2ᵀ with v_mfma_f32_32x32x2_f32 (exact fp32,
+// one rounding per product — no reduced-precision path exists for f32 on
+// gfx950), then bias, activation, the row L2 norm (the whole row is in the
+// block, reduced across the 32 lanes that hold it) and the cross-relation
+// accumulate into `out`.
+//
+// Tiling: 4 waves, each owning 32 rows × BN columns (BN/32 accumulators of
+// 16 regs).  K is staged through LDS 32 deep; the A and W tiles are stored
+// [row][k] with a 36-float row stride so the per-lane ds_read_b128 of 4
+// consecutive k is bank-conflict free (r·36 mod 64 covers 16 distinct 4-bank
+// slots).  Lane half h of the MFMA consumes k ∈ [16h, 16h+16) of the tile — a
+// permutation of the summation order inside the tile that keeps both operand
+// reads vectorised (fp32 sums stay within the 1e-4 parity tolerance).
+#include "common.hpp"
+#include <cmath>
+
+namespace gnnrec {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128;
+constexpr int BK = 32;
+constexpr int LDSK = 36;  // padded k stride (floats)
+
+struct GemmArgs {
+  const float* A1; int64_t lda1; int64_t K1; const float* W1;
+  const float* A2; int64_t lda2; int64_t K2; const float* W2;
+  const int32_t* a2_deg; int a2_mode;
+  const float* bias;
+  int64_t M; int64_t N;
+  int epilogue; int accum; float out_div;
+  float* out; int64_t ldo;
+  int vecA1, vecA2, vecW1, vecW2;
+};
+
+__device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t ld, int64_t k,
+                                        int64_t K, bool rowok, bool vec) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (!rowok || k >= K) return v;
+  const float* p = base + row * ld + k;
+  if (vec) {
+    v = *reinterpret_cast<const f32x4*>(p);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k + j < K) v[j] = p[j];
+  }
+  return v;
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * LDSK];
+  float* As = smem;
+  float* Ws = smem + BM * LDSK;
+  constexpr int NT = BN / 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+
+#pragma unroll 1
+  for (int seg = 0; seg < 2; ++seg) {
+    const float* A = seg ? g.A2 : g.A1;
+    const float* W = seg ? g.W2 : g.W1;
+    const int64_t K = seg ? g.K2 : g.K1;
+    const int64_t lda = seg ? g.lda2 : g.lda1;
+    const bool vecA = seg ? g.vecA2 : g.vecA1;
+    const bool vecW = seg ? g.vecW2 : g.vecW1;
+    if (K == 0) continue;
+    // per-thread row transform factor for the A rows this thread stages
+    float rowmul[4];
+    bool rowzero[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + i * 256;
+      const int64_t gm = m0 + (idx >> 3);
+      rowmul[i] = 1.f;
+      rowzero[i] = false;
+      if (seg == 1 && g.a2_mode != GNNREC_A2_NONE && gm < g.M) {
+        const int32_t dg = g.a2_deg[gm];
+        if (g.a2_mode == GNNREC_A2_DIV_DEG) rowmul[i] = (float)(dg > 0 ? dg : 1);
+        else rowzero[i] = (dg == 0);
+      }
+    }
+#pragma unroll 1
+    for (int64_t k0 = 0; k0 < K; k0 += BK) {
+      f32x4 ra[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = tid + i * 256;
+        const int64_t gm = m0 + (idx >> 3);
+        const int64_t gk = k0 + (idx & 7) * 4;
+        ra[i] = load4(A, gm, lda, gk, K, gm < g.M, vecA);
+        if (seg == 1) {
+          if (g.a2_mode == GNNREC_A2_DIV_DEG) ra[i] = ra[i] / rowmul[i];
+          else if (rowzero[i]) ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      f32x4 rw[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int idx = tid + i * 256;
+        const int64_t gn = n0 + (idx >> 3);
+        const int64_t gk = k0 + (idx & 7) * 4;
+        rw[i] = load4(W, gn, K, gk, K, gn < g.N, vecW);
+      }
+      __syncthreads();  // previous tile fully consumed
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = tid + i * 256;
+        *reinterpret_cast<f32x4*>(As + (idx >> 3) * LDSK + (idx & 7) * 4) = ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int idx = tid + i * 256;
+        *reinterpret_cast<f32x4*>(Ws + (idx >> 3) * LDSK + (idx & 7) * 4) = rw[i];
+      }
+      __syncthreads();
+      const float* Ar = As + (wave * 32 + r) * LDSK + h * 16;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(Ar + s4 * 4);
+        f32x4 b[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          b[t] = *reinterpret_cast<const f32x4*>(Ws + (t * 32 + r) * LDSK + h * 16 + s4 * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (v&3) + 8(v>>2) + 4h
+  const bool relu = g.epilogue & GNNREC_EPI_RELU;
+  const bool sigm = g.epilogue & GNNREC_EPI_SIGMOID;
+  const bool l2 = g.epilogue & GNNREC_EPI_L2NORM;
+  float bias_t[NT];
+  bool colok[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t col = n0 + t * 32 + r;
+    colok[t] = col < g.N;
+    bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+    float z[NT];
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float x = acc[t][v] + bias_t[t];
+      if (relu) x = fmaxf(x, 0.f);
+      if (sigm) x = 1.f / (1.f + expf(-x));
+      if (!colok[t]) x = 0.f;
+      z[t] = x;
+      ss += x * x;
+    }
+    if (l2) {
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) ss += __shfl_xor(ss, off);
+      float nrm = sqrtf(ss);
+      if (nrm == 0.f) nrm = 1.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) z[t] = z[t] / nrm;
+    }
+    if (row < g.M) {
+      float* orow = g.out + row * g.ldo + n0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (!colok[t]) continue;
+        float* p = orow + t * 32 + r;
+        float y = z[t];
+        if (g.accum == GNNREC_ACC_ADD) y = *p + y;
+        else if (g.accum == GNNREC_ACC_MAX) y = fmaxf(*p, y);
+        if (g.out_div > 0.f) y = y / g.out_div;
+        *p = y;
+      }
+    }
+  }
+}
+
+template <int BN>
+int launch_gemm(const GemmArgs& g, hipStream_t s) {
+  dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.N + BN - 1) / BN));
+  hipLaunchKernelGGL(gemm_f32_kernel<BN>, grid, dim3(256), 0, s, g);
+  return check_launch("gnnrec_gemm_f32");
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
+                               const float* A2, int64_t lda2, int64_t K2, const float* W2,
+                               const int32_t* a2_deg, int a2_mode, const float* bias, int64_t M,
+                               int64_t N, int epilogue, int accum, float out_div, float* out,
+                               int64_t ldo, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "gnnrec_gemm_f32: negative size");
+  if (M == 0 || N == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(out != nullptr && ldo >= N, "gnnrec_gemm_f32: bad output");
+  GNNREC_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1), "gnnrec_gemm_f32: bad A1/W1");
+  GNNREC_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2), "gnnrec_gemm_f32: bad A2/W2");
+  GNNREC_REQUIRE(a2_mode == GNNREC_A2_NONE || a2_deg != nullptr,
+                 "gnnrec_gemm_f32: a2_mode needs a2_deg");
+  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_MAX,
+                 "gnnrec_gemm_f32: unknown accumulate mode %d", accum);
+  GNNREC_REQUIRE(!(epilogue & GNNREC_EPI_L2NORM) || N <= 256,
+                 "gnnrec_gemm_f32: L2NORM needs N <= 256 (got %lld)", (long long)N);
+  GemmArgs g;
+  g.A1 = A1; g.lda1 = lda1; g.K1 = K1; g.W1 = W1;
+  g.A2 = A2; g.lda2 = lda2; g.K2 = K2; g.W2 = W2;
+  g.a2_deg = a2_deg; g.a2_mode = a2_mode; g.bias = bias;
+  g.M = M; g.N = N; g.epilogue = epilogue; g.accum = accum; g.out_div = out_div;
+  g.out = out; g.ldo = ldo;
+  g.vecA1 = (K1 % 4 == 0) && (lda1 % 4 == 0) && aligned16(A1);
+  g.vecA2 = (K2 % 4 == 0) && (lda2 % 4 == 0) && aligned16(A2);
+  g.vecW1 = (K1 % 4 == 0) && aligned16(W1);
+  g.vecW2 = (K2 % 4 == 0) && aligned16(W2);
+  hipStream_t s = as_stream(stream);
+  if (N <= 32) return launch_gemm<32>(g, s);
+  if (N <= 64) return launch_gemm<64>(g, s);
+  if (N <= 128) return launch_gemm<128>(g, s);
+  return launch_gemm<256>(g, s);
+}

@@ -1,0 +1,325 @@
+// a9 — block sampler building blocks (DGL MultiLayerFullNeighborSampler /
+// MultiLayerNeighborSampler + to_block), reference src/sampling.py:153-161,
+// main_inference.py:129-138; DGL 0.5.2 semantics restated:
+//   * frontier = in-edges of the seeds (all of them, or `fanout` of them drawn
+//     without replacement), THEN edges whose eid is excluded are removed
+//     (BlockSampler.sample_blocks removes exclude_eids after sampling);
+//   * to_block: per node type, dst nodes form the prefix of the src nodes, new
+//     src nodes follow.  DGL orders them by first appearance (hash map); this
+//     build orders them ascending by global id (a set-equal, deterministic
+//     choice — see DESIGN.md §parity).
+// Pipeline per relation: count -> exclusive scan -> fill; per node type:
+// mark -> scan -> compact (new src ids) -> relabel (local src ids).
+#include "common.hpp"
+
+namespace gnnrec {
+namespace {
+
+// Fanout choice for one seed: positions 0..deg-1 -> pick k distinct, ascending.
+// Robert Floyd's algorithm keyed on a counter hash (restated in oracle.c).
+constexpr int kMaxFanout = 64;
+
+__device__ int choose_positions(uint64_t key, int64_t v, int64_t deg, int k, int64_t* pos) {
+  int n = 0;
+  for (int64_t j = deg - k; j < deg; ++j) {
+    const uint64_t hsh = hash3(key, (uint64_t)v, (uint64_t)j);
+    const int64_t t = (int64_t)(hsh % (uint64_t)(j + 1));
+    bool dup = false;
+    for (int q = 0; q < n; ++q) dup |= (pos[q] == t);
+    pos[n++] = dup ? j : t;
+  }
+  // insertion sort ascending
+  for (int a = 1; a < n; ++a) {
+    const int64_t x = pos[a];
+    int b = a - 1;
+    while (b >= 0 && pos[b] > x) { pos[b + 1] = pos[b]; --b; }
+    pos[b + 1] = x;
+  }
+  return n;
+}
+
+__global__ void sample_count_kernel(const int64_t* __restrict__ indptr,
+                                    const int64_t* __restrict__ eids,
+                                    const uint8_t* __restrict__ excluded,
+                                    const int64_t* __restrict__ seeds, int64_t n_seeds,
+                                    int64_t fanout, uint64_t key, int64_t* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_seeds) return;
+  const int64_t v = seeds[i];
+  const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+  int64_t c = 0;
+  if (fanout < 0 || deg <= fanout) {
+    if (!excluded) c = deg;
+    else
+      for (int64_t e = beg; e < end; ++e) c += excluded[eids[e]] ? 0 : 1;
+  } else {
+    int64_t pos[kMaxFanout];
+    const int n = choose_positions(key, v, deg, (int)fanout, pos);
+    for (int q = 0; q < n; ++q) c += (excluded && excluded[eids[beg + pos[q]]]) ? 0 : 1;
+  }
+  counts[i] = c;
+}
+
+__global__ void sample_fill_kernel(const int64_t* __restrict__ indptr,
+                                   const int64_t* __restrict__ indices,
+                                   const int64_t* __restrict__ eids,
+                                   const uint8_t* __restrict__ excluded,
+                                   const int64_t* __restrict__ seeds, int64_t n_seeds,
+                                   int64_t fanout, uint64_t key,
+                                   const int64_t* __restrict__ out_indptr,
+                                   int64_t* __restrict__ out_src, int64_t* __restrict__ out_eid) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_seeds) return;
+  const int64_t v = seeds[i];
+  const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+  int64_t o = out_indptr[i];
+  if (fanout < 0 || deg <= fanout) {
+    for (int64_t e = beg; e < end; ++e) {
+      const int64_t id = eids[e];
+      if (excluded && excluded[id]) continue;
+      out_src[o] = indices[e];
+      out_eid[o] = id;
+      ++o;
+    }
+  } else {
+    int64_t pos[kMaxFanout];
+    const int n = choose_positions(key, v, deg, (int)fanout, pos);
+    for (int q = 0; q < n; ++q) {
+      const int64_t e = beg + pos[q];
+      const int64_t id = eids[e];
+      if (excluded && excluded[id]) continue;
+      out_src[o] = indices[e];
+      out_eid[o] = id;
+      ++o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- scan -----
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;  // per thread
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+template <typename T>
+__device__ int64_t block_exclusive_scan(int64_t x, int64_t* sh) {
+  // x: per-thread value; returns exclusive prefix within block; sh[kScanBlock] scratch
+  const int t = threadIdx.x;
+  sh[t] = x;
+  __syncthreads();
+  for (int off = 1; off < kScanBlock; off <<= 1) {
+    const int64_t y = t >= off ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  const int64_t incl = sh[t];
+  return incl - x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanBlock) void scan_tile_sums(const T* __restrict__ in, int64_t n,
+                                                             int64_t* __restrict__ sums) {
+  __shared__ int64_t sh[kScanBlock];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j)
+    if (base + j < n) s += (int64_t)in[base + j];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kScanBlock / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = sh[0];
+}
+
+// single block: exclusive scan of the tile sums in place, total at sums[n]
+__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(int64_t* __restrict__ sums,
+                                                               int64_t n) {
+  __shared__ int64_t sh[kScanBlock];
+  int64_t carry = 0;
+  for (int64_t b = 0; b < n; b += kScanBlock) {
+    const int64_t i = b + threadIdx.x;
+    const int64_t x = i < n ? sums[i] : 0;
+    const int64_t ex = block_exclusive_scan<int64_t>(x, sh);
+    const int64_t tot = sh[kScanBlock - 1];
+    __syncthreads();
+    if (i < n) sums[i] = carry + ex;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[n] = carry;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const T* in, int64_t n,
+                                                                const int64_t* __restrict__ sums,
+                                                                int64_t* out) {
+  __shared__ int64_t sh[kScanBlock];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t vals[kScanItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    vals[j] = base + j < n ? (int64_t)in[base + j] : 0;
+    s += vals[j];
+  }
+  __syncthreads();  // in may alias out: all reads of this tile precede writes
+  int64_t run = block_exclusive_scan<int64_t>(s, sh) + sums[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += vals[j];
+  }
+  const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  if (blockIdx.x == n_tiles - 1 && threadIdx.x == kScanBlock - 1) out[n] = sums[n_tiles];
+}
+
+template <typename T>
+int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStream_t s) {
+  GNNREC_REQUIRE(n >= 0, "scan: negative n");
+  if (n == 0) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(int64_t), s);
+    if (e != hipSuccess) {
+      set_error("scan: %s", hipGetErrorString(e));
+      return GNNREC_EHIP;
+    }
+    return GNNREC_OK;
+  }
+  GNNREC_REQUIRE(workspace != nullptr, "scan: null workspace");
+  const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  int64_t* sums = reinterpret_cast<int64_t*>(workspace);
+  hipLaunchKernelGGL(scan_tile_sums<T>, dim3((unsigned)n_tiles), dim3(kScanBlock), 0, s, in, n,
+                     sums);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanBlock), 0, s, sums, n_tiles);
+  hipLaunchKernelGGL(scan_apply_kernel<T>, dim3((unsigned)n_tiles), dim3(kScanBlock), 0, s, in, n,
+                     sums, out);
+  return check_launch("gnnrec_exclusive_scan");
+}
+
+// -------------------------------------------------------------- relabel ----
+__global__ void mark_ids_kernel(const int64_t* __restrict__ ids, int64_t n,
+                                const int64_t* __restrict__ prefix_pos, int32_t* __restrict__ mark) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  if (prefix_pos[id] < 0) mark[id] = 1;  // benign race: all writers store 1
+}
+
+__global__ void relabel_kernel(const int64_t* __restrict__ ids, int64_t n,
+                               const int64_t* __restrict__ prefix_pos,
+                               const int64_t* __restrict__ rank, int64_t n_prefix,
+                               int64_t* __restrict__ local) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t id = ids[i];
+  const int64_t p = prefix_pos[id];
+  local[i] = p >= 0 ? p : n_prefix + rank[id];
+}
+
+__global__ void compact_kernel(const int32_t* __restrict__ mark, const int64_t* __restrict__ rank,
+                               int64_t n_nodes, int64_t* __restrict__ out_ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  if (mark[i]) out_ids[rank[i]] = i;
+}
+
+__global__ void set_prefix_kernel(const int64_t* __restrict__ prefix, int64_t n,
+                                  int64_t* __restrict__ prefix_pos, int clear) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  prefix_pos[prefix[i]] = clear ? -1 : i;
+}
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+extern "C" int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids,
+                                   const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
+                                   int64_t fanout, uint64_t seed_key, int64_t* counts,
+                                   void* stream) {
+  GNNREC_REQUIRE(n_seeds >= 0, "gnnrec_sample_count: negative n_seeds");
+  GNNREC_REQUIRE(fanout < 0 || fanout <= kMaxFanout, "gnnrec_sample_count: fanout > %d",
+                 kMaxFanout);
+  GNNREC_REQUIRE(!excluded || eids, "gnnrec_sample_count: exclusion needs eids");
+  if (n_seeds == 0) return GNNREC_OK;
+  hipLaunchKernelGGL(sample_count_kernel, dim3(nblk(n_seeds)), dim3(256), 0, as_stream(stream),
+                     indptr, eids, excluded, seeds, n_seeds, fanout, seed_key, counts);
+  return check_launch("gnnrec_sample_count");
+}
+
+extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int64_t* indices,
+                                  const int64_t* eids, const uint8_t* excluded,
+                                  const int64_t* seeds, int64_t n_seeds, int64_t fanout,
+                                  uint64_t seed_key, const int64_t* out_indptr, int64_t* out_src,
+                                  int64_t* out_eid, void* stream) {
+  GNNREC_REQUIRE(n_seeds >= 0, "gnnrec_sample_fill: negative n_seeds");
+  GNNREC_REQUIRE(fanout < 0 || fanout <= kMaxFanout, "gnnrec_sample_fill: fanout > %d",
+                 kMaxFanout);
+  if (n_seeds == 0) return GNNREC_OK;
+  hipLaunchKernelGGL(sample_fill_kernel, dim3(nblk(n_seeds)), dim3(256), 0, as_stream(stream),
+                     indptr, indices, eids, excluded, seeds, n_seeds, fanout, seed_key,
+                     out_indptr, out_src, out_eid);
+  return check_launch("gnnrec_sample_fill");
+}
+
+extern "C" int64_t gnnrec_scan_workspace_bytes(int64_t n) {
+  const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  return (n_tiles + 1) * (int64_t)sizeof(int64_t);
+}
+
+extern "C" int gnnrec_exclusive_scan_i64(const int64_t* in, int64_t n, int64_t* out,
+                                         void* workspace, void* stream) {
+  return exclusive_scan<int64_t>(in, n, out, workspace, as_stream(stream));
+}
+
+extern "C" int gnnrec_exclusive_scan_i32(const int32_t* in, int64_t n, int64_t* out,
+                                         void* workspace, void* stream) {
+  return exclusive_scan<int32_t>(in, n, out, workspace, as_stream(stream));
+}
+
+extern "C" int gnnrec_mark_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos,
+                               int32_t* mark, void* stream) {
+  if (n <= 0) return GNNREC_OK;
+  hipLaunchKernelGGL(mark_ids_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), ids, n,
+                     prefix_pos, mark);
+  return check_launch("gnnrec_mark_ids");
+}
+
+extern "C" int gnnrec_relabel_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos,
+                                  const int64_t* rank, int64_t n_prefix, int64_t* local,
+                                  void* stream) {
+  if (n <= 0) return GNNREC_OK;
+  hipLaunchKernelGGL(relabel_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), ids, n,
+                     prefix_pos, rank, n_prefix, local);
+  return check_launch("gnnrec_relabel_ids");
+}
+
+extern "C" int gnnrec_compact_marked(const int32_t* mark, const int64_t* rank, int64_t n_nodes,
+                                     int64_t* out_ids, void* stream) {
+  if (n_nodes <= 0) return GNNREC_OK;
+  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n_nodes)), dim3(256), 0, as_stream(stream), mark,
+                     rank, n_nodes, out_ids);
+  return check_launch("gnnrec_compact_marked");
+}
+
+extern "C" int gnnrec_set_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos,
+                                     void* stream) {
+  if (n <= 0) return GNNREC_OK;
+  hipLaunchKernelGGL(set_prefix_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), prefix, n,
+                     prefix_pos, 0);
+  return check_launch("gnnrec_set_prefix_pos");
+}
+
+extern "C" int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos,
+                                       void* stream) {
+  if (n <= 0) return GNNREC_OK;
+  hipLaunchKernelGGL(set_prefix_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), prefix, n,
+                     prefix_pos, 1);
+  return check_launch("gnnrec_clear_prefix_pos");
+}

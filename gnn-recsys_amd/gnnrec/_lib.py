@@ -1,0 +1,115 @@
+"""Loader for libgnnrec.so — the C ABI declared in include/gnnrec.h.
+
+The library is the product: there is no CPU or eager-PyTorch fallback.  If it
+is missing or cannot be loaded every op raises ``GnnrecLibraryError``.
+
+torch is imported first on purpose: torch ROCm ships its own libamdhip64
+(soname libamdhip64.so.7) and libgnnrec.so's NEEDED entry resolves to that
+already-loaded copy, so both share one HIP runtime, one device context and
+torch's streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GNNREC_LIB", os.path.join(_HERE, "libgnnrec.so"))
+
+# status codes / enums (mirror include/gnnrec.h)
+OK = 0
+REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
+SPMM_EMPTY_NEGINF = 1
+EPI_RELU, EPI_L2NORM, EPI_SIGMOID = 1, 2, 4
+ACC_STORE, ACC_ADD, ACC_MAX = 0, 1, 2
+A2_NONE, A2_DIV_DEG, A2_ZERO_DEG = 0, 1, 2
+
+
+class GnnrecLibraryError(RuntimeError):
+    pass
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_INT = ctypes.c_int
+_F32 = ctypes.c_float
+
+# name -> (restype, argtypes); every symbol declared in include/gnnrec.h
+SIGNATURES = {
+    "gnnrec_version": (_INT, []),
+    "gnnrec_last_error": (ctypes.c_char_p, []),
+    "gnnrec_spmm_csr_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64, _P]),
+    "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P,
+                               _I64, _I64, _INT, _INT, _F32, _P, _I64, _P]),
+    "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),
+    "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
+    "gnnrec_sample_fill": (_INT, [_P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P, _P, _P]),
+    "gnnrec_scan_workspace_bytes": (_I64, [_I64]),
+    "gnnrec_exclusive_scan_i64": (_INT, [_P, _I64, _P, _P, _P]),
+    "gnnrec_exclusive_scan_i32": (_INT, [_P, _I64, _P, _P, _P]),
+    "gnnrec_mark_ids": (_INT, [_P, _I64, _P, _P, _P]),
+    "gnnrec_relabel_ids": (_INT, [_P, _I64, _P, _P, _I64, _P, _P]),
+    "gnnrec_compact_marked": (_INT, [_P, _P, _I64, _P, _P]),
+    "gnnrec_set_prefix_pos": (_INT, [_P, _I64, _P, _P]),
+    "gnnrec_clear_prefix_pos": (_INT, [_P, _I64, _P, _P]),
+    "gnnrec_synth_edges": (_INT, [_U64, _I64, _I64, _I64, _I64, _P, _P, _P, _P]),
+}
+
+_lib = None
+_load_error = None
+
+
+def load() -> ctypes.CDLL:
+    """Return the loaded library, raising GnnrecLibraryError if unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise GnnrecLibraryError(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = (f"libgnnrec.so not found at {LIB_PATH}; build it with "
+                       f"`make -C gnn-recsys_amd/csrc` (or __graft_entry__.build()). "
+                       f"There is no fallback path.")
+        raise GnnrecLibraryError(_load_error)
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        _load_error = f"failed to load {LIB_PATH}: {exc}"
+        raise GnnrecLibraryError(_load_error) from exc
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except GnnrecLibraryError:
+        return False
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        msg = load().gnnrec_last_error().decode(errors="replace")
+        if rc == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg} (status {rc})")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (0 for None)."""
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

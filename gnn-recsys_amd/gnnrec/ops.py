@@ -1,0 +1,260 @@
+"""Torch-facing wrappers over the gnnrec C ABI (include/gnnrec.h).
+
+Each function validates shapes/dtypes/devices on the host, allocates the output
+with torch (device memory plumbing only) and launches the HIP kernel on the
+current HIP stream.  There is no fallback: a missing library or a CPU tensor is
+an error.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+
+REDUCE = {"sum": _lib.REDUCE_SUM, "mean": _lib.REDUCE_MEAN, "max": _lib.REDUCE_MAX}
+ACCUM = {"store": _lib.ACC_STORE, "add": _lib.ACC_ADD, "max": _lib.ACC_MAX}
+
+
+def _dev(t: torch.Tensor, name: str, dtype=None) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor (got {t.device}); "
+                         f"gnnrec has no CPU path")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+
+
+def _rowmajor(t: torch.Tensor, name: str) -> int:
+    """Leading dimension of a 2-D tensor with unit column stride."""
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D (got shape {tuple(t.shape)})")
+    if t.stride(1) != 1 and t.shape[1] > 1:
+        raise ValueError(f"{name} must have unit column stride")
+    return max(t.stride(0), t.shape[1], 1)
+
+
+def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: str = "mean",
+         edge_weight: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+         empty_neginf: bool = False) -> torch.Tensor:
+    """a1: out[v] = reduce_{e in row v} X[indices[e]] (* edge_weight[e]).
+
+    indptr int64 [n_dst+1], indices int32 [E] (local rows of X), X fp32 [n_src, d].
+    """
+    lib = _lib.load()
+    _dev(indptr, "indptr", torch.int64)
+    _dev(indices, "indices", torch.int32)
+    _dev(X, "X", torch.float32)
+    if reduce not in REDUCE:
+        raise KeyError(f"Aggregator reduce {reduce} not recognized.")
+    n_dst = indptr.numel() - 1
+    d = X.shape[1]
+    ldx = _rowmajor(X, "X")
+    if edge_weight is not None:
+        _dev(edge_weight, "edge_weight", torch.float32)
+        if edge_weight.numel() != indices.numel():
+            raise ValueError("edge_weight must have one value per edge")
+        edge_weight = edge_weight.contiguous()
+    if out is None:
+        out = torch.empty((n_dst, d), dtype=torch.float32, device=X.device)
+    else:
+        _dev(out, "out", torch.float32)
+        if tuple(out.shape) != (n_dst, d):
+            raise ValueError(f"out must be [{n_dst}, {d}]")
+    ldo = _rowmajor(out, "out")
+    flags = _lib.SPMM_EMPTY_NEGINF if empty_neginf else 0
+    rc = lib.gnnrec_spmm_csr_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx, n_dst,
+                                 d, REDUCE[reduce], flags, ptr(out), ldo, stream_ptr(X.device))
+    check(rc, "gnnrec_spmm_csr_f32")
+    return out
+
+
+def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
+         W2: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None, *,
+         relu: bool = False, l2norm: bool = False, sigmoid: bool = False,
+         accum: str = "store", out_div: float = 0.0, out: Optional[torch.Tensor] = None,
+         a2_deg: Optional[torch.Tensor] = None, a2_mode: int = _lib.A2_NONE) -> torch.Tensor:
+    """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias).  W are nn.Linear weights [N, K]."""
+    lib = _lib.load()
+    _dev(A1, "A1", torch.float32)
+    _dev(W1, "W1", torch.float32)
+    M, K1 = A1.shape
+    N = W1.shape[0]
+    if W1.shape[1] != K1:
+        raise ValueError(f"W1 shape {tuple(W1.shape)} does not match A1 K={K1}")
+    W1 = W1.contiguous()
+    lda1 = _rowmajor(A1, "A1")
+    K2, lda2 = 0, 1
+    if A2 is not None:
+        _dev(A2, "A2", torch.float32)
+        _dev(W2, "W2", torch.float32)
+        if A2.shape[0] != M or W2.shape[0] != N or W2.shape[1] != A2.shape[1]:
+            raise ValueError("A2/W2 shape mismatch")
+        K2 = A2.shape[1]
+        lda2 = _rowmajor(A2, "A2")
+        W2 = W2.contiguous()
+    if bias is not None:
+        _dev(bias, "bias", torch.float32)
+        bias = bias.contiguous()
+    if a2_mode != _lib.A2_NONE:
+        _dev(a2_deg, "a2_deg", torch.int32)
+    epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0) | (
+        _lib.EPI_SIGMOID if sigmoid else 0)
+    if out is None:
+        if accum != "store":
+            raise ValueError("accumulating gemm needs an out tensor")
+        out = torch.empty((M, N), dtype=torch.float32, device=A1.device)
+    else:
+        _dev(out, "out", torch.float32)
+        if tuple(out.shape) != (M, N):
+            raise ValueError(f"out must be [{M}, {N}]")
+    ldo = _rowmajor(out, "out")
+    rc = lib.gnnrec_gemm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2), ptr(a2_deg),
+                             a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div), ptr(out),
+                             ldo, stream_ptr(A1.device))
+    check(rc, "gnnrec_gemm_f32")
+    return out
+
+
+def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
+              Hd: torch.Tensor) -> torch.Tensor:
+    """a7: cosine of the L2-normalised endpoint rows, one value per edge -> [E]."""
+    lib = _lib.load()
+    _dev(src, "src", torch.int64)
+    _dev(dst, "dst", torch.int64)
+    _dev(Hs, "Hs", torch.float32)
+    _dev(Hd, "Hd", torch.float32)
+    E = src.numel()
+    if dst.numel() != E:
+        raise ValueError("src/dst length mismatch")
+    if Hs.shape[1] != Hd.shape[1]:
+        raise ValueError("endpoint feature sizes differ")
+    out = torch.empty(E, dtype=torch.float32, device=Hs.device)
+    rc = lib.gnnrec_sddmm_cos_f32(ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(Hs),
+                                  _rowmajor(Hs, "Hs"), ptr(Hd), _rowmajor(Hd, "Hd"), Hs.shape[1],
+                                  ptr(out), stream_ptr(Hs.device))
+    check(rc, "gnnrec_sddmm_cos_f32")
+    return out
+
+
+def edge_mlp(src: torch.Tensor, dst: torch.Tensor, P: torch.Tensor, Q: torch.Tensor,
+             W2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor) -> torch.Tensor:
+    """a8 tail: sigmoid(w3·relu(W2·relu(P[src]+Q[dst]) + b2) + b3) -> [E]."""
+    lib = _lib.load()
+    for t, n in ((P, "P"), (Q, "Q"), (W2, "W2"), (b2, "b2"), (w3, "w3"), (b3, "b3")):
+        _dev(t, n, torch.float32)
+    _dev(src, "src", torch.int64)
+    _dev(dst, "dst", torch.int64)
+    if P.shape[1] != 128 or Q.shape[1] != 128 or tuple(W2.shape) != (32, 128):
+        raise ValueError("edge_mlp expects the reference's 128/32 hidden sizes")
+    P, Q, W2 = P.contiguous(), Q.contiguous(), W2.contiguous()
+    E = src.numel()
+    out = torch.empty(E, dtype=torch.float32, device=P.device)
+    rc = lib.gnnrec_edge_mlp_f32(ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(P), ptr(Q),
+                                 ptr(W2), ptr(b2.contiguous()), ptr(w3.contiguous()),
+                                 ptr(b3.contiguous()), ptr(out), stream_ptr(P.device))
+    check(rc, "gnnrec_edge_mlp_f32")
+    return out
+
+
+def synth_edges(seed: int, e0: int, n: int, n_u: int, n_i: int, device,
+                zipf_cdf: Optional[torch.Tensor] = None):
+    """Counter-hash bipartite edges [e0, e0+n) -> (u int32 [n], i int32 [n])."""
+    lib = _lib.load()
+    u = torch.empty(n, dtype=torch.int32, device=device)
+    i = torch.empty(n, dtype=torch.int32, device=device)
+    if zipf_cdf is not None:
+        _dev(zipf_cdf, "zipf_cdf", torch.float64)
+    rc = lib.gnnrec_synth_edges(seed & 0xFFFFFFFFFFFFFFFF, e0, n, n_u, n_i, ptr(zipf_cdf), ptr(u),
+                                ptr(i), stream_ptr(u.device))
+    check(rc, "gnnrec_synth_edges")
+    return u, i
+
+
+def exclusive_scan(x: torch.Tensor) -> torch.Tensor:
+    """[n] int32/int64 -> [n+1] int64 exclusive prefix sums (last = total)."""
+    lib = _lib.load()
+    _dev(x, "x")
+    n = x.numel()
+    out = torch.empty(n + 1, dtype=torch.int64, device=x.device)
+    ws = torch.empty(max(1, (lib.gnnrec_scan_workspace_bytes(n) + 7) // 8), dtype=torch.int64,
+                     device=x.device)
+    x = x.contiguous()
+    if x.dtype == torch.int64:
+        rc = lib.gnnrec_exclusive_scan_i64(ptr(x), n, ptr(out), ptr(ws), stream_ptr(x.device))
+    elif x.dtype == torch.int32:
+        rc = lib.gnnrec_exclusive_scan_i32(ptr(x), n, ptr(out), ptr(ws), stream_ptr(x.device))
+    else:
+        raise ValueError("exclusive_scan supports int32/int64")
+    check(rc, "gnnrec_exclusive_scan")
+    return out
+
+
+def sample_neighbors(indptr, indices, eids, seeds, fanout: int, seed_key: int = 0,
+                     excluded: Optional[torch.Tensor] = None):
+    """a9: in-edges of `seeds` (all, or `fanout` without replacement), minus excluded eids.
+
+    Returns (out_indptr [n_seeds+1], src global ids [E'], eids [E'])."""
+    lib = _lib.load()
+    for t, n in ((indptr, "indptr"), (indices, "indices"), (eids, "eids"), (seeds, "seeds")):
+        _dev(t, n, torch.int64)
+    if excluded is not None:
+        _dev(excluded, "excluded", torch.uint8)
+    s = stream_ptr(seeds.device)
+    n = seeds.numel()
+    fan = -1 if fanout is None or fanout < 0 else int(fanout)
+    key = seed_key & 0xFFFFFFFFFFFFFFFF
+    counts = torch.empty(n, dtype=torch.int64, device=seeds.device)
+    check(lib.gnnrec_sample_count(ptr(indptr), ptr(eids), ptr(excluded), ptr(seeds), n, fan, key,
+                                  ptr(counts), s), "gnnrec_sample_count")
+    out_indptr = exclusive_scan(counts)
+    total = int(out_indptr[-1].item())  # size readback (the sampler's one host sync)
+    out_src = torch.empty(total, dtype=torch.int64, device=seeds.device)
+    out_eid = torch.empty(total, dtype=torch.int64, device=seeds.device)
+    check(lib.gnnrec_sample_fill(ptr(indptr), ptr(indices), ptr(eids), ptr(excluded), ptr(seeds),
+                                 n, fan, key, ptr(out_indptr), ptr(out_src), ptr(out_eid), s),
+          "gnnrec_sample_fill")
+    return out_indptr, out_src, out_eid
+
+
+class Relabeler:
+    """Per-node-type scratch for to_block relabelling (mark array + prefix map).
+
+    Keeps two arrays of size n_nodes resident on the device (reset after each
+    use by touching only the ids that were set)."""
+
+    def __init__(self, n_nodes: int, device):
+        self.n_nodes = n_nodes
+        self.prefix_pos = torch.full((n_nodes,), -1, dtype=torch.int64, device=device)
+        self.mark = torch.zeros(n_nodes, dtype=torch.int32, device=device)
+
+    def relabel(self, prefix: torch.Tensor, id_lists):
+        """prefix: dst ids [n_p]; id_lists: list of global src id tensors.
+
+        Returns (src_nodes [n_p + n_new] global ids, [local ids per list])."""
+        lib = _lib.load()
+        s = stream_ptr(prefix.device)
+        n_p = prefix.numel()
+        check(lib.gnnrec_set_prefix_pos(ptr(prefix), n_p, ptr(self.prefix_pos), s), "set_prefix")
+        for ids in id_lists:
+            check(lib.gnnrec_mark_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(self.mark),
+                                      s), "mark_ids")
+        rank = exclusive_scan(self.mark)
+        n_new = int(rank[-1].item())
+        src_nodes = torch.empty(n_p + n_new, dtype=torch.int64, device=prefix.device)
+        src_nodes[:n_p] = prefix
+        check(lib.gnnrec_compact_marked(ptr(self.mark), ptr(rank), self.n_nodes,
+                                        ptr(src_nodes[n_p:]) if n_new else 0, s), "compact")
+        locals_ = []
+        for ids in id_lists:
+            loc = torch.empty(ids.numel(), dtype=torch.int64, device=prefix.device)
+            check(lib.gnnrec_relabel_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(rank),
+                                         n_p, ptr(loc), s), "relabel")
+            locals_.append(loc)
+        # reset scratch: prefix map by the prefix ids, mark by the new ids
+        check(lib.gnnrec_clear_prefix_pos(ptr(prefix), n_p, ptr(self.prefix_pos), s),
+              "clear_prefix")
+        if n_new:
+            self.mark.index_fill_(0, src_nodes[n_p:], 0)
+        return src_nodes, locals_

@@ -1,0 +1,158 @@
+/*
+ * gnnrec.h — C ABI of the MI355X-native message-passing path for the
+ * hieucnm/GNN-RecSys user–item GNN.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and
+ * returns an int status (GNNREC_OK == 0).  On failure gnnrec_last_error()
+ * returns a thread-local message.  All data pointers are DEVICE pointers,
+ * owned by the caller; outputs are preallocated by the caller (the same
+ * contract as DGL's `_CAPI_DGLKernelSpMM`, whose outputs are allocated in
+ * Python before the call).  `stream` is a hipStream_t passed as void*
+ * (NULL = legacy default stream).  No entry point allocates, synchronises
+ * or blocks the host unless its comment says so, so every call can be
+ * captured into a hipGraph.
+ *
+ * Reference interfaces replaced (DGL 0.5.2 is the reference's pinned
+ * third-party dependency, requirements.txt:2; it is not vendored):
+ *   - gnnrec_spmm_csr_f32      <- graph.update_all(fn.copy_src|fn.u_mul_e,
+ *                                 fn.mean|fn.max)  src/model.py:143-208
+ *                                 (DGL gspmm -> _CAPI_DGLKernelSpMM)
+ *   - gnnrec_gemm_f32          <- nn.Linear fc_self/fc_neigh/fc_preagg +
+ *                                 relu + zero-guarded L2 norm + HeteroGraphConv
+ *                                 aggregate, src/model.py:98-102,151,226-235,
+ *                                 384-406; NodeEmbedding src/model.py:19-24;
+ *                                 PredictingLayer src/model.py:258-271
+ *   - gnnrec_sddmm_cos_f32     <- CosinePrediction.forward, F.normalize +
+ *                                 apply_edges(fn.u_dot_v) src/model.py:317-327
+ *                                 (DGL gsddmm -> _CAPI_DGLKernelSDDMM)
+ *   - gnnrec_edge_mlp_f32      <- PredictingModule.forward src/model.py:290-305
+ *   - gnnrec_sample_*          <- dgl.dataloading.MultiLayer{Full,}Neighbor-
+ *                                 Sampler / to_block, src/sampling.py:153-161
+ *                                 (_CAPI_DGLSampleNeighbors, _CAPI_DGLToBlock)
+ *   - gnnrec_synth_edges       <- (no reference counterpart: synthetic graph
+ *                                 generator for the benchmark shapes)
+ */
+#ifndef GNNREC_H_
+#define GNNREC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNNREC_OK 0
+#define GNNREC_EINVAL 1 /* bad argument (shape, null pointer, unsupported mode) */
+#define GNNREC_EHIP 2   /* HIP runtime error (launch failure, ...) */
+
+/* reduce op for gnnrec_spmm_csr_f32 (DGL fn.sum / fn.mean / fn.max) */
+#define GNNREC_REDUCE_SUM 0
+#define GNNREC_REDUCE_MEAN 1
+#define GNNREC_REDUCE_MAX 2
+
+/* gnnrec_spmm_csr_f32 flags */
+#define GNNREC_SPMM_EMPTY_NEGINF 1 /* MAX: leave rows with no edge at -inf (partial
+                                      maxima that are max-reduced across ranks) */
+
+/* gnnrec_gemm_f32 epilogue bits */
+#define GNNREC_EPI_RELU 1
+#define GNNREC_EPI_L2NORM 2 /* z /= ||z||_2, rows with ||z|| == 0 left unchanged */
+#define GNNREC_EPI_SIGMOID 4
+
+/* gnnrec_gemm_f32 accumulate modes (HeteroGraphConv aggregate across relations) */
+#define GNNREC_ACC_STORE 0
+#define GNNREC_ACC_ADD 1
+#define GNNREC_ACC_MAX 2
+
+/* gnnrec_gemm_f32 row transform applied to A2 rows before the product */
+#define GNNREC_A2_NONE 0
+#define GNNREC_A2_DIV_DEG 1  /* row / max(deg,1)   (mean of a summed neighbourhood) */
+#define GNNREC_A2_ZERO_DEG 2 /* row := 0 where deg == 0 (max of an empty neighbourhood) */
+
+/* ---- library ---------------------------------------------------------- */
+int gnnrec_version(void);
+const char* gnnrec_last_error(void);
+
+/* ---- a1: gather + aggregate over a dst-major CSR (K1-K3) ----------------
+ * out[v, :] = reduce_{e in [indptr[v], indptr[v+1])} X[indices[e], :] * (ew ? ew[e] : 1)
+ * MEAN divides the sum by max(deg,1); MAX of an empty row is 0 (or -inf with
+ * GNNREC_SPMM_EMPTY_NEGINF).  Per-row reduction order is fixed, so results are
+ * bitwise reproducible run to run.  indices are LOCAL row ids of X.
+ * Replaces graph.update_all(...) at src/model.py:143-208. */
+int gnnrec_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                        const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
+                        int flags, float* out, int64_t ldo, void* stream);
+
+/* ---- a2/a3/a4: fp32 MFMA GEMM with fused SAGE epilogue (K4, K7) ---------
+ * acc[m,n] = sum_k A1[m,k] W1[n,k] + sum_k T(A2)[m,k] W2[n,k]   (W row-major [N,K] = nn.Linear.weight)
+ * z = epi(acc + bias)      epi: relu / sigmoid, then optional row L2 norm
+ * out = accumulate(out, z) (store | add | max), then out /= out_div if out_div > 0.
+ * A2/W2 may be NULL with K2 == 0.  bias may be NULL.  N <= 256 when L2NORM.
+ * Replaces fc_self(h_self)+fc_neigh(h_neigh), relu, norm (src/model.py:226-235) and
+ * HeteroGraphConv's cross-relation sum/mean/max (src/model.py:384-406). */
+int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
+                    const float* A2, int64_t lda2, int64_t K2, const float* W2,
+                    const int32_t* a2_deg, int a2_mode, const float* bias,
+                    int64_t M, int64_t N, int epilogue, int accum, float out_div,
+                    float* out, int64_t ldo, void* stream);
+
+/* ---- a7: cosine edge score (K5) ------------------------------------------
+ * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >
+ * Replaces CosinePrediction.forward, src/model.py:317-327. */
+int gnnrec_sddmm_cos_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
+                         const float* Hs, int64_t lds, const float* Hd, int64_t ldd, int64_t d,
+                         float* out, void* stream);
+
+/* ---- a8: PredictingLayer over gathered edge endpoints (K6) ---------------
+ * P = Hs W1a^T + b1 and Q = Hd W1b^T are precomputed per node by gnnrec_gemm_f32
+ * (W1 = [W1a | W1b], hidden_1 of PredictingLayer).  Per edge:
+ * out[e] = sigmoid( w3 . relu( W2 relu(P[src[e]] + Q[dst[e]]) + b2 ) + b3 )
+ * with hidden sizes fixed by the reference at 128 and 32 (src/model.py:258-260). */
+int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
+                        const float* P, const float* Q, const float* W2, const float* b2,
+                        const float* w3, const float* b3, float* out, void* stream);
+
+/* ---- a9: block sampler (K8) ----------------------------------------------
+ * Per relation, for each seed (dst) v: collect its in-edges from the global
+ * in-CSR (indptr/indices/eids), skipping edges whose eid is marked in
+ * `excluded` (byte per eid, may be NULL), keeping all of them (fanout < 0)
+ * or min(fanout, deg) chosen without replacement by a counter-based RNG
+ * keyed on (seed_key, v).  Two phases: count, then fill at caller offsets. */
+int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids, const uint8_t* excluded,
+                        const int64_t* seeds, int64_t n_seeds, int64_t fanout,
+                        uint64_t seed_key, int64_t* counts, void* stream);
+int gnnrec_sample_fill(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                       const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
+                       int64_t fanout, uint64_t seed_key, const int64_t* out_indptr,
+                       int64_t* out_src, int64_t* out_eid, void* stream);
+/* exclusive prefix sum of n int64 values (in-place allowed); workspace of
+ * gnnrec_scan_workspace_bytes(n) bytes; out[n] receives the total. */
+int64_t gnnrec_scan_workspace_bytes(int64_t n);
+int gnnrec_exclusive_scan_i64(const int64_t* in, int64_t n, int64_t* out, void* workspace,
+                              void* stream);
+int gnnrec_exclusive_scan_i32(const int32_t* in, int64_t n, int64_t* out, void* workspace,
+                              void* stream);
+/* relabel (DGL to_block): mark[id] = 1 for every id in ids (global), then
+ * after a scan of mark, local[i] = n_prefix + rank(ids[i]) unless ids[i] is
+ * one of the dst-prefix nodes (prefix_pos[id] >= 0), which keep their slot. */
+int gnnrec_mark_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos, int32_t* mark,
+                    void* stream);
+int gnnrec_relabel_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos,
+                       const int64_t* rank, int64_t n_prefix, int64_t* local, void* stream);
+int gnnrec_compact_marked(const int32_t* mark, const int64_t* rank, int64_t n_nodes,
+                          int64_t* out_ids, void* stream);
+int gnnrec_set_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
+int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
+
+/* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
+ * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),
+ * item() uniform (zipf_s == 0) or inverse-CDF Zipf over the table `zipf_cdf`
+ * (n_i doubles, NULL for uniform).  h = splitmix64-based counter hash.
+ * Reproduced bit-exactly by oracle/oracle.c. */
+int gnnrec_synth_edges(uint64_t seed, int64_t e0, int64_t n, int64_t n_u, int64_t n_i,
+                       const double* zipf_cdf, int32_t* u, int32_t* i, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNNREC_H_ */
