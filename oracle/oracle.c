@@ -1,0 +1,182 @@
+/*
+ * oracle.c — CPU restatement of the reference's hot path (TEST INFRASTRUCTURE).
+ *
+ * This file is the parity checker and the CPU baseline, never the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+ * it.  The product (gnn-recsys_amd/) never links or calls it.
+ *
+ * What it restates:
+ *   oracle_spmm_csr_f32     DGL 0.5.2 CPU SpMM over a dst-major CSR as used by
+ *                           graph.update_all(fn.copy_src|fn.u_mul_e, fn.mean|fn.max)
+ *                           at reference src/model.py:143-208: row-parallel
+ *                           OpenMP loop over dst rows, sequential neighbour loop,
+ *                           inner feature loop, fp32 accumulator (DGL's
+ *                           SpMMSumCsr / SpMMCmpCsr shape).  mean = sum/max(deg,1),
+ *                           max of an empty row = 0.
+ *   oracle_synth_edges      the benchmark generator (gnn-recsys_amd/csrc/synth.hip),
+ *                           bit for bit.
+ *   oracle_sample_*         DGL MultiLayer{Full,}NeighborSampler frontier +
+ *                           exclusion (reference src/sampling.py:153-161): all
+ *                           in-edges, or `fanout` of them by Floyd's algorithm on
+ *                           the same counter hash as the HIP sampler, minus
+ *                           excluded eids (removed after sampling, as DGL's
+ *                           BlockSampler.sample_blocks does).
+ * Parity status: the SpMM semantics are pinned by golden vectors produced by
+ * the reference's own ConvLayer code (tests/golden/make_golden.py); the
+ * sampler's RNG is build-defined (DGL's is not reproducible offline) and is
+ * pinned structurally (subset / count / no-duplicate checks) — see DESIGN.md.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t oracle_hash3(uint64_t seed, uint64_t a, uint64_t b) {
+  return mix64(mix64(seed ^ mix64(a)) ^ (b * 0xD1B54A32D192ED03ull));
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* reduce: 0 sum, 1 mean, 2 max */
+void oracle_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                         const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
+                         float* out, int64_t ldo) {
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t v = 0; v < n_dst; ++v) {
+    float* o = out + v * ldo;
+    const int64_t beg = indptr[v], end = indptr[v + 1];
+    if (reduce == 2) {
+      for (int64_t c = 0; c < d; ++c) o[c] = -INFINITY;
+    } else {
+      for (int64_t c = 0; c < d; ++c) o[c] = 0.f;
+    }
+    for (int64_t e = beg; e < end; ++e) {
+      const float* x = X + (int64_t)indices[e] * ldx;
+      const float w = ew ? ew[e] : 1.f;
+      if (reduce == 2) {
+        for (int64_t c = 0; c < d; ++c) {
+          const float m = ew ? x[c] * w : x[c];
+          o[c] = m > o[c] ? m : o[c];
+        }
+      } else if (ew) {
+        for (int64_t c = 0; c < d; ++c) o[c] += x[c] * w;
+      } else {
+        for (int64_t c = 0; c < d; ++c) o[c] += x[c];
+      }
+    }
+    const int64_t deg = end - beg;
+    if (reduce == 1) {
+      const float dd = (float)(deg > 0 ? deg : 1);
+      for (int64_t c = 0; c < d; ++c) o[c] = o[c] / dd;
+    } else if (reduce == 2 && deg == 0) {
+      for (int64_t c = 0; c < d; ++c) o[c] = 0.f;
+    }
+  }
+}
+
+void oracle_synth_edges(uint64_t seed, int64_t e0, int64_t n, int64_t n_u, int64_t n_i,
+                        const double* cdf, int32_t* u, int32_t* it) {
+#pragma omp parallel for schedule(static)
+  for (int64_t k = 0; k < n; ++k) {
+    const uint64_t e = (uint64_t)(e0 + k);
+    u[k] = (int32_t)(oracle_hash3(seed, e, 0) % (uint64_t)n_u);
+    const uint64_t hi = oracle_hash3(seed, e, 1);
+    if (!cdf) {
+      it[k] = (int32_t)(hi % (uint64_t)n_i);
+    } else {
+      const double x = (double)(hi >> 11) * (1.0 / 9007199254740992.0);
+      int64_t lo = 0, h = n_i - 1;
+      while (lo < h) {
+        const int64_t mid = (lo + h) >> 1;
+        if (cdf[mid] > x) h = mid;
+        else lo = mid + 1;
+      }
+      it[k] = (int32_t)lo;
+    }
+  }
+}
+
+/* Floyd's sampling of k distinct positions in [0, deg), ascending. */
+static int choose_positions(uint64_t key, int64_t v, int64_t deg, int k, int64_t* pos) {
+  int n = 0;
+  for (int64_t j = deg - k; j < deg; ++j) {
+    const int64_t t = (int64_t)(oracle_hash3(key, (uint64_t)v, (uint64_t)j) % (uint64_t)(j + 1));
+    int dup = 0;
+    for (int q = 0; q < n; ++q) dup |= (pos[q] == t);
+    pos[n++] = dup ? j : t;
+  }
+  for (int a = 1; a < n; ++a) {
+    const int64_t x = pos[a];
+    int b = a - 1;
+    while (b >= 0 && pos[b] > x) {
+      pos[b + 1] = pos[b];
+      --b;
+    }
+    pos[b + 1] = x;
+  }
+  return n;
+}
+
+void oracle_sample_count(const int64_t* indptr, const int64_t* eids, const uint8_t* excluded,
+                         const int64_t* seeds, int64_t n_seeds, int64_t fanout, uint64_t key,
+                         int64_t* counts) {
+  for (int64_t i = 0; i < n_seeds; ++i) {
+    const int64_t v = seeds[i];
+    const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+    int64_t c = 0;
+    if (fanout < 0 || deg <= fanout) {
+      for (int64_t e = beg; e < end; ++e) c += (excluded && excluded[eids[e]]) ? 0 : 1;
+    } else {
+      int64_t pos[64];
+      const int n = choose_positions(key, v, deg, (int)fanout, pos);
+      for (int q = 0; q < n; ++q) c += (excluded && excluded[eids[beg + pos[q]]]) ? 0 : 1;
+    }
+    counts[i] = c;
+  }
+}
+
+void oracle_sample_fill(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+                        const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
+                        int64_t fanout, uint64_t key, const int64_t* out_indptr, int64_t* out_src,
+                        int64_t* out_eid) {
+  for (int64_t i = 0; i < n_seeds; ++i) {
+    const int64_t v = seeds[i];
+    const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+    int64_t o = out_indptr[i];
+    if (fanout < 0 || deg <= fanout) {
+      for (int64_t e = beg; e < end; ++e) {
+        if (excluded && excluded[eids[e]]) continue;
+        out_src[o] = indices[e];
+        out_eid[o] = eids[e];
+        ++o;
+      }
+    } else {
+      int64_t pos[64];
+      const int n = choose_positions(key, v, deg, (int)fanout, pos);
+      for (int q = 0; q < n; ++q) {
+        const int64_t e = beg + pos[q];
+        if (excluded && excluded[eids[e]]) continue;
+        out_src[o] = indices[e];
+        out_eid[o] = eids[e];
+        ++o;
+      }
+    }
+  }
+}

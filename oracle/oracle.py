@@ -1,0 +1,340 @@
+"""CPU restatement of the reference's message-passing hot path — TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / the CPU baseline.  The product
+(gnn-recsys_amd/gnnrec) never imports it and has no CPU path.
+
+Layers (each function cites the reference code it restates):
+  * C, via ctypes (oracle/oracle.c -> oracle/_build/liboracle.so):
+      spmm_csr         DGL 0.5.2 CPU SpMM behind update_all (src/model.py:143-208)
+      synth_edges      the benchmark generator, bit-exact with the HIP one
+      sample_neighbors DGL full / fanout neighbour sampling + eid exclusion
+                       (src/sampling.py:153-161), build-defined RNG
+  * numpy (fp32, the reference's precision):
+      conv_layer       ConvLayer.forward (src/model.py:123-237)
+      hetero_conv      DGL HeteroGraphConv semantics around it (src/model.py:384-406)
+      model_full_graph ConvModel.get_repr on one batch holding every node,
+                       preceded by NodeEmbedding (src/model.py:371-421,
+                       src/train/run.py:340-348)
+      cosine_prediction / predicting_module / max_margin_loss
+                       (src/model.py:317-327, 290-305, 256-271, 473-533)
+      to_block         DGL to_block relabel, ascending new-src order
+
+Parity pinning: tests/test_oracle_golden.py checks every numpy/C function above
+against golden vectors produced by running the reference's own src/model.py
+(tests/golden/make_golden.py).  The sampler RNG is build-defined (DGL's is not
+reproducible offline): "parity unpinned" for fanout choices, pinned
+structurally instead.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+USER_ITEM = ("user", "item")
+CONV_AGGREGATORS = ("mean", "mean_nn", "pool_nn", "lstm", "mean_edge", "mean_nn_edge",
+                    "pool_nn_edge", "lstm_edge")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+        L = ctypes.CDLL(LIB_PATH)
+        P, I64, U64, INT = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
+        L.oracle_spmm_csr_f32.argtypes = [P, P, P, P, I64, I64, I64, INT, P, I64]
+        L.oracle_spmm_csr_f32.restype = None
+        L.oracle_synth_edges.argtypes = [U64, I64, I64, I64, I64, P, P, P]
+        L.oracle_synth_edges.restype = None
+        L.oracle_sample_count.argtypes = [P, P, P, P, I64, I64, U64, P]
+        L.oracle_sample_count.restype = None
+        L.oracle_sample_fill.argtypes = [P, P, P, P, P, I64, I64, U64, P, P, P]
+        L.oracle_sample_fill.restype = None
+        L.oracle_hash3.argtypes = [U64, U64, U64]
+        L.oracle_hash3.restype = U64
+        L.oracle_num_threads.restype = INT
+        _lib = L
+    return _lib
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ------------------------------------------------------------------ graph ---
+def csr_from_coo(src: np.ndarray, dst: np.ndarray, n_dst: int):
+    """dst-major CSR with in-row order = eid order (DGL's in-CSR of a COO graph).
+
+    Returns indptr int64 [n_dst+1], indices int32 [E] (src ids), eids int64 [E]."""
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    order = np.argsort(dst, kind="stable")
+    indptr = np.zeros(n_dst + 1, np.int64)
+    np.cumsum(np.bincount(dst, minlength=n_dst), out=indptr[1:])
+    return indptr, src[order].astype(np.int32), order.astype(np.int64)
+
+
+class Graph:
+    """Heterograph restated: COO per canonical etype (reverse relations share
+    the forward eid order, reference src/utils_data.py:205-238)."""
+
+    def __init__(self, num_nodes: Dict[str, int], edges: Dict[Tuple[str, str, str], tuple],
+                 occurrence: Optional[dict] = None):
+        self.num_nodes = dict(num_nodes)
+        self.edges = {ce: (np.asarray(s, np.int64), np.asarray(d, np.int64))
+                      for ce, (s, d) in edges.items()}
+        self.canonical_etypes = list(edges.keys())
+        self.occurrence = dict(occurrence or {})
+        self._csr = {}
+
+    def csr(self, ce):
+        if ce not in self._csr:
+            s, d = self.edges[ce]
+            self._csr[ce] = csr_from_coo(s, d, self.num_nodes[ce[2]])
+        return self._csr[ce]
+
+    def num_edges(self, ce):
+        return self.edges[ce][0].size
+
+
+# ------------------------------------------------------------------- ops ----
+def spmm_csr(indptr, indices, X, reduce: str, ew=None) -> np.ndarray:
+    """DGL 0.5.2 CPU SpMM (fp32 accumulator, sequential neighbour order)."""
+    X = np.ascontiguousarray(X, np.float32)
+    indptr = np.ascontiguousarray(indptr, np.int64)
+    indices = np.ascontiguousarray(indices, np.int32)
+    n_dst = indptr.size - 1
+    d = X.shape[1]
+    out = np.empty((n_dst, d), np.float32)
+    if ew is not None:
+        ew = np.ascontiguousarray(ew, np.float32)
+    red = {"sum": 0, "mean": 1, "max": 2}[reduce]
+    lib().oracle_spmm_csr_f32(_p(indptr), _p(indices), _p(ew), _p(X), d, n_dst, d, red, _p(out), d)
+    return out
+
+
+def relu(x):
+    return np.maximum(x, np.float32(0))
+
+
+def linear(x, W, b=None):
+    y = np.asarray(x, np.float32) @ np.asarray(W, np.float32).T
+    if b is not None:
+        y = y + np.asarray(b, np.float32)
+    return y.astype(np.float32)
+
+
+def l2_normalize_rows_guarded(z):
+    """src/model.py:230-235: z / ||z||, rows with ||z|| == 0 divided by 1."""
+    n = np.linalg.norm(z, axis=1, keepdims=True).astype(np.float32)
+    n = np.where(n == 0, np.float32(1), n)
+    return (z / n).astype(np.float32)
+
+
+def conv_layer(graph: Graph, ce, h_neigh, h_self, w: dict, aggregator_type: str, norm: bool):
+    """ConvLayer.forward, src/model.py:123-237 (eval mode: dropout = identity).
+
+    w: {'fc_self.weight', 'fc_neigh.weight'[, 'fc_preagg.weight']}."""
+    agg = aggregator_type
+    if agg not in CONV_AGGREGATORS:
+        raise KeyError("Aggregator type {} not recognized.".format(agg))
+    if agg.startswith("lstm"):
+        raise NotImplementedError("lstm aggregators are out of scope (SURVEY.md §2 row 1)")
+    if agg in ("mean_nn", "pool_nn", "mean_nn_edge", "pool_nn_edge"):
+        m = relu(linear(h_neigh, w["fc_preagg.weight"]))  # :151,158,185,198
+    else:
+        m = np.asarray(h_neigh, np.float32)
+    indptr, indices, eids = graph.csr(ce)
+    ew = None
+    if agg.endswith("_edge") and ce[0] in USER_ITEM and ce[2] in USER_ITEM:  # :173,186,199
+        ew = graph.occurrence[ce].astype(np.float32)[eids]
+    reduce = "max" if agg.startswith("pool") else "mean"
+    h_n = spmm_csr(indptr, indices, m, reduce, ew)
+    z = relu(linear(h_self, w["fc_self.weight"]) + linear(h_n, w["fc_neigh.weight"]))  # :226-227
+    if norm:
+        z = l2_normalize_rows_guarded(z)
+    return z
+
+
+def hetero_conv(graph: Graph, h: Dict[str, np.ndarray], layer_w: Dict[str, dict],
+                aggregator_type: str, norm: bool, aggregator_hetero: str):
+    """DGL 0.5.2 HeteroGraphConv (restated) around ConvLayer (src/model.py:384-406).
+
+    Relations with no edges, or whose src/dst type has no input, are skipped;
+    outputs of the active relations are stacked per dst type and reduced."""
+    outs: Dict[str, list] = {}
+    for ce in graph.canonical_etypes:
+        s, rel, d = ce
+        if graph.num_edges(ce) == 0 or s not in h or d not in h:
+            continue
+        outs.setdefault(d, []).append(
+            conv_layer(graph, ce, h[s], h[d], layer_w[rel], aggregator_type, norm))
+    res = {}
+    for nt, lst in outs.items():
+        st = np.stack(lst, 0)
+        if aggregator_hetero == "sum":
+            res[nt] = st.sum(0, dtype=np.float32)
+        elif aggregator_hetero == "mean":
+            res[nt] = st.mean(0, dtype=np.float32)
+        elif aggregator_hetero == "max":
+            res[nt] = st.max(0)
+        else:
+            raise KeyError(aggregator_hetero)
+    return res
+
+
+def split_state_dict(sd: Dict[str, np.ndarray]):
+    """state_dict -> (embed {ntype: (W, b)}, layers [{rel: {name: W}}], pred {name: W})."""
+    embed, layers, pred = {}, {}, {}
+    for k, v in sd.items():
+        parts = k.split(".")
+        if parts[0].endswith("_embed"):
+            nt = parts[0][: -len("_embed")]
+            e = embed.setdefault(nt, [None, None])
+            e[0 if parts[-1] == "weight" else 1] = v
+        elif parts[0] == "layers":
+            i, rel = int(parts[1]), parts[3]
+            layers.setdefault(i, {}).setdefault(rel, {})[".".join(parts[4:])] = v
+        elif parts[0] == "pred_fn":
+            pred[".".join(parts[1:])] = v
+    return embed, [layers[i] for i in sorted(layers)], pred
+
+
+def model_full_graph(graph: Graph, feats: Dict[str, np.ndarray], sd: Dict[str, np.ndarray],
+                     aggregator_type: str, aggregator_hetero: str, norm: bool,
+                     embedding_layer: bool):
+    """get_embeddings on one batch holding every node (src/train/run.py:334-348):
+    NodeEmbedding per ntype (src/model.py:19-24) then ConvModel.get_repr
+    (src/model.py:415-421) with the full graph as every block."""
+    embed, layers, _ = split_state_dict(sd)
+    h = {nt: np.asarray(v, np.float32) for nt, v in feats.items()}
+    if embedding_layer:
+        for nt in ("user", "item", "sport"):
+            if nt in h and nt in embed:
+                W, b = embed[nt]
+                h[nt] = linear(h[nt], W, b)
+    for lw in layers:
+        h = hetero_conv(graph, h, lw, aggregator_type, norm, aggregator_hetero)
+    return h
+
+
+def normalize_rows(x, eps=1e-12):
+    """F.normalize(p=2, dim=-1): x / max(||x||, eps)."""
+    n = np.linalg.norm(x, axis=-1, keepdims=True)
+    return (x / np.maximum(n, eps)).astype(np.float32)
+
+
+def cosine_prediction(pair_edges: Dict[tuple, tuple], h: Dict[str, np.ndarray]):
+    """CosinePrediction.forward, src/model.py:317-327 -> {etype: [E,1]}."""
+    out = {}
+    for ce, (s, d) in pair_edges.items():
+        if ce[0] not in h or ce[2] not in h:
+            continue  # KeyError branch, :324-325
+        hs, hd = normalize_rows(h[ce[0]]), normalize_rows(h[ce[2]])
+        out[ce] = (hs[s] * hd[d]).sum(-1, keepdims=True).astype(np.float32)
+    return out
+
+
+def sigmoid(x):
+    return (1.0 / (1.0 + np.exp(-x))).astype(np.float32)
+
+
+def predicting_layer(x, p: dict):
+    """PredictingLayer.forward, src/model.py:265-271."""
+    x = relu(linear(x, p["hidden_1.weight"], p["hidden_1.bias"]))
+    x = relu(linear(x, p["hidden_2.weight"], p["hidden_2.bias"]))
+    return sigmoid(linear(x, p["output.weight"], p["output.bias"]))
+
+
+def predicting_module(pair_edges, h, p: dict):
+    """PredictingModule.forward, src/model.py:290-305 (concatenation form)."""
+    out = {}
+    for ce, (s, d) in pair_edges.items():
+        if ce[0] in USER_ITEM and ce[2] in USER_ITEM:
+            cat = np.concatenate([h[ce[0]][s], h[ce[2]][d]], 1)
+            out[ce] = predicting_layer(cat, p).reshape(-1, 1)
+    return out
+
+
+def max_margin_loss(pos, neg, delta, K, use_recency=False, recency=None,
+                    remove_false_negative=False, mask=None):
+    """max_margin_loss, src/model.py:473-533."""
+    allv = []
+    for ce in pos:
+        ns = neg[ce].reshape(-1, K)
+        m = mask[ce].reshape(-1, K) if remove_false_negative else np.zeros_like(ns)
+        sc = relu(ns + np.float32(delta) - pos[ce] - m)
+        if use_recency and recency is not None and ce in recency:
+            sc = sc / np.asarray(recency[ce], np.float32)[:, None]
+        allv.append(sc.reshape(-1))
+    return np.float32(np.concatenate(allv).mean()) if allv else np.float32(np.nan)
+
+
+# --------------------------------------------------------------- sampler ----
+def sample_neighbors(indptr, indices, eids, seeds, fanout: int, key: int = 0, excluded=None):
+    indptr = np.ascontiguousarray(indptr, np.int64)
+    indices = np.ascontiguousarray(indices, np.int64)
+    eids = np.ascontiguousarray(eids, np.int64)
+    seeds = np.ascontiguousarray(seeds, np.int64)
+    if excluded is not None:
+        excluded = np.ascontiguousarray(excluded, np.uint8)
+    n = seeds.size
+    fan = -1 if fanout is None or fanout < 0 else int(fanout)
+    counts = np.empty(n, np.int64)
+    L = lib()
+    L.oracle_sample_count(_p(indptr), _p(eids), _p(excluded), _p(seeds), n, fan, key, _p(counts))
+    out_indptr = np.zeros(n + 1, np.int64)
+    np.cumsum(counts, out=out_indptr[1:])
+    total = int(out_indptr[-1])
+    src = np.empty(total, np.int64)
+    eid = np.empty(total, np.int64)
+    L.oracle_sample_fill(_p(indptr), _p(indices), _p(eids), _p(excluded), _p(seeds), n, fan, key,
+                         _p(out_indptr), _p(src), _p(eid))
+    return out_indptr, src, eid
+
+
+def to_block_relabel(prefix: np.ndarray, id_lists):
+    """DGL to_block relabel: dst prefix first, then new ids ASCENDING (build order)."""
+    prefix = np.asarray(prefix, np.int64)
+    pos = {int(v): i for i, v in enumerate(prefix)}
+    allids = np.concatenate([np.asarray(x, np.int64) for x in id_lists]) if id_lists else \
+        np.zeros(0, np.int64)
+    new = np.unique(allids[~np.isin(allids, prefix)])
+    rank = {int(v): prefix.size + i for i, v in enumerate(new)}
+    src_nodes = np.concatenate([prefix, new])
+    locs = [np.array([pos[int(v)] if int(v) in pos else rank[int(v)] for v in x], np.int64)
+            for x in id_lists]
+    return src_nodes, locs
+
+
+# ----------------------------------------------------------------- synth ----
+def synth_edges(seed: int, e0: int, n: int, n_u: int, n_i: int, cdf=None):
+    u = np.empty(n, np.int32)
+    i = np.empty(n, np.int32)
+    if cdf is not None:
+        cdf = np.ascontiguousarray(cdf, np.float64)
+    lib().oracle_synth_edges(seed, e0, n, n_u, n_i, _p(cdf), _p(u), _p(i))
+    return u, i
+
+
+def zipf_cdf(n: int, s: float) -> np.ndarray:
+    w = 1.0 / np.arange(1, n + 1, dtype=np.float64) ** s
+    c = np.cumsum(w)
+    return c / c[-1]
+
+
+def hash3(seed, a, b) -> int:
+    return int(lib().oracle_hash3(seed, a, b))
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())

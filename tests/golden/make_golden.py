@@ -1,0 +1,217 @@
+"""Generate golden vectors by running the reference's own model code.
+
+TEST INFRASTRUCTURE.  Runs ONLY in the build container, where the read-only
+reference is mounted at /root/reference; skips cleanly elsewhere (the GPU box
+has no reference).  It imports /root/reference/src/model.py UNMODIFIED, with
+tests/golden/dgl_shim.py registered as `dgl` (DGL 0.5.2 is not installable
+offline), runs the reference's ConvLayer / ConvModel / CosinePrediction /
+PredictingModule / max_margin_loss on small seeded synthetic heterographs, and
+writes inputs + state_dict + outputs as .npz fixtures next to this script.
+No reference source is copied: only numbers are stored.
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("GNNREC_REFERENCE", "/root/reference")
+
+USER_ITEM = ("user", "item")
+
+
+def load_reference_model():
+    sys.dont_write_bytecode = True  # never write into the read-only reference tree
+    sys.path.insert(0, HERE)
+    import dgl_shim  # noqa: E402
+
+    dgl_shim.install()
+    spec = importlib.util.spec_from_file_location("ref_model", os.path.join(REF, "src", "model.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod, dgl_shim
+
+
+def make_graph(rng, num_nodes, rel_sizes, zero_rels=()):
+    """Reverse relations share the forward relation's eid order (utils_data.py:205-238)."""
+    edges = {}
+    occ = {}
+    pairs = [(("user", "buys", "item"), ("item", "bought-by", "user")),
+             (("user", "clicks", "item"), ("item", "clicked-by", "user")),
+             (("item", "utilized-for", "sport"), ("sport", "utilizes", "item")),
+             (("user", "practices", "sport"), ("sport", "practiced-by", "user")),
+             (("sport", "belongs-to", "sport"), ("sport", "includes", "sport"))]
+    for fwd, rev in pairs:
+        if fwd[1] not in rel_sizes:
+            continue
+        n = rel_sizes[fwd[1]]
+        s = rng.integers(0, num_nodes[fwd[0]], n)
+        d = rng.integers(0, num_nodes[fwd[2]], n)
+        o = rng.integers(1, 9, n)
+        edges[fwd] = (s, d)
+        occ[fwd] = o
+        if rev[1] in zero_rels:
+            edges[rev] = (np.zeros(0, np.int64), np.zeros(0, np.int64))
+            occ[rev] = np.zeros(0, np.int64)
+        else:
+            edges[rev] = (d, s)
+            occ[rev] = o
+    return edges, occ
+
+
+def to_shim(dgl_shim, edges, occ, num_nodes):
+    g = dgl_shim.HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d))
+                              for ce, (s, d) in edges.items()}, num_nodes)
+    for ce in edges:
+        if ce[0] in USER_ITEM and ce[2] in USER_ITEM:
+            g._edata[ce]["occurrence"] = torch.from_numpy(occ[ce])
+    return g
+
+
+def etype_key(ce):
+    return "__".join(ce)
+
+
+def save_graph(arrs, edges, occ, num_nodes, prefix="g"):
+    for nt, n in num_nodes.items():
+        arrs[f"{prefix}/num_nodes/{nt}"] = np.array(n, np.int64)
+    for ce, (s, d) in edges.items():
+        k = etype_key(ce)
+        arrs[f"{prefix}/src/{k}"] = s.astype(np.int64)
+        arrs[f"{prefix}/dst/{k}"] = d.astype(np.int64)
+        arrs[f"{prefix}/occurrence/{k}"] = occ[ce].astype(np.int64)
+
+
+def gen_convlayer_cases(ref, dgl_shim, manifest):
+    rng = np.random.default_rng(11)
+    num_nodes = {"user": 37, "item": 29, "sport": 5}
+    edges, occ = make_graph(rng, num_nodes, {"buys": 180, "practices": 20})
+    g = to_shim(dgl_shim, edges, occ, num_nodes)
+    dims = {"user": 5, "item": 6, "sport": 3}
+    feats = {nt: rng.standard_normal((n, dims[nt])).astype(np.float32) for nt, n in num_nodes.items()}
+    for ce in (("user", "buys", "item"), ("item", "bought-by", "user"),
+               ("user", "practices", "sport")):
+        for agg in ("mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge"):
+            for norm in (True, False):
+                torch.manual_seed(7)
+                layer = ref.ConvLayer((dims[ce[0]], dims[ce[2]]), 12, 0.0, agg, norm)
+                layer.eval()
+                with torch.no_grad():
+                    z = layer(g[ce], (torch.from_numpy(feats[ce[0]]), torch.from_numpy(feats[ce[2]])))
+                name = f"convlayer_{ce[1]}_{agg}_{'norm' if norm else 'nonorm'}"
+                arrs = {"x_neigh": feats[ce[0]], "x_self": feats[ce[2]], "out": z.numpy()}
+                for k, v in layer.state_dict().items():
+                    arrs[f"w/{k}"] = v.numpy()
+                save_graph(arrs, edges, occ, num_nodes)
+                np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+                manifest[name] = {"kind": "convlayer", "etype": list(ce), "aggregator_type": agg,
+                                  "norm": norm, "out_feats": 12}
+
+
+def gen_model_cases(ref, dgl_shim, manifest):
+    cases = [
+        # (name, graph kind, agg, hetero, embedding_layer, n_layers, pred, norm)
+        ("model_bip_mean_sum_emb", "bip", "mean", "sum", True, 3, "cos", True),
+        ("model_bip_meannn_sum_noemb", "bip", "mean_nn", "sum", False, 3, "cos", True),
+        ("model_bip_poolnn_max_noemb_nn", "bip", "pool_nn", "max", False, 2, "nn", True),
+        ("model_het_meannnedge_mean_emb", "het", "mean_nn_edge", "mean", True, 3, "cos", True),
+        ("model_het_pooledge_sum_noemb_nn", "het", "pool_nn_edge", "sum", False, 2, "nn", False),
+        ("model_het_meanedge_max_emb", "het", "mean_edge", "max", True, 2, "cos", True),
+        ("model_het_mean_sum_skip", "het_skip", "mean", "sum", False, 3, "cos", True),
+    ]
+    for case_no, (name, kind, agg, hagg, emb, n_layers, pred, norm) in enumerate(cases):
+        rng = np.random.default_rng(1234 + case_no)
+        if kind == "bip":
+            num_nodes = {"user": 41, "item": 23}
+            edges, occ = make_graph(rng, num_nodes, {"buys": 160})
+            dims = {"user": 5, "item": 6}
+        else:
+            num_nodes = {"user": 43, "item": 31, "sport": 6}
+            edges, occ = make_graph(rng, num_nodes, {"buys": 120, "clicks": 150, "utilized-for": 40,
+                                                     "practices": 30, "belongs-to": 8},
+                                    zero_rels=("includes",) if kind == "het_skip" else ())
+            dims = {"user": 5, "item": 6, "sport": 3}
+        g = to_shim(dgl_shim, edges, occ, num_nodes)
+        dim_dict = dict(dims)
+        dim_dict.update({"hidden": 16, "out": 8})
+        torch.manual_seed(3)
+        model = ref.ConvModel(g, n_layers, dim_dict, norm, 0.0, agg, pred, hagg, emb)
+        model.eval()
+        feats = {nt: rng.standard_normal((n, dims[nt])).astype(np.float32)
+                 for nt, n in num_nodes.items()}
+        # pair graphs on the full node sets (pos: first 16 buys edges; neg: K per positive)
+        K = 5
+        bs, bd = edges[("user", "buys", "item")]
+        pos_s, pos_d = bs[:16], bd[:16]
+        neg_s = np.repeat(pos_s, K)
+        neg_d = rng.integers(0, num_nodes["item"], neg_s.size)
+        empty = (np.zeros(0, np.int64), np.zeros(0, np.int64))
+        pos_edges = {ce: ((pos_s, pos_d) if ce == ("user", "buys", "item") else empty)
+                     for ce in edges}
+        neg_edges = {ce: ((neg_s, neg_d) if ce == ("user", "buys", "item") else empty)
+                     for ce in edges}
+        pos_g = dgl_shim.HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d))
+                                      for ce, (s, d) in pos_edges.items()}, num_nodes)
+        neg_g = dgl_shim.HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d))
+                                      for ce, (s, d) in neg_edges.items()}, num_nodes)
+        n_blocks = n_layers - 1 if emb else n_layers
+        with torch.no_grad():
+            h_in = {nt: torch.from_numpy(v) for nt, v in feats.items()}
+            h, pos_score, neg_score = model([g] * n_blocks, dict(h_in), pos_g, neg_g, emb)
+            recency = {("user", "buys", "item"): torch.from_numpy(
+                rng.integers(1, 30, pos_s.size).astype(np.int64))}
+            mask = {ce: torch.from_numpy((rng.random(neg_edges[ce][0].size) < 0.1)
+                                         .astype(np.float32)) for ce in pos_score}
+            loss = ref.max_margin_loss(pos_score, neg_score, 0.266, K, use_recency=True,
+                                       recency_scores=recency, remove_false_negative=True,
+                                       negative_mask=mask)
+        arrs = {}
+        save_graph(arrs, edges, occ, num_nodes)
+        for nt, v in feats.items():
+            arrs[f"feat/{nt}"] = v
+        for nt, v in h.items():
+            arrs[f"h/{nt}"] = v.numpy()
+        for k, v in model.state_dict().items():
+            arrs[f"w/{k}"] = v.numpy()
+        arrs["pos/src"], arrs["pos/dst"] = pos_s, pos_d
+        arrs["neg/src"], arrs["neg/dst"] = neg_s, neg_d
+        for ce, v in pos_score.items():
+            arrs[f"pos_score/{etype_key(ce)}"] = v.numpy()
+        for ce, v in neg_score.items():
+            arrs[f"neg_score/{etype_key(ce)}"] = v.numpy()
+        arrs["recency"] = recency[("user", "buys", "item")].numpy()
+        for ce, v in mask.items():
+            arrs[f"mask/{etype_key(ce)}"] = v.numpy()
+        arrs["loss"] = np.array(loss.item(), np.float32)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        manifest[name] = {"kind": "model", "aggregator_type": agg, "aggregator_hetero": hagg,
+                          "embedding_layer": emb, "n_layers": n_layers, "pred": pred,
+                          "norm": norm, "dim_dict": dim_dict, "neg_sample_size": K,
+                          "delta": 0.266, "canonical_etypes": [list(ce) for ce in edges]}
+
+
+def main():
+    if not os.path.exists(os.path.join(REF, "src", "model.py")):
+        print(f"reference not found at {REF}: skipping golden generation")
+        return 0
+    ref, dgl_shim = load_reference_model()
+    manifest = {}
+    gen_convlayer_cases(ref, dgl_shim, manifest)
+    gen_model_cases(ref, dgl_shim, manifest)
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py",
+                   "reference_files": ["src/model.py"],
+                   "torch": torch.__version__, "cases": manifest}, f, indent=1, sort_keys=True)
+    print(f"wrote {len(manifest)} golden cases to {HERE}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,91 @@
+"""Pin the CPU oracle (oracle/oracle.py + oracle.c) to golden vectors produced by
+the reference's own src/model.py (tests/golden/make_golden.py).
+
+Tolerance: fp32 end to end on both sides; reductions run in different orders
+(DGL-shim index_add vs the oracle's sequential CSR loop), so we require
+|a-b| <= 1e-5 + 1e-5·|b| — two orders tighter than the north-star 1e-4."""
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import oracle
+
+RTOL, ATOL = 1e-5, 1e-5
+
+CASES = golden_io.manifest()
+CONV = sorted(k for k, v in CASES.items() if v["kind"] == "convlayer")
+MODEL = sorted(k for k, v in CASES.items() if v["kind"] == "model")
+
+
+def test_manifest_covers_every_aggregator_and_hetero_mode():
+    aggs = {CASES[k]["aggregator_type"] for k in CONV}
+    assert aggs == {"mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge"}
+    assert {CASES[k]["aggregator_hetero"] for k in MODEL} == {"sum", "mean", "max"}
+    assert {CASES[k]["pred"] for k in MODEL} == {"cos", "nn"}
+
+
+@pytest.mark.parametrize("name", CONV)
+def test_conv_layer_matches_reference(name):
+    meta = CASES[name]
+    a = golden_io.load(name)
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = oracle.Graph(num_nodes, edges, occ)
+    ce = tuple(meta["etype"])
+    z = oracle.conv_layer(g, ce, a["x_neigh"], a["x_self"], golden_io.state_dict(a),
+                          meta["aggregator_type"], meta["norm"])
+    np.testing.assert_allclose(z, a["out"], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("name", MODEL)
+def test_full_graph_model_matches_reference(name):
+    meta = CASES[name]
+    a = golden_io.load(name)
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = oracle.Graph(num_nodes, edges, occ)
+    feats = {k[5:]: v for k, v in a.items() if k.startswith("feat/")}
+    sd = golden_io.state_dict(a)
+    h = oracle.model_full_graph(g, feats, sd, meta["aggregator_type"], meta["aggregator_hetero"],
+                                meta["norm"], meta["embedding_layer"])
+    ref_h = {k[2:]: v for k, v in a.items() if k.startswith("h/")}
+    assert set(h) == set(ref_h)
+    for nt in ref_h:
+        np.testing.assert_allclose(h[nt], ref_h[nt], rtol=RTOL, atol=ATOL)
+
+    # edge-score heads and the loss on the reference's own embeddings
+    pos = {ce: ((a["pos/src"], a["pos/dst"]) if ce == ("user", "buys", "item") else
+                (np.zeros(0, np.int64), np.zeros(0, np.int64))) for ce in edges}
+    neg = {ce: ((a["neg/src"], a["neg/dst"]) if ce == ("user", "buys", "item") else
+                (np.zeros(0, np.int64), np.zeros(0, np.int64))) for ce in edges}
+    if meta["pred"] == "cos":
+        ps, ns = oracle.cosine_prediction(pos, ref_h), oracle.cosine_prediction(neg, ref_h)
+    else:
+        _, _, p = oracle.split_state_dict(sd)
+        p = {k[len("layer_nn."):]: v for k, v in p.items()}
+        ps, ns = oracle.predicting_module(pos, ref_h, p), oracle.predicting_module(neg, ref_h, p)
+    ref_ps = golden_io.by_etype(a, "pos_score")
+    ref_ns = golden_io.by_etype(a, "neg_score")
+    assert set(ps) == set(ref_ps) and set(ns) == set(ref_ns)
+    for ce in ref_ps:
+        np.testing.assert_allclose(ps[ce], ref_ps[ce], rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(ns[ce], ref_ns[ce], rtol=RTOL, atol=ATOL)
+    mask = golden_io.by_etype(a, "mask")
+    rec = {("user", "buys", "item"): a["recency"]}
+    loss = oracle.max_margin_loss(ref_ps, ref_ns, meta["delta"], meta["neg_sample_size"],
+                                  use_recency=True, recency=rec, remove_false_negative=True,
+                                  mask=mask)
+    np.testing.assert_allclose(loss, a["loss"], rtol=RTOL, atol=ATOL)
+
+
+def test_relation_skip_case_present():
+    """The het_skip fixture has an empty relation; the reference skips it."""
+    a = golden_io.load("model_het_mean_sum_skip")
+    _, edges, _ = golden_io.graph_parts(a)
+    assert edges[("sport", "includes", "sport")][0].size == 0
+
+
+def test_unknown_aggregator_raises_keyerror():
+    g = oracle.Graph({"user": 2, "item": 2}, {("user", "buys", "item"): ([0], [1])})
+    w = {"fc_self.weight": np.zeros((3, 2), np.float32), "fc_neigh.weight": np.zeros((3, 2), np.float32)}
+    with pytest.raises(KeyError):
+        oracle.conv_layer(g, ("user", "buys", "item"), np.zeros((2, 2), np.float32),
+                          np.zeros((2, 2), np.float32), w, "median", True)
