@@ -1,0 +1,96 @@
+"""Collective exchange for the sharded full-graph pass.
+
+One process per GPU, torch.distributed over RCCL ("nccl" backend on ROCm),
+xGMI between the 8 MI355X of a node.  Two collectives per layer and per
+replicated node type, both sized by the SMALL side of the bipartite graph:
+
+  reduce-scatter  partial aggregates of the relations whose destination type
+                  is replicated (user→item: each rank aggregates the edges of
+                  its own users into every item row) -> the item rows it owns;
+  all-gather      the item rows each rank projected -> the full item table
+                  every rank reads as sources of item→user edges next layer.
+
+Replicated tables are padded to P·S rows (S = ceil(N/P)) so both collectives
+are the equal-count RCCL forms.  On gloo (CPU tests) reduce-scatter is
+emulated by all_reduce + slice and all-gather by the list form.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.distributed as dist
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def world() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def even_ranges(n: int, parts: int) -> List[int]:
+    """Boundaries b[0..parts] of a contiguous, count-balanced split of [0, n)."""
+    return [(n * p) // parts for p in range(parts + 1)]
+
+
+def padded_shard(n: int, parts: int) -> int:
+    """Rows per rank of a replicated table padded to parts·S rows."""
+    return (n + parts - 1) // parts if n else 0
+
+
+class Exchange:
+    """reduce-scatter / all-gather of equal row blocks of a [P·S, d] table."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.ws = world()
+        self.rk = rank()
+        self.backend = dist.get_backend(group) if is_initialized() else None
+
+    def reduce_scatter_rows(self, full: torch.Tensor, op: str, async_op: bool = False):
+        """full [P·S, d] partial on every rank -> (own [S, d], work|None)."""
+        if self.ws == 1:
+            return full, None
+        S = full.shape[0] // self.ws
+        rop = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+        if self.backend == "nccl":
+            out = torch.empty((S,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+            work = dist.reduce_scatter_tensor(out, full, op=rop, group=self.group,
+                                              async_op=async_op)
+            return out, work
+        dist.all_reduce(full, op=rop, group=self.group)
+        return full[self.rk * S:(self.rk + 1) * S], None
+
+    def all_gather_rows(self, own: torch.Tensor, out: torch.Tensor, async_op: bool = False):
+        """own [S, d] -> out [P·S, d] in rank order, returns (out, work|None)."""
+        if self.ws == 1:
+            if out.data_ptr() != own.data_ptr():
+                out.copy_(own)
+            return out, None
+        if self.backend == "nccl":
+            work = dist.all_gather_into_tensor(out, own.contiguous(), group=self.group,
+                                               async_op=async_op)
+            return out, work
+        S = own.shape[0]
+        tmp = [torch.empty_like(own) for _ in range(self.ws)]
+        dist.all_gather(tmp, own.contiguous(), group=self.group)
+        for i, t in enumerate(tmp):
+            out[i * S:(i + 1) * S].copy_(t)
+        return out, None
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum"):
+        if self.ws > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX,
+                            group=self.group)
+        return t
+
+    def max_scalar(self, x: float, device) -> float:
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        self.all_reduce_(t, "max")
+        return float(t.item())

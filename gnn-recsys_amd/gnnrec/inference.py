@@ -1,0 +1,330 @@
+"""Full-graph inference embedding pass (rows a5/a6/e of SURVEY.md §8).
+
+Replaces reference src/train/run.py:311-349 `get_embeddings` as driven by
+main_inference.py:123-152 (NodeDataLoader over every user and item,
+MultiLayerFullNeighborSampler, 128-seed batches).  With full neighbourhoods
+and eval-mode dropout that loop computes, for every node, the L-layer
+ConvModel output over its complete L-hop neighbourhood; here the same
+function is computed LAYER-WISE over the whole graph (every edge aggregated
+once per layer instead of once per batch that touches it), which is the
+reference run with one batch containing every node.
+
+Sharding (P ranks, one per GPU, RCCL over xGMI):
+  * the large node type (users) is partitioned into contiguous ranges; every
+    relation INTO users is aggregated by the owner of the destination row
+    (sources read from the replicated item table);
+  * relations into the replicated types (items, sports) are aggregated from
+    the edges each rank holds (its users' edges, or an eid range) into a
+    partial table of every destination row, then reduce-scattered (sum, or max
+    for pool aggregators) to the row owner, which divides by the GLOBAL
+    in-degree inside the projection GEMM's operand load and projects;
+  * the projected replicated rows are all-gathered for the next layer.
+Per layer each rank moves 2·(P−1)/P·N_item·d·4 bytes instead of the
+(P−1)/P·(N_user+N_item)·d·4 of an all-gather-everything scheme, and the
+collectives overlap the user-side aggregation (async RCCL work handles).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib, ops
+from .dist import Exchange, even_ranges, padded_shard
+from .graph import HeteroGraph, RelGraph, build_csr
+
+
+# --------------------------------------------------------- single process ---
+@torch.no_grad()
+def full_graph_embeddings(g: HeteroGraph, model, feats: Optional[Dict[str, torch.Tensor]] = None,
+                          embedding_layer: Optional[bool] = None) -> Dict[str, torch.Tensor]:
+    """Layer-wise full-graph pass on one device: {ntype: [N, out_dim]}."""
+    if feats is None:
+        feats = g.ndata['features']
+    if embedding_layer is None:
+        embedding_layer = model.embedding_layer
+    h = model.embed(feats) if embedding_layer else dict(feats)
+    for layer in model.layers:
+        h = layer(g, h)
+    return h
+
+
+@torch.no_grad()
+def get_embeddings(g, out_dim: int, trained_model, nodeloader_test, num_batches_valid: int = 0,
+                   cuda: bool = True, device=None, embedding_layer: bool = True):
+    """Drop-in for reference src/train/run.py:311-349 (minibatch loop over a node loader)."""
+    dev = device if device is not None else torch.device('cuda')
+    y = {nt: torch.zeros(g.num_nodes(nt), out_dim, device=dev) for nt in g.ntypes}
+    for input_nodes, output_nodes, blocks in nodeloader_test:
+        blocks = [b.to(dev) for b in blocks]
+        input_features = blocks[0].srcdata['features']
+        if embedding_layer:
+            input_features = trained_model.embed(input_features)
+        h = trained_model.get_repr(blocks, input_features)
+        for ntype in h.keys():
+            y[ntype][output_nodes[ntype]] = h[ntype]
+    return y
+
+
+# ------------------------------------------------------------- sharded ------
+class RelShard:
+    """One relation's edges held by this rank, as a dst-major CSR."""
+
+    def __init__(self, ce, kind: str, indptr, indices, weights, n_rows: int, global_edges: int,
+                 deg_own: Optional[torch.Tensor] = None):
+        self.ce = ce
+        self.kind = kind              # 'local_dst' (dst rows owned here) | 'partial'
+        self.indptr = indptr
+        self.indices = indices
+        self.weights = weights        # float32 per edge in CSR order, or None
+        self.n_rows = n_rows
+        self.global_edges = global_edges
+        self.deg_own = deg_own        # int32 global in-degree of the owned dst rows ('partial')
+
+    @property
+    def local_edges(self) -> int:
+        return int(self.indices.numel())
+
+
+class GraphShard:
+    """This rank's share of a heterograph for the sharded full-graph pass."""
+
+    def __init__(self, rank: int, world: int, ptype: str, num_nodes: Dict[str, int],
+                 canonical_etypes: List[tuple], device):
+        self.rank, self.world, self.ptype = rank, world, ptype
+        self.num_nodes = dict(num_nodes)
+        self.canonical_etypes = list(canonical_etypes)
+        self.device = torch.device(device)
+        b = even_ranges(num_nodes[ptype], world)
+        self.p_lo, self.p_hi = b[rank], b[rank + 1]
+        self.shard_rows = {nt: padded_shard(n, world) for nt, n in num_nodes.items()
+                           if nt != ptype}
+        self.rels: Dict[tuple, RelShard] = {}
+
+    @property
+    def n_own(self) -> int:
+        return self.p_hi - self.p_lo
+
+    def padded_rows(self, nt) -> int:
+        return self.shard_rows[nt] * self.world
+
+    def own_slice(self, nt):
+        S = self.shard_rows[nt]
+        return slice(self.rank * S, (self.rank + 1) * S)
+
+    def local_edge_count(self) -> int:
+        return sum(r.local_edges for r in self.rels.values())
+
+    def global_edge_count(self) -> int:
+        return sum(r.global_edges for r in self.rels.values())
+
+    def add_relation(self, ce, src: torch.Tensor, dst: torch.Tensor, eid: torch.Tensor,
+                     global_edges: int, weights: Optional[torch.Tensor] = None,
+                     dst_global_deg: Optional[torch.Tensor] = None):
+        """Register this rank's edges of relation ce.
+
+        src/dst are GLOBAL ids of the edges this rank holds; for relations into
+        ptype they must be exactly the edges whose dst is owned here."""
+        s_t, _, d_t = ce
+        dev = self.device
+        if d_t == self.ptype:
+            if s_t == self.ptype:
+                raise NotImplementedError("relations between two rows of the partitioned type "
+                                          "need the full partitioned table (not in the schema)")
+            rows = dst - self.p_lo
+            indptr, indices, order = build_csr(src, rows, self.n_own)
+            w = None if weights is None else weights[order].float().contiguous()
+            self.rels[ce] = RelShard(ce, 'local_dst', indptr.to(dev), indices.to(dev),
+                                     None if w is None else w.to(dev), self.n_own, global_edges)
+            return
+        src_loc = src - self.p_lo if s_t == self.ptype else src
+        n_rows = self.padded_rows(d_t)
+        indptr, indices, order = build_csr(src_loc, dst, n_rows)
+        w = None if weights is None else weights[order].float().contiguous()
+        deg = torch.zeros(n_rows, dtype=torch.int32, device=dst_global_deg.device)
+        deg[: dst_global_deg.numel()] = dst_global_deg.to(torch.int32)
+        self.rels[ce] = RelShard(ce, 'partial', indptr.to(dev), indices.to(dev),
+                                 None if w is None else w.to(dev), n_rows, global_edges,
+                                 deg[self.own_slice(d_t)].contiguous().to(dev))
+
+    @classmethod
+    def from_graph(cls, g: HeteroGraph, rank: int, world: int, ptype: str = 'user', device=None,
+                   weight_field: Optional[str] = 'occurrence'):
+        """Shard a full HeteroGraph held by every rank (tests / moderate graphs)."""
+        dev = device if device is not None else g.device
+        sh = cls(rank, world, ptype, {nt: g.num_nodes(nt) for nt in g.ntypes},
+                 g.canonical_etypes, dev)
+        for ce in g.canonical_etypes:
+            s, d = g.all_edges(etype=ce)
+            E = s.numel()
+            eid = torch.arange(E, device=s.device)
+            w = g._edata[ce].get(weight_field) if weight_field else None
+            if ce[2] == ptype:
+                keep = (d >= sh.p_lo) & (d < sh.p_hi)
+            elif ce[0] == ptype:
+                keep = (s >= sh.p_lo) & (s < sh.p_hi)
+            else:
+                lo, hi = even_ranges(E, world)[rank], even_ranges(E, world)[rank + 1]
+                keep = (eid >= lo) & (eid < hi)
+            gdeg = torch.bincount(d, minlength=g.num_nodes(ce[2])) if ce[2] != ptype else None
+            sh.add_relation(ce, s[keep], d[keep], eid[keep], E,
+                            None if w is None else w[keep], gdeg)
+        return sh
+
+    def local_features(self, feats: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Full per-type feature tables -> this rank's inputs (own ptype rows, padded tables)."""
+        out = {}
+        for nt, x in feats.items():
+            if nt == self.ptype:
+                out[nt] = x[self.p_lo:self.p_hi].contiguous().to(self.device)
+            else:
+                t = torch.zeros((self.padded_rows(nt), x.shape[1]), dtype=x.dtype,
+                                device=self.device)
+                t[: x.shape[0]] = x.to(self.device)
+                out[nt] = t
+        return out
+
+
+class ShardedFullGraphPass:
+    """Layer-wise full-graph ConvModel pass over a GraphShard (one rank's view).
+
+    `ops_backend` defaults to the HIP ops (gnnrec.ops); tests on CPU ranks
+    inject a checker backend with the same signatures."""
+
+    def __init__(self, model, shard: GraphShard, exchange: Optional[Exchange] = None,
+                 ops_backend=None, overlap: bool = True):
+        self.model = model
+        self.shard = shard
+        self.ex = exchange if exchange is not None else Exchange()
+        self.ops = ops_backend if ops_backend is not None else ops
+        self.overlap = overlap
+        self._pending = {}
+        self.timers = None  # optional callable(tag) -> context manager (bench)
+
+    def _wait(self, nt):
+        w = self._pending.pop(nt, None)
+        if w is not None:
+            w.wait()
+
+    def _get(self, h, nt):
+        self._wait(nt)
+        return h[nt]
+
+    def _time(self, tag):
+        import contextlib
+        return self.timers(tag) if self.timers is not None else contextlib.nullcontext()
+
+    @torch.no_grad()
+    def run(self, feats: Dict[str, torch.Tensor], embedding_layer: Optional[bool] = None):
+        """feats: this rank's inputs (see GraphShard.local_features) -> this rank's outputs:
+        {ptype: [n_own, out]} and the replicated types as full padded tables."""
+        m = self.model
+        if embedding_layer is None:
+            embedding_layer = m.embedding_layer
+        h = dict(feats)
+        if embedding_layer:
+            for nt, mod in (('user', getattr(m, 'user_embed', None)),
+                            ('item', getattr(m, 'item_embed', None)),
+                            ('sport', getattr(m, 'sport_embed', None))):
+                if mod is not None and nt in h:
+                    h[nt] = self.ops.gemm(h[nt], mod.proj_feats.weight, bias=mod.proj_feats.bias)
+        for layer in m.layers:
+            h = self._layer(layer, h)
+        for nt in list(self._pending):
+            self._wait(nt)
+        return h
+
+    def _layer(self, hconv, h):
+        sh, O = self.shard, self.ops
+        agg = hconv.aggregate
+        active: Dict[str, list] = {}
+        for ce in sh.canonical_etypes:
+            rs = sh.rels[ce]
+            if rs.global_edges == 0 or ce[0] not in h or ce[2] not in h:
+                continue
+            active.setdefault(ce[2], []).append(ce)
+        out = {}
+        # phase 1: partial aggregates into replicated types -> async reduce-scatter
+        partials = {}
+        for T, ces in active.items():
+            if T == sh.ptype:
+                continue
+            for ce in ces:
+                mod = hconv.mods[ce[1]]
+                preagg, weighted, reduce = mod._plan_rel(ce)
+                rs = sh.rels[ce]
+                src = self._get(h, ce[0])
+                msg = O.gemm(src, mod.fc_preagg.weight, relu=True) if preagg else src
+                with self._time('spmm'):
+                    part = O.spmm(rs.indptr, rs.indices, msg, 'max' if reduce == 'max' else 'sum',
+                                  edge_weight=rs.weights if weighted else None,
+                                  empty_neginf=reduce == 'max')
+                own, work = self.ex.reduce_scatter_rows(part, 'max' if reduce == 'max' else 'sum',
+                                                        async_op=self.overlap)
+                partials[ce] = (own, work, reduce)
+        # phase 2: relations into the partitioned type (dst rows owned here)
+        for T, ces in active.items():
+            if T != sh.ptype:
+                continue
+            R = len(ces)
+            o = None
+            for j, ce in enumerate(ces):
+                mod = hconv.mods[ce[1]]
+                preagg, weighted, reduce = mod._plan_rel(ce)
+                rs = sh.rels[ce]
+                src = self._get(h, ce[0])
+                msg = O.gemm(src, mod.fc_preagg.weight, relu=True) if preagg else src
+                with self._time('spmm'):
+                    a = O.spmm(rs.indptr, rs.indices, msg, reduce,
+                               edge_weight=rs.weights if weighted else None)
+                if o is None:
+                    o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
+                                    device=a.device)
+                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
+                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+                O.gemm(h[T], mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
+                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
+            out[T] = o
+        # phase 3: owners project their replicated rows, then all-gather the table
+        for T, ces in active.items():
+            if T == sh.ptype:
+                continue
+            R = len(ces)
+            o = None
+            self_rows = self._get(h, T)[sh.own_slice(T)]
+            for j, ce in enumerate(ces):
+                mod = hconv.mods[ce[1]]
+                own, work, reduce = partials[ce]
+                if work is not None:
+                    work.wait()
+                if o is None:
+                    o = torch.empty((own.shape[0], mod._out_feats), dtype=torch.float32,
+                                    device=own.device)
+                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
+                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+                O.gemm(self_rows, mod.fc_self.weight, own, mod.fc_neigh.weight, relu=True,
+                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
+                       a2_deg=sh.rels[ce].deg_own,
+                       a2_mode=_lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG)
+            table = torch.empty((sh.padded_rows(T), o.shape[1]), dtype=torch.float32,
+                                device=o.device)
+            table, work = self.ex.all_gather_rows(o, table, async_op=self.overlap)
+            if work is not None:
+                self._pending[T] = work
+            out[T] = table
+        return out
+
+
+def gather_partitioned(shard: GraphShard, rows: torch.Tensor, exchange: Exchange) -> torch.Tensor:
+    """Assemble the full [N_ptype, d] table from every rank's owned rows (tests/tools)."""
+    if exchange.ws == 1:
+        return rows
+    import torch.distributed as dist
+    n = shard.num_nodes[shard.ptype]
+    S = padded_shard(n, exchange.ws)
+    pad = torch.zeros((S, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    pad[: rows.shape[0]] = rows
+    parts = [torch.empty_like(pad) for _ in range(exchange.ws)]
+    dist.all_gather(parts, pad, group=exchange.group)
+    b = even_ranges(n, exchange.ws)
+    return torch.cat([parts[r][: b[r + 1] - b[r]] for r in range(exchange.ws)], 0)

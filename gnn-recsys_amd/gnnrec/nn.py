@@ -1,0 +1,362 @@
+"""Drop-in nn.Modules for reference src/model.py, backed by the HIP kernels.
+
+Same class names, constructor signatures, parameter names/shapes (so a
+reference state_dict loads unchanged), forward signatures and error behaviour
+as the reference:
+
+  NodeEmbedding      src/model.py:10-24
+  ConvLayer          src/model.py:27-237   (aggregators mean / mean_nn / pool_nn /
+                                            *_edge; lstm* construct but raise in
+                                            forward: out of this tier's scope)
+  HeteroGraphConv    DGL 0.5.2 dgl.nn.pytorch.HeteroGraphConv as used at
+                     src/model.py:384-406 (relation-skip rule, sum/mean/max)
+  PredictingLayer    src/model.py:240-272
+  PredictingModule   src/model.py:275-305
+  CosinePrediction   src/model.py:308-327
+  ConvModel          src/model.py:330-470
+  max_margin_loss    src/model.py:473-533
+
+Inference (no autograd) runs entirely in HIP kernels: gather+aggregate
+(gnnrec_spmm_csr_f32) then ONE fused fp32-MFMA GEMM per relation that also
+applies ReLU, the zero-guarded L2 norm and the cross-relation
+sum/mean/max straight into the destination buffer (no torch.stack).
+With autograd active the forward values still come from the same kernels;
+gradients are computed by the Functions in gnnrec/autograd.py.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+from . import autograd as ag
+
+USER_ITEM = ("user", "item")
+_PREAGG = ("pool_nn", "pool_nn_edge", "mean_nn", "mean_nn_edge")
+_KNOWN = ("mean", "mean_nn", "pool_nn", "lstm", "mean_edge", "mean_nn_edge", "pool_nn_edge",
+          "lstm_edge")
+
+
+def _grad_mode(*tensors, module: nn.Module = None) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    if any(t is not None and t.requires_grad for t in tensors):
+        return True
+    return module is not None and any(p.requires_grad for p in module.parameters())
+
+
+class NodeEmbedding(nn.Module):
+    """Projects the node features into embedding space (src/model.py:10-24)."""
+
+    def __init__(self, in_feats, out_feats):
+        super().__init__()
+        self.proj_feats = nn.Linear(in_feats, out_feats)
+
+    def forward(self, node_feats):
+        W, b = self.proj_feats.weight, self.proj_feats.bias
+        if _grad_mode(node_feats, module=self):
+            return ag.LinearFn.apply(node_feats, W, b, False, False)
+        return ops.gemm(node_feats, W, bias=b)
+
+
+class ConvLayer(nn.Module):
+    """One relation of message passing + aggregation (src/model.py:27-237)."""
+
+    def reset_parameters(self):
+        gain = nn.init.calculate_gain('relu')
+        nn.init.xavier_uniform_(self.fc_self.weight, gain=gain)
+        nn.init.xavier_uniform_(self.fc_neigh.weight, gain=gain)
+        if self._aggre_type in _PREAGG:
+            nn.init.xavier_uniform_(self.fc_preagg.weight, gain=gain)
+        if self._aggre_type == 'lstm':
+            self.lstm.reset_parameters()
+
+    def __init__(self, in_feats: Tuple[int, int], out_feats: int, dropout: float,
+                 aggregator_type: str, norm):
+        super().__init__()
+        self._in_neigh_feats, self._in_self_feats = in_feats
+        self._out_feats = out_feats
+        self._aggre_type = aggregator_type
+        self.dropout_fn = nn.Dropout(dropout)
+        self.norm = norm
+        self.fc_self = nn.Linear(self._in_self_feats, out_feats, bias=False)
+        self.fc_neigh = nn.Linear(self._in_neigh_feats, out_feats, bias=False)
+        if aggregator_type in _PREAGG:
+            self.fc_preagg = nn.Linear(self._in_neigh_feats, self._in_neigh_feats, bias=False)
+        if aggregator_type == 'lstm':
+            self.lstm = nn.LSTM(self._in_neigh_feats, self._in_neigh_feats, batch_first=True)
+        self.reset_parameters()
+
+    # --- helpers -------------------------------------------------------------
+    def _plan(self, graph):
+        return self._plan_rel(graph.canonical_etypes[0])
+
+    def _plan_rel(self, ce):
+        """(fc_preagg applies, edge weight applies, 'mean'|'max') — src/model.py:143-224."""
+        agg = self._aggre_type
+        if agg not in _KNOWN:
+            raise KeyError('Aggregator type {} not recognized.'.format(agg))
+        if agg.startswith('lstm'):
+            raise NotImplementedError(
+                "lstm/lstm_edge aggregators are outside the MI355X hot-path scope "
+                "(SURVEY.md §2 row 1, §8f row f4)")
+        weighted = agg.endswith('_edge') and ce[0] in USER_ITEM and ce[2] in USER_ITEM
+        reduce = 'max' if agg.startswith('pool') else 'mean'
+        return agg in _PREAGG, weighted, reduce
+
+    @staticmethod
+    def _edge_weight(graph):
+        """graph.edata['occurrence'].float() in CSR order (src/model.py:174)."""
+        w = graph.edata['occurrence']
+        return w if w.dtype == torch.float32 else w.float()
+
+    def forward(self, graph, x):
+        """Reference ConvLayer.forward(graph, (h_neigh, h_self)) -> z [n_dst, out_feats]."""
+        return self._run(graph, x, None, 'store', 0.0)
+
+    def _run(self, graph, x, out, accum: str, out_div: float):
+        h_neigh, h_self = x
+        preagg, weighted, reduce = self._plan(graph)
+        if self.training and self.dropout_fn.p > 0:
+            h_neigh = self.dropout_fn(h_neigh)
+            h_self = self.dropout_fn(h_self)
+        ew = self._edge_weight(graph) if weighted else None
+        if _grad_mode(h_neigh, h_self, module=self):
+            m = ag.LinearFn.apply(h_neigh, self.fc_preagg.weight, None, True, False) \
+                if preagg else h_neigh
+            agg = ag.SpmmFn.apply(m, graph.indptr, graph.indices, ew, reduce, graph.n_dst)
+            z = ag.SageProjectFn.apply(h_self, agg, self.fc_self.weight, self.fc_neigh.weight,
+                                       bool(self.norm))
+            return z if out is None else z  # caller combines relations in grad mode
+        m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
+        agg = ops.spmm(graph.indptr, graph.indices, m, reduce, edge_weight=ew)
+        return ops.gemm(h_self, self.fc_self.weight, agg, self.fc_neigh.weight, relu=True,
+                        l2norm=bool(self.norm), accum=accum, out_div=out_div, out=out)
+
+
+class HeteroGraphConv(nn.Module):
+    """DGL 0.5.2 HeteroGraphConv semantics (restated), fused cross-relation aggregate.
+
+    Relations with zero edges in `g`, or whose src / dst type has no input, are
+    skipped; the outputs of the active relations are reduced per dst type with
+    sum / mean / max.  Modules live in an nn.ModuleDict keyed by relation name,
+    so state_dict keys are `mods.{rel}.*` exactly as in the reference."""
+
+    def __init__(self, mods: Dict[str, nn.Module], aggregate: str = 'sum'):
+        super().__init__()
+        self.mods = nn.ModuleDict(mods)
+        if aggregate not in ('sum', 'mean', 'max'):
+            raise KeyError('Invalid cross type reducer: {}'.format(aggregate))
+        self.aggregate = aggregate
+
+    def forward(self, g, inputs):
+        if isinstance(inputs, tuple):
+            src_inputs, dst_inputs = inputs
+        elif g.is_block:
+            src_inputs = inputs
+            dst_inputs = {k: v[:g.number_of_dst_nodes(k)] for k, v in inputs.items()}
+        else:
+            src_inputs = dst_inputs = inputs
+        active: Dict[str, list] = {}
+        for ce in g.canonical_etypes:
+            stype, etype, dtype = ce
+            if g.num_edges(ce) == 0:
+                continue
+            if stype not in src_inputs or dtype not in dst_inputs:
+                continue
+            active.setdefault(dtype, []).append(ce)
+        grad = _grad_mode(*src_inputs.values(), *dst_inputs.values(), module=self)
+        rsts = {}
+        for dtype, ces in active.items():
+            if grad:
+                outs = [self.mods[ce[1]](g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype]))
+                        for ce in ces]
+                st = torch.stack(outs, 0)
+                rsts[dtype] = (st.sum(0) if self.aggregate == 'sum' else
+                               st.mean(0) if self.aggregate == 'mean' else st.max(0)[0])
+                continue
+            n_dst = dst_inputs[dtype].shape[0]
+            out_feats = self.mods[ces[0][1]]._out_feats
+            out = torch.empty((n_dst, out_feats), dtype=torch.float32,
+                              device=dst_inputs[dtype].device)
+            R = len(ces)
+            for j, ce in enumerate(ces):
+                accum = 'store' if j == 0 else ('max' if self.aggregate == 'max' else 'add')
+                div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
+                self.mods[ce[1]]._run(g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype]),
+                                      out, accum, div)
+            rsts[dtype] = out
+        return rsts
+
+
+class PredictingLayer(nn.Module):
+    """MLP edge scorer (src/model.py:240-272)."""
+
+    def reset_parameters(self):
+        gain_relu = nn.init.calculate_gain('relu')
+        gain_sigmoid = nn.init.calculate_gain('sigmoid')
+        nn.init.xavier_uniform_(self.hidden_1.weight, gain=gain_relu)
+        nn.init.xavier_uniform_(self.hidden_2.weight, gain=gain_relu)
+        nn.init.xavier_uniform_(self.output.weight, gain=gain_sigmoid)
+
+    def __init__(self, embed_dim: int):
+        super(PredictingLayer, self).__init__()
+        self.hidden_1 = nn.Linear(embed_dim * 2, 128)
+        self.hidden_2 = nn.Linear(128, 32)
+        self.output = nn.Linear(32, 1)
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.reset_parameters()
+
+    def forward(self, x):
+        if _grad_mode(x, module=self):
+            x = ag.LinearFn.apply(x, self.hidden_1.weight, self.hidden_1.bias, True, False)
+            x = ag.LinearFn.apply(x, self.hidden_2.weight, self.hidden_2.bias, True, False)
+            return ag.LinearFn.apply(x, self.output.weight, self.output.bias, False, True)
+        x = ops.gemm(x, self.hidden_1.weight, bias=self.hidden_1.bias, relu=True)
+        x = ops.gemm(x, self.hidden_2.weight, bias=self.hidden_2.bias, relu=True)
+        return ops.gemm(x, self.output.weight, bias=self.output.bias, sigmoid=True)
+
+    def score_edges(self, h_src, h_dst, src, dst):
+        """Edge scores without materialising [E, 2d]: W1[hu‖hv] = (W1a hu + b1) + W1b hv."""
+        d = h_src.shape[1]
+        W1 = self.hidden_1.weight
+        if src.numel() < h_src.shape[0] + h_dst.shape[0]:
+            # fewer edges than table rows: score the gathered rows
+            hu, hv = h_src.index_select(0, src), h_dst.index_select(0, dst)
+            src = dst = torch.arange(src.numel(), device=src.device)
+        else:
+            hu, hv = h_src, h_dst
+        P = ops.gemm(hu, W1[:, :d], bias=self.hidden_1.bias)
+        Q = ops.gemm(hv, W1[:, d:])
+        return ops.edge_mlp(src, dst, P, Q, self.hidden_2.weight, self.hidden_2.bias,
+                            self.output.weight.reshape(-1), self.output.bias)
+
+
+class PredictingModule(nn.Module):
+    """src/model.py:275-305: scores user/item etypes of `graph` with the MLP."""
+
+    def __init__(self, predicting_layer, embed_dim: int):
+        super(PredictingModule, self).__init__()
+        self.layer_nn = predicting_layer(embed_dim)
+
+    def forward(self, graph, h):
+        ratings_dict = {}
+        for etype in graph.canonical_etypes:
+            if etype[0] in USER_ITEM and etype[2] in USER_ITEM:
+                utype, _, vtype = etype
+                src_nid, dst_nid = graph.all_edges(etype=etype)
+                if _grad_mode(h[utype], h[vtype], module=self):
+                    cat_embed = torch.cat((h[utype][src_nid], h[vtype][dst_nid]), 1)
+                    ratings = self.layer_nn(cat_embed)
+                else:
+                    ratings = self.layer_nn.score_edges(h[utype], h[vtype], src_nid, dst_nid)
+                ratings_dict[etype] = torch.flatten(ratings)
+        return {k: torch.unsqueeze(v, 1) for k, v in ratings_dict.items()}
+
+
+class CosinePrediction(nn.Module):
+    """src/model.py:308-327: per-etype cosine of L2-normalised endpoints."""
+
+    def __init__(self):
+        super().__init__()
+
+    def forward(self, graph, h):
+        ratings = {}
+        for etype in graph.canonical_etypes:
+            if etype[0] not in h or etype[2] not in h:
+                continue  # etypes whose node types have no 'h' (reference KeyError branch)
+            src, dst = graph.all_edges(etype=etype)
+            if _grad_mode(h[etype[0]], h[etype[2]]):
+                cos = ag.CosineFn.apply(h[etype[0]], h[etype[2]], src, dst)
+            else:
+                cos = ops.sddmm_cos(src, dst, h[etype[0]], h[etype[2]])
+            ratings[etype] = cos.unsqueeze(1)
+        return ratings
+
+
+class ConvModel(nn.Module):
+    """Embedding layers + ConvLayers + prediction head (src/model.py:330-470)."""
+
+    def __init__(self, g, n_layers: int, dim_dict, norm: bool = True, dropout: float = 0.0,
+                 aggregator_type: str = 'mean', pred: str = 'cos',
+                 aggregator_hetero: str = 'sum', embedding_layer: bool = True):
+        super().__init__()
+        self.embedding_layer = embedding_layer
+        if embedding_layer:
+            self.user_embed = NodeEmbedding(dim_dict['user'], dim_dict['hidden'])
+            self.item_embed = NodeEmbedding(dim_dict['item'], dim_dict['hidden'])
+            if 'sport' in g.ntypes:
+                self.sport_embed = NodeEmbedding(dim_dict['sport'], dim_dict['hidden'])
+        self.layers = nn.ModuleList()
+        if not embedding_layer:
+            self.layers.append(HeteroGraphConv(
+                {etype[1]: ConvLayer((dim_dict[etype[0]], dim_dict[etype[2]]), dim_dict['hidden'],
+                                     dropout, aggregator_type, norm)
+                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+        for _ in range(n_layers - 2):
+            self.layers.append(HeteroGraphConv(
+                {etype[1]: ConvLayer((dim_dict['hidden'], dim_dict['hidden']), dim_dict['hidden'],
+                                     dropout, aggregator_type, norm)
+                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+        self.layers.append(HeteroGraphConv(
+            {etype[1]: ConvLayer((dim_dict['hidden'], dim_dict['hidden']), dim_dict['out'],
+                                 dropout, aggregator_type, norm)
+             for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+        if pred == 'cos':
+            self.pred_fn = CosinePrediction()
+        elif pred == 'nn':
+            self.pred_fn = PredictingModule(PredictingLayer, dim_dict['out'])
+        else:
+            raise KeyError('Prediction function {} not recognized.'.format(pred))
+
+    def get_repr(self, blocks, h):
+        for i in range(len(blocks)):
+            layer = self.layers[i]
+            h = layer(blocks[i], h)
+        return h
+
+    def embed(self, h):
+        """The embedding step of forward / get_embeddings (src/model.py:462-466)."""
+        h = dict(h)
+        h['user'] = self.user_embed(h['user'])
+        h['item'] = self.item_embed(h['item'])
+        if 'sport' in h.keys():
+            h['sport'] = self.sport_embed(h['sport'])
+        return h
+
+    def forward(self, blocks, h, pos_g, neg_g, embedding_layer: bool = True):
+        if embedding_layer:
+            h = self.embed(h)
+        h = self.get_repr(blocks, h)
+        pos_score = self.pred_fn(pos_g, h)
+        neg_score = self.pred_fn(neg_g, h)
+        return h, pos_score, neg_score
+
+
+def max_margin_loss(pos_score, neg_score, delta: float, neg_sample_size: int,
+                    use_recency: bool = False, recency_scores=None,
+                    remove_false_negative: bool = False, negative_mask=None, cuda=False,
+                    device=None):
+    """Max-margin loss (src/model.py:473-533), same arguments and semantics."""
+    parts = []
+    for etype in pos_score.keys():
+        neg = neg_score[etype].reshape(-1, neg_sample_size)
+        pos = pos_score[etype]
+        if remove_false_negative:
+            mask = negative_mask[etype].reshape(-1, neg_sample_size).to(neg)
+        else:
+            mask = torch.zeros_like(neg)
+        scores = torch.relu(neg + delta - pos - mask)
+        if use_recency and recency_scores is not None and etype in recency_scores:
+            scores = scores / torch.unsqueeze(recency_scores[etype].to(scores), 1)
+        parts.append(scores)
+    if not parts:
+        return torch.tensor(float('nan'))
+    return torch.mean(torch.cat(parts, 0))
+
+
+def library_available() -> bool:
+    return _lib.available()

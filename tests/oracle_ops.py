@@ -1,0 +1,54 @@
+"""Checker backend with the gnnrec.ops signatures, computed by the CPU oracle.
+
+TEST INFRASTRUCTURE: lets the multi-process (gloo, CPU) tests drive the
+product's partition / exchange / orchestration code (gnnrec.inference) while
+the per-rank arithmetic is done by oracle/ — the product itself never falls
+back to this (it raises when libgnnrec.so is missing)."""
+import numpy as np
+import torch
+
+from oracle import oracle
+
+
+def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_neginf=False):
+    ip = indptr.cpu().numpy()
+    res = oracle.spmm_csr(ip, indices.cpu().numpy(), X.detach().cpu().numpy(), reduce,
+                          None if edge_weight is None else edge_weight.cpu().numpy())
+    if reduce == "max" and empty_neginf:
+        res[(ip[1:] - ip[:-1]) == 0] = -np.inf
+    t = torch.from_numpy(res)
+    if out is not None:
+        out.copy_(t)
+        return out
+    return t
+
+
+def gemm(A1, W1, A2=None, W2=None, bias=None, *, relu=False, l2norm=False, sigmoid=False,
+         accum="store", out_div=0.0, out=None, a2_deg=None, a2_mode=0):
+    z = oracle.linear(A1.detach().cpu().numpy(), W1.detach().cpu().numpy(),
+                      None if bias is None else bias.detach().cpu().numpy())
+    if A2 is not None:
+        a2 = A2.detach().cpu().numpy().astype(np.float32)
+        if a2_mode == 1:
+            deg = np.maximum(a2_deg.cpu().numpy(), 1).astype(np.float32)
+            a2 = a2 / deg[:, None]
+        elif a2_mode == 2:
+            a2 = np.where((a2_deg.cpu().numpy() == 0)[:, None], np.float32(0), a2)
+        z = (z + oracle.linear(a2, W2.detach().cpu().numpy())).astype(np.float32)
+    if relu:
+        z = oracle.relu(z)
+    if sigmoid:
+        z = oracle.sigmoid(z)
+    if l2norm:
+        z = oracle.l2_normalize_rows_guarded(z)
+    t = torch.from_numpy(np.ascontiguousarray(z, np.float32))
+    if out is None:
+        return t
+    if accum == "add":
+        t = out + t
+    elif accum == "max":
+        t = torch.maximum(out, t)
+    if out_div > 0:
+        t = t / out_div
+    out.copy_(t)
+    return out
