@@ -306,6 +306,9 @@ class ShardedFullGraphPass:
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                        a2_deg=sh.rels[ce].deg_own,
                        a2_mode=_lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG)
+            if self.ex.ws == 1:  # the owned rows ARE the table
+                out[T] = o
+                continue
             table = torch.empty((sh.padded_rows(T), o.shape[1]), dtype=torch.float32,
                                 device=o.device)
             table, work = self.ex.all_gather_rows(o, table, async_op=self.overlap)

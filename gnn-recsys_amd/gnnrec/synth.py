@@ -1,0 +1,80 @@
+"""Synthetic benchmark graphs of the BASELINE.json shapes, built on the device.
+
+Edge e of the user–item relation is a pure function of (seed, e)
+(gnnrec_synth_edges, a counter hash), so each rank regenerates the stream and
+keeps the edges of its own users without any graph exchange.
+The reverse relation (item -> user, "bought-by") reuses the same edges and eid
+order, as reference src/utils_data.py:205-214 builds reverse relations.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import ops
+from .inference import GraphShard
+
+BUYS = ("user", "buys", "item")
+BOUGHT_BY = ("item", "bought-by", "user")
+
+
+class GraphMeta:
+    """Minimal metagraph for constructing a ConvModel (reference ConvModel only
+    reads g.canonical_etypes and g.ntypes, src/model.py:376-406)."""
+
+    def __init__(self, canonical_etypes, ntypes):
+        self.canonical_etypes = list(canonical_etypes)
+        self.ntypes = list(ntypes)
+
+
+def zipf_cdf(n: int, s: float, device) -> torch.Tensor:
+    w = 1.0 / torch.arange(1, n + 1, dtype=torch.float64, device=device) ** s
+    c = torch.cumsum(w, 0)
+    return c / c[-1]
+
+
+def bipartite_shard(n_users: int, n_items: int, n_edges: int, rank: int, world: int, device,
+                    seed: int = 11, zipf_s: float = 0.0, chunk: int = 1 << 26,
+                    occurrence: bool = False) -> GraphShard:
+    """This rank's GraphShard of the synthetic (user, buys, item) graph + reverse."""
+    dev = torch.device(device)
+    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, [BUYS, BOUGHT_BY],
+                    dev)
+    cdf = zipf_cdf(n_items, zipf_s, dev) if zipf_s > 0 else None
+    keep_u, keep_i, keep_e = [], [], []
+    item_deg = torch.zeros(n_items, dtype=torch.int64, device=dev)
+    for e0 in range(0, n_edges, chunk):
+        n = min(chunk, n_edges - e0)
+        u, i = ops.synth_edges(seed, e0, n, n_users, n_items, dev, cdf)
+        item_deg += torch.bincount(i, minlength=n_items)
+        if world == 1:
+            keep_u.append(u)
+            keep_i.append(i)
+            keep_e.append(torch.arange(e0, e0 + n, device=dev))
+        else:
+            m = (u >= sh.p_lo) & (u < sh.p_hi)
+            idx = torch.nonzero(m).squeeze(1)
+            keep_u.append(u[idx])
+            keep_i.append(i[idx])
+            keep_e.append(idx + e0)
+        del u, i
+    u = torch.cat(keep_u).to(torch.int64)
+    i = torch.cat(keep_i).to(torch.int64)
+    eid = torch.cat(keep_e)
+    del keep_u, keep_i, keep_e
+    w = ((eid % 8) + 1) if occurrence else None  # deterministic 1..8 'occurrence' counts
+    sh.add_relation(BUYS, u, i, eid, n_edges, weights=w, dst_global_deg=item_deg)
+    sh.add_relation(BOUGHT_BY, i, u, eid, n_edges, weights=w)
+    return sh
+
+
+def node_features(n: int, d: int, seed: int, device, rows: Optional[slice] = None) -> torch.Tensor:
+    """N(0,1) fp32 features from a seeded device generator (partition-independent:
+    every rank draws the full table and keeps its rows)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    x = torch.randn((n, d), generator=gen, device=device, dtype=torch.float32)
+    if rows is not None:
+        x = x[rows].contiguous()
+    return x

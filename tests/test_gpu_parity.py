@@ -1,0 +1,327 @@
+"""GPU parity: every HIP entry point of libgnnrec.so vs the CPU oracle / the
+reference's golden vectors, on seeded inputs.
+
+Tolerances (stated per the north star): embeddings within 1e-4 relative fp32
+(we assert rtol=1e-4, atol=1e-5 element-wise); max-aggregation, sampler index
+sets, generator output and scans bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-4, 1e-5
+DEV = "cuda"
+
+
+def _csr(rng, n_dst, n_src, max_deg, zero_frac=0.2, heavy=None):
+    deg = rng.integers(0, max_deg + 1, n_dst)
+    deg[rng.random(n_dst) < zero_frac] = 0
+    if heavy:
+        deg[0] = heavy  # one huge-degree row
+    indptr = np.zeros(n_dst + 1, np.int64)
+    np.cumsum(deg, out=indptr[1:])
+    idx = rng.integers(0, n_src, int(indptr[-1])).astype(np.int32)
+    return indptr, idx
+
+
+def _t(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.to(DEV) if dtype is None else t.to(DEV, dtype)
+
+
+@pytest.mark.parametrize("d", [16, 32, 64, 100, 128, 256, 7, 300])
+@pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_matches_oracle(d, reduce, weighted):
+    from gnnrec import ops
+    rng = np.random.default_rng(d * 7 + len(reduce) + weighted)
+    indptr, idx = _csr(rng, 700, 900, 12, heavy=3000)
+    X = rng.standard_normal((900, d)).astype(np.float32)
+    w = (rng.integers(1, 9, idx.size)).astype(np.float32) if weighted else None
+    out = ops.spmm(_t(indptr), _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w))
+    ref = oracle.spmm_csr(indptr, idx, X, reduce, w)
+    got = out.cpu().numpy()
+    if reduce == "max":
+        np.testing.assert_array_equal(got, ref)  # max is order-independent: bit-exact
+    else:
+        np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL * max(1, np.abs(ref).max()))
+
+
+def test_spmm_bitwise_deterministic_and_strided_output():
+    from gnnrec import ops
+    rng = np.random.default_rng(5)
+    indptr, idx = _csr(rng, 5000, 4000, 40)
+    X = _t(rng.standard_normal((4000, 128)).astype(np.float32))
+    a = ops.spmm(_t(indptr), _t(idx), X, "mean")
+    b = ops.spmm(_t(indptr), _t(idx), X, "mean")
+    assert torch.equal(a, b)
+    big = torch.zeros(5000, 256, device=DEV)
+    ops.spmm(_t(indptr), _t(idx), X, "mean", out=big[:, 64:192])
+    assert torch.equal(big[:, 64:192], a)
+    assert big[:, :64].abs().sum().item() == 0 and big[:, 192:].abs().sum().item() == 0
+
+
+def test_spmm_empty_and_neginf():
+    from gnnrec import ops
+    indptr = _t(np.array([0, 0, 2, 2], np.int64))
+    idx = _t(np.array([0, 1], np.int32))
+    X = _t(np.array([[1.0, -2.0, 3.0, 4.0], [5.0, -6.0, 0.5, 1.0]], np.float32))
+    out = ops.spmm(indptr, idx, X, "max").cpu().numpy()
+    assert (out[0] == 0).all() and (out[2] == 0).all()
+    np.testing.assert_array_equal(out[1], [5.0, -2.0, 3.0, 4.0])
+    out = ops.spmm(indptr, idx, X, "max", empty_neginf=True).cpu().numpy()
+    assert np.isneginf(out[0]).all() and np.isneginf(out[2]).all()
+    out = ops.spmm(indptr, idx, X, "mean").cpu().numpy()
+    np.testing.assert_allclose(out[1], [3.0, -4.0, 1.75, 2.5])
+    # zero rows / zero edges
+    e = ops.spmm(_t(np.zeros(1, np.int64)), _t(np.zeros(0, np.int32)), X, "mean")
+    assert e.shape == (0, 4)
+
+
+@pytest.mark.parametrize("M,K1,K2,N", [(1000, 128, 128, 128), (777, 64, 64, 64), (300, 5, 256, 256),
+                                       (513, 2, 0, 32), (129, 128, 0, 1), (64, 6, 6, 12),
+                                       (2000, 256, 0, 300)])
+@pytest.mark.parametrize("epi", ["relu_norm", "plain", "sigmoid"])
+def test_gemm_matches_fp64(M, K1, K2, N, epi):
+    from gnnrec import ops
+    if epi == "relu_norm" and N > 256:
+        pytest.skip("L2 norm needs the whole row in one block (N <= 256)")
+    rng = np.random.default_rng(M + K1 + N)
+    A1 = rng.standard_normal((M, K1)).astype(np.float32)
+    W1 = (rng.standard_normal((N, K1)) * 0.1).astype(np.float32)
+    A2 = rng.standard_normal((M, K2)).astype(np.float32) if K2 else None
+    W2 = (rng.standard_normal((N, K2)) * 0.1).astype(np.float32) if K2 else None
+    b = rng.standard_normal(N).astype(np.float32)
+    z = A1.astype(np.float64) @ W1.T.astype(np.float64) + b
+    if K2:
+        z += A2.astype(np.float64) @ W2.T.astype(np.float64)
+    kw = {}
+    if epi == "relu_norm":
+        z = np.maximum(z, 0)
+        n = np.linalg.norm(z, axis=1, keepdims=True)
+        z = z / np.where(n == 0, 1, n)
+        kw = dict(relu=True, l2norm=True)
+    elif epi == "sigmoid":
+        z = 1 / (1 + np.exp(-z))
+        kw = dict(sigmoid=True)
+    out = ops.gemm(_t(A1), _t(W1), None if A2 is None else _t(A2), None if W2 is None else _t(W2),
+                   _t(b), **kw)
+    np.testing.assert_allclose(out.cpu().numpy(), z, rtol=RTOL, atol=ATOL)
+
+
+def test_gemm_accumulate_modes_and_a2_transform():
+    from gnnrec import _lib, ops
+    rng = np.random.default_rng(3)
+    M, K, N = 300, 32, 64
+    A1, A2 = rng.standard_normal((M, K)).astype(np.float32), rng.standard_normal((M, K)).astype(np.float32)
+    W1, W2 = rng.standard_normal((N, K)).astype(np.float32), rng.standard_normal((N, K)).astype(np.float32)
+    deg = rng.integers(0, 4, M).astype(np.int32)
+    base = rng.standard_normal((M, N)).astype(np.float32)
+    a2d = A2 / np.maximum(deg, 1)[:, None]
+    z = np.maximum(A1 @ W1.T + a2d @ W2.T, 0)
+    out = _t(base.copy())
+    ops.gemm(_t(A1), _t(W1), _t(A2), _t(W2), relu=True, accum="add", out_div=2.0, out=out,
+             a2_deg=_t(deg), a2_mode=_lib.A2_DIV_DEG)
+    np.testing.assert_allclose(out.cpu().numpy(), (base + z) / 2, rtol=RTOL, atol=ATOL)
+    a2z = np.where((deg == 0)[:, None], 0, A2)
+    z = np.maximum(A1 @ W1.T + a2z @ W2.T, 0)
+    out = _t(base.copy())
+    ops.gemm(_t(A1), _t(W1), _t(A2), _t(W2), relu=True, accum="max", out=out, a2_deg=_t(deg),
+             a2_mode=_lib.A2_ZERO_DEG)
+    np.testing.assert_allclose(out.cpu().numpy(), np.maximum(base, z), rtol=RTOL, atol=ATOL)
+
+
+def test_sddmm_cos_and_edge_mlp_match_oracle():
+    from gnnrec import ops
+    rng = np.random.default_rng(9)
+    hs = rng.standard_normal((50, 128)).astype(np.float32)
+    hd = rng.standard_normal((40, 128)).astype(np.float32)
+    hs[3] = 0  # zero row -> eps guard
+    src = rng.integers(0, 50, 3000)
+    dst = rng.integers(0, 40, 3000)
+    cos = ops.sddmm_cos(_t(src), _t(dst), _t(hs), _t(hd)).cpu().numpy()
+    ref = oracle.cosine_prediction({("user", "buys", "item"): (src, dst)},
+                                   {"user": hs, "item": hd})[("user", "buys", "item")][:, 0]
+    np.testing.assert_allclose(cos, ref, rtol=RTOL, atol=ATOL)
+    # edge MLP (PredictingLayer re-associated) vs the concatenation form
+    from gnnrec.nn import PredictingLayer
+    torch.manual_seed(0)
+    pl = PredictingLayer(128)
+    p = {k: v.numpy() for k, v in pl.state_dict().items()}
+    ref = oracle.predicting_module({("user", "buys", "item"): (src, dst)},
+                                   {"user": hs, "item": hd}, p)[("user", "buys", "item")][:, 0]
+    pl = pl.to(DEV).eval()
+    with torch.no_grad():
+        got = pl.score_edges(_t(hs), _t(hd), _t(src), _t(dst)).cpu().numpy()
+        got2 = pl(torch.cat([_t(hs)[_t(src)], _t(hd)[_t(dst)]], 1)).cpu().numpy()[:, 0]
+    np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(got2, ref, rtol=RTOL, atol=ATOL)
+
+
+# ----------------------------------------------------------- golden models --
+def _gpu_graph(a):
+    from gnnrec.graph import HeteroGraph
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d)) for ce, (s, d) in edges.items()},
+                    num_nodes, device=DEV)
+    for ce, o in occ.items():
+        if ce[0] in ("user", "item") and ce[2] in ("user", "item"):
+            g._edata[ce]["occurrence"] = torch.from_numpy(o).to(DEV)
+    return g, num_nodes, edges
+
+
+CASES = golden_io.manifest()
+
+
+@pytest.mark.parametrize("name", sorted(k for k, v in CASES.items() if v["kind"] == "convlayer"))
+def test_convlayer_golden(name):
+    from gnnrec.nn import ConvLayer
+    meta = CASES[name]
+    a = golden_io.load(name)
+    g, _, _ = _gpu_graph(a)
+    ce = tuple(meta["etype"])
+    layer = ConvLayer((a["x_neigh"].shape[1], a["x_self"].shape[1]), meta["out_feats"], 0.0,
+                      meta["aggregator_type"], meta["norm"])
+    layer.load_state_dict({k: torch.from_numpy(v) for k, v in golden_io.state_dict(a).items()})
+    layer = layer.to(DEV).eval()
+    with torch.no_grad():
+        z = layer(g[ce], (_t(a["x_neigh"]), _t(a["x_self"])))
+    np.testing.assert_allclose(z.cpu().numpy(), a["out"], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("name", sorted(k for k, v in CASES.items() if v["kind"] == "model"))
+def test_model_golden_full_graph_heads_loss(name):
+    from gnnrec import nn as gnn
+    from gnnrec.graph import PairGraph
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    meta = CASES[name]
+    a = golden_io.load(name)
+    g, num_nodes, edges = _gpu_graph(a)
+    model = gnn.ConvModel(g, meta["n_layers"], meta["dim_dict"], meta["norm"], 0.0,
+                          meta["aggregator_type"], meta["pred"], meta["aggregator_hetero"],
+                          meta["embedding_layer"])
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in golden_io.state_dict(a).items()})
+    model = model.to(DEV).eval()
+    feats = {k[5:]: _t(v) for k, v in a.items() if k.startswith("feat/")}
+    with torch.no_grad():
+        h = full_graph_embeddings(g, model, feats)
+        for nt in h:
+            np.testing.assert_allclose(h[nt].cpu().numpy(), a["h/" + nt], rtol=RTOL, atol=ATOL)
+        # the sharded driver at world size 1 is the same computation, bit for bit
+        sh = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
+        hs = ShardedFullGraphPass(model, sh).run(sh.local_features(feats))
+        for nt in h:
+            assert torch.equal(hs[nt][: num_nodes[nt]], h[nt]), nt
+        # ConvModel.forward with the full graph as every block + heads + loss
+        empty = (torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64))
+        pos = PairGraph({ce: ((torch.from_numpy(a["pos/src"]), torch.from_numpy(a["pos/dst"]))
+                              if ce == ("user", "buys", "item") else empty) for ce in edges},
+                        {nt: torch.arange(n) for nt, n in num_nodes.items()}).to(DEV)
+        neg = PairGraph({ce: ((torch.from_numpy(a["neg/src"]), torch.from_numpy(a["neg/dst"]))
+                              if ce == ("user", "buys", "item") else empty) for ce in edges},
+                        {nt: torch.arange(n) for nt, n in num_nodes.items()}).to(DEV)
+        n_blocks = meta["n_layers"] - 1 if meta["embedding_layer"] else meta["n_layers"]
+        h2, ps, ns = model([g] * n_blocks, dict(feats), pos, neg, meta["embedding_layer"])
+        ref_ps, ref_ns = golden_io.by_etype(a, "pos_score"), golden_io.by_etype(a, "neg_score")
+        assert set(ps) == set(ref_ps)
+        for ce in ref_ps:
+            np.testing.assert_allclose(ps[ce].cpu().numpy(), ref_ps[ce], rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(ns[ce].cpu().numpy(), ref_ns[ce], rtol=RTOL, atol=ATOL)
+        mask = {ce: _t(v) for ce, v in golden_io.by_etype(a, "mask").items()}
+        loss = gnn.max_margin_loss(ps, ns, meta["delta"], meta["neg_sample_size"], True,
+                                   {("user", "buys", "item"): _t(a["recency"])}, True, mask)
+        np.testing.assert_allclose(loss.item(), a["loss"], rtol=RTOL, atol=ATOL)
+
+
+# ---------------------------------------------------------------- sampler ---
+@pytest.mark.parametrize("fanout", [-1, 1, 3, 10])
+@pytest.mark.parametrize("exclude", [False, True])
+def test_sampler_bit_exact_vs_oracle(fanout, exclude):
+    from gnnrec import ops
+    rng = np.random.default_rng(21)
+    n, E = 2000, 30000
+    src = rng.integers(0, 3000, E)
+    dst = rng.integers(0, n, E)
+    indptr, indices, eids = oracle.csr_from_coo(src, dst, n)
+    seeds = rng.choice(n, 300, replace=False).astype(np.int64)
+    excl = (rng.random(E) < 0.3).astype(np.uint8) if exclude else None
+    key = 12345
+    r_ip, r_src, r_eid = oracle.sample_neighbors(indptr, indices.astype(np.int64), eids, seeds,
+                                                 fanout, key, excl)
+    g_ip, g_src, g_eid = ops.sample_neighbors(_t(indptr), _t(indices.astype(np.int64)), _t(eids),
+                                              _t(seeds), fanout, key,
+                                              None if excl is None else _t(excl))
+    np.testing.assert_array_equal(g_ip.cpu().numpy(), r_ip)
+    np.testing.assert_array_equal(g_src.cpu().numpy(), r_src)
+    np.testing.assert_array_equal(g_eid.cpu().numpy(), r_eid)
+    # structural: every sampled edge is a real in-edge of its seed, none excluded, no dup
+    for i in range(0, seeds.size, 37):
+        es = g_eid.cpu().numpy()[r_ip[i]:r_ip[i + 1]]
+        assert (dst[es] == seeds[i]).all()
+        assert len(set(es.tolist())) == es.size
+        if excl is not None:
+            assert not excl[es].any()
+        deg = indptr[seeds[i] + 1] - indptr[seeds[i]]
+        if fanout >= 0 and excl is None:
+            assert es.size == min(deg, fanout)
+
+
+def test_relabel_and_scan_bit_exact():
+    from gnnrec import ops
+    rng = np.random.default_rng(4)
+    for n in (0, 1, 5, 2047, 2048, 2049, 100_000):
+        x = rng.integers(0, 50, n).astype(np.int64)
+        got = ops.exclusive_scan(_t(x)).cpu().numpy()
+        ref = np.concatenate([[0], np.cumsum(x)])
+        np.testing.assert_array_equal(got, ref)
+    N = 5000
+    prefix = rng.choice(N, 200, replace=False).astype(np.int64)
+    lists = [rng.integers(0, N, 3000).astype(np.int64), rng.integers(0, N, 10).astype(np.int64)]
+    rl = ops.Relabeler(N, DEV)
+    nodes, locs = rl.relabel(_t(prefix), [_t(x) for x in lists])
+    r_nodes, r_locs = oracle.to_block_relabel(prefix, lists)
+    np.testing.assert_array_equal(nodes.cpu().numpy(), r_nodes)
+    for l, r in zip(locs, r_locs):
+        np.testing.assert_array_equal(l.cpu().numpy(), r)
+    # scratch is clean for the next batch
+    assert rl.mark.sum().item() == 0 and (rl.prefix_pos == -1).all().item()
+
+
+def test_synth_edges_bit_exact():
+    from gnnrec import ops
+    for cdf in (None, oracle.zipf_cdf(1000, 1.0)):
+        u, i = ops.synth_edges(11, 12345, 100_000, 7919, 1000, DEV,
+                               None if cdf is None else _t(cdf))
+        ru, ri = oracle.synth_edges(11, 12345, 100_000, 7919, 1000, cdf)
+        np.testing.assert_array_equal(u.cpu().numpy(), ru)
+        np.testing.assert_array_equal(i.cpu().numpy(), ri)
+
+
+# -------------------------------------------------- full-size properties ---
+def test_c2_scale_rows_vs_oracle_and_determinism():
+    """C2-shaped relation (1M dst rows, 50M edges, d=64): spot-check rows against the
+    oracle and require bitwise run-to-run equality (size-independent properties)."""
+    from gnnrec import ops
+    from gnnrec.graph import build_csr
+    n_u, n_i, E, d = 1_000_000, 100_000, 50_000_000, 64
+    u, i = ops.synth_edges(11, 0, E, n_u, n_i, DEV)
+    indptr, idx, _ = build_csr(i.long(), u.long(), n_u)   # item -> user (dst user)
+    X = torch.randn(n_i, d, device=DEV)
+    a = ops.spmm(indptr, idx, X, "mean")
+    b = ops.spmm(indptr, idx, X, "mean")
+    assert torch.equal(a, b)
+    rows = torch.randint(0, n_u, (2000,), device=DEV)
+    ip = indptr.cpu().numpy()
+    sel = rows.cpu().numpy()
+    sub_ip = np.zeros(sel.size + 1, np.int64)
+    np.cumsum(ip[sel + 1] - ip[sel], out=sub_ip[1:])
+    ix = idx.cpu().numpy()
+    sub_idx = np.concatenate([ix[ip[r]:ip[r + 1]] for r in sel]).astype(np.int32)
+    ref = oracle.spmm_csr(sub_ip, sub_idx, X.cpu().numpy(), "mean")
+    np.testing.assert_allclose(a[rows].cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    # degree conservation: sum of degrees == E, mean degree 50
+    assert int(indptr[-1].item()) == E
