@@ -92,6 +92,26 @@ def spmm_algorithmic_bytes(shard, d):
     return tot, n
 
 
+def pmc_traffic(args, world):
+    """HBM bytes per aggregation launch from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x2 for gfx950's half-counted wide reads + WRITE_SIZE, KB -> B), for
+    the default single-GPU C4 workload they were collected on; None otherwise."""
+    import csv
+    default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator) == \
+        (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean")
+    f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch_size.csv")
+    w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write_size.csv")
+    if world != 1 or not default or not (os.path.exists(f) and os.path.exists(w)):
+        return None
+    tot, n = 0.0, 0
+    for path, scale in ((f, 2.0), (w, 1.0)):
+        for r in csv.DictReader(open(path)):
+            if "spmm" in r["Kernel_Name"]:
+                tot += float(r["Counter_Value"]) * 1024 * scale
+                n += scale == 2.0
+    return tot / n if n else None
+
+
 def cpu_baseline(args, d):
     """Bounded sample of the same workload on the host cores: the oracle's C/OpenMP
     restatement of DGL 0.5's CPU SpMM + numpy fp32 GEMMs (kind 'port')."""
@@ -141,10 +161,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if world > 1:
+        # RCCL over xGMI; GNNREC_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        backend = os.environ.get("GNNREC_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from gnnrec import nn as gnn
     from gnnrec.dist import Exchange
@@ -216,7 +241,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": None,
+                         "traffic": pmc_traffic(args, world),
                          "kernel": "gnnrec spmm_csr_kernel (gather + segmented mean)",
                          "bytes_per_launch": bytes_per_launch, "launch_ms": spmm_ms,
                          "launches_timed": n_launch},

@@ -1,0 +1,318 @@
+"""GPU block sampling and loaders — drop-ins for the DGL 0.5.2 dataloading API
+used by reference src/sampling.py:117-243 and main_inference.py:124-138.
+
+  MultiLayerFullNeighborSampler(n_layers)        sampling.py:157, main_inference.py:129
+  MultiLayerNeighborSampler(fanouts, replace=False)  sampling.py:159
+  negative_sampler.Uniform(k)                    sampling.py:163-165
+  NodeDataLoader(g, nids, sampler, batch_size, shuffle, drop_last, ...)  :209-241
+  EdgeDataLoader(g, eids, sampler, exclude='reverse_types', reverse_etypes,
+                 g_sampling, negative_sampler, batch_size, shuffle, ...)  :167-207
+
+Everything runs on the device in the caller's process: per relation the
+in-edges of the seeds are counted, scanned and copied by the HIP sampler
+(gnnrec_sample_count/fill — fanout choices by a counter hash, eid exclusion
+after sampling as DGL's BlockSampler does), then per node type the sources
+are relabelled by mark/scan/compact (dst prefix first, new ids ascending).
+There are no DataLoader worker processes, no pinned host copies and no
+per-batch host->device transfer of blocks (reference run.py:104-107, 338-339).
+`num_workers` / `pin_memory` are accepted and ignored.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+from .graph import Block, EID, HeteroGraph, NID, PairGraph
+
+
+def _mix(*xs) -> int:
+    h = 0x9E3779B97F4A7C15
+    for x in xs:
+        h = ((h ^ (int(x) & 0xFFFFFFFFFFFFFFFF)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        h ^= h >> 31
+    return h
+
+
+class BlockSampler:
+    """Multi-layer block sampler base (DGL BlockSampler.sample_blocks semantics)."""
+
+    def __init__(self, num_layers: int, fanouts=None, replace: bool = False, seed: int = None):
+        if replace:
+            raise NotImplementedError("sampling with replacement is not used by the reference")
+        self.num_layers = num_layers
+        self.fanouts = fanouts
+        self.seed = int(seed) if seed is not None else int(torch.initial_seed())
+        self._calls = 0
+        self._relabelers = {}
+        self._exclude_masks = {}
+
+    def _fanout(self, block_id: int, ce) -> int:
+        if self.fanouts is None:
+            return -1
+        f = self.fanouts[block_id]
+        if isinstance(f, dict):
+            f = f.get(ce, f.get(ce[1], -1))
+        return -1 if f is None else int(f)
+
+    def _relabeler(self, g, nt):
+        key = (id(g), nt)
+        r = self._relabelers.get(key)
+        if r is None:
+            r = ops.Relabeler(g.num_nodes(nt), g.device)
+            self._relabelers[key] = r
+        return r
+
+    def _mask(self, g, ce):
+        key = (id(g), ce)
+        m = self._exclude_masks.get(key)
+        if m is None:
+            m = torch.zeros(g.num_edges(ce), dtype=torch.uint8, device=g.device)
+            self._exclude_masks[key] = m
+        return m
+
+    def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
+                      exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None) -> List[Block]:
+        self._calls += 1
+        seeds = {nt: torch.as_tensor(v, dtype=torch.int64, device=g.device)
+                 for nt, v in seed_nodes.items()}
+        masks = {}
+        if exclude_eids:
+            for ce, eids in exclude_eids.items():
+                ce = g.to_canonical_etype(ce)
+                m = self._mask(g, ce)
+                m[eids] = 1
+                masks[ce] = (m, eids)
+        blocks = []
+        try:
+            for block_id in reversed(range(self.num_layers)):
+                block = self._one_block(g, seeds, block_id, masks)
+                blocks.insert(0, block)
+                seeds = {nt: block.srcdata[NID][nt] for nt in block.ntypes
+                         if block.number_of_src_nodes(nt) > 0}
+        finally:
+            for ce, (m, eids) in masks.items():
+                m[eids] = 0
+        # copy edge data into every block and node data into the input block (DGL copies
+        # features at block creation; the reference reads blocks[0].srcdata['features'])
+        for b in blocks:
+            for ce in b.canonical_etypes:
+                eid = b._edata[ce][EID]
+                for k, v in g._edata[ce].items():
+                    b._edata[ce][k] = v[eid]
+        b0 = blocks[0]
+        for nt in b0.ntypes:
+            ids = b0._src[nt][NID]
+            for k, v in g._ndata[nt].items():
+                b0._src[nt][k] = v[ids]
+        return blocks
+
+    def _one_block(self, g, seeds, block_id, masks) -> Block:
+        rels = {}
+        src_lists: Dict[str, list] = {}
+        for r_idx, ce in enumerate(g.canonical_etypes):
+            s_t, _, d_t = ce
+            dseeds = seeds.get(d_t)
+            if dseeds is None:
+                dseeds = torch.zeros(0, dtype=torch.int64, device=g.device)
+            indptr, indices, eids = g.in_csr_global(ce)
+            key = _mix(self.seed, self._calls, block_id, r_idx)
+            mask = masks.get(ce, (None,))[0]
+            o_ip, o_src, o_eid = ops.sample_neighbors(indptr, indices, eids, dseeds,
+                                                      self._fanout(block_id, ce), key, mask)
+            rels[ce] = [o_ip, o_src, o_eid]
+            src_lists.setdefault(s_t, []).append(ce)
+        src_nid, num_dst = {}, {}
+        for nt in g.ntypes:
+            prefix = seeds.get(nt, torch.zeros(0, dtype=torch.int64, device=g.device))
+            num_dst[nt] = int(prefix.numel())
+            ces = src_lists.get(nt, [])
+            nodes, locs = self._relabeler(g, nt).relabel(prefix, [rels[ce][1] for ce in ces])
+            src_nid[nt] = nodes
+            for ce, loc in zip(ces, locs):
+                rels[ce][1] = loc.to(torch.int32)
+        return Block(src_nid, num_dst, {ce: tuple(v) for ce, v in rels.items()})
+
+
+class MultiLayerFullNeighborSampler(BlockSampler):
+    """All in-edges of every seed at every layer (dgl.dataloading, reference sampling.py:157)."""
+
+    def __init__(self, n_layers: int, return_eids: bool = False):
+        super().__init__(n_layers, None)
+
+
+class MultiLayerNeighborSampler(BlockSampler):
+    """fanouts[i] in-edges per seed (without replacement) for block i (sampling.py:159)."""
+
+    def __init__(self, fanouts, replace: bool = False, return_eids: bool = False, seed=None):
+        super().__init__(len(fanouts), list(fanouts), replace, seed)
+
+
+class _Uniform:
+    """negative_sampler.Uniform(k): src repeated k times, dst uniform over the dst type."""
+
+    def __init__(self, k: int):
+        self.k = k
+
+    def __call__(self, g: HeteroGraph, eids: Dict[tuple, torch.Tensor]):
+        out = {}
+        for ce, e in eids.items():
+            ce = g.to_canonical_etype(ce)
+            src, _ = g.find_edges(e, etype=ce)
+            src = src.repeat_interleave(self.k)
+            dst = torch.randint(0, g.num_nodes(ce[2]), (src.numel(),), device=src.device)
+            out[ce] = (src, dst)
+        return out
+
+
+class _NegNS:
+    Uniform = _Uniform
+
+
+negative_sampler = _NegNS
+
+
+def _batches(n: int, batch_size: int, shuffle: bool, drop_last: bool, device):
+    order = torch.randperm(n, device=device) if shuffle else torch.arange(n, device=device)
+    stop = (n // batch_size) * batch_size if drop_last else n
+    for i in range(0, stop, batch_size):
+        yield order[i:i + batch_size]
+
+
+class NodeDataLoader:
+    """Yields (input_nodes, output_nodes, blocks) for batches of seed nodes."""
+
+    def __init__(self, g: HeteroGraph, nids, block_sampler: BlockSampler, device=None,
+                 batch_size: int = 1, shuffle: bool = False, drop_last: bool = False,
+                 num_workers: int = 0, **kwargs):
+        self.g = g
+        self.sampler = block_sampler
+        dev = g.device
+        if not isinstance(nids, dict):
+            nids = {g.ntypes[0]: nids}
+        self.types = list(nids.keys())
+        ids = [torch.as_tensor(nids[nt], dtype=torch.int64).to(dev) for nt in self.types]
+        self.flat_ids = torch.cat(ids) if ids else torch.zeros(0, dtype=torch.int64, device=dev)
+        self.flat_type = torch.cat([torch.full((t.numel(),), i, dtype=torch.int64, device=dev)
+                                    for i, t in enumerate(ids)]) if ids else self.flat_ids
+        self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+
+    def __len__(self):
+        n = self.flat_ids.numel()
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
+                            self.drop_last, self.g.device):
+            ids, ty = self.flat_ids[idx], self.flat_type[idx]
+            seeds = {nt: ids[ty == i] for i, nt in enumerate(self.types)}
+            seeds = {nt: v for nt, v in seeds.items() if v.numel() > 0}
+            blocks = self.sampler.sample_blocks(self.g, seeds)
+            input_nodes = blocks[0].srcdata[NID]
+            output_nodes = {nt: blocks[-1].dstdata[NID][nt] for nt in seeds}
+            yield input_nodes, output_nodes, blocks
+
+
+class EdgeDataLoader:
+    """Yields (input_nodes, pos_graph, neg_graph, blocks) for batches of edges
+    (or (input_nodes, pair_graph, blocks) without a negative sampler)."""
+
+    def __init__(self, g: HeteroGraph, eids, block_sampler: BlockSampler, device=None,
+                 g_sampling: Optional[HeteroGraph] = None, exclude: Optional[str] = None,
+                 reverse_eids=None, reverse_etypes: Optional[dict] = None,
+                 negative_sampler=None, batch_size: int = 1, shuffle: bool = False,
+                 drop_last: bool = False, num_workers: int = 0, pin_memory: bool = False,
+                 **kwargs):
+        self.g = g
+        self.g_sampling = g_sampling if g_sampling is not None else g
+        self.sampler = block_sampler
+        self.exclude = exclude
+        if exclude not in (None, 'reverse_types', 'self'):
+            raise NotImplementedError(f"exclude={exclude!r}")
+        self.reverse_etypes = {self.g.to_canonical_etype(k): self.g.to_canonical_etype(v)
+                               for k, v in (reverse_etypes or {}).items()}
+        self.negative_sampler = negative_sampler
+        dev = g.device
+        if not isinstance(eids, dict):
+            eids = {g.canonical_etypes[0]: eids}
+        self.types = [g.to_canonical_etype(k) for k in eids]
+        ids = [torch.as_tensor(eids[k], dtype=torch.int64).to(dev) for k in eids]
+        self.flat_ids = torch.cat(ids)
+        self.flat_type = torch.cat([torch.full((t.numel(),), i, dtype=torch.int64, device=dev)
+                                    for i, t in enumerate(ids)])
+        self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+
+    def __len__(self):
+        n = self.flat_ids.numel()
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def _compact(self, pos_edges, neg_edges):
+        """DGL compact_graphs([pos, neg]): both pair graphs over the union of their nodes
+        (ascending global id per type)."""
+        g = self.g
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        per_type: Dict[str, list] = {}
+        for edges in (pos_edges, neg_edges):
+            for ce, (s, d) in edges.items():
+                per_type.setdefault(ce[0], []).append(s)
+                per_type.setdefault(ce[2], []).append(d)
+        node_ids, local = {}, {}
+        for nt in g.ntypes:
+            lists = per_type.get(nt, [])
+            r = self.sampler._relabeler(g, nt)
+            nodes, locs = r.relabel(empty, lists)
+            node_ids[nt] = nodes
+            local[nt] = locs
+        cursor = {nt: 0 for nt in g.ntypes}
+
+        def take(nt):
+            v = local[nt][cursor[nt]]
+            cursor[nt] += 1
+            return v
+
+        pos_l = {ce: None for ce in pos_edges}
+        neg_l = {ce: None for ce in neg_edges}
+        for edges, dst_map in ((pos_edges, pos_l), (neg_edges, neg_l)):
+            for ce in edges:
+                s = take(ce[0])
+                d = take(ce[2])
+                dst_map[ce] = (s, d)
+        return node_ids, pos_l, neg_l
+
+    def __iter__(self):
+        g = self.g
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
+                            self.drop_last, g.device):
+            ids, ty = self.flat_ids[idx], self.flat_type[idx]
+            batch = {ce: ids[ty == i] for i, ce in enumerate(self.types)}
+            batch = {ce: v for ce, v in batch.items() if v.numel() > 0}
+            pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch else (empty, empty)
+                         for ce in g.canonical_etypes}
+            neg_edges = {}
+            if self.negative_sampler is not None:
+                neg = self.negative_sampler(g, batch)
+                neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
+            node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
+            pos_g = PairGraph(pos_l, node_ids)
+            for ce, e in batch.items():
+                for k, v in g._edata[ce].items():
+                    pos_g._edata[ce][k] = v[e]
+                pos_g._edata[ce][EID] = e
+            exclude = None
+            if self.exclude == 'reverse_types':
+                exclude = {}
+                for ce, e in batch.items():
+                    exclude[ce] = e
+                    if ce in self.reverse_etypes:
+                        exclude[self.reverse_etypes[ce]] = e
+            elif self.exclude == 'self':
+                exclude = dict(batch)
+            seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
+            blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude)
+            input_nodes = blocks[0].srcdata[NID]
+            if self.negative_sampler is None:
+                yield input_nodes, pos_g, blocks
+            else:
+                yield input_nodes, pos_g, PairGraph(neg_l, node_ids), blocks

@@ -1,0 +1,78 @@
+"""Two ranks on ONE GPU (gloo transport, HIP kernels for all arithmetic): the sharded
+full-graph pass must reproduce the single-process GPU pass.  (RCCL itself needs
+one GPU per rank; the collectives' nccl forms run in the driver's multi-GPU bench.)"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _build(agg, hetero):
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    rng = np.random.default_rng(0)
+    n_u, n_i, E = 3000, 700, 40000
+    u = rng.integers(0, n_u, E)
+    i = rng.integers(0, n_i, E)
+    g = HeteroGraph({("user", "buys", "item"): (torch.from_numpy(u), torch.from_numpy(i)),
+                     ("item", "bought-by", "user"): (torch.from_numpy(i), torch.from_numpy(u))},
+                    {"user": n_u, "item": n_i}, device="cuda")
+    occ = torch.from_numpy(rng.integers(1, 9, E)).cuda()
+    g.edges["buys"].data["occurrence"] = occ
+    g.edges["bought-by"].data["occurrence"] = occ
+    feats = {"user": torch.from_numpy(rng.standard_normal((n_u, 32)).astype(np.float32)).cuda(),
+             "item": torch.from_numpy(rng.standard_normal((n_i, 32)).astype(np.float32)).cuda()}
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 32, "item": 32, "hidden": 64, "out": 32}, True, 0.0, agg,
+                          "cos", hetero, True).cuda().eval()
+    return g, feats, model
+
+
+def _worker(rank, world, port, agg, hetero, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gnnrec.dist import Exchange
+        from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
+        g, feats, model = _build(agg, hetero)
+        ex = Exchange()
+        sh = GraphShard.from_graph(g, rank, world, "user", device="cuda")
+        out = ShardedFullGraphPass(model, sh, ex).run(sh.local_features(feats))
+        users = gather_partitioned(sh, out["user"], ex)
+        q.put((rank, users.cpu().numpy(), out["item"][:700].cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("agg,hetero", [("mean", "sum"), ("pool_nn_edge", "max")])
+def test_two_ranks_one_gpu_match_single_process(agg, hetero):
+    import torch.multiprocessing as mp
+    from gnnrec.inference import full_graph_embeddings
+    g, feats, model = _build(agg, hetero)
+    with torch.no_grad():
+        ref = full_graph_embeddings(g, model, feats)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, agg, hetero, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, users, items in res:
+        np.testing.assert_allclose(users, ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(items, ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
