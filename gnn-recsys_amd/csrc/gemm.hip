@@ -104,9 +104,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         else rowzero[i] = (dg == 0);
       }
     }
-#pragma unroll 1
-    for (int64_t k0 = 0; k0 < K; k0 += BK) {
-      f32x4 ra[4];
+    // register prefetch: tile k+1 is loaded from global while tile k is in the MFMAs
+    f32x4 ra[4], rw[NT];
+    auto load_tile = [&](int64_t k0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int idx = tid + i * 256;
@@ -118,7 +118,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
           else if (rowzero[i]) ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      f32x4 rw[NT];
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         const int idx = tid + i * 256;
@@ -126,6 +125,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         const int64_t gk = k0 + (idx & 7) * 4;
         rw[i] = load4(W, gn, K, gk, K, gn < g.N, vecW);
       }
+    };
+    load_tile(0);
+#pragma unroll 1
+    for (int64_t k0 = 0; k0 < K; k0 += BK) {
       __syncthreads();  // previous tile fully consumed
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         *reinterpret_cast<f32x4*>(Ws + (idx >> 3) * LDSK + (idx & 7) * 4) = rw[i];
       }
       __syncthreads();
+      if (k0 + BK < K) load_tile(k0 + BK);
       const float* Ar = As + (wave * 32 + r) * LDSK + h * 16;
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {

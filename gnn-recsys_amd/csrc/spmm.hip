@@ -14,10 +14,12 @@
 //   * 64 neighbour indices are fetched with one coalesced 256-B load and
 //     broadcast with ds_bpermute (__shfl); UNROLL wave-instructions are issued
 //     back to back so every lane keeps UNROLL x 16 B in flight;
-//   * neighbour k of a row always lands in lane group k % NPI and groups are
-//     combined by a fixed xor-tree, so the per-row reduction order depends only
-//     on the CSR row: results are bitwise reproducible and identical for any
-//     row partition across ranks.
+//   * neighbour k of a range always lands in lane group k % NPI and groups are
+//     combined by a fixed xor-tree, so the reduction order depends only on the
+//     CSR row: results are bitwise reproducible run to run.
+// Heavy rows (deg > split, e.g. Zipf-popular items) are skipped by the row
+// kernel and reduced instead by one wave per `split`-edge chunk into a
+// workspace, then combined per row in chunk order (deterministic two-phase).
 #include "common.hpp"
 #include <cmath>
 
@@ -48,134 +50,254 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   }
 }
 
+template <int REDUCE>
+__device__ __forceinline__ float combine(float a, float b) {
+  return REDUCE == GNNREC_REDUCE_MAX ? fmaxf(a, b) : a + b;
+}
+
+// Per-lane partial reduction of edges [beg, end) (lane group grp takes k % NPI == grp).
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
+__device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
+                                             const int32_t* __restrict__ indices,
+                                             const float* __restrict__ ew,
+                                             const float* __restrict__ X, int64_t ldx, int col,
+                                             bool colok, int lane, int grp, Frag<VEC>& acc) {
+  constexpr int NPI = kWave / LPR;
+  for (int64_t base = beg; base < end; base += 64) {
+    const int cnt = (int)((end - base) < 64 ? (end - base) : 64);
+    const int myidx = lane < cnt ? indices[base + lane] : 0;
+    float myw = 0.f;
+    if constexpr (WEIGHTED) myw = lane < cnt ? ew[base + lane] : 0.f;
+    for (int j = 0; j < cnt; j += NPI * UNROLL) {
+      Frag<VEC> val[UNROLL];
+      bool ok[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int k = j + u * NPI + grp;
+        ok[u] = (k < cnt) && colok;
+        const int src = __shfl(myidx, k & 63);
+        if (ok[u]) {
+          load_frag<VEC>(val[u], X + (int64_t)src * ldx + col);
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        float w = 1.f;
+        if constexpr (WEIGHTED) w = __shfl(myw, (j + u * NPI + grp) & 63);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const float m = WEIGHTED ? val[u].v[v] * w : val[u].v[v];
+          if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+            if (ok[u]) acc.v[v] = fmaxf(acc.v[v], m);
+          } else {
+            acc.v[v] += m;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int LPR, int VEC, int REDUCE>
+__device__ __forceinline__ void combine_groups(Frag<VEC>& acc) {
+#pragma unroll
+  for (int off = LPR; off < kWave; off <<= 1) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(acc.v[v], __shfl_xor(acc.v[v], off));
+  }
+}
+
+template <int VEC, int REDUCE>
+__device__ __forceinline__ void finalize(Frag<VEC>& acc, int64_t deg, int empty_neginf) {
+  if constexpr (REDUCE == GNNREC_REDUCE_MEAN) {
+    const float dd = (float)(deg > 0 ? deg : 1);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc.v[v] = acc.v[v] / dd;
+  } else if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+    if (deg == 0 && !empty_neginf) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
+    }
+  }
+}
+
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
-    float* __restrict__ out, int64_t ldo, int empty_neginf) {
-  constexpr int NPI = kWave / LPR;  // neighbour rows per wave-instruction
+    float* __restrict__ out, int64_t ldo, int empty_neginf, int64_t max_deg) {
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
   const int col = blockIdx.y * (LPR * VEC) + (lane % LPR) * VEC;
   const bool colok = col < d;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_dst; row += wstride) {
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
+    if (end - beg > max_deg) continue;  // heavy row: reduced by the chunk kernels
     Frag<VEC> acc;
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc.v[v] = init;
-
-    for (int64_t base = beg; base < end; base += 64) {
-      const int cnt = (int)((end - base) < 64 ? (end - base) : 64);
-      const int myidx = lane < cnt ? indices[base + lane] : 0;
-      float myw = 0.f;
-      if constexpr (WEIGHTED) myw = lane < cnt ? ew[base + lane] : 0.f;
-      for (int j = 0; j < cnt; j += NPI * UNROLL) {
-        Frag<VEC> val[UNROLL];
-        bool ok[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-          const int k = j + u * NPI + grp;
-          ok[u] = (k < cnt) && colok;
-          const int src = __shfl(myidx, k & 63);
-          if (ok[u]) {
-            load_frag<VEC>(val[u], X + (int64_t)src * ldx + col);
-          } else {
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-          float w = 1.f;
-          if constexpr (WEIGHTED) w = __shfl(myw, (j + u * NPI + grp) & 63);
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            const float m = WEIGHTED ? val[u].v[v] * w : val[u].v[v];
-            if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
-              if (ok[u]) acc.v[v] = fmaxf(acc.v[v], m);
-            } else {
-              acc.v[v] += m;
-            }
-          }
-        }
-      }
-    }
-    // combine the NPI lane groups with a fixed xor tree
-#pragma unroll
-    for (int off = LPR; off < kWave; off <<= 1) {
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        const float o = __shfl_xor(acc.v[v], off);
-        acc.v[v] = (REDUCE == GNNREC_REDUCE_MAX) ? fmaxf(acc.v[v], o) : acc.v[v] + o;
-      }
-    }
-    const int64_t deg = end - beg;
-    if constexpr (REDUCE == GNNREC_REDUCE_MEAN) {
-      const float dd = (float)(deg > 0 ? deg : 1);
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) acc.v[v] = acc.v[v] / dd;
-    } else if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
-      if (deg == 0 && !empty_neginf) {
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
-      }
-    }
+    gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL>(beg, end, indices, ew, X, ldx, col, colok,
+                                                     lane, grp, acc);
+    combine_groups<LPR, VEC, REDUCE>(acc);
+    finalize<VEC, REDUCE>(acc, end - beg, empty_neginf);
     if (grp == 0 && colok) store_frag<VEC>(out + row * ldo + col, acc);
   }
 }
 
-template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
-int launch4(const int64_t* indptr, const int32_t* indices, const float* ew, const float* X,
-            int64_t ldx, int64_t n_dst, int d, float* out, int64_t ldo, int flags, hipStream_t s) {
-  constexpr int UNROLL = (VEC == 4) ? 4 : 2;
-  const int64_t waves_needed = n_dst;
-  int64_t blocks = (waves_needed + 3) / 4;
+// phase 1 of heavy rows: one wave per chunk of `split` edges -> raw partial in ws[chunk]
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
+__global__ __launch_bounds__(256) void spmm_chunk_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int d,
+    int64_t split, const int64_t* __restrict__ heavy_rows, const int64_t* __restrict__ chunk_ptr,
+    const int64_t* __restrict__ chunk_row, int64_t n_chunks, float* __restrict__ ws) {
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / LPR;
+  const int col = blockIdx.y * (LPR * VEC) + (lane % LPR) * VEC;
+  const bool colok = col < d;
+  const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += wstride) {
+    const int64_t h = chunk_row[c];
+    const int64_t row = heavy_rows[h];
+    const int64_t rbeg = indptr[row], rend = indptr[row + 1];
+    const int64_t beg = rbeg + (c - chunk_ptr[h]) * split;
+    const int64_t end = (beg + split < rend) ? beg + split : rend;
+    Frag<VEC> acc;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc.v[v] = init;
+    gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL>(beg, end, indices, ew, X, ldx, col, colok,
+                                                     lane, grp, acc);
+    combine_groups<LPR, VEC, REDUCE>(acc);
+    if (grp == 0 && colok) store_frag<VEC>(ws + c * (int64_t)d + col, acc);
+  }
+}
+
+// phase 2 of heavy rows: one wave per heavy row, partials combined in chunk order
+template <int VEC, int REDUCE>
+__global__ __launch_bounds__(256) void spmm_combine_kernel(
+    const int64_t* __restrict__ indptr, int d, const int64_t* __restrict__ heavy_rows,
+    int64_t n_heavy, const int64_t* __restrict__ chunk_ptr, const float* __restrict__ ws,
+    float* __restrict__ out, int64_t ldo, int empty_neginf) {
+  const int lane = threadIdx.x & 63;
+  const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); h < n_heavy; h += wstride) {
+    const int64_t row = heavy_rows[h];
+    const int64_t deg = indptr[row + 1] - indptr[row];
+    for (int col = blockIdx.y * 64 * VEC + lane * VEC; col < d; col += gridDim.y * 64 * VEC) {
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = init;
+      for (int64_t c = chunk_ptr[h]; c < chunk_ptr[h + 1]; ++c) {
+        Frag<VEC> p;
+        load_frag<VEC>(p, ws + c * (int64_t)d + col);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(acc.v[v], p.v[v]);
+      }
+      finalize<VEC, REDUCE>(acc, deg, empty_neginf);
+      store_frag<VEC>(out + row * ldo + col, acc);
+    }
+  }
+}
+
+struct SpmmArgs {
+  const int64_t* indptr; const int32_t* indices; const float* ew; const float* X; int64_t ldx;
+  int64_t n_dst; int d; float* out; int64_t ldo; int flags;
+  int64_t split; const int64_t* heavy_rows; int64_t n_heavy; const int64_t* chunk_ptr;
+  const int64_t* chunk_row; int64_t n_chunks; float* ws;
+};
+
+inline unsigned grid_waves(int64_t units) {
+  int64_t blocks = (units + 3) / 4;
   const int64_t max_blocks = 256 * 32;  // 256 CUs x 32 blocks: grid-stride beyond that
   if (blocks > max_blocks) blocks = max_blocks;
-  if (blocks < 1) blocks = 1;
+  return (unsigned)(blocks < 1 ? 1 : blocks);
+}
+
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
+int launch_all(const SpmmArgs& a, hipStream_t s) {
+  constexpr int UNROLL = (VEC == 4) ? 4 : 2;
   const int cols_per_slice = LPR * VEC;
-  dim3 grid((unsigned)blocks, (unsigned)((d + cols_per_slice - 1) / cols_per_slice));
-  hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>), grid, dim3(256), 0, s,
-                     indptr, indices, ew, X, ldx, n_dst, d, out, ldo,
-                     (flags & GNNREC_SPMM_EMPTY_NEGINF) ? 1 : 0);
+  const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
+  const int eni = (a.flags & GNNREC_SPMM_EMPTY_NEGINF) ? 1 : 0;
+  const int64_t max_deg = a.n_heavy > 0 ? a.split : INT64_MAX;
+  hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
+                     dim3(grid_waves(a.n_dst), slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
+                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg);
+  if (a.n_heavy > 0) {
+    hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
+                       dim3(grid_waves(a.n_chunks), slices), dim3(256), 0, s, a.indptr, a.indices,
+                       a.ew, a.X, a.ldx, a.d, a.split, a.heavy_rows, a.chunk_ptr, a.chunk_row,
+                       a.n_chunks, a.ws);
+    const unsigned cslices = (unsigned)((a.d + 64 * VEC - 1) / (64 * VEC));
+    hipLaunchKernelGGL((spmm_combine_kernel<VEC, REDUCE>), dim3(grid_waves(a.n_heavy), cslices),
+                       dim3(256), 0, s, a.indptr, a.d, a.heavy_rows, a.n_heavy, a.chunk_ptr, a.ws,
+                       a.out, a.ldo, eni);
+  }
   return check_launch("gnnrec_spmm_csr_f32");
 }
 
 template <int VEC, int REDUCE, bool WEIGHTED>
-int dispatch_lpr(int lpr, const int64_t* indptr, const int32_t* indices, const float* ew,
-                 const float* X, int64_t ldx, int64_t n_dst, int d, float* out, int64_t ldo,
-                 int flags, hipStream_t s) {
+int dispatch_lpr(int lpr, const SpmmArgs& a, hipStream_t s) {
   if constexpr (VEC == 1) {
-    return launch4<64, 1, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
+    return launch_all<64, 1, REDUCE, WEIGHTED>(a, s);
   } else {
     switch (lpr) {
-      case 4: return launch4<4, 4, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
-      case 8: return launch4<8, 4, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
-      case 16: return launch4<16, 4, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
-      case 32: return launch4<32, 4, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
-      default: return launch4<64, 4, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
+      case 4: return launch_all<4, 4, REDUCE, WEIGHTED>(a, s);
+      case 8: return launch_all<8, 4, REDUCE, WEIGHTED>(a, s);
+      case 16: return launch_all<16, 4, REDUCE, WEIGHTED>(a, s);
+      case 32: return launch_all<32, 4, REDUCE, WEIGHTED>(a, s);
+      default: return launch_all<64, 4, REDUCE, WEIGHTED>(a, s);
     }
   }
 }
 
 template <int VEC>
-int dispatch_reduce(int reduce, bool weighted, int lpr, const int64_t* indptr,
-                    const int32_t* indices, const float* ew, const float* X, int64_t ldx,
-                    int64_t n_dst, int d, float* out, int64_t ldo, int flags, hipStream_t s) {
-#define GNNREC_SPMM_CASE(R)                                                                          \
-  if (weighted)                                                                                      \
-    return dispatch_lpr<VEC, R, true>(lpr, indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s); \
-  return dispatch_lpr<VEC, R, false>(lpr, indptr, indices, ew, X, ldx, n_dst, d, out, ldo, flags, s);
+int dispatch_reduce(int reduce, int lpr, const SpmmArgs& a, hipStream_t s) {
+  const bool w = a.ew != nullptr;
   switch (reduce) {
-    case GNNREC_REDUCE_SUM: { GNNREC_SPMM_CASE(GNNREC_REDUCE_SUM) }
-    case GNNREC_REDUCE_MEAN: { GNNREC_SPMM_CASE(GNNREC_REDUCE_MEAN) }
-    default: { GNNREC_SPMM_CASE(GNNREC_REDUCE_MAX) }
+    case GNNREC_REDUCE_SUM:
+      return w ? dispatch_lpr<VEC, GNNREC_REDUCE_SUM, true>(lpr, a, s)
+               : dispatch_lpr<VEC, GNNREC_REDUCE_SUM, false>(lpr, a, s);
+    case GNNREC_REDUCE_MEAN:
+      return w ? dispatch_lpr<VEC, GNNREC_REDUCE_MEAN, true>(lpr, a, s)
+               : dispatch_lpr<VEC, GNNREC_REDUCE_MEAN, false>(lpr, a, s);
+    default:
+      return w ? dispatch_lpr<VEC, GNNREC_REDUCE_MAX, true>(lpr, a, s)
+               : dispatch_lpr<VEC, GNNREC_REDUCE_MAX, false>(lpr, a, s);
   }
-#undef GNNREC_SPMM_CASE
+}
+
+int spmm_entry(SpmmArgs a, int64_t d, int reduce, void* stream) {
+  GNNREC_REQUIRE(a.n_dst >= 0 && d >= 0, "gnnrec_spmm_csr_f32: negative size");
+  GNNREC_REQUIRE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN ||
+                     reduce == GNNREC_REDUCE_MAX,
+                 "gnnrec_spmm_csr_f32: unknown reduce %d", reduce);
+  GNNREC_REQUIRE(d <= (1 << 20), "gnnrec_spmm_csr_f32: d=%lld too large", (long long)d);
+  if (a.n_dst == 0 || d == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(a.indptr && a.out, "gnnrec_spmm_csr_f32: null indptr/out");
+  GNNREC_REQUIRE(a.ldx >= d && a.ldo >= d, "gnnrec_spmm_csr_f32: leading dimension < d");
+  GNNREC_REQUIRE(a.n_heavy == 0 || (a.split > 0 && a.heavy_rows && a.chunk_ptr && a.chunk_row &&
+                                    a.ws && a.n_chunks > 0),
+                 "gnnrec_spmm_csr_split_f32: incomplete heavy-row plan");
+  a.d = (int)d;
+  const bool vec4 = (d % 4 == 0) && (a.ldx % 4 == 0) && (a.ldo % 4 == 0) && aligned16(a.X) &&
+                    aligned16(a.out) && (a.n_heavy == 0 || aligned16(a.ws));
+  int lpr = 64;
+  if (vec4) {
+    const int64_t lanes = d / 4;
+    lpr = 4;
+    while (lpr < lanes && lpr < 64) lpr <<= 1;
+  }
+  hipStream_t s = as_stream(stream);
+  return vec4 ? dispatch_reduce<4>(reduce, lpr, a, s) : dispatch_reduce<1>(reduce, lpr, a, s);
 }
 
 }  // namespace
@@ -184,27 +306,19 @@ int dispatch_reduce(int reduce, bool weighted, int lpr, const int64_t* indptr,
 extern "C" int gnnrec_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
                                    const float* X, int64_t ldx, int64_t n_dst, int64_t d,
                                    int reduce, int flags, float* out, int64_t ldo, void* stream) {
-  using namespace gnnrec;
-  GNNREC_REQUIRE(n_dst >= 0 && d >= 0, "gnnrec_spmm_csr_f32: negative size");
-  GNNREC_REQUIRE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN ||
-                     reduce == GNNREC_REDUCE_MAX,
-                 "gnnrec_spmm_csr_f32: unknown reduce %d", reduce);
-  GNNREC_REQUIRE(d <= (1 << 20), "gnnrec_spmm_csr_f32: d=%lld too large", (long long)d);
-  if (n_dst == 0 || d == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(indptr && out, "gnnrec_spmm_csr_f32: null indptr/out");
-  GNNREC_REQUIRE(ldx >= d && ldo >= d, "gnnrec_spmm_csr_f32: leading dimension < d");
-  const bool vec4 = (d % 4 == 0) && (ldx % 4 == 0) && (ldo % 4 == 0) && aligned16(X) &&
-                    aligned16(out);
-  int lpr = 64;
-  if (vec4) {
-    const int64_t lanes = d / 4;
-    lpr = 4;
-    while (lpr < lanes && lpr < 64) lpr <<= 1;
-  }
-  hipStream_t s = as_stream(stream);
-  if (vec4)
-    return dispatch_reduce<4>(reduce, ew != nullptr, lpr, indptr, indices, ew, X, ldx, n_dst,
-                              (int)d, out, ldo, flags, s);
-  return dispatch_reduce<1>(reduce, ew != nullptr, lpr, indptr, indices, ew, X, ldx, n_dst, (int)d,
-                            out, ldo, flags, s);
+  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
+                     0, nullptr, 0, nullptr, nullptr, 0, nullptr};
+  return gnnrec::spmm_entry(a, d, reduce, stream);
+}
+
+extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* indices,
+                                         const float* ew, const float* X, int64_t ldx,
+                                         int64_t n_dst, int64_t d, int reduce, int flags,
+                                         float* out, int64_t ldo, int64_t split,
+                                         const int64_t* heavy_rows, int64_t n_heavy,
+                                         const int64_t* chunk_ptr, const int64_t* chunk_row,
+                                         int64_t n_chunks, float* workspace, void* stream) {
+  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
+                     split, heavy_rows, n_heavy, chunk_ptr, chunk_row, n_chunks, workspace};
+  return gnnrec::spmm_entry(a, d, reduce, stream);
 }

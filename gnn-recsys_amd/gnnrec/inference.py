@@ -188,6 +188,17 @@ class GraphShard:
 class ShardedFullGraphPass:
     """Layer-wise full-graph ConvModel pass over a GraphShard (one rank's view).
 
+    Streams (when `overlap` and the tensors live on a HIP device):
+      main  aggregation kernels and the replicated-type GEMMs;
+      side  the projection GEMMs of the partitioned type (users), which are
+            MFMA-bound and run concurrently with the HBM-bound aggregation of
+            the other relation (events order every hand-off);
+      RCCL  reduce-scatter / all-gather, issued async_op=True.
+    Order per layer: at world size 1, user-dst aggregation first so its GEMM
+    overlaps the item-dst aggregation; with several ranks, partial aggregation
+    first so the reduce-scatter overlaps the user-dst aggregation and the
+    all-gather overlaps the next layer's partial aggregation.
+
     `ops_backend` defaults to the HIP ops (gnnrec.ops); tests on CPU ranks
     inject a checker backend with the same signatures."""
 
@@ -198,53 +209,83 @@ class ShardedFullGraphPass:
         self.ex = exchange if exchange is not None else Exchange()
         self.ops = ops_backend if ops_backend is not None else ops
         self.overlap = overlap
-        self._pending = {}
+        self._pending = {}   # nt -> RCCL work producing h[nt]
+        self._ready = {}     # nt -> event on the side stream producing h[nt]
+        self.side = (torch.cuda.Stream(device=shard.device)
+                     if overlap and shard.device.type == 'cuda' else None)
         self.timers = None  # optional callable(tag) -> context manager (bench)
 
-    def _wait(self, nt):
+    def _get(self, h, nt):
         w = self._pending.pop(nt, None)
         if w is not None:
             w.wait()
-
-    def _get(self, h, nt):
-        self._wait(nt)
+        ev = self._ready.pop(nt, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.shard.device).wait_event(ev)
         return h[nt]
 
     def _time(self, tag):
         import contextlib
         return self.timers(tag) if self.timers is not None else contextlib.nullcontext()
 
+    def _on_side(self, fn, *tensors):
+        """Run fn() on the side stream after everything queued on main; returns its event."""
+        if self.side is None:
+            fn()
+            return None
+        main = torch.cuda.current_stream(self.shard.device)
+        self.side.wait_stream(main)
+        for t in tensors:  # keep the allocator from recycling them under the side stream
+            t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            fn()
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        return ev
+
     @torch.no_grad()
     def run(self, feats: Dict[str, torch.Tensor], embedding_layer: Optional[bool] = None):
         """feats: this rank's inputs (see GraphShard.local_features) -> this rank's outputs:
         {ptype: [n_own, out]} and the replicated types as full padded tables."""
-        m = self.model
+        m, O, sh = self.model, self.ops, self.shard
         if embedding_layer is None:
             embedding_layer = m.embedding_layer
         h = dict(feats)
         if embedding_layer:
-            for nt, mod in (('user', getattr(m, 'user_embed', None)),
-                            ('item', getattr(m, 'item_embed', None)),
-                            ('sport', getattr(m, 'sport_embed', None))):
-                if mod is not None and nt in h:
-                    h[nt] = self.ops.gemm(h[nt], mod.proj_feats.weight, bias=mod.proj_feats.bias)
+            embeds = [(nt, getattr(m, nt + '_embed', None)) for nt in ('item', 'sport', 'user')]
+            for nt, mod in embeds:
+                if mod is None or nt not in h:
+                    continue
+                W, b, x = mod.proj_feats.weight, mod.proj_feats.bias, h[nt]
+                if nt == sh.ptype and self.side is not None:
+                    y = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float32, device=x.device)
+                    self._ready[nt] = self._on_side(
+                        lambda: O.gemm(x, W, bias=b, out=y), x, y)
+                    h[nt] = y
+                else:
+                    h[nt] = O.gemm(x, W, bias=b)
         for layer in m.layers:
             h = self._layer(layer, h)
-        for nt in list(self._pending):
-            self._wait(nt)
+        for nt in list(h):
+            self._get(h, nt)
         return h
 
-    def _layer(self, hconv, h):
-        sh, O = self.shard, self.ops
-        agg = hconv.aggregate
+    def _active(self, hconv, h):
         active: Dict[str, list] = {}
-        for ce in sh.canonical_etypes:
-            rs = sh.rels[ce]
+        for ce in self.shard.canonical_etypes:
+            rs = self.shard.rels[ce]
             if rs.global_edges == 0 or ce[0] not in h or ce[2] not in h:
                 continue
             active.setdefault(ce[2], []).append(ce)
-        out = {}
-        # phase 1: partial aggregates into replicated types -> async reduce-scatter
+        return active
+
+    def _message(self, mod, ce, h, preagg):
+        src = self._get(h, ce[0])
+        return self.ops.gemm(src, mod.fc_preagg.weight, relu=True) if preagg else src
+
+    def _partials(self, hconv, h, active):
+        """user->item style relations: partial aggregates of the local edges -> reduce-scatter."""
+        sh, O = self.shard, self.ops
         partials = {}
         for T, ces in active.items():
             if T == sh.ptype:
@@ -253,8 +294,7 @@ class ShardedFullGraphPass:
                 mod = hconv.mods[ce[1]]
                 preagg, weighted, reduce = mod._plan_rel(ce)
                 rs = sh.rels[ce]
-                src = self._get(h, ce[0])
-                msg = O.gemm(src, mod.fc_preagg.weight, relu=True) if preagg else src
+                msg = self._message(mod, ce, h, preagg)
                 with self._time('spmm'):
                     part = O.spmm(rs.indptr, rs.indices, msg, 'max' if reduce == 'max' else 'sum',
                                   edge_weight=rs.weights if weighted else None,
@@ -262,30 +302,48 @@ class ShardedFullGraphPass:
                 own, work = self.ex.reduce_scatter_rows(part, 'max' if reduce == 'max' else 'sum',
                                                         async_op=self.overlap)
                 partials[ce] = (own, work, reduce)
-        # phase 2: relations into the partitioned type (dst rows owned here)
-        for T, ces in active.items():
-            if T != sh.ptype:
-                continue
-            R = len(ces)
-            o = None
-            for j, ce in enumerate(ces):
-                mod = hconv.mods[ce[1]]
-                preagg, weighted, reduce = mod._plan_rel(ce)
-                rs = sh.rels[ce]
-                src = self._get(h, ce[0])
-                msg = O.gemm(src, mod.fc_preagg.weight, relu=True) if preagg else src
-                with self._time('spmm'):
-                    a = O.spmm(rs.indptr, rs.indices, msg, reduce,
-                               edge_weight=rs.weights if weighted else None)
-                if o is None:
-                    o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
-                                    device=a.device)
-                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
-                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
-                O.gemm(h[T], mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
+        return partials
+
+    def _local(self, hconv, h, active, out):
+        """item->user style relations: dst rows owned here; GEMMs on the side stream."""
+        sh, O = self.shard, self.ops
+        agg = hconv.aggregate
+        T = sh.ptype
+        ces = active.get(T, [])
+        if not ces:
+            return
+        R = len(ces)
+        # the self rows of the partitioned type were produced on the side stream (or by main
+        # when not overlapping): the side-stream GEMM is ordered after them without making
+        # the main stream wait, so this relation's aggregation can start right away
+        self_rows = h[T] if self.side is not None else self._get(h, T)
+        o = None
+        ev = None
+        for j, ce in enumerate(ces):
+            mod = hconv.mods[ce[1]]
+            preagg, weighted, reduce = mod._plan_rel(ce)
+            rs = sh.rels[ce]
+            msg = self._message(mod, ce, h, preagg)
+            with self._time('spmm'):
+                a = O.spmm(rs.indptr, rs.indices, msg, reduce,
+                           edge_weight=rs.weights if weighted else None)
+            if o is None:
+                o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
+            acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
+            div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+
+            def proj(mod=mod, a=a, acc=acc, div=div, o=o):
+                O.gemm(self_rows, mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
-            out[T] = o
-        # phase 3: owners project their replicated rows, then all-gather the table
+            ev = self._on_side(proj, self_rows, a, o)
+        out[T] = o
+        if ev is not None:
+            self._ready[T] = ev
+
+    def _owned(self, hconv, h, active, partials, out):
+        """owners project their replicated rows, then all-gather the table."""
+        sh, O = self.shard, self.ops
+        agg = hconv.aggregate
         for T, ces in active.items():
             if T == sh.ptype:
                 continue
@@ -315,6 +373,17 @@ class ShardedFullGraphPass:
             if work is not None:
                 self._pending[T] = work
             out[T] = table
+
+    def _layer(self, hconv, h):
+        active = self._active(hconv, h)
+        out = {}
+        if self.ex.ws > 1:
+            partials = self._partials(hconv, h, active)
+            self._local(hconv, h, active, out)
+        else:
+            self._local(hconv, h, active, out)
+            partials = self._partials(hconv, h, active)
+        self._owned(hconv, h, active, partials, out)
         return out
 
 

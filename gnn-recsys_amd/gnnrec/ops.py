@@ -35,12 +35,41 @@ def _rowmajor(t: torch.Tensor, name: str) -> int:
     return max(t.stride(0), t.shape[1], 1)
 
 
+DEFAULT_SPLIT = 2048  # edges per chunk for rows split across wavefronts
+
+
+def split_plan(indptr: torch.Tensor, split: int = DEFAULT_SPLIT):
+    """Heavy-row plan for a CSR, computed once and cached on the indptr tensor.
+
+    Returns None when no row has more than `split` edges, else
+    (heavy_rows, chunk_ptr, chunk_row, n_chunks)."""
+    cached = getattr(indptr, "_gnnrec_split_plan", None)
+    if cached is not None and cached[0] == split:
+        return cached[1]
+    deg = indptr[1:] - indptr[:-1]
+    heavy = torch.nonzero(deg > split).squeeze(1)
+    plan = None
+    if heavy.numel() > 0:
+        nch = (deg[heavy] + split - 1) // split
+        chunk_ptr = torch.zeros(heavy.numel() + 1, dtype=torch.int64, device=indptr.device)
+        torch.cumsum(nch, 0, out=chunk_ptr[1:])
+        chunk_row = torch.repeat_interleave(
+            torch.arange(heavy.numel(), device=indptr.device), nch)
+        plan = (heavy.contiguous(), chunk_ptr, chunk_row.contiguous(), int(chunk_ptr[-1].item()))
+    try:
+        indptr._gnnrec_split_plan = (split, plan)
+    except AttributeError:  # pragma: no cover
+        pass
+    return plan
+
+
 def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: str = "mean",
          edge_weight: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-         empty_neginf: bool = False) -> torch.Tensor:
+         empty_neginf: bool = False, split: Optional[int] = DEFAULT_SPLIT) -> torch.Tensor:
     """a1: out[v] = reduce_{e in row v} X[indices[e]] (* edge_weight[e]).
 
     indptr int64 [n_dst+1], indices int32 [E] (local rows of X), X fp32 [n_src, d].
+    Rows with more than `split` edges are reduced in parallel chunks (split=None: never).
     """
     lib = _lib.load()
     _dev(indptr, "indptr", torch.int64)
@@ -64,9 +93,20 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
             raise ValueError(f"out must be [{n_dst}, {d}]")
     ldo = _rowmajor(out, "out")
     flags = _lib.SPMM_EMPTY_NEGINF if empty_neginf else 0
-    rc = lib.gnnrec_spmm_csr_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx, n_dst,
-                                 d, REDUCE[reduce], flags, ptr(out), ldo, stream_ptr(X.device))
-    check(rc, "gnnrec_spmm_csr_f32")
+    plan = split_plan(indptr, split) if split else None
+    if plan is None:
+        rc = lib.gnnrec_spmm_csr_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx,
+                                     n_dst, d, REDUCE[reduce], flags, ptr(out), ldo,
+                                     stream_ptr(X.device))
+        check(rc, "gnnrec_spmm_csr_f32")
+        return out
+    heavy, chunk_ptr, chunk_row, n_chunks = plan
+    ws = torch.empty((n_chunks, d), dtype=torch.float32, device=X.device)
+    rc = lib.gnnrec_spmm_csr_split_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx,
+                                       n_dst, d, REDUCE[reduce], flags, ptr(out), ldo, split,
+                                       ptr(heavy), heavy.numel(), ptr(chunk_ptr), ptr(chunk_row),
+                                       n_chunks, ptr(ws), stream_ptr(X.device))
+    check(rc, "gnnrec_spmm_csr_split_f32")
     return out
 
 

@@ -83,6 +83,19 @@ int gnnrec_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const flo
                         const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
                         int flags, float* out, int64_t ldo, void* stream);
 
+/* Same, with heavy rows split for load balance (Zipf-skewed degrees): rows
+ * with deg > split are skipped by the row kernel and reduced instead by one
+ * wave per `split`-edge chunk into workspace[n_chunks, d], then combined per
+ * row in chunk order (deterministic).  heavy_rows[n_heavy] = the rows with
+ * deg > split; chunk_ptr[n_heavy+1] = prefix sum of ceil(deg/split);
+ * chunk_row[n_chunks] = index into heavy_rows of each chunk. */
+int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                              const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
+                              int flags, float* out, int64_t ldo, int64_t split,
+                              const int64_t* heavy_rows, int64_t n_heavy, const int64_t* chunk_ptr,
+                              const int64_t* chunk_row, int64_t n_chunks, float* workspace,
+                              void* stream);
+
 /* ---- a2/a3/a4: fp32 MFMA GEMM with fused SAGE epilogue (K4, K7) ---------
  * acc[m,n] = sum_k A1[m,k] W1[n,k] + sum_k T(A2)[m,k] W2[n,k]   (W row-major [N,K] = nn.Linear.weight)
  * z = epi(acc + bias)      epi: relu / sigmoid, then optional row L2 norm

@@ -51,6 +51,37 @@ def test_spmm_matches_oracle(d, reduce, weighted):
         np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL * max(1, np.abs(ref).max()))
 
 
+@pytest.mark.parametrize("split", [64, 2048])
+@pytest.mark.parametrize("d,reduce,weighted", [(128, "mean", False), (128, "max", True),
+                                               (7, "sum", True), (64, "mean", True)])
+def test_spmm_heavy_row_split_matches_oracle(split, d, reduce, weighted):
+    """Zipf-like degrees: many rows above the split threshold, reduced in chunks."""
+    from gnnrec import ops
+    rng = np.random.default_rng(split + d)
+    n_dst, n_src = 400, 5000
+    deg = (20000 / np.arange(1, n_dst + 1)).astype(np.int64)  # 20000, 10000, ... , 50
+    deg[rng.random(n_dst) < 0.05] = 0
+    indptr = np.zeros(n_dst + 1, np.int64)
+    np.cumsum(deg, out=indptr[1:])
+    idx = rng.integers(0, n_src, int(indptr[-1])).astype(np.int32)
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    w = rng.integers(1, 9, idx.size).astype(np.float32) if weighted else None
+    ti = _t(indptr)
+    out = ops.spmm(ti, _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w),
+                   split=split)
+    plan = ops.split_plan(ti, split)
+    assert plan is not None and plan[3] > plan[0].numel()  # several chunks per heavy row
+    ref = oracle.spmm_csr(indptr, idx, X, reduce, w)
+    if reduce == "max":
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    else:
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL,
+                                   atol=ATOL * max(1, np.abs(ref).max()))
+    again = ops.spmm(ti, _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w),
+                     split=split)
+    assert torch.equal(out, again)
+
+
 def test_spmm_bitwise_deterministic_and_strided_output():
     from gnnrec import ops
     rng = np.random.default_rng(5)
