@@ -161,8 +161,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_idx = local_rank % max(1, torch.cuda.device_count())  # rehearsals may share one GPU
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
         # RCCL over xGMI; GNNREC_DIST_BACKEND=gloo rehearses several ranks on one GPU
         backend = os.environ.get("GNNREC_DIST_BACKEND", "nccl")
@@ -232,7 +233,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (counter-hash graph seed 11, N(0,1) features, xavier weights)",
-            "config": {"workload": f"C4 full-graph embed pass: {args.users} users x {args.items} "
+            "config": {"workload": ("C4" if (args.users, args.items, args.edges) ==
+                                    (10_000_000, 1_000_000, 500_000_000) else "custom")
+                                   + f" full-graph embed pass: {args.users} users x {args.items} "
                                    f"items, {args.edges} edges/direction, NodeEmbedding + L=2 "
                                    f"ConvLayer '{args.aggregator}', hetero sum, norm, d={d}"
                                    + (f", item zipf s={args.zipf}" if args.zipf else ""),

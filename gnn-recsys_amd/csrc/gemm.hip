@@ -42,7 +42,7 @@ struct GemmArgs {
   int64_t M; int64_t N;
   int epilogue; int accum; float out_div;
   float* out; int64_t ldo;
-  int vecA1, vecA2, vecW1, vecW2;
+  int vecA1, vecA2, vecW1, vecW2, vecO;
 };
 
 __device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t ld, int64_t k,
@@ -60,9 +60,18 @@ __device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t l
   return v;
 }
 
+// FAST: every operand 16-B aligned with K1, K2 multiples of BK.  The loads are
+// then unconditional (out-of-range rows are clamped and zeroed by a select at
+// LDS-store time), so the next tile's loads stay in flight across the MFMAs —
+// a bounds check per load makes hipcc branch around it and wait vmcnt(0).
 template <int BN>
+constexpr int smem_floats() {
+  return (BM + BN) * LDSK > BM * (BN + 4) ? (BM + BN) * LDSK : BM * (BN + 4);
+}
+
+template <int BN, bool FAST>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * LDSK];
+  __shared__ __attribute__((aligned(16))) float smem[smem_floats<BN>()];
   float* As = smem;
   float* Ws = smem + BM * LDSK;
   constexpr int NT = BN / 32;
@@ -80,6 +89,25 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
 
+  // rows / columns this thread stages (fixed for the whole kernel)
+  bool arow_ok[4];
+  int64_t arow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t gm = m0 + ((tid + i * 256) >> 3);
+    arow_ok[i] = gm < g.M;
+    arow[i] = arow_ok[i] ? gm : g.M - 1;
+  }
+  bool wrow_ok[NT];
+  int64_t wrow[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int64_t gn = n0 + ((tid + i * 256) >> 3);
+    wrow_ok[i] = gn < g.N;
+    wrow[i] = wrow_ok[i] ? gn : g.N - 1;
+  }
+  const int kc = (tid & 7) * 4;  // k offset of this thread's float4 inside a tile
+
 #pragma unroll 1
   for (int seg = 0; seg < 2; ++seg) {
     const float* A = seg ? g.A2 : g.A1;
@@ -89,56 +117,57 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     const bool vecA = seg ? g.vecA2 : g.vecA1;
     const bool vecW = seg ? g.vecW2 : g.vecW1;
     if (K == 0) continue;
-    // per-thread row transform factor for the A rows this thread stages
-    float rowmul[4];
+    const int mode = seg ? g.a2_mode : GNNREC_A2_NONE;
+    // per-row transform of the A rows this thread stages (uniform branch on `mode`)
+    float rowdiv[4];
     bool rowzero[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * 256;
-      const int64_t gm = m0 + (idx >> 3);
-      rowmul[i] = 1.f;
-      rowzero[i] = false;
-      if (seg == 1 && g.a2_mode != GNNREC_A2_NONE && gm < g.M) {
-        const int32_t dg = g.a2_deg[gm];
-        if (g.a2_mode == GNNREC_A2_DIV_DEG) rowmul[i] = (float)(dg > 0 ? dg : 1);
-        else rowzero[i] = (dg == 0);
-      }
+      rowdiv[i] = 1.f;
+      rowzero[i] = !arow_ok[i];
     }
-    // register prefetch: tile k+1 is loaded from global while tile k is in the MFMAs
-    f32x4 ra[4], rw[NT];
-    auto load_tile = [&](int64_t k0) {
+    if (mode != GNNREC_A2_NONE) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int idx = tid + i * 256;
-        const int64_t gm = m0 + (idx >> 3);
-        const int64_t gk = k0 + (idx & 7) * 4;
-        ra[i] = load4(A, gm, lda, gk, K, gm < g.M, vecA);
-        if (seg == 1) {
-          if (g.a2_mode == GNNREC_A2_DIV_DEG) ra[i] = ra[i] / rowmul[i];
-          else if (rowzero[i]) ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        const int32_t dg = g.a2_deg[arow[i]];
+        if (mode == GNNREC_A2_DIV_DEG) rowdiv[i] = (float)(dg > 0 ? dg : 1);
+        else rowzero[i] = rowzero[i] || dg == 0;
       }
+    }
+    f32x4 ra[4], rw[NT];
+    auto load_tile = [&](int64_t k0) {
+      if constexpr (FAST) {
 #pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        const int idx = tid + i * 256;
-        const int64_t gn = n0 + (idx >> 3);
-        const int64_t gk = k0 + (idx & 7) * 4;
-        rw[i] = load4(W, gn, K, gk, K, gn < g.N, vecW);
+        for (int i = 0; i < 4; ++i)
+          ra[i] = *reinterpret_cast<const f32x4*>(A + arow[i] * lda + k0 + kc);
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          rw[i] = *reinterpret_cast<const f32x4*>(W + wrow[i] * K + k0 + kc);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[i] = load4(A, arow[i], lda, k0 + kc, K, true, vecA);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) rw[i] = load4(W, wrow[i], K, k0 + kc, K, true, vecW);
       }
     };
     load_tile(0);
 #pragma unroll 1
     for (int64_t k0 = 0; k0 < K; k0 += BK) {
       __syncthreads();  // previous tile fully consumed
+      const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+      if (mode == GNNREC_A2_DIV_DEG) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[i] = ra[i] / rowdiv[i];
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int idx = tid + i * 256;
-        *reinterpret_cast<f32x4*>(As + (idx >> 3) * LDSK + (idx & 7) * 4) = ra[i];
+        *reinterpret_cast<f32x4*>(As + (idx >> 3) * LDSK + kc) = rowzero[i] ? zero : ra[i];
       }
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
         const int idx = tid + i * 256;
-        *reinterpret_cast<f32x4*>(Ws + (idx >> 3) * LDSK + (idx & 7) * 4) = rw[i];
+        *reinterpret_cast<f32x4*>(Ws + (idx >> 3) * LDSK + kc) = wrow_ok[i] ? rw[i] : zero;
       }
       __syncthreads();
       if (k0 + BK < K) load_tile(k0 + BK);
@@ -171,9 +200,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     colok[t] = col < g.N;
     bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
   }
+  // staged store: the wave's 32 x BN tile goes through LDS and leaves as whole rows of
+  // 16-B stores (4x fewer, fully coalesced store instructions than per-lane scalars)
+  constexpr int OSTR = BN + 4;
+  const bool staged = g.vecO;
+  float* Ot = smem + wave * 32 * OSTR;
+  if (staged) __syncthreads();  // every wave is done reading the K-loop tiles
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
-    const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+    const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+    const int64_t row = m0 + wave * 32 + rl;
     float z[NT];
     float ss = 0.f;
 #pragma unroll
@@ -193,7 +229,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) z[t] = z[t] / nrm;
     }
-    if (row < g.M) {
+    if (staged) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) Ot[rl * OSTR + t * 32 + r] = z[t];
+    } else if (row < g.M) {
       float* orow = g.out + row * g.ldo + n0;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -207,12 +246,38 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
       }
     }
   }
+  if (!staged) return;
+  __syncthreads();
+  constexpr int C4 = BN / 4;               // float4 per row
+  constexpr int ITER = 32 * C4 / kWave;    // float4 per lane
+#pragma unroll 4
+  for (int q = 0; q < ITER; ++q) {
+    const int flat = q * kWave + lane;
+    const int rl = flat / C4;
+    const int c = (flat % C4) * 4;
+    const int64_t row = m0 + wave * 32 + rl;
+    if (row >= g.M || n0 + c >= g.N) continue;
+    f32x4 y = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+    f32x4* p = reinterpret_cast<f32x4*>(g.out + row * g.ldo + n0 + c);
+    if (g.accum == GNNREC_ACC_ADD) {
+      y = *p + y;
+    } else if (g.accum == GNNREC_ACC_MAX) {
+      const f32x4 o = *p;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+    }
+    if (g.out_div > 0.f) y = y / g.out_div;
+    *p = y;
+  }
 }
 
 template <int BN>
 int launch_gemm(const GemmArgs& g, hipStream_t s) {
   dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.N + BN - 1) / BN));
-  hipLaunchKernelGGL(gemm_f32_kernel<BN>, grid, dim3(256), 0, s, g);
+  const bool fast = g.vecA1 && g.vecW1 && g.K1 % BK == 0 &&
+                    (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK == 0));
+  if (fast) hipLaunchKernelGGL((gemm_f32_kernel<BN, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BN, false>), grid, dim3(256), 0, s, g);
   return check_launch("gnnrec_gemm_f32");
 }
 
@@ -246,6 +311,7 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   g.vecA2 = (K2 % 4 == 0) && (lda2 % 4 == 0) && aligned16(A2);
   g.vecW1 = (K1 % 4 == 0) && aligned16(W1);
   g.vecW2 = (K2 % 4 == 0) && aligned16(W2);
+  g.vecO = (N % 4 == 0) && (ldo % 4 == 0) && aligned16(out);
   hipStream_t s = as_stream(stream);
   if (N <= 32) return launch_gemm<32>(g, s);
   if (N <= 64) return launch_gemm<64>(g, s);

@@ -22,6 +22,7 @@
 // workspace, then combined per row in chunk order (deterministic two-phase).
 #include "common.hpp"
 #include <cmath>
+#include <cstdlib>
 
 namespace gnnrec {
 namespace {
@@ -214,9 +215,21 @@ struct SpmmArgs {
   const int64_t* chunk_row; int64_t n_chunks; float* ws;
 };
 
+// Resident 256-thread blocks per CU the row kernels may occupy (grid-stride beyond).
+// 8 = every wave slot of a CU; fewer leaves room for a concurrent kernel (the
+// projection GEMM on the side stream).  GNNREC_SPMM_BLOCKS_PER_CU overrides.
+inline int64_t blocks_per_cu() {
+  static int64_t v = [] {
+    const char* e = getenv("GNNREC_SPMM_BLOCKS_PER_CU");
+    const long x = e ? atol(e) : 0;
+    return (int64_t)(x > 0 && x <= 64 ? x : 8);
+  }();
+  return v;
+}
+
 inline unsigned grid_waves(int64_t units) {
   int64_t blocks = (units + 3) / 4;
-  const int64_t max_blocks = 256 * 32;  // 256 CUs x 32 blocks: grid-stride beyond that
+  const int64_t max_blocks = 256 * blocks_per_cu();
   if (blocks > max_blocks) blocks = max_blocks;
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
