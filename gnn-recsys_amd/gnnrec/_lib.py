@@ -58,6 +58,7 @@ SIGNATURES = {
     "gnnrec_compact_marked": (_INT, [_P, _P, _I64, _P, _P]),
     "gnnrec_set_prefix_pos": (_INT, [_P, _I64, _P, _P]),
     "gnnrec_clear_prefix_pos": (_INT, [_P, _I64, _P, _P]),
+    "gnnrec_topk_rows_f32": (_INT, [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "gnnrec_synth_edges": (_INT, [_U64, _I64, _I64, _I64, _I64, _P, _P, _P, _P]),
 }
 

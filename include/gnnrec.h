@@ -157,6 +157,17 @@ int gnnrec_compact_marked(const int32_t* mark, const int64_t* rank, int64_t n_no
 int gnnrec_set_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
 int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
 
+/* ---- f1: recommendation top-k --------------------------------------------
+ * For each row r of scores[n_rows, n_cols] (leading dimension ld): the k
+ * (1..64) best columns ordered by (score desc, column asc), skipping the
+ * columns listed in exclude_indices[exclude_indptr[r] .. exclude_indptr[r+1])
+ * (already-bought items; both pointers may be NULL).  Rows with fewer than k
+ * eligible columns are padded with (-inf, -1).
+ * Replaces the per-user argsort / filter loop of src/metrics.py:52-77. */
+int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_rows, int64_t n_cols,
+                         int64_t k, const int64_t* exclude_indptr, const int64_t* exclude_indices,
+                         float* out_vals, int64_t* out_idx, void* stream);
+
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),
  * item() uniform (zipf_s == 0) or inverse-CDF Zipf over the table `zipf_cdf`

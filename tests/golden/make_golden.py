@@ -197,6 +197,64 @@ def gen_model_cases(ref, dgl_shim, manifest):
                           "delta": 0.266, "canonical_etypes": [list(ce) for ce in edges]}
 
 
+class _StubGraph:
+    """What reference src/metrics.py reads from g: num_nodes('item'), ndata['popularity']."""
+
+    def __init__(self, n_items, popularity):
+        self._n = n_items
+        self.ndata = {"popularity": {"item": torch.from_numpy(popularity)}}
+
+    def num_nodes(self, nt):
+        assert nt == "item"
+        return self._n
+
+
+def gen_metrics_cases(ref, manifest):
+    """Reference src/metrics.py get_recs / recs_to_metrics (imported unmodified)."""
+    import importlib
+    sys.path.insert(0, REF)
+    ref_metrics = importlib.import_module("src.metrics")
+    cases = [("recs_cos", "cos", False), ("recs_cos_pop", "cos", True), ("recs_nn", "nn", False)]
+    for case_no, (name, pred, pop) in enumerate(cases):
+        rng = np.random.default_rng(500 + case_no)
+        n_u, n_i, d, k = 40, 300, 16, 10
+        hu = rng.standard_normal((n_u, d)).astype(np.float32)
+        hi = rng.standard_normal((n_i, d)).astype(np.float32)
+        popularity = rng.random(n_i).astype(np.float32)
+        bu = rng.integers(0, n_u, 400)
+        bi = rng.integers(0, n_i, 400)
+        already = ref_metrics.create_ground_truth(bu, bi)
+        user_ids = list(range(0, n_u, 2))
+        torch.manual_seed(9)
+        model = type("M", (), {})()
+        model.pred_fn = type("P", (), {})()
+        model.pred_fn.layer_nn = ref.PredictingLayer(d)
+        model.pred_fn.layer_nn.eval()
+        g = _StubGraph(n_i, popularity)
+        with torch.no_grad():
+            recs = ref_metrics.get_recs(g, {"user": torch.from_numpy(hu), "item": torch.from_numpy(hi)},
+                                        model, d, k, user_ids, already, True, False, None, pred,
+                                        pop, 0.5)
+        gu = rng.integers(0, n_u, 120)
+        gi = rng.integers(0, n_i, 120)
+        gt = ref_metrics.create_ground_truth(gu, gi)
+        recs_gt = {u: v for u, v in recs.items()}
+        for u in recs_gt:
+            gt[u]  # defaultdict: materialise every user key, as the reference does
+        prec, rec, cov = ref_metrics.recs_to_metrics(recs_gt, gt, g)
+        arrs = {"h/user": hu, "h/item": hi, "popularity": popularity, "bought/u": bu,
+                "bought/i": bi, "user_ids": np.array(user_ids, np.int64),
+                "recs": np.stack([np.pad(np.asarray(recs[u], np.int64), (0, k - len(recs[u])),
+                                         constant_values=-1) for u in user_ids]),
+                "gt/u": gu, "gt/i": gi,
+                "metrics": np.array([prec, rec, cov], np.float64)}
+        for kk, v in model.pred_fn.layer_nn.state_dict().items():
+            arrs[f"w/{kk}"] = v.numpy()
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        manifest[name] = {"kind": "recs", "pred": pred, "use_popularity": pop,
+                          "weight_popularity": 0.5, "k": k, "embed_dim": d}
+
+
 def main():
     if not os.path.exists(os.path.join(REF, "src", "model.py")):
         print(f"reference not found at {REF}: skipping golden generation")
@@ -205,9 +263,10 @@ def main():
     manifest = {}
     gen_convlayer_cases(ref, dgl_shim, manifest)
     gen_model_cases(ref, dgl_shim, manifest)
+    gen_metrics_cases(ref, manifest)
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
-                   "reference_files": ["src/model.py"],
+                   "reference_files": ["src/model.py", "src/metrics.py"],
                    "torch": torch.__version__, "cases": manifest}, f, indent=1, sort_keys=True)
     print(f"wrote {len(manifest)} golden cases to {HERE}")
     return 0
