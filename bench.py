@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--zipf", type=float, default=0.0, help="item Zipf exponent (0 = uniform)")
     ap.add_argument("--aggregator", default="mean")
+    ap.add_argument("--config", choices=["c4", "c5"], default="c4",
+                    help="c5: the C4 graph split 80%% clicks / 20%% buys -> 4 relations")
+    ap.add_argument("--hetero", choices=["sum", "mean", "max"], default="sum")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-scale", type=float, default=0.1,
@@ -97,8 +100,8 @@ def pmc_traffic(args, world):
     (FETCH_SIZE x2 for gfx950's half-counted wide reads + WRITE_SIZE, KB -> B), for
     the default single-GPU C4 workload they were collected on; None otherwise."""
     import csv
-    default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator) == \
-        (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean")
+    default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
+               args.config) == (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4")
     f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch_size.csv")
     w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write_size.csv")
     if world != 1 or not default or not (os.path.exists(f) and os.path.exists(w)):
@@ -175,18 +178,20 @@ def main():
     from gnnrec import nn as gnn
     from gnnrec.dist import Exchange
     from gnnrec.inference import ShardedFullGraphPass
-    from gnnrec.synth import BOUGHT_BY, BUYS, GraphMeta, bipartite_shard, node_features
+    from gnnrec.synth import GraphMeta, bipartite_shard, node_features
 
     d = args.dim
+    split = ((("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2)) if args.config == "c5"
+             else (("buys", "bought-by", 1.0),))
     shard = bipartite_shard(args.users, args.items, args.edges, rank, world, dev,
-                            zipf_s=args.zipf)
+                            zipf_s=args.zipf, split=split)
     feats = {"user": node_features(args.users, d, 0, dev, slice(shard.p_lo, shard.p_hi)),
              "item": torch.zeros((shard.padded_rows("item"), d), device=dev)}
     feats["item"][: args.items] = node_features(args.items, d, 1, dev)
     torch.manual_seed(0)
-    meta = GraphMeta([BUYS, BOUGHT_BY], ["item", "user"])
+    meta = GraphMeta(shard.canonical_etypes, ["item", "user"])
     model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
-                          args.aggregator, "cos", "sum", True).to(dev).eval()
+                          args.aggregator, "cos", args.hetero, True).to(dev).eval()
     ex = Exchange()
     runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap)
     timers = EventTimers()
@@ -233,11 +238,14 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (counter-hash graph seed 11, N(0,1) features, xavier weights)",
-            "config": {"workload": ("C4" if (args.users, args.items, args.edges) ==
+            "config": {"workload": (args.config.upper() if (args.users, args.items, args.edges) ==
                                     (10_000_000, 1_000_000, 500_000_000) else "custom")
                                    + f" full-graph embed pass: {args.users} users x {args.items} "
-                                   f"items, {args.edges} edges/direction, NodeEmbedding + L=2 "
-                                   f"ConvLayer '{args.aggregator}', hetero sum, norm, d={d}"
+                                   f"items, {args.edges} edges/direction"
+                                   + (" (80% clicks / 20% buys, 4 relations)"
+                                      if args.config == "c5" else "")
+                                   + f", NodeEmbedding + L=2 ConvLayer '{args.aggregator}', "
+                                     f"hetero {args.hetero}, norm, d={d}"
                                    + (f", item zipf s={args.zipf}" if args.zipf else ""),
                        "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
                        "overlap": not args.no_overlap},

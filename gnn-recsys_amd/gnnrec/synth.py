@@ -34,38 +34,55 @@ def zipf_cdf(n: int, s: float, device) -> torch.Tensor:
     return c / c[-1]
 
 
+def relation_pairs(split):
+    """[(fwd canonical etype, reverse canonical etype, fraction)] for user->item relations."""
+    return [(("user", rel, "item"), ("item", rev, "user"), frac) for rel, rev, frac in split]
+
+
 def bipartite_shard(n_users: int, n_items: int, n_edges: int, rank: int, world: int, device,
                     seed: int = 11, zipf_s: float = 0.0, chunk: int = 1 << 26,
-                    occurrence: bool = False) -> GraphShard:
-    """This rank's GraphShard of the synthetic (user, buys, item) graph + reverse."""
+                    occurrence: bool = False,
+                    split=(("buys", "bought-by", 1.0),)) -> GraphShard:
+    """This rank's GraphShard of the synthetic user->item graph (+ reverse relations).
+
+    `split` assigns consecutive eid ranges of the generated edge stream to relations
+    (e.g. C5: clicks 80 % / buys 20 %); eids are per relation, reverse relations share
+    the forward eid order."""
     dev = torch.device(device)
-    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, [BUYS, BOUGHT_BY],
-                    dev)
+    pairs = relation_pairs(split)
+    etypes = [ce for f, r, _ in pairs for ce in (f, r)]
+    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, etypes, dev)
     cdf = zipf_cdf(n_items, zipf_s, dev) if zipf_s > 0 else None
-    keep_u, keep_i, keep_e = [], [], []
-    item_deg = torch.zeros(n_items, dtype=torch.int64, device=dev)
-    for e0 in range(0, n_edges, chunk):
-        n = min(chunk, n_edges - e0)
-        u, i = ops.synth_edges(seed, e0, n, n_users, n_items, dev, cdf)
-        item_deg += torch.bincount(i, minlength=n_items)
-        if world == 1:
-            keep_u.append(u)
-            keep_i.append(i)
-            keep_e.append(torch.arange(e0, e0 + n, device=dev))
-        else:
-            m = (u >= sh.p_lo) & (u < sh.p_hi)
-            idx = torch.nonzero(m).squeeze(1)
-            keep_u.append(u[idx])
-            keep_i.append(i[idx])
-            keep_e.append(idx + e0)
-        del u, i
-    u = torch.cat(keep_u).to(torch.int64)
-    i = torch.cat(keep_i).to(torch.int64)
-    eid = torch.cat(keep_e)
-    del keep_u, keep_i, keep_e
-    w = ((eid % 8) + 1) if occurrence else None  # deterministic 1..8 'occurrence' counts
-    sh.add_relation(BUYS, u, i, eid, n_edges, weights=w, dst_global_deg=item_deg)
-    sh.add_relation(BOUGHT_BY, i, u, eid, n_edges, weights=w)
+    bounds = [0]
+    for _, _, frac in pairs:
+        bounds.append(min(n_edges, bounds[-1] + int(round(frac * n_edges))))
+    bounds[-1] = n_edges
+    for (fwd, rev, _), lo, hi in zip(pairs, bounds[:-1], bounds[1:]):
+        keep_u, keep_i, keep_e = [], [], []
+        item_deg = torch.zeros(n_items, dtype=torch.int64, device=dev)
+        for e0 in range(lo, hi, chunk):
+            n = min(chunk, hi - e0)
+            u, i = ops.synth_edges(seed, e0, n, n_users, n_items, dev, cdf)
+            item_deg += torch.bincount(i, minlength=n_items)
+            if world == 1:
+                keep_u.append(u)
+                keep_i.append(i)
+                keep_e.append(torch.arange(e0 - lo, e0 - lo + n, device=dev))
+            else:
+                m = (u >= sh.p_lo) & (u < sh.p_hi)
+                idx = torch.nonzero(m).squeeze(1)
+                keep_u.append(u[idx])
+                keep_i.append(i[idx])
+                keep_e.append(idx + (e0 - lo))
+            del u, i
+        u = torch.cat(keep_u).to(torch.int64)
+        i = torch.cat(keep_i).to(torch.int64)
+        eid = torch.cat(keep_e)
+        del keep_u, keep_i, keep_e
+        w = ((eid % 8) + 1) if occurrence else None  # deterministic 1..8 'occurrence' counts
+        sh.add_relation(fwd, u, i, eid, hi - lo, weights=w, dst_global_deg=item_deg)
+        sh.add_relation(rev, i, u, eid, hi - lo, weights=w)
+        del u, i, eid, w
     return sh
 
 
