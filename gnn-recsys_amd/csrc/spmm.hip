@@ -335,3 +335,80 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* i
                      split, heavy_rows, n_heavy, chunk_ptr, chunk_row, n_chunks, workspace};
   return gnnrec::spmm_entry(a, d, reduce, stream);
 }
+
+// ---------------------------------------------------------------- backward --
+// f2 — gradient of a1 w.r.t. the source rows (training through ConvLayer,
+// reference src/train/run.py:136-138).  sum/mean: grad_X[src_e] += w_e/deg·g[v];
+// max: the gradient of column c goes to the FIRST edge (CSR order) whose message
+// equals the forward maximum (DGL's arg-max convention).  Float atomics into
+// grad_X (no reproducibility requirement on training gradients).
+namespace gnnrec {
+namespace {
+
+template <int REDUCE, bool WEIGHTED>
+__global__ __launch_bounds__(256) void spmm_backward_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ ew, const float* __restrict__ G, int64_t ldg,
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ Y, int64_t ldy,
+    int64_t n_dst, int d, float* __restrict__ gX, int64_t ldgx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < n_dst; v += wstride) {
+    const int64_t beg = indptr[v], end = indptr[v + 1];
+    if (beg == end) continue;
+    const float scale = REDUCE == GNNREC_REDUCE_MEAN ? 1.f / (float)(end - beg) : 1.f;
+    for (int c = lane; c < d; c += kWave) {
+      const float g = G[v * ldg + c] * scale;
+      if (g == 0.f) continue;
+      if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+        const float y = Y[v * ldy + c];
+        for (int64_t e = beg; e < end; ++e) {
+          const int64_t u = indices[e];
+          const float m = WEIGHTED ? X[u * ldx + c] * ew[e] : X[u * ldx + c];
+          if (m == y) {
+            atomicAdd(gX + u * ldgx + c, WEIGHTED ? g * ew[e] : g);
+            break;
+          }
+        }
+      } else {
+        for (int64_t e = beg; e < end; ++e) {
+          const int64_t u = indices[e];
+          atomicAdd(gX + u * ldgx + c, WEIGHTED ? g * ew[e] : g);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* indices,
+                                        const float* ew, const float* grad_out, int64_t ldg,
+                                        const float* X, int64_t ldx, const float* out,
+                                        int64_t ldo, int64_t n_dst, int64_t d, int reduce,
+                                        float* grad_X, int64_t ldgx, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_dst >= 0 && d >= 0, "gnnrec_spmm_backward_f32: negative size");
+  if (n_dst == 0 || d == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(indptr && grad_out && grad_X, "gnnrec_spmm_backward_f32: null pointer");
+  GNNREC_REQUIRE(reduce != GNNREC_REDUCE_MAX || (X && out),
+                 "gnnrec_spmm_backward_f32: max needs the forward input and output");
+  hipStream_t s = as_stream(stream);
+  const unsigned grid = grid_waves(n_dst);
+#define GNNREC_BWD(R)                                                                         \
+  if (ew)                                                                                     \
+    hipLaunchKernelGGL((spmm_backward_kernel<R, true>), dim3(grid), dim3(256), 0, s, indptr,   \
+                       indices, ew, grad_out, ldg, X, ldx, out, ldo, n_dst, (int)d, grad_X, ldgx); \
+  else                                                                                        \
+    hipLaunchKernelGGL((spmm_backward_kernel<R, false>), dim3(grid), dim3(256), 0, s, indptr,  \
+                       indices, ew, grad_out, ldg, X, ldx, out, ldo, n_dst, (int)d, grad_X, ldgx);
+  switch (reduce) {
+    case GNNREC_REDUCE_SUM: GNNREC_BWD(GNNREC_REDUCE_SUM) break;
+    case GNNREC_REDUCE_MEAN: GNNREC_BWD(GNNREC_REDUCE_MEAN) break;
+    case GNNREC_REDUCE_MAX: GNNREC_BWD(GNNREC_REDUCE_MAX) break;
+    default: GNNREC_REQUIRE(false, "gnnrec_spmm_backward_f32: unknown reduce %d", reduce);
+  }
+#undef GNNREC_BWD
+  return check_launch("gnnrec_spmm_backward_f32");
+}

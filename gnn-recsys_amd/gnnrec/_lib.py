@@ -44,6 +44,8 @@ SIGNATURES = {
     "gnnrec_spmm_csr_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64, _P]),
     "gnnrec_spmm_csr_split_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,
                                          _I64, _P, _I64, _P, _P, _I64, _P, _P]),
+    "gnnrec_spmm_backward_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _I64, _I64,
+                                        _INT, _P, _I64, _P]),
     "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P,
                                _I64, _I64, _INT, _INT, _F32, _P, _I64, _P]),
     "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),

@@ -1,10 +1,10 @@
 """Autograd Functions for training through the drop-in modules.
 
 Forward values always come from the HIP kernels (the same launches as the
-inference path, so train/eval numerics agree).  Backward: the transposed
-aggregation and the weight/input gradients are computed with device tensor
-ops on the same stream (recompute-and-differentiate for the fused epilogues).
-Dedicated HIP backward kernels are the next step of row f2.
+inference path, so train/eval numerics agree).  Backward of the aggregation is
+the HIP transposed scatter (gnnrec_spmm_backward_f32, first-arg-max routing
+for max); the projection / linear weight and input gradients are device GEMMs
+on the same stream (recompute-and-differentiate for the fused epilogues).
 """
 from __future__ import annotations
 
@@ -54,22 +54,9 @@ class SpmmFn(torch.autograd.Function):
         m, indptr, indices, ew, out = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
             return None, None, None, None, None, None
-        deg = indptr[1:] - indptr[:-1]
-        dst = torch.repeat_interleave(torch.arange(deg.numel(), device=deg.device), deg)
-        src = indices.long()
-        coef = ew if ew is not None else None
-        if ctx.reduce == 'max':
-            msg = m[src] if coef is None else m[src] * coef[:, None]
-            hit = (msg == out[dst]).to(g.dtype)
-            contrib = g[dst] * hit
-        else:
-            contrib = g[dst]
-            if ctx.reduce == 'mean':
-                contrib = contrib / deg.clamp(min=1).to(g.dtype)[dst][:, None]
-        if coef is not None:
-            contrib = contrib * coef[:, None]
-        gm = torch.zeros_like(m)
-        gm.index_add_(0, src, contrib)
+        gm = ops.spmm_backward(indptr, indices, g, ctx.reduce, edge_weight=ew,
+                               X=m if ctx.reduce == 'max' else None,
+                               out=out if ctx.reduce == 'max' else None, n_src=m.shape[0])
         return gm, None, None, None, None, None
 
 

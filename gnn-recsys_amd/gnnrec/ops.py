@@ -110,6 +110,24 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
     return out
 
 
+def spmm_backward(indptr, indices, grad_out, reduce, edge_weight=None, X=None, out=None,
+                  grad_X=None, n_src=None):
+    """Gradient of spmm w.r.t. its source rows (accumulated into grad_X, created if None)."""
+    lib = _lib.load()
+    _dev(grad_out, "grad_out", torch.float32)
+    n_dst, d = grad_out.shape
+    if grad_X is None:
+        grad_X = torch.zeros((n_src, d), dtype=torch.float32, device=grad_out.device)
+    grad_out = grad_out.contiguous()
+    rc = lib.gnnrec_spmm_backward_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(grad_out),
+                                      d, ptr(X), 0 if X is None else _rowmajor(X, "X"), ptr(out),
+                                      0 if out is None else _rowmajor(out, "out"), n_dst, d,
+                                      REDUCE[reduce], ptr(grad_X), _rowmajor(grad_X, "grad_X"),
+                                      stream_ptr(grad_out.device))
+    check(rc, "gnnrec_spmm_backward_f32")
+    return grad_X
+
+
 def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
          W2: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None, *,
          relu: bool = False, l2norm: bool = False, sigmoid: bool = False,

@@ -96,6 +96,15 @@ int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* indices, con
                               const int64_t* chunk_row, int64_t n_chunks, float* workspace,
                               void* stream);
 
+/* Gradient of gnnrec_spmm_csr_f32 w.r.t. X (training):
+ * grad_X[indices[e]] += (ew ? ew[e] : 1) * grad_out[v] (/ deg for MEAN); for MAX the
+ * gradient of each column goes to the first edge whose message equals out[v]
+ * (X and out are required then).  grad_X is ACCUMULATED with float atomics. */
+int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                             const float* grad_out, int64_t ldg, const float* X, int64_t ldx,
+                             const float* out, int64_t ldo, int64_t n_dst, int64_t d, int reduce,
+                             float* grad_X, int64_t ldgx, void* stream);
+
 /* ---- a2/a3/a4: fp32 MFMA GEMM with fused SAGE epilogue (K4, K7) ---------
  * acc[m,n] = sum_k A1[m,k] W1[n,k] + sum_k T(A2)[m,k] W2[n,k]   (W row-major [N,K] = nn.Linear.weight)
  * z = epi(acc + bias)      epi: relu / sigmoid, then optional row L2 norm

@@ -356,3 +356,35 @@ def test_c2_scale_rows_vs_oracle_and_determinism():
     np.testing.assert_allclose(a[rows].cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
     # degree conservation: sum of degrees == E, mean degree 50
     assert int(indptr[-1].item()) == E
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_backward_matches_reference(reduce, weighted):
+    """f2: HIP transposed scatter vs a numpy restatement (max: first arg-max edge)."""
+    from gnnrec import ops
+    rng = np.random.default_rng(17 + weighted)
+    indptr, idx = _csr(rng, 300, 200, 9)
+    d = 40
+    X = rng.standard_normal((200, d)).astype(np.float32)
+    X[:, :3] = np.round(X[:, :3])  # plenty of exact ties in a few columns
+    w = rng.integers(1, 4, idx.size).astype(np.float32) if weighted else None
+    G = rng.standard_normal((300, d)).astype(np.float32)
+    out = ops.spmm(_t(indptr), _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w))
+    gx = ops.spmm_backward(_t(indptr), _t(idx), _t(G), reduce, None if w is None else _t(w),
+                           X=_t(X), out=out, n_src=200).cpu().numpy()
+    ref = np.zeros_like(X, dtype=np.float64)
+    Y = out.cpu().numpy()
+    for v in range(300):
+        a, b = indptr[v], indptr[v + 1]
+        for c in range(d):
+            g = G[v, c] / ((b - a) if reduce == "mean" and b > a else 1)
+            for e in range(a, b):
+                m = X[idx[e], c] * (w[e] if w is not None else 1)
+                if reduce == "max":
+                    if np.float32(m) == Y[v, c]:
+                        ref[idx[e], c] += g * (w[e] if w is not None else 1)
+                        break
+                else:
+                    ref[idx[e], c] += g * (w[e] if w is not None else 1)
+    np.testing.assert_allclose(gx, ref, rtol=1e-4, atol=1e-5)
