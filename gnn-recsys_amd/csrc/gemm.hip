@@ -33,6 +33,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int LDSK = 36;  // padded k stride (floats)
+#ifndef GEMM_WAVES_PER_SIMD
+#define GEMM_WAVES_PER_SIMD 2
+#endif
 
 struct GemmArgs {
   const float* A1; int64_t lda1; int64_t K1; const float* W1;
@@ -64,13 +67,19 @@ __device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t l
 // then unconditional (out-of-range rows are clamped and zeroed by a select at
 // LDS-store time), so the next tile's loads stay in flight across the MFMAs —
 // a bounds check per load makes hipcc branch around it and wait vmcnt(0).
+// the epilogue stages the output tile in LDS in column halves, so the block's LDS
+// is just the K-loop tiles (36.9 KB at BN=128) and LDS never limits occupancy
+template <int BN>
+constexpr int stage_cols() { return BN >= 64 ? BN / 2 : BN; }
+
 template <int BN>
 constexpr int smem_floats() {
-  return (BM + BN) * LDSK > BM * (BN + 4) ? (BM + BN) * LDSK : BM * (BN + 4);
+  return (BM + BN) * LDSK > BM * (stage_cols<BN>() + 4) ? (BM + BN) * LDSK
+                                                        : BM * (stage_cols<BN>() + 4);
 }
 
 template <int BN, bool FAST>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float smem[smem_floats<BN>()];
   float* As = smem;
   float* Ws = smem + BM * LDSK;
@@ -200,17 +209,16 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     colok[t] = col < g.N;
     bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
   }
-  // staged store: the wave's 32 x BN tile goes through LDS and leaves as whole rows of
-  // 16-B stores (4x fewer, fully coalesced store instructions than per-lane scalars)
-  constexpr int OSTR = BN + 4;
+  // staged store: the wave's 32 x BN tile goes through LDS (in column halves) and leaves
+  // as whole rows of 16-B stores (4x fewer, fully coalesced store instructions)
+  constexpr int SC = stage_cols<BN>();
+  constexpr int OSTR = SC + 4;
+  constexpr int TPR = SC / 32;  // accumulator tiles per staging round
   const bool staged = g.vecO;
   float* Ot = smem + wave * 32 * OSTR;
-  if (staged) __syncthreads();  // every wave is done reading the K-loop tiles
+  float z[16][NT];
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
-    const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
-    const int64_t row = m0 + wave * 32 + rl;
-    float z[NT];
     float ss = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -218,7 +226,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
       if (relu) x = fmaxf(x, 0.f);
       if (sigm) x = 1.f / (1.f + expf(-x));
       if (!colok[t]) x = 0.f;
-      z[t] = x;
+      z[v][t] = x;
       ss += x * x;
     }
     if (l2) {
@@ -227,47 +235,60 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
       float nrm = sqrtf(ss);
       if (nrm == 0.f) nrm = 1.f;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) z[t] = z[t] / nrm;
+      for (int t = 0; t < NT; ++t) z[v][t] = z[v][t] / nrm;
     }
-    if (staged) {
+  }
+  if (!staged) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) Ot[rl * OSTR + t * 32 + r] = z[t];
-    } else if (row < g.M) {
+    for (int v = 0; v < 16; ++v) {
+      const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      if (row >= g.M) continue;
       float* orow = g.out + row * g.ldo + n0;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (!colok[t]) continue;
         float* p = orow + t * 32 + r;
-        float y = z[t];
+        float y = z[v][t];
         if (g.accum == GNNREC_ACC_ADD) y = *p + y;
         else if (g.accum == GNNREC_ACC_MAX) y = fmaxf(*p, y);
         if (g.out_div > 0.f) y = y / g.out_div;
         *p = y;
       }
     }
+    return;
   }
-  if (!staged) return;
-  __syncthreads();
-  constexpr int C4 = BN / 4;               // float4 per row
-  constexpr int ITER = 32 * C4 / kWave;    // float4 per lane
-#pragma unroll 4
-  for (int q = 0; q < ITER; ++q) {
-    const int flat = q * kWave + lane;
-    const int rl = flat / C4;
-    const int c = (flat % C4) * 4;
-    const int64_t row = m0 + wave * 32 + rl;
-    if (row >= g.M || n0 + c >= g.N) continue;
-    f32x4 y = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
-    f32x4* p = reinterpret_cast<f32x4*>(g.out + row * g.ldo + n0 + c);
-    if (g.accum == GNNREC_ACC_ADD) {
-      y = *p + y;
-    } else if (g.accum == GNNREC_ACC_MAX) {
-      const f32x4 o = *p;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+  for (int round = 0; round < NT / TPR; ++round) {
+    __syncthreads();  // K-loop tiles (or the previous round) fully read
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < TPR; ++tt) Ot[rl * OSTR + tt * 32 + r] = z[v][round * TPR + tt];
     }
-    if (g.out_div > 0.f) y = y / g.out_div;
-    *p = y;
+    __syncthreads();
+    constexpr int C4 = SC / 4;               // float4 per staged row
+    constexpr int ITER = 32 * C4 / kWave;    // float4 per lane
+#pragma unroll 4
+    for (int q = 0; q < ITER; ++q) {
+      const int flat = q * kWave + lane;
+      const int rl = flat / C4;
+      const int c = (flat % C4) * 4;
+      const int64_t row = m0 + wave * 32 + rl;
+      const int64_t col = n0 + round * SC + c;
+      if (row >= g.M || col >= g.N) continue;
+      f32x4 y = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+      f32x4* p = reinterpret_cast<f32x4*>(g.out + row * g.ldo + col);
+      if (g.accum == GNNREC_ACC_ADD) {
+        y = *p + y;
+      } else if (g.accum == GNNREC_ACC_MAX) {
+        const f32x4 o = *p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+      }
+      if (g.out_div > 0.f) y = y / g.out_div;
+      *p = y;
+    }
   }
 }
 

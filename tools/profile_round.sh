@@ -24,3 +24,8 @@ timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex 'spmm|gemm' 
   -d "$OUT/${TAG}_write" -o run -- python3 $R/bench.py --steps 1 --warmup 0 --cpu-baseline off $* \
   > "$OUT/${TAG}_write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 1; }
 echo "write pass ok"
+timeout -k 10 420 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE \
+  --kernel-include-regex 'gemm' --output-format csv \
+  -d "$OUT/${TAG}_mfma" -o run -- python3 $R/bench.py --steps 1 --warmup 0 --cpu-baseline off $* \
+  > "$OUT/${TAG}_mfma.log" 2>&1 || { echo "mfma pass failed rc=$?"; exit 1; }
+echo "mfma pass ok"
