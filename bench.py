@@ -102,8 +102,8 @@ def pmc_traffic(args, world):
     import csv
     default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
                args.config) == (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4")
-    f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch_size.csv")
-    w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write_size.csv")
+    f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch.csv")
+    w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write.csv")
     if world != 1 or not default or not (os.path.exists(f) and os.path.exists(w)):
         return None
     tot, n = 0.0, 0
