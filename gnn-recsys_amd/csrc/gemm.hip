@@ -23,6 +23,7 @@
 // reads vectorised (fp32 sums stay within the 1e-4 parity tolerance).
 #include "common.hpp"
 #include <cmath>
+#include <cstdlib>
 
 namespace gnnrec {
 namespace {
@@ -76,6 +77,110 @@ template <int BN>
 constexpr int smem_floats() {
   return (BM + BN) * LDSK > BM * (stage_cols<BN>() + 4) ? (BM + BN) * LDSK
                                                         : BM * (stage_cols<BN>() + 4);
+}
+
+// Shared epilogue: bias, activation, zero-guarded row L2 norm, then the cross-relation
+// accumulate into `out`, staged through LDS (column halves) into whole-row 16-B stores.
+template <int BN>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[BN / 32],
+                                              float* smem, int64_t m0, int64_t n0, int wave,
+                                              int lane) {
+  constexpr int NT = BN / 32;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  // ---- epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (v&3) + 8(v>>2) + 4h
+  const bool relu = g.epilogue & GNNREC_EPI_RELU;
+  const bool sigm = g.epilogue & GNNREC_EPI_SIGMOID;
+  const bool l2 = g.epilogue & GNNREC_EPI_L2NORM;
+  float bias_t[NT];
+  bool colok[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t col = n0 + t * 32 + r;
+    colok[t] = col < g.N;
+    bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
+  }
+  // staged store: the wave's 32 x BN tile goes through LDS (in column halves) and leaves
+  // as whole rows of 16-B stores (4x fewer, fully coalesced store instructions)
+  constexpr int SC = stage_cols<BN>();
+  constexpr int OSTR = SC + 4;
+  constexpr int TPR = SC / 32;  // accumulator tiles per staging round
+  const bool staged = g.vecO;
+  float* Ot = smem + wave * 32 * OSTR;
+  float z[16][NT];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float x = acc[t][v] + bias_t[t];
+      if (relu) x = fmaxf(x, 0.f);
+      if (sigm) x = 1.f / (1.f + expf(-x));
+      if (!colok[t]) x = 0.f;
+      z[v][t] = x;
+      ss += x * x;
+    }
+    if (l2) {
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) ss += __shfl_xor(ss, off);
+      float nrm = sqrtf(ss);
+      if (nrm == 0.f) nrm = 1.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) z[v][t] = z[v][t] / nrm;
+    }
+  }
+  if (!staged) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      if (row >= g.M) continue;
+      float* orow = g.out + row * g.ldo + n0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (!colok[t]) continue;
+        float* p = orow + t * 32 + r;
+        float y = z[v][t];
+        if (g.accum == GNNREC_ACC_ADD) y = *p + y;
+        else if (g.accum == GNNREC_ACC_MAX) y = fmaxf(*p, y);
+        if (g.out_div > 0.f) y = y / g.out_div;
+        *p = y;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int round = 0; round < NT / TPR; ++round) {
+    __syncthreads();  // K-loop tiles (or the previous round) fully read
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < TPR; ++tt) Ot[rl * OSTR + tt * 32 + r] = z[v][round * TPR + tt];
+    }
+    __syncthreads();
+    constexpr int C4 = SC / 4;               // float4 per staged row
+    constexpr int ITER = 32 * C4 / kWave;    // float4 per lane
+#pragma unroll 4
+    for (int q = 0; q < ITER; ++q) {
+      const int flat = q * kWave + lane;
+      const int rl = flat / C4;
+      const int c = (flat % C4) * 4;
+      const int64_t row = m0 + wave * 32 + rl;
+      const int64_t col = n0 + round * SC + c;
+      if (row >= g.M || col >= g.N) continue;
+      f32x4 y = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+      f32x4* p = reinterpret_cast<f32x4*>(g.out + row * g.ldo + col);
+      if (g.accum == GNNREC_ACC_ADD) {
+        y = *p + y;
+      } else if (g.accum == GNNREC_ACC_MAX) {
+        const f32x4 o = *p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+      }
+      if (g.out_div > 0.f) y = y / g.out_div;
+      *p = y;
+    }
+  }
 }
 
 template <int BN, bool FAST>
@@ -197,99 +302,140 @@ __global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(Gemm
     }
   }
 
-  // ---- epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (v&3) + 8(v>>2) + 4h
-  const bool relu = g.epilogue & GNNREC_EPI_RELU;
-  const bool sigm = g.epilogue & GNNREC_EPI_SIGMOID;
-  const bool l2 = g.epilogue & GNNREC_EPI_L2NORM;
-  float bias_t[NT];
-  bool colok[NT];
+  gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
+}
+
+// ---- LDS-DMA variant (aligned operands, K1/K2 multiples of 32) -------------------
+// Tiles move global -> LDS with global_load_lds_dwordx4 (no staging registers), double
+// buffered: tile k+1 is in flight while the MFMAs consume tile k; a counted
+// `s_waitcnt vmcnt` + raw s_barrier publishes it (a __syncthreads() would drain the DMA).
+// The LDS image is lane-linear per wave-instruction (1 KiB = 8 rows x 128 B, unpadded), so
+// bank conflicts are removed on the SOURCE side: 16-B chunk j of tile row R is stored at
+// chunk j ^ ((R >> 1) & 7) of that row, which makes every 16-lane ds_read_b128 group of the
+// fragment reads hit 16 distinct 4-bank slots.
+// one 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane L's bytes land at lds + 16 L.
+// (Kept out of lambdas and host-invisible: a device builtin inside a kernel-template
+// lambda makes hipcc drop the kernel's host launch stub.)
+__device__ __forceinline__ void dma16(const float* src, float* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+#endif
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_barrier() {
+  static_assert(N >= 0 && N <= 15, "vmcnt immediate");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  else static_assert(N == 0, "add the vmcnt immediate");
+}
+
+template <int BN>
+constexpr int glds_smem_floats() {
+  return 2 * (BM + BN) * BK > smem_floats<BN>() ? 2 * (BM + BN) * BK : smem_floats<BN>();
+}
+
+template <int BN>
+__global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_glds_kernel(GemmArgs g) {
+  constexpr int NT = BN / 32;
+  constexpr int AI = BM * BK * 4 / 1024 / 4;   // A-tile DMA instructions per wave (4)
+  constexpr int WI = BN * BK * 4 / 1024 / 4;   // W-tile DMA instructions per wave (BN/32)
+  constexpr int TILE = (BM + BN) * BK;         // floats per buffer
+  __shared__ __attribute__((aligned(16))) float smem[glds_smem_floats<BN>()];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int sw = (r >> 1) & 7;                 // read-side swizzle of this lane's rows
+
+  f32x16 acc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int64_t col = n0 + t * 32 + r;
-    colok[t] = col < g.N;
-    bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+
+  // DMA source rows of this lane (tile row R = instr*8 + lane/8, physical chunk lane%8)
+  int64_t a_row[AI], w_row[WI];
+  int a_chk[AI], w_chk[WI];
+#pragma unroll
+  for (int q = 0; q < AI; ++q) {
+    const int R = (wave * AI + q) * 8 + (lane >> 3);
+    const int64_t gm = m0 + R;
+    a_row[q] = gm < g.M ? gm : g.M - 1;
+    a_chk[q] = ((lane & 7) ^ ((R >> 1) & 7)) * 4;
   }
-  // staged store: the wave's 32 x BN tile goes through LDS (in column halves) and leaves
-  // as whole rows of 16-B stores (4x fewer, fully coalesced store instructions)
-  constexpr int SC = stage_cols<BN>();
-  constexpr int OSTR = SC + 4;
-  constexpr int TPR = SC / 32;  // accumulator tiles per staging round
-  const bool staged = g.vecO;
-  float* Ot = smem + wave * 32 * OSTR;
-  float z[16][NT];
 #pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    float ss = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float x = acc[t][v] + bias_t[t];
-      if (relu) x = fmaxf(x, 0.f);
-      if (sigm) x = 1.f / (1.f + expf(-x));
-      if (!colok[t]) x = 0.f;
-      z[v][t] = x;
-      ss += x * x;
-    }
-    if (l2) {
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) ss += __shfl_xor(ss, off);
-      float nrm = sqrtf(ss);
-      if (nrm == 0.f) nrm = 1.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) z[v][t] = z[v][t] / nrm;
-    }
+  for (int q = 0; q < WI; ++q) {
+    const int R = (wave * WI + q) * 8 + (lane >> 3);
+    const int64_t gn = n0 + R;
+    w_row[q] = gn < g.N ? gn : g.N - 1;
+    w_chk[q] = ((lane & 7) ^ ((R >> 1) & 7)) * 4;
   }
-  if (!staged) {
+  const int64_t my_row = m0 + wave * 32 + r;  // the A row this lane's fragments come from
+
+#pragma unroll 1
+  for (int seg = 0; seg < 2; ++seg) {
+    const float* A = seg ? g.A2 : g.A1;
+    const float* W = seg ? g.W2 : g.W1;
+    const int64_t K = seg ? g.K2 : g.K1;
+    const int64_t lda = seg ? g.lda2 : g.lda1;
+    if (K == 0) continue;
+    const int mode = seg ? g.a2_mode : GNNREC_A2_NONE;
+    float rowdiv = 1.f;
+    bool rowzero = false;
+    if (mode != GNNREC_A2_NONE) {
+      const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
+      if (mode == GNNREC_A2_DIV_DEG) rowdiv = (float)(dg > 0 ? dg : 1);
+      else rowzero = dg == 0;
+    }
+    auto issue = [&](int64_t k0, int buf) {
+      float* base = smem + buf * TILE;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-      if (row >= g.M) continue;
-      float* orow = g.out + row * g.ldo + n0;
+      for (int q = 0; q < AI; ++q)
+        dma16(A + a_row[q] * lda + k0 + a_chk[q], base + (wave * AI + q) * 256);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (!colok[t]) continue;
-        float* p = orow + t * 32 + r;
-        float y = z[v][t];
-        if (g.accum == GNNREC_ACC_ADD) y = *p + y;
-        else if (g.accum == GNNREC_ACC_MAX) y = fmaxf(*p, y);
-        if (g.out_div > 0.f) y = y / g.out_div;
-        *p = y;
+      for (int q = 0; q < WI; ++q)
+        dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK + (wave * WI + q) * 256);
+    };
+    const int nk = (int)(K / BK);
+    issue(0, 0);
+#pragma unroll 1
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) {
+        issue((int64_t)(kt + 1) * BK, buf ^ 1);
+        wait_vmcnt_barrier<AI + WI>();  // this wave's tile-kt DMA landed; all waves past it
+      } else {
+        wait_vmcnt_barrier<0>();
       }
-    }
-    return;
-  }
+      const float* As = smem + buf * TILE + (wave * 32 + r) * BK;
+      const float* Ws = smem + buf * TILE + BM * BK + r * BK;
 #pragma unroll
-  for (int round = 0; round < NT / TPR; ++round) {
-    __syncthreads();  // K-loop tiles (or the previous round) fully read
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int pc = ((h * 4 + s4) ^ sw) * 4;
+        f32x4 a = *reinterpret_cast<const f32x4*>(As + pc);
+        if (mode == GNNREC_A2_DIV_DEG) a = a / rowdiv;
+        else if (rowzero) a = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 b[NT];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+        for (int t = 0; t < NT; ++t)
+          b[t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK + pc);
 #pragma unroll
-      for (int tt = 0; tt < TPR; ++tt) Ot[rl * OSTR + tt * 32 + r] = z[v][round * TPR + tt];
-    }
-    __syncthreads();
-    constexpr int C4 = SC / 4;               // float4 per staged row
-    constexpr int ITER = 32 * C4 / kWave;    // float4 per lane
-#pragma unroll 4
-    for (int q = 0; q < ITER; ++q) {
-      const int flat = q * kWave + lane;
-      const int rl = flat / C4;
-      const int c = (flat % C4) * 4;
-      const int64_t row = m0 + wave * 32 + rl;
-      const int64_t col = n0 + round * SC + c;
-      if (row >= g.M || col >= g.N) continue;
-      f32x4 y = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
-      f32x4* p = reinterpret_cast<f32x4*>(g.out + row * g.ldo + col);
-      if (g.accum == GNNREC_ACC_ADD) {
-        y = *p + y;
-      } else if (g.accum == GNNREC_ACC_MAX) {
-        const f32x4 o = *p;
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
       }
-      if (g.out_div > 0.f) y = y / g.out_div;
-      *p = y;
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
     }
   }
+  gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
 }
 
 template <int BN>
@@ -297,7 +443,12 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.N + BN - 1) / BN));
   const bool fast = g.vecA1 && g.vecW1 && g.K1 % BK == 0 &&
                     (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK == 0));
-  if (fast) hipLaunchKernelGGL((gemm_f32_kernel<BN, true>), grid, dim3(256), 0, s, g);
+  static const bool use_dma = [] {
+    const char* e = getenv("GNNREC_GEMM_DMA");
+    return !(e && e[0] == '0');
+  }();
+  if (fast && use_dma) hipLaunchKernelGGL((gemm_f32_glds_kernel<BN>), grid, dim3(256), 0, s, g);
+  else if (fast) hipLaunchKernelGGL((gemm_f32_kernel<BN, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gemm_f32_kernel<BN, false>), grid, dim3(256), 0, s, g);
   return check_launch("gnnrec_gemm_f32");
 }
