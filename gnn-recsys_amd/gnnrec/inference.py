@@ -400,3 +400,35 @@ def gather_partitioned(shard: GraphShard, rows: torch.Tensor, exchange: Exchange
     dist.all_gather(parts, pad, group=exchange.group)
     b = even_ranges(n, exchange.ws)
     return torch.cat([parts[r][: b[r + 1] - b[r]] for r in range(exchange.ws)], 0)
+
+
+@torch.no_grad()
+def inference_ondemand(graph, trained_model, user_ids='all', k: int = 10,
+                       already_bought_dict=None, remove_already_bought: bool = True,
+                       pred: str = 'cos', use_popularity: bool = False,
+                       weight_popularity: float = 1.0, embedding_layer=None):
+    """Embedding pass + recommendations on the device, the hot part of reference
+    main_inference.py:20-175 (`inference_ondemand`): full-graph embeddings of every
+    user and item (:123-152), then top-k per requested user with already-bought items
+    removed (:153-166).  `graph` is a HeteroGraph (or a path written by gnnrec.io).
+
+    Returns (recs {user: np.ndarray[k]}, embeddings {ntype: tensor})."""
+    import numpy as np
+
+    from .io import read_graph
+    from .recs import create_already_bought, get_recs
+    g = read_graph(graph, device=torch.device('cuda')) if isinstance(graph, str) else graph
+    trained_model.eval()
+    h = full_graph_embeddings(g, trained_model, embedding_layer=embedding_layer)
+    if isinstance(user_ids, str) and user_ids == 'all':
+        user_ids = np.arange(g.num_nodes('user'))
+    if already_bought_dict is None:
+        users = torch.as_tensor(user_ids, device=g.device)
+        s, _ = g.all_edges(etype='buys')
+        bought = torch.nonzero(torch.isin(s, users)).squeeze(1)
+        already_bought_dict = create_already_bought(g, bought, etype='buys')
+    out_dim = h['item'].shape[1]
+    recs = get_recs(g, h, trained_model, out_dim, k, list(np.asarray(user_ids).tolist()),
+                    already_bought_dict, remove_already_bought, True, g.device, pred,
+                    use_popularity, weight_popularity)
+    return recs, h

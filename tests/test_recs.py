@@ -70,3 +70,41 @@ def test_topk_rows_edge_cases():
         np.testing.assert_array_equal(idx[r], ref)
     assert idx[1][0] == 10 and 20 not in idx[1]
     assert (idx[2] == -1).all()
+
+
+@pytest.mark.gpu
+def test_inference_ondemand_end_to_end(tmp_path):
+    """graph file -> ConvModel -> full-graph embeddings -> top-k, vs the oracle composition."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.inference import inference_ondemand
+    from gnnrec.io import save_graphs
+    from oracle import oracle
+    rng = np.random.default_rng(3)
+    n_u, n_i, E = 120, 80, 900
+    u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+    edges = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d)) for ce, (s, d) in edges.items()},
+                    {"user": n_u, "item": n_i})
+    feats = {"user": rng.standard_normal((n_u, 5)).astype(np.float32),
+             "item": rng.standard_normal((n_i, 6)).astype(np.float32)}
+    for nt, f in feats.items():
+        g.nodes[nt].data["features"] = torch.from_numpy(f)
+    path = str(tmp_path / "g.bin")
+    save_graphs(path, [g])
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 5, "item": 6, "hidden": 32, "out": 16}, True, 0.0,
+                          "mean_nn", "cos", "sum", True).cuda()
+    recs, h = inference_ondemand(path, model, user_ids=[0, 5, 7], k=5)
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    ref = oracle.model_full_graph(oracle.Graph({"user": n_u, "item": n_i}, edges), feats, sd,
+                                  "mean_nn", "sum", True, True)
+    for nt in ref:
+        np.testing.assert_allclose(h[nt].cpu().numpy(), ref[nt], rtol=1e-4, atol=1e-5)
+    iu = ref["item"] / np.maximum(np.linalg.norm(ref["item"], axis=1, keepdims=True), 1e-12)
+    for user in (0, 5, 7):
+        hu = ref["user"][user] / max(np.linalg.norm(ref["user"][user]), 1e-12)
+        scores = iu @ hu
+        bought = set(i[u == user].tolist())
+        order = [j for j in np.argsort(-scores, kind="stable") if j not in bought][:5]
+        np.testing.assert_array_equal(recs[user], order)
