@@ -15,84 +15,143 @@
 namespace gnnrec {
 namespace {
 
-// Fanout choice for one seed: positions 0..deg-1 -> pick k distinct, ascending.
-// Robert Floyd's algorithm keyed on a counter hash (restated in oracle.c).
+// A group of G lanes (G = 8..64, a power of two >= fanout) per seed.  Fanout
+// choice for a row of degree deg > k: Robert Floyd's algorithm keyed on a
+// counter hash (restated in oracle.c).  The hash of every step is independent
+// of the others, so lane s computes step s's candidate; only the duplicate
+// resolution is sequential (a ballot over the group's lanes < s per step).
+// Picks are emitted in ascending position order: a lane's output slot = number
+// of kept picks with a smaller position (picks are distinct), so no sort and
+// no scratch array is needed.
 constexpr int kMaxFanout = 64;
+constexpr int kBlock = 256;
 
-__device__ int choose_positions(uint64_t key, int64_t v, int64_t deg, int k, int64_t* pos) {
-  int n = 0;
-  for (int64_t j = deg - k; j < deg; ++j) {
-    const uint64_t hsh = hash3(key, (uint64_t)v, (uint64_t)j);
-    const int64_t t = (int64_t)(hsh % (uint64_t)(j + 1));
-    bool dup = false;
-    for (int q = 0; q < n; ++q) dup |= (pos[q] == t);
-    pos[n++] = dup ? j : t;
+template <int G>
+struct Group {
+  int lane;        // lane within the group
+  int base;        // first wave lane of the group
+  uint64_t bits;   // the group's bits in a wave ballot
+  __device__ Group() {
+    const int wl = (int)(threadIdx.x & (kWave - 1));
+    lane = wl & (G - 1);
+    base = wl - lane;
+    bits = (G == 64 ? ~0ull : ((1ull << G) - 1)) << base;
   }
-  // insertion sort ascending
-  for (int a = 1; a < n; ++a) {
-    const int64_t x = pos[a];
-    int b = a - 1;
-    while (b >= 0 && pos[b] > x) { pos[b + 1] = pos[b]; --b; }
-    pos[b + 1] = x;
+  __device__ uint64_t ballot(bool p) const { return __ballot(p) & bits; }
+  // set lanes of the group below this one
+  __device__ int below(uint64_t mask) const {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
   }
-  return n;
+};
+
+template <int G>
+__device__ inline int64_t floyd_pick(const Group<G>& grp, uint64_t key, int64_t v, int64_t deg,
+                                     int k) {
+  const int64_t jl = deg - k + grp.lane;  // this lane's step (valid for lane < k)
+  const int64_t tl = grp.lane < k
+      ? (int64_t)(hash3(key, (uint64_t)v, (uint64_t)jl) % (uint64_t)(jl + 1)) : -1;
+  int64_t mine = -1;
+  for (int s = 0; s < k; ++s) {
+    const int64_t t = __shfl(tl, grp.base + s);
+    const bool dup = grp.ballot(grp.lane < s && mine == t) != 0ull;
+    if (grp.lane == s) mine = dup ? jl : t;
+  }
+  return mine;  // lanes >= k: -1
 }
 
-__global__ void sample_count_kernel(const int64_t* __restrict__ indptr,
-                                    const int64_t* __restrict__ eids,
-                                    const uint8_t* __restrict__ excluded,
-                                    const int64_t* __restrict__ seeds, int64_t n_seeds,
-                                    int64_t fanout, uint64_t key, int64_t* __restrict__ counts) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_seeds) return;
+template <int G>
+__global__ __launch_bounds__(kBlock) void sample_count_kernel(
+    const int64_t* __restrict__ indptr, const int64_t* __restrict__ eids,
+    const uint8_t* __restrict__ excluded, const int64_t* __restrict__ seeds, int64_t n_seeds,
+    int64_t fanout, uint64_t key, int64_t* __restrict__ counts) {
+  const Group<G> grp;
+  const int64_t i = (int64_t)blockIdx.x * (kBlock / G) + (threadIdx.x / G);
+  if (i >= n_seeds) return;  // uniform per group; groups never share a ballot result
   const int64_t v = seeds[i];
   const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
-  int64_t c = 0;
+  int64_t c;
   if (fanout < 0 || deg <= fanout) {
-    if (!excluded) c = deg;
-    else
-      for (int64_t e = beg; e < end; ++e) c += excluded[eids[e]] ? 0 : 1;
+    if (!excluded) {
+      c = deg;
+    } else {
+      c = 0;
+      for (int64_t e0 = beg; e0 < end; e0 += G) {
+        const int64_t e = e0 + grp.lane;
+        c += __popcll(grp.ballot(e < end && !excluded[eids[e]]));
+      }
+    }
+  } else if (!excluded) {
+    c = fanout;
   } else {
-    int64_t pos[kMaxFanout];
-    const int n = choose_positions(key, v, deg, (int)fanout, pos);
-    for (int q = 0; q < n; ++q) c += (excluded && excluded[eids[beg + pos[q]]]) ? 0 : 1;
+    const int64_t p = floyd_pick(grp, key, v, deg, (int)fanout);
+    c = __popcll(grp.ballot(p >= 0 && !excluded[eids[beg + p]]));
   }
-  counts[i] = c;
+  if (grp.lane == 0) counts[i] = c;
 }
 
-__global__ void sample_fill_kernel(const int64_t* __restrict__ indptr,
-                                   const int64_t* __restrict__ indices,
-                                   const int64_t* __restrict__ eids,
-                                   const uint8_t* __restrict__ excluded,
-                                   const int64_t* __restrict__ seeds, int64_t n_seeds,
-                                   int64_t fanout, uint64_t key,
-                                   const int64_t* __restrict__ out_indptr,
-                                   int64_t* __restrict__ out_src, int64_t* __restrict__ out_eid) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+template <int G>
+__global__ __launch_bounds__(kBlock) void sample_fill_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const int64_t* __restrict__ eids, const uint8_t* __restrict__ excluded,
+    const int64_t* __restrict__ seeds, int64_t n_seeds, int64_t fanout, uint64_t key,
+    const int64_t* __restrict__ out_indptr, int64_t* __restrict__ out_src,
+    int64_t* __restrict__ out_eid) {
+  const Group<G> grp;
+  const int64_t i = (int64_t)blockIdx.x * (kBlock / G) + (threadIdx.x / G);
   if (i >= n_seeds) return;
   const int64_t v = seeds[i];
   const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
   int64_t o = out_indptr[i];
   if (fanout < 0 || deg <= fanout) {
-    for (int64_t e = beg; e < end; ++e) {
-      const int64_t id = eids[e];
-      if (excluded && excluded[id]) continue;
-      out_src[o] = indices[e];
-      out_eid[o] = id;
-      ++o;
+    // whole row in edge order; two chunks in flight per iteration
+    for (int64_t e0 = beg; e0 < end; e0 += 2 * G) {
+      const int64_t ea = e0 + grp.lane, eb = ea + G;
+      const bool va = ea < end, vb = eb < end;
+      const int64_t ida = va ? eids[ea] : 0, idb = vb ? eids[eb] : 0;
+      const int32_t sa = va ? indices[ea] : 0, sb = vb ? indices[eb] : 0;
+      const bool ka = va && !(excluded && excluded[ida]);
+      const bool kb = vb && !(excluded && excluded[idb]);
+      const uint64_t ma = grp.ballot(ka), mb = grp.ballot(kb);
+      if (ka) {
+        const int64_t q = o + grp.below(ma);
+        out_src[q] = sa;
+        out_eid[q] = ida;
+      }
+      o += __popcll(ma);
+      if (kb) {
+        const int64_t q = o + grp.below(mb);
+        out_src[q] = sb;
+        out_eid[q] = idb;
+      }
+      o += __popcll(mb);
     }
   } else {
-    int64_t pos[kMaxFanout];
-    const int n = choose_positions(key, v, deg, (int)fanout, pos);
-    for (int q = 0; q < n; ++q) {
-      const int64_t e = beg + pos[q];
-      const int64_t id = eids[e];
-      if (excluded && excluded[id]) continue;
-      out_src[o] = indices[e];
-      out_eid[o] = id;
-      ++o;
+    const int k = (int)fanout;
+    const int64_t p = floyd_pick(grp, key, v, deg, k);
+    const bool valid = p >= 0;
+    const int64_t e = beg + (valid ? p : 0);
+    const int64_t id = valid ? eids[e] : 0;
+    const bool keep = valid && !(excluded && excluded[id]);
+    int slot = 0;
+    for (int r = 0; r < k; ++r) {
+      const int64_t pr = __shfl(p, grp.base + r);
+      const int kr = __shfl((int)keep, grp.base + r);
+      slot += (kr && pr < p) ? 1 : 0;
+    }
+    if (keep) {
+      out_src[o + slot] = indices[e];
+      out_eid[o + slot] = id;
     }
   }
+}
+
+// lanes per seed: full rows 64 (long rows stream), else the smallest power of two >= fanout
+inline int group_size(int64_t fanout) {
+  if (fanout < 0 || fanout > 32) return 64;
+  if (fanout > 16) return 32;
+  if (fanout > 8) return 16;
+  return 8;
 }
 
 // ---------------------------------------------------------------- scan -----
@@ -248,12 +307,22 @@ extern "C" int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids,
                  kMaxFanout);
   GNNREC_REQUIRE(!excluded || eids, "gnnrec_sample_count: exclusion needs eids");
   if (n_seeds == 0) return GNNREC_OK;
-  hipLaunchKernelGGL(sample_count_kernel, dim3(nblk(n_seeds)), dim3(256), 0, as_stream(stream),
-                     indptr, eids, excluded, seeds, n_seeds, fanout, seed_key, counts);
+  const int G = group_size(fanout);
+  const dim3 grid((unsigned)((n_seeds + kBlock / G - 1) / (kBlock / G)));
+#define GNNREC_COUNT(g)                                                                     \
+  hipLaunchKernelGGL(sample_count_kernel<g>, grid, dim3(kBlock), 0, as_stream(stream), indptr, \
+                     eids, excluded, seeds, n_seeds, fanout, seed_key, counts)
+  switch (G) {
+    case 8: GNNREC_COUNT(8); break;
+    case 16: GNNREC_COUNT(16); break;
+    case 32: GNNREC_COUNT(32); break;
+    default: GNNREC_COUNT(64); break;
+  }
+#undef GNNREC_COUNT
   return check_launch("gnnrec_sample_count");
 }
 
-extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int64_t* indices,
+extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int32_t* indices,
                                   const int64_t* eids, const uint8_t* excluded,
                                   const int64_t* seeds, int64_t n_seeds, int64_t fanout,
                                   uint64_t seed_key, const int64_t* out_indptr, int64_t* out_src,
@@ -262,9 +331,19 @@ extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int64_t* indices,
   GNNREC_REQUIRE(fanout < 0 || fanout <= kMaxFanout, "gnnrec_sample_fill: fanout > %d",
                  kMaxFanout);
   if (n_seeds == 0) return GNNREC_OK;
-  hipLaunchKernelGGL(sample_fill_kernel, dim3(nblk(n_seeds)), dim3(256), 0, as_stream(stream),
-                     indptr, indices, eids, excluded, seeds, n_seeds, fanout, seed_key,
-                     out_indptr, out_src, out_eid);
+  const int G = group_size(fanout);
+  const dim3 grid((unsigned)((n_seeds + kBlock / G - 1) / (kBlock / G)));
+#define GNNREC_FILL(g)                                                                      \
+  hipLaunchKernelGGL(sample_fill_kernel<g>, grid, dim3(kBlock), 0, as_stream(stream), indptr,  \
+                     indices, eids, excluded, seeds, n_seeds, fanout, seed_key, out_indptr,    \
+                     out_src, out_eid)
+  switch (G) {
+    case 8: GNNREC_FILL(8); break;
+    case 16: GNNREC_FILL(16); break;
+    case 32: GNNREC_FILL(32); break;
+    default: GNNREC_FILL(64); break;
+  }
+#undef GNNREC_FILL
   return check_launch("gnnrec_sample_fill");
 }
 

@@ -1,17 +1,23 @@
 """Autograd Functions for training through the drop-in modules.
 
 Forward values always come from the HIP kernels (the same launches as the
-inference path, so train/eval numerics agree).  Backward of the aggregation is
-the HIP transposed scatter (gnnrec_spmm_backward_f32, first-arg-max routing
-for max); the projection / linear weight and input gradients are device GEMMs
-on the same stream (recompute-and-differentiate for the fused epilogues).
+inference path, so train/eval numerics agree).  Backward, all HIP:
+  * aggregation: the transposed scatter (gnnrec_spmm_backward_f32, first-arg-max
+    routing for max, as DGL's gSpMM backward);
+  * projections: the pre-activation is recomputed by gnnrec_gemm_f32, the
+    ReLU/zero-guarded-norm epilogue is differentiated by gnnrec_act_backward_f32,
+    input gradients are gnnrec_gemm_f32 against the transposed weights and weight
+    gradients the split-K gnnrec_gemm_tn_f32 (dW = dYᵀ X);
+  * cosine head: the two reduction sides of gSDDMM's backward are weighted
+    gSpMMs over the pair graph sorted by src and by dst (DGL's rule: the
+    backward of an SDDMM is an SpMM on the same / reversed graph).
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
+from .graph import build_csr
 
 
 class LinearFn(torch.autograd.Function):
@@ -29,12 +35,13 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, W, y = ctx.saved_tensors
-        if ctx.relu:
-            gy = gy * (y > 0).to(gy.dtype)
+        if ctx.relu:  # y = relu(u): y > 0 exactly where u > 0
+            gy = ops.act_backward(y, gy, relu=True, l2norm=False)
         elif ctx.sigmoid:
             gy = gy * y * (1 - y)
-        gx = gy @ W if ctx.needs_input_grad[0] else None
-        gW = gy.t() @ x if ctx.needs_input_grad[1] else None
+        gy = gy.contiguous()
+        gx = ops.gemm(gy, W.t().contiguous()) if ctx.needs_input_grad[0] else None
+        gW = ops.gemm_tn(gy, x.contiguous()) if ctx.needs_input_grad[1] else None
         gb = gy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         return gx, gW, gb, None, None
 
@@ -74,15 +81,15 @@ class SageProjectFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gz):
         h_self, agg, Ws, Wn = ctx.saved_tensors
-        with torch.enable_grad():
-            ins = [t.detach().requires_grad_(True) for t in (h_self, agg, Ws, Wn)]
-            z = torch.relu(ins[0] @ ins[2].t() + ins[1] @ ins[3].t())
-            if ctx.norm:
-                n = z.norm(2, 1, keepdim=True)
-                z = z / torch.where(n == 0, torch.ones_like(n), n)
-            grads = torch.autograd.grad(z, ins, gz, allow_unused=True)
-        return tuple(gr if need else None for gr, need in
-                     zip(grads, ctx.needs_input_grad[:4])) + (None,)
+        need = ctx.needs_input_grad
+        u = ops.gemm(h_self.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach())
+        gu = ops.act_backward(u, gz, relu=True, l2norm=ctx.norm)
+        del u
+        g_self = ops.gemm(gu, Ws.t().contiguous()) if need[0] else None
+        g_agg = ops.gemm(gu, Wn.t().contiguous()) if need[1] else None
+        g_Ws = ops.gemm_tn(gu, h_self.contiguous()) if need[2] else None
+        g_Wn = ops.gemm_tn(gu, agg.contiguous()) if need[3] else None
+        return g_self, g_agg, g_Ws, g_Wn, None
 
 
 class CosineFn(torch.autograd.Function):
@@ -97,9 +104,34 @@ class CosineFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         hs, hd, src, dst = ctx.saved_tensors
-        with torch.enable_grad():
-            a = hs.detach().requires_grad_(True)
-            b = hd.detach().requires_grad_(True)
-            cos = (F.normalize(a, p=2, dim=-1)[src] * F.normalize(b, p=2, dim=-1)[dst]).sum(-1)
-            ga, gb = torch.autograd.grad(cos, (a, b), g, allow_unused=True)
+        need = ctx.needs_input_grad
+        g = g.reshape(-1).contiguous()
+        # â = h / max(‖h‖, eps): gradient wrt â, then through the normalisation
+        a_hat, a_n = _normalize(hs)
+        b_hat, b_n = _normalize(hd)
+        ga = gb = None
+        if need[0]:  # Gâ[s] = Σ_{e: src_e = s} g_e b̂[dst_e]
+            ip, ix, perm = build_csr(dst, src, hs.shape[0])
+            ga = _normalize_backward(a_hat, a_n, ops.spmm(ip, ix, b_hat, "sum",
+                                                          edge_weight=g[perm]))
+        if need[1]:  # Gb̂[d] = Σ_{e: dst_e = d} g_e â[src_e]
+            ip, ix, perm = build_csr(src, dst, hd.shape[0])
+            gb = _normalize_backward(b_hat, b_n, ops.spmm(ip, ix, a_hat, "sum",
+                                                          edge_weight=g[perm]))
         return ga, gb, None, None
+
+
+_EPS = 1e-12
+
+
+def _normalize(h):
+    """F.normalize(h, p=2, dim=-1) (eps 1e-12) and the row norms."""
+    n = h.norm(2, 1, keepdim=True)
+    return h / n.clamp_min(_EPS), n
+
+
+def _normalize_backward(h_hat, n, g_hat):
+    """gradient of h_hat = h / max(‖h‖, eps) given d/dh_hat."""
+    big = n > _EPS
+    dot = (h_hat * g_hat).sum(1, keepdim=True)
+    return torch.where(big, (g_hat - h_hat * dot) / n.clamp_min(_EPS), g_hat / _EPS)

@@ -226,9 +226,9 @@ class HeteroGraph:
         return self._csr[ce]
 
     def in_csr_global(self, etype):
-        """CSR for sampling: (indptr, src int64 global, eids)."""
-        indptr, indices, eids = self.in_csr(etype)
-        return indptr, indices.to(torch.int64), eids
+        """CSR for sampling: (indptr, src global ids int32, eids) -- the cached in_csr
+        arrays themselves (the sampler widens ids to int64 as it copies them)."""
+        return self.in_csr(etype)
 
     def in_degrees(self, etype) -> torch.Tensor:
         indptr = self.in_csr(etype)[0]

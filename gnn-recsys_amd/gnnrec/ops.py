@@ -175,6 +175,55 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
     return out
 
 
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
+            accumulate: bool = False) -> torch.Tensor:
+    """f2 weight gradient: out [M,N] (+)= Aᵀ B for A [K,M], B [K,N] (dW = dYᵀ X).
+
+    Deterministic split-K MFMA (gnnrec_gemm_tn_f32)."""
+    lib = _lib.load()
+    _dev(A, "A", torch.float32)
+    _dev(B, "B", torch.float32)
+    K, M = A.shape
+    if B.shape[0] != K:
+        raise ValueError(f"gemm_tn: A {tuple(A.shape)} and B {tuple(B.shape)} differ in K")
+    N = B.shape[1]
+    lda, ldb = _rowmajor(A, "A"), _rowmajor(B, "B")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulating gemm_tn needs an out tensor")
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    else:
+        _dev(out, "out", torch.float32)
+        if tuple(out.shape) != (M, N):
+            raise ValueError(f"out must be [{M}, {N}]")
+    ldc = _rowmajor(out, "out")
+    nbytes = lib.gnnrec_gemm_tn_workspace_bytes(K, M, N)
+    ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=A.device)
+    check(lib.gnnrec_gemm_tn_f32(ptr(A), lda, ptr(B), ldb, K, M, N, ptr(out), ldc,
+                                 int(accumulate), ptr(ws), stream_ptr(A.device)),
+          "gnnrec_gemm_tn_f32")
+    return out
+
+
+def act_backward(u: torch.Tensor, gz: torch.Tensor, relu: bool, l2norm: bool,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """f2: gradient through z = norm?(relu?(u)) (zero-guarded row norm) for pre-activation u."""
+    lib = _lib.load()
+    _dev(u, "u", torch.float32)
+    _dev(gz, "gz", torch.float32)
+    if gz.shape != u.shape:
+        raise ValueError("act_backward: u and gz shapes differ")
+    n, d = u.shape
+    gz = gz.contiguous()
+    if out is None:
+        out = torch.empty_like(u)
+    flags = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
+    check(lib.gnnrec_act_backward_f32(ptr(u), _rowmajor(u, "u"), ptr(gz), _rowmajor(gz, "gz"), n,
+                                      d, flags, ptr(out), _rowmajor(out, "out"),
+                                      stream_ptr(u.device)), "gnnrec_act_backward_f32")
+    return out
+
+
 def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
               Hd: torch.Tensor) -> torch.Tensor:
     """a7: cosine of the L2-normalised endpoint rows, one value per edge -> [E]."""
@@ -249,30 +298,51 @@ def exclusive_scan(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def sample_count(indptr, eids, seeds, fanout: int, seed_key: int = 0,
+                 excluded: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a9 phase 1: per-seed sampled in-edge counts -> out_indptr [n_seeds+1] (device)."""
+    lib = _lib.load()
+    for t, n in ((indptr, "indptr"), (eids, "eids"), (seeds, "seeds")):
+        _dev(t, n, torch.int64)
+    if excluded is not None:
+        _dev(excluded, "excluded", torch.uint8)
+    n = seeds.numel()
+    fan = -1 if fanout is None or fanout < 0 else int(fanout)
+    counts = torch.empty(n, dtype=torch.int64, device=seeds.device)
+    check(lib.gnnrec_sample_count(ptr(indptr), ptr(eids), ptr(excluded), ptr(seeds), n, fan,
+                                  seed_key & 0xFFFFFFFFFFFFFFFF, ptr(counts),
+                                  stream_ptr(seeds.device)), "gnnrec_sample_count")
+    return exclusive_scan(counts)
+
+
+def sample_fill(indptr, indices, eids, seeds, fanout: int, seed_key: int, out_indptr,
+                total: int, excluded: Optional[torch.Tensor] = None):
+    """a9 phase 2: copy the sampled edges at out_indptr offsets -> (src ids, eids).
+
+    indices: the CSR's int32 source ids (graph.in_csr); outputs are int64."""
+    lib = _lib.load()
+    _dev(indices, "indices", torch.int32)
+    n = seeds.numel()
+    fan = -1 if fanout is None or fanout < 0 else int(fanout)
+    out_src = torch.empty(total, dtype=torch.int64, device=seeds.device)
+    out_eid = torch.empty(total, dtype=torch.int64, device=seeds.device)
+    check(lib.gnnrec_sample_fill(ptr(indptr), ptr(indices), ptr(eids), ptr(excluded), ptr(seeds),
+                                 n, fan, seed_key & 0xFFFFFFFFFFFFFFFF, ptr(out_indptr),
+                                 ptr(out_src), ptr(out_eid), stream_ptr(seeds.device)),
+          "gnnrec_sample_fill")
+    return out_src, out_eid
+
+
 def sample_neighbors(indptr, indices, eids, seeds, fanout: int, seed_key: int = 0,
                      excluded: Optional[torch.Tensor] = None):
     """a9: in-edges of `seeds` (all, or `fanout` without replacement), minus excluded eids.
 
-    Returns (out_indptr [n_seeds+1], src global ids [E'], eids [E'])."""
-    lib = _lib.load()
-    for t, n in ((indptr, "indptr"), (indices, "indices"), (eids, "eids"), (seeds, "seeds")):
-        _dev(t, n, torch.int64)
-    if excluded is not None:
-        _dev(excluded, "excluded", torch.uint8)
-    s = stream_ptr(seeds.device)
-    n = seeds.numel()
-    fan = -1 if fanout is None or fanout < 0 else int(fanout)
-    key = seed_key & 0xFFFFFFFFFFFFFFFF
-    counts = torch.empty(n, dtype=torch.int64, device=seeds.device)
-    check(lib.gnnrec_sample_count(ptr(indptr), ptr(eids), ptr(excluded), ptr(seeds), n, fan, key,
-                                  ptr(counts), s), "gnnrec_sample_count")
-    out_indptr = exclusive_scan(counts)
-    total = int(out_indptr[-1].item())  # size readback (the sampler's one host sync)
-    out_src = torch.empty(total, dtype=torch.int64, device=seeds.device)
-    out_eid = torch.empty(total, dtype=torch.int64, device=seeds.device)
-    check(lib.gnnrec_sample_fill(ptr(indptr), ptr(indices), ptr(eids), ptr(excluded), ptr(seeds),
-                                 n, fan, key, ptr(out_indptr), ptr(out_src), ptr(out_eid), s),
-          "gnnrec_sample_fill")
+    indices is the CSR's int32 source-id array; returns (out_indptr [n_seeds+1],
+    src global ids int64 [E'], eids [E'])."""
+    out_indptr = sample_count(indptr, eids, seeds, fanout, seed_key, excluded)
+    total = int(out_indptr[-1].item())  # size readback
+    out_src, out_eid = sample_fill(indptr, indices, eids, seeds, fanout, seed_key, out_indptr,
+                                   total, excluded)
     return out_indptr, out_src, out_eid
 
 
@@ -280,39 +350,51 @@ class Relabeler:
     """Per-node-type scratch for to_block relabelling (mark array + prefix map).
 
     Keeps two arrays of size n_nodes resident on the device (reset after each
-    use by touching only the ids that were set)."""
+    use by touching only the ids that were set).  `relabel` is the one-shot form;
+    begin / mark / finish split it so a caller can batch the size readback of
+    several node types into one host sync."""
 
     def __init__(self, n_nodes: int, device):
         self.n_nodes = n_nodes
         self.prefix_pos = torch.full((n_nodes,), -1, dtype=torch.int64, device=device)
         self.mark = torch.zeros(n_nodes, dtype=torch.int32, device=device)
 
-    def relabel(self, prefix: torch.Tensor, id_lists):
-        """prefix: dst ids [n_p]; id_lists: list of global src id tensors.
-
-        Returns (src_nodes [n_p + n_new] global ids, [local ids per list])."""
+    def begin(self, prefix: torch.Tensor, id_lists):
+        """set the prefix map, mark new ids, scan -> rank (device; rank[-1] = n_new)."""
         lib = _lib.load()
         s = stream_ptr(prefix.device)
-        n_p = prefix.numel()
-        check(lib.gnnrec_set_prefix_pos(ptr(prefix), n_p, ptr(self.prefix_pos), s), "set_prefix")
+        check(lib.gnnrec_set_prefix_pos(ptr(prefix), prefix.numel(), ptr(self.prefix_pos), s),
+              "set_prefix")
         for ids in id_lists:
             check(lib.gnnrec_mark_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(self.mark),
                                       s), "mark_ids")
-        rank = exclusive_scan(self.mark)
-        n_new = int(rank[-1].item())
+        return exclusive_scan(self.mark)
+
+    def finish(self, prefix: torch.Tensor, id_lists, rank: torch.Tensor, n_new: int):
+        """compact the new ids, relabel every list, reset the scratch."""
+        lib = _lib.load()
+        s = stream_ptr(prefix.device)
+        n_p = prefix.numel()
         src_nodes = torch.empty(n_p + n_new, dtype=torch.int64, device=prefix.device)
         src_nodes[:n_p] = prefix
-        check(lib.gnnrec_compact_marked(ptr(self.mark), ptr(rank), self.n_nodes,
-                                        ptr(src_nodes[n_p:]) if n_new else 0, s), "compact")
+        if n_new:
+            check(lib.gnnrec_compact_marked(ptr(self.mark), ptr(rank), self.n_nodes,
+                                            ptr(src_nodes[n_p:]), s), "compact")
         locals_ = []
         for ids in id_lists:
             loc = torch.empty(ids.numel(), dtype=torch.int64, device=prefix.device)
             check(lib.gnnrec_relabel_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(rank),
                                          n_p, ptr(loc), s), "relabel")
             locals_.append(loc)
-        # reset scratch: prefix map by the prefix ids, mark by the new ids
         check(lib.gnnrec_clear_prefix_pos(ptr(prefix), n_p, ptr(self.prefix_pos), s),
               "clear_prefix")
         if n_new:
             self.mark.index_fill_(0, src_nodes[n_p:], 0)
         return src_nodes, locals_
+
+    def relabel(self, prefix: torch.Tensor, id_lists):
+        """prefix: dst ids [n_p]; id_lists: list of global src id tensors.
+
+        Returns (src_nodes [n_p + n_new] global ids, [local ids per list])."""
+        rank = self.begin(prefix, id_lists)
+        return self.finish(prefix, id_lists, rank, int(rank[-1].item()))

@@ -109,27 +109,38 @@ class BlockSampler:
         return blocks
 
     def _one_block(self, g, seeds, block_id, masks) -> Block:
-        rels = {}
-        src_lists: Dict[str, list] = {}
+        """One layer: counts of every relation, ONE size readback, fills; then the
+        new-source marks of every node type, ONE size readback, compaction/relabel."""
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        plan = []
         for r_idx, ce in enumerate(g.canonical_etypes):
-            s_t, _, d_t = ce
-            dseeds = seeds.get(d_t)
-            if dseeds is None:
-                dseeds = torch.zeros(0, dtype=torch.int64, device=g.device)
+            dseeds = seeds.get(ce[2], empty)
             indptr, indices, eids = g.in_csr_global(ce)
             key = _mix(self.seed, self._calls, block_id, r_idx)
             mask = masks.get(ce, (None,))[0]
-            o_ip, o_src, o_eid = ops.sample_neighbors(indptr, indices, eids, dseeds,
-                                                      self._fanout(block_id, ce), key, mask)
+            fan = self._fanout(block_id, ce)
+            o_ip = ops.sample_count(indptr, eids, dseeds, fan, key, mask)
+            plan.append((ce, indptr, indices, eids, dseeds, fan, key, mask, o_ip))
+        totals = torch.stack([p[-1][-1] for p in plan]).tolist() if plan else []
+        rels = {}
+        src_lists: Dict[str, list] = {}
+        for (ce, indptr, indices, eids, dseeds, fan, key, mask, o_ip), tot in zip(plan, totals):
+            o_src, o_eid = ops.sample_fill(indptr, indices, eids, dseeds, fan, key, o_ip, tot, mask)
             rels[ce] = [o_ip, o_src, o_eid]
-            src_lists.setdefault(s_t, []).append(ce)
-        src_nid, num_dst = {}, {}
+            src_lists.setdefault(ce[0], []).append(ce)
+        prefixes, ranks = {}, {}
         for nt in g.ntypes:
-            prefix = seeds.get(nt, torch.zeros(0, dtype=torch.int64, device=g.device))
-            num_dst[nt] = int(prefix.numel())
+            prefixes[nt] = seeds.get(nt, empty)
+            ranks[nt] = self._relabeler(g, nt).begin(
+                prefixes[nt], [rels[ce][1] for ce in src_lists.get(nt, [])])
+        n_new = torch.stack([ranks[nt][-1] for nt in g.ntypes]).tolist()
+        src_nid, num_dst = {}, {}
+        for nt, nn_ in zip(g.ntypes, n_new):
             ces = src_lists.get(nt, [])
-            nodes, locs = self._relabeler(g, nt).relabel(prefix, [rels[ce][1] for ce in ces])
+            nodes, locs = self._relabeler(g, nt).finish(prefixes[nt], [rels[ce][1] for ce in ces],
+                                                        ranks[nt], int(nn_))
             src_nid[nt] = nodes
+            num_dst[nt] = int(prefixes[nt].numel())
             for ce, loc in zip(ces, locs):
                 rels[ce][1] = loc.to(torch.int32)
         return Block(src_nid, num_dst, {ce: tuple(v) for ce, v in rels.items()})
@@ -180,6 +191,26 @@ def _batches(n: int, batch_size: int, shuffle: bool, drop_last: bool, device):
         yield order[i:i + batch_size]
 
 
+def _split_by_type(idx, flat_ids, type_starts, n_types):
+    """Batch positions -> per-type id slices, batch order kept within a type; one readback."""
+    ty = torch.bucketize(idx, type_starts[1:], right=True)
+    order = torch.argsort(ty, stable=True)
+    ids = flat_ids[idx[order]]
+    counts = torch.bincount(ty, minlength=n_types).tolist()
+    out, c = [], 0
+    for n in counts:
+        out.append(ids[c:c + n])
+        c += n
+    return out
+
+
+def _type_starts(ids, dev):
+    starts = [0]
+    for t in ids:
+        starts.append(starts[-1] + t.numel())
+    return torch.tensor(starts, dtype=torch.int64, device=dev)
+
+
 class NodeDataLoader:
     """Yields (input_nodes, output_nodes, blocks) for batches of seed nodes."""
 
@@ -194,8 +225,7 @@ class NodeDataLoader:
         self.types = list(nids.keys())
         ids = [torch.as_tensor(nids[nt], dtype=torch.int64).to(dev) for nt in self.types]
         self.flat_ids = torch.cat(ids) if ids else torch.zeros(0, dtype=torch.int64, device=dev)
-        self.flat_type = torch.cat([torch.full((t.numel(),), i, dtype=torch.int64, device=dev)
-                                    for i, t in enumerate(ids)]) if ids else self.flat_ids
+        self.type_starts = _type_starts(ids, dev)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
 
     def __len__(self):
@@ -205,9 +235,8 @@ class NodeDataLoader:
     def __iter__(self):
         for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
                             self.drop_last, self.g.device):
-            ids, ty = self.flat_ids[idx], self.flat_type[idx]
-            seeds = {nt: ids[ty == i] for i, nt in enumerate(self.types)}
-            seeds = {nt: v for nt, v in seeds.items() if v.numel() > 0}
+            parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
+            seeds = {nt: v for nt, v in zip(self.types, parts) if v.numel() > 0}
             blocks = self.sampler.sample_blocks(self.g, seeds)
             input_nodes = blocks[0].srcdata[NID]
             output_nodes = {nt: blocks[-1].dstdata[NID][nt] for nt in seeds}
@@ -239,8 +268,7 @@ class EdgeDataLoader:
         self.types = [g.to_canonical_etype(k) for k in eids]
         ids = [torch.as_tensor(eids[k], dtype=torch.int64).to(dev) for k in eids]
         self.flat_ids = torch.cat(ids)
-        self.flat_type = torch.cat([torch.full((t.numel(),), i, dtype=torch.int64, device=dev)
-                                    for i, t in enumerate(ids)])
+        self.type_starts = _type_starts(ids, dev)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
 
     def __len__(self):
@@ -258,10 +286,12 @@ class EdgeDataLoader:
                 per_type.setdefault(ce[0], []).append(s)
                 per_type.setdefault(ce[2], []).append(d)
         node_ids, local = {}, {}
-        for nt in g.ntypes:
-            lists = per_type.get(nt, [])
-            r = self.sampler._relabeler(g, nt)
-            nodes, locs = r.relabel(empty, lists)
+        ranks = [self.sampler._relabeler(g, nt).begin(empty, per_type.get(nt, []))
+                 for nt in g.ntypes]
+        n_new = torch.stack([r[-1] for r in ranks]).tolist()  # one readback for all types
+        for nt, rank, n in zip(g.ntypes, ranks, n_new):
+            nodes, locs = self.sampler._relabeler(g, nt).finish(empty, per_type.get(nt, []),
+                                                                rank, int(n))
             node_ids[nt] = nodes
             local[nt] = locs
         cursor = {nt: 0 for nt in g.ntypes}
@@ -285,9 +315,8 @@ class EdgeDataLoader:
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
         for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
                             self.drop_last, g.device):
-            ids, ty = self.flat_ids[idx], self.flat_type[idx]
-            batch = {ce: ids[ty == i] for i, ce in enumerate(self.types)}
-            batch = {ce: v for ce, v in batch.items() if v.numel() > 0}
+            parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
+            batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
             pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch else (empty, empty)
                          for ce in g.canonical_etypes}
             neg_edges = {}

@@ -29,6 +29,8 @@
  *   - gnnrec_sample_*          <- dgl.dataloading.MultiLayer{Full,}Neighbor-
  *                                 Sampler / to_block, src/sampling.py:153-161
  *                                 (_CAPI_DGLSampleNeighbors, _CAPI_DGLToBlock)
+ *   - gnnrec_gemm_tn_f32,      <- torch autograd of those layers in the
+ *     gnnrec_act_backward_f32     training step, src/train/run.py:124-138
  *   - gnnrec_synth_edges       <- (no reference counterpart: synthetic graph
  *                                 generator for the benchmark shapes)
  */
@@ -143,7 +145,7 @@ int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
 int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids, const uint8_t* excluded,
                         const int64_t* seeds, int64_t n_seeds, int64_t fanout,
                         uint64_t seed_key, int64_t* counts, void* stream);
-int gnnrec_sample_fill(const int64_t* indptr, const int64_t* indices, const int64_t* eids,
+int gnnrec_sample_fill(const int64_t* indptr, const int32_t* indices, const int64_t* eids,
                        const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
                        int64_t fanout, uint64_t seed_key, const int64_t* out_indptr,
                        int64_t* out_src, int64_t* out_eid, void* stream);
@@ -176,6 +178,25 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
 int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_rows, int64_t n_cols,
                          int64_t k, const int64_t* exclude_indptr, const int64_t* exclude_indices,
                          float* out_vals, int64_t* out_idx, void* stream);
+
+/* ---- f2: projection backward (training step) -----------------------------
+ * Replace torch autograd of the reference's nn.Linear layers and the
+ * relu/normalise epilogue when train_model calls loss.backward()
+ * (src/train/run.py:124-138; layers src/model.py:98-102,226-235,258-271).
+ *
+ * Weight gradient, C[M,N] (+)= A[K,M]^T B[K,N] (A = dY, B = X, K = rows):
+ * deterministic split-K fp32 MFMA.  workspace: gnnrec_gemm_tn_workspace_bytes(K,M,N)
+ * bytes of device memory (may be NULL when that is 0). */
+int64_t gnnrec_gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t N);
+int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K,
+                       int64_t M, int64_t N, float* C, int64_t ldc, int accumulate,
+                       float* workspace, void* stream);
+/* gu = d/du of z = norm?(relu?(u)) applied to gz, flags = GNNREC_EPI_RELU|GNNREC_EPI_L2NORM
+ * (norm: z = a / ||a||, rows with ||a|| == 0 unchanged — the zero-guarded norm of
+ * src/model.py:231-235).  u: the pre-activation rows [n_rows, d]. */
+int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_t ldg,
+                            int64_t n_rows, int64_t d, int flags, float* gu, int64_t ldo,
+                            void* stream);
 
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),

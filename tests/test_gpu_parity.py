@@ -269,6 +269,27 @@ def test_model_golden_full_graph_heads_loss(name):
 
 
 # ---------------------------------------------------------------- sampler ---
+@pytest.mark.parametrize("fanout", [-1, 10, 63, 64])
+@pytest.mark.parametrize("exclude", [False, True])
+def test_sampler_heavy_rows_bit_exact(fanout, exclude):
+    """rows of degree 0..700 (several 128-edge chunks per wave) and the maximum fanout."""
+    from gnnrec import ops
+    rng = np.random.default_rng(5)
+    n = 400
+    deg = rng.integers(0, 700, n)
+    deg[:5] = [0, 1, 63, 64, 65]
+    dst = np.repeat(np.arange(n), deg)
+    src = rng.integers(0, 5000, dst.size)
+    indptr, indices, eids = oracle.csr_from_coo(src, dst, n)
+    seeds = rng.permutation(n).astype(np.int64)
+    excl = (rng.random(dst.size) < 0.4).astype(np.uint8) if exclude else None
+    r = oracle.sample_neighbors(indptr, indices, eids, seeds, fanout, 99, excl)
+    g = ops.sample_neighbors(_t(indptr), _t(indices.astype(np.int32)), _t(eids), _t(seeds),
+                             fanout, 99, None if excl is None else _t(excl))
+    for a, b in zip(g, r):
+        np.testing.assert_array_equal(a.cpu().numpy(), b)
+
+
 @pytest.mark.parametrize("fanout", [-1, 1, 3, 10])
 @pytest.mark.parametrize("exclude", [False, True])
 def test_sampler_bit_exact_vs_oracle(fanout, exclude):
@@ -283,7 +304,7 @@ def test_sampler_bit_exact_vs_oracle(fanout, exclude):
     key = 12345
     r_ip, r_src, r_eid = oracle.sample_neighbors(indptr, indices.astype(np.int64), eids, seeds,
                                                  fanout, key, excl)
-    g_ip, g_src, g_eid = ops.sample_neighbors(_t(indptr), _t(indices.astype(np.int64)), _t(eids),
+    g_ip, g_src, g_eid = ops.sample_neighbors(_t(indptr), _t(indices.astype(np.int32)), _t(eids),
                                               _t(seeds), fanout, key,
                                               None if excl is None else _t(excl))
     np.testing.assert_array_equal(g_ip.cpu().numpy(), r_ip)
@@ -388,3 +409,67 @@ def test_spmm_backward_matches_reference(reduce, weighted):
                 else:
                     ref[idx[e], c] += g * (w[e] if w is not None else 1)
     np.testing.assert_allclose(gx, ref, rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------- f2 backward kernels ---
+@pytest.mark.parametrize("K,M,N", [(1, 1, 1), (37, 5, 7), (1000, 128, 128), (4099, 200, 96),
+                                   (70001, 128, 256), (0, 4, 3)])
+def test_gemm_tn_matches_fp64(K, M, N):
+    from gnnrec import ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(K + M + N)
+    A = torch.randn(K, M + 3, device="cuda", generator=gen)[:, :M]  # strided lda
+    B = torch.randn(K, N, device="cuda", generator=gen)
+    out = ops.gemm_tn(A, B)
+    ref = (A.double().t() @ B.double())
+    tol = 1e-5 * max(1.0, float(np.sqrt(K)))
+    np.testing.assert_allclose(out.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=tol)
+    C = torch.randn(M, N + 2, device="cuda", generator=gen)[:, :N]
+    C0 = C.clone()
+    ops.gemm_tn(A, B, out=C, accumulate=True)
+    np.testing.assert_allclose(C.cpu().numpy(), (C0.double() + ref).cpu().numpy(), rtol=1e-4,
+                               atol=tol)
+    # deterministic: same bits twice
+    assert torch.equal(ops.gemm_tn(A, B), out)
+
+
+@pytest.mark.parametrize("relu,l2", [(True, False), (False, True), (True, True)])
+def test_act_backward_matches_autograd(relu, l2):
+    from gnnrec import ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(3)
+    u = torch.randn(300, 130, device="cuda", generator=gen)
+    u[5] = -1.0  # relu kills the whole row -> zero norm row
+    u[6] = 0.0
+    gz = torch.randn(300, 130, device="cuda", generator=gen)
+    x = u.clone().requires_grad_(True)
+    z = torch.relu(x) if relu else x
+    if l2:
+        n = z.norm(2, 1, keepdim=True)
+        z = z / torch.where(n == 0, torch.ones_like(n), n)
+    (ref,) = torch.autograd.grad(z, x, gz)
+    got = ops.act_backward(u, gz, relu=relu, l2norm=l2)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_cosine_backward_matches_autograd():
+    import torch.nn.functional as F
+    from gnnrec.autograd import CosineFn
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(4)
+    hs = torch.randn(50, 64, device="cuda", generator=gen)
+    hd = torch.randn(300, 64, device="cuda", generator=gen)
+    hs[3] = 0.0  # zero row (eps branch)
+    src = torch.randint(0, 50, (3000,), device="cuda", generator=gen).repeat_interleave(3)
+    dst = torch.randint(0, 300, (9000,), device="cuda", generator=gen)
+    g = torch.randn(9000, device="cuda", generator=gen)
+    a, b = hs.clone().requires_grad_(True), hd.clone().requires_grad_(True)
+    (CosineFn.apply(a, b, src, dst).reshape(-1) * g).sum().backward()
+    a2, b2 = hs.clone().requires_grad_(True), hd.clone().requires_grad_(True)
+    ((F.normalize(a2, dim=-1)[src] * F.normalize(b2, dim=-1)[dst]).sum(-1) * g).sum().backward()
+    ga, ga_ref = a.grad.cpu().numpy(), a2.grad.cpu().numpy()
+    keep = np.arange(50) != 3
+    np.testing.assert_allclose(ga[keep], ga_ref[keep], rtol=1e-4, atol=1e-5)
+    # the zero row's gradient is a 1/eps-scaled sum of ~180 terms: summation order shows
+    np.testing.assert_allclose(ga[3], ga_ref[3], rtol=1e-3)
+    np.testing.assert_allclose(b.grad.cpu().numpy(), b2.grad.cpu().numpy(), rtol=1e-4, atol=1e-5)

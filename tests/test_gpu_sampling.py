@@ -187,7 +187,12 @@ def test_autograd_matches_torch_reference():
     h = model.embed(feats)
     for layer in model.layers:
         h = layer(g, h)
-    loss = sum((v ** 2).sum() * (i + 1) for i, v in enumerate(h.values()))
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(7)
+    R = {k: torch.randn(v.shape, generator=gen, device=DEV) for k, v in h.items()}
+    # a random linear read-out: (unlike sum(z**2)) its gradient is not orthogonal to the
+    # normalised rows, so the norm backward is exercised
+    loss = sum((v * R[k]).sum() * (i + 1) for i, (k, v) in enumerate(h.items()))
     grads = torch.autograd.grad(loss, list(model.parameters()) + list(feats.values()),
                                 allow_unused=True)
 
@@ -214,7 +219,7 @@ def test_autograd_matches_torch_reference():
             z = z / torch.where(n == 0, torch.ones_like(n), n)
             out.setdefault(ce[2], []).append(z)
         hh = {nt: torch.stack(v).sum(0) for nt, v in out.items()}
-    loss_ref = sum((v ** 2).sum() * (i + 1) for i, v in enumerate(hh[k] for k in h))
+    loss_ref = sum((hh[k] * R[k]).sum() * (i + 1) for i, k in enumerate(h))
     ref = torch.autograd.grad(loss_ref, list(model.parameters()) + list(x.values()),
                               allow_unused=True)
     np.testing.assert_allclose(loss.item(), loss_ref.item(), rtol=1e-5)

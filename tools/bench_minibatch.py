@@ -78,7 +78,7 @@ def main():
         "ms_per_batch": dt / args.batches * 1e3, "edges_per_batch": n_edges / args.batches}
     # CPU oracle sampler on the same CSR and the same seeds (one layer, single thread)
     from oracle import oracle
-    indptr, indices, eids = [t.cpu().numpy() for t in g.in_csr_global(BOUGHT)]
+    indptr, indices, eids = [t.cpu().numpy().astype(np.int64) for t in g.in_csr_global(BOUGHT)]
     seeds = np.random.default_rng(0).choice(1_000_000, 1024 * 8, replace=False).astype(np.int64)
     t = time.perf_counter()
     _, s_cpu, _ = oracle.sample_neighbors(indptr, indices, eids, seeds, 10, 7)
