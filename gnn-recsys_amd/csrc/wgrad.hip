@@ -13,82 +13,156 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTile = 128;       // output super-tile per block (M and N)
-constexpr int kKStep = 16;       // rows per unrolled step (8 MFMA k-pairs)
-constexpr int kTargetBlocks = 1024;
+constexpr int kKStep = 16;       // input rows per pipeline step (8 MFMA k-pairs)
+constexpr int kLdsStride = kTile + 4;
+constexpr int kTargetBlocks = 512;
 
-// Block: 4 waves; wave w owns output rows [32w, 32w+32) of the super-tile and all
-// four 32-column blocks.  MFMA 32x32x2 f32 operands: lane l supplies
-// A^T[i=l&31][k=l>>5] = A[k][i] and B[k=l>>5][j=l&31]; both are 32 consecutive
-// floats of one input row per half-wave (coalesced 128-B segments).
-__global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
-    int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int li = lane & 31, lk = lane >> 5;
-  const int64_t split = blockIdx.x;
-  const int64_t i0 = (int64_t)blockIdx.y * kTile + 32 * w;
-  const int64_t j0 = (int64_t)blockIdx.z * kTile;
-  const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
-
-  f32x16 acc[4];
-  for (int q = 0; q < 4; ++q)
-    for (int v = 0; v < 16; ++v) acc[q][v] = 0.f;
-
-  // clamped (always in-bounds) addresses, zeroed by select: branch-free loads
-  const bool ia_ok = i0 + li < M;
-  const int64_t ia = ia_ok ? i0 + li : 0;
-  bool jb_ok[4];
-  int64_t jb[4];
-  for (int q = 0; q < 4; ++q) {
-    jb_ok[q] = j0 + 32 * q + li < N;
-    jb[q] = jb_ok[q] ? j0 + 32 * q + li : 0;
-  }
-  if (kb < ke) {
-    for (int64_t k0 = kb; k0 < ke; k0 += kKStep) {
-      float a[kKStep / 2], b[kKStep / 2][4];
+// One 16-row step of a [K, ld] operand restricted to columns [c0, c0+128):
+// 512 float4 slots, two per thread (row = slot / 32, cols 4*(slot % 32) .. +3).
+// VEC: 16-B loads (ld % 4 == 0, 16-B aligned base, full columns checked per slot);
+// otherwise per-element loads.  Rows >= ke and columns >= ncol read as zero.
+template <bool VEC>
+__device__ inline void load_step(const float* __restrict__ X, int64_t ld, int64_t ncol,
+                                 int64_t c0, int64_t k0, int64_t ke, float4 (&r)[2]) {
 #pragma unroll
-      for (int s = 0; s < kKStep / 2; ++s) {
-        const int64_t k = k0 + 2 * s + lk;
-        const bool k_ok = k < ke;
-        const int64_t kc = k_ok ? k : ke - 1;
-        const float av = A[kc * lda + ia];
-        a[s] = (k_ok && ia_ok) ? av : 0.f;
+  for (int h = 0; h < 2; ++h) {
+    const int slot = threadIdx.x + 256 * h;
+    const int64_t k = k0 + (slot >> 5);
+    const int64_t c = c0 + 4 * (slot & 31);
+    const bool k_ok = k < ke;
+    const int64_t kc = k_ok ? k : ke - 1;
+    const float* row = X + kc * ld;
+    if (VEC) {
+      const bool c_ok = c < ncol;  // ncol % 4 == 0 on this path
+      const float4 v = *reinterpret_cast<const float4*>(row + (c_ok ? c : 0));
+      const bool ok = k_ok && c_ok;
+      r[h] = make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+    } else {
+      float e[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float bv = B[kc * ldb + jb[q]];
-          b[s][q] = (k_ok && jb_ok[q]) ? bv : 0.f;
-        }
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = k_ok && c + q < ncol;
+        const float v = row[ok ? c + q : 0];
+        e[q] = ok ? v : 0.f;
       }
-#pragma unroll
-      for (int s = 0; s < kKStep / 2; ++s)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s][q], acc[q], 0, 0, 0);
-    }
-  }
-  float* P = part + split * M * N;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t j = j0 + 32 * q + li;
-    if (j >= N) continue;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int64_t i = i0 + (v & 3) + 8 * (v >> 2) + 4 * lk;
-      if (i < M) P[i * N + j] = acc[q][v];
+      r[h] = make_float4(e[0], e[1], e[2], e[3]);
     }
   }
 }
 
-__global__ void gemm_tn_reduce_kernel(const float* __restrict__ part, int64_t splits, int64_t M,
-                                      int64_t N, float* __restrict__ C, int64_t ldc,
-                                      int accumulate) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= M * N) return;
+__device__ inline void store_step(float* lds, const float4 (&r)[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int slot = threadIdx.x + 256 * h;
+    *reinterpret_cast<float4*>(lds + (slot >> 5) * kLdsStride + 4 * (slot & 31)) = r[h];
+  }
+}
+
+// Block: 4 waves as 2x2 wave tiles of 64x64 (2x2 MFMA 32x32 tiles each) over a
+// 128x128 output super-tile; K slice [kb, ke) streamed through double-buffered LDS
+// with a register prefetch of the next 16-row step (one barrier per step).
+// MFMA 32x32x2 f32 operands: lane l supplies A^T[i=l&31][k=l>>5] = A[k][i] and
+// B[k=l>>5][j=l&31]; both are consecutive LDS words across the half-wave.
+template <bool VEC>
+__global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+    int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part) {
+  __shared__ float As[2][kKStep * kLdsStride];
+  __shared__ float Bs[2][kKStep * kLdsStride];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 31, lk = lane >> 5;
+  const int wi = (w & 1) * 64, wj = (w >> 1) * 64;
+  const int64_t split = blockIdx.x;
+  const int64_t i_base = (int64_t)blockIdx.y * kTile, j_base = (int64_t)blockIdx.z * kTile;
+  const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[x][y][v] = 0.f;
+
+  if (kb < ke) {  // uniform per block
+    float4 ra[2], rb[2];
+    load_step<VEC>(A, lda, M, i_base, kb, ke, ra);
+    load_step<VEC>(B, ldb, N, j_base, kb, ke, rb);
+    store_step(As[0], ra);
+    store_step(Bs[0], rb);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += kKStep) {
+      const bool more = k0 + kKStep < ke;
+      if (more) {
+        load_step<VEC>(A, lda, M, i_base, k0 + kKStep, ke, ra);
+        load_step<VEC>(B, ldb, N, j_base, k0 + kKStep, ke, rb);
+      }
+      const float* as = As[buf];
+      const float* bs = Bs[buf];
+#pragma unroll
+      for (int s = 0; s < kKStep / 2; ++s) {
+        const int kr = (2 * s + lk) * kLdsStride;
+        const float a0 = as[kr + wi + li], a1 = as[kr + wi + 32 + li];
+        const float b0 = bs[kr + wj + li], b1 = bs[kr + wj + 32 + li];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (more) {
+        store_step(As[buf ^ 1], ra);
+        store_step(Bs[buf ^ 1], rb);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  float* P = part + split * M * N;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int64_t j = j_base + wj + 32 * y + li;
+      if (j >= N) continue;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t i = i_base + wi + 32 * x + (v & 3) + 8 * (v >> 2) + 4 * lk;
+        if (i < M) P[i * N + j] = acc[x][y][v];
+      }
+    }
+}
+
+// C = (accumulate ? C : 0) + sum_p part[p]; 64 outputs per block, the 4 waves sum
+// interleaved quarters of the splits, combined in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
+    const float* __restrict__ part, int64_t splits, int64_t M, int64_t N, float* __restrict__ C,
+    int64_t ldc, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t mn = M * N;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int64_t p = 0; p < splits; ++p) s += part[p * M * N + t];
-  const int64_t i = t / N, j = t - i * N;
-  float* c = C + i * ldc + j;
-  *c = accumulate ? *c + s : s;
+  if (t < mn) {
+    int64_t p = w;
+    for (; p + 12 < splits; p += 16) {
+      const float x0 = part[p * mn + t], x1 = part[(p + 4) * mn + t];
+      const float x2 = part[(p + 8) * mn + t], x3 = part[(p + 12) * mn + t];
+      s += x0;
+      s += x1;
+      s += x2;
+      s += x3;
+    }
+    for (; p < splits; p += 4) s += part[p * mn + t];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && t < mn) {
+    const float tot = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const int64_t i = t / N, j = t - i * N;
+    float* c = C + i * ldc + j;
+    *c = accumulate ? *c + tot : tot;
+  }
 }
 
 inline int64_t tn_splits(int64_t K, int64_t M, int64_t N) {
@@ -171,10 +245,16 @@ extern "C" int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, i
   const int64_t splits = tn_splits(K, M, N), chunk = tn_chunk(K, splits);
   const dim3 grid((unsigned)splits, (unsigned)((M + kTile - 1) / kTile),
                   (unsigned)((N + kTile - 1) / kTile));
-  hipLaunchKernelGGL(gemm_tn_partial_kernel, grid, dim3(256), 0, s, A, lda, B, ldb, K, M, N,
-                     chunk, workspace);
+  const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 &&
+                   M % 4 == 0 && N % 4 == 0;
+  if (vec)
+    hipLaunchKernelGGL(gemm_tn_partial_kernel<true>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
+                       N, chunk, workspace);
+  else
+    hipLaunchKernelGGL(gemm_tn_partial_kernel<false>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
+                       N, chunk, workspace);
   const int64_t mn = M * N;
-  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((mn + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((mn + 63) / 64)), dim3(256), 0, s,
                      workspace, splits, M, N, C, ldc, accumulate);
   return check_launch("gnnrec_gemm_tn_f32");
 }
