@@ -55,6 +55,8 @@ SIGNATURES = {
     "gnnrec_scan_workspace_bytes": (_I64, [_I64]),
     "gnnrec_gemm_tn_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "gnnrec_gemm_tn_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _INT, _P, _P]),
+    "gnnrec_lstm_step_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P,
+                                    _I64, _P]),
     "gnnrec_act_backward_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _INT, _P, _I64, _P]),
     "gnnrec_exclusive_scan_i64": (_INT, [_P, _I64, _P, _P, _P]),
     "gnnrec_exclusive_scan_i32": (_INT, [_P, _I64, _P, _P, _P]),

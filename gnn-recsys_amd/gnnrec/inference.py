@@ -295,6 +295,15 @@ class ShardedFullGraphPass:
                 preagg, weighted, reduce = mod._plan_rel(ce)
                 rs = sh.rels[ce]
                 msg = self._message(mod, ce, h, preagg)
+                if reduce == 'lstm':
+                    if self.ex.ws > 1:
+                        raise NotImplementedError(
+                            "the LSTM reducer runs over each destination's whole in-edge "
+                            "sequence and does not split into per-rank partials: run the "
+                            "lstm aggregator with one rank")
+                    partials[ce] = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm'), None,
+                                    reduce)
+                    continue
                 with self._time('spmm'):
                     part = O.spmm(rs.indptr, rs.indices, msg, 'max' if reduce == 'max' else 'sum',
                                   edge_weight=rs.weights if weighted else None,
@@ -325,8 +334,9 @@ class ShardedFullGraphPass:
             rs = sh.rels[ce]
             msg = self._message(mod, ce, h, preagg)
             with self._time('spmm'):
-                a = O.spmm(rs.indptr, rs.indices, msg, reduce,
-                           edge_weight=rs.weights if weighted else None)
+                a = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm') if reduce == 'lstm' else
+                     O.spmm(rs.indptr, rs.indices, msg, reduce,
+                            edge_weight=rs.weights if weighted else None))
             if o is None:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
             acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
@@ -363,7 +373,8 @@ class ShardedFullGraphPass:
                 O.gemm(self_rows, mod.fc_self.weight, own, mod.fc_neigh.weight, relu=True,
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                        a2_deg=sh.rels[ce].deg_own,
-                       a2_mode=_lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG)
+                       a2_mode=(_lib.A2_NONE if reduce == 'lstm' else
+                                _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG))
             if self.ex.ws == 1:  # the owned rows ARE the table
                 out[T] = o
                 continue

@@ -6,8 +6,8 @@ as the reference:
 
   NodeEmbedding      src/model.py:10-24
   ConvLayer          src/model.py:27-237   (aggregators mean / mean_nn / pool_nn /
-                                            *_edge; lstm* construct but raise in
-                                            forward: out of this tier's scope)
+                                            lstm / *_edge; lstm_edge fails on the
+                                            missing self.lstm exactly as the reference)
   HeteroGraphConv    DGL 0.5.2 dgl.nn.pytorch.HeteroGraphConv as used at
                      src/model.py:384-406 (relation-skip rule, sum/mean/max)
   PredictingLayer    src/model.py:240-272
@@ -94,14 +94,15 @@ class ConvLayer(nn.Module):
         return self._plan_rel(graph.canonical_etypes[0])
 
     def _plan_rel(self, ce):
-        """(fc_preagg applies, edge weight applies, 'mean'|'max') — src/model.py:143-224."""
+        """(fc_preagg applies, edge weight applies, 'mean'|'max'|'lstm') — src/model.py:143-224."""
         agg = self._aggre_type
         if agg not in _KNOWN:
             raise KeyError('Aggregator type {} not recognized.'.format(agg))
         if agg.startswith('lstm'):
-            raise NotImplementedError(
-                "lstm/lstm_edge aggregators are outside the MI355X hot-path scope "
-                "(SURVEY.md §2 row 1, §8f row f4)")
+            # reference :164-169 / :210-221; self.lstm exists only for 'lstm' (:103-104),
+            # so 'lstm_edge' raises AttributeError here as it does in the reference
+            self.lstm  # noqa: B018
+            return False, False, 'lstm'
         weighted = agg.endswith('_edge') and ce[0] in USER_ITEM and ce[2] in USER_ITEM
         reduce = 'max' if agg.startswith('pool') else 'mean'
         return agg in _PREAGG, weighted, reduce
@@ -111,6 +112,14 @@ class ConvLayer(nn.Module):
         """graph.edata['occurrence'].float() in CSR order (src/model.py:174)."""
         w = graph.edata['occurrence']
         return w if w.dtype == torch.float32 else w.float()
+
+    def aggregate(self, indptr, indices, m, reduce: str, ew=None, **kw):
+        """Inference neighbourhood reduction over a CSR: gSpMM mean/max/sum or the LSTM."""
+        if reduce == 'lstm':
+            L = self.lstm
+            return ops.lstm_aggregate(indptr, indices, m, L.weight_ih_l0, L.weight_hh_l0,
+                                      L.bias_ih_l0, L.bias_hh_l0)
+        return ops.spmm(indptr, indices, m, reduce, edge_weight=ew, **kw)
 
     def forward(self, graph, x):
         """Reference ConvLayer.forward(graph, (h_neigh, h_self)) -> z [n_dst, out_feats]."""
@@ -126,12 +135,17 @@ class ConvLayer(nn.Module):
         if _grad_mode(h_neigh, h_self, module=self):
             m = ag.LinearFn.apply(h_neigh, self.fc_preagg.weight, None, True, False) \
                 if preagg else h_neigh
-            agg = ag.SpmmFn.apply(m, graph.indptr, graph.indices, ew, reduce, graph.n_dst)
+            if reduce == 'lstm':
+                L = self.lstm
+                agg = ag.LstmAggFn.apply(m, L.weight_ih_l0, L.weight_hh_l0, L.bias_ih_l0,
+                                         L.bias_hh_l0, graph.indptr, graph.indices)
+            else:
+                agg = ag.SpmmFn.apply(m, graph.indptr, graph.indices, ew, reduce, graph.n_dst)
             z = ag.SageProjectFn.apply(h_self, agg, self.fc_self.weight, self.fc_neigh.weight,
                                        bool(self.norm))
             return z if out is None else z  # caller combines relations in grad mode
         m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
-        agg = ops.spmm(graph.indptr, graph.indices, m, reduce, edge_weight=ew)
+        agg = self.aggregate(graph.indptr, graph.indices, m, reduce, ew)
         return ops.gemm(h_self, self.fc_self.weight, agg, self.fc_neigh.weight, relu=True,
                         l2norm=bool(self.norm), accum=accum, out_div=out_div, out=out)
 

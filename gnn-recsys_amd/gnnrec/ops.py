@@ -224,6 +224,61 @@ def act_backward(u: torch.Tensor, gz: torch.Tensor, relu: bool, l2norm: bool,
     return out
 
 
+class LstmPlan:
+    """Degree-descending visiting order of a CSR's rows and the running-row count of
+    every step (one host readback of the degree histogram, cached on the indptr)."""
+
+    def __init__(self, indptr: torch.Tensor):
+        deg = indptr[1:] - indptr[:-1]
+        self.order = torch.argsort(deg, descending=True, stable=True)
+        hist = torch.bincount(deg, minlength=1).tolist()
+        n = indptr.numel() - 1
+        running, steps = n - hist[0], []
+        for t in range(len(hist) - 1):
+            steps.append(running)
+            running -= hist[t + 1]
+        self.n_active = steps  # n_active[t] = #rows with in-degree > t
+        self.n_rows = steps[0] if steps else 0
+
+    @classmethod
+    def of(cls, indptr):
+        p = getattr(indptr, "_gnnrec_lstm_plan", None)
+        if p is None:
+            p = cls(indptr)
+            indptr._gnnrec_lstm_plan = p
+        return p
+
+
+def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """f4: per destination, nn.LSTM over its in-neighbour rows of X in CSR (edge) order ->
+    final hidden state [n_dst, d]; 0 for zero in-degree (ConvLayer._lstm_reducer)."""
+    lib = _lib.load()
+    _dev(indptr, "indptr", torch.int64)
+    _dev(indices, "indices", torch.int32)
+    d = W_hh.shape[1]
+    n_dst = indptr.numel() - 1
+    plan = LstmPlan.of(indptr)
+    P = gemm(X.contiguous(), W_ih.detach(), bias=(b_ih + b_hh).detach())  # [N_src, 4d]
+    if out is None:
+        out = torch.zeros((n_dst, d), dtype=torch.float32, device=X.device)
+    else:
+        out.zero_()
+    if plan.n_rows == 0:
+        return out
+    h = [torch.zeros((plan.n_rows, d), dtype=torch.float32, device=X.device),
+         torch.empty((plan.n_rows, d), dtype=torch.float32, device=X.device)]
+    c = torch.zeros((plan.n_rows, d), dtype=torch.float32, device=X.device)
+    WT = W_hh.detach().t().contiguous()
+    s = stream_ptr(X.device)
+    for t, n_act in enumerate(plan.n_active):
+        check(lib.gnnrec_lstm_step_f32(ptr(P), P.stride(0), ptr(indptr), ptr(indices),
+                                       ptr(plan.order), t, n_act, ptr(h[t % 2]),
+                                       ptr(h[(t + 1) % 2]), ptr(c), d, ptr(WT), ptr(out),
+                                       out.stride(0), s), "gnnrec_lstm_step_f32")
+    return out
+
+
 def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
               Hd: torch.Tensor) -> torch.Tensor:
     """a7: cosine of the L2-normalised endpoint rows, one value per edge -> [E]."""

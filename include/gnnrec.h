@@ -31,6 +31,7 @@
  *                                 (_CAPI_DGLSampleNeighbors, _CAPI_DGLToBlock)
  *   - gnnrec_gemm_tn_f32,      <- torch autograd of those layers in the
  *     gnnrec_act_backward_f32     training step, src/train/run.py:124-138
+ *   - gnnrec_lstm_step_f32     <- ConvLayer._lstm_reducer src/model.py:106-121
  *   - gnnrec_synth_edges       <- (no reference counterpart: synthetic graph
  *                                 generator for the benchmark shapes)
  */
@@ -197,6 +198,20 @@ int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
 int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_t ldg,
                             int64_t n_rows, int64_t d, int flags, float* gu, int64_t ldo,
                             void* stream);
+
+/* ---- f4: LSTM neighbourhood reducer (one recurrence step) ------------------
+ * Replaces ConvLayer._lstm_reducer (src/model.py:106-121, update_all at :164-169;
+ * DGL 0.5.2 degree bucketing, messages in edge order).  Destinations are visited in
+ * `order` (sorted by in-degree, descending); at step t the n_act rows order[0..n_act)
+ * all have in-degree > t.  For those rows:
+ *   gates = P[indices[indptr[v] + t]] + h_in W_hh^T     (P = X W_ih^T + b_ih + b_hh,
+ *                                                         [N_src, 4d], gate order i,f,g,o)
+ *   c = sig(f) c + sig(i) tanh(g);  h_out = sig(o) tanh(c);  out[v] = h_out at v's last step.
+ * h_in/h_out/c: [n_rows, d] dense, row p = order[p]; W_hhT: [d, 4d]; d <= 512. */
+int gnnrec_lstm_step_f32(const float* P, int64_t ldp, const int64_t* indptr,
+                         const int32_t* indices, const int64_t* order, int64_t t, int64_t n_act,
+                         const float* h_in, float* h_out, float* c, int64_t d,
+                         const float* W_hhT, float* out, int64_t ldo, void* stream);
 
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),

@@ -126,6 +126,38 @@ def relu(x):
     return np.maximum(x, np.float32(0))
 
 
+def _sigmoid(x):
+    return (np.float32(1) / (np.float32(1) + np.exp(-x))).astype(np.float32)
+
+
+def lstm_reduce(indptr, indices, X, W_ih, W_hh, b_ih, b_hh) -> np.ndarray:
+    """ConvLayer._lstm_reducer (src/model.py:106-121) under DGL 0.5.2 degree bucketing:
+    per destination, torch nn.LSTM (one layer, batch_first, h0 = c0 = 0, gate order
+    i, f, g, o) over its in-neighbour messages in edge order; the output is the final
+    hidden state.  Zero-in-degree destinations are not reduced and receive 0."""
+    X = np.asarray(X, np.float32)
+    d = W_hh.shape[1]
+    n_dst = indptr.size - 1
+    deg = np.diff(indptr)
+    out = np.zeros((n_dst, d), np.float32)
+    rows = np.nonzero(deg > 0)[0]
+    if rows.size == 0:
+        return out
+    P = linear(X, W_ih, np.asarray(b_ih, np.float32) + np.asarray(b_hh, np.float32))
+    h = np.zeros((rows.size, d), np.float32)
+    c = np.zeros((rows.size, d), np.float32)
+    for t in range(int(deg[rows].max())):
+        act = deg[rows] > t
+        src = indices[indptr[rows[act]] + t]
+        gates = P[src] + h[act] @ np.asarray(W_hh, np.float32).T
+        i, f = _sigmoid(gates[:, :d]), _sigmoid(gates[:, d:2 * d])
+        g, o = np.tanh(gates[:, 2 * d:3 * d]), _sigmoid(gates[:, 3 * d:])
+        c[act] = f * c[act] + i * g
+        h[act] = o * np.tanh(c[act])
+    out[rows] = h
+    return out
+
+
 def linear(x, W, b=None):
     y = np.asarray(x, np.float32) @ np.asarray(W, np.float32).T
     if b is not None:
@@ -147,8 +179,16 @@ def conv_layer(graph: Graph, ce, h_neigh, h_self, w: dict, aggregator_type: str,
     agg = aggregator_type
     if agg not in CONV_AGGREGATORS:
         raise KeyError("Aggregator type {} not recognized.".format(agg))
-    if agg.startswith("lstm"):
-        raise NotImplementedError("lstm aggregators are out of scope (SURVEY.md §2 row 1)")
+    if agg == "lstm_edge":
+        # the reference builds self.lstm only for 'lstm' (src/model.py:103-104), so its
+        # lstm_edge branch (:210-221) fails on the attribute lookup
+        raise AttributeError("'ConvLayer' object has no attribute 'lstm'")
+    if agg == "lstm":  # :164-169 -> _lstm_reducer :106-121
+        indptr, indices, _ = graph.csr(ce)
+        h_n = lstm_reduce(indptr, indices, h_neigh, w["lstm.weight_ih_l0"], w["lstm.weight_hh_l0"],
+                          w["lstm.bias_ih_l0"], w["lstm.bias_hh_l0"])
+        z = relu(linear(h_self, w["fc_self.weight"]) + linear(h_n, w["fc_neigh.weight"]))
+        return l2_normalize_rows_guarded(z) if norm else z
     if agg in ("mean_nn", "pool_nn", "mean_nn_edge", "pool_nn_edge"):
         m = relu(linear(h_neigh, w["fc_preagg.weight"]))  # :151,158,185,198
     else:

@@ -9,6 +9,10 @@ restates from DGL 0.5.2 (unpinned by any reference test — see DESIGN.md):
   * builtin message/reduce functions fn.copy_src / fn.u_mul_e / fn.u_dot_v and
     fn.mean / fn.max: zero-in-degree destinations receive 0, mean divides the
     sum by the in-degree;
+  * user-defined reduce functions (ConvLayer._lstm_reducer): degree bucketing —
+    destinations with the same in-degree D are reduced together on a mailbox
+    [n, D, ...] whose messages are in edge-id order; zero-in-degree
+    destinations are not reduced and receive 0 (the zero frame initialiser);
   * HeteroGraphConv(mods, aggregate): per canonical etype, skip relations with
     no edges or whose src/dst type has no input; stack the outputs of the
     active relations per dst type and reduce with sum / mean / max
@@ -97,6 +101,25 @@ class RelGraph:
             raise NotImplementedError(msg.kind)
         n_dst = self.parent.num_nodes(d)
         out = torch.zeros((n_dst,) + tuple(m.shape[1:]), dtype=m.dtype)
+        if callable(red) and not isinstance(red, _Red):
+            deg = torch.bincount(dst, minlength=n_dst)
+            order = torch.argsort(dst, stable=True)  # per destination: edge-id order
+            start = torch.zeros(n_dst + 1, dtype=torch.int64)
+            torch.cumsum(deg, 0, out=start[1:])
+            key = None
+            for D in sorted(set(deg.tolist()) - {0}):
+                nodes = torch.nonzero(deg == D).flatten()
+                eids = order[start[nodes].view(-1, 1) + torch.arange(D).view(1, -1)]
+                mailbox = types.SimpleNamespace(mailbox={"m": m[eids]})
+                res = red(mailbox)
+                key = next(iter(res))
+                out = out.to(res[key].dtype)
+                out[nodes] = res[key]
+            if key is not None:
+                self.dstdata[key] = out
+            else:
+                self.dstdata["neigh"] = out
+            return
         if red.kind in ("sum", "mean"):
             out.index_add_(0, dst, m)
             if red.kind == "mean":

@@ -25,6 +25,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REF = os.environ.get("GNNREC_REFERENCE", "/root/reference")
 
 USER_ITEM = ("user", "item")
+ONLY: list = []  # name filters from the command line (empty: write every case)
+
+
+def _write(name, arrs):
+    if not ONLY or any(o in name for o in ONLY):
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
 
 
 def load_reference_model():
@@ -98,7 +104,8 @@ def gen_convlayer_cases(ref, dgl_shim, manifest):
     feats = {nt: rng.standard_normal((n, dims[nt])).astype(np.float32) for nt, n in num_nodes.items()}
     for ce in (("user", "buys", "item"), ("item", "bought-by", "user"),
                ("user", "practices", "sport")):
-        for agg in ("mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge"):
+        for agg in ("mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge",
+                    "lstm"):
             for norm in (True, False):
                 torch.manual_seed(7)
                 layer = ref.ConvLayer((dims[ce[0]], dims[ce[2]]), 12, 0.0, agg, norm)
@@ -110,7 +117,7 @@ def gen_convlayer_cases(ref, dgl_shim, manifest):
                 for k, v in layer.state_dict().items():
                     arrs[f"w/{k}"] = v.numpy()
                 save_graph(arrs, edges, occ, num_nodes)
-                np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+                _write(name, arrs)
                 manifest[name] = {"kind": "convlayer", "etype": list(ce), "aggregator_type": agg,
                                   "norm": norm, "out_feats": 12}
 
@@ -125,6 +132,8 @@ def gen_model_cases(ref, dgl_shim, manifest):
         ("model_het_pooledge_sum_noemb_nn", "het", "pool_nn_edge", "sum", False, 2, "nn", False),
         ("model_het_meanedge_max_emb", "het", "mean_edge", "max", True, 2, "cos", True),
         ("model_het_mean_sum_skip", "het_skip", "mean", "sum", False, 3, "cos", True),
+        ("model_bip_lstm_sum_emb", "bip", "lstm", "sum", True, 3, "cos", True),
+        ("model_het_lstm_mean_noemb_nn", "het", "lstm", "mean", False, 2, "nn", True),
     ]
     for case_no, (name, kind, agg, hagg, emb, n_layers, pred, norm) in enumerate(cases):
         rng = np.random.default_rng(1234 + case_no)
@@ -190,7 +199,7 @@ def gen_model_cases(ref, dgl_shim, manifest):
         for ce, v in mask.items():
             arrs[f"mask/{etype_key(ce)}"] = v.numpy()
         arrs["loss"] = np.array(loss.item(), np.float32)
-        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        _write(name, arrs)
         manifest[name] = {"kind": "model", "aggregator_type": agg, "aggregator_hetero": hagg,
                           "embedding_layer": emb, "n_layers": n_layers, "pred": pred,
                           "norm": norm, "dim_dict": dim_dict, "neg_sample_size": K,
@@ -250,20 +259,30 @@ def gen_metrics_cases(ref, manifest):
                 "metrics": np.array([prec, rec, cov], np.float64)}
         for kk, v in model.pred_fn.layer_nn.state_dict().items():
             arrs[f"w/{kk}"] = v.numpy()
-        np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrs)
+        _write(name, arrs)
         manifest[name] = {"kind": "recs", "pred": pred, "use_popularity": pop,
                           "weight_popularity": 0.5, "k": k, "embed_dim": d}
 
 
 def main():
+    """python make_golden.py [substring ...]: regenerate every case, or only the cases whose
+    name contains one of the substrings (the others keep their files and manifest entries)."""
     if not os.path.exists(os.path.join(REF, "src", "model.py")):
         print(f"reference not found at {REF}: skipping golden generation")
         return 0
     ref, dgl_shim = load_reference_model()
+    only = sys.argv[1:]
+    ONLY[:] = only
     manifest = {}
     gen_convlayer_cases(ref, dgl_shim, manifest)
     gen_model_cases(ref, dgl_shim, manifest)
     gen_metrics_cases(ref, manifest)
+    if only:
+        # cases outside the filter keep their files and manifest entries
+        old = json.load(open(os.path.join(HERE, "MANIFEST.json")))["cases"]
+        for name in list(manifest):
+            if not any(o in name for o in only):
+                manifest[name] = old.get(name, manifest[name])
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference_files": ["src/model.py", "src/metrics.py"],

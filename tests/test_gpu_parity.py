@@ -473,3 +473,73 @@ def test_cosine_backward_matches_autograd():
     # the zero row's gradient is a 1/eps-scaled sum of ~180 terms: summation order shows
     np.testing.assert_allclose(ga[3], ga_ref[3], rtol=1e-3)
     np.testing.assert_allclose(b.grad.cpu().numpy(), b2.grad.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------ f4 LSTM reducer ---
+@pytest.mark.parametrize("d", [5, 64, 128, 200])
+def test_lstm_aggregate_matches_oracle(d):
+    from gnnrec import ops
+    rng = np.random.default_rng(d)
+    n_dst, n_src = 300, 250
+    deg = rng.integers(0, 40, n_dst)
+    deg[:3] = [0, 1, 150]
+    dst = np.repeat(np.arange(n_dst), deg)
+    src = rng.integers(0, n_src, dst.size)
+    perm = rng.permutation(dst.size)  # edge ids not grouped by destination
+    src, dst = src[perm], dst[perm]
+    indptr, indices, _ = oracle.csr_from_coo(src, dst, n_dst)
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    s = 1.0 / np.sqrt(d)
+    W_ih, W_hh = [rng.uniform(-s, s, (4 * d, d)).astype(np.float32) for _ in range(2)]
+    b_ih, b_hh = [rng.uniform(-s, s, 4 * d).astype(np.float32) for _ in range(2)]
+    ref = oracle.lstm_reduce(indptr, indices, X, W_ih, W_hh, b_ih, b_hh)
+    got = ops.lstm_aggregate(_t(indptr), _t(indices.astype(np.int32)), _t(X), _t(W_ih), _t(W_hh),
+                             _t(b_ih), _t(b_hh))
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-4, atol=2e-5)
+    assert not got[0].any()  # zero in-degree -> 0
+
+
+def test_lstm_layer_matches_torch_lstm_and_trains():
+    """ConvLayer('lstm') forward and gradients vs the reference mechanics in torch:
+    degree buckets, each run through the layer's own nn.LSTM (src/model.py:106-121)."""
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.nn import ConvLayer
+    torch.manual_seed(0)
+    rng = np.random.default_rng(8)
+    n_u, n_i, E = 60, 40, 500
+    u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+    ce = ("user", "buys", "item")
+    g = HeteroGraph({ce: (torch.from_numpy(u), torch.from_numpy(i))}, {"user": n_u, "item": n_i},
+                    device=DEV)
+    layer = ConvLayer((16, 12), 24, 0.0, "lstm", True).to(DEV).train()
+    xu = torch.randn(n_u, 16, device=DEV, requires_grad=True)
+    xi = torch.randn(n_i, 12, device=DEV, requires_grad=True)
+    R = torch.randn(n_i, 24, device=DEV)
+    z = layer(g.rel_graph(ce), (xu, xi))
+    params = list(layer.parameters())
+    grads = torch.autograd.grad((z * R).sum(), params + [xu, xi])
+
+    # torch restatement: degree bucketing with the layer's own nn.LSTM
+    ut, it = torch.from_numpy(u).to(DEV), torch.from_numpy(i).to(DEV)
+    order = torch.argsort(it, stable=True)
+    deg = torch.bincount(it, minlength=n_i)
+    start = torch.zeros(n_i + 1, dtype=torch.int64, device=DEV)
+    start[1:] = torch.cumsum(deg, 0)
+    neigh = torch.zeros(n_i, 16, device=DEV)
+    for D in sorted(set(deg.tolist()) - {0}):
+        nodes = torch.nonzero(deg == D).flatten()
+        eids = order[start[nodes].view(-1, 1) + torch.arange(D, device=DEV).view(1, -1)]
+        m = xu[ut[eids]]
+        h0 = m.new_zeros((1, nodes.numel(), 16))
+        _, (rst, _) = layer.lstm(m, (h0, h0))
+        neigh = neigh.index_put((nodes,), rst.squeeze(0))
+    zr = torch.relu(xi @ layer.fc_self.weight.t() + neigh @ layer.fc_neigh.weight.t())
+    n = zr.norm(2, 1, keepdim=True)
+    zr = zr / torch.where(n == 0, torch.ones_like(n), n)
+    np.testing.assert_allclose(z.detach().cpu().numpy(), zr.detach().cpu().numpy(), rtol=1e-4,
+                               atol=1e-5)
+    ref = torch.autograd.grad((zr * R).sum(), params + [xu, xi])
+    names = [n for n, _ in layer.named_parameters()] + ["xu", "xi"]
+    for name, a, b in zip(names, grads, ref):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=2e-4, atol=2e-5,
+                                   err_msg=name)

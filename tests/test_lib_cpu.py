@@ -83,3 +83,24 @@ def test_modules_keep_reference_state_dict_layout():
     assert "pred_fn.layer_nn.hidden_1.weight" in keys and "pred_fn.layer_nn.output.bias" in keys
     with pytest.raises(KeyError):
         gnn.ConvModel(meta, 2, {"user": 4, "item": 6, "hidden": 16, "out": 8}, pred="dot")
+
+
+def test_lstm_aggregators_follow_the_reference():
+    """'lstm' builds an nn.LSTM with the reference's state_dict keys; 'lstm_edge' never
+    builds one (src/model.py:103-104) and fails on the attribute in forward, as the
+    reference does; LSTM step validation runs before any launch."""
+    from gnnrec import _lib
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    layer = gnn.ConvLayer((6, 5), 8, 0.0, "lstm", True)
+    assert {"lstm.weight_ih_l0", "lstm.weight_hh_l0", "lstm.bias_ih_l0",
+            "lstm.bias_hh_l0"} <= set(layer.state_dict())
+    g = HeteroGraph({("user", "buys", "item"): (torch.tensor([0, 1]), torch.tensor([1, 0]))},
+                    {"user": 2, "item": 2})
+    with pytest.raises(AttributeError, match="lstm"):
+        gnn.ConvLayer((6, 5), 8, 0.0, "lstm_edge", True)(
+            g.rel_graph(("user", "buys", "item")), (torch.zeros(2, 6), torch.zeros(2, 5)))
+    lib = _lib.load()
+    rc = lib.gnnrec_lstm_step_f32(None, 4, None, None, None, 0, 1, None, None, None, 1000, None,
+                                  None, 1000, None)
+    assert rc != 0 and b"hidden size" in lib.gnnrec_last_error()

@@ -19,7 +19,8 @@ MODEL = sorted(k for k, v in CASES.items() if v["kind"] == "model")
 
 def test_manifest_covers_every_aggregator_and_hetero_mode():
     aggs = {CASES[k]["aggregator_type"] for k in CONV}
-    assert aggs == {"mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge"}
+    assert aggs == {"mean", "mean_nn", "pool_nn", "mean_edge", "mean_nn_edge", "pool_nn_edge",
+                    "lstm"}
     assert {CASES[k]["aggregator_hetero"] for k in MODEL} == {"sum", "mean", "max"}
     assert {CASES[k]["pred"] for k in MODEL} == {"cos", "nn"}
 
@@ -89,3 +90,14 @@ def test_unknown_aggregator_raises_keyerror():
     with pytest.raises(KeyError):
         oracle.conv_layer(g, ("user", "buys", "item"), np.zeros((2, 2), np.float32),
                           np.zeros((2, 2), np.float32), w, "median", True)
+
+
+def test_lstm_edge_fails_like_the_reference():
+    """reference ConvLayer builds self.lstm only for 'lstm' (src/model.py:103-104): its
+    'lstm_edge' forward fails on the missing attribute."""
+    a = golden_io.load(CONV[0])
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = oracle.Graph(num_nodes, edges, occ)
+    with pytest.raises(AttributeError):
+        oracle.conv_layer(g, ("user", "buys", "item"), a["x_neigh"], a["x_self"], {},
+                          "lstm_edge", True)
