@@ -105,6 +105,23 @@ def main():
     res["C2 full-neighbour 2-layer blocks, batch 128"] = {
         "ms_per_batch": dt / 5 * 1e3, "edges_per_batch": n_edges / 5,
         "sampled_edges_per_s": n_edges / dt}
+    # ---- f4: LSTM reducer on a fanout-10 block (C2 shape: 10k seeds x 10, d=64) -----------
+    from gnnrec.graph import build_csr
+    for n_dst, fan, d in ((10_240, 10, 64), (100_000, 10, 128)):
+        dst = torch.arange(n_dst, device=dev).repeat_interleave(fan)
+        src = torch.randint(0, 1_000_000, (dst.numel(),), device=dev)
+        ip, ix, _ = build_csr(src, dst, n_dst)
+        X = torch.randn(1_000_000, d, device=dev)
+        W_ih, W_hh = torch.randn(4 * d, d, device=dev) * 0.1, torch.randn(4 * d, d, device=dev) * 0.1
+        b = torch.zeros(4 * d, device=dev)
+        ops.lstm_aggregate(ip, ix, X, W_ih, W_hh, b, b)
+        tl, _ = sync_time(lambda: [ops.lstm_aggregate(ip, ix, X, W_ih, W_hh, b, b)
+                                   for _ in range(5)])
+        tl /= 5
+        fl = 2.0 * dst.numel() * d * 4 * d + 2.0 * X.shape[0] * d * 4 * d
+        res[f"LSTM reducer {n_dst} dst x {fan} steps, d={d} (incl. input-projection GEMM)"] = {
+            "ms": tl * 1e3, "TFLOPs": fl / tl / 1e12}
+        del X
     del g, loader, fl, it, blocks
     torch.cuda.empty_cache()
 
