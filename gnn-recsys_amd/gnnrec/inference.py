@@ -209,17 +209,20 @@ class ShardedFullGraphPass:
         self.ex = exchange if exchange is not None else Exchange()
         self.ops = ops_backend if ops_backend is not None else ops
         self.overlap = overlap
-        self._pending = {}   # nt -> RCCL work producing h[nt]
-        self._ready = {}     # nt -> event on the side stream producing h[nt]
+        # keyed by the id of the tensor being produced (a layer's input and output tables
+        # of one node type are alive together; keying by ntype would make a consumer of
+        # the input wait for the producer of the output)
+        self._pending = {}   # id(table) -> RCCL work producing it
+        self._ready = {}     # id(table) -> event on the side stream producing it
         self.side = (torch.cuda.Stream(device=shard.device)
                      if overlap and shard.device.type == 'cuda' else None)
         self.timers = None  # optional callable(tag) -> context manager (bench)
 
     def _get(self, h, nt):
-        w = self._pending.pop(nt, None)
+        w = self._pending.pop(id(h[nt]), None)
         if w is not None:
             w.wait()
-        ev = self._ready.pop(nt, None)
+        ev = self._ready.pop(id(h[nt]), None)
         if ev is not None:
             torch.cuda.current_stream(self.shard.device).wait_event(ev)
         return h[nt]
@@ -259,7 +262,7 @@ class ShardedFullGraphPass:
                 W, b, x = mod.proj_feats.weight, mod.proj_feats.bias, h[nt]
                 if nt == sh.ptype and self.side is not None:
                     y = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float32, device=x.device)
-                    self._ready[nt] = self._on_side(
+                    self._ready[id(y)] = self._on_side(
                         lambda: O.gemm(x, W, bias=b, out=y), x, y)
                     h[nt] = y
                 else:
@@ -348,7 +351,7 @@ class ShardedFullGraphPass:
             ev = self._on_side(proj, self_rows, a, o)
         out[T] = o
         if ev is not None:
-            self._ready[T] = ev
+            self._ready[id(o)] = ev
 
     def _owned(self, hconv, h, active, partials, out):
         """owners project their replicated rows, then all-gather the table."""
@@ -382,7 +385,7 @@ class ShardedFullGraphPass:
                                 device=o.device)
             table, work = self.ex.all_gather_rows(o, table, async_op=self.overlap)
             if work is not None:
-                self._pending[T] = work
+                self._pending[id(table)] = work
             out[T] = table
 
     def _layer(self, hconv, h):
