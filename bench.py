@@ -84,13 +84,14 @@ class EventTimers:
         return sum(s.elapsed_time(e) for s, e in ev) / len(ev), len(ev)
 
 
-def spmm_algorithmic_bytes(shard, d):
+def spmm_algorithmic_bytes(shard, d, fused=()):
     """Per-pass algorithmic bytes of the gather+aggregate launches:
-    per edge d*4 (fp32 source row) + 4 (int32 index); per dst row 8 (int64 indptr) + d*4 (write)."""
+    per edge d*4 (fp32 source row) + 4 (int32 index); per dst row 8 (int64 indptr) + d*4
+    (write), + d*4 for the h_self row when the projection is fused into the launch."""
     tot = 0
     n = 0
-    for rs in shard.rels.values():
-        tot += rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + d * 4)
+    for ce, rs in shard.rels.items():
+        tot += rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + d * 4 * (2 if ce in fused else 1))
         n += 1
     return tot, n
 
@@ -109,7 +110,7 @@ def pmc_traffic(args, world):
     tot, n = 0.0, 0
     for path, scale in ((f, 2.0), (w, 1.0)):
         for r in csv.DictReader(open(path)):
-            if "spmm" in r["Kernel_Name"]:
+            if "spmm_csr_kernel" in r["Kernel_Name"] or "spmm_project_kernel" in r["Kernel_Name"]:
                 tot += float(r["Counter_Value"]) * 1024 * scale
                 n += scale == 2.0
     return tot / n if n else None
@@ -219,7 +220,7 @@ def main():
     value = edges_per_step * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
     spmm_ms, n_launch = timers.mean_ms("spmm")
-    bytes_pass, n_rel = spmm_algorithmic_bytes(shard, d)
+    bytes_pass, n_rel = spmm_algorithmic_bytes(shard, d, runner.fused)
     bytes_per_launch = bytes_pass / n_rel  # each relation launched once per layer
     achieved = bytes_per_launch / (spmm_ms * 1e-3) / 1e9 if spmm_ms == spmm_ms else None
 
@@ -253,7 +254,12 @@ def main():
                          "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": pmc_traffic(args, world),
-                         "kernel": "gnnrec spmm_csr_kernel (gather + segmented mean)",
+                         "kernel": ("gnnrec spmm_project_kernel (gather + segmented mean + "
+                                    "fused SAGE projection, ReLU, L2 norm)"
+                                    if len(runner.fused) == n_rel else
+                                    "gnnrec spmm_csr_kernel / spmm_project_kernel (gather + "
+                                    f"segmented mean; {len(runner.fused)}/{n_rel} relations "
+                                    "with the projection fused)"),
                          "bytes_per_launch": bytes_per_launch, "launch_ms": spmm_ms,
                          "launches_timed": n_launch},
             "cpu_baseline": cpu,

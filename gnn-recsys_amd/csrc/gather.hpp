@@ -1,0 +1,110 @@
+// Shared device helpers of the neighbour gather (a1): used by the plain
+// aggregation kernels (spmm.hip) and the fused aggregate+project kernel
+// (spmm_project.hip), so both reduce every row in the same fixed order.
+#pragma once
+#include "common.hpp"
+#include <cmath>
+
+namespace gnnrec {
+namespace {
+
+template <int VEC>
+struct Frag {
+  float v[VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ void load_frag(Frag<VEC>& f, const float* p) {
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    f.v[0] = t.x; f.v[1] = t.y; f.v[2] = t.z; f.v[3] = t.w;
+  } else {
+    f.v[0] = *p;
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
+  } else {
+    *p = f.v[0];
+  }
+}
+
+template <int REDUCE>
+__device__ __forceinline__ float combine(float a, float b) {
+  return REDUCE == GNNREC_REDUCE_MAX ? fmaxf(a, b) : a + b;
+}
+
+// Per-lane partial reduction of edges [beg, end) (lane group grp takes k % NPI == grp).
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
+__device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
+                                             const int32_t* __restrict__ indices,
+                                             const float* __restrict__ ew,
+                                             const float* __restrict__ X, int64_t ldx, int col,
+                                             bool colok, int lane, int grp, Frag<VEC>& acc) {
+  constexpr int NPI = kWave / LPR;
+  for (int64_t base = beg; base < end; base += 64) {
+    const int cnt = (int)((end - base) < 64 ? (end - base) : 64);
+    const int myidx = lane < cnt ? indices[base + lane] : 0;
+    float myw = 0.f;
+    if constexpr (WEIGHTED) myw = lane < cnt ? ew[base + lane] : 0.f;
+    for (int j = 0; j < cnt; j += NPI * UNROLL) {
+      Frag<VEC> val[UNROLL];
+      bool ok[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int k = j + u * NPI + grp;
+        ok[u] = (k < cnt) && colok;
+        const int src = __shfl(myidx, k & 63);
+        if (ok[u]) {
+          load_frag<VEC>(val[u], X + (int64_t)src * ldx + col);
+        } else {
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        float w = 1.f;
+        if constexpr (WEIGHTED) w = __shfl(myw, (j + u * NPI + grp) & 63);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const float m = WEIGHTED ? val[u].v[v] * w : val[u].v[v];
+          if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+            if (ok[u]) acc.v[v] = fmaxf(acc.v[v], m);
+          } else {
+            acc.v[v] += m;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int LPR, int VEC, int REDUCE>
+__device__ __forceinline__ void combine_groups(Frag<VEC>& acc) {
+#pragma unroll
+  for (int off = LPR; off < kWave; off <<= 1) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(acc.v[v], __shfl_xor(acc.v[v], off));
+  }
+}
+
+template <int VEC, int REDUCE>
+__device__ __forceinline__ void finalize(Frag<VEC>& acc, int64_t deg, int empty_neginf) {
+  if constexpr (REDUCE == GNNREC_REDUCE_MEAN) {
+    const float dd = (float)(deg > 0 ? deg : 1);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) acc.v[v] = acc.v[v] / dd;
+  } else if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+    if (deg == 0 && !empty_neginf) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace gnnrec

@@ -217,6 +217,7 @@ class ShardedFullGraphPass:
         self.side = (torch.cuda.Stream(device=shard.device)
                      if overlap and shard.device.type == 'cuda' else None)
         self.timers = None  # optional callable(tag) -> context manager (bench)
+        self.fused = set()  # relations whose aggregation ran with the projection fused
 
     def _get(self, h, nt):
         w = self._pending.pop(id(h[nt]), None)
@@ -298,6 +299,14 @@ class ShardedFullGraphPass:
                 preagg, weighted, reduce = mod._plan_rel(ce)
                 rs = sh.rels[ce]
                 msg = self._message(mod, ce, h, preagg)
+                can_fuse = getattr(O, 'can_spmm_project', None)
+                if self.ex.ws == 1 and reduce != 'lstm' and can_fuse is not None:
+                    self_rows = self._get(h, T)
+                    if can_fuse(rs.indptr, msg, self_rows, mod.fc_self.weight,
+                                mod.fc_neigh.weight):
+                        # one rank: no partials to exchange, aggregate + project in _owned
+                        partials[ce] = ('fused', msg, reduce, weighted)
+                        continue
                 if reduce == 'lstm':
                     if self.ex.ws > 1:
                         raise NotImplementedError(
@@ -331,19 +340,38 @@ class ShardedFullGraphPass:
         self_rows = h[T] if self.side is not None else self._get(h, T)
         o = None
         ev = None
+        can_fuse = getattr(O, 'can_spmm_project', None)
         for j, ce in enumerate(ces):
             mod = hconv.mods[ce[1]]
             preagg, weighted, reduce = mod._plan_rel(ce)
             rs = sh.rels[ce]
             msg = self._message(mod, ce, h, preagg)
+            acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
+            div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+            if reduce != 'lstm' and can_fuse is not None and can_fuse(
+                    rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight):
+                # aggregation and projection in one launch on the main stream: the self rows
+                # must be ready here (they may come from the side stream)
+                self_rows = self._get(h, T)
+                if ev is not None:  # an earlier relation's projection ran on the side stream
+                    torch.cuda.current_stream(self.shard.device).wait_event(ev)
+                    ev = None
+                if o is None:
+                    o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
+                                    device=msg.device)
+                with self._time('spmm'):
+                    O.spmm_project(rs.indptr, rs.indices, msg, self_rows, mod.fc_self.weight,
+                                   mod.fc_neigh.weight, reduce,
+                                   rs.weights if weighted else None, relu=True,
+                                   l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
+                self.fused.add(ce)
+                continue
             with self._time('spmm'):
                 a = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm') if reduce == 'lstm' else
                      O.spmm(rs.indptr, rs.indices, msg, reduce,
                             edge_weight=rs.weights if weighted else None))
             if o is None:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
-            acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
-            div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
 
             def proj(mod=mod, a=a, acc=acc, div=div, o=o):
                 O.gemm(self_rows, mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
@@ -365,14 +393,27 @@ class ShardedFullGraphPass:
             self_rows = self._get(h, T)[sh.own_slice(T)]
             for j, ce in enumerate(ces):
                 mod = hconv.mods[ce[1]]
+                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
+                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+                if isinstance(partials[ce][0], str):  # ('fused', msg, reduce, weighted)
+                    _, msg, reduce, weighted = partials[ce]
+                    rs = sh.rels[ce]
+                    if o is None:
+                        o = torch.empty((self_rows.shape[0], mod._out_feats),
+                                        dtype=torch.float32, device=msg.device)
+                    with self._time('spmm'):
+                        O.spmm_project(rs.indptr, rs.indices, msg, self_rows,
+                                       mod.fc_self.weight, mod.fc_neigh.weight, reduce,
+                                       rs.weights if weighted else None, relu=True,
+                                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
+                    self.fused.add(ce)
+                    continue
                 own, work, reduce = partials[ce]
                 if work is not None:
                     work.wait()
                 if o is None:
                     o = torch.empty((own.shape[0], mod._out_feats), dtype=torch.float32,
                                     device=own.device)
-                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
-                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
                 O.gemm(self_rows, mod.fc_self.weight, own, mod.fc_neigh.weight, relu=True,
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                        a2_deg=sh.rels[ce].deg_own,

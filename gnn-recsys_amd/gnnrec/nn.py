@@ -145,6 +145,12 @@ class ConvLayer(nn.Module):
                                        bool(self.norm))
             return z if out is None else z  # caller combines relations in grad mode
         m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
+        if reduce != 'lstm' and ops.can_spmm_project(graph.indptr, m, h_self, self.fc_self.weight,
+                                                     self.fc_neigh.weight):
+            return ops.spmm_project(graph.indptr, graph.indices, m, h_self, self.fc_self.weight,
+                                    self.fc_neigh.weight, reduce, ew, relu=True,
+                                    l2norm=bool(self.norm), accum=accum, out_div=out_div,
+                                    out=out)
         agg = self.aggregate(graph.indptr, graph.indices, m, reduce, ew)
         return ops.gemm(h_self, self.fc_self.weight, agg, self.fc_neigh.weight, relu=True,
                         l2norm=bool(self.norm), accum=accum, out_div=out_div, out=out)

@@ -7,6 +7,8 @@ an error.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -172,6 +174,61 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
                              a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div), ptr(out),
                              ldo, stream_ptr(A1.device))
     check(rc, "gnnrec_gemm_f32")
+    return out
+
+
+FUSED_D = 128  # gnnrec_spmm_project_f32 handles d_neigh = d_self = out = 128
+
+
+def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT) -> bool:
+    """True when the fused aggregation+projection kernel applies (shapes, alignment, no
+    heavy rows, GPU tensors; GNNREC_FUSED=0 disables it)."""
+    if os.environ.get("GNNREC_FUSED", "1") == "0":
+        return False
+    D = FUSED_D
+    if not (X.is_cuda and H.is_cuda and X.dim() == 2 and H.dim() == 2):
+        return False
+    if X.shape[1] != D or H.shape[1] != D or tuple(W_self.shape) != (D, D) or \
+            tuple(W_neigh.shape) != (D, D):
+        return False
+    if X.dtype != torch.float32 or H.dtype != torch.float32:
+        return False
+    for t in (X, H):
+        if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+            return False
+    return not split or split_plan(indptr, split) is None
+
+
+def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
+                 edge_weight: Optional[torch.Tensor] = None, relu: bool = True,
+                 l2norm: bool = False, accum: str = "store", out_div: float = 0.0,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ), d = 128."""
+    lib = _lib.load()
+    _dev(indptr, "indptr", torch.int64)
+    _dev(indices, "indices", torch.int32)
+    _dev(X, "X", torch.float32)
+    _dev(H, "H", torch.float32)
+    n_dst = indptr.numel() - 1
+    if H.shape[0] < n_dst:
+        raise ValueError(f"H has {H.shape[0]} rows, the CSR {n_dst} destinations")
+    if edge_weight is not None:
+        _dev(edge_weight, "edge_weight", torch.float32)
+        edge_weight = edge_weight.contiguous()
+    D = FUSED_D
+    if out is None:
+        if accum != "store":
+            raise ValueError("accumulating spmm_project needs an out tensor")
+        out = torch.empty((n_dst, D), dtype=torch.float32, device=X.device)
+    WsT = W_self.detach().t().contiguous()
+    WnT = W_neigh.detach().t().contiguous()
+    epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
+    check(lib.gnnrec_spmm_project_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
+                                      _rowmajor(X, "X"), ptr(H), _rowmajor(H, "H"), ptr(WsT),
+                                      ptr(WnT), n_dst, X.shape[1], REDUCE[reduce], epi,
+                                      ACCUM[accum], float(out_div), ptr(out),
+                                      _rowmajor(out, "out"), stream_ptr(X.device)),
+          "gnnrec_spmm_project_f32")
     return out
 
 

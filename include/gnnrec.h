@@ -17,6 +17,8 @@
  *   - gnnrec_spmm_csr_f32      <- graph.update_all(fn.copy_src|fn.u_mul_e,
  *                                 fn.mean|fn.max)  src/model.py:143-208
  *                                 (DGL gspmm -> _CAPI_DGLKernelSpMM)
+ *   - gnnrec_spmm_project_f32  <- the two above fused for d = 128 (update_all +
+ *                                 fc_self/fc_neigh + relu + norm in one launch)
  *   - gnnrec_gemm_f32          <- nn.Linear fc_self/fc_neigh/fc_preagg +
  *                                 relu + zero-guarded L2 norm + HeteroGraphConv
  *                                 aggregate, src/model.py:98-102,151,226-235,
@@ -120,6 +122,21 @@ int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                     const int32_t* a2_deg, int a2_mode, const float* bias,
                     int64_t M, int64_t N, int epilogue, int accum, float out_div,
                     float* out, int64_t ldo, void* stream);
+
+/* ---- a1+a3 fused: aggregation with the projection in its epilogue -----------
+ * out[v] (accum)= epi( H[v] W_self^T + agg(v) W_neigh^T ),  agg(v) = reduce over v's
+ * in-edges of X[indices[e]] (* ew[e]) exactly as gnnrec_spmm_csr_f32 computes it
+ * (bit-identical aggregate), epi = RELU / L2NORM bits, accum / out_div as gnnrec_gemm_f32.
+ * W_selfT / W_neighT: the TRANSPOSED nn.Linear weights, [d, d] row-major (k-major).
+ * d = 128 only (d_neigh = d_self = out); X, H, W 16-B aligned with ld % 4 == 0.
+ * Rows of any degree are reduced by one wavefront (callers route CSRs with heavy
+ * rows to spmm_csr_split + gemm).  Replaces update_all + fc_self/fc_neigh + relu +
+ * norm, src/model.py:143-208,226-235, and HeteroGraphConv's aggregate (:384-406). */
+int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                            const float* X, int64_t ldx, const float* H, int64_t ldh,
+                            const float* W_selfT, const float* W_neighT, int64_t n_dst,
+                            int64_t d, int reduce, int epilogue, int accum, float out_div,
+                            float* out, int64_t ldo, void* stream);
 
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >

@@ -543,3 +543,98 @@ def test_lstm_layer_matches_torch_lstm_and_trains():
     for name, a, b in zip(names, grads, ref):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=2e-4, atol=2e-5,
                                    err_msg=name)
+
+
+# ------------------------------------------- a1+a3 fused aggregate + project ---
+@pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("epi", ["relu_norm", "relu"])
+def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
+    from gnnrec import ops
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"{reduce}{weighted}{epi}".encode()))
+    n_dst, n_src, d = 3001, 1700, 128
+    deg = rng.integers(0, 90, n_dst)
+    deg[:4] = [0, 1, 2, 700]
+    dst = np.repeat(np.arange(n_dst), deg)
+    src = rng.integers(0, n_src, dst.size)
+    perm = rng.permutation(dst.size)
+    src, dst = src[perm], dst[perm]
+    indptr, indices, eids = oracle.csr_from_coo(src, dst, n_dst)
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    ew = rng.integers(1, 9, dst.size).astype(np.float32)[eids] if weighted else None
+    l2 = epi == "relu_norm"
+    agg = oracle.spmm_csr(indptr, indices, X, reduce, ew)
+    ref = oracle.relu(oracle.linear(H, Ws) + oracle.linear(agg, Wn))
+    if l2:
+        ref = oracle.l2_normalize_rows_guarded(ref)
+    g = [_t(indptr), _t(indices.astype(np.int32)), _t(X), _t(H), _t(Ws), _t(Wn)]
+    w = None if ew is None else _t(ew)
+    assert ops.can_spmm_project(g[0], g[2], g[3], g[4], g[5])
+    got = ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2)
+    # unnormalised sums over 700-edge rows reach |z| ~ 1e2: fp32 cancellation in a
+    # 256-term dot product is relative to that scale, not to the (small) result
+    atol = ATOL * max(1.0, float(np.abs(ref).max()))
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=RTOL, atol=atol)
+    # the unfused HIP path (same aggregate bits, MFMA projection) agrees as closely
+    a = ops.spmm(g[0], g[1], g[2], reduce, edge_weight=w)
+    unf = ops.gemm(g[3], g[4], a, g[5], relu=True, l2norm=l2)
+    np.testing.assert_allclose(got.cpu().numpy(), unf.cpu().numpy(), rtol=RTOL, atol=atol)
+    # deterministic
+    assert torch.equal(ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2), got)
+
+
+def test_spmm_project_accumulate_modes_and_strides():
+    from gnnrec import ops
+    rng = np.random.default_rng(77)
+    n_dst, n_src, d = 500, 400, 128
+    dst = rng.integers(0, n_dst, 6000)
+    src = rng.integers(0, n_src, 6000)
+    indptr, indices, _ = oracle.csr_from_coo(src, dst, n_dst)
+    X = rng.standard_normal((n_src, d + 4)).astype(np.float32)  # strided source table
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    Xt = _t(X)[:, :d]
+    agg = oracle.spmm_csr(indptr, indices, X[:, :d], "mean")
+    z = oracle.l2_normalize_rows_guarded(oracle.relu(oracle.linear(H, Ws) + oracle.linear(agg, Wn)))
+    base = rng.standard_normal((n_dst, d + 2)).astype(np.float32)
+    for mode, fn in (("add", lambda o: o + z), ("max", lambda o: np.maximum(o, z))):
+        out = _t(base)[:, :d]
+        ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), Xt, _t(H), _t(Ws), _t(Wn),
+                         "mean", None, relu=True, l2norm=True, accum=mode, out_div=2.0, out=out)
+        np.testing.assert_allclose(out.cpu().numpy(), fn(base[:, :d]) / 2.0, rtol=RTOL, atol=ATOL)
+
+
+def test_fused_sharded_pass_equals_modules_bitwise():
+    """d=128 models run the fused kernel in both the module path and the sharded pass:
+    at P=1 the two are bitwise identical and match the oracle."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    rng = np.random.default_rng(5)
+    n_u, n_i, E, d = 700, 300, 20000, 128
+    u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+    edges = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in edges.items()},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    feats = {"user": rng.standard_normal((n_u, d)).astype(np.float32),
+             "item": rng.standard_normal((n_i, d)).astype(np.float32)}
+    for nt, f in feats.items():
+        g.nodes[nt].data["features"] = _t(f)
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
+                          "cos", "sum", True).to(DEV).eval()
+    h1 = full_graph_embeddings(g, model)
+    shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
+    h2 = ShardedFullGraphPass(model, shard).run(shard.local_features(g.ndata["features"]))
+    for nt in h1:
+        assert torch.equal(h1[nt], h2[nt][: h1[nt].shape[0]]), nt
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    ref = oracle.model_full_graph(oracle.Graph({"user": n_u, "item": n_i}, edges), feats, sd,
+                                  "mean", "sum", True, True)
+    for nt in ref:
+        np.testing.assert_allclose(h1[nt].cpu().numpy(), ref[nt], rtol=RTOL, atol=ATOL)
