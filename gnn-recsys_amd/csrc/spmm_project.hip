@@ -33,7 +33,8 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx,
     const float* __restrict__ H, int64_t ldh, const float* __restrict__ WsT,
-    const float* __restrict__ WnT, int64_t n_dst, int epilogue, int accum, float out_div,
+    const float* __restrict__ WnT, const float* __restrict__ bias,
+    const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
     float* __restrict__ out, int64_t ldo) {
   __shared__ float Ws[kPD * kPD];
   __shared__ float Wn[kPD * kPD];
@@ -53,9 +54,12 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   const bool l2 = epilogue & GNNREC_EPI_L2NORM;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t stride = (int64_t)gridDim.x * kPWaves * kPRows;
+  const float b0 = bias ? bias[j0] : 0.f, b1 = bias ? bias[j0 + 1] : 0.f;
+  const float c0 = bias_ne ? bias_ne[j0] : 0.f, c1 = bias_ne ? bias_ne[j0 + 1] : 0.f;
 
   for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
        row0 += stride) {
+    bool nonempty[kPRows];
 #pragma unroll
     for (int r = 0; r < kPRows; ++r) {
       const int64_t row = row0 + r;
@@ -74,6 +78,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
       }
       combine_groups<LPR, VEC, REDUCE>(acc);
       finalize<VEC, REDUCE>(acc, deg, 0);
+      nonempty[r] = deg > 0;
       if (grp == 0)
         *reinterpret_cast<float4*>(&slots[wave][r][0][col]) =
             make_float4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
@@ -84,9 +89,14 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     // clobber keeps the compiler from hoisting the reads above the writes
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
+    // bias: a folded NodeEmbedding's W_self·b; bias_ne: its W_neigh·b, which only
+    // rows with at least one neighbour receive (the mean of an empty set is 0)
     float z[kPRows][2];
 #pragma unroll
-    for (int r = 0; r < kPRows; ++r) z[r][0] = z[r][1] = 0.f;
+    for (int r = 0; r < kPRows; ++r) {
+      z[r][0] = b0 + (nonempty[r] ? c0 : 0.f);
+      z[r][1] = b1 + (nonempty[r] ? c1 : 0.f);
+    }
 #pragma unroll 2
     for (int k = 0; k < kPD; k += 4) {
       float4 a4[kPRows], s4[kPRows];
@@ -160,7 +170,8 @@ using namespace gnnrec;
 extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices,
                                        const float* ew, const float* X, int64_t ldx,
                                        const float* H, int64_t ldh, const float* W_selfT,
-                                       const float* W_neighT, int64_t n_dst, int64_t d,
+                                       const float* W_neighT, const float* bias,
+                                       const float* bias_nonempty, int64_t n_dst, int64_t d,
                                        int reduce, int epilogue, int accum, float out_div,
                                        float* out, int64_t ldo, void* stream) {
   GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project_f32: only d = %d (got %lld)", kPD,
@@ -193,7 +204,8 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   hipStream_t s = as_stream(stream);
 #define GNNREC_SPP(R, W)                                                                     \
   hipLaunchKernelGGL((spmm_project_kernel<R, W>), grid, block, 0, s, indptr, indices, ew, X, \
-                     ldx, H, ldh, W_selfT, W_neighT, n_dst, epilogue, accum, out_div, out, ldo)
+                     ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum,  \
+                     out_div, out, ldo)
   if (ew) {
     if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPP(GNNREC_REDUCE_SUM, true);
     else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPP(GNNREC_REDUCE_MEAN, true);

@@ -203,8 +203,12 @@ class ShardedFullGraphPass:
     inject a checker backend with the same signatures."""
 
     def __init__(self, model, shard: GraphShard, exchange: Optional[Exchange] = None,
-                 ops_backend=None, overlap: bool = True):
+                 ops_backend=None, overlap: bool = True, fold_embedding: bool = True):
         self.model = model
+        # fold the partitioned type's NodeEmbedding into the first layer's fused launches
+        # (one rank, mean/sum reducers): its 10M-row GEMM and table disappear
+        self.fold_embedding = fold_embedding
+        self._fold = {}  # nt -> (W_emb, b_emb) while h[nt] holds that type's raw features
         self.shard = shard
         self.ex = exchange if exchange is not None else Exchange()
         self.ops = ops_backend if ops_backend is not None else ops
@@ -261,6 +265,10 @@ class ShardedFullGraphPass:
                 if mod is None or nt not in h:
                     continue
                 W, b, x = mod.proj_feats.weight, mod.proj_feats.bias, h[nt]
+                if nt == sh.ptype and self.fold_embedding and m.layers and \
+                        self._foldable(m.layers[0], h, nt, W):
+                    self._fold[nt] = (W.detach(), b.detach())
+                    continue  # h[nt] stays the raw features
                 if nt == sh.ptype and self.side is not None:
                     y = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float32, device=x.device)
                     self._ready[id(y)] = self._on_side(
@@ -273,6 +281,47 @@ class ShardedFullGraphPass:
         for nt in list(h):
             self._get(h, nt)
         return h
+
+    def _foldable(self, hconv, h, nt, W_emb) -> bool:
+        """Every first-layer relation touching nt runs fused with the embedding folded in:
+        one rank, W_emb square at the fused width, no fc_preagg (it is non-linear), reducers
+        mean/sum without edge weights on the source side (linear in the source rows)."""
+        can = getattr(self.ops, 'can_spmm_project', None)
+        if self.ex.ws != 1 or can is None or tuple(W_emb.shape) != (ops.FUSED_D, ops.FUSED_D):
+            return False
+        x = h[nt]
+        for ces in self._active(hconv, h).values():
+            for ce in ces:
+                if nt not in (ce[0], ce[2]):
+                    continue
+                mod = hconv.mods[ce[1]]
+                preagg, weighted, reduce = mod._plan_rel(ce)
+                if reduce == 'lstm' or ce[0] == ce[2]:
+                    return False
+                if ce[0] == nt and (preagg or weighted or reduce not in ('mean', 'sum')):
+                    return False
+                rs = self.shard.rels[ce]
+                msg = x if ce[0] == nt else h[ce[0]]
+                own = x if ce[2] == nt else h[ce[2]]
+                if preagg or not can(rs.indptr, msg, own, mod.fc_self.weight,
+                                     mod.fc_neigh.weight):
+                    return False
+        return True
+
+    def _folded(self, mod, ce):
+        """(W_self, W_neigh, bias, bias_nonempty) of a fused launch, with a NodeEmbedding
+        (W_e, b_e) folded in where its node type's raw features stand in for h:
+        (x W_eᵀ + b_e) W_sᵀ = x (W_s W_e)ᵀ + W_s b_e; mean/sum over x[src] then W_n W_e,
+        plus W_n b_e on rows that have neighbours."""
+        Ws, Wn = mod.fc_self.weight.detach(), mod.fc_neigh.weight.detach()
+        bias = bias_ne = None
+        if ce[2] in self._fold:
+            We, be = self._fold[ce[2]]
+            Ws, bias = Ws @ We, Ws @ be
+        if ce[0] in self._fold:
+            We, be = self._fold[ce[0]]
+            Wn, bias_ne = Wn @ We, Wn @ be
+        return Ws, Wn, bias, bias_ne
 
     def _active(self, hconv, h):
         active: Dict[str, list] = {}
@@ -359,11 +408,12 @@ class ShardedFullGraphPass:
                 if o is None:
                     o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
                                     device=msg.device)
+                Ws, Wn, bias, bias_ne = self._folded(mod, ce)
                 with self._time('spmm'):
-                    O.spmm_project(rs.indptr, rs.indices, msg, self_rows, mod.fc_self.weight,
-                                   mod.fc_neigh.weight, reduce,
+                    O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                    rs.weights if weighted else None, relu=True,
-                                   l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
+                                   l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
+                                   bias=bias, bias_nonempty=bias_ne)
                 self.fused.add(ce)
                 continue
             with self._time('spmm'):
@@ -401,11 +451,12 @@ class ShardedFullGraphPass:
                     if o is None:
                         o = torch.empty((self_rows.shape[0], mod._out_feats),
                                         dtype=torch.float32, device=msg.device)
+                    Ws, Wn, bias, bias_ne = self._folded(mod, ce)
                     with self._time('spmm'):
-                        O.spmm_project(rs.indptr, rs.indices, msg, self_rows,
-                                       mod.fc_self.weight, mod.fc_neigh.weight, reduce,
+                        O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                        rs.weights if weighted else None, relu=True,
-                                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
+                                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
+                                       bias=bias, bias_nonempty=bias_ne)
                     self.fused.add(ce)
                     continue
                 own, work, reduce = partials[ce]
@@ -439,6 +490,7 @@ class ShardedFullGraphPass:
             self._local(hconv, h, active, out)
             partials = self._partials(hconv, h, active)
         self._owned(hconv, h, active, partials, out)
+        self._fold.clear()  # a folded embedding only stands in for the first layer's input
         return out
 
 

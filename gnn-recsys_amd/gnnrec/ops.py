@@ -202,8 +202,10 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
 def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                  edge_weight: Optional[torch.Tensor] = None, relu: bool = True,
                  l2norm: bool = False, accum: str = "store", out_div: float = 0.0,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ), d = 128."""
+                 out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+                 bias_nonempty: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ + bias
+    + [deg > 0]·bias_nonempty), d = 128."""
     lib = _lib.load()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
@@ -222,10 +224,18 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
         out = torch.empty((n_dst, D), dtype=torch.float32, device=X.device)
     WsT = W_self.detach().t().contiguous()
     WnT = W_neigh.detach().t().contiguous()
+    for t, name in ((bias, "bias"), (bias_nonempty, "bias_nonempty")):
+        if t is not None:
+            _dev(t, name, torch.float32)
+            if t.numel() != D:
+                raise ValueError(f"{name} must have {D} entries")
+    bias = None if bias is None else bias.detach().contiguous()
+    bias_nonempty = None if bias_nonempty is None else bias_nonempty.detach().contiguous()
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
     check(lib.gnnrec_spmm_project_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
                                       _rowmajor(X, "X"), ptr(H), _rowmajor(H, "H"), ptr(WsT),
-                                      ptr(WnT), n_dst, X.shape[1], REDUCE[reduce], epi,
+                                      ptr(WnT), ptr(bias), ptr(bias_nonempty), n_dst,
+                                      X.shape[1], REDUCE[reduce], epi,
                                       ACCUM[accum], float(out_div), ptr(out),
                                       _rowmajor(out, "out"), stream_ptr(X.device)),
           "gnnrec_spmm_project_f32")

@@ -128,15 +128,20 @@ int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
  * in-edges of X[indices[e]] (* ew[e]) exactly as gnnrec_spmm_csr_f32 computes it
  * (bit-identical aggregate), epi = RELU / L2NORM bits, accum / out_div as gnnrec_gemm_f32.
  * W_selfT / W_neighT: the TRANSPOSED nn.Linear weights, [d, d] row-major (k-major).
+ * bias [d] (nullable) is added to every row before epi; bias_nonempty [d] (nullable) only
+ * to rows with in-degree > 0 — together they carry a NodeEmbedding folded into the layer
+ * (H = raw features, W_self <- W_self W_emb, bias = W_self b_emb; X = raw features,
+ * W_neigh <- W_neigh W_emb, bias_nonempty = W_neigh b_emb; mean/sum reducers only).
  * d = 128 only (d_neigh = d_self = out); X, H, W 16-B aligned with ld % 4 == 0.
  * Rows of any degree are reduced by one wavefront (callers route CSRs with heavy
  * rows to spmm_csr_split + gemm).  Replaces update_all + fc_self/fc_neigh + relu +
  * norm, src/model.py:143-208,226-235, and HeteroGraphConv's aggregate (:384-406). */
 int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
                             const float* X, int64_t ldx, const float* H, int64_t ldh,
-                            const float* W_selfT, const float* W_neighT, int64_t n_dst,
-                            int64_t d, int reduce, int epilogue, int accum, float out_div,
-                            float* out, int64_t ldo, void* stream);
+                            const float* W_selfT, const float* W_neighT, const float* bias,
+                            const float* bias_nonempty, int64_t n_dst, int64_t d, int reduce,
+                            int epilogue, int accum, float out_div, float* out, int64_t ldo,
+                            void* stream);
 
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >

@@ -630,7 +630,8 @@ def test_fused_sharded_pass_equals_modules_bitwise():
                           "cos", "sum", True).to(DEV).eval()
     h1 = full_graph_embeddings(g, model)
     shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
-    h2 = ShardedFullGraphPass(model, shard).run(shard.local_features(g.ndata["features"]))
+    lf = shard.local_features(g.ndata["features"])
+    h2 = ShardedFullGraphPass(model, shard, fold_embedding=False).run(lf)
     for nt in h1:
         assert torch.equal(h1[nt], h2[nt][: h1[nt].shape[0]]), nt
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
@@ -638,3 +639,44 @@ def test_fused_sharded_pass_equals_modules_bitwise():
                                   "mean", "sum", True, True)
     for nt in ref:
         np.testing.assert_allclose(h1[nt].cpu().numpy(), ref[nt], rtol=RTOL, atol=ATOL)
+    # the user NodeEmbedding folded into the first layer's launches: no embedding table,
+    # same function up to fp32 rounding
+    runner = ShardedFullGraphPass(model, shard)
+    h3 = runner.run(lf)
+    assert runner.fused == set(shard.canonical_etypes)
+    for nt in ref:
+        np.testing.assert_allclose(h3[nt][: ref[nt].shape[0]].cpu().numpy(), ref[nt], rtol=RTOL,
+                                   atol=ATOL)
+
+
+def test_embedding_fold_rows_without_neighbours():
+    """Users with no purchases and items never bought: the folded bias W_neigh·b_emb must
+    not reach rows whose mean is over an empty set."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass
+    rng = np.random.default_rng(9)
+    n_u, n_i, E, d = 400, 200, 3000, 128
+    u, i = rng.integers(0, n_u // 2, E), rng.integers(0, n_i // 2, E)  # upper halves isolated
+    edges = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in edges.items()},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    feats = {"user": rng.standard_normal((n_u, d)).astype(np.float32),
+             "item": rng.standard_normal((n_i, d)).astype(np.float32)}
+    for nt, f in feats.items():
+        g.nodes[nt].data["features"] = _t(f)
+    torch.manual_seed(1)
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
+                          "cos", "sum", True).to(DEV).eval()
+    with torch.no_grad():
+        for p in model.parameters():  # large embedding biases make a leak obvious
+            if p.dim() == 1:
+                p.add_(1.0)
+    shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
+    h = ShardedFullGraphPass(model, shard).run(shard.local_features(g.ndata["features"]))
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    ref = oracle.model_full_graph(oracle.Graph({"user": n_u, "item": n_i}, edges), feats, sd,
+                                  "mean", "sum", True, True)
+    for nt in ref:
+        np.testing.assert_allclose(h[nt][: ref[nt].shape[0]].cpu().numpy(), ref[nt], rtol=RTOL,
+                                   atol=ATOL)
