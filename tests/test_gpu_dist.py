@@ -17,7 +17,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _build(agg, hetero):
+def _build(agg, hetero, d=32):
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     rng = np.random.default_rng(0)
@@ -30,15 +30,16 @@ def _build(agg, hetero):
     occ = torch.from_numpy(rng.integers(1, 9, E)).cuda()
     g.edges["buys"].data["occurrence"] = occ
     g.edges["bought-by"].data["occurrence"] = occ
-    feats = {"user": torch.from_numpy(rng.standard_normal((n_u, 32)).astype(np.float32)).cuda(),
-             "item": torch.from_numpy(rng.standard_normal((n_i, 32)).astype(np.float32)).cuda()}
+    feats = {"user": torch.from_numpy(rng.standard_normal((n_u, d)).astype(np.float32)).cuda(),
+             "item": torch.from_numpy(rng.standard_normal((n_i, d)).astype(np.float32)).cuda()}
     torch.manual_seed(0)
-    model = gnn.ConvModel(g, 3, {"user": 32, "item": 32, "hidden": 64, "out": 32}, True, 0.0, agg,
+    hidden = 64 if d == 32 else d  # d = 128: every layer takes the fused aggregate+project path
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": hidden, "out": d}, True, 0.0, agg,
                           "cos", hetero, True).cuda().eval()
     return g, feats, model
 
 
-def _worker(rank, world, port, agg, hetero, q):
+def _worker(rank, world, port, agg, hetero, d, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -46,7 +47,7 @@ def _worker(rank, world, port, agg, hetero, q):
     try:
         from gnnrec.dist import Exchange
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
-        g, feats, model = _build(agg, hetero)
+        g, feats, model = _build(agg, hetero, d)
         ex = Exchange()
         sh = GraphShard.from_graph(g, rank, world, "user", device="cuda")
         out = ShardedFullGraphPass(model, sh, ex).run(sh.local_features(feats))
@@ -56,17 +57,18 @@ def _worker(rank, world, port, agg, hetero, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("agg,hetero", [("mean", "sum"), ("pool_nn_edge", "max")])
-def test_two_ranks_one_gpu_match_single_process(agg, hetero):
+@pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 32), ("pool_nn_edge", "max", 32),
+                                          ("mean", "sum", 128), ("pool_nn", "mean", 128)])
+def test_two_ranks_one_gpu_match_single_process(agg, hetero, d):
     import torch.multiprocessing as mp
     from gnnrec.inference import full_graph_embeddings
-    g, feats, model = _build(agg, hetero)
+    g, feats, model = _build(agg, hetero, d)
     with torch.no_grad():
         ref = full_graph_embeddings(g, model, feats)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, agg, hetero, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, agg, hetero, d, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(2)]
