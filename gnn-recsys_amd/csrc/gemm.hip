@@ -488,5 +488,9 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   if (N <= 32) return launch_gemm<32>(g, s);
   if (N <= 64) return launch_gemm<64>(g, s);
   if (N <= 128) return launch_gemm<128>(g, s);
+  // wider outputs: 128-column blocks (two waves per SIMD) unless the row norm needs the
+  // whole row in one block (the 256-column tile runs at one wave per SIMD)
+  if (!(epilogue & GNNREC_EPI_L2NORM) && getenv("GNNREC_GEMM_BN256") == nullptr)
+    return launch_gemm<128>(g, s);
   return launch_gemm<256>(g, s);
 }
