@@ -83,6 +83,7 @@ def _run(case, world):
     ("model_het_pooledge_sum_noemb_nn", 2),
     ("model_het_meanedge_max_emb", 4),
     ("model_het_mean_sum_skip", 2),
+    ("model_bip_poolnn_max_noemb_nn", 8),  # 41 users over 8 ranks: ragged and tiny shards
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
     meta = golden_io.manifest()[case]

@@ -563,6 +563,7 @@ def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
     indptr, indices, eids = oracle.csr_from_coo(src, dst, n_dst)
     X = rng.standard_normal((n_src, d)).astype(np.float32)
     H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    H[0] = 0.0  # row 0 has no neighbours either: z = 0, the zero-norm guard keeps it 0
     Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
     Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
     ew = rng.integers(1, 9, dst.size).astype(np.float32)[eids] if weighted else None
@@ -579,6 +580,7 @@ def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
     # 256-term dot product is relative to that scale, not to the (small) result
     atol = ATOL * max(1.0, float(np.abs(ref).max()))
     np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=RTOL, atol=atol)
+    assert torch.isfinite(got).all() and not got[0].any()
     # the unfused HIP path (same aggregate bits, MFMA projection) agrees as closely
     a = ops.spmm(g[0], g[1], g[2], reduce, edge_weight=w)
     unf = ops.gemm(g[3], g[4], a, g[5], relu=True, l2norm=l2)
