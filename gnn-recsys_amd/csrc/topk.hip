@@ -30,7 +30,7 @@ template <int KMAX>
 __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
     const float* __restrict__ S, int64_t ld, int64_t n_rows, int64_t n_cols, int k,
     const int64_t* __restrict__ ex_ptr, const int64_t* __restrict__ ex_idx,
-    float* __restrict__ out_v, int64_t* __restrict__ out_i) {
+    float* __restrict__ out_v, int64_t* __restrict__ out_i, bool vec) {
   __shared__ int64_t excl[kMaxExcl];
   __shared__ float red_v[kTopkThreads / 64];
   __shared__ int64_t red_i[kTopkThreads / 64];
@@ -76,10 +76,9 @@ __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
   for (int j = 0; j < KMAX; ++j) { tv[j] = -INFINITY; ti[j] = INT64_MAX; }
   float thr_v = -INFINITY;  // current k-th best of this thread (kept out of the
   int64_t thr_i = INT64_MAX;  // register array: a runtime index would spill it to scratch)
-  for (int64_t c = tid; c < n_cols; c += kTopkThreads) {
-    const float v = srow[c];
-    if (!better(v, c, thr_v, thr_i)) continue;
-    if (n_ex && excluded(c)) continue;
+  auto offer = [&](float v, int64_t c) {
+    if (!better(v, c, thr_v, thr_i)) return;
+    if (n_ex && excluded(c)) return;
     // insert (unrolled bubble from the tail)
     float cv = v;
     int64_t ci = c;
@@ -94,7 +93,39 @@ __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
 #pragma unroll
     for (int j = 0; j < KMAX; ++j)
       if (j == k - 1) { thr_v = tv[j]; thr_i = ti[j]; }
+  };
+  // streaming scan: 16-B loads, kUnroll of them in flight per thread before the
+  // (almost always rejecting) threshold tests; scalar loop for the tail / unaligned rows
+  int64_t c_tail = 0;
+  if (vec) {
+    constexpr int kUnroll = 4;
+    constexpr int64_t kStep = (int64_t)kTopkThreads * 4;
+    const int64_t n4 = n_cols & ~int64_t(3);
+    int64_t c0 = (int64_t)tid * 4;
+    for (; c0 + (kUnroll - 1) * kStep < n4; c0 += kUnroll * kStep) {
+      float4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        v[u] = *reinterpret_cast<const float4*>(srow + c0 + u * kStep);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t c = c0 + u * kStep;
+        offer(v[u].x, c);
+        offer(v[u].y, c + 1);
+        offer(v[u].z, c + 2);
+        offer(v[u].w, c + 3);
+      }
+    }
+    for (; c0 < n4; c0 += kStep) {
+      const float4 v = *reinterpret_cast<const float4*>(srow + c0);
+      offer(v.x, c0);
+      offer(v.y, c0 + 1);
+      offer(v.z, c0 + 2);
+      offer(v.w, c0 + 3);
+    }
+    c_tail = n4;
   }
+  for (int64_t c = c_tail + tid; c < n_cols; c += kTopkThreads) offer(srow[c], c);
 
   // k rounds of block argmax over the list heads
   int head = 0;
@@ -148,14 +179,15 @@ extern "C" int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_r
                  "gnnrec_topk_rows_f32: exclusion indptr without indices");
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)n_rows);
+  const bool vec = aligned16(scores) && ld % 4 == 0;
   if (k <= 16)
     hipLaunchKernelGGL((topk_rows_kernel<16>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx);
+                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
   else if (k <= 32)
     hipLaunchKernelGGL((topk_rows_kernel<32>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx);
+                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
   else
     hipLaunchKernelGGL((topk_rows_kernel<64>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx);
+                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
   return check_launch("gnnrec_topk_rows_f32");
 }
