@@ -682,3 +682,51 @@ def test_embedding_fold_rows_without_neighbours():
     for nt in ref:
         np.testing.assert_allclose(h[nt][: ref[nt].shape[0]].cpu().numpy(), ref[nt], rtol=RTOL,
                                    atol=ATOL)
+
+
+@pytest.mark.parametrize("N,K1,K2,epi,mode", [(128, 128, 128, "relu_norm", "div"),
+                                              (128, 128, 0, "bias", "none"),
+                                              (64, 64, 96, "relu", "zero"),
+                                              (32, 32, 32, "sigmoid", "none")])
+def test_gemm_large_m_persistent_path(N, K1, K2, epi, mode):
+    """M large enough that the persistent row-tile walk (prefetch across tiles) runs,
+    with the A2 row transforms, bias, every epilogue and accumulate-add."""
+    from gnnrec import _lib, ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(N + K1 + K2)
+    M = 300_001
+    A1 = torch.randn(M, K1, device="cuda", generator=gen)
+    W1 = torch.randn(N, K1, device="cuda", generator=gen) * 0.1
+    A2 = torch.randn(M, K2, device="cuda", generator=gen) if K2 else None
+    W2 = torch.randn(N, K2, device="cuda", generator=gen) * 0.1 if K2 else None
+    bias = torch.randn(N, device="cuda", generator=gen) if epi == "bias" else None
+    deg = torch.randint(0, 4, (M,), device="cuda", generator=gen, dtype=torch.int32)
+    amode = {"none": _lib.A2_NONE, "div": _lib.A2_DIV_DEG, "zero": _lib.A2_ZERO_DEG}[mode]
+    kw = dict(relu=epi in ("relu", "relu_norm"), l2norm=epi == "relu_norm",
+              sigmoid=epi == "sigmoid")
+    out = ops.gemm(A1, W1, A2, W2, bias, a2_deg=deg if K2 else None,
+                   a2_mode=amode if K2 else _lib.A2_NONE, **kw)
+    ref = A1.double() @ W1.double().t()
+    if K2:
+        a2 = A2.double()
+        if mode == "div":
+            a2 = a2 / deg.clamp(min=1).double()[:, None]
+        elif mode == "zero":
+            a2 = a2 * (deg > 0).double()[:, None]
+        ref = ref + a2 @ W2.double().t()
+    if bias is not None:
+        ref = ref + bias.double()
+    if kw["relu"]:
+        ref = ref.clamp(min=0)
+    if kw["sigmoid"]:
+        ref = torch.sigmoid(ref)
+    if kw["l2norm"]:
+        n = ref.norm(dim=1, keepdim=True)
+        ref = ref / torch.where(n == 0, torch.ones_like(n), n)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.float().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    acc = torch.randn(M, N, device="cuda", generator=gen)
+    acc0 = acc.clone()
+    ops.gemm(A1, W1, A2, W2, bias, a2_deg=deg if K2 else None,
+             a2_mode=amode if K2 else _lib.A2_NONE, accum="add", out=acc, **kw)
+    np.testing.assert_allclose(acc.cpu().numpy(), (acc0 + out).cpu().numpy(), rtol=1e-5,
+                               atol=1e-5)
