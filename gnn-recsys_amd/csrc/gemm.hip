@@ -339,7 +339,7 @@ constexpr int glds_smem_floats() {
 }
 
 template <int BN>
-__global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_glds_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (BN > 128 ? 1 : GEMM_WAVES_PER_SIMD)) void gemm_f32_glds_kernel(GemmArgs g) {
   constexpr int NT = BN / 32;
   constexpr int AI = BM * BK * 4 / 1024 / 4;   // A-tile DMA instructions per wave (4)
   constexpr int WI = BN * BK * 4 / 1024 / 4;   // W-tile DMA instructions per wave (BN/32)

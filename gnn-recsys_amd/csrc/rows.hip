@@ -1,0 +1,62 @@
+// a10 — block feature / edge-data gather: dst[i] = src[idx[i]] for rows of any
+// fixed byte width (reference: DGL copies node features into blocks[0].srcdata
+// and edge data into every block at block creation, read by src/train/run.py:112,340).
+// Rows are moved in the widest unit their alignment allows (16, 8, 4 or 1 B), one
+// unit per thread, consecutive threads on consecutive units of a row — so a 512-B
+// feature row is one coalesced 16-B-per-lane sweep and 8-B edge ids pack 8 rows per
+// 64 B.
+#include "common.hpp"
+
+namespace gnnrec {
+namespace {
+
+template <typename U>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const char* __restrict__ src,
+                                                          int64_t src_ld,
+                                                          const int64_t* __restrict__ idx,
+                                                          int64_t n, int64_t units_per_row,
+                                                          char* __restrict__ dst, int64_t dst_ld) {
+  const int64_t total = n * units_per_row;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / units_per_row, u = t - row * units_per_row;
+    const U* s = reinterpret_cast<const U*>(src + idx[row] * src_ld) + u;
+    U* d = reinterpret_cast<U*>(dst + row * dst_ld) + u;
+    *d = *s;
+  }
+}
+
+template <typename U>
+int launch(const void* src, int64_t src_ld, const int64_t* idx, int64_t n, int64_t row_bytes,
+           void* dst, int64_t dst_ld, hipStream_t s) {
+  const int64_t upr = row_bytes / (int64_t)sizeof(U);
+  const int64_t total = n * upr;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(gather_rows_kernel<U>, dim3((unsigned)blocks), dim3(256), 0, s,
+                     static_cast<const char*>(src), src_ld, idx, n, upr, static_cast<char*>(dst),
+                     dst_ld);
+  return check_launch("gnnrec_gather_rows");
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+extern "C" int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx,
+                                  int64_t n, int64_t row_bytes, void* dst, int64_t dst_ld_bytes,
+                                  void* stream) {
+  GNNREC_REQUIRE(n >= 0 && row_bytes >= 0, "gnnrec_gather_rows: negative size");
+  if (n == 0 || row_bytes == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(src && idx && dst, "gnnrec_gather_rows: null pointer");
+  GNNREC_REQUIRE(src_ld_bytes >= row_bytes && dst_ld_bytes >= row_bytes,
+                 "gnnrec_gather_rows: row stride below the row width");
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                       (uintptr_t)src_ld_bytes | (uintptr_t)dst_ld_bytes | (uintptr_t)row_bytes;
+  hipStream_t s = as_stream(stream);
+  if ((al & 15u) == 0) return launch<uint4>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
+  if ((al & 7u) == 0) return launch<uint64_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
+  if ((al & 3u) == 0) return launch<uint32_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
+  return launch<uint8_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
+}

@@ -346,6 +346,30 @@ def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh,
     return out
 
 
+def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """a10: src[idx] along dim 0 for a device tensor of any dtype whose rows are contiguous
+    (node features into blocks[0].srcdata, edge data into blocks)."""
+    lib = _lib.load()
+    _dev(idx, "idx", torch.int64)
+    if not src.is_cuda:
+        raise ValueError("src: expected a device tensor (there is no CPU path)")
+    if src.dim() == 0:
+        raise ValueError("src: expected at least one dimension")
+    row = src[0] if src.shape[0] else src.new_empty(src.shape[1:])
+    if not (row.is_contiguous() and (src.dim() == 1 or src.stride(0) >= row.numel())):
+        src = src.contiguous()
+    out = torch.empty((idx.numel(),) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    es = src.element_size()
+    row_elems = 1
+    for n in src.shape[1:]:
+        row_elems *= n
+    row_bytes = es * row_elems
+    idx = idx.contiguous()
+    check(lib.gnnrec_gather_rows(ptr(src), src.stride(0) * es, ptr(idx), idx.numel(), row_bytes,
+                                 ptr(out), row_bytes, stream_ptr(src.device)), "gnnrec_gather_rows")
+    return out
+
+
 def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
               Hd: torch.Tensor) -> torch.Tensor:
     """a7: cosine of the L2-normalised endpoint rows, one value per edge -> [E]."""

@@ -100,12 +100,12 @@ class BlockSampler:
             for ce in b.canonical_etypes:
                 eid = b._edata[ce][EID]
                 for k, v in g._edata[ce].items():
-                    b._edata[ce][k] = v[eid]
+                    b._edata[ce][k] = ops.gather_rows(v, eid)
         b0 = blocks[0]
         for nt in b0.ntypes:
             ids = b0._src[nt][NID]
             for k, v in g._ndata[nt].items():
-                b0._src[nt][k] = v[ids]
+                b0._src[nt][k] = ops.gather_rows(v, ids)
         return blocks
 
     def _one_block(self, g, seeds, block_id, masks) -> Block:
@@ -327,7 +327,7 @@ class EdgeDataLoader:
             pos_g = PairGraph(pos_l, node_ids)
             for ce, e in batch.items():
                 for k, v in g._edata[ce].items():
-                    pos_g._edata[ce][k] = v[e]
+                    pos_g._edata[ce][k] = ops.gather_rows(v, e)
                 pos_g._edata[ce][EID] = e
             exclude = None
             if self.exclude == 'reverse_types':

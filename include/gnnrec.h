@@ -34,6 +34,8 @@
  *   - gnnrec_gemm_tn_f32,      <- torch autograd of those layers in the
  *     gnnrec_act_backward_f32     training step, src/train/run.py:124-138
  *   - gnnrec_lstm_step_f32     <- ConvLayer._lstm_reducer src/model.py:106-121
+ *   - gnnrec_gather_rows       <- blocks[0].srcdata / block edata copies
+ *                                 (src/train/run.py:112,340)
  *   - gnnrec_synth_edges       <- (no reference counterpart: synthetic graph
  *                                 generator for the benchmark shapes)
  */
@@ -234,6 +236,13 @@ int gnnrec_lstm_step_f32(const float* P, int64_t ldp, const int64_t* indptr,
                          const int32_t* indices, const int64_t* order, int64_t t, int64_t n_act,
                          const float* h_in, float* h_out, float* c, int64_t d,
                          const float* W_hhT, float* out, int64_t ldo, void* stream);
+
+/* ---- a10: row gather (block features / edge data) -------------------------
+ * dst row i (dst_ld_bytes apart) = src row idx[i] (src_ld_bytes apart), row_bytes each,
+ * any dtype.  Replaces DGL's copy of node features into blocks[0].srcdata and of edge
+ * data into the blocks (read at src/train/run.py:112,340). */
+int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx, int64_t n,
+                       int64_t row_bytes, void* dst, int64_t dst_ld_bytes, void* stream);
 
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),

@@ -730,3 +730,18 @@ def test_gemm_large_m_persistent_path(N, K1, K2, epi, mode):
              a2_mode=amode if K2 else _lib.A2_NONE, accum="add", out=acc, **kw)
     np.testing.assert_allclose(acc.cpu().numpy(), (acc0 + out).cpu().numpy(), rtol=1e-5,
                                atol=1e-5)
+
+
+def test_gather_rows_any_dtype_and_stride():
+    from gnnrec import ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(2)
+    idx = torch.randint(0, 1000, (5000,), device="cuda", generator=gen)
+    cases = [torch.randn(1000, 128, device="cuda", generator=gen),
+             torch.randn(1000, 131, device="cuda", generator=gen)[:, :5],   # strided rows
+             torch.randint(0, 99, (1000,), device="cuda", generator=gen),     # int64 edge data
+             torch.randn(1000, 3, device="cuda", generator=gen).half(),       # 6-B rows
+             torch.randint(0, 9, (1000, 7), device="cuda", generator=gen).to(torch.uint8)]
+    for x in cases:
+        assert torch.equal(ops.gather_rows(x, idx), x[idx]), (x.dtype, tuple(x.shape))
+    assert ops.gather_rows(cases[0], idx[:0]).shape == (0, 128)
