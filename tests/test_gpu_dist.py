@@ -21,7 +21,7 @@ def _build(agg, hetero, d=32):
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     rng = np.random.default_rng(0)
-    n_u, n_i, E = 3000, 700, 40000
+    n_u, n_i, E = 3000, 700, (40000 if d == 32 else 100000)  # d=128: >= 24 edges/row, fused
     u = rng.integers(0, n_u, E)
     i = rng.integers(0, n_i, E)
     g = HeteroGraph({("user", "buys", "item"): (torch.from_numpy(u), torch.from_numpy(i)),

@@ -658,7 +658,7 @@ def test_embedding_fold_rows_without_neighbours():
     from gnnrec.graph import HeteroGraph
     from gnnrec.inference import GraphShard, ShardedFullGraphPass
     rng = np.random.default_rng(9)
-    n_u, n_i, E, d = 400, 200, 3000, 128
+    n_u, n_i, E, d = 400, 200, 20000, 128  # >= 24 edges per row on average: the fused path
     u, i = rng.integers(0, n_u // 2, E), rng.integers(0, n_i // 2, E)  # upper halves isolated
     edges = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
     g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in edges.items()},
@@ -675,7 +675,9 @@ def test_embedding_fold_rows_without_neighbours():
             if p.dim() == 1:
                 p.add_(1.0)
     shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
-    h = ShardedFullGraphPass(model, shard).run(shard.local_features(g.ndata["features"]))
+    runner = ShardedFullGraphPass(model, shard)
+    h = runner.run(shard.local_features(g.ndata["features"]))
+    assert runner.fused == set(shard.canonical_etypes)
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
     ref = oracle.model_full_graph(oracle.Graph({"user": n_u, "item": n_i}, edges), feats, sd,
                                   "mean", "sum", True, True)
@@ -745,3 +747,16 @@ def test_gather_rows_any_dtype_and_stride():
     for x in cases:
         assert torch.equal(ops.gather_rows(x, idx), x[idx]), (x.dtype, tuple(x.shape))
     assert ops.gather_rows(cases[0], idx[:0]).shape == (0, 128)
+
+
+def test_fused_dispatch_skips_low_degree_csr():
+    """Below FUSED_MIN_DEG edges per row the in-kernel projection is LDS-bound: such CSRs
+    take the aggregation + GEMM path."""
+    from gnnrec import ops
+    d = 128
+    X, H = torch.zeros(10, d, device=DEV), torch.zeros(100, d, device=DEV)
+    W = torch.zeros(d, d, device=DEV)
+    sparse = torch.arange(0, 1001, 10, device=DEV)        # 100 rows x 10 edges
+    dense = torch.arange(0, 100 * 30 + 1, 30, device=DEV)  # 100 rows x 30 edges
+    assert not ops.can_spmm_project(sparse, X, H, W, W)
+    assert ops.can_spmm_project(dense, X, H, W, W)

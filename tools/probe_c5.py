@@ -1,0 +1,50 @@
+"""Per-relation timing of the fused aggregate+project launches on the C5 graph
+(80 % clicks / 20 % buys): which launch is slow and why.
+
+    python tools/probe_c5.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gnn-recsys_amd"))
+import torch  # noqa: E402
+
+from gnnrec import ops  # noqa: E402
+from gnnrec.synth import bipartite_shard  # noqa: E402
+
+
+def t(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    dev = torch.device("cuda")
+    split = (("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2))
+    sh = bipartite_shard(10_000_000, 1_000_000, 500_000_000, 0, 1, dev, split=split)
+    d = 128
+    X = {"user": torch.randn(10_000_000, d, device=dev), "item": torch.randn(1_000_000, d, device=dev)}
+    W = torch.randn(d, d, device=dev) * 0.1
+    for ce, rs in sh.rels.items():
+        n = rs.indptr.numel() - 1
+        deg = (rs.indptr[1:] - rs.indptr[:-1])
+        out = torch.empty(n, d, device=dev)
+        ms = t(lambda: ops.spmm_project(rs.indptr, rs.indices, X[ce[0]], X[ce[2]][:n], W, W,
+                                        "mean", None, relu=True, l2norm=True, out=out))
+        ms2 = t(lambda: ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean"))
+        E = int(rs.indptr[-1])
+        print(f"{ce}: rows {n} edges {E} deg max {int(deg.max())} mean {E / n:.1f} "
+              f"fused {ms:.2f} ms ({E * 516 / ms / 1e9:.2f} TB/s) spmm {ms2:.2f} ms "
+              f"split_plan {'yes' if ops.split_plan(rs.indptr) is not None else 'no'}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
