@@ -243,6 +243,12 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
         if accum != "store":
             raise ValueError("accumulating spmm_project needs an out tensor")
         out = torch.empty((n_dst, D), dtype=torch.float32, device=X.device)
+    else:
+        _dev(out, "out", torch.float32)
+        if tuple(out.shape) != (n_dst, D):
+            raise ValueError(f"out must be [{n_dst}, {D}], got {tuple(out.shape)}")
+    if tuple(W_self.shape) != (D, D) or tuple(W_neigh.shape) != (D, D):
+        raise ValueError(f"spmm_project needs {D}x{D} weights")
     WsT = W_self.detach().t().contiguous()
     WnT = W_neigh.detach().t().contiguous()
     for t, name in ((bias, "bias"), (bias_nonempty, "bias_nonempty")):
