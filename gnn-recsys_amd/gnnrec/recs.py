@@ -140,3 +140,22 @@ def get_metrics_at_k(h, g, model, embed_dim, ground_truth, bought_eids, k,
     recs = get_recs(g, h, model, embed_dim, k, user_ids, already_bought_dict,
                     remove_already_bought, cuda, device, pred, use_popularity, weight_popularity)
     return recs_to_metrics(recs, ground_truth_dict, g)
+
+
+def MRR_neg_edges(model, blocks, pos_g, neg_g, etype, neg_sample_size):
+    """Mean reciprocal rank of each positive edge among its negatives (reference
+    src/metrics.py:137-157, marked "currently not used" there).  The reference passes
+    `etype` where ConvModel.forward expects `embedding_layer` and reshapes the per-etype
+    score dict directly; here the model runs with its own embedding_layer setting and the
+    scores of `etype` are ranked: rank = #{neg >= pos} + 1 over the positive's
+    neg_sample_size negatives (negatives grouped [E_pos, K], sampling.py:163-165)."""
+    input_features = blocks[0].srcdata['features']
+    with torch.no_grad():
+        _, pos_score, neg_score = model(blocks, input_features, pos_g, neg_g,
+                                        getattr(model, 'embedding_layer', True))
+    if isinstance(pos_score, dict):
+        ce = next(c for c in pos_score if etype in (c, c[1]))
+        pos_score, neg_score = pos_score[ce], neg_score[ce]
+    neg = neg_score.reshape(-1, neg_sample_size)
+    rankings = torch.sum(neg >= pos_score.reshape(-1, 1), dim=1) + 1
+    return float(np.mean(1.0 / rankings.cpu().numpy()))

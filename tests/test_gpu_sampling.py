@@ -229,3 +229,23 @@ def test_autograd_matches_torch_reference():
             continue
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=2e-4, atol=2e-5,
                                    err_msg=name)
+
+
+def test_mrr_neg_edges_ranks_positives_among_their_negatives():
+    from gnnrec.recs import MRR_neg_edges
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    g, _ = _graph()
+    model = _model(g, "mean", "sum", emb=True).eval()
+    K = 7
+    loader = EdgeDataLoader(g, {("user", "buys", "item"): torch.arange(40)},
+                            MultiLayerNeighborSampler([3, 3], seed=3),
+                            negative_sampler=negative_sampler.Uniform(K), batch_size=40)
+    _, pos_g, neg_g, blocks = next(iter(loader))
+    mrr = MRR_neg_edges(model, blocks, pos_g, neg_g, "buys", K)
+    with torch.no_grad():
+        _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+    ce = ("user", "buys", "item")
+    p = ps[ce].reshape(-1, 1).cpu().numpy()
+    n = ns[ce].reshape(-1, K).cpu().numpy()
+    ref = np.mean(1.0 / ((n >= p).sum(1) + 1))
+    assert 0 < mrr <= 1 and abs(mrr - ref) < 1e-12
