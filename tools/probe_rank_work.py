@@ -1,0 +1,75 @@
+"""Per-rank compute of the sharded C4 pass at P ranks, measured on one GPU.
+
+Builds rank 0's shard of the P-way partition (its users' edges, the replicated item
+table) and runs ShardedFullGraphPass with an exchange that reports world size P but
+moves nothing (reduce-scatter = slice of the local partial, all-gather = local copy).
+The time is what one rank computes per pass; the collectives come on top (overlapped
+with the local aggregation in the real run).
+
+    python tools/probe_rank_work.py [P ...]
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gnn-recsys_amd"))
+import torch  # noqa: E402
+
+from gnnrec import nn as gnn  # noqa: E402
+from gnnrec.inference import ShardedFullGraphPass  # noqa: E402
+from gnnrec.synth import GraphMeta, bipartite_shard, node_features  # noqa: E402
+
+
+class LocalExchange:
+    """World size P, rank 0, no data movement (compute-only timing)."""
+
+    def __init__(self, ws):
+        self.ws, self.rk, self.backend = ws, 0, None
+
+    def reduce_scatter_rows(self, full, op, async_op=False):
+        S = full.shape[0] // self.ws
+        return full[:S], None
+
+    def all_gather_rows(self, own, out, async_op=False):
+        out[: own.shape[0]].copy_(own)
+        return out, None
+
+    def all_reduce_(self, t, op="sum"):
+        return t
+
+    def max_scalar(self, x, device):
+        return x
+
+
+def main():
+    ps = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+    dev = torch.device("cuda")
+    n_u, n_i, E, d = 10_000_000, 1_000_000, 500_000_000, 128
+    res = {}
+    for P in ps:
+        sh = bipartite_shard(n_u, n_i, E, 0, P, dev)
+        feats = sh.local_features({"user": node_features(n_u, d, 0, dev),
+                                   "item": node_features(n_i, d, 1, dev)})
+        torch.manual_seed(0)
+        meta = GraphMeta(sh.canonical_etypes, ["item", "user"])
+        model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
+                              "mean", "cos", "sum", True).to(dev).eval()
+        runner = ShardedFullGraphPass(model, sh, LocalExchange(P))
+        for _ in range(2):
+            runner.run(feats)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(3):
+            runner.run(feats)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / 3 * 1e3
+        res[f"P={P}"] = {"rank0_compute_ms": ms, "local_edges": sh.local_edge_count(),
+                         "fused": sorted(ce[1] for ce in runner.fused)}
+        print(json.dumps(res), flush=True)
+        del sh, feats, runner, model
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
