@@ -31,7 +31,7 @@ import torch
 
 from . import _lib, ops
 from .dist import Exchange, even_ranges, padded_shard
-from .graph import HeteroGraph, RelGraph, build_csr
+from .graph import HeteroGraph, build_csr
 
 
 # --------------------------------------------------------- single process ---
