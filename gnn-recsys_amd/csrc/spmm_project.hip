@@ -20,6 +20,7 @@
 // ds_read_b64) + per wave ROWS × (agg, self) row slots read back as broadcasts.
 #include "common.hpp"
 #include "gather.hpp"
+#include <cstdlib>
 
 namespace gnnrec {
 namespace {
@@ -28,7 +29,7 @@ constexpr int kPD = 128;       // d_neigh = d_self = N
 constexpr int kPWaves = 16;    // waves per block (one persistent block per CU)
 constexpr int kPRows = 2;      // rows per wave per iteration (halves the LDS weight reads)
 
-template <int REDUCE, bool WEIGHTED>
+template <int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx,
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   }
   __syncthreads();
 
-  constexpr int LPR = 32, VEC = 4, UNROLL = 4;
+  constexpr int LPR = 32, VEC = 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane / LPR;
   const int col = (lane % LPR) * VEC;
@@ -202,10 +203,20 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   if (blocks > g_num_cus) blocks = g_num_cus;
   const dim3 grid((unsigned)blocks), block(kPWaves * 64);
   hipStream_t s = as_stream(stream);
-#define GNNREC_SPP(R, W)                                                                     \
-  hipLaunchKernelGGL((spmm_project_kernel<R, W>), grid, block, 0, s, indptr, indices, ew, X, \
-                     ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum,  \
+  static const int unroll = [] {  // gather wave-instructions in flight per lane (tuning knob)
+    const char* e = getenv("GNNREC_SPP_UNROLL");
+    return e ? atoi(e) : 4;
+  }();
+#define GNNREC_SPP_ONE(R, W, U)                                                              \
+  hipLaunchKernelGGL((spmm_project_kernel<R, W, U>), grid, block, 0, s, indptr, indices, ew, X, \
+                     ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum, \
                      out_div, out, ldo)
+#define GNNREC_SPP(R, W)                                  \
+  do {                                                    \
+    if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \
+    else if (unroll == 2) GNNREC_SPP_ONE(R, W, 2);        \
+    else GNNREC_SPP_ONE(R, W, 4);                         \
+  } while (0)
   if (ew) {
     if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPP(GNNREC_REDUCE_SUM, true);
     else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPP(GNNREC_REDUCE_MEAN, true);
@@ -216,5 +227,6 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
     else GNNREC_SPP(GNNREC_REDUCE_MAX, false);
   }
 #undef GNNREC_SPP
+#undef GNNREC_SPP_ONE
   return check_launch("gnnrec_spmm_project_f32");
 }
