@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--aggregator", default="mean")
     ap.add_argument("--config", choices=["c4", "c5"], default="c4",
                     help="c5: the C4 graph split 80%% clicks / 20%% buys -> 4 relations")
-    ap.add_argument("--hetero", choices=["sum", "mean", "max"], default="sum")
+    ap.add_argument("--hetero", choices=["sum", "mean", "max", "attention"], default="sum")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-scale", type=float, default=0.1,

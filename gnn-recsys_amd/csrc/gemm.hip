@@ -45,6 +45,7 @@ struct GemmArgs {
   const float* bias;
   int64_t M; int64_t N;
   int epilogue; int accum; float out_div;
+  const float* attn_vec; float* attn_state;
   float* out; int64_t ldo;
   int vecA1, vecA2, vecW1, vecW2, vecO;
 };
@@ -105,9 +106,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   constexpr int SC = stage_cols<BN>();
   constexpr int OSTR = SC + 4;
   constexpr int TPR = SC / 32;  // accumulator tiles per staging round
-  const bool staged = g.vecO;
+  const bool attn = g.accum >= GNNREC_ACC_ATTN_FIRST;
+  const bool staged = g.vecO && !attn;
   float* Ot = smem + wave * 32 * OSTR;
   float z[16][NT];
+  float a_t[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) a_t[t] = (attn && colok[t]) ? g.attn_vec[n0 + t * 32 + r] : 0.f;
+  float keep[16], norm[16];  // attention: weight of the running out, 1 / running sum
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
     float ss = 0.f;
@@ -128,6 +134,29 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
 #pragma unroll
       for (int t = 0; t < NT; ++t) z[v][t] = z[v][t] / nrm;
     }
+    keep[v] = 0.f;
+    norm[v] = 1.f;
+    if (attn) {  // online softmax over relations: score e = a . z(row)
+      float e = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) e += z[v][t] * a_t[t];
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) e += __shfl_xor(e, off);
+      const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      float mnew = e, snew = 1.f, cnew = 1.f;
+      if (row < g.M && g.accum != GNNREC_ACC_ATTN_FIRST) {
+        const float2 st = reinterpret_cast<const float2*>(g.attn_state)[row];
+        mnew = fmaxf(st.x, e);
+        keep[v] = expf(st.x - mnew);
+        cnew = expf(e - mnew);
+        snew = st.y * keep[v] + cnew;
+      }
+      if (g.accum == GNNREC_ACC_ATTN_LAST) norm[v] = 1.f / snew;
+      if (row < g.M && r == 0)
+        reinterpret_cast<float2*>(g.attn_state)[row] = make_float2(mnew, snew);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) z[v][t] *= cnew;
+    }
   }
   if (!staged) {
 #pragma unroll
@@ -142,6 +171,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
         float y = z[v][t];
         if (g.accum == GNNREC_ACC_ADD) y = *p + y;
         else if (g.accum == GNNREC_ACC_MAX) y = fmaxf(*p, y);
+        else if (attn) {
+          if (g.accum != GNNREC_ACC_ATTN_FIRST) y = *p * keep[v] + y;
+          y = y * norm[v];
+        }
         if (g.out_div > 0.f) y = y / g.out_div;
         *p = y;
       }
@@ -459,7 +492,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
 extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                                const float* A2, int64_t lda2, int64_t K2, const float* W2,
                                const int32_t* a2_deg, int a2_mode, const float* bias, int64_t M,
-                               int64_t N, int epilogue, int accum, float out_div, float* out,
+                               int64_t N, int epilogue, int accum, float out_div,
+                               const float* attn_vec, float* attn_state, float* out,
                                int64_t ldo, void* stream) {
   using namespace gnnrec;
   GNNREC_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "gnnrec_gemm_f32: negative size");
@@ -469,8 +503,11 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   GNNREC_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2), "gnnrec_gemm_f32: bad A2/W2");
   GNNREC_REQUIRE(a2_mode == GNNREC_A2_NONE || a2_deg != nullptr,
                  "gnnrec_gemm_f32: a2_mode needs a2_deg");
-  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_MAX,
+  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_ATTN_LAST,
                  "gnnrec_gemm_f32: unknown accumulate mode %d", accum);
+  const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
+  GNNREC_REQUIRE(!attn || (attn_vec && attn_state && N <= 256),
+                 "gnnrec_gemm_f32: attention accumulation needs attn_vec, attn_state, N <= 256");
   GNNREC_REQUIRE(!(epilogue & GNNREC_EPI_L2NORM) || N <= 256,
                  "gnnrec_gemm_f32: L2NORM needs N <= 256 (got %lld)", (long long)N);
   GemmArgs g;
@@ -478,6 +515,7 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   g.A2 = A2; g.lda2 = lda2; g.K2 = K2; g.W2 = W2;
   g.a2_deg = a2_deg; g.a2_mode = a2_mode; g.bias = bias;
   g.M = M; g.N = N; g.epilogue = epilogue; g.accum = accum; g.out_div = out_div;
+  g.attn_vec = attn_vec; g.attn_state = attn_state;
   g.out = out; g.ldo = ldo;
   g.vecA1 = (K1 % 4 == 0) && (lda1 % 4 == 0) && aligned16(A1);
   g.vecA2 = (K2 % 4 == 0) && (lda2 % 4 == 0) && aligned16(A2);
@@ -490,7 +528,7 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   if (N <= 128) return launch_gemm<128>(g, s);
   // wider outputs: 128-column blocks (two waves per SIMD) unless the row norm needs the
   // whole row in one block (the 256-column tile runs at one wave per SIMD)
-  if (!(epilogue & GNNREC_EPI_L2NORM) && getenv("GNNREC_GEMM_BN256") == nullptr)
+  if (!(epilogue & GNNREC_EPI_L2NORM) && !attn && getenv("GNNREC_GEMM_BN256") == nullptr)
     return launch_gemm<128>(g, s);
   return launch_gemm<256>(g, s);
 }

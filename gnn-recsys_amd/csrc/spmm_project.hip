@@ -36,6 +36,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const float* __restrict__ H, int64_t ldh, const float* __restrict__ WsT,
     const float* __restrict__ WnT, const float* __restrict__ bias,
     const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
+    const float* __restrict__ attn_vec, float* __restrict__ attn_state,
     float* __restrict__ out, int64_t ldo) {
   __shared__ float Ws[kPD * kPD];
   __shared__ float Wn[kPD * kPD];
@@ -57,6 +58,8 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   const int64_t stride = (int64_t)gridDim.x * kPWaves * kPRows;
   const float b0 = bias ? bias[j0] : 0.f, b1 = bias ? bias[j0 + 1] : 0.f;
   const float c0 = bias_ne ? bias_ne[j0] : 0.f, c1 = bias_ne ? bias_ne[j0 + 1] : 0.f;
+  const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
+  const float a0 = attn ? attn_vec[j0] : 0.f, a1 = attn ? attn_vec[j0 + 1] : 0.f;
 
   for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
        row0 += stride) {
@@ -140,9 +143,36 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
         y0 = y0 / nrm;
         y1 = y1 / nrm;
       }
+      float keep = 0.f, nrm_attn = 1.f;
+      if (attn) {  // online softmax over relations, score e = a . y (row-uniform)
+        float e = y0 * a0 + y1 * a1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) e += __shfl_xor(e, off);
+        float mnew = e, snew = 1.f, cnew = 1.f;
+        if (row < n_dst && accum != GNNREC_ACC_ATTN_FIRST) {
+          const float2 st = reinterpret_cast<const float2*>(attn_state)[row];
+          mnew = fmaxf(st.x, e);
+          keep = expf(st.x - mnew);
+          cnew = expf(e - mnew);
+          snew = st.y * keep + cnew;
+        }
+        if (accum == GNNREC_ACC_ATTN_LAST) nrm_attn = 1.f / snew;
+        if (row < n_dst && lane == 0)
+          reinterpret_cast<float2*>(attn_state)[row] = make_float2(mnew, snew);
+        y0 *= cnew;
+        y1 *= cnew;
+      }
       if (row >= n_dst) continue;
       float2* p = reinterpret_cast<float2*>(out + row * ldo + j0);
-      if (accum != GNNREC_ACC_STORE) {
+      if (attn) {
+        if (accum != GNNREC_ACC_ATTN_FIRST) {
+          const float2 o = *p;
+          y0 = o.x * keep + y0;
+          y1 = o.y * keep + y1;
+        }
+        y0 *= nrm_attn;
+        y1 *= nrm_attn;
+      } else if (accum != GNNREC_ACC_STORE) {
         const float2 o = *p;
         if (accum == GNNREC_ACC_ADD) {
           y0 = o.x + y0;
@@ -174,7 +204,8 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
                                        const float* W_neighT, const float* bias,
                                        const float* bias_nonempty, int64_t n_dst, int64_t d,
                                        int reduce, int epilogue, int accum, float out_div,
-                                       float* out, int64_t ldo, void* stream) {
+                                       const float* attn_vec, float* attn_state, float* out,
+                                       int64_t ldo, void* stream) {
   GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project_f32: only d = %d (got %lld)", kPD,
                  (long long)d);
   GNNREC_REQUIRE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN ||
@@ -182,8 +213,10 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
                  "gnnrec_spmm_project_f32: unknown reduce %d", reduce);
   GNNREC_REQUIRE((epilogue & ~(GNNREC_EPI_RELU | GNNREC_EPI_L2NORM)) == 0,
                  "gnnrec_spmm_project_f32: epilogue must be RELU|L2NORM");
-  GNNREC_REQUIRE(accum == GNNREC_ACC_STORE || accum == GNNREC_ACC_ADD || accum == GNNREC_ACC_MAX,
+  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_ATTN_LAST,
                  "gnnrec_spmm_project_f32: unknown accumulate mode %d", accum);
+  GNNREC_REQUIRE(accum < GNNREC_ACC_ATTN_FIRST || (attn_vec && attn_state),
+                 "gnnrec_spmm_project_f32: attention accumulation needs attn_vec, attn_state");
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
   GNNREC_REQUIRE(indptr && X && H && W_selfT && W_neighT && out,
@@ -210,7 +243,7 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
 #define GNNREC_SPP_ONE(R, W, U)                                                              \
   hipLaunchKernelGGL((spmm_project_kernel<R, W, U>), grid, block, 0, s, indptr, indices, ew, X, \
                      ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum, \
-                     out_div, out, ldo)
+                     out_div, attn_vec, attn_state, out, ldo)
 #define GNNREC_SPP(R, W)                                  \
   do {                                                    \
     if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \

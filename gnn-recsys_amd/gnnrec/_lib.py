@@ -24,6 +24,7 @@ REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 SPMM_EMPTY_NEGINF = 1
 EPI_RELU, EPI_L2NORM, EPI_SIGMOID = 1, 2, 4
 ACC_STORE, ACC_ADD, ACC_MAX = 0, 1, 2
+ACC_ATTN_FIRST, ACC_ATTN, ACC_ATTN_LAST = 3, 4, 5
 A2_NONE, A2_DIV_DEG, A2_ZERO_DEG = 0, 1, 2
 
 
@@ -47,7 +48,7 @@ SIGNATURES = {
     "gnnrec_spmm_backward_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _I64, _I64,
                                         _INT, _P, _I64, _P]),
     "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P,
-                               _I64, _I64, _INT, _INT, _F32, _P, _I64, _P]),
+                               _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
@@ -58,7 +59,7 @@ SIGNATURES = {
     "gnnrec_lstm_step_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P,
                                     _I64, _P]),
     "gnnrec_spmm_project_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,
-                                       _INT, _INT, _INT, _F32, _P, _I64, _P]),
+                                       _INT, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_gather_rows": (_INT, [_P, _I64, _P, _I64, _I64, _P, _I64, _P]),
     "gnnrec_act_backward_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _INT, _P, _I64, _P]),
     "gnnrec_exclusive_scan_i64": (_INT, [_P, _I64, _P, _P, _P]),

@@ -323,6 +323,15 @@ class ShardedFullGraphPass:
             Wn, bias_ne = Wn @ We, Wn @ be
         return Ws, Wn, bias, bias_ne
 
+    @staticmethod
+    def _attn(hconv, T, n_rows, device):
+        """kwargs of the attention accumulate modes for dst type T (empty otherwise): the
+        type's attention vector and a fresh per-row (running max, running sum) state."""
+        if hconv.aggregate != 'attention':
+            return {}
+        return {'attn_vec': hconv.attn[T],
+                'attn_state': torch.empty((n_rows, 2), dtype=torch.float32, device=device)}
+
     def _active(self, hconv, h):
         active: Dict[str, list] = {}
         for ce in self.shard.canonical_etypes:
@@ -377,7 +386,6 @@ class ShardedFullGraphPass:
     def _local(self, hconv, h, active, out):
         """item->user style relations: dst rows owned here; GEMMs on the side stream."""
         sh, O = self.shard, self.ops
-        agg = hconv.aggregate
         T = sh.ptype
         ces = active.get(T, [])
         if not ces:
@@ -395,8 +403,7 @@ class ShardedFullGraphPass:
             preagg, weighted, reduce = mod._plan_rel(ce)
             rs = sh.rels[ce]
             msg = self._message(mod, ce, h, preagg)
-            acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
-            div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+            acc, div = hconv.accum_mode(j, R)
             if reduce != 'lstm' and can_fuse is not None and can_fuse(
                     rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight):
                 # aggregation and projection in one launch on the main stream: the self rows
@@ -408,12 +415,13 @@ class ShardedFullGraphPass:
                 if o is None:
                     o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
                                     device=msg.device)
+                    akw = self._attn(hconv, T, sh.n_own, o.device)
                 Ws, Wn, bias, bias_ne = self._folded(mod, ce)
                 with self._time('spmm'):
                     O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                    rs.weights if weighted else None, relu=True,
                                    l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
-                                   bias=bias, bias_nonempty=bias_ne)
+                                   bias=bias, bias_nonempty=bias_ne, **akw)
                 self.fused.add(ce)
                 continue
             with self._time('spmm'):
@@ -422,11 +430,12 @@ class ShardedFullGraphPass:
                             edge_weight=rs.weights if weighted else None))
             if o is None:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
+                akw = self._attn(hconv, T, sh.n_own, o.device)
 
-            def proj(mod=mod, a=a, acc=acc, div=div, o=o):
+            def proj(mod=mod, a=a, acc=acc, div=div, o=o, akw=akw):
                 O.gemm(self_rows, mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
-                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o)
-            ev = self._on_side(proj, self_rows, a, o)
+                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o, **akw)
+            ev = self._on_side(proj, self_rows, a, o, *akw.values())
         out[T] = o
         if ev is not None:
             self._ready[id(o)] = ev
@@ -434,17 +443,16 @@ class ShardedFullGraphPass:
     def _owned(self, hconv, h, active, partials, out):
         """owners project their replicated rows, then all-gather the table."""
         sh, O = self.shard, self.ops
-        agg = hconv.aggregate
         for T, ces in active.items():
             if T == sh.ptype:
                 continue
             R = len(ces)
             o = None
             self_rows = self._get(h, T)[sh.own_slice(T)]
+            akw = self._attn(hconv, T, self_rows.shape[0], self_rows.device)
             for j, ce in enumerate(ces):
                 mod = hconv.mods[ce[1]]
-                acc = 'store' if j == 0 else ('max' if agg == 'max' else 'add')
-                div = float(R) if (agg == 'mean' and j == R - 1 and R > 1) else 0.0
+                acc, div = hconv.accum_mode(j, R)
                 if isinstance(partials[ce][0], str):  # ('fused', msg, reduce, weighted)
                     _, msg, reduce, weighted = partials[ce]
                     rs = sh.rels[ce]
@@ -456,7 +464,7 @@ class ShardedFullGraphPass:
                         O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                        rs.weights if weighted else None, relu=True,
                                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
-                                       bias=bias, bias_nonempty=bias_ne)
+                                       bias=bias, bias_nonempty=bias_ne, **akw)
                     self.fused.add(ce)
                     continue
                 own, work, reduce = partials[ce]
@@ -469,7 +477,8 @@ class ShardedFullGraphPass:
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                        a2_deg=sh.rels[ce].deg_own,
                        a2_mode=(_lib.A2_NONE if reduce == 'lstm' else
-                                _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG))
+                                _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG),
+                       **akw)
             if self.ex.ws == 1:  # the owned rows ARE the table
                 out[T] = o
                 continue

@@ -125,7 +125,9 @@ class ConvLayer(nn.Module):
         """Reference ConvLayer.forward(graph, (h_neigh, h_self)) -> z [n_dst, out_feats]."""
         return self._run(graph, x, None, 'store', 0.0)
 
-    def _run(self, graph, x, out, accum: str, out_div: float):
+    def _run(self, graph, x, out, accum: str, out_div: float, attn=None):
+        """attn: (attn_vec, attn_state) for the attention accumulate modes."""
+        av, ast = attn if attn is not None else (None, None)
         h_neigh, h_self = x
         preagg, weighted, reduce = self._plan(graph)
         if self.training and self.dropout_fn.p > 0:
@@ -150,10 +152,11 @@ class ConvLayer(nn.Module):
             return ops.spmm_project(graph.indptr, graph.indices, m, h_self, self.fc_self.weight,
                                     self.fc_neigh.weight, reduce, ew, relu=True,
                                     l2norm=bool(self.norm), accum=accum, out_div=out_div,
-                                    out=out)
+                                    out=out, attn_vec=av, attn_state=ast)
         agg = self.aggregate(graph.indptr, graph.indices, m, reduce, ew)
         return ops.gemm(h_self, self.fc_self.weight, agg, self.fc_neigh.weight, relu=True,
-                        l2norm=bool(self.norm), accum=accum, out_div=out_div, out=out)
+                        l2norm=bool(self.norm), accum=accum, out_div=out_div, out=out,
+                        attn_vec=av, attn_state=ast)
 
 
 class HeteroGraphConv(nn.Module):
@@ -162,14 +165,35 @@ class HeteroGraphConv(nn.Module):
     Relations with zero edges in `g`, or whose src / dst type has no input, are
     skipped; the outputs of the active relations are reduced per dst type with
     sum / mean / max.  Modules live in an nn.ModuleDict keyed by relation name,
-    so state_dict keys are `mods.{rel}.*` exactly as in the reference."""
+    so state_dict keys are `mods.{rel}.*` exactly as in the reference.
 
-    def __init__(self, mods: Dict[str, nn.Module], aggregate: str = 'sum'):
+    aggregate='attention' (build-defined, for BASELINE config C5 — the reference offers
+    only sum/mean/max, main.py:486): per dst node, a softmax over its active relations
+    of a_Tᵀ z_r weighs the relation outputs z_r; one learnable vector a_T per dst type
+    (`attn.{ntype}`, needs attn_dims {ntype: out_feats}).  In inference the softmax is
+    accumulated online across the relation launches (running max and sum per row)."""
+
+    def __init__(self, mods: Dict[str, nn.Module], aggregate: str = 'sum',
+                 attn_dims: Dict[str, int] = None):
         super().__init__()
         self.mods = nn.ModuleDict(mods)
-        if aggregate not in ('sum', 'mean', 'max'):
+        if aggregate not in ('sum', 'mean', 'max', 'attention'):
             raise KeyError('Invalid cross type reducer: {}'.format(aggregate))
         self.aggregate = aggregate
+        self.attn = None
+        if aggregate == 'attention':
+            if not attn_dims:
+                raise ValueError("aggregate='attention' needs attn_dims {dst ntype: out_feats}")
+            self.attn = nn.ParameterDict({nt: nn.Parameter(torch.randn(d) / d ** 0.5)
+                                          for nt, d in attn_dims.items()})
+
+    def accum_mode(self, j: int, R: int):
+        """(accumulate mode, out_div) of the j-th of R active relations into one dst type."""
+        if self.aggregate == 'attention':
+            return ('attn_first' if j == 0 else 'attn_last' if j == R - 1 else 'attn'), 0.0
+        acc = 'store' if j == 0 else ('max' if self.aggregate == 'max' else 'add')
+        div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
+        return acc, div
 
     def forward(self, g, inputs):
         if isinstance(inputs, tuple):
@@ -194,6 +218,10 @@ class HeteroGraphConv(nn.Module):
                 outs = [self.mods[ce[1]](g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype]))
                         for ce in ces]
                 st = torch.stack(outs, 0)
+                if self.aggregate == 'attention':
+                    w = torch.softmax((st * self.attn[dtype]).sum(-1), dim=0)  # [R, n_dst]
+                    rsts[dtype] = (w.unsqueeze(-1) * st).sum(0)
+                    continue
                 rsts[dtype] = (st.sum(0) if self.aggregate == 'sum' else
                                st.mean(0) if self.aggregate == 'mean' else st.max(0)[0])
                 continue
@@ -202,11 +230,14 @@ class HeteroGraphConv(nn.Module):
             out = torch.empty((n_dst, out_feats), dtype=torch.float32,
                               device=dst_inputs[dtype].device)
             R = len(ces)
+            attn = None
+            if self.aggregate == 'attention':
+                attn = (self.attn[dtype], torch.empty((n_dst, 2), dtype=torch.float32,
+                                                      device=out.device))
             for j, ce in enumerate(ces):
-                accum = 'store' if j == 0 else ('max' if self.aggregate == 'max' else 'add')
-                div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
+                accum, div = self.accum_mode(j, R)
                 self.mods[ce[1]]._run(g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype]),
-                                      out, accum, div)
+                                      out, accum, div, attn)
             rsts[dtype] = out
         return rsts
 
@@ -311,20 +342,28 @@ class ConvModel(nn.Module):
             if 'sport' in g.ntypes:
                 self.sport_embed = NodeEmbedding(dim_dict['sport'], dim_dict['hidden'])
         self.layers = nn.ModuleList()
+
+        def attn_dims(d):  # every ConvLayer of a layer has the same out_feats
+            if aggregator_hetero != 'attention':
+                return None
+            return {etype[2]: d for etype in g.canonical_etypes}
         if not embedding_layer:
             self.layers.append(HeteroGraphConv(
                 {etype[1]: ConvLayer((dim_dict[etype[0]], dim_dict[etype[2]]), dim_dict['hidden'],
                                      dropout, aggregator_type, norm)
-                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero,
+                attn_dims=attn_dims(dim_dict['hidden'])))
         for _ in range(n_layers - 2):
             self.layers.append(HeteroGraphConv(
                 {etype[1]: ConvLayer((dim_dict['hidden'], dim_dict['hidden']), dim_dict['hidden'],
                                      dropout, aggregator_type, norm)
-                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+                 for etype in g.canonical_etypes}, aggregate=aggregator_hetero,
+                attn_dims=attn_dims(dim_dict['hidden'])))
         self.layers.append(HeteroGraphConv(
             {etype[1]: ConvLayer((dim_dict['hidden'], dim_dict['hidden']), dim_dict['out'],
                                  dropout, aggregator_type, norm)
-             for etype in g.canonical_etypes}, aggregate=aggregator_hetero))
+             for etype in g.canonical_etypes}, aggregate=aggregator_hetero,
+            attn_dims=attn_dims(dim_dict['out'])))
         if pred == 'cos':
             self.pred_fn = CosinePrediction()
         elif pred == 'nn':

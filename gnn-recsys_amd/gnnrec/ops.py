@@ -17,7 +17,24 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 REDUCE = {"sum": _lib.REDUCE_SUM, "mean": _lib.REDUCE_MEAN, "max": _lib.REDUCE_MAX}
-ACCUM = {"store": _lib.ACC_STORE, "add": _lib.ACC_ADD, "max": _lib.ACC_MAX}
+ACCUM = {"store": _lib.ACC_STORE, "add": _lib.ACC_ADD, "max": _lib.ACC_MAX,
+         "attn_first": _lib.ACC_ATTN_FIRST, "attn": _lib.ACC_ATTN,
+         "attn_last": _lib.ACC_ATTN_LAST}
+
+
+def _attn_args(accum, attn_vec, attn_state, n_rows, n_cols):
+    """Validated (attn_vec, attn_state) for the attention accumulate modes, else (None, None)."""
+    if not accum.startswith("attn"):
+        return None, None
+    if attn_vec is None or attn_state is None:
+        raise ValueError(f"accum={accum!r} needs attn_vec and attn_state")
+    _dev(attn_vec, "attn_vec", torch.float32)
+    _dev(attn_state, "attn_state", torch.float32)
+    if attn_vec.numel() != n_cols or tuple(attn_state.shape) != (n_rows, 2) or \
+            not attn_state.is_contiguous():
+        raise ValueError(f"attention needs attn_vec [{n_cols}] and a contiguous attn_state "
+                         f"[{n_rows}, 2]")
+    return attn_vec.detach().contiguous(), attn_state
 
 
 def _dev(t: torch.Tensor, name: str, dtype=None) -> None:
@@ -134,7 +151,9 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
          W2: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None, *,
          relu: bool = False, l2norm: bool = False, sigmoid: bool = False,
          accum: str = "store", out_div: float = 0.0, out: Optional[torch.Tensor] = None,
-         a2_deg: Optional[torch.Tensor] = None, a2_mode: int = _lib.A2_NONE) -> torch.Tensor:
+         a2_deg: Optional[torch.Tensor] = None, a2_mode: int = _lib.A2_NONE,
+         attn_vec: Optional[torch.Tensor] = None,
+         attn_state: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias).  W are nn.Linear weights [N, K]."""
     lib = _lib.load()
     _dev(A1, "A1", torch.float32)
@@ -162,7 +181,7 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0) | (
         _lib.EPI_SIGMOID if sigmoid else 0)
     if out is None:
-        if accum != "store":
+        if accum not in ("store", "attn_first"):
             raise ValueError("accumulating gemm needs an out tensor")
         out = torch.empty((M, N), dtype=torch.float32, device=A1.device)
     else:
@@ -170,9 +189,10 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
         if tuple(out.shape) != (M, N):
             raise ValueError(f"out must be [{M}, {N}]")
     ldo = _rowmajor(out, "out")
+    av, ast = _attn_args(accum, attn_vec, attn_state, M, N)
     rc = lib.gnnrec_gemm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2), ptr(a2_deg),
-                             a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div), ptr(out),
-                             ldo, stream_ptr(A1.device))
+                             a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div),
+                             ptr(av), ptr(ast), ptr(out), ldo, stream_ptr(A1.device))
     check(rc, "gnnrec_gemm_f32")
     return out
 
@@ -224,7 +244,9 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                  edge_weight: Optional[torch.Tensor] = None, relu: bool = True,
                  l2norm: bool = False, accum: str = "store", out_div: float = 0.0,
                  out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
-                 bias_nonempty: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 bias_nonempty: Optional[torch.Tensor] = None,
+                 attn_vec: Optional[torch.Tensor] = None,
+                 attn_state: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ + bias
     + [deg > 0]·bias_nonempty), d = 128."""
     lib = _lib.load()
@@ -240,7 +262,7 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
         edge_weight = edge_weight.contiguous()
     D = FUSED_D
     if out is None:
-        if accum != "store":
+        if accum not in ("store", "attn_first"):
             raise ValueError("accumulating spmm_project needs an out tensor")
         out = torch.empty((n_dst, D), dtype=torch.float32, device=X.device)
     else:
@@ -258,12 +280,13 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                 raise ValueError(f"{name} must have {D} entries")
     bias = None if bias is None else bias.detach().contiguous()
     bias_nonempty = None if bias_nonempty is None else bias_nonempty.detach().contiguous()
+    av, ast = _attn_args(accum, attn_vec, attn_state, n_dst, D)
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
     check(lib.gnnrec_spmm_project_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
                                       _rowmajor(X, "X"), ptr(H), _rowmajor(H, "H"), ptr(WsT),
                                       ptr(WnT), ptr(bias), ptr(bias_nonempty), n_dst,
                                       X.shape[1], REDUCE[reduce], epi,
-                                      ACCUM[accum], float(out_div), ptr(out),
+                                      ACCUM[accum], float(out_div), ptr(av), ptr(ast), ptr(out),
                                       _rowmajor(out, "out"), stream_ptr(X.device)),
           "gnnrec_spmm_project_f32")
     return out

@@ -70,6 +70,15 @@ extern "C" {
 #define GNNREC_ACC_STORE 0
 #define GNNREC_ACC_ADD 1
 #define GNNREC_ACC_MAX 2
+/* per-relation attention across relations (build-defined, for C5; not in the reference):
+ * out(v) = sum_r softmax_r(a . z_r(v)) z_r(v), accumulated online over the relation
+ * launches with a per-row (running max, running sum) state [M, 2] floats:
+ * FIRST initialises out/state, ATTN folds in one more relation, ATTN_LAST folds in the
+ * last one and divides by the sum.  Needs attn_vec [N] and attn_state; the row must fit
+ * one block (N <= 256 for gnnrec_gemm_f32). */
+#define GNNREC_ACC_ATTN_FIRST 3
+#define GNNREC_ACC_ATTN 4
+#define GNNREC_ACC_ATTN_LAST 5
 
 /* gnnrec_gemm_f32 row transform applied to A2 rows before the product */
 #define GNNREC_A2_NONE 0
@@ -123,6 +132,7 @@ int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                     const float* A2, int64_t lda2, int64_t K2, const float* W2,
                     const int32_t* a2_deg, int a2_mode, const float* bias,
                     int64_t M, int64_t N, int epilogue, int accum, float out_div,
+                    const float* attn_vec, float* attn_state,
                     float* out, int64_t ldo, void* stream);
 
 /* ---- a1+a3 fused: aggregation with the projection in its epilogue -----------
@@ -142,8 +152,8 @@ int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices, const
                             const float* X, int64_t ldx, const float* H, int64_t ldh,
                             const float* W_selfT, const float* W_neighT, const float* bias,
                             const float* bias_nonempty, int64_t n_dst, int64_t d, int reduce,
-                            int epilogue, int accum, float out_div, float* out, int64_t ldo,
-                            void* stream);
+                            int epilogue, int accum, float out_div, const float* attn_vec,
+                            float* attn_state, float* out, int64_t ldo, void* stream);
 
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >

@@ -227,6 +227,14 @@ def hetero_conv(graph: Graph, h: Dict[str, np.ndarray], layer_w: Dict[str, dict]
             res[nt] = st.mean(0, dtype=np.float32)
         elif aggregator_hetero == "max":
             res[nt] = st.max(0)
+        elif aggregator_hetero == "attention":
+            # build-defined (not in the reference, main.py:486): per dst node a softmax over
+            # its active relations of a_T . z_r weighs the relation outputs
+            a = np.asarray(layer_w["__attn__"][nt], np.float64)
+            e = st.astype(np.float64) @ a                      # [R, n]
+            w = np.exp(e - e.max(0, keepdims=True))
+            w /= w.sum(0, keepdims=True)
+            res[nt] = (w[..., None] * st).sum(0).astype(np.float32)
         else:
             raise KeyError(aggregator_hetero)
     return res
@@ -241,6 +249,8 @@ def split_state_dict(sd: Dict[str, np.ndarray]):
             nt = parts[0][: -len("_embed")]
             e = embed.setdefault(nt, [None, None])
             e[0 if parts[-1] == "weight" else 1] = v
+        elif parts[0] == "layers" and parts[2] == "attn":  # build-defined attention vectors
+            layers.setdefault(int(parts[1]), {}).setdefault("__attn__", {})[parts[3]] = v
         elif parts[0] == "layers":
             i, rel = int(parts[1]), parts[3]
             layers.setdefault(i, {}).setdefault(rel, {})[".".join(parts[4:])] = v

@@ -23,8 +23,27 @@ def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_ne
     return t
 
 
+def _attn_update(out, t, accum, attn_vec, attn_state):
+    """online softmax over relations (the product's ACC_ATTN_* semantics) in numpy."""
+    z = t.numpy().astype(np.float64)
+    e = z @ attn_vec.detach().cpu().numpy().astype(np.float64)
+    if accum == "attn_first":
+        m, ssum, acc = e, np.ones_like(e), z
+    else:
+        st = attn_state.cpu().numpy().astype(np.float64)
+        m = np.maximum(st[:, 0], e)
+        keep, new = np.exp(st[:, 0] - m), np.exp(e - m)
+        ssum = st[:, 1] * keep + new
+        acc = out.cpu().numpy().astype(np.float64) * keep[:, None] + z * new[:, None]
+    if accum == "attn_last":
+        acc = acc / ssum[:, None]
+    attn_state.copy_(torch.from_numpy(np.stack([m, ssum], 1).astype(np.float32)))
+    return torch.from_numpy(acc.astype(np.float32))
+
+
 def gemm(A1, W1, A2=None, W2=None, bias=None, *, relu=False, l2norm=False, sigmoid=False,
-         accum="store", out_div=0.0, out=None, a2_deg=None, a2_mode=0):
+         accum="store", out_div=0.0, out=None, a2_deg=None, a2_mode=0, attn_vec=None,
+         attn_state=None):
     z = oracle.linear(A1.detach().cpu().numpy(), W1.detach().cpu().numpy(),
                       None if bias is None else bias.detach().cpu().numpy())
     if A2 is not None:
@@ -42,6 +61,12 @@ def gemm(A1, W1, A2=None, W2=None, bias=None, *, relu=False, l2norm=False, sigmo
     if l2norm:
         z = oracle.l2_normalize_rows_guarded(z)
     t = torch.from_numpy(np.ascontiguousarray(z, np.float32))
+    if accum.startswith("attn"):
+        t = _attn_update(out, t, accum, attn_vec, attn_state)
+        if out is None:
+            return t
+        out.copy_(t)
+        return out
     if out is None:
         return t
     if accum == "add":

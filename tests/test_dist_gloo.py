@@ -35,7 +35,10 @@ def _worker(rank, world, port, case, q):
         from gnnrec.graph import HeteroGraph
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
 
-        meta = golden_io.manifest()[case]
+        case, _, hetero = case.partition("@")  # "@attention": build-defined hetero mode
+        meta = dict(golden_io.manifest()[case])
+        if hetero:
+            meta["aggregator_hetero"] = hetero
         a = golden_io.load(case)
         num_nodes, edges, occ = golden_io.graph_parts(a)
         g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d)) for ce, (s, d) in
@@ -46,7 +49,9 @@ def _worker(rank, world, port, case, q):
         model = gnn.ConvModel(g, meta["n_layers"], meta["dim_dict"], meta["norm"], 0.0,
                               meta["aggregator_type"], meta["pred"], meta["aggregator_hetero"],
                               meta["embedding_layer"])
-        model.load_state_dict({k: torch.from_numpy(v) for k, v in golden_io.state_dict(a).items()})
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in golden_io.state_dict(a).items()},
+                              strict=not hetero)
+        _set_attention(model)
         model.eval()
         ex = Exchange()
         shard = GraphShard.from_graph(g, rank, world, "user", device="cpu")
@@ -61,6 +66,15 @@ def _worker(rank, world, port, case, q):
         q.put((rank, res, shard.local_edge_count(), shard.global_edge_count()))
     finally:
         dist.destroy_process_group()
+
+
+def _set_attention(model):
+    """Deterministic attention vectors (the goldens have none: the mode is build-defined)."""
+    with torch.no_grad():
+        for i, layer in enumerate(model.layers):
+            if getattr(layer, "attn", None) is not None:
+                for nt, p in layer.attn.items():
+                    p.copy_(torch.linspace(-1.0, 1.0, p.numel()) * (i + 1) * (1 if nt == "user" else -1))
 
 
 def _run(case, world):
@@ -84,14 +98,27 @@ def _run(case, world):
     ("model_het_meanedge_max_emb", 4),
     ("model_het_mean_sum_skip", 2),
     ("model_bip_poolnn_max_noemb_nn", 8),  # 41 users over 8 ranks: ragged and tiny shards
+    ("model_het_meannnedge_mean_emb@attention", 2),
+    ("model_het_mean_sum_skip@attention", 4),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
-    meta = golden_io.manifest()[case]
-    a = golden_io.load(case)
+    name, _, hetero = case.partition("@")
+    meta = dict(golden_io.manifest()[name])
+    a = golden_io.load(name)
     num_nodes, edges, occ = golden_io.graph_parts(a)
     g = oracle.Graph(num_nodes, edges, occ)
     feats = {k[5:]: v for k, v in a.items() if k.startswith("feat/")}
-    ref = oracle.model_full_graph(g, feats, golden_io.state_dict(a), meta["aggregator_type"],
+    sd = golden_io.state_dict(a)
+    if hetero:
+        meta["aggregator_hetero"] = hetero
+        from gnnrec import nn as gnn
+        from gnnrec.synth import GraphMeta
+        m = gnn.ConvModel(GraphMeta(list(edges), sorted(num_nodes)), meta["n_layers"],
+                          meta["dim_dict"], meta["norm"], 0.0, meta["aggregator_type"],
+                          meta["pred"], hetero, meta["embedding_layer"])
+        _set_attention(m)
+        sd = dict(sd, **{k: v.detach().numpy() for k, v in m.state_dict().items() if ".attn." in k})
+    ref = oracle.model_full_graph(g, feats, sd, meta["aggregator_type"],
                                   meta["aggregator_hetero"], meta["norm"], meta["embedding_layer"])
     results = _run(case, world)
     # every rank holds the same replicated tables and the same assembled user table
@@ -103,5 +130,7 @@ def test_sharded_pass_matches_single_process_oracle(case, world):
     # edges are partitioned: every edge aggregated by exactly one rank
     assert sum(r[2] for r in results) == results[0][3]
     # and the golden (the reference's own output) agrees too
+    if hetero:
+        return  # attention is build-defined: no reference output to compare with
     for nt in ref:
         np.testing.assert_allclose(results[0][1][nt], a["h/" + nt], rtol=1e-5, atol=1e-5)
