@@ -24,12 +24,16 @@ def _build(agg, hetero, d=32):
     n_u, n_i, E = 3000, 700, (40000 if d == 32 else 100000)  # d=128: >= 24 edges/row, fused
     u = rng.integers(0, n_u, E)
     i = rng.integers(0, n_i, E)
-    g = HeteroGraph({("user", "buys", "item"): (torch.from_numpy(u), torch.from_numpy(i)),
-                     ("item", "bought-by", "user"): (torch.from_numpy(i), torch.from_numpy(u))},
+    rels = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
+    if hetero == "attention":  # a second relation per dst type (sparser: the GEMM path)
+        Ec = E // 3
+        uc, ic = rng.integers(0, n_u, Ec), rng.integers(0, n_i, Ec)
+        rels[("user", "clicks", "item")] = (uc, ic)
+        rels[("item", "clicked-by", "user")] = (ic, uc)
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in rels.items()},
                     {"user": n_u, "item": n_i}, device="cuda")
-    occ = torch.from_numpy(rng.integers(1, 9, E)).cuda()
-    g.edges["buys"].data["occurrence"] = occ
-    g.edges["bought-by"].data["occurrence"] = occ
+    for ce, (s, _) in rels.items():
+        g.edges[ce].data["occurrence"] = torch.from_numpy(rng.integers(1, 9, s.size)).cuda()
     feats = {"user": torch.from_numpy(rng.standard_normal((n_u, d)).astype(np.float32)).cuda(),
              "item": torch.from_numpy(rng.standard_normal((n_i, d)).astype(np.float32)).cuda()}
     torch.manual_seed(0)
@@ -58,7 +62,8 @@ def _worker(rank, world, port, agg, hetero, d, q):
 
 
 @pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 32), ("pool_nn_edge", "max", 32),
-                                          ("mean", "sum", 128), ("pool_nn", "mean", 128)])
+                                          ("mean", "sum", 128), ("pool_nn", "mean", 128),
+                                          ("mean", "attention", 128), ("mean_edge", "attention", 32)])
 def test_two_ranks_one_gpu_match_single_process(agg, hetero, d):
     import torch.multiprocessing as mp
     from gnnrec.inference import full_graph_embeddings
