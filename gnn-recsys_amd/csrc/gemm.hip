@@ -76,8 +76,10 @@ constexpr int stage_cols() { return BN >= 64 ? BN / 2 : BN; }
 
 template <int BN>
 constexpr int smem_floats() {
-  return (BM + BN) * LDSK > BM * (stage_cols<BN>() + 4) ? (BM + BN) * LDSK
-                                                        : BM * (stage_cols<BN>() + 4);
+  // K-loop tiles, or the epilogue's output staging + 2 attention factors per row
+  return (BM + BN) * LDSK > BM * (stage_cols<BN>() + 4) + 2 * BM
+             ? (BM + BN) * LDSK
+             : BM * (stage_cols<BN>() + 4) + 2 * BM;
 }
 
 // Shared epilogue: bias, activation, zero-guarded row L2 norm, then the cross-relation
@@ -107,8 +109,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   constexpr int OSTR = SC + 4;
   constexpr int TPR = SC / 32;  // accumulator tiles per staging round
   const bool attn = g.accum >= GNNREC_ACC_ATTN_FIRST;
-  const bool staged = g.vecO && !attn;
+  const bool staged = g.vecO;
   float* Ot = smem + wave * 32 * OSTR;
+  float* Fa = smem + BM * OSTR + wave * 64;  // attention: (keep, norm) per staged row
   float z[16][NT];
   float a_t[NT];
 #pragma unroll
@@ -154,6 +157,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
       if (g.accum == GNNREC_ACC_ATTN_LAST) norm[v] = 1.f / snew;
       if (row < g.M && r == 0)
         reinterpret_cast<float2*>(g.attn_state)[row] = make_float2(mnew, snew);
+
 #pragma unroll
       for (int t = 0; t < NT; ++t) z[v][t] *= cnew;
     }
@@ -184,6 +188,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
 #pragma unroll
   for (int round = 0; round < NT / TPR; ++round) {
     __syncthreads();  // K-loop tiles (or the previous round) fully read
+    if (attn && round == 0 && r == 0) {  // per-row factors for the store loop (Fa may
+#pragma unroll                              // overlap the K-loop tiles: written after the barrier)
+      for (int v = 0; v < 16; ++v) {
+        const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+        Fa[2 * rl] = keep[v];
+        Fa[2 * rl + 1] = norm[v];
+      }
+    }
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
@@ -209,6 +221,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
         const f32x4 o = *p;
 #pragma unroll
         for (int j = 0; j < 4; ++j) y[j] = fmaxf(o[j], y[j]);
+      } else if (attn) {
+        if (g.accum != GNNREC_ACC_ATTN_FIRST) y = *p * Fa[2 * rl] + y;
+        y = y * Fa[2 * rl + 1];
       }
       if (g.out_div > 0.f) y = y / g.out_div;
       *p = y;
