@@ -249,3 +249,26 @@ def test_mrr_neg_edges_ranks_positives_among_their_negatives():
     n = ns[ce].reshape(-1, K).cpu().numpy()
     ref = np.mean(1.0 / ((n >= p).sum(1) + 1))
     assert 0 < mrr <= 1 and abs(mrr - ref) < 1e-12
+
+
+def test_reversed_gather_backward_matches_atomic(monkeypatch):
+    """GNNREC_SPMM_BWD=gather (deterministic reversed-CSR gSpMM) == the atomic scatter."""
+    from gnnrec.autograd import SpmmFn
+    rng = np.random.default_rng(12)
+    n_dst, n_src = 300, 200
+    deg = rng.integers(0, 30, n_dst)
+    indptr = torch.from_numpy(np.concatenate([[0], np.cumsum(deg)])).cuda()
+    indices = torch.from_numpy(rng.integers(0, n_src, int(deg.sum())).astype(np.int32)).cuda()
+    ew = torch.from_numpy(rng.random(int(deg.sum())).astype(np.float32)).cuda()
+    m = torch.randn(n_src, 40, device="cuda")
+    g = torch.randn(n_dst, 40, device="cuda")
+    for reduce in ("mean", "sum"):
+        for w in (None, ew):
+            grads = []
+            for mode in ("atomic", "gather"):
+                monkeypatch.setenv("GNNREC_SPMM_BWD", mode)
+                x = m.clone().requires_grad_(True)
+                (SpmmFn.apply(x, indptr, indices, w, reduce, n_dst) * g).sum().backward()
+                grads.append(x.grad)
+            np.testing.assert_allclose(grads[0].cpu().numpy(), grads[1].cpu().numpy(), rtol=1e-5,
+                                       atol=1e-6)
