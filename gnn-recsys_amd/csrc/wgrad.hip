@@ -271,3 +271,86 @@ extern "C" int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float*
                      as_stream(stream), u, ldu, gz, ldg, n_rows, d, flags, gu, ldo);
   return check_launch("gnnrec_act_backward_f32");
 }
+
+// ---- row epilogue for outputs wider than one GEMM block ------------------------------
+// gnnrec_gemm_f32 applies the zero-guarded row L2 norm and the attention accumulation
+// inside a block that holds the whole output row (N <= 256).  The reference's widest
+// layers (hidden 384 / 512, main.py:87) go GEMM -> this kernel: one wave per row, the row
+// read once into registers-as-needed, norm, then store / add / max / attention update.
+namespace gnnrec {
+namespace {
+
+__global__ __launch_bounds__(256) void row_epilogue_kernel(
+    const float* __restrict__ z, int64_t ldz, int64_t M, int64_t N, int l2, int accum,
+    float out_div, const float* __restrict__ attn_vec, float* __restrict__ attn_state,
+    float* __restrict__ out, int64_t ldo) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int lane = threadIdx.x & 63;
+  const float* zr = z + row * ldz;
+  float* orow = out + row * ldo;
+  float ss = 0.f, e = 0.f;
+  for (int64_t c = lane; c < N; c += 64) {
+    const float x = zr[c];
+    ss += x * x;
+    if (attn_vec) e += x * attn_vec[c];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    ss += __shfl_xor(ss, off);
+    e += __shfl_xor(e, off);
+  }
+  float nrm = 1.f;
+  if (l2) {
+    nrm = sqrtf(ss);
+    if (nrm == 0.f) nrm = 1.f;
+    e = e / nrm;
+  }
+  const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
+  float keep = 0.f, cnew = 1.f, fin = 1.f;
+  if (attn) {
+    float mnew = e, snew = 1.f;
+    if (accum != GNNREC_ACC_ATTN_FIRST) {
+      const float2 st = reinterpret_cast<const float2*>(attn_state)[row];
+      mnew = fmaxf(st.x, e);
+      keep = expf(st.x - mnew);
+      cnew = expf(e - mnew);
+      snew = st.y * keep + cnew;
+    }
+    if (accum == GNNREC_ACC_ATTN_LAST) fin = 1.f / snew;
+    if (lane == 0) reinterpret_cast<float2*>(attn_state)[row] = make_float2(mnew, snew);
+  }
+  for (int64_t c = lane; c < N; c += 64) {
+    float y = zr[c] / nrm;
+    if (attn) {
+      y *= cnew;
+      if (accum != GNNREC_ACC_ATTN_FIRST) y = orow[c] * keep + y;
+      y *= fin;
+    } else if (accum == GNNREC_ACC_ADD) {
+      y = orow[c] + y;
+    } else if (accum == GNNREC_ACC_MAX) {
+      y = fmaxf(orow[c], y);
+    }
+    if (out_div > 0.f) y = y / out_div;
+    orow[c] = y;
+  }
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_row_epilogue_f32(const float* z, int64_t ldz, int64_t M, int64_t N, int l2norm,
+                                       int accum, float out_div, const float* attn_vec,
+                                       float* attn_state, float* out, int64_t ldo, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(M >= 0 && N >= 0 && ldz >= N && ldo >= N,
+                 "gnnrec_row_epilogue_f32: bad sizes / leading dims");
+  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_ATTN_LAST,
+                 "gnnrec_row_epilogue_f32: unknown accumulate mode %d", accum);
+  GNNREC_REQUIRE(accum < GNNREC_ACC_ATTN_FIRST || (attn_vec && attn_state),
+                 "gnnrec_row_epilogue_f32: attention needs attn_vec and attn_state");
+  if (M == 0 || N == 0) return GNNREC_OK;
+  hipLaunchKernelGGL(row_epilogue_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), z, ldz, M, N, l2norm, accum, out_div,
+                     accum >= GNNREC_ACC_ATTN_FIRST ? attn_vec : nullptr, attn_state, out, ldo);
+  return check_launch("gnnrec_row_epilogue_f32");
+}

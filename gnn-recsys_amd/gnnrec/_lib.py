@@ -61,6 +61,8 @@ SIGNATURES = {
     "gnnrec_spmm_project_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,
                                        _INT, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_gather_rows": (_INT, [_P, _I64, _P, _I64, _I64, _P, _I64, _P]),
+    "gnnrec_row_epilogue_f32": (_INT, [_P, _I64, _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64,
+                                       _P]),
     "gnnrec_act_backward_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _INT, _P, _I64, _P]),
     "gnnrec_exclusive_scan_i64": (_INT, [_P, _I64, _P, _P, _P]),
     "gnnrec_exclusive_scan_i32": (_INT, [_P, _I64, _P, _P, _P]),

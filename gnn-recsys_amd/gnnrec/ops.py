@@ -190,6 +190,15 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
             raise ValueError(f"out must be [{M}, {N}]")
     ldo = _rowmajor(out, "out")
     av, ast = _attn_args(accum, attn_vec, attn_state, M, N)
+    if N > GEMM_ROW_N and (l2norm or av is not None):
+        # the row norm / attention score needs the whole row: GEMM (bias, ReLU, sigmoid)
+        # into a scratch table, then one row-epilogue pass into out
+        z = gemm(A1, W1, A2, W2, bias, relu=relu, sigmoid=sigmoid, a2_deg=a2_deg,
+                 a2_mode=a2_mode)
+        check(lib.gnnrec_row_epilogue_f32(ptr(z), N, M, N, int(l2norm), ACCUM[accum],
+                                          float(out_div), ptr(av), ptr(ast), ptr(out), ldo,
+                                          stream_ptr(A1.device)), "gnnrec_row_epilogue_f32")
+        return out
     rc = lib.gnnrec_gemm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2), ptr(a2_deg),
                              a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div),
                              ptr(av), ptr(ast), ptr(out), ldo, stream_ptr(A1.device))
@@ -198,6 +207,7 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
 
 
 FUSED_D = 128  # gnnrec_spmm_project_f32 handles d_neigh = d_self = out = 128
+GEMM_ROW_N = 256  # widest output row gnnrec_gemm_f32 normalises / attends in one block
 
 
 def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT) -> bool:

@@ -233,6 +233,14 @@ int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_
                             int64_t n_rows, int64_t d, int flags, float* gu, int64_t ldo,
                             void* stream);
 
+/* Row epilogue for projections wider than one GEMM block (N > 256): out (accum)=
+ * l2norm?(z) row by row, accum / out_div / attention as gnnrec_gemm_f32.  z holds the
+ * GEMM result with bias and ReLU already applied (the reference's hidden 384 / 512 with
+ * norm=True, main.py:87, src/model.py:226-235). */
+int gnnrec_row_epilogue_f32(const float* z, int64_t ldz, int64_t M, int64_t N, int l2norm,
+                            int accum, float out_div, const float* attn_vec, float* attn_state,
+                            float* out, int64_t ldo, void* stream);
+
 /* ---- f4: LSTM neighbourhood reducer (one recurrence step) ------------------
  * Replaces ConvLayer._lstm_reducer (src/model.py:106-121, update_all at :164-169;
  * DGL 0.5.2 degree bucketing, messages in edge order).  Destinations are visited in
