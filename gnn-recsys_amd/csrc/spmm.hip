@@ -60,13 +60,15 @@ __global__ __launch_bounds__(256) void spmm_chunk_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int d,
     int64_t split, const int64_t* __restrict__ heavy_rows, const int64_t* __restrict__ chunk_ptr,
-    const int64_t* __restrict__ chunk_row, int64_t n_chunks, float* __restrict__ ws) {
+    const int64_t* __restrict__ chunk_row, int64_t n_chunks, const int64_t* __restrict__ counts,
+    float* __restrict__ ws) {
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
   const int col = blockIdx.y * (LPR * VEC) + (lane % LPR) * VEC;
   const bool colok = col < d;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
+  if (counts) n_chunks = counts[1];  // device-built plan: the grid covers its capacity
   for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += wstride) {
     const int64_t h = chunk_row[c];
     const int64_t row = heavy_rows[h];
@@ -88,10 +90,11 @@ template <int VEC, int REDUCE>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int64_t* __restrict__ indptr, int d, const int64_t* __restrict__ heavy_rows,
     int64_t n_heavy, const int64_t* __restrict__ chunk_ptr, const float* __restrict__ ws,
-    float* __restrict__ out, int64_t ldo, int empty_neginf) {
+    float* __restrict__ out, int64_t ldo, int empty_neginf, const int64_t* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
+  if (counts) n_heavy = counts[0];
   for (int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); h < n_heavy; h += wstride) {
     const int64_t row = heavy_rows[h];
     const int64_t deg = indptr[row + 1] - indptr[row];
@@ -116,6 +119,8 @@ struct SpmmArgs {
   int64_t n_dst; int d; float* out; int64_t ldo; int flags;
   int64_t split; const int64_t* heavy_rows; int64_t n_heavy; const int64_t* chunk_ptr;
   const int64_t* chunk_row; int64_t n_chunks; float* ws;
+  const int64_t* counts;  // device-built plan: {n_heavy, n_chunks}; n_heavy/n_chunks above
+                          // are then the plan's capacities (grid sizes)
 };
 
 // Resident 256-thread blocks per CU the row kernels may occupy (grid-stride beyond).
@@ -151,11 +156,11 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                        dim3(grid_waves(a.n_chunks), slices), dim3(256), 0, s, a.indptr, a.indices,
                        a.ew, a.X, a.ldx, a.d, a.split, a.heavy_rows, a.chunk_ptr, a.chunk_row,
-                       a.n_chunks, a.ws);
+                       a.n_chunks, a.counts, a.ws);
     const unsigned cslices = (unsigned)((a.d + 64 * VEC - 1) / (64 * VEC));
     hipLaunchKernelGGL((spmm_combine_kernel<VEC, REDUCE>), dim3(grid_waves(a.n_heavy), cslices),
                        dim3(256), 0, s, a.indptr, a.d, a.heavy_rows, a.n_heavy, a.chunk_ptr, a.ws,
-                       a.out, a.ldo, eni);
+                       a.out, a.ldo, eni, a.counts);
   }
   return check_launch("gnnrec_spmm_csr_f32");
 }
@@ -223,7 +228,7 @@ extern "C" int gnnrec_spmm_csr_f32(const int64_t* indptr, const int32_t* indices
                                    const float* X, int64_t ldx, int64_t n_dst, int64_t d,
                                    int reduce, int flags, float* out, int64_t ldo, void* stream) {
   gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
-                     0, nullptr, 0, nullptr, nullptr, 0, nullptr};
+                     0, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr};
   return gnnrec::spmm_entry(a, d, reduce, stream);
 }
 
@@ -235,7 +240,104 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* i
                                          const int64_t* chunk_ptr, const int64_t* chunk_row,
                                          int64_t n_chunks, float* workspace, void* stream) {
   gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
-                     split, heavy_rows, n_heavy, chunk_ptr, chunk_row, n_chunks, workspace};
+                     split, heavy_rows, n_heavy, chunk_ptr, chunk_row, n_chunks, workspace,
+                     nullptr};
+  return gnnrec::spmm_entry(a, d, reduce, stream);
+}
+
+// ---- device-built heavy-row plan (no host readback) ----------------------------------
+// Rows of degree > split number at most n_edges / (split + 1) and give at most
+// n_edges / split + n_heavy chunks, so the plan is sized on the host from n_edges alone and
+// filled on the device; the chunk / combine grids cover those capacities and read the real
+// counts from plan[0..1].  Heavy rows land in atomic order, which only changes which wave
+// reduces which chunk: each row still sums its own chunks in edge order (deterministic).
+namespace gnnrec {
+namespace {
+
+__global__ __launch_bounds__(256) void plan_mark_kernel(const int64_t* __restrict__ indptr,
+                                                        int64_t n_dst, int64_t split,
+                                                        int64_t cap_h,
+                                                        unsigned long long* __restrict__ counts,
+                                                        int64_t* __restrict__ heavy_rows) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_dst; v += stride) {
+    if (indptr[v + 1] - indptr[v] > split) {
+      const unsigned long long h = atomicAdd(counts, 1ull);
+      if ((int64_t)h < cap_h) heavy_rows[h] = v;
+    }
+  }
+}
+
+// one block: chunk_ptr = exclusive scan of ceil(deg/split) over the heavy rows, then
+// chunk_row[c] = owning heavy row
+__global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __restrict__ indptr,
+                                                           int64_t split, int64_t* __restrict__ plan,
+                                                           int64_t cap_h) {
+  __shared__ int64_t buf[1024];
+  int64_t* heavy_rows = plan + 2;
+  int64_t* chunk_ptr = heavy_rows + cap_h;
+  int64_t* chunk_row = chunk_ptr + cap_h + 1;
+  const int64_t n = plan[0] < cap_h ? plan[0] : cap_h;
+  const int t = threadIdx.x;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += 1024) {
+    int64_t x = 0;
+    if (base + t < n) {
+      const int64_t r = heavy_rows[base + t];
+      x = (indptr[r + 1] - indptr[r] + split - 1) / split;
+    }
+    buf[t] = x;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int64_t y = t >= off ? buf[t - off] : 0;
+      __syncthreads();
+      buf[t] += y;
+      __syncthreads();
+    }
+    if (base + t < n) chunk_ptr[base + t] = carry + buf[t] - x;
+    carry += buf[1023];
+    __syncthreads();
+  }
+  if (t == 0) {
+    chunk_ptr[n] = carry;
+    plan[1] = carry;
+  }
+  __syncthreads();
+  for (int64_t h = t; h < n; h += 1024)
+    for (int64_t c = chunk_ptr[h]; c < chunk_ptr[h + 1]; ++c) chunk_row[c] = h;
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split,
+                                      int64_t cap_h, int64_t* plan, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_dst >= 0 && split > 0 && cap_h >= 0, "gnnrec_spmm_plan_build: bad sizes");
+  GNNREC_REQUIRE(indptr && plan, "gnnrec_spmm_plan_build: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(plan, 0, 2 * sizeof(int64_t), s) != hipSuccess)
+    return check_launch("gnnrec_spmm_plan_build");
+  if (n_dst > 0 && cap_h > 0) {
+    int64_t blocks = (n_dst + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(plan_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, s, indptr, n_dst,
+                       split, cap_h, reinterpret_cast<unsigned long long*>(plan), plan + 2);
+    hipLaunchKernelGGL(plan_chunks_kernel, dim3(1), dim3(1024), 0, s, indptr, split, plan, cap_h);
+  }
+  return check_launch("gnnrec_spmm_plan_build");
+}
+
+extern "C" int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices,
+                                           const float* ew, const float* X, int64_t ldx,
+                                           int64_t n_dst, int64_t d, int reduce, int flags,
+                                           float* out, int64_t ldo, int64_t split,
+                                           const int64_t* plan, int64_t cap_h, int64_t cap_c,
+                                           float* workspace, void* stream) {
+  GNNREC_REQUIRE(plan && cap_h > 0 && cap_c > 0, "gnnrec_spmm_csr_planned_f32: empty plan");
+  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
+                     split, plan + 2, cap_h, plan + 2 + cap_h, plan + 3 + 2 * cap_h, cap_c,
+                     workspace, plan};
   return gnnrec::spmm_entry(a, d, reduce, stream);
 }
 
@@ -248,7 +350,12 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* i
 namespace gnnrec {
 namespace {
 
-template <int REDUCE, bool WEIGHTED>
+// One wave per dst row.  The row's gradient slice (NC columns per lane) stays in registers
+// while the wave walks its edges 64 at a time: one coalesced load of 64 indices (and
+// weights), then per edge a broadcast source id and NC no-return global_atomic_add_f32 on
+// a contiguous 256-B column run, so many atomics are in flight per wave instead of one
+// dependent index load per edge.
+template <int REDUCE, bool WEIGHTED, int NC>
 __global__ __launch_bounds__(256) void spmm_backward_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ G, int64_t ldg,
@@ -260,23 +367,50 @@ __global__ __launch_bounds__(256) void spmm_backward_kernel(
     const int64_t beg = indptr[v], end = indptr[v + 1];
     if (beg == end) continue;
     const float scale = REDUCE == GNNREC_REDUCE_MEAN ? 1.f / (float)(end - beg) : 1.f;
-    for (int c = lane; c < d; c += kWave) {
-      const float g = G[v * ldg + c] * scale;
-      if (g == 0.f) continue;
-      if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
-        const float y = Y[v * ldy + c];
-        for (int64_t e = beg; e < end; ++e) {
-          const int64_t u = indices[e];
-          const float m = WEIGHTED ? X[u * ldx + c] * ew[e] : X[u * ldx + c];
-          if (m == y) {
-            atomicAdd(gX + u * ldgx + c, WEIGHTED ? g * ew[e] : g);
-            break;
+    for (int c0 = 0; c0 < d; c0 += kWave * NC) {
+      float g[NC], y[NC];
+      bool live[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int c = c0 + lane + kWave * j;
+        g[j] = c < d ? G[v * ldg + c] * scale : 0.f;
+        live[j] = g[j] != 0.f;
+        if constexpr (REDUCE == GNNREC_REDUCE_MAX) y[j] = live[j] ? Y[v * ldy + c] : 0.f;
+      }
+      for (int64_t eb = beg; eb < end; eb += kWave) {
+        const int n = (int)(end - eb < kWave ? end - eb : kWave);
+        const int my_u = lane < n ? indices[eb + lane] : 0;
+        const float my_w = WEIGHTED && lane < n ? ew[eb + lane] : 1.f;
+        if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+          // first edge (CSR order) whose message equals the forward maximum, per column
+          for (int k = 0; k < n; ++k) {
+            const int64_t u = __shfl(my_u, k);
+            const float w = __shfl(my_w, k);
+            const float* xr = X + u * ldx + c0 + lane;
+            float* gr = gX + u * ldgx + c0 + lane;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+              if (!live[j]) continue;
+              const float m = WEIGHTED ? xr[kWave * j] * w : xr[kWave * j];
+              if (m == y[j]) {
+                unsafeAtomicAdd(gr + kWave * j, WEIGHTED ? g[j] * w : g[j]);
+                live[j] = false;
+              }
+            }
           }
-        }
-      } else {
-        for (int64_t e = beg; e < end; ++e) {
-          const int64_t u = indices[e];
-          atomicAdd(gX + u * ldgx + c, WEIGHTED ? g * ew[e] : g);
+          bool any = false;
+#pragma unroll
+          for (int j = 0; j < NC; ++j) any |= live[j];
+          if (__ballot(any) == 0) break;
+        } else {
+          for (int k = 0; k < n; ++k) {
+            const int64_t u = __shfl(my_u, k);
+            const float w = WEIGHTED ? __shfl(my_w, k) : 1.f;
+            float* gr = gX + u * ldgx + c0 + lane;
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+              if (live[j]) unsafeAtomicAdd(gr + kWave * j, WEIGHTED ? g[j] * w : g[j]);
+          }
         }
       }
     }
@@ -299,13 +433,15 @@ extern "C" int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* in
                  "gnnrec_spmm_backward_f32: max needs the forward input and output");
   hipStream_t s = as_stream(stream);
   const unsigned grid = grid_waves(n_dst);
+#define GNNREC_BWD_NC(R, W, NC)                                                               \
+  hipLaunchKernelGGL((spmm_backward_kernel<R, W, NC>), dim3(grid), dim3(256), 0, s, indptr,      \
+                     indices, ew, grad_out, ldg, X, ldx, out, ldo, n_dst, (int)d, grad_X, ldgx)
+#define GNNREC_BWD_W(R, W)                                                                    \
+  if (d <= 64) GNNREC_BWD_NC(R, W, 1);                                                        \
+  else if (d <= 128) GNNREC_BWD_NC(R, W, 2);                                                  \
+  else GNNREC_BWD_NC(R, W, 4);
 #define GNNREC_BWD(R)                                                                         \
-  if (ew)                                                                                     \
-    hipLaunchKernelGGL((spmm_backward_kernel<R, true>), dim3(grid), dim3(256), 0, s, indptr,   \
-                       indices, ew, grad_out, ldg, X, ldx, out, ldo, n_dst, (int)d, grad_X, ldgx); \
-  else                                                                                        \
-    hipLaunchKernelGGL((spmm_backward_kernel<R, false>), dim3(grid), dim3(256), 0, s, indptr,  \
-                       indices, ew, grad_out, ldg, X, ldx, out, ldo, n_dst, (int)d, grad_X, ldgx);
+  if (ew) { GNNREC_BWD_W(R, true) } else { GNNREC_BWD_W(R, false) }
   switch (reduce) {
     case GNNREC_REDUCE_SUM: GNNREC_BWD(GNNREC_REDUCE_SUM) break;
     case GNNREC_REDUCE_MEAN: GNNREC_BWD(GNNREC_REDUCE_MEAN) break;
@@ -313,5 +449,7 @@ extern "C" int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* in
     default: GNNREC_REQUIRE(false, "gnnrec_spmm_backward_f32: unknown reduce %d", reduce);
   }
 #undef GNNREC_BWD
+#undef GNNREC_BWD_W
+#undef GNNREC_BWD_NC
   return check_launch("gnnrec_spmm_backward_f32");
 }

@@ -1,0 +1,199 @@
+// f2 — source-major transpose of a dst-major CSR block, for the aggregation backward.
+//
+// The forward gather (a1) walks in-edges per destination row.  Its gradient w.r.t. the
+// source rows is the same sum with the roles swapped: grad_X[u] = Σ_{e: src_e = u}
+// w_e · g[dst_e].  Scattering that with float atomics is capped by the L2 atomic units
+// (≈0.32 T float atomics/s measured, tools/bench_spmm_bwd.py), well below what a gather
+// moves; transposing the block once (stable LSD radix sort of the int32 source ids, then
+// a bounds pass) turns it into the same bandwidth-bound gather as the forward, and the
+// stable order (ascending edge id inside each source row) makes the gradient bitwise
+// repeatable.  Reference: DGL's backward of update_all(copy_u, mean/sum) used by
+// ConvLayer training (src/model.py:161-167, src/train/run.py:136-138).
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.hpp"
+
+namespace gnnrec {
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+inline unsigned key_bits(int64_t n_src) {
+  unsigned b = 0;
+  while (b < 32 && (int64_t(1) << b) < n_src) ++b;
+  return b < 1 ? 1 : b;
+}
+
+size_t sort_temp_bytes(int64_t E, int64_t n_src, hipStream_t s) {
+  size_t bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                            (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)E, 0,
+                            key_bits(n_src), s);
+  return bytes;
+}
+
+// one wave per dst row: edge id, dst id and the per-edge weight (ew · 1/deg for mean)
+__global__ __launch_bounds__(256) void edge_rows_kernel(const int64_t* __restrict__ indptr,
+                                                        const float* __restrict__ ew,
+                                                        int64_t n_dst, int mean,
+                                                        int32_t* __restrict__ eid,
+                                                        int32_t* __restrict__ dst_of,
+                                                        float* __restrict__ w_e) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < n_dst; v += wstride) {
+    const int64_t beg = indptr[v], end = indptr[v + 1];
+    const float inv = mean && end > beg ? 1.f / (float)(end - beg) : 1.f;
+    for (int64_t e = beg + lane; e < end; e += kWave) {
+      eid[e] = (int32_t)e;
+      dst_of[e] = (int32_t)v;
+      if (w_e) w_e[e] = ew ? ew[e] * inv : inv;
+    }
+  }
+}
+
+// indptr_t[u] = first k with keys[k] >= u (lower bound in the sorted keys; one thread per
+// source row, so long runs of unused source ids cost nothing extra)
+__global__ __launch_bounds__(256) void bounds_kernel(const int32_t* __restrict__ keys,
+                                                     int64_t E, int64_t n_src,
+                                                     int64_t* __restrict__ indptr_t) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= n_src; u += stride) {
+    int64_t lo = 0, hi = E;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)keys[mid] < u) lo = mid + 1;
+      else hi = mid;
+    }
+    indptr_t[u] = lo;
+  }
+}
+
+__global__ __launch_bounds__(256) void permute_kernel(const int32_t* __restrict__ perm,
+                                                      const int32_t* __restrict__ dst_of,
+                                                      const float* __restrict__ w_e, int64_t E,
+                                                      int32_t* __restrict__ indices_t,
+                                                      float* __restrict__ ew_t) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < E; k += stride) {
+    const int32_t e = perm[k];
+    indices_t[k] = dst_of[e];
+    if (ew_t) ew_t[k] = w_e[e];
+  }
+}
+
+inline unsigned flat_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 256 * 16) b = 256 * 16;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+__global__ __launch_bounds__(256) void iota_kernel(int32_t* __restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
+    out[k] = (int32_t)k;
+}
+
+// stable sort of row keys: perm = edge ids ordered by (key, edge id); indptr[n_rows+1].
+// Scratch: [values | sorted keys | radix temp]; values = 0..E-1 written here unless the
+// caller supplies them (eid_ready), in which case the first slot is free for perm.
+int sort_rows(const int32_t* keys_in, int64_t E, int64_t n_rows, char* p, size_t bytes,
+              int64_t* indptr, int32_t* perm, int32_t* eid_ready, hipStream_t s) {
+  const size_t slot = align_up((size_t)E * 4);
+  int32_t* eid = eid_ready ? eid_ready : reinterpret_cast<int32_t*>(p);
+  int32_t* keys = reinterpret_cast<int32_t*>(p + slot);
+  void* temp = p + 2 * slot;
+  size_t temp_bytes = bytes - 2 * slot;
+  if (!eid_ready)
+    hipLaunchKernelGGL(iota_kernel, dim3(flat_grid(E)), dim3(256), 0, s, eid, E);
+  if (hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys, eid, perm,
+                                               (unsigned)E, 0, key_bits(n_rows), s);
+      e != hipSuccess) {
+    set_error("radix sort failed: %s", hipGetErrorString(e));
+    return GNNREC_EHIP;
+  }
+  hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_rows + 1)), dim3(256), 0, s, keys, E,
+                     n_rows, indptr);
+  return GNNREC_OK;
+}
+
+size_t sort_rows_bytes(int64_t E, int64_t n_rows) {
+  return 2 * align_up((size_t)E * 4) + align_up(sort_temp_bytes(E, n_rows, nullptr));
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" size_t gnnrec_csr_transpose_workspace_bytes(int64_t n_edges, int64_t n_src) {
+  using namespace gnnrec;
+  if (n_edges <= 0) return 0;
+  return 3 * align_up((size_t)n_edges * 4) + sort_rows_bytes(n_edges, n_src);
+}
+
+extern "C" int gnnrec_csr_transpose(const int64_t* indptr, const int32_t* indices,
+                                    const float* ew, int64_t n_dst, int64_t n_src,
+                                    int64_t n_edges, int mean, void* workspace,
+                                    size_t workspace_bytes, int64_t* indptr_t,
+                                    int32_t* indices_t, float* ew_t, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_dst >= 0 && n_src >= 0 && n_edges >= 0, "gnnrec_csr_transpose: negative size");
+  GNNREC_REQUIRE(n_edges < (int64_t(1) << 31) && n_src < (int64_t(1) << 31),
+                 "gnnrec_csr_transpose: int32 edge / node ids");
+  GNNREC_REQUIRE(indptr && indptr_t, "gnnrec_csr_transpose: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (n_edges == 0) {
+    hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_src + 1)), dim3(256), 0, s,
+                       (const int32_t*)nullptr, (int64_t)0, n_src, indptr_t);
+    return check_launch("gnnrec_csr_transpose");
+  }
+  GNNREC_REQUIRE(indices && indices_t && workspace, "gnnrec_csr_transpose: null pointer");
+  GNNREC_REQUIRE(!(ew || mean) || ew_t, "gnnrec_csr_transpose: weights need ew_t");
+  const size_t need = gnnrec_csr_transpose_workspace_bytes(n_edges, n_src);
+  GNNREC_REQUIRE(workspace_bytes >= need, "gnnrec_csr_transpose: workspace %zu < %zu bytes",
+                 workspace_bytes, need);
+  char* p = static_cast<char*>(workspace);
+  const size_t slot = align_up((size_t)n_edges * 4);
+  int32_t* eid = reinterpret_cast<int32_t*>(p);
+  int32_t* dst_of = reinterpret_cast<int32_t*>(p + slot);
+  float* w_e = (ew || mean) ? reinterpret_cast<float*>(p + 2 * slot) : nullptr;
+  hipLaunchKernelGGL(edge_rows_kernel, dim3(flat_grid(n_dst * 16)), dim3(256), 0, s, indptr, ew,
+                     n_dst, mean, eid, dst_of, w_e);
+  // sort_rows' scratch follows the three edge arrays; with eid supplied as the sort's
+  // values its first slot is free and holds the permutation
+  char* q = p + 3 * slot;
+  int32_t* perm = reinterpret_cast<int32_t*>(q);
+  const int rc = sort_rows(indices, n_edges, n_src, q, need - 3 * slot, indptr_t, perm, eid, s);
+  if (rc != GNNREC_OK) return rc;
+  hipLaunchKernelGGL(permute_kernel, dim3(flat_grid(n_edges)), dim3(256), 0, s, perm, dst_of,
+                     w_e, n_edges, indices_t, (ew || mean) ? ew_t : nullptr);
+  return check_launch("gnnrec_csr_transpose");
+}
+
+extern "C" size_t gnnrec_csr_from_keys_workspace_bytes(int64_t n_edges, int64_t n_rows) {
+  return n_edges <= 0 ? 0 : gnnrec::sort_rows_bytes(n_edges, n_rows);
+}
+
+extern "C" int gnnrec_csr_from_keys(const int32_t* keys, int64_t n_edges, int64_t n_rows,
+                                    void* workspace, size_t workspace_bytes, int64_t* indptr,
+                                    int32_t* perm, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_edges >= 0 && n_rows >= 0, "gnnrec_csr_from_keys: negative size");
+  GNNREC_REQUIRE(n_edges < (int64_t(1) << 31) && n_rows < (int64_t(1) << 31),
+                 "gnnrec_csr_from_keys: int32 edge / row ids");
+  GNNREC_REQUIRE(indptr, "gnnrec_csr_from_keys: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (n_edges == 0) {
+    hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_rows + 1)), dim3(256), 0, s,
+                       (const int32_t*)nullptr, (int64_t)0, n_rows, indptr);
+    return check_launch("gnnrec_csr_from_keys");
+  }
+  GNNREC_REQUIRE(keys && perm && workspace, "gnnrec_csr_from_keys: null pointer");
+  const size_t need = gnnrec_csr_from_keys_workspace_bytes(n_edges, n_rows);
+  GNNREC_REQUIRE(workspace_bytes >= need, "gnnrec_csr_from_keys: workspace %zu < %zu bytes",
+                 workspace_bytes, need);
+  int rc = sort_rows(keys, n_edges, n_rows, static_cast<char*>(workspace), need, indptr, perm,
+                     nullptr, s);
+  if (rc != GNNREC_OK) return rc;
+  return check_launch("gnnrec_csr_from_keys");
+}

@@ -45,6 +45,9 @@ SIGNATURES = {
     "gnnrec_spmm_csr_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64, _P]),
     "gnnrec_spmm_csr_split_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,
                                          _I64, _P, _I64, _P, _P, _I64, _P, _P]),
+    "gnnrec_spmm_plan_build": (_INT, [_P, _I64, _I64, _I64, _P, _P]),
+    "gnnrec_spmm_csr_planned_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,
+                                           _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_spmm_backward_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _I64, _I64,
                                         _INT, _P, _I64, _P]),
     "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P,
@@ -61,6 +64,10 @@ SIGNATURES = {
     "gnnrec_spmm_project_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,
                                        _INT, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_gather_rows": (_INT, [_P, _I64, _P, _I64, _I64, _P, _I64, _P]),
+    "gnnrec_csr_transpose_workspace_bytes": (_U64, [_I64, _I64]),
+    "gnnrec_csr_transpose": (_INT, [_P, _P, _P, _I64, _I64, _I64, _INT, _P, _U64, _P, _P, _P, _P]),
+    "gnnrec_csr_from_keys_workspace_bytes": (_U64, [_I64, _I64]),
+    "gnnrec_csr_from_keys": (_INT, [_P, _I64, _I64, _P, _U64, _P, _P, _P]),
     "gnnrec_row_epilogue_f32": (_INT, [_P, _I64, _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64,
                                        _P]),
     "gnnrec_act_backward_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _INT, _P, _I64, _P]),

@@ -19,7 +19,6 @@ import os
 import torch
 
 from . import ops
-from .graph import build_csr
 
 
 class LinearFn(torch.autograd.Function):
@@ -56,6 +55,7 @@ class SpmmFn(torch.autograd.Function):
         out = ops.spmm(indptr, indices, m.contiguous(), reduce, edge_weight=ew)
         ctx.save_for_backward(m, indptr, indices, ew, out)
         ctx.reduce = reduce
+        ctx.nnz = getattr(indptr, "_gnnrec_nnz", None)  # host edge count if already known
         return out
 
     @staticmethod
@@ -63,32 +63,24 @@ class SpmmFn(torch.autograd.Function):
         m, indptr, indices, ew, out = ctx.saved_tensors
         if not ctx.needs_input_grad[0]:
             return None, None, None, None, None, None
-        if ctx.reduce in ('sum', 'mean') and os.environ.get("GNNREC_SPMM_BWD") == "gather":
-            # DGL's rule: the backward of a gSpMM is a gSpMM on the reversed graph — a
-            # deterministic gather over the source-major CSR instead of the atomic scatter.
-            # Opt-in: the per-batch sort that builds that CSR costs more than the atomics
-            # save (C3 step 18.8 vs 18.2-18.5 ms), but it makes training bitwise repeatable
-            return (_spmm_reversed(indptr, indices, g, ew, ctx.reduce, m.shape[0]),
+        if ctx.reduce in ('sum', 'mean') and os.environ.get("GNNREC_SPMM_BWD") != "atomic":
+            # DGL's rule: the backward of a gSpMM is a gSpMM on the reversed graph.  The
+            # block is transposed on the device (stable radix sort) and the gradient is
+            # the forward's bandwidth-bound gather over that CSR: deterministic, and not
+            # capped by the L2 float-atomic rate as the scatter is
+            # (GNNREC_SPMM_BWD=atomic keeps the scatter)
+            return (_spmm_reversed(indptr, indices, g, ew, ctx.reduce, m.shape[0], ctx.nnz),
                     None, None, None, None, None)
         gm = ops.spmm_backward(indptr, indices, g, ctx.reduce, edge_weight=ew,
                                X=m, out=out, n_src=m.shape[0])
         return gm, None, None, None, None, None
 
 
-def _spmm_reversed(indptr, indices, g, ew, reduce: str, n_src: int):
+def _spmm_reversed(indptr, indices, g, ew, reduce: str, n_src: int, nnz=None):
     """grad_X[u] = Σ_{e: src_e = u} g[dst_e] · (ew_e) (/ deg(dst_e) for mean), as a sum
     gSpMM over the source-major CSR of the same edges (rows = sources)."""
-    n_dst = indptr.numel() - 1
-    deg = indptr[1:] - indptr[:-1]
-    dst = torch.repeat_interleave(torch.arange(n_dst, device=indptr.device), deg,
-                                  output_size=indices.numel())
-    ip_t, ix_t, perm = build_csr(dst, indices.long(), n_src)
-    w = None
-    if reduce == 'mean':
-        w = (1.0 / deg.clamp(min=1).to(torch.float32))[dst]
-    if ew is not None:
-        w = ew if w is None else w * ew
-    w_t = None if w is None else w[perm].contiguous()
+    ip_t, ix_t, w_t = ops.csr_transpose(indptr, indices, n_src, edge_weight=ew,
+                                        mean=reduce == 'mean', n_edges=nnz)
     return ops.spmm(ip_t, ix_t, g.contiguous(), 'sum', edge_weight=w_t)
 
 
@@ -176,13 +168,13 @@ class CosineFn(torch.autograd.Function):
         b_hat, b_n = _normalize(hd)
         ga = gb = None
         if need[0]:  # Gâ[s] = Σ_{e: src_e = s} g_e b̂[dst_e]
-            ip, ix, perm = build_csr(dst, src, hs.shape[0])
-            ga = _normalize_backward(a_hat, a_n, ops.spmm(ip, ix, b_hat, "sum",
-                                                          edge_weight=g[perm]))
+            ip, perm = ops.csr_from_keys(src, hs.shape[0])
+            ga = _normalize_backward(a_hat, a_n, ops.spmm(ip, dst[perm].to(torch.int32), b_hat,
+                                                          "sum", edge_weight=g[perm]))
         if need[1]:  # Gb̂[d] = Σ_{e: dst_e = d} g_e â[src_e]
-            ip, ix, perm = build_csr(src, dst, hd.shape[0])
-            gb = _normalize_backward(b_hat, b_n, ops.spmm(ip, ix, a_hat, "sum",
-                                                          edge_weight=g[perm]))
+            ip, perm = ops.csr_from_keys(dst, hd.shape[0])
+            gb = _normalize_backward(b_hat, b_n, ops.spmm(ip, src[perm].to(torch.int32), a_hat,
+                                                          "sum", edge_weight=g[perm]))
         return ga, gb, None, None
 
 

@@ -82,6 +82,29 @@ def split_plan(indptr: torch.Tensor, split: int = DEFAULT_SPLIT):
     return plan
 
 
+def _device_plan(indptr: torch.Tensor, split: int):
+    """Device-built heavy-row plan sized from the host edge count (cached on indptr);
+    None when no row can have more than `split` edges."""
+    cached = getattr(indptr, "_gnnrec_dev_plan", None)
+    if cached is not None and cached[0] == split:
+        return cached[1]
+    n_dst, E = indptr.numel() - 1, indptr._gnnrec_nnz
+    cap_h = min(n_dst, E // (split + 1))
+    res = None
+    if cap_h > 0:
+        cap_c = E // split + cap_h
+        pl = torch.empty(2 + cap_h + cap_h + 1 + cap_c, dtype=torch.int64, device=indptr.device)
+        check(_lib.load().gnnrec_spmm_plan_build(ptr(indptr), n_dst, split, cap_h, ptr(pl),
+                                                 stream_ptr(indptr.device)),
+              "gnnrec_spmm_plan_build")
+        res = (pl, cap_h, cap_c)
+    try:
+        indptr._gnnrec_dev_plan = (split, res)
+    except AttributeError:  # pragma: no cover
+        pass
+    return res
+
+
 def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: str = "mean",
          edge_weight: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
          empty_neginf: bool = False, split: Optional[int] = DEFAULT_SPLIT) -> torch.Tensor:
@@ -112,6 +135,19 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
             raise ValueError(f"out must be [{n_dst}, {d}]")
     ldo = _rowmajor(out, "out")
     flags = _lib.SPMM_EMPTY_NEGINF if empty_neginf else 0
+    if split and getattr(indptr, "_gnnrec_split_plan", None) is None and \
+            getattr(indptr, "_gnnrec_nnz", None) is not None:
+        # edge count known, degrees not: heavy-row plan built on the device (no readback)
+        dplan = _device_plan(indptr, split)
+        if dplan is not None:
+            pl, cap_h, cap_c = dplan
+            ws = torch.empty((cap_c, d), dtype=torch.float32, device=X.device)
+            check(lib.gnnrec_spmm_csr_planned_f32(
+                ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx, n_dst, d,
+                REDUCE[reduce], flags, ptr(out), ldo, split, ptr(pl), cap_h, cap_c, ptr(ws),
+                stream_ptr(X.device)), "gnnrec_spmm_csr_planned_f32")
+            return out
+        split = None  # no row can exceed split
     plan = split_plan(indptr, split) if split else None
     if plan is None:
         rc = lib.gnnrec_spmm_csr_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx,
@@ -127,6 +163,54 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
                                        n_chunks, ptr(ws), stream_ptr(X.device))
     check(rc, "gnnrec_spmm_csr_split_f32")
     return out
+
+
+def csr_transpose(indptr: torch.Tensor, indices: torch.Tensor, n_src: int,
+                  edge_weight: Optional[torch.Tensor] = None, mean: bool = False,
+                  n_edges: Optional[int] = None):
+    """Source-major CSR of a dst-major block (stable: ascending edge id per source row).
+    -> (indptr_t int64 [n_src+1], indices_t int32 = dst rows, ew_t float32 or None), where
+    ew_t = edge_weight (· 1/deg(dst) when mean) in the transposed order."""
+    lib = _lib.load()
+    _dev(indptr, "indptr", torch.int64)
+    _dev(indices, "indices", torch.int32)
+    dev = indptr.device
+    n_dst, E = indptr.numel() - 1, _nnz(indptr) if n_edges is None else int(n_edges)
+    if indices.numel() < E:
+        raise ValueError("csr_transpose: indices shorter than the edge count")
+    if edge_weight is not None:
+        _dev(edge_weight, "edge_weight", torch.float32)
+        if edge_weight.numel() < E:
+            raise ValueError("csr_transpose: edge_weight shorter than the edge count")
+    ip_t = torch.empty(n_src + 1, dtype=torch.int64, device=dev)
+    ix_t = torch.empty(E, dtype=torch.int32, device=dev)
+    w_t = torch.empty(E, dtype=torch.float32, device=dev) if (edge_weight is not None or mean) else None
+    nbytes = int(lib.gnnrec_csr_transpose_workspace_bytes(E, n_src))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    check(lib.gnnrec_csr_transpose(ptr(indptr), ptr(indices), ptr(edge_weight), n_dst, n_src, E,
+                                   int(mean), ptr(ws), nbytes, ptr(ip_t), ptr(ix_t), ptr(w_t),
+                                   stream_ptr(dev)), "gnnrec_csr_transpose")
+    ip_t._gnnrec_nnz = E
+    return ip_t, ix_t, w_t
+
+
+def csr_from_keys(keys: torch.Tensor, n_rows: int):
+    """Rows of a COO list: -> (indptr int64 [n_rows+1], perm int32 [E]) with perm the edge
+    ids grouped by keys[e] (ascending edge id inside a row).  keys: int32/int64 in [0, n_rows)."""
+    lib = _lib.load()
+    if keys.dtype != torch.int32:
+        keys = keys.to(torch.int32)
+    _dev(keys, "keys", torch.int32)
+    keys = keys.contiguous()
+    dev, E = keys.device, keys.numel()
+    ip = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+    perm = torch.empty(E, dtype=torch.int32, device=dev)
+    nbytes = int(lib.gnnrec_csr_from_keys_workspace_bytes(E, n_rows))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    check(lib.gnnrec_csr_from_keys(ptr(keys), E, n_rows, ptr(ws), nbytes, ptr(ip), ptr(perm),
+                                   stream_ptr(dev)), "gnnrec_csr_from_keys")
+    ip._gnnrec_nnz = E
+    return ip, perm
 
 
 def spmm_backward(indptr, indices, grad_out, reduce, edge_weight=None, X=None, out=None,

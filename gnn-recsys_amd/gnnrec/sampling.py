@@ -126,6 +126,9 @@ class BlockSampler:
         src_lists: Dict[str, list] = {}
         for (ce, indptr, indices, eids, dseeds, fan, key, mask, o_ip), tot in zip(plan, totals):
             o_src, o_eid = ops.sample_fill(indptr, indices, eids, dseeds, fan, key, o_ip, tot, mask)
+            o_ip._gnnrec_nnz = int(tot)  # edge count known on the host: no later readback
+            if fan is not None and 0 <= fan <= ops.DEFAULT_SPLIT:
+                o_ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows possible
             rels[ce] = [o_ip, o_src, o_eid]
             src_lists.setdefault(ce[0], []).append(ce)
         prefixes, ranks = {}, {}

@@ -112,6 +112,21 @@ int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* indices, con
                               const int64_t* chunk_row, int64_t n_chunks, float* workspace,
                               void* stream);
 
+/* The same split with the plan built on the device (no host readback of the heavy-row
+ * count): plan = int64[2 + cap_h + (cap_h + 1) + cap_c] laid out {n_heavy, n_chunks,
+ * heavy_rows[cap_h], chunk_ptr[cap_h+1], chunk_row[cap_c]}, with cap_h = min(n_dst,
+ * n_edges / (split + 1)) and cap_c = n_edges / split + cap_h (bounds that hold for any
+ * degree distribution).  gnnrec_spmm_plan_build fills it; gnnrec_spmm_csr_planned_f32
+ * reduces with workspace[cap_c, d].  Used for blocks whose edge count is known on the
+ * host but whose degrees are not (sampled blocks, the backward's transposed blocks). */
+int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split, int64_t cap_h,
+                           int64_t* plan, void* stream);
+int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                                const float* X, int64_t ldx, int64_t n_dst, int64_t d,
+                                int reduce, int flags, float* out, int64_t ldo, int64_t split,
+                                const int64_t* plan, int64_t cap_h, int64_t cap_c,
+                                float* workspace, void* stream);
+
 /* Gradient of gnnrec_spmm_csr_f32 w.r.t. X (training):
  * grad_X[indices[e]] += (ew ? ew[e] : 1) * grad_out[v] (/ deg for MEAN); for MAX the
  * gradient of each column goes to the first edge whose message equals out[v]
@@ -232,6 +247,25 @@ int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
 int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_t ldg,
                             int64_t n_rows, int64_t d, int flags, float* gu, int64_t ldo,
                             void* stream);
+
+/* f2: source-major transpose of a dst-major CSR block (training backward of a1; the
+ * reference's DGL update_all backward, src/model.py:161-167).  indptr_t[n_src+1] (int64),
+ * indices_t[n_edges] = dst row of each edge, grouped by source row, ascending edge id
+ * inside a row (stable).  ew_t[k] = ew[e] (· 1/deg(dst_e) when mean != 0); ew_t may be
+ * NULL when ew is NULL and mean == 0.  int32 ids (n_edges, n_src < 2^31).  Workspace
+ * from gnnrec_csr_transpose_workspace_bytes (radix-sort scratch + 5 edge arrays). */
+size_t gnnrec_csr_transpose_workspace_bytes(int64_t n_edges, int64_t n_src);
+int gnnrec_csr_transpose(const int64_t* indptr, const int32_t* indices, const float* ew,
+                         int64_t n_dst, int64_t n_src, int64_t n_edges, int mean,
+                         void* workspace, size_t workspace_bytes, int64_t* indptr_t,
+                         int32_t* indices_t, float* ew_t, void* stream);
+
+/* Rows of a COO edge list: stable sort of int32 row keys.  indptr[n_rows+1] (int64),
+ * perm[n_edges] = edge ids grouped by row, ascending inside a row.  Replaces the
+ * argsort/bincount/cumsum CSR build on the training path (no host readback). */
+size_t gnnrec_csr_from_keys_workspace_bytes(int64_t n_edges, int64_t n_rows);
+int gnnrec_csr_from_keys(const int32_t* keys, int64_t n_edges, int64_t n_rows, void* workspace,
+                         size_t workspace_bytes, int64_t* indptr, int32_t* perm, void* stream);
 
 /* Row epilogue for projections wider than one GEMM block (N > 256): out (accum)=
  * l2norm?(z) row by row, accum / out_div / attention as gnnrec_gemm_f32.  z holds the

@@ -80,6 +80,16 @@ def test_spmm_heavy_row_split_matches_oracle(split, d, reduce, weighted):
     again = ops.spmm(ti, _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w),
                      split=split)
     assert torch.equal(out, again)
+    # the device-built plan (edge count known on the host, degrees not) chunks the same
+    # rows the same way: bitwise the host-plan result
+    td = _t(indptr)
+    td._gnnrec_nnz = int(indptr[-1])
+    dev_out = ops.spmm(td, _t(idx), _t(X), reduce, edge_weight=None if w is None else _t(w),
+                       split=split)
+    assert getattr(td, "_gnnrec_split_plan", None) is None and td._gnnrec_dev_plan[1] is not None
+    pl = td._gnnrec_dev_plan[1][0].cpu().numpy()
+    assert pl[0] == plan[0].numel() and pl[1] == plan[3]
+    assert torch.equal(out, dev_out)
 
 
 def test_spmm_bitwise_deterministic_and_strided_output():
@@ -933,3 +943,35 @@ def test_reference_wide_dims_match_oracle(hidden, out, agg, hagg):
                 continue
             np.testing.assert_allclose(a_.cpu().numpy(), b_.cpu().numpy(), rtol=1e-4, atol=1e-5,
                                        err_msg=k)
+
+
+@pytest.mark.parametrize("n_dst,n_src,max_deg,weighted,mean", [(0, 5, 1, False, False),
+                                                               (300, 1, 9, False, True),
+                                                               (1000, 777, 40, True, True),
+                                                               (5000, 70000, 12, True, False),
+                                                               (2000, 3000, 0, False, True)])
+def test_csr_transpose_bit_exact(n_dst, n_src, max_deg, weighted, mean):
+    """Source-major transpose of a block: stable (ascending edge id per source row), the
+    weights carried along (· 1/deg for mean) — bit-exact vs a numpy stable sort."""
+    from gnnrec import ops
+    rng = np.random.default_rng(n_dst + n_src)
+    deg = rng.integers(0, max_deg + 1, n_dst)
+    indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    E = int(indptr[-1])
+    idx = rng.integers(0, n_src, E).astype(np.int32)
+    ew = rng.random(E).astype(np.float32) if weighted else None
+    ip_t, ix_t, w_t = ops.csr_transpose(_t(indptr), _t(idx), n_src,
+                                        edge_weight=None if ew is None else _t(ew), mean=mean)
+    order = np.argsort(idx, kind="stable")
+    dst = np.repeat(np.arange(n_dst), deg)
+    ref_ip = np.concatenate([[0], np.cumsum(np.bincount(idx, minlength=n_src))])
+    np.testing.assert_array_equal(ip_t.cpu().numpy(), ref_ip)
+    np.testing.assert_array_equal(ix_t.cpu().numpy(), dst[order])
+    if ew is None and not mean:
+        assert w_t is None
+    else:
+        w = np.ones(E, np.float32) if ew is None else ew
+        if mean:
+            inv = (np.float32(1) / np.maximum(deg, 1).astype(np.float32))[dst]
+            w = (w * inv).astype(np.float32)
+        np.testing.assert_array_equal(w_t.cpu().numpy(), w[order])

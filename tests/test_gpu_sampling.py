@@ -252,7 +252,8 @@ def test_mrr_neg_edges_ranks_positives_among_their_negatives():
 
 
 def test_reversed_gather_backward_matches_atomic(monkeypatch):
-    """GNNREC_SPMM_BWD=gather (deterministic reversed-CSR gSpMM) == the atomic scatter."""
+    """The default sum/mean backward (device transpose + gather over the source-major CSR,
+    deterministic) == the atomic scatter (GNNREC_SPMM_BWD=atomic), and is bitwise repeatable."""
     from gnnrec.autograd import SpmmFn
     rng = np.random.default_rng(12)
     n_dst, n_src = 300, 200
@@ -265,10 +266,11 @@ def test_reversed_gather_backward_matches_atomic(monkeypatch):
     for reduce in ("mean", "sum"):
         for w in (None, ew):
             grads = []
-            for mode in ("atomic", "gather"):
+            for mode in ("atomic", "gather", "gather"):
                 monkeypatch.setenv("GNNREC_SPMM_BWD", mode)
                 x = m.clone().requires_grad_(True)
                 (SpmmFn.apply(x, indptr, indices, w, reduce, n_dst) * g).sum().backward()
                 grads.append(x.grad)
             np.testing.assert_allclose(grads[0].cpu().numpy(), grads[1].cpu().numpy(), rtol=1e-5,
                                        atol=1e-6)
+            assert torch.equal(grads[1], grads[2])
