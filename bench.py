@@ -52,6 +52,8 @@ def parse():
                     help="c5: the C4 graph split 80%% clicks / 20%% buys -> 4 relations")
     ap.add_argument("--hetero", choices=["sum", "mean", "max", "attention"], default="sum")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="segment mode (segments=8): outputs bitwise equal at 1/2/4/8 GPUs")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-scale", type=float, default=0.1,
                     help="fraction of the graph used for the bounded CPU-baseline sample")
@@ -185,7 +187,8 @@ def main():
     split = ((("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2)) if args.config == "c5"
              else (("buys", "bought-by", 1.0),))
     shard = bipartite_shard(args.users, args.items, args.edges, rank, world, dev,
-                            zipf_s=args.zipf, split=split)
+                            zipf_s=args.zipf, split=split,
+                            segments=8 if args.deterministic else None)
     feats = {"user": node_features(args.users, d, 0, dev, slice(shard.p_lo, shard.p_hi)),
              "item": torch.zeros((shard.padded_rows("item"), d), device=dev)}
     feats["item"][: args.items] = node_features(args.items, d, 1, dev)
@@ -194,7 +197,8 @@ def main():
     model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
                           args.aggregator, "cos", args.hetero, True).to(dev).eval()
     ex = Exchange()
-    runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap)
+    runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap,
+                                  deterministic=args.deterministic)
     timers = EventTimers()
     runner.timers = timers
     torch.cuda.synchronize()
@@ -247,7 +251,8 @@ def main():
                                       if args.config == "c5" else "")
                                    + f", NodeEmbedding + L=2 ConvLayer '{args.aggregator}', "
                                      f"hetero {args.hetero}, norm, d={d}"
-                                   + (f", item zipf s={args.zipf}" if args.zipf else ""),
+                                   + (f", item zipf s={args.zipf}" if args.zipf else "")
+                                   + (", deterministic segments=8" if args.deterministic else ""),
                        "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
                        "overlap": not args.no_overlap},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -382,19 +382,33 @@ __global__ __launch_bounds__(256) void spmm_backward_kernel(
         const int my_u = lane < n ? indices[eb + lane] : 0;
         const float my_w = WEIGHTED && lane < n ? ew[eb + lane] : 1.f;
         if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
-          // first edge (CSR order) whose message equals the forward maximum, per column
-          for (int k = 0; k < n; ++k) {
-            const int64_t u = __shfl(my_u, k);
-            const float w = __shfl(my_w, k);
-            const float* xr = X + u * ldx + c0 + lane;
-            float* gr = gX + u * ldgx + c0 + lane;
+          // first edge (CSR order) whose message equals the forward maximum, per column;
+          // 8 edges' values are loaded before any compare so 8·NC loads are in flight
+          constexpr int kB = 8;
+          for (int k0 = 0; k0 < n; k0 += kB) {
+            float m[kB][NC], wv[kB];
+            int64_t uv[kB];
 #pragma unroll
-            for (int j = 0; j < NC; ++j) {
-              if (!live[j]) continue;
-              const float m = WEIGHTED ? xr[kWave * j] * w : xr[kWave * j];
-              if (m == y[j]) {
-                unsafeAtomicAdd(gr + kWave * j, WEIGHTED ? g[j] * w : g[j]);
-                live[j] = false;
+            for (int q = 0; q < kB; ++q) {
+              const bool ok = k0 + q < n;
+              uv[q] = __shfl(my_u, ok ? k0 + q : 0);
+              wv[q] = WEIGHTED ? __shfl(my_w, ok ? k0 + q : 0) : 1.f;
+              const float* xr = X + uv[q] * ldx + c0 + lane;
+#pragma unroll
+              for (int j = 0; j < NC; ++j) m[q][j] = (ok && live[j]) ? xr[kWave * j] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < kB; ++q) {
+              if (k0 + q >= n) break;
+              float* gr = gX + uv[q] * ldgx + c0 + lane;
+#pragma unroll
+              for (int j = 0; j < NC; ++j) {
+                if (!live[j]) continue;
+                const float mv = WEIGHTED ? m[q][j] * wv[q] : m[q][j];
+                if (mv == y[j]) {
+                  unsafeAtomicAdd(gr + kWave * j, WEIGHTED ? g[j] * wv[q] : g[j]);
+                  live[j] = false;
+                }
               }
             }
           }

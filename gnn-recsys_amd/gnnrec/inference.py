@@ -71,7 +71,7 @@ class RelShard:
     """One relation's edges held by this rank, as a dst-major CSR."""
 
     def __init__(self, ce, kind: str, indptr, indices, weights, n_rows: int, global_edges: int,
-                 deg_own: Optional[torch.Tensor] = None):
+                 deg_own: Optional[torch.Tensor] = None, segs: Optional[list] = None):
         self.ce = ce
         self.kind = kind              # 'local_dst' (dst rows owned here) | 'partial'
         self.indptr = indptr
@@ -80,6 +80,8 @@ class RelShard:
         self.n_rows = n_rows
         self.global_edges = global_edges
         self.deg_own = deg_own        # int32 global in-degree of the owned dst rows ('partial')
+        self.segs = segs              # 'partial' + segments: [(indptr, indices, weights)] per
+                                      # owned segment, in segment order
 
     @property
     def local_edges(self) -> int:
@@ -90,7 +92,16 @@ class GraphShard:
     """This rank's share of a heterograph for the sharded full-graph pass."""
 
     def __init__(self, rank: int, world: int, ptype: str, num_nodes: Dict[str, int],
-                 canonical_etypes: List[tuple], device):
+                 canonical_etypes: List[tuple], device, segments: Optional[int] = None):
+        """segments: split every 'partial' relation's edges into this many fixed key ranges
+        (source id of the partitioned type, else edge id), `segments // world` per rank, so
+        ShardedFullGraphPass(deterministic=True) sums the same partials in the same tree at
+        any world size dividing `segments` (bitwise-equal outputs at P=1/2/4/8)."""
+        if segments is not None and (segments < world or segments % world or
+                                     segments & (segments - 1)):
+            raise ValueError(f"segments={segments} must be a power of two and a multiple of "
+                             f"the world size {world}")
+        self.segments = segments
         self.rank, self.world, self.ptype = rank, world, ptype
         self.num_nodes = dict(num_nodes)
         self.canonical_etypes = list(canonical_etypes)
@@ -143,17 +154,33 @@ class GraphShard:
         w = None if weights is None else weights[order].float().contiguous()
         deg = torch.zeros(n_rows, dtype=torch.int32, device=dst_global_deg.device)
         deg[: dst_global_deg.numel()] = dst_global_deg.to(torch.int32)
+        segs = None
+        if self.segments is not None:
+            # key ranges fixed by the global sizes alone: the source id when the source is
+            # the partitioned type (rank ranges are unions of them), else the edge id (the
+            # edge split of from_graph); each segment's rows keep the edges' input order
+            k = self.segments // self.world
+            if s_t == self.ptype:
+                key, bounds = src, even_ranges(self.num_nodes[self.ptype], self.segments)
+            else:
+                key, bounds = eid, even_ranges(global_edges, self.segments)
+            segs = []
+            for sg in range(self.rank * k, (self.rank + 1) * k):
+                sel = (key >= bounds[sg]) & (key < bounds[sg + 1])
+                ip, ix, od = build_csr(src_loc[sel], dst[sel], n_rows)
+                ws = None if weights is None else weights[sel][od].float().contiguous().to(dev)
+                segs.append((ip.to(dev), ix.to(dev), ws))
         self.rels[ce] = RelShard(ce, 'partial', indptr.to(dev), indices.to(dev),
                                  None if w is None else w.to(dev), n_rows, global_edges,
-                                 deg[self.own_slice(d_t)].contiguous().to(dev))
+                                 deg[self.own_slice(d_t)].contiguous().to(dev), segs)
 
     @classmethod
     def from_graph(cls, g: HeteroGraph, rank: int, world: int, ptype: str = 'user', device=None,
-                   weight_field: Optional[str] = 'occurrence'):
+                   weight_field: Optional[str] = 'occurrence', segments: Optional[int] = None):
         """Shard a full HeteroGraph held by every rank (tests / moderate graphs)."""
         dev = device if device is not None else g.device
         sh = cls(rank, world, ptype, {nt: g.num_nodes(nt) for nt in g.ntypes},
-                 g.canonical_etypes, dev)
+                 g.canonical_etypes, dev, segments)
         for ce in g.canonical_etypes:
             s, d = g.all_edges(etype=ce)
             E = s.numel()
@@ -203,8 +230,19 @@ class ShardedFullGraphPass:
     inject a checker backend with the same signatures."""
 
     def __init__(self, model, shard: GraphShard, exchange: Optional[Exchange] = None,
-                 ops_backend=None, overlap: bool = True, fold_embedding: bool = True):
+                 ops_backend=None, overlap: bool = True, fold_embedding: bool = True,
+                 deterministic: bool = False):
         self.model = model
+        # deterministic: outputs bitwise independent of the world size (needs a shard built
+        # with `segments`): replicated-type sums are per-segment partials folded in a fixed
+        # pairwise tree (locally, then across ranks after an all-to-all), every kernel choice
+        # is made from global sizes, and the embedding is not folded.  Costs the fused launch
+        # on the replicated side at one rank and the partials' extra HBM passes.
+        if deterministic and shard.segments is None:
+            raise ValueError("deterministic=True needs a GraphShard built with segments")
+        self.deterministic = deterministic
+        if deterministic:
+            fold_embedding = False
         # fold the partitioned type's NodeEmbedding into the first layer's fused launches
         # (one rank, mean/sum reducers): its 10M-row GEMM and table disappear
         self.fold_embedding = fold_embedding
@@ -358,7 +396,11 @@ class ShardedFullGraphPass:
                 rs = sh.rels[ce]
                 msg = self._message(mod, ce, h, preagg)
                 can_fuse = getattr(O, 'can_spmm_project', None)
-                if self.ex.ws == 1 and reduce != 'lstm' and can_fuse is not None:
+                if self.deterministic and reduce in ('sum', 'mean'):
+                    partials[ce] = self._tree_partial(rs, msg, weighted, reduce)
+                    continue
+                if self.ex.ws == 1 and reduce != 'lstm' and can_fuse is not None and \
+                        not self.deterministic:
                     self_rows = self._get(h, T)
                     if can_fuse(rs.indptr, msg, self_rows, mod.fc_self.weight,
                                 mod.fc_neigh.weight):
@@ -383,6 +425,18 @@ class ShardedFullGraphPass:
                 partials[ce] = (own, work, reduce)
         return partials
 
+    def _tree_partial(self, rs, msg, weighted, reduce):
+        """Σ over this relation's segments in one fixed pairwise tree: the rank folds its
+        own contiguous block of segments (a subtree), the all-to-all hands every owner the
+        P subtree roots of its rows in rank order, and the owner folds those.  The tree is
+        the same at every world size dividing the segment count."""
+        with self._time('spmm'):
+            parts = [self.ops.spmm(ip, ix, msg, 'sum', edge_weight=w if weighted else None)
+                     for ip, ix, w in rs.segs]
+        local = _tree_sum(parts)
+        blocks = self.ex.all_to_all_rows(local)
+        return _tree_sum(list(blocks.unbind(0))), None, reduce
+
     def _local(self, hconv, h, active, out):
         """item->user style relations: dst rows owned here; GEMMs on the side stream."""
         sh, O = self.shard, self.ops
@@ -404,8 +458,10 @@ class ShardedFullGraphPass:
             rs = sh.rels[ce]
             msg = self._message(mod, ce, h, preagg)
             acc, div = hconv.accum_mode(j, R)
+            avg = (rs.global_edges / max(sh.num_nodes[T], 1)) if self.deterministic else None
             if reduce != 'lstm' and can_fuse is not None and can_fuse(
-                    rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight):
+                    rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight,
+                    avg_deg=avg):
                 # aggregation and projection in one launch on the main stream: the self rows
                 # must be ready here (they may come from the side stream)
                 self_rows = self._get(h, T)
@@ -501,6 +557,13 @@ class ShardedFullGraphPass:
         self._owned(hconv, h, active, partials, out)
         self._fold.clear()  # a folded embedding only stands in for the first layer's input
         return out
+
+
+def _tree_sum(parts: List[torch.Tensor]) -> torch.Tensor:
+    """Pairwise tree ((p0+p1)+(p2+p3))+... over a power-of-two list, in order."""
+    while len(parts) > 1:
+        parts = [torch.add(parts[i], parts[i + 1]) for i in range(0, len(parts), 2)]
+    return parts[0]
 
 
 def gather_partitioned(shard: GraphShard, rows: torch.Tensor, exchange: Exchange) -> torch.Tensor:

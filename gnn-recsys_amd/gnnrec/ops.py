@@ -294,9 +294,11 @@ FUSED_D = 128  # gnnrec_spmm_project_f32 handles d_neigh = d_self = out = 128
 GEMM_ROW_N = 256  # widest output row gnnrec_gemm_f32 normalises / attends in one block
 
 
-def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT) -> bool:
+def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT,
+                     avg_deg: Optional[float] = None) -> bool:
     """True when the fused aggregation+projection kernel applies (shapes, alignment, no
-    heavy rows, GPU tensors; GNNREC_FUSED=0 disables it)."""
+    heavy rows, GPU tensors; GNNREC_FUSED=0 disables it).  avg_deg: edges per row to judge
+    the degree threshold by (default: this CSR's own)."""
     if os.environ.get("GNNREC_FUSED", "1") == "0":
         return False
     D = FUSED_D
@@ -315,6 +317,8 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
     # the in-kernel projection reads both weight matrices from LDS once per 2 rows
     # (64 KiB/row): below ~24 edges per row that LDS traffic, not the gather, bounds the
     # launch (C5 bought-by, 10 edges/row: fused 20.3 ms vs spmm 8.1 + GEMM 7.7 ms)
+    if avg_deg is not None:
+        return avg_deg >= FUSED_MIN_DEG
     n = indptr.numel() - 1
     return n == 0 or _nnz(indptr) >= FUSED_MIN_DEG * n
 

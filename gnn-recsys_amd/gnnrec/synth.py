@@ -42,7 +42,8 @@ def relation_pairs(split):
 def bipartite_shard(n_users: int, n_items: int, n_edges: int, rank: int, world: int, device,
                     seed: int = 11, zipf_s: float = 0.0, chunk: int = 1 << 26,
                     occurrence: bool = False,
-                    split=(("buys", "bought-by", 1.0),)) -> GraphShard:
+                    split=(("buys", "bought-by", 1.0),),
+                    segments: Optional[int] = None) -> GraphShard:
     """This rank's GraphShard of the synthetic user->item graph (+ reverse relations).
 
     `split` assigns consecutive eid ranges of the generated edge stream to relations
@@ -51,7 +52,8 @@ def bipartite_shard(n_users: int, n_items: int, n_edges: int, rank: int, world: 
     dev = torch.device(device)
     pairs = relation_pairs(split)
     etypes = [ce for f, r, _ in pairs for ce in (f, r)]
-    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, etypes, dev)
+    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, etypes, dev,
+                    segments)
     cdf = zipf_cdf(n_items, zipf_s, dev) if zipf_s > 0 else None
     bounds = [0]
     for _, _, frac in pairs:

@@ -35,6 +35,7 @@ def _worker(rank, world, port, case, q):
         from gnnrec.graph import HeteroGraph
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
 
+        case, _, det = case.partition("#")  # "#det": deterministic segment mode
         case, _, hetero = case.partition("@")  # "@attention": build-defined hetero mode
         meta = dict(golden_io.manifest()[case])
         if hetero:
@@ -54,9 +55,10 @@ def _worker(rank, world, port, case, q):
         _set_attention(model)
         model.eval()
         ex = Exchange()
-        shard = GraphShard.from_graph(g, rank, world, "user", device="cpu")
+        shard = GraphShard.from_graph(g, rank, world, "user", device="cpu",
+                                      segments=8 if det else None)
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
-        p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops)
+        p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
         out = p.run(shard.local_features(feats))
         users = gather_partitioned(shard, out["user"], ex)
         res = {"user": users.numpy()}
@@ -100,9 +102,16 @@ def _run(case, world):
     ("model_bip_poolnn_max_noemb_nn", 8),  # 41 users over 8 ranks: ragged and tiny shards
     ("model_het_meannnedge_mean_emb@attention", 2),
     ("model_het_mean_sum_skip@attention", 4),
+    ("model_bip_mean_sum_emb#det", 1),
+    ("model_het_meannnedge_mean_emb#det", 2),
+    ("model_het_mean_sum_skip@attention#det", 4),
+    ("model_het_meanedge_max_emb#det", 8),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
-    name, _, hetero = case.partition("@")
+    """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a
+    fixed tree and exchanged all-to-all; its bitwise independence of the world size is
+    checked on the GPU, tests/test_gpu_dist.py, where the arithmetic is the product's.)"""
+    name, _, hetero = case.split("#")[0].partition("@")
     meta = dict(golden_io.manifest()[name])
     a = golden_io.load(name)
     num_nodes, edges, occ = golden_io.graph_parts(a)

@@ -43,7 +43,7 @@ def _build(agg, hetero, d=32):
     return g, feats, model
 
 
-def _worker(rank, world, port, agg, hetero, d, q):
+def _worker(rank, world, port, agg, hetero, d, q, segments=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -53,8 +53,9 @@ def _worker(rank, world, port, agg, hetero, d, q):
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
         g, feats, model = _build(agg, hetero, d)
         ex = Exchange()
-        sh = GraphShard.from_graph(g, rank, world, "user", device="cuda")
-        out = ShardedFullGraphPass(model, sh, ex).run(sh.local_features(feats))
+        sh = GraphShard.from_graph(g, rank, world, "user", device="cuda", segments=segments)
+        out = ShardedFullGraphPass(model, sh, ex, deterministic=segments is not None).run(
+            sh.local_features(feats))
         users = gather_partitioned(sh, out["user"], ex)
         q.put((rank, users.cpu().numpy(), out["item"][:700].cpu().numpy()))
     finally:
@@ -83,3 +84,37 @@ def test_two_ranks_one_gpu_match_single_process(agg, hetero, d):
     for _, users, items in res:
         np.testing.assert_allclose(users, ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(items, ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 128), ("mean_edge", "attention", 32)])
+def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
+    """with segments=8 the outputs are bitwise identical at P = 1, 2 and 4
+    (the replicated type's sums are the same per-segment partials folded in the same tree
+    whatever the rank count; every kernel choice is made from global sizes)."""
+    import torch.multiprocessing as mp
+    from gnnrec.dist import Exchange
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    g, feats, model = _build(agg, hetero, d)
+    with torch.no_grad():
+        ref = full_graph_embeddings(g, model, feats)
+    sh = GraphShard.from_graph(g, 0, 1, "user", device="cuda", segments=8)
+    one = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True).run(
+        sh.local_features(feats))
+    base = (one["user"].cpu().numpy(), one["item"][:700].cpu().numpy())
+    np.testing.assert_allclose(base[0], ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(base[1], ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+    ctx = mp.get_context("spawn")
+    for world in (2, 4):
+        q = ctx.Queue()
+        port = _port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, agg, hetero, d, q, 8))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        for rank, users, items in res:
+            assert np.array_equal(users, base[0]), f"P={world} rank {rank}: users differ"
+            assert np.array_equal(items, base[1]), f"P={world} rank {rank}: items differ"
