@@ -52,8 +52,12 @@ def parse():
                     help="c5: the C4 graph split 80%% clicks / 20%% buys -> 4 relations")
     ap.add_argument("--hetero", choices=["sum", "mean", "max", "attention"], default="sum")
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--deterministic", action="store_true",
-                    help="segment mode (segments=8): outputs bitwise equal at 1/2/4/8 GPUs")
+    ap.add_argument("--mode", choices=["deterministic", "fast"], default="deterministic",
+                    help="deterministic: outputs bitwise equal at 1/2/4/8 GPUs (fixed segment "
+                         "tree + all-to-all); fast: tiles accumulated in place + reduce-scatter")
+    ap.add_argument("--segments", type=int, default=8,
+                    help="source-range tiles of the user->item relation (0: none; "
+                         "deterministic mode needs a power of two divisible by the GPU count)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-scale", type=float, default=0.1,
                     help="fraction of the graph used for the bounded CPU-baseline sample")
@@ -86,25 +90,45 @@ class EventTimers:
         return sum(s.elapsed_time(e) for s, e in ev) / len(ev), len(ev)
 
 
-def spmm_algorithmic_bytes(shard, d, fused=()):
-    """Per-pass algorithmic bytes of the gather+aggregate launches:
-    per edge d*4 (fp32 source row) + 4 (int32 index); per dst row 8 (int64 indptr) + d*4
-    (write), + d*4 for the h_self row when the projection is fused into the launch."""
-    tot = 0
-    n = 0
+KERNELS = {
+    "spmm_project": ("spmm_project_kernel", "gnnrec spmm_project_kernel (gather + segmented "
+                     "mean + fused SAGE projection, ReLU, L2 norm)"),
+    "spmm_tile": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented sum of one "
+                  "source-range tile, accumulated in place)"),
+    "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
+}
+
+
+def launch_bytes(shard, d, fused, deterministic):
+    """Algorithmic bytes per layer and launches per layer of each aggregation kernel tag
+    (SURVEY §8d row d4): per edge d*4 (fp32 source row) + 4 (int32 index); per dst row 8
+    (int64 indptr) + d*4 (write), + d*4 for the h_self row when the projection is fused
+    into the launch, + d*4 for the partial read back when a tile accumulates in place."""
+    out = {}
     for ce, rs in shard.rels.items():
-        tot += rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + d * 4 * (2 if ce in fused else 1))
-        n += 1
-    return tot, n
+        if ce in fused:
+            tag, b, n = "spmm_project", rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + 8 * d), 1
+        elif rs.segs is not None:
+            tag, b, n = "spmm_tile", 0, len(rs.segs)
+            for j, (ip, ix, _) in enumerate(rs.segs):
+                acc = (j % 2 == 1) if deterministic else j > 0
+                b += ix.numel() * (d * 4 + 4) + rs.n_rows * (8 + 4 * d * (2 if acc else 1))
+        else:
+            tag, b, n = "spmm", rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + 4 * d), 1
+        tb, tn = out.get(tag, (0, 0))
+        out[tag] = (tb + b, tn + n)
+    return out
 
 
-def pmc_traffic(args, world):
-    """HBM bytes per aggregation launch from the committed rocprofv3 PMC passes
+def pmc_traffic(args, world, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (FETCH_SIZE x2 for gfx950's half-counted wide reads + WRITE_SIZE, KB -> B), for
     the default single-GPU C4 workload they were collected on; None otherwise."""
     import csv
     default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
-               args.config) == (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4")
+               args.config, args.mode, args.segments) == (10_000_000, 1_000_000, 500_000_000,
+                                                          128, 0.0, "mean", "c4",
+                                                          "deterministic", 8)
     f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch.csv")
     w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write.csv")
     if world != 1 or not default or not (os.path.exists(f) and os.path.exists(w)):
@@ -112,7 +136,7 @@ def pmc_traffic(args, world):
     tot, n = 0.0, 0
     for path, scale in ((f, 2.0), (w, 1.0)):
         for r in csv.DictReader(open(path)):
-            if "spmm_csr_kernel" in r["Kernel_Name"] or "spmm_project_kernel" in r["Kernel_Name"]:
+            if kernel in r["Kernel_Name"]:
                 tot += float(r["Counter_Value"]) * 1024 * scale
                 n += scale == 2.0
     return tot / n if n else None
@@ -186,9 +210,14 @@ def main():
     d = args.dim
     split = ((("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2)) if args.config == "c5"
              else (("buys", "bought-by", 1.0),))
+    segments = args.segments or None
+    det = args.mode == "deterministic"
+    if det and (segments is None or segments % world or segments & (segments - 1)):
+        det = False  # the fixed tree needs a power-of-two segment count divisible by P
+    if segments is not None and segments < world:
+        segments = None
     shard = bipartite_shard(args.users, args.items, args.edges, rank, world, dev,
-                            zipf_s=args.zipf, split=split,
-                            segments=8 if args.deterministic else None)
+                            zipf_s=args.zipf, split=split, segments=segments)
     feats = {"user": node_features(args.users, d, 0, dev, slice(shard.p_lo, shard.p_hi)),
              "item": torch.zeros((shard.padded_rows("item"), d), device=dev)}
     feats["item"][: args.items] = node_features(args.items, d, 1, dev)
@@ -198,7 +227,7 @@ def main():
                           args.aggregator, "cos", args.hetero, True).to(dev).eval()
     ex = Exchange()
     runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap,
-                                  deterministic=args.deterministic)
+                                  deterministic=det)
     timers = EventTimers()
     runner.timers = timers
     torch.cuda.synchronize()
@@ -223,10 +252,22 @@ def main():
     edges_per_step = 2 * sum(rs.global_edges for rs in shard.rels.values())  # L=2 layers
     value = edges_per_step * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-    spmm_ms, n_launch = timers.mean_ms("spmm")
-    bytes_pass, n_rel = spmm_algorithmic_bytes(shard, d, runner.fused)
-    bytes_per_launch = bytes_pass / n_rel  # each relation launched once per layer
-    achieved = bytes_per_launch / (spmm_ms * 1e-3) / 1e9 if spmm_ms == spmm_ms else None
+    # roofline of the aggregation kernels: the fused gather+projection launch when the pass
+    # has one (C4: the user side, ~half the pass), else the busiest tag; the other
+    # aggregation kernel (C4: the item side's source-range tiles) is reported beside it
+    per_tag = launch_bytes(shard, d, runner.fused, det)
+    ran = [t for t in per_tag if timers.mean_ms(t)[1]]
+
+    def line(t):
+        ms, n = timers.mean_ms(t)
+        b = per_tag[t][0] / per_tag[t][1]  # bytes per layer / launches per layer
+        return ms, n, b, b / (ms * 1e-3) / 1e9
+
+    tag = "spmm_project" if "spmm_project" in ran else max(
+        ran, key=lambda t: timers.mean_ms(t)[0] * timers.mean_ms(t)[1]) if ran else "spmm"
+    spmm_ms, n_launch, bytes_per_launch, achieved = line(tag) if ran else (None, 0, None, None)
+    others = {t: dict(zip(("launch_ms", "launches_timed", "bytes_per_launch", "achieved"),
+                          line(t)), kernel=KERNELS[t][1]) for t in ran if t != tag}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
@@ -252,21 +293,21 @@ def main():
                                    + f", NodeEmbedding + L=2 ConvLayer '{args.aggregator}', "
                                      f"hetero {args.hetero}, norm, d={d}"
                                    + (f", item zipf s={args.zipf}" if args.zipf else "")
-                                   + (", deterministic segments=8" if args.deterministic else ""),
+                                   + (f", {shard.segments} source tiles" if shard.segments
+                                      else "")
+                                   + (", deterministic (bitwise equal at 1/2/4/8 GPUs)" if det
+                                      else ""),
                        "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
                        "overlap": not args.no_overlap},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": pmc_traffic(args, world),
-                         "kernel": ("gnnrec spmm_project_kernel (gather + segmented mean + "
-                                    "fused SAGE projection, ReLU, L2 norm)"
-                                    if len(runner.fused) == n_rel else
-                                    "gnnrec spmm_csr_kernel / spmm_project_kernel (gather + "
-                                    f"segmented mean; {len(runner.fused)}/{n_rel} relations "
-                                    "with the projection fused)"),
+                         "traffic": pmc_traffic(args, world, KERNELS[tag][0]),
+                         "kernel": KERNELS[tag][1],
                          "bytes_per_launch": bytes_per_launch, "launch_ms": spmm_ms,
-                         "launches_timed": n_launch},
+                         "launches_timed": n_launch,
+                         "other_kernels": {t: dict(o, frac=o["achieved"] / HBM_PEAK_GBS)
+                                           for t, o in others.items()}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

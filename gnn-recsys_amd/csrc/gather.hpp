@@ -92,6 +92,15 @@ __device__ __forceinline__ void combine_groups(Frag<VEC>& acc) {
   }
 }
 
+// acc = out[row] (+ | max) acc: a source-range tile added to the partial of earlier tiles
+template <int VEC, int REDUCE>
+__device__ __forceinline__ void accumulate_into(Frag<VEC>& acc, const float* p) {
+  Frag<VEC> o;
+  load_frag<VEC>(o, p);
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(o.v[v], acc.v[v]);
+}
+
 template <int VEC, int REDUCE>
 __device__ __forceinline__ void finalize(Frag<VEC>& acc, int64_t deg, int empty_neginf) {
   if constexpr (REDUCE == GNNREC_REDUCE_MEAN) {

@@ -43,6 +43,7 @@ struct GemmArgs {
   const float* A2; int64_t lda2; int64_t K2; const float* W2;
   const int32_t* a2_deg; int a2_mode;
   const float* bias;
+  const float* bias_ne;  // added on rows with a2_deg > 0 (a folded NodeEmbedding's W_n b_e)
   int64_t M; int64_t N;
   int epilogue; int accum; float out_div;
   const float* attn_vec; float* attn_state;
@@ -95,13 +96,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   const bool relu = g.epilogue & GNNREC_EPI_RELU;
   const bool sigm = g.epilogue & GNNREC_EPI_SIGMOID;
   const bool l2 = g.epilogue & GNNREC_EPI_L2NORM;
-  float bias_t[NT];
+  float bias_t[NT], bne_t[NT];
   bool colok[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int64_t col = n0 + t * 32 + r;
     colok[t] = col < g.N;
     bias_t[t] = (g.bias && colok[t]) ? g.bias[col] : 0.f;
+    bne_t[t] = (g.bias_ne && colok[t]) ? g.bias_ne[col] : 0.f;
   }
   // staged store: the wave's 32 x BN tile goes through LDS (in column halves) and leaves
   // as whole rows of 16-B stores (4x fewer, fully coalesced store instructions)
@@ -120,9 +122,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
 #pragma unroll
   for (int v = 0; v < 16; ++v) {
     float ss = 0.f;
+    bool ne = false;
+    if (g.bias_ne) {
+      const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      ne = row < g.M && g.a2_deg[row] > 0;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       float x = acc[t][v] + bias_t[t];
+      if (ne) x += bne_t[t];
       if (relu) x = fmaxf(x, 0.f);
       if (sigm) x = 1.f / (1.f + expf(-x));
       if (!colok[t]) x = 0.f;
@@ -506,7 +514,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
 
 extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                                const float* A2, int64_t lda2, int64_t K2, const float* W2,
-                               const int32_t* a2_deg, int a2_mode, const float* bias, int64_t M,
+                               const int32_t* a2_deg, int a2_mode, const float* bias,
+                               const float* bias_nonempty, int64_t M,
                                int64_t N, int epilogue, int accum, float out_div,
                                const float* attn_vec, float* attn_state, float* out,
                                int64_t ldo, void* stream) {
@@ -518,6 +527,8 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   GNNREC_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2), "gnnrec_gemm_f32: bad A2/W2");
   GNNREC_REQUIRE(a2_mode == GNNREC_A2_NONE || a2_deg != nullptr,
                  "gnnrec_gemm_f32: a2_mode needs a2_deg");
+  GNNREC_REQUIRE(bias_nonempty == nullptr || a2_deg != nullptr,
+                 "gnnrec_gemm_f32: bias_nonempty needs a2_deg");
   GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_ATTN_LAST,
                  "gnnrec_gemm_f32: unknown accumulate mode %d", accum);
   const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
@@ -528,7 +539,7 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   GemmArgs g;
   g.A1 = A1; g.lda1 = lda1; g.K1 = K1; g.W1 = W1;
   g.A2 = A2; g.lda2 = lda2; g.K2 = K2; g.W2 = W2;
-  g.a2_deg = a2_deg; g.a2_mode = a2_mode; g.bias = bias;
+  g.a2_deg = a2_deg; g.a2_mode = a2_mode; g.bias = bias; g.bias_ne = bias_nonempty;
   g.M = M; g.N = N; g.epilogue = epilogue; g.accum = accum; g.out_div = out_div;
   g.attn_vec = attn_vec; g.attn_state = attn_state;
   g.out = out; g.ldo = ldo;

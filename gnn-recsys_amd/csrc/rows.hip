@@ -60,3 +60,64 @@ extern "C" int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const i
   if ((al & 3u) == 0) return launch<uint32_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
   return launch<uint8_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
 }
+
+// ---- partial-table add (the deterministic pass's fixed tree over source-range tiles) ----
+namespace gnnrec {
+namespace {
+
+// 4 float4 per thread, all loads issued before the adds (8 x 16 B in flight per lane)
+constexpr int kAddU = 4;
+__global__ __launch_bounds__(256) void add_f32x4_kernel(const float4* __restrict__ a,
+                                                        const float4* __restrict__ b,
+                                                        float4* __restrict__ out, int64_t n4) {
+  const int64_t base = (int64_t)blockIdx.x * (256 * kAddU) + threadIdx.x;
+  float4 x[kAddU], y[kAddU];
+#pragma unroll
+  for (int k = 0; k < kAddU; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n4) {
+      x[k] = a[i];
+      y[k] = b[i];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kAddU; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n4) out[i] = make_float4(x[k].x + y[k].x, x[k].y + y[k].y, x[k].z + y[k].z,
+                                     x[k].w + y[k].w);
+  }
+}
+
+__global__ __launch_bounds__(256) void add_f32_kernel(const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      float* __restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = a[i] + b[i];
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_add_f32(const float* a, const float* b, float* out, int64_t n,
+                              void* stream) {
+  GNNREC_REQUIRE(n >= 0, "gnnrec_add_f32: negative size");
+  if (n == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(a && b && out, "gnnrec_add_f32: null pointer");
+  hipStream_t s = as_stream(stream);
+  const bool v4 = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                    reinterpret_cast<uintptr_t>(out)) & 15u) == 0 && n % 4 == 0;
+  if (v4) {
+    const int64_t n4 = n / 4;
+    const int64_t blocks = (n4 + 256 * kAddU - 1) / (256 * kAddU);
+    GNNREC_REQUIRE(blocks < (int64_t(1) << 31), "gnnrec_add_f32: n too large");
+    hipLaunchKernelGGL(add_f32x4_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b),
+                       reinterpret_cast<float4*>(out), n4);
+  } else {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 256 * 32) blocks = 256 * 32;
+    hipLaunchKernelGGL(add_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, out, n);
+  }
+  return check_launch("gnnrec_add_f32");
+}

@@ -32,7 +32,8 @@ template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
-    float* __restrict__ out, int64_t ldo, int empty_neginf, int64_t max_deg) {
+    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg) {
+  const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
   const int col = blockIdx.y * (LPR * VEC) + (lane % LPR) * VEC;
@@ -50,7 +51,10 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
                                                      lane, grp, acc);
     combine_groups<LPR, VEC, REDUCE>(acc);
     finalize<VEC, REDUCE>(acc, end - beg, empty_neginf);
-    if (grp == 0 && colok) store_frag<VEC>(out + row * ldo + col, acc);
+    if (grp == 0 && colok) {
+      if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(acc, out + row * ldo + col);
+      store_frag<VEC>(out + row * ldo + col, acc);
+    }
   }
 }
 
@@ -90,7 +94,8 @@ template <int VEC, int REDUCE>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int64_t* __restrict__ indptr, int d, const int64_t* __restrict__ heavy_rows,
     int64_t n_heavy, const int64_t* __restrict__ chunk_ptr, const float* __restrict__ ws,
-    float* __restrict__ out, int64_t ldo, int empty_neginf, const int64_t* __restrict__ counts) {
+    float* __restrict__ out, int64_t ldo, int flags, const int64_t* __restrict__ counts) {
+  const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
   const int lane = threadIdx.x & 63;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
@@ -109,6 +114,7 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
         for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(acc.v[v], p.v[v]);
       }
       finalize<VEC, REDUCE>(acc, deg, empty_neginf);
+      if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(acc, out + row * ldo + col);
       store_frag<VEC>(out + row * ldo + col, acc);
     }
   }
@@ -147,7 +153,7 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   constexpr int UNROLL = (VEC == 4) ? 4 : 2;
   const int cols_per_slice = LPR * VEC;
   const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
-  const int eni = (a.flags & GNNREC_SPMM_EMPTY_NEGINF) ? 1 : 0;
+  const int eni = a.flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
   const int64_t max_deg = a.n_heavy > 0 ? a.split : INT64_MAX;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid_waves(a.n_dst), slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,

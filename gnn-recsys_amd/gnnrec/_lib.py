@@ -22,6 +22,7 @@ LIB_PATH = os.environ.get("GNNREC_LIB", os.path.join(_HERE, "libgnnrec.so"))
 OK = 0
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
 SPMM_EMPTY_NEGINF = 1
+SPMM_ACCUM = 2
 EPI_RELU, EPI_L2NORM, EPI_SIGMOID = 1, 2, 4
 ACC_STORE, ACC_ADD, ACC_MAX = 0, 1, 2
 ACC_ATTN_FIRST, ACC_ATTN, ACC_ATTN_LAST = 3, 4, 5
@@ -50,7 +51,7 @@ SIGNATURES = {
                                            _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_spmm_backward_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _I64, _I64,
                                         _INT, _P, _I64, _P]),
-    "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P,
+    "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P, _P,
                                _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -68,6 +69,7 @@ SIGNATURES = {
     "gnnrec_csr_transpose": (_INT, [_P, _P, _P, _I64, _I64, _I64, _INT, _P, _U64, _P, _P, _P, _P]),
     "gnnrec_csr_from_keys_workspace_bytes": (_U64, [_I64, _I64]),
     "gnnrec_csr_from_keys": (_INT, [_P, _I64, _I64, _P, _U64, _P, _P, _P]),
+    "gnnrec_add_f32": (_INT, [_P, _P, _P, _I64, _P]),
     "gnnrec_row_epilogue_f32": (_INT, [_P, _I64, _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64,
                                        _P]),
     "gnnrec_act_backward_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _INT, _P, _I64, _P]),

@@ -84,21 +84,24 @@ class Exchange:
             out[i * S:(i + 1) * S].copy_(t)
         return out, None
 
-    def all_to_all_rows(self, full: torch.Tensor) -> torch.Tensor:
-        """full [P·S, d] on every rank -> [P, S, d]: block rk of every rank's table, in
-        source-rank order (the deterministic pass folds them in a fixed tree)."""
+    def all_to_all_rows(self, full: torch.Tensor, async_op: bool = False):
+        """full [P·S, d] on every rank -> ([P, S, d], work|None): block rk of every rank's
+        table, in source-rank order (the deterministic pass folds them in a fixed tree)."""
         S = full.shape[0] // self.ws
+        shape = (self.ws, S) + tuple(full.shape[1:])
         if self.ws == 1:
-            return full.view((1, S) + tuple(full.shape[1:]))
+            return full.view(shape), None
         out = torch.empty_like(full)
         if self.backend == "nccl":
-            dist.all_to_all_single(out, full.contiguous(), group=self.group)
-        else:  # gloo (tests): gather every table, keep our block of each
-            tmp = [torch.empty_like(full) for _ in range(self.ws)]
-            dist.all_gather(tmp, full.contiguous(), group=self.group)
-            for i, t in enumerate(tmp):
-                out[i * S:(i + 1) * S].copy_(t[self.rk * S:(self.rk + 1) * S])
-        return out.view((self.ws, S) + tuple(full.shape[1:]))
+            work = dist.all_to_all_single(out, full.contiguous(), group=self.group,
+                                          async_op=async_op)
+            return out.view(shape), work
+        # gloo (tests): gather every table, keep our block of each
+        tmp = [torch.empty_like(full) for _ in range(self.ws)]
+        dist.all_gather(tmp, full.contiguous(), group=self.group)
+        for i, t in enumerate(tmp):
+            out[i * S:(i + 1) * S].copy_(t[self.rk * S:(self.rk + 1) * S])
+        return out.view(shape), None
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum"):
         if self.ws > 1:

@@ -241,12 +241,11 @@ class ShardedFullGraphPass:
         if deterministic and shard.segments is None:
             raise ValueError("deterministic=True needs a GraphShard built with segments")
         self.deterministic = deterministic
-        if deterministic:
-            fold_embedding = False
         # fold the partitioned type's NodeEmbedding into the first layer's fused launches
         # (one rank, mean/sum reducers): its 10M-row GEMM and table disappear
         self.fold_embedding = fold_embedding
         self._fold = {}  # nt -> (W_emb, b_emb) while h[nt] holds that type's raw features
+        self._folded_types = set()  # types whose embedding was folded in the last run
         self.shard = shard
         self.ex = exchange if exchange is not None else Exchange()
         self.ops = ops_backend if ops_backend is not None else ops
@@ -306,6 +305,7 @@ class ShardedFullGraphPass:
                 if nt == sh.ptype and self.fold_embedding and m.layers and \
                         self._foldable(m.layers[0], h, nt, W):
                     self._fold[nt] = (W.detach(), b.detach())
+                    self._folded_types.add(nt)
                     continue  # h[nt] stays the raw features
                 if nt == sh.ptype and self.side is not None:
                     y = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float32, device=x.device)
@@ -321,28 +321,23 @@ class ShardedFullGraphPass:
         return h
 
     def _foldable(self, hconv, h, nt, W_emb) -> bool:
-        """Every first-layer relation touching nt runs fused with the embedding folded in:
-        one rank, W_emb square at the fused width, no fc_preagg (it is non-linear), reducers
-        mean/sum without edge weights on the source side (linear in the source rows)."""
-        can = getattr(self.ops, 'can_spmm_project', None)
-        if self.ex.ws != 1 or can is None or tuple(W_emb.shape) != (ops.FUSED_D, ops.FUSED_D):
+        """The partitioned type's NodeEmbedding folds into every first-layer relation that
+        touches nt: as the destination (W_self·W_e, bias W_self·b_e — fused kernel or GEMM
+        alike) and as the source when the reducer is linear in the source rows and adds one
+        b_e per non-empty row: mean, no fc_preagg (non-linear), no edge weights (they would
+        scale b_e).  Needs the HIP backend (bias_nonempty) and W_e square at the fused width.
+        Nothing here depends on the world size, so the deterministic mode folds too."""
+        if getattr(self.ops, 'can_spmm_project', None) is None or \
+                tuple(W_emb.shape) != (ops.FUSED_D, ops.FUSED_D):
             return False
-        x = h[nt]
         for ces in self._active(hconv, h).values():
             for ce in ces:
                 if nt not in (ce[0], ce[2]):
                     continue
-                mod = hconv.mods[ce[1]]
-                preagg, weighted, reduce = mod._plan_rel(ce)
+                preagg, weighted, reduce = hconv.mods[ce[1]]._plan_rel(ce)
                 if reduce == 'lstm' or ce[0] == ce[2]:
                     return False
-                if ce[0] == nt and (preagg or weighted or reduce not in ('mean', 'sum')):
-                    return False
-                rs = self.shard.rels[ce]
-                msg = x if ce[0] == nt else h[ce[0]]
-                own = x if ce[2] == nt else h[ce[2]]
-                if preagg or not can(rs.indptr, msg, own, mod.fc_self.weight,
-                                     mod.fc_neigh.weight):
+                if ce[0] == nt and (preagg or weighted or reduce != 'mean'):
                     return False
         return True
 
@@ -399,6 +394,19 @@ class ShardedFullGraphPass:
                 if self.deterministic and reduce in ('sum', 'mean'):
                     partials[ce] = self._tree_partial(rs, msg, weighted, reduce)
                     continue
+                if rs.segs is not None and reduce != 'lstm':
+                    # source-range tiles: each tile gathers from a slice of the source table
+                    # small enough to stay in the Infinity Cache; accumulated in place
+                    op = 'max' if reduce == 'max' else 'sum'
+                    part = torch.empty((rs.n_rows, msg.shape[1]), dtype=torch.float32,
+                                       device=msg.device)
+                    for j, (ip, ix, w) in enumerate(rs.segs):
+                        with self._time('spmm_tile'):
+                            O.spmm(ip, ix, msg, op, edge_weight=w if weighted else None,
+                                   empty_neginf=op == 'max', out=part, accumulate=j > 0)
+                    own, work = self.ex.reduce_scatter_rows(part, op, async_op=self.overlap)
+                    partials[ce] = (own, work, reduce)
+                    continue
                 if self.ex.ws == 1 and reduce != 'lstm' and can_fuse is not None and \
                         not self.deterministic:
                     self_rows = self._get(h, T)
@@ -430,12 +438,20 @@ class ShardedFullGraphPass:
         own contiguous block of segments (a subtree), the all-to-all hands every owner the
         P subtree roots of its rows in rank order, and the owner folds those.  The tree is
         the same at every world size dividing the segment count."""
-        with self._time('spmm'):
-            parts = [self.ops.spmm(ip, ix, msg, 'sum', edge_weight=w if weighted else None)
-                     for ip, ix, w in rs.segs]
-        local = _tree_sum(parts)
-        blocks = self.ex.all_to_all_rows(local)
-        return _tree_sum(list(blocks.unbind(0))), None, reduce
+        # the tree's leaf pairs are formed in the kernel (tile 2i+1 accumulated onto tile 2i:
+        # the same single add), the upper levels by _tree_sum
+        parts = []
+        for j, (ip, ix, w) in enumerate(rs.segs):
+            ew = w if weighted else None
+            with self._time('spmm_tile'):
+                if j % 2 == 0:
+                    parts.append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew))
+                else:
+                    self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[-1],
+                                  accumulate=True)
+        blocks, work = self.ex.all_to_all_rows(_tree_sum(parts, self.ops),
+                                               async_op=self.overlap)
+        return blocks, work, reduce, 'tree'  # the owner's fold waits for the exchange
 
     def _local(self, hconv, h, active, out):
         """item->user style relations: dst rows owned here; GEMMs on the side stream."""
@@ -473,7 +489,7 @@ class ShardedFullGraphPass:
                                     device=msg.device)
                     akw = self._attn(hconv, T, sh.n_own, o.device)
                 Ws, Wn, bias, bias_ne = self._folded(mod, ce)
-                with self._time('spmm'):
+                with self._time('spmm_project'):
                     O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                    rs.weights if weighted else None, relu=True,
                                    l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
@@ -488,9 +504,11 @@ class ShardedFullGraphPass:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
                 akw = self._attn(hconv, T, sh.n_own, o.device)
 
-            def proj(mod=mod, a=a, acc=acc, div=div, o=o, akw=akw):
-                O.gemm(self_rows, mod.fc_self.weight, a, mod.fc_neigh.weight, relu=True,
-                       l2norm=bool(mod.norm), accum=acc, out_div=div, out=o, **akw)
+            Ws, Wn, bias, _ = self._folded(mod, ce)  # the source side is never folded here
+
+            def proj(Ws=Ws, Wn=Wn, bias=bias, mod=mod, a=a, acc=acc, div=div, o=o, akw=akw):
+                O.gemm(self_rows, Ws, a, Wn, bias, relu=True, l2norm=bool(mod.norm), accum=acc,
+                       out_div=div, out=o, **akw)
             ev = self._on_side(proj, self_rows, a, o, *akw.values())
         out[T] = o
         if ev is not None:
@@ -516,25 +534,29 @@ class ShardedFullGraphPass:
                         o = torch.empty((self_rows.shape[0], mod._out_feats),
                                         dtype=torch.float32, device=msg.device)
                     Ws, Wn, bias, bias_ne = self._folded(mod, ce)
-                    with self._time('spmm'):
+                    with self._time('spmm_project'):
                         O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                        rs.weights if weighted else None, relu=True,
                                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                                        bias=bias, bias_nonempty=bias_ne, **akw)
                     self.fused.add(ce)
                     continue
-                own, work, reduce = partials[ce]
+                own, work, reduce = partials[ce][:3]
                 if work is not None:
                     work.wait()
+                if len(partials[ce]) == 4:  # deterministic: fold the P subtree roots
+                    own = _tree_sum(list(own.unbind(0)), self.ops)
                 if o is None:
                     o = torch.empty((own.shape[0], mod._out_feats), dtype=torch.float32,
                                     device=own.device)
-                O.gemm(self_rows, mod.fc_self.weight, own, mod.fc_neigh.weight, relu=True,
+                Ws, Wn, bias, bias_ne = self._folded(mod, ce)
+                fkw = {} if bias_ne is None else {'bias_nonempty': bias_ne}
+                O.gemm(self_rows, Ws, own, Wn, bias, relu=True,
                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
                        a2_deg=sh.rels[ce].deg_own,
                        a2_mode=(_lib.A2_NONE if reduce == 'lstm' else
                                 _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG),
-                       **akw)
+                       **akw, **fkw)
             if self.ex.ws == 1:  # the owned rows ARE the table
                 out[T] = o
                 continue
@@ -559,10 +581,12 @@ class ShardedFullGraphPass:
         return out
 
 
-def _tree_sum(parts: List[torch.Tensor]) -> torch.Tensor:
-    """Pairwise tree ((p0+p1)+(p2+p3))+... over a power-of-two list, in order."""
+def _tree_sum(parts: List[torch.Tensor], O) -> torch.Tensor:
+    """Pairwise tree ((p0+p1)+(p2+p3))+... over a power-of-two list, in order (in place
+    into the left operand: one add kernel per node)."""
+    parts = [p.contiguous() for p in parts]
     while len(parts) > 1:
-        parts = [torch.add(parts[i], parts[i + 1]) for i in range(0, len(parts), 2)]
+        parts = [O.add_(parts[i], parts[i + 1]) for i in range(0, len(parts), 2)]
     return parts[0]
 
 

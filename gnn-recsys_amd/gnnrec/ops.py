@@ -107,11 +107,14 @@ def _device_plan(indptr: torch.Tensor, split: int):
 
 def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: str = "mean",
          edge_weight: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-         empty_neginf: bool = False, split: Optional[int] = DEFAULT_SPLIT) -> torch.Tensor:
+         empty_neginf: bool = False, split: Optional[int] = DEFAULT_SPLIT,
+         accumulate: bool = False) -> torch.Tensor:
     """a1: out[v] = reduce_{e in row v} X[indices[e]] (* edge_weight[e]).
 
     indptr int64 [n_dst+1], indices int32 [E] (local rows of X), X fp32 [n_src, d].
     Rows with more than `split` edges are reduced in parallel chunks (split=None: never).
+    accumulate: out[v] = out[v] (+ | max) that (source-range tiles of one relation; max
+    needs empty_neginf so rows without edges in the tile leave out unchanged).
     """
     lib = _lib.load()
     _dev(indptr, "indptr", torch.int64)
@@ -128,6 +131,8 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
             raise ValueError("edge_weight must have one value per edge")
         edge_weight = edge_weight.contiguous()
     if out is None:
+        if accumulate:
+            raise ValueError("spmm: accumulate needs out")
         out = torch.empty((n_dst, d), dtype=torch.float32, device=X.device)
     else:
         _dev(out, "out", torch.float32)
@@ -135,6 +140,10 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
             raise ValueError(f"out must be [{n_dst}, {d}]")
     ldo = _rowmajor(out, "out")
     flags = _lib.SPMM_EMPTY_NEGINF if empty_neginf else 0
+    if accumulate:
+        if reduce == "max" and not empty_neginf:
+            raise ValueError("spmm: max accumulation needs empty_neginf")
+        flags |= _lib.SPMM_ACCUM
     if split and getattr(indptr, "_gnnrec_split_plan", None) is None and \
             getattr(indptr, "_gnnrec_nnz", None) is not None:
         # edge count known, degrees not: heavy-row plan built on the device (no readback)
@@ -213,6 +222,18 @@ def csr_from_keys(keys: torch.Tensor, n_rows: int):
     return ip, perm
 
 
+def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a += b (same shape, contiguous fp32) with the library's add kernel; returns a."""
+    lib = _lib.load()
+    _dev(a, "a", torch.float32)
+    _dev(b, "b", torch.float32)
+    if a.shape != b.shape or not (a.is_contiguous() and b.is_contiguous()):
+        raise ValueError("add_: operands must be contiguous and of one shape")
+    check(lib.gnnrec_add_f32(ptr(a), ptr(b), ptr(a), a.numel(), stream_ptr(a.device)),
+          "gnnrec_add_f32")
+    return a
+
+
 def spmm_backward(indptr, indices, grad_out, reduce, edge_weight=None, X=None, out=None,
                   grad_X=None, n_src=None):
     """Gradient of spmm w.r.t. its source rows (accumulated into grad_X, created if None)."""
@@ -237,8 +258,10 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
          accum: str = "store", out_div: float = 0.0, out: Optional[torch.Tensor] = None,
          a2_deg: Optional[torch.Tensor] = None, a2_mode: int = _lib.A2_NONE,
          attn_vec: Optional[torch.Tensor] = None,
-         attn_state: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias).  W are nn.Linear weights [N, K]."""
+         attn_state: Optional[torch.Tensor] = None,
+         bias_nonempty: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias [+ bias_nonempty where
+    a2_deg > 0]).  W are nn.Linear weights [N, K]."""
     lib = _lib.load()
     _dev(A1, "A1", torch.float32)
     _dev(W1, "W1", torch.float32)
@@ -260,8 +283,11 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
     if bias is not None:
         _dev(bias, "bias", torch.float32)
         bias = bias.contiguous()
-    if a2_mode != _lib.A2_NONE:
+    if a2_mode != _lib.A2_NONE or bias_nonempty is not None:
         _dev(a2_deg, "a2_deg", torch.int32)
+    if bias_nonempty is not None:
+        _dev(bias_nonempty, "bias_nonempty", torch.float32)
+        bias_nonempty = bias_nonempty.contiguous()
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0) | (
         _lib.EPI_SIGMOID if sigmoid else 0)
     if out is None:
@@ -278,13 +304,14 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
         # the row norm / attention score needs the whole row: GEMM (bias, ReLU, sigmoid)
         # into a scratch table, then one row-epilogue pass into out
         z = gemm(A1, W1, A2, W2, bias, relu=relu, sigmoid=sigmoid, a2_deg=a2_deg,
-                 a2_mode=a2_mode)
+                 a2_mode=a2_mode, bias_nonempty=bias_nonempty)
         check(lib.gnnrec_row_epilogue_f32(ptr(z), N, M, N, int(l2norm), ACCUM[accum],
                                           float(out_div), ptr(av), ptr(ast), ptr(out), ldo,
                                           stream_ptr(A1.device)), "gnnrec_row_epilogue_f32")
         return out
     rc = lib.gnnrec_gemm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2), ptr(a2_deg),
-                             a2_mode, ptr(bias), M, N, epi, ACCUM[accum], float(out_div),
+                             a2_mode, ptr(bias), ptr(bias_nonempty), M, N, epi, ACCUM[accum],
+                             float(out_div),
                              ptr(av), ptr(ast), ptr(out), ldo, stream_ptr(A1.device))
     check(rc, "gnnrec_gemm_f32")
     return out

@@ -60,6 +60,8 @@ extern "C" {
 /* gnnrec_spmm_csr_f32 flags */
 #define GNNREC_SPMM_EMPTY_NEGINF 1 /* MAX: leave rows with no edge at -inf (partial
                                       maxima that are max-reduced across ranks) */
+#define GNNREC_SPMM_ACCUM 2        /* out = out (+ | max) result: accumulate source-range
+                                      tiles of one relation into one partial table */
 
 /* gnnrec_gemm_f32 epilogue bits */
 #define GNNREC_EPI_RELU 1
@@ -141,12 +143,16 @@ int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* indices, cons
  * z = epi(acc + bias)      epi: relu / sigmoid, then optional row L2 norm
  * out = accumulate(out, z) (store | add | max), then out /= out_div if out_div > 0.
  * A2/W2 may be NULL with K2 == 0.  bias may be NULL.  N <= 256 when L2NORM.
+ * bias_nonempty (nullable, needs a2_deg) is added before epi only on rows with
+ * a2_deg > 0: a NodeEmbedding (W_e, b_e) folded into the neighbour side contributes
+ * W_neigh b_e exactly on rows that have neighbours (the empty mean is 0, not b_e).
  * Replaces fc_self(h_self)+fc_neigh(h_neigh), relu, norm (src/model.py:226-235) and
  * HeteroGraphConv's cross-relation sum/mean/max (src/model.py:384-406). */
 int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                     const float* A2, int64_t lda2, int64_t K2, const float* W2,
                     const int32_t* a2_deg, int a2_mode, const float* bias,
-                    int64_t M, int64_t N, int epilogue, int accum, float out_div,
+                    const float* bias_nonempty, int64_t M, int64_t N, int epilogue, int accum,
+                    float out_div,
                     const float* attn_vec, float* attn_state,
                     float* out, int64_t ldo, void* stream);
 
@@ -266,6 +272,10 @@ int gnnrec_csr_transpose(const int64_t* indptr, const int32_t* indices, const fl
 size_t gnnrec_csr_from_keys_workspace_bytes(int64_t n_edges, int64_t n_rows);
 int gnnrec_csr_from_keys(const int32_t* keys, int64_t n_edges, int64_t n_rows, void* workspace,
                          size_t workspace_bytes, int64_t* indptr, int32_t* perm, void* stream);
+
+/* out[i] = a[i] + b[i] over n floats (out may alias a or b): the upper levels of the
+ * deterministic pass's fixed pairwise tree over source-range partial tables. */
+int gnnrec_add_f32(const float* a, const float* b, float* out, int64_t n, void* stream);
 
 /* Row epilogue for projections wider than one GEMM block (N > 256): out (accum)=
  * l2norm?(z) row by row, accum / out_div / attention as gnnrec_gemm_f32.  z holds the

@@ -10,13 +10,16 @@ import torch
 from oracle import oracle
 
 
-def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_neginf=False):
+def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_neginf=False,
+         accumulate=False):
     ip = indptr.cpu().numpy()
     res = oracle.spmm_csr(ip, indices.cpu().numpy(), X.detach().cpu().numpy(), reduce,
                           None if edge_weight is None else edge_weight.cpu().numpy())
     if reduce == "max" and empty_neginf:
         res[(ip[1:] - ip[:-1]) == 0] = -np.inf
     t = torch.from_numpy(res)
+    if accumulate:
+        t = torch.maximum(out, t) if reduce == "max" else out + t
     if out is not None:
         out.copy_(t)
         return out
@@ -43,9 +46,12 @@ def _attn_update(out, t, accum, attn_vec, attn_state):
 
 def gemm(A1, W1, A2=None, W2=None, bias=None, *, relu=False, l2norm=False, sigmoid=False,
          accum="store", out_div=0.0, out=None, a2_deg=None, a2_mode=0, attn_vec=None,
-         attn_state=None):
+         attn_state=None, bias_nonempty=None):
     z = oracle.linear(A1.detach().cpu().numpy(), W1.detach().cpu().numpy(),
                       None if bias is None else bias.detach().cpu().numpy())
+    if bias_nonempty is not None:
+        ne = (a2_deg.cpu().numpy() > 0)[:, None]
+        z = (z + np.where(ne, bias_nonempty.detach().cpu().numpy(), np.float32(0))).astype(np.float32)
     if A2 is not None:
         a2 = A2.detach().cpu().numpy().astype(np.float32)
         if a2_mode == 1:
@@ -77,3 +83,8 @@ def gemm(A1, W1, A2=None, W2=None, bias=None, *, relu=False, l2norm=False, sigmo
         t = t / out_div
     out.copy_(t)
     return out
+
+
+def add_(a, b):
+    a += b
+    return a

@@ -35,7 +35,8 @@ def _worker(rank, world, port, case, q):
         from gnnrec.graph import HeteroGraph
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
 
-        case, _, det = case.partition("#")  # "#det": deterministic segment mode
+        case, _, det = case.partition("#")  # "#det": deterministic segment mode, "#seg": tiles
+        seg, det = det == "seg", det == "det"
         case, _, hetero = case.partition("@")  # "@attention": build-defined hetero mode
         meta = dict(golden_io.manifest()[case])
         if hetero:
@@ -56,7 +57,7 @@ def _worker(rank, world, port, case, q):
         model.eval()
         ex = Exchange()
         shard = GraphShard.from_graph(g, rank, world, "user", device="cpu",
-                                      segments=8 if det else None)
+                                      segments=8 if (det or seg) else None)
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
         p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
         out = p.run(shard.local_features(feats))
@@ -106,6 +107,8 @@ def _run(case, world):
     ("model_het_meannnedge_mean_emb#det", 2),
     ("model_het_mean_sum_skip@attention#det", 4),
     ("model_het_meanedge_max_emb#det", 8),
+    ("model_het_meannnedge_mean_emb#seg", 1),
+    ("model_het_meanedge_max_emb#seg", 2),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
     """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a

@@ -43,7 +43,7 @@ def _build(agg, hetero, d=32):
     return g, feats, model
 
 
-def _worker(rank, world, port, agg, hetero, d, q, segments=None):
+def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -54,8 +54,8 @@ def _worker(rank, world, port, agg, hetero, d, q, segments=None):
         g, feats, model = _build(agg, hetero, d)
         ex = Exchange()
         sh = GraphShard.from_graph(g, rank, world, "user", device="cuda", segments=segments)
-        out = ShardedFullGraphPass(model, sh, ex, deterministic=segments is not None).run(
-            sh.local_features(feats))
+        det = segments is not None if det is None else det
+        out = ShardedFullGraphPass(model, sh, ex, deterministic=det).run(sh.local_features(feats))
         users = gather_partitioned(sh, out["user"], ex)
         q.put((rank, users.cpu().numpy(), out["item"][:700].cpu().numpy()))
     finally:
@@ -118,3 +118,40 @@ def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
         for rank, users, items in res:
             assert np.array_equal(users, base[0]), f"P={world} rank {rank}: users differ"
             assert np.array_equal(items, base[1]), f"P={world} rank {rank}: items differ"
+
+
+@pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 128), ("mean_nn", "attention", 128),
+                                          ("pool_nn", "max", 32)])
+def test_source_tiles_match_single_process(agg, hetero, d):
+    """Source-range tiles (segments=8, default mode): the user->item relation is gathered
+    tile by tile into one partial (GNNREC_SPMM_ACCUM), with the NodeEmbedding folded into
+    the GEMM (bias on non-empty rows) — at one rank and at two."""
+    import torch.multiprocessing as mp
+    from gnnrec.dist import Exchange
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    g, feats, model = _build(agg, hetero, d)
+    with torch.no_grad():
+        ref = full_graph_embeddings(g, model, feats)
+    sh = GraphShard.from_graph(g, 0, 1, "user", device="cuda", segments=8)
+    runner = ShardedFullGraphPass(model, sh, Exchange())
+    one = runner.run(sh.local_features(feats))
+    if agg == "mean" and d == 128:
+        assert runner._fold == {} and "user" in runner._folded_types
+    np.testing.assert_allclose(one["user"].cpu().numpy(), ref["user"].cpu().numpy(), rtol=1e-4,
+                               atol=1e-5)
+    np.testing.assert_allclose(one["item"][:700].cpu().numpy(), ref["item"].cpu().numpy(),
+                               rtol=1e-4, atol=1e-5)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, agg, hetero, d, q, 8, False))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for _, users, items in res:
+        np.testing.assert_allclose(users, ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(items, ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)

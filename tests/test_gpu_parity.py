@@ -975,3 +975,31 @@ def test_csr_transpose_bit_exact(n_dst, n_src, max_deg, weighted, mean):
             inv = (np.float32(1) / np.maximum(deg, 1).astype(np.float32))[dst]
             w = (w * inv).astype(np.float32)
         np.testing.assert_array_equal(w_t.cpu().numpy(), w[order])
+
+
+@pytest.mark.parametrize("reduce,split", [("sum", None), ("max", None), ("sum", 64), ("max", 64)])
+def test_spmm_accumulate_tiles_equal_whole_relation(reduce, split):
+    """Source-range tiles of one relation accumulated in place (GNNREC_SPMM_ACCUM) == the
+    whole relation's aggregate (max: exactly; sum: to rounding), heavy rows included."""
+    from gnnrec import ops
+    rng = np.random.default_rng(7)
+    n_dst, n_src, d = 500, 4000, 64
+    deg = rng.integers(0, 300, n_dst)
+    deg[:3] = 3000
+    indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    idx = rng.integers(0, n_src, int(indptr[-1])).astype(np.int32)
+    X = _t(rng.standard_normal((n_src, d)).astype(np.float32))
+    whole = ops.spmm(_t(indptr), _t(idx), X, reduce, empty_neginf=reduce == "max", split=split)
+    dst = np.repeat(np.arange(n_dst), deg)
+    out = torch.empty((n_dst, d), device=DEV)
+    for j, (lo, hi) in enumerate([(0, 1000), (1000, 2500), (2500, n_src)]):
+        sel = (idx >= lo) & (idx < hi)
+        ip = np.concatenate([[0], np.cumsum(np.bincount(dst[sel], minlength=n_dst))])
+        ops.spmm(_t(ip.astype(np.int64)), _t(idx[sel]), X, reduce, out=out,
+                 empty_neginf=reduce == "max", split=split, accumulate=j > 0)
+    if reduce == "max":
+        assert torch.equal(out, whole)
+    else:
+        np.testing.assert_allclose(out.cpu().numpy(), whole.cpu().numpy(), rtol=1e-5, atol=1e-4)
+    with pytest.raises(ValueError):
+        ops.spmm(_t(indptr), _t(idx), X, "max", out=out, accumulate=True)

@@ -271,6 +271,7 @@ def test_reversed_gather_backward_matches_atomic(monkeypatch):
                 x = m.clone().requires_grad_(True)
                 (SpmmFn.apply(x, indptr, indices, w, reduce, n_dst) * g).sum().backward()
                 grads.append(x.grad)
+            # atomic order is arbitrary: sums of ~30 terms of size ~1 agree to ~1e-6 absolute
             np.testing.assert_allclose(grads[0].cpu().numpy(), grads[1].cpu().numpy(), rtol=1e-5,
-                                       atol=1e-6)
+                                       atol=1e-5)
             assert torch.equal(grads[1], grads[2])

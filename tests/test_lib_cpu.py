@@ -43,10 +43,10 @@ def test_argument_validation_without_a_gpu():
     rc = lib.gnnrec_spmm_csr_f32(None, None, None, None, 4, 3, 4, 7, 0, None, 4, None)
     assert rc == _lib.OK + 1
     assert b"unknown reduce" in lib.gnnrec_last_error()
-    rc = lib.gnnrec_gemm_f32(None, 4, 4, None, None, 1, 0, None, None, 0, None, 10, 300,
+    rc = lib.gnnrec_gemm_f32(None, 4, 4, None, None, 1, 0, None, None, 0, None, None, 10, 300,
                              _lib.EPI_L2NORM, 0, 0.0, None, None, ctypes.c_void_p(16), 300, None)
     assert rc != 0 and b"A1" in lib.gnnrec_last_error()
-    rc = lib.gnnrec_gemm_f32(None, 4, 0, None, None, 1, 0, None, None, 0, None, 10, 8, 0,
+    rc = lib.gnnrec_gemm_f32(None, 4, 0, None, None, 1, 0, None, None, 0, None, None, 10, 8, 0,
                              _lib.ACC_ATTN, 0.0, None, None, ctypes.c_void_p(16), 8, None)
     assert rc != 0 and b"attention" in lib.gnnrec_last_error()
     # empty problems are no-ops that succeed without touching memory

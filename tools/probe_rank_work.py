@@ -1,8 +1,9 @@
 """Per-rank compute of the sharded C4 pass at P ranks, measured on one GPU.
 
-Builds rank 0's shard of the P-way partition (its users' edges, the replicated item
-table) and runs ShardedFullGraphPass with an exchange that reports world size P but
-moves nothing (reduce-scatter = slice of the local partial, all-gather = local copy).
+Builds rank 0's shard of the P-way partition (its users' edges in 8/P source tiles, the
+replicated item table) and runs the bench's default pass (deterministic mode) with an
+exchange that reports world size P but moves nothing (all-to-all = the local partial's P
+blocks, all-gather = local copy).
 The time is what one rank computes per pass; the collectives come on top (overlapped
 with the local aggregation in the real run).
 
@@ -31,6 +32,10 @@ class LocalExchange:
         S = full.shape[0] // self.ws
         return full[:S], None
 
+    def all_to_all_rows(self, full, async_op=False):
+        S = full.shape[0] // self.ws
+        return full.view((self.ws, S) + tuple(full.shape[1:])), None
+
     def all_gather_rows(self, own, out, async_op=False):
         out[: own.shape[0]].copy_(own)
         return out, None
@@ -48,14 +53,14 @@ def main():
     n_u, n_i, E, d = 10_000_000, 1_000_000, 500_000_000, 128
     res = {}
     for P in ps:
-        sh = bipartite_shard(n_u, n_i, E, 0, P, dev)
+        sh = bipartite_shard(n_u, n_i, E, 0, P, dev, segments=8)
         feats = sh.local_features({"user": node_features(n_u, d, 0, dev),
                                    "item": node_features(n_i, d, 1, dev)})
         torch.manual_seed(0)
         meta = GraphMeta(sh.canonical_etypes, ["item", "user"])
         model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
                               "mean", "cos", "sum", True).to(dev).eval()
-        runner = ShardedFullGraphPass(model, sh, LocalExchange(P))
+        runner = ShardedFullGraphPass(model, sh, LocalExchange(P), deterministic=True)
         for _ in range(2):
             runner.run(feats)
         torch.cuda.synchronize()
