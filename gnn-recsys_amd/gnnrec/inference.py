@@ -259,6 +259,7 @@ class ShardedFullGraphPass:
                      if overlap and shard.device.type == 'cuda' else None)
         self.timers = None  # optional callable(tag) -> context manager (bench)
         self.fused = set()  # relations whose aggregation ran with the projection fused
+        self._last, self._replicate_last = False, True
 
     def _get(self, h, nt):
         w = self._pending.pop(id(h[nt]), None)
@@ -289,10 +290,14 @@ class ShardedFullGraphPass:
         return ev
 
     @torch.no_grad()
-    def run(self, feats: Dict[str, torch.Tensor], embedding_layer: Optional[bool] = None):
+    def run(self, feats: Dict[str, torch.Tensor], embedding_layer: Optional[bool] = None,
+            replicate_output: bool = True):
         """feats: this rank's inputs (see GraphShard.local_features) -> this rank's outputs:
-        {ptype: [n_own, out]} and the replicated types as full padded tables."""
+        {ptype: [n_own, out]} and the replicated types as full padded tables, or — with
+        replicate_output=False — as this rank's own row block of them (own_slice), so the
+        last layer's all-gather is skipped and every type's output stays partitioned."""
         m, O, sh = self.model, self.ops, self.shard
+        self._replicate_last = replicate_output
         if embedding_layer is None:
             embedding_layer = m.embedding_layer
         h = dict(feats)
@@ -314,7 +319,8 @@ class ShardedFullGraphPass:
                     h[nt] = y
                 else:
                     h[nt] = O.gemm(x, W, bias=b)
-        for layer in m.layers:
+        for i, layer in enumerate(m.layers):
+            self._last = i == len(m.layers) - 1
             h = self._layer(layer, h)
         for nt in list(h):
             self._get(h, nt)
@@ -557,8 +563,8 @@ class ShardedFullGraphPass:
                        a2_mode=(_lib.A2_NONE if reduce == 'lstm' else
                                 _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG),
                        **akw, **fkw)
-            if self.ex.ws == 1:  # the owned rows ARE the table
-                out[T] = o
+            if self.ex.ws == 1 or (self._last and not self._replicate_last):
+                out[T] = o  # the owned rows ARE the table (one rank), or stay partitioned
                 continue
             table = torch.empty((sh.padded_rows(T), o.shape[1]), dtype=torch.float32,
                                 device=o.device)

@@ -36,7 +36,7 @@ def _worker(rank, world, port, case, q):
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
 
         case, _, det = case.partition("#")  # "#det": deterministic segment mode, "#seg": tiles
-        seg, det = det == "seg", det == "det"
+        seg, part, det = det == "seg", det == "part", det == "det"
         case, _, hetero = case.partition("@")  # "@attention": build-defined hetero mode
         meta = dict(golden_io.manifest()[case])
         if hetero:
@@ -60,12 +60,17 @@ def _worker(rank, world, port, case, q):
                                       segments=8 if (det or seg) else None)
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
         p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
-        out = p.run(shard.local_features(feats))
+        out = p.run(shard.local_features(feats), replicate_output=not part)
         users = gather_partitioned(shard, out["user"], ex)
         res = {"user": users.numpy()}
         for nt in out:
             if nt != "user":
-                res[nt] = out[nt][: num_nodes[nt]].numpy()
+                if part:  # each rank holds its own row block: assemble them here to compare
+                    full = torch.empty((shard.padded_rows(nt), out[nt].shape[1]))
+                    ex.all_gather_rows(out[nt].contiguous(), full)
+                    res[nt] = full[: num_nodes[nt]].numpy()
+                else:
+                    res[nt] = out[nt][: num_nodes[nt]].numpy()
         q.put((rank, res, shard.local_edge_count(), shard.global_edge_count()))
     finally:
         dist.destroy_process_group()
@@ -109,6 +114,7 @@ def _run(case, world):
     ("model_het_meanedge_max_emb#det", 8),
     ("model_het_meannnedge_mean_emb#seg", 1),
     ("model_het_meanedge_max_emb#seg", 2),
+    ("model_het_mean_sum_skip#part", 4),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
     """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a
