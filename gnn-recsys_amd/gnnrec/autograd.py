@@ -129,19 +129,19 @@ class SageProjectFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h_self, agg, Ws, Wn, norm: bool):
-        z = ops.gemm(h_self.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True,
-                     l2norm=norm)
-        ctx.save_for_backward(h_self, agg, Ws, Wn)
+        # y = relu(u) is kept for the backward (its mask and row norm are all the epilogue's
+        # Jacobian needs), so the backward does not recompute the K=2d GEMM
+        y = ops.gemm(h_self.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True)
+        z = ops.l2_normalize_rows(y) if norm else y
+        ctx.save_for_backward(h_self, agg, Ws, Wn, y)
         ctx.norm = norm
         return z
 
     @staticmethod
     def backward(ctx, gz):
-        h_self, agg, Ws, Wn = ctx.saved_tensors
+        h_self, agg, Ws, Wn, y = ctx.saved_tensors
         need = ctx.needs_input_grad
-        u = ops.gemm(h_self.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach())
-        gu = ops.act_backward(u, gz, relu=True, l2norm=ctx.norm)
-        del u
+        gu = ops.act_backward(y, gz, relu=True, l2norm=ctx.norm)  # relu(y) = y, same mask
         g_self = ops.gemm(gu, Ws.t().contiguous()) if need[0] else None
         g_agg = ops.gemm(gu, Wn.t().contiguous()) if need[1] else None
         g_Ws = ops.gemm_tn(gu, h_self.contiguous()) if need[2] else None

@@ -234,6 +234,21 @@ def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return a
 
 
+def l2_normalize_rows(y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = y / ‖y‖ per row, rows with ‖y‖ == 0 unchanged (src/model.py:230-235), one
+    wave per row (gnnrec_row_epilogue_f32)."""
+    lib = _lib.load()
+    _dev(y, "y", torch.float32)
+    M, N = y.shape
+    ldy = _rowmajor(y, "y")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=y.device)
+    check(lib.gnnrec_row_epilogue_f32(ptr(y), ldy, M, N, 1, ACCUM["store"], 0.0, 0, 0, ptr(out),
+                                      _rowmajor(out, "out"), stream_ptr(y.device)),
+          "gnnrec_row_epilogue_f32")
+    return out
+
+
 def spmm_backward(indptr, indices, grad_out, reduce, edge_weight=None, X=None, out=None,
                   grad_X=None, n_src=None):
     """Gradient of spmm w.r.t. its source rows (accumulated into grad_X, created if None)."""
