@@ -27,7 +27,7 @@ inline unsigned key_bits(int64_t n_src) {
 
 size_t sort_temp_bytes(int64_t E, int64_t n_src, hipStream_t s) {
   size_t bytes = 0;
-  rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
                             (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)E, 0,
                             key_bits(n_src), s);
   return bytes;

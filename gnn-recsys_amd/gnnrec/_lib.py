@@ -82,6 +82,13 @@ SIGNATURES = {
     "gnnrec_clear_prefix_pos": (_INT, [_P, _I64, _P, _P]),
     "gnnrec_topk_rows_f32": (_INT, [_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "gnnrec_synth_edges": (_INT, [_U64, _I64, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "gnnrec_margin_loss_blocks": (_I64, [_I64]),
+    "gnnrec_margin_loss_f32": (_INT, [_P, _P, _I64, _I64, _F32, _P, _P, _INT, _P, _P, _P, _I64,
+                                      _P]),
+    "gnnrec_sum_scaled_f32": (_INT, [_P, _I64, _F32, _P, _P]),
+    "gnnrec_sddmm_cos_backward_workspace_bytes": (_U64, [_I64, _I64, _I64, _I64]),
+    "gnnrec_sddmm_cos_backward_f32": (_INT, [_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64,
+                                             _P, _P, _P, _P, _U64, _P]),
 }
 
 _lib = None

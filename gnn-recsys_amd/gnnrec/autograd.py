@@ -81,7 +81,9 @@ def _spmm_reversed(indptr, indices, g, ew, reduce: str, n_src: int, nnz=None):
     gSpMM over the source-major CSR of the same edges (rows = sources)."""
     ip_t, ix_t, w_t = ops.csr_transpose(indptr, indices, n_src, edge_weight=ew,
                                         mean=reduce == 'mean', n_edges=nnz)
-    return ops.spmm(ip_t, ix_t, g.contiguous(), 'sum', edge_weight=w_t)
+    if g.stride(-1) != 1:
+        g = g.contiguous()
+    return ops.spmm(ip_t, ix_t, g, 'sum', edge_weight=w_t)  # g may be a strided row view
 
 
 class LstmAggFn(torch.autograd.Function):
@@ -125,32 +127,59 @@ class LstmAggFn(torch.autograd.Function):
 
 
 class SageProjectFn(torch.autograd.Function):
-    """z = norm?(relu(h_self W_selfᵀ + agg W_neighᵀ)); forward = fused gnnrec_gemm_f32."""
+    """z = norm?(relu(h_self W_selfᵀ + agg W_neighᵀ)); forward = fused gnnrec_gemm_f32.
+
+    n_self > 0: h_self is a block's whole source table, whose first n_self rows are the
+    destination rows (DGL blocks keep the dst nodes as the src prefix).  Its gradient then
+    comes back for the whole table (zero past n_self) and autograd adds it to the table's
+    other gradient directly, instead of a slice backward (zero fill + copy) and an add."""
 
     @staticmethod
-    def forward(ctx, h_self, agg, Ws, Wn, norm: bool):
+    def forward(ctx, h_self, agg, Ws, Wn, norm: bool, n_self: int = 0):
+        hs = h_self[:n_self] if n_self else h_self
         # y = relu(u) is kept for the backward (its mask and row norm are all the epilogue's
         # Jacobian needs), so the backward does not recompute the K=2d GEMM
-        y = ops.gemm(h_self.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True)
+        y = ops.gemm(hs.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True)
         z = ops.l2_normalize_rows(y) if norm else y
         ctx.save_for_backward(h_self, agg, Ws, Wn, y)
-        ctx.norm = norm
+        ctx.norm, ctx.n_self = norm, n_self
         return z
 
     @staticmethod
     def backward(ctx, gz):
         h_self, agg, Ws, Wn, y = ctx.saved_tensors
         need = ctx.needs_input_grad
+        M = y.shape[0]
+        hs = h_self[:M]
         gu = ops.act_backward(y, gz, relu=True, l2norm=ctx.norm)  # relu(y) = y, same mask
-        g_self = ops.gemm(gu, Ws.t().contiguous()) if need[0] else None
-        g_agg = ops.gemm(gu, Wn.t().contiguous()) if need[1] else None
-        g_Ws = ops.gemm_tn(gu, h_self.contiguous()) if need[2] else None
+        g_self = g_agg = None
+        if need[0] and need[1]:
+            # both input gradients from one GEMM: gu · [W_self | W_neigh] -> [rows, d_s + d_n]
+            d_s = Ws.shape[1]
+            R = torch.empty((h_self.shape[0], d_s + Wn.shape[1]), dtype=torch.float32,
+                            device=gu.device)
+            ops.gemm(gu, torch.cat([Ws.detach().t(), Wn.detach().t()], 0), out=R[:M])
+            if h_self.shape[0] > M:
+                R[M:, :d_s].zero_()
+            g_self, g_agg = R[:, :d_s], R[:M, d_s:]
+        elif need[0] or need[1]:
+            W = Ws if need[0] else Wn
+            g = ops.gemm(gu, W.detach().t().contiguous())
+            if need[0] and h_self.shape[0] > M:
+                full = torch.zeros((h_self.shape[0], g.shape[1]), dtype=g.dtype,
+                                   device=g.device)
+                full[:M] = g
+                g = full
+            g_self, g_agg = (g, None) if need[0] else (None, g)
+        g_Ws = ops.gemm_tn(gu, hs.contiguous()) if need[2] else None
         g_Wn = ops.gemm_tn(gu, agg.contiguous()) if need[3] else None
-        return g_self, g_agg, g_Ws, g_Wn, None
+        return g_self, g_agg, g_Ws, g_Wn, None, None
 
 
 class CosineFn(torch.autograd.Function):
-    """cos_e = <ĥs[src_e], ĥd[dst_e]>; forward = gnnrec_sddmm_cos_f32."""
+    """cos_e = <ĥs[src_e], ĥd[dst_e]>; forward = gnnrec_sddmm_cos_f32, backward =
+    gnnrec_sddmm_cos_backward_f32 (both reduction sides of the SDDMM backward as weighted
+    gathers over the pair graph grouped by src / by dst, in one library call)."""
 
     @staticmethod
     def forward(ctx, hs, hd, src, dst):
@@ -162,33 +191,35 @@ class CosineFn(torch.autograd.Function):
     def backward(ctx, g):
         hs, hd, src, dst = ctx.saved_tensors
         need = ctx.needs_input_grad
-        g = g.reshape(-1).contiguous()
-        # â = h / max(‖h‖, eps): gradient wrt â, then through the normalisation
-        a_hat, a_n = _normalize(hs)
-        b_hat, b_n = _normalize(hd)
-        ga = gb = None
-        if need[0]:  # Gâ[s] = Σ_{e: src_e = s} g_e b̂[dst_e]
-            ip, perm = ops.csr_from_keys(src, hs.shape[0])
-            ga = _normalize_backward(a_hat, a_n, ops.spmm(ip, dst[perm].to(torch.int32), b_hat,
-                                                          "sum", edge_weight=g[perm]))
-        if need[1]:  # Gb̂[d] = Σ_{e: dst_e = d} g_e â[src_e]
-            ip, perm = ops.csr_from_keys(dst, hd.shape[0])
-            gb = _normalize_backward(b_hat, b_n, ops.spmm(ip, src[perm].to(torch.int32), a_hat,
-                                                          "sum", edge_weight=g[perm]))
+        if not (need[0] or need[1]):
+            return None, None, None, None
+        ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(),
+                                        g.reshape(-1), need[0], need[1])
         return ga, gb, None, None
 
 
-_EPS = 1e-12
+class MarginLossFn(torch.autograd.Function):
+    """max_margin_loss (src/model.py:473-533) over every etype at once: the forward kernel
+    also writes d(sum of scores)/d(score), so the backward is one scale.
+    apply(spec, pos_0, neg_0, pos_1, neg_1, ...) with spec = (delta, [(K, mask, recency)])."""
 
+    @staticmethod
+    def forward(ctx, spec, *scores):
+        delta, meta = spec
+        parts = [(scores[2 * i].reshape(-1), scores[2 * i + 1].reshape(-1), K, mask, rec)
+                 for i, (K, mask, rec) in enumerate(meta)]
+        loss, total, grads = ops.margin_loss(parts, delta)
+        ctx.grads, ctx.total = grads, total
+        ctx.shapes = [t.shape for t in scores]
+        return loss
 
-def _normalize(h):
-    """F.normalize(h, p=2, dim=-1) (eps 1e-12) and the row norms."""
-    n = h.norm(2, 1, keepdim=True)
-    return h / n.clamp_min(_EPS), n
-
-
-def _normalize_backward(h_hat, n, g_hat):
-    """gradient of h_hat = h / max(‖h‖, eps) given d/dh_hat."""
-    big = n > _EPS
-    dot = (h_hat * g_hat).sum(1, keepdim=True)
-    return torch.where(big, (g_hat - h_hat * dot) / n.clamp_min(_EPS), g_hat / _EPS)
+    @staticmethod
+    def backward(ctx, g):
+        scale = g / ctx.total
+        out = [None]
+        for i, (gp, gn) in enumerate(ctx.grads):
+            out.append((gp * scale).view(ctx.shapes[2 * i]) if ctx.needs_input_grad[1 + 2 * i]
+                       else None)
+            out.append((gn * scale).view(ctx.shapes[2 * i + 1])
+                       if ctx.needs_input_grad[2 + 2 * i] else None)
+        return tuple(out)

@@ -125,16 +125,24 @@ class ConvLayer(nn.Module):
         """Reference ConvLayer.forward(graph, (h_neigh, h_self)) -> z [n_dst, out_feats]."""
         return self._run(graph, x, None, 'store', 0.0)
 
-    def _run(self, graph, x, out, accum: str, out_div: float, attn=None):
-        """attn: (attn_vec, attn_state) for the attention accumulate modes."""
+    def _dropout_active(self) -> bool:
+        return self.training and self.dropout_fn.p > 0
+
+    def _run(self, graph, x, out, accum: str, out_div: float, attn=None, n_self: int = 0):
+        """attn: (attn_vec, attn_state) for the attention accumulate modes.  n_self > 0
+        (autograd, no dropout): x[1] is the block's whole source table of the dst type and
+        its first n_self rows are the dst rows."""
         av, ast = attn if attn is not None else (None, None)
         h_neigh, h_self = x
         preagg, weighted, reduce = self._plan(graph)
-        if self.training and self.dropout_fn.p > 0:
+        if self._dropout_active():
             h_neigh = self.dropout_fn(h_neigh)
             h_self = self.dropout_fn(h_self)
         ew = self._edge_weight(graph) if weighted else None
-        if _grad_mode(h_neigh, h_self, module=self):
+        grad = _grad_mode(h_neigh, h_self, module=self)
+        if n_self and not grad:
+            h_self = h_self[:n_self]
+        if grad:
             m = ag.LinearFn.apply(h_neigh, self.fc_preagg.weight, None, True, False) \
                 if preagg else h_neigh
             if reduce == 'lstm':
@@ -144,7 +152,7 @@ class ConvLayer(nn.Module):
             else:
                 agg = ag.SpmmFn.apply(m, graph.indptr, graph.indices, ew, reduce, graph.n_dst)
             z = ag.SageProjectFn.apply(h_self, agg, self.fc_self.weight, self.fc_neigh.weight,
-                                       bool(self.norm))
+                                       bool(self.norm), n_self)
             return z if out is None else z  # caller combines relations in grad mode
         m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
         if reduce != 'lstm' and ops.can_spmm_project(graph.indptr, m, h_self, self.fc_self.weight,
@@ -215,8 +223,24 @@ class HeteroGraphConv(nn.Module):
         rsts = {}
         for dtype, ces in active.items():
             if grad:
-                outs = [self.mods[ce[1]](g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype]))
-                        for ce in ces]
+                outs = []
+                for ce in ces:
+                    mod = self.mods[ce[1]]
+                    if (g.is_block and not isinstance(inputs, tuple) and not mod._dropout_active()
+                            and dst_inputs[dtype].shape[0] > 0):
+                        # dst rows = prefix of the src table: hand over the whole table so
+                        # the self-gradient needs no slice backward
+                        outs.append(mod._run(g.rel_graph(ce), (src_inputs[ce[0]],
+                                                               src_inputs[dtype]), None,
+                                             'store', 0.0, n_self=dst_inputs[dtype].shape[0]))
+                    else:
+                        outs.append(mod(g.rel_graph(ce), (src_inputs[ce[0]], dst_inputs[dtype])))
+                if len(outs) == 1 and self.aggregate != 'attention':
+                    rsts[dtype] = outs[0]  # sum / mean / max of one relation is itself
+                    continue
+                if len(outs) == 2 and self.aggregate == 'sum':
+                    rsts[dtype] = outs[0] + outs[1]
+                    continue
                 st = torch.stack(outs, 0)
                 if self.aggregate == 'attention':
                     w = torch.softmax((st * self.attn[dtype]).sum(-1), dim=0)  # [R, n_dst]
@@ -399,22 +423,21 @@ def max_margin_loss(pos_score, neg_score, delta: float, neg_sample_size: int,
                     use_recency: bool = False, recency_scores=None,
                     remove_false_negative: bool = False, negative_mask=None, cuda=False,
                     device=None):
-    """Max-margin loss (src/model.py:473-533), same arguments and semantics."""
-    parts = []
+    """Max-margin loss (src/model.py:473-533), same arguments and semantics: the mean over
+    every etype of relu(neg + delta - pos - mask) (/ recency).  One HIP launch per etype
+    computes the scores' sum and their gradient (gnnrec_margin_loss_f32)."""
+    scores, meta = [], []
     for etype in pos_score.keys():
-        neg = neg_score[etype].reshape(-1, neg_sample_size)
-        pos = pos_score[etype]
-        if remove_false_negative:
-            mask = negative_mask[etype].reshape(-1, neg_sample_size).to(neg)
-        else:
-            mask = torch.zeros_like(neg)
-        scores = torch.relu(neg + delta - pos - mask)
+        neg, pos = neg_score[etype], pos_score[etype]
+        mask = negative_mask[etype] if remove_false_negative else None
+        rec = None
         if use_recency and recency_scores is not None and etype in recency_scores:
-            scores = scores / torch.unsqueeze(recency_scores[etype].to(scores), 1)
-        parts.append(scores)
-    if not parts:
+            rec = recency_scores[etype]
+        scores += [pos, neg]
+        meta.append((neg_sample_size, mask, rec))
+    if not meta:
         return torch.tensor(float('nan'))
-    return torch.mean(torch.cat(parts, 0))
+    return ag.MarginLossFn.apply((delta, meta), *scores)
 
 
 def library_available() -> bool:

@@ -581,6 +581,78 @@ def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
     return out
 
 
+def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, Hd: torch.Tensor,
+                       grad: torch.Tensor, need_src: bool = True, need_dst: bool = True):
+    """f2: gradients of sddmm_cos w.r.t. Hs and Hd given dL/dcos [E] -> (gHs|None, gHd|None),
+    one library call (key sort, planned weighted gather, normalisation Jacobian)."""
+    lib = _lib.load()
+    _dev(src, "src", torch.int64)
+    _dev(dst, "dst", torch.int64)
+    _dev(Hs, "Hs", torch.float32)
+    _dev(Hd, "Hd", torch.float32)
+    _dev(grad, "grad", torch.float32)
+    E, d = src.numel(), Hs.shape[1]
+    if dst.numel() != E or grad.numel() != E:
+        raise ValueError("sddmm_cos_backward: src/dst/grad length mismatch")
+    if Hd.shape[1] != d:
+        raise ValueError("endpoint feature sizes differ")
+    n_s, n_d = Hs.shape[0], Hd.shape[0]
+    gHs = torch.empty((n_s, d), dtype=torch.float32, device=Hs.device) if need_src else None
+    gHd = torch.empty((n_d, d), dtype=torch.float32, device=Hs.device) if need_dst else None
+    nbytes = int(lib.gnnrec_sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=Hs.device)
+    check(lib.gnnrec_sddmm_cos_backward_f32(
+        ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(Hs), _rowmajor(Hs, "Hs"), n_s,
+        ptr(Hd), _rowmajor(Hd, "Hd"), n_d, d, ptr(grad.contiguous()), ptr(gHs), ptr(gHd),
+        ptr(ws), nbytes, stream_ptr(Hs.device)), "gnnrec_sddmm_cos_backward_f32")
+    return gHs, gHd
+
+
+def margin_loss(parts, delta: float):
+    """f2: max_margin_loss forward + unscaled gradients for a list of etype parts
+    [(pos [E], neg [E*K], K, mask|None, recency|None)] -> (loss 0-d tensor, N_total,
+    [(g_pos, g_neg)]).  Gradients are d(sum of scores)/d(score); the loss is the mean."""
+    lib = _lib.load()
+    dev = parts[0][0].device
+    blocks = [int(lib.gnnrec_margin_loss_blocks(p[0].numel())) for p in parts]
+    partial = torch.empty(sum(blocks), dtype=torch.float32, device=dev)
+    grads, off, total = [], 0, 0
+    for (pos, neg, K, mask, rec), nb in zip(parts, blocks):
+        _dev(pos, "pos_score", torch.float32)
+        _dev(neg, "neg_score", torch.float32)
+        n_pos = pos.numel()
+        if neg.numel() != n_pos * K:
+            raise RuntimeError(f"shape '[-1, {K}]' is invalid for input of size {neg.numel()}")
+        if mask is not None:
+            mask = mask.to(device=dev, dtype=torch.float32).contiguous()
+            if mask.numel() != neg.numel():
+                raise ValueError("negative_mask must have one value per negative score")
+        rec_i64 = 0
+        if rec is not None:
+            rec = rec.to(dev).reshape(-1)
+            if rec.dtype == torch.int64:
+                rec_i64 = 1
+            elif rec.dtype != torch.float32:
+                rec = rec.float()
+            rec = rec.contiguous()
+            if rec.numel() != n_pos:
+                raise ValueError("recency must have one value per positive edge")
+        g_pos = torch.empty_like(pos)
+        g_neg = torch.empty_like(neg)
+        check(lib.gnnrec_margin_loss_f32(ptr(pos.contiguous()), ptr(neg.contiguous()), n_pos, K,
+                                         float(delta), ptr(mask), ptr(rec), rec_i64, ptr(g_pos),
+                                         ptr(g_neg), ptr(partial[off:]), nb, stream_ptr(dev)),
+              "gnnrec_margin_loss_f32")
+        grads.append((g_pos, g_neg))
+        off += nb
+        total += neg.numel()
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    check(lib.gnnrec_sum_scaled_f32(ptr(partial), partial.numel(),
+                                    1.0 / total if total else float('nan'), ptr(loss),
+                                    stream_ptr(dev)), "gnnrec_sum_scaled_f32")
+    return loss, total, grads
+
+
 def edge_mlp(src: torch.Tensor, dst: torch.Tensor, P: torch.Tensor, Q: torch.Tensor,
              W2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor) -> torch.Tensor:
     """a8 tail: sigmoid(w3·relu(W2·relu(P[src]+Q[dst]) + b2) + b3) -> [E]."""

@@ -306,6 +306,35 @@ int gnnrec_lstm_step_f32(const float* P, int64_t ldp, const int64_t* indptr,
 int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx, int64_t n,
                        int64_t row_bytes, void* dst, int64_t dst_ld_bytes, void* stream);
 
+/* ---- f2: edge-score side of the training step ----------------------------
+ * max_margin_loss (src/model.py:473-533) for one etype, forward and gradient in one pass:
+ *   s[e,k] = relu(((neg[e,k] + delta) - pos[e]) - mask[e,k]) / recency[e]
+ * partial[b] (b < gnnrec_margin_loss_blocks(n_pos)) = sum of s over block b's rows (fixed
+ * grid, fixed order); g_neg[e,k] = [pre > 0] / recency[e], g_pos[e] = -sum_k g_neg[e,k]
+ * (unscaled: the caller multiplies by dL/dloss / N_total).  mask, recency nullable (0 / 1);
+ * recency float32, or int64 when recency_i64 != 0.  neg is [n_pos, K] row-major. */
+int64_t gnnrec_margin_loss_blocks(int64_t n_pos);
+int gnnrec_margin_loss_f32(const float* pos, const float* neg, int64_t n_pos, int64_t K,
+                           float delta, const float* mask, const void* recency, int recency_i64,
+                           float* g_pos, float* g_neg, float* partial, int64_t n_partial,
+                           void* stream);
+/* out[0] = scale * sum(x[0..n)) in a fixed order (one block): the loss mean. */
+int gnnrec_sum_scaled_f32(const float* x, int64_t n, float scale, float* out, void* stream);
+
+/* Backward of gnnrec_sddmm_cos_f32 (CosinePrediction under loss.backward(), DGL's
+ * SDDMM backward = SpMM): for cos_e = <u_s, v_t> / (max(|u_s|,eps) max(|v_t|,eps)),
+ *   gHs[s] = inv_s (G_s - û_s (û_s . G_s)),  G_s = sum_{e: src_e = s} grad_e v_t / max(|v_t|,eps)
+ * (G_s inv_s for rows with |u_s| <= eps), and symmetrically gHd.  Either output may be NULL.
+ * Rows grouped by a stable key sort, heavy rows split (deterministic).  gHs / gHd are
+ * dense [n, d].  Workspace: gnnrec_sddmm_cos_backward_workspace_bytes. */
+size_t gnnrec_sddmm_cos_backward_workspace_bytes(int64_t n_edges, int64_t n_src, int64_t n_dst,
+                                                 int64_t d);
+int gnnrec_sddmm_cos_backward_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
+                                  const float* Hs, int64_t lds, int64_t n_src, const float* Hd,
+                                  int64_t ldd, int64_t n_dst, int64_t d, const float* grad,
+                                  float* gHs, float* gHd, void* workspace,
+                                  size_t workspace_bytes, void* stream);
+
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),
  * item() uniform (zipf_s == 0) or inverse-CDF Zipf over the table `zipf_cdf`

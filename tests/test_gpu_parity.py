@@ -483,6 +483,79 @@ def test_cosine_backward_matches_autograd():
     np.testing.assert_allclose(b.grad.cpu().numpy(), b2.grad.cpu().numpy(), rtol=1e-4, atol=1e-5)
 
 
+def test_cosine_backward_one_side_and_empty():
+    from gnnrec import ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(5)
+    hs = torch.randn(40, 128, device="cuda", generator=gen)
+    hd = torch.randn(3000, 128, device="cuda", generator=gen)
+    # one heavy src row (5000 edges > the 2048-edge split) beside light ones
+    src = torch.cat([torch.zeros(5000, dtype=torch.int64, device="cuda"),
+                     torch.randint(1, 40, (700,), device="cuda", generator=gen)])
+    dst = torch.randint(0, 3000, (5700,), device="cuda", generator=gen)
+    g = torch.randn(5700, device="cuda", generator=gen)
+    ga, gb = ops.sddmm_cos_backward(src, dst, hs, hd, g)
+    ga1, none_b = ops.sddmm_cos_backward(src, dst, hs, hd, g, need_dst=False)
+    none_a, gb1 = ops.sddmm_cos_backward(src, dst, hs, hd, g, need_src=False)
+    assert none_a is None and none_b is None
+    assert torch.equal(ga, ga1) and torch.equal(gb, gb1)  # bitwise: same launches per side
+    a, b = hs.clone().requires_grad_(True), hd.clone().requires_grad_(True)
+    cos = (torch.nn.functional.normalize(a, dim=-1)[src] *
+           torch.nn.functional.normalize(b, dim=-1)[dst]).sum(-1)
+    (cos * g).sum().backward()
+    np.testing.assert_allclose(ga.cpu().numpy(), a.grad.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(gb.cpu().numpy(), b.grad.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    e = torch.zeros(0, dtype=torch.int64, device="cuda")
+    za, zb = ops.sddmm_cos_backward(e, e, hs, hd, torch.zeros(0, device="cuda"))
+    assert not za.any() and not zb.any()
+
+
+@pytest.mark.parametrize("K,mask,rec", [(1, False, None), (7, True, "i64"), (2500, False, "f32"),
+                                        (100, True, "f32")])
+def test_margin_loss_matches_torch_autograd(K, mask, rec):
+    """gnnrec.nn.max_margin_loss (HIP) vs the reference's torch formula (src/model.py:
+    513-533) restated here, loss and both score gradients, two etypes + an empty one."""
+    from gnnrec import nn as gnn
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(K)
+    ets = [("user", "buys", "item"), ("user", "clicks", "item"), ("item", "bought-by", "user")]
+    sizes = [300, 77, 0]
+    ps = {ce: torch.rand(n, 1, device="cuda", generator=gen) for ce, n in zip(ets, sizes)}
+    ns = {ce: torch.rand(n * K, 1, device="cuda", generator=gen) for ce, n in zip(ets, sizes)}
+    masks = {ce: (torch.rand(n * K, device="cuda", generator=gen) < 0.1).float()
+             for ce, n in zip(ets, sizes)} if mask else None
+    recs = None
+    if rec:
+        recs = {ets[0]: torch.randint(1, 30, (sizes[0],), device="cuda", generator=gen)}
+        if rec == "f32":
+            recs = {k: v.float() * 0.5 for k, v in recs.items()}
+    ps_a = {k: v.clone().requires_grad_(True) for k, v in ps.items()}
+    ns_a = {k: v.clone().requires_grad_(True) for k, v in ns.items()}
+    loss = gnn.max_margin_loss(ps_a, ns_a, 0.266, K, rec is not None, recs, mask, masks)
+    loss.backward()
+    ps_b = {k: v.clone().requires_grad_(True) for k, v in ps.items()}
+    ns_b = {k: v.clone().requires_grad_(True) for k, v in ns.items()}
+    parts = []
+    for ce in ets:
+        neg = ns_b[ce].reshape(-1, K)
+        m = masks[ce].reshape(-1, K) if mask else torch.zeros_like(neg)
+        sc = torch.relu(neg + 0.266 - ps_b[ce] - m)
+        if rec and ce in recs:
+            sc = sc / torch.unsqueeze(recs[ce], 1)
+        parts.append(sc)
+    ref = torch.mean(torch.cat(parts, 0))
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5, atol=1e-7)
+    for ce in ets:
+        np.testing.assert_allclose(ps_a[ce].grad.cpu().numpy(), ps_b[ce].grad.cpu().numpy(),
+                                   rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(ns_a[ce].grad.cpu().numpy(), ns_b[ce].grad.cpu().numpy(),
+                                   rtol=1e-5, atol=1e-9)
+    # bitwise repeatable
+    assert torch.equal(gnn.max_margin_loss(ps, ns, 0.266, K, rec is not None, recs, mask, masks),
+                       gnn.max_margin_loss(ps, ns, 0.266, K, rec is not None, recs, mask, masks))
+
+
 # ------------------------------------------------------------ f4 LSTM reducer ---
 @pytest.mark.parametrize("d", [5, 64, 128, 200])
 def test_lstm_aggregate_matches_oracle(d):
