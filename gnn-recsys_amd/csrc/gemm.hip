@@ -48,6 +48,7 @@ struct GemmArgs {
   int epilogue; int accum; float out_div;
   const float* attn_vec; float* attn_state;
   float* out; int64_t ldo;
+  float* row_norm;  // nullable: |row| before the L2 norm (training keeps it for the backward)
   int vecA1, vecA2, vecW1, vecW2, vecO;
 };
 
@@ -141,6 +142,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
 #pragma unroll
       for (int off = 1; off < 32; off <<= 1) ss += __shfl_xor(ss, off);
       float nrm = sqrtf(ss);
+      if (g.row_norm && r == 0) {
+        const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (row < g.M) g.row_norm[row] = nrm;
+      }
       if (nrm == 0.f) nrm = 1.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) z[v][t] = z[v][t] / nrm;
@@ -519,7 +524,22 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
                                int64_t N, int epilogue, int accum, float out_div,
                                const float* attn_vec, float* attn_state, float* out,
                                int64_t ldo, void* stream) {
+  return gnnrec_gemm_rownorm_f32(A1, lda1, K1, W1, A2, lda2, K2, W2, a2_deg, a2_mode, bias,
+                                 bias_nonempty, M, N, epilogue, accum, out_div, attn_vec,
+                                 attn_state, out, ldo, nullptr, stream);
+}
+
+extern "C" int gnnrec_gemm_rownorm_f32(const float* A1, int64_t lda1, int64_t K1,
+                                       const float* W1, const float* A2, int64_t lda2,
+                                       int64_t K2, const float* W2, const int32_t* a2_deg,
+                                       int a2_mode, const float* bias,
+                                       const float* bias_nonempty, int64_t M, int64_t N,
+                                       int epilogue, int accum, float out_div,
+                                       const float* attn_vec, float* attn_state, float* out,
+                                       int64_t ldo, float* row_norm, void* stream) {
   using namespace gnnrec;
+  GNNREC_REQUIRE(row_norm == nullptr || (epilogue & GNNREC_EPI_L2NORM),
+                 "gnnrec_gemm_rownorm_f32: row_norm needs the L2NORM epilogue");
   GNNREC_REQUIRE(M >= 0 && N >= 0 && K1 >= 0 && K2 >= 0, "gnnrec_gemm_f32: negative size");
   if (M == 0 || N == 0) return GNNREC_OK;
   GNNREC_REQUIRE(out != nullptr && ldo >= N, "gnnrec_gemm_f32: bad output");
@@ -543,6 +563,7 @@ extern "C" int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const 
   g.M = M; g.N = N; g.epilogue = epilogue; g.accum = accum; g.out_div = out_div;
   g.attn_vec = attn_vec; g.attn_state = attn_state;
   g.out = out; g.ldo = ldo;
+  g.row_norm = row_norm;
   g.vecA1 = (K1 % 4 == 0) && (lda1 % 4 == 0) && aligned16(A1);
   g.vecA2 = (K2 % 4 == 0) && (lda2 % 4 == 0) && aligned16(A2);
   g.vecW1 = (K1 % 4 == 0) && aligned16(W1);

@@ -53,6 +53,30 @@ __global__ __launch_bounds__(256) void edge_rows_kernel(const int64_t* __restric
   }
 }
 
+// unweighted blocks: dst row of every edge, and 1 / deg(dst) per dst row for mean (the
+// sort then carries the dst rows themselves, no edge-id permutation)
+__global__ __launch_bounds__(256) void edge_dst_kernel(const int64_t* __restrict__ indptr,
+                                                       int64_t n_dst, int mean,
+                                                       int32_t* __restrict__ dst_of,
+                                                       float* __restrict__ inv_deg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < n_dst; v += wstride) {
+    const int64_t beg = indptr[v], end = indptr[v + 1];
+    if (mean && lane == 0) inv_deg[v] = end > beg ? 1.f / (float)(end - beg) : 1.f;
+    for (int64_t e = beg + lane; e < end; e += kWave) dst_of[e] = (int32_t)v;
+  }
+}
+
+// ew_t[k] = 1 / deg(indices_t[k]) (the table is n_dst floats: L2-resident)
+__global__ __launch_bounds__(256) void row_weight_kernel(const int32_t* __restrict__ rows,
+                                                         const float* __restrict__ inv_deg,
+                                                         int64_t E, float* __restrict__ w) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < E; k += stride)
+    w[k] = inv_deg[rows[k]];
+}
+
 // indptr_t[u] = first k with keys[k] >= u (lower bound in the sorted keys; one thread per
 // source row, so long runs of unused source ids cost nothing extra)
 __global__ __launch_bounds__(256) void bounds_kernel(const int32_t* __restrict__ keys,
@@ -128,6 +152,8 @@ size_t sort_rows_bytes(int64_t E, int64_t n_rows) {
 extern "C" size_t gnnrec_csr_transpose_workspace_bytes(int64_t n_edges, int64_t n_src) {
   using namespace gnnrec;
   if (n_edges <= 0) return 0;
+  // weighted: eid | dst_of | w_e | sort_rows scratch; unweighted: dst_of | keys | inv_deg
+  // | radix temp (taken only when inv_deg fits in three edge slots)
   return 3 * align_up((size_t)n_edges * 4) + sort_rows_bytes(n_edges, n_src);
 }
 
@@ -154,6 +180,31 @@ extern "C" int gnnrec_csr_transpose(const int64_t* indptr, const int32_t* indice
                  workspace_bytes, need);
   char* p = static_cast<char*>(workspace);
   const size_t slot = align_up((size_t)n_edges * 4);
+  if (!ew && (!mean || align_up((size_t)(n_dst + 1) * 4) <= 3 * slot)) {
+    // unweighted: sort (source id, dst row) pairs straight into indices_t; mean weights
+    // from a per-dst-row table.  Scratch: dst_of | sorted keys | inv_deg | radix temp
+    int32_t* dst_of = reinterpret_cast<int32_t*>(p);
+    int32_t* keys = reinterpret_cast<int32_t*>(p + slot);
+    float* inv_deg = reinterpret_cast<float*>(p + 2 * slot);
+    const size_t deg_bytes = align_up((size_t)(n_dst + 1) * 4);
+    void* temp = p + 2 * slot + deg_bytes;
+    size_t temp_bytes = need - 2 * slot - deg_bytes;
+    hipLaunchKernelGGL(edge_dst_kernel, dim3(flat_grid(n_dst * 16)), dim3(256), 0, s, indptr,
+                       n_dst, mean, dst_of, inv_deg);
+    if (hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, indices, keys, dst_of,
+                                                 indices_t, (unsigned)n_edges, 0,
+                                                 key_bits(n_src), s);
+        e != hipSuccess) {
+      set_error("radix sort failed: %s", hipGetErrorString(e));
+      return GNNREC_EHIP;
+    }
+    hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_src + 1)), dim3(256), 0, s, keys,
+                       n_edges, n_src, indptr_t);
+    if (mean)
+      hipLaunchKernelGGL(row_weight_kernel, dim3(flat_grid(n_edges)), dim3(256), 0, s, indices_t,
+                         inv_deg, n_edges, ew_t);
+    return check_launch("gnnrec_csr_transpose");
+  }
   int32_t* eid = reinterpret_cast<int32_t*>(p);
   int32_t* dst_of = reinterpret_cast<int32_t*>(p + slot);
   float* w_e = (ew || mean) ? reinterpret_cast<float*>(p + 2 * slot) : nullptr;

@@ -66,7 +66,8 @@ __device__ inline void store_step(float* lds, const float4 (&r)[2]) {
 template <bool VEC>
 __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
-    int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part) {
+    int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part,
+    float* __restrict__ part_b) {
   __shared__ float As[2][kKStep * kLdsStride];
   __shared__ float Bs[2][kKStep * kLdsStride];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -76,6 +77,10 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
   const int64_t i_base = (int64_t)blockIdx.y * kTile, j_base = (int64_t)blockIdx.z * kTile;
   const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
 
+  // part_b: column sums of A over this split (the bias gradient Σ_k dY[k, i]); the blocks
+  // of the first N tile add up the A tiles they already hold in LDS
+  const bool colsum = part_b != nullptr && blockIdx.z == 0 && threadIdx.x < kTile;
+  float csum = 0.f;
   f32x16 acc[2][2];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -110,6 +115,10 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
+      if (colsum) {
+#pragma unroll
+        for (int r = 0; r < kKStep; ++r) csum += as[r * kLdsStride + threadIdx.x];
+      }
       if (more) {
         store_step(As[buf ^ 1], ra);
         store_step(Bs[buf ^ 1], rb);
@@ -118,6 +127,7 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
       buf ^= 1;
     }
   }
+  if (colsum && i_base + threadIdx.x < M) part_b[split * M + i_base + threadIdx.x] = csum;
   float* P = part + split * M * N;
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -136,31 +146,40 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
 // C = (accumulate ? C : 0) + sum_p part[p]; 64 outputs per block, the 4 waves sum
 // interleaved quarters of the splits, combined in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
-    const float* __restrict__ part, int64_t splits, int64_t M, int64_t N, float* __restrict__ C,
-    int64_t ldc, int accumulate) {
+    const float* __restrict__ part, const float* __restrict__ part_b, int64_t splits, int64_t M,
+    int64_t N, float* __restrict__ C, int64_t ldc, float* __restrict__ Cb, int accumulate) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t mn = M * N;
   const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  // outputs [0, mn) are C, [mn, mn + M) the column sums (when Cb)
+  const int64_t nout = mn + (Cb ? M : 0);
+  const float* src = t < mn ? part + t : part_b + (t - mn);
+  const int64_t pstride = t < mn ? mn : M;
   float s = 0.f;
-  if (t < mn) {
+  if (t < nout) {
     int64_t p = w;
     for (; p + 12 < splits; p += 16) {
-      const float x0 = part[p * mn + t], x1 = part[(p + 4) * mn + t];
-      const float x2 = part[(p + 8) * mn + t], x3 = part[(p + 12) * mn + t];
+      const float x0 = src[p * pstride], x1 = src[(p + 4) * pstride];
+      const float x2 = src[(p + 8) * pstride], x3 = src[(p + 12) * pstride];
       s += x0;
       s += x1;
       s += x2;
       s += x3;
     }
-    for (; p < splits; p += 4) s += part[p * mn + t];
+    for (; p < splits; p += 4) s += src[p * pstride];
   }
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && t < mn) {
+  if (w == 0 && t < nout) {
     const float tot = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    const int64_t i = t / N, j = t - i * N;
-    float* c = C + i * ldc + j;
+    float* c;
+    if (t < mn) {
+      const int64_t i = t / N, j = t - i * N;
+      c = C + i * ldc + j;
+    } else {
+      c = Cb + (t - mn);
+    }
     *c = accumulate ? *c + tot : tot;
   }
 }
@@ -216,6 +235,33 @@ __global__ __launch_bounds__(256) void act_backward_kernel(
   }
 }
 
+// z = a / |a| (a = relu(u)) kept with the row norms: gu = [z > 0] (gz - z (z.gz)) / |a|,
+// or gz masked when |a| == 0 — the same Jacobian as act_backward_kernel without u
+__global__ __launch_bounds__(256) void act_backward_normed_kernel(
+    const float* __restrict__ z, int64_t ldz, const float* __restrict__ nrm,
+    const float* __restrict__ gz, int64_t ldg, int64_t n_rows, int64_t d, int relu,
+    float* __restrict__ gu, int64_t ldo) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n_rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* zr = z + r * ldz;
+  const float* gr = gz + r * ldg;
+  float* orow = gu + r * ldo;
+  float dot = 0.f;
+  for (int64_t c = lane; c < d; c += 64) dot += zr[c] * gr[c];
+  for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+  const float n = nrm[r];
+  const bool scale = n != 0.f;
+  const float inv = scale ? 1.f / n : 1.f;
+  const float coef = scale ? dot : 0.f;
+  for (int64_t c = lane; c < d; c += 64) {
+    const float x = zr[c];
+    float g = (gr[c] - x * coef) * inv;
+    if (relu && !(x > 0.f)) g = 0.f;
+    orow[c] = g;
+  }
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -223,19 +269,21 @@ using namespace gnnrec;
 
 extern "C" int64_t gnnrec_gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t N) {
   if (K <= 0 || M <= 0 || N <= 0) return 0;
-  return tn_splits(K, M, N) * M * N * (int64_t)sizeof(float);
+  return tn_splits(K, M, N) * (M * N + M) * (int64_t)sizeof(float);
 }
 
-extern "C" int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
-                                  int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
-                                  int accumulate, float* workspace, void* stream) {
+extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
+                                       int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
+                                       float* colsum, int accumulate, float* workspace,
+                                       void* stream) {
   GNNREC_REQUIRE(K >= 0 && M >= 0 && N >= 0, "gnnrec_gemm_tn_f32: negative size");
   GNNREC_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gnnrec_gemm_tn_f32: bad leading dims");
   if (M == 0 || N == 0) return GNNREC_OK;
   hipStream_t s = as_stream(stream);
   if (K == 0) {
     if (accumulate) return GNNREC_OK;
-    if (hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) != hipSuccess) {
+    if (hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s) != hipSuccess ||
+        (colsum && hipMemsetAsync(colsum, 0, M * sizeof(float), s) != hipSuccess)) {
       set_error("gnnrec_gemm_tn_f32: hipMemset2DAsync failed");
       return GNNREC_EHIP;
     }
@@ -247,16 +295,24 @@ extern "C" int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, i
                   (unsigned)((N + kTile - 1) / kTile));
   const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 &&
                    M % 4 == 0 && N % 4 == 0;
+  float* part_b = colsum ? workspace + splits * M * N : nullptr;
   if (vec)
     hipLaunchKernelGGL(gemm_tn_partial_kernel<true>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
-                       N, chunk, workspace);
+                       N, chunk, workspace, part_b);
   else
     hipLaunchKernelGGL(gemm_tn_partial_kernel<false>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
-                       N, chunk, workspace);
-  const int64_t mn = M * N;
-  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((mn + 63) / 64)), dim3(256), 0, s,
-                     workspace, splits, M, N, C, ldc, accumulate);
+                       N, chunk, workspace, part_b);
+  const int64_t nout = M * N + (colsum ? M : 0);
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s,
+                     workspace, part_b, splits, M, N, C, ldc, colsum, accumulate);
   return check_launch("gnnrec_gemm_tn_f32");
+}
+
+extern "C" int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
+                                  int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
+                                  int accumulate, float* workspace, void* stream) {
+  return gnnrec_gemm_tn_bias_f32(A, lda, B, ldb, K, M, N, C, ldc, nullptr, accumulate, workspace,
+                                 stream);
 }
 
 extern "C" int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_t ldg,
@@ -353,4 +409,17 @@ extern "C" int gnnrec_row_epilogue_f32(const float* z, int64_t ldz, int64_t M, i
                      as_stream(stream), z, ldz, M, N, l2norm, accum, out_div,
                      accum >= GNNREC_ACC_ATTN_FIRST ? attn_vec : nullptr, attn_state, out, ldo);
   return check_launch("gnnrec_row_epilogue_f32");
+}
+
+extern "C" int gnnrec_act_backward_normed_f32(const float* z, int64_t ldz, const float* row_norm,
+                                              const float* gz, int64_t ldg, int64_t n_rows,
+                                              int64_t d, int relu, float* gu, int64_t ldo,
+                                              void* stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && d >= 0 && ldz >= d && ldg >= d && ldo >= d,
+                 "gnnrec_act_backward_normed_f32: bad sizes");
+  if (n_rows == 0 || d == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(z && row_norm && gz && gu, "gnnrec_act_backward_normed_f32: null pointer");
+  hipLaunchKernelGGL(act_backward_normed_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0,
+                     as_stream(stream), z, ldz, row_norm, gz, ldg, n_rows, d, relu, gu, ldo);
+  return check_launch("gnnrec_act_backward_normed_f32");
 }

@@ -53,6 +53,10 @@ SIGNATURES = {
                                         _INT, _P, _I64, _P]),
     "gnnrec_gemm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P, _P,
                                _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
+    "gnnrec_gemm_rownorm_f32": (_INT, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _INT, _P, _P,
+                                       _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64, _P, _P]),
+    "gnnrec_act_backward_normed_f32": (_INT, [_P, _I64, _P, _P, _I64, _I64, _I64, _INT, _P, _I64,
+                                              _P]),
     "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
@@ -60,6 +64,8 @@ SIGNATURES = {
     "gnnrec_scan_workspace_bytes": (_I64, [_I64]),
     "gnnrec_gemm_tn_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "gnnrec_gemm_tn_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _INT, _P, _P]),
+    "gnnrec_gemm_tn_bias_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _INT,
+                                       _P, _P]),
     "gnnrec_lstm_step_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P,
                                     _I64, _P]),
     "gnnrec_spmm_project_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,

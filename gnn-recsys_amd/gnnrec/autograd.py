@@ -42,8 +42,15 @@ class LinearFn(torch.autograd.Function):
             gy = gy * y * (1 - y)
         gy = gy.contiguous()
         gx = ops.gemm(gy, W.t().contiguous()) if ctx.needs_input_grad[0] else None
-        gW = ops.gemm_tn(gy, x.contiguous()) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        gb = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = torch.empty(gy.shape[1], dtype=torch.float32, device=gy.device)
+        if ctx.needs_input_grad[1]:
+            gW = ops.gemm_tn(gy, x.contiguous(), colsum=gb)  # db from the same pass
+        else:
+            gW = None
+            if gb is not None:
+                gb = gy.sum(0)
         return gx, gW, gb, None, None
 
 
@@ -137,40 +144,45 @@ class SageProjectFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h_self, agg, Ws, Wn, norm: bool, n_self: int = 0):
         hs = h_self[:n_self] if n_self else h_self
-        # y = relu(u) is kept for the backward (its mask and row norm are all the epilogue's
-        # Jacobian needs), so the backward does not recompute the K=2d GEMM
-        y = ops.gemm(hs.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True)
-        z = ops.l2_normalize_rows(y) if norm else y
-        ctx.save_for_backward(h_self, agg, Ws, Wn, y)
+        # the backward needs the epilogue's Jacobian, not the GEMM again: z = relu(u)/|relu(u)|
+        # and the row norms (one fused launch) — or y = relu(u) kept before a separate
+        # normalisation when the row is wider than one GEMM block
+        nrm = None
+        if norm and Ws.shape[0] <= ops.GEMM_ROW_N:
+            nrm = torch.empty(hs.shape[0], dtype=torch.float32, device=hs.device)
+            z = ops.gemm(hs.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True,
+                         l2norm=True, row_norm=nrm)
+            y = z
+        else:
+            y = ops.gemm(hs.contiguous(), Ws.detach(), agg.contiguous(), Wn.detach(), relu=True)
+            z = ops.l2_normalize_rows(y) if norm else y
+        ctx.save_for_backward(h_self, agg, Ws, Wn, y, nrm)
         ctx.norm, ctx.n_self = norm, n_self
         return z
 
     @staticmethod
     def backward(ctx, gz):
-        h_self, agg, Ws, Wn, y = ctx.saved_tensors
+        h_self, agg, Ws, Wn, y, nrm = ctx.saved_tensors
         need = ctx.needs_input_grad
         M = y.shape[0]
         hs = h_self[:M]
-        gu = ops.act_backward(y, gz, relu=True, l2norm=ctx.norm)  # relu(y) = y, same mask
+        gz = gz.contiguous()
+        if nrm is not None:  # y is the normalised output
+            gu = ops.act_backward_normed(y, nrm, gz, relu=True)
+        else:  # y = relu(u): relu(y) = y, same mask
+            gu = ops.act_backward(y, gz, relu=True, l2norm=ctx.norm)
         g_self = g_agg = None
-        if need[0] and need[1]:
-            # both input gradients from one GEMM: gu · [W_self | W_neigh] -> [rows, d_s + d_n]
-            d_s = Ws.shape[1]
-            R = torch.empty((h_self.shape[0], d_s + Wn.shape[1]), dtype=torch.float32,
-                            device=gu.device)
-            ops.gemm(gu, torch.cat([Ws.detach().t(), Wn.detach().t()], 0), out=R[:M])
+        if need[0]:
+            # contiguous [rows, d_s] with the tail past the dst rows zeroed: autograd adds it
+            # to the table's other gradient with a vectorised kernel (a strided view of a
+            # [rows, d_s + d_n] GEMM output took a slow strided add, more than the GEMM saved)
+            g_self = torch.empty((h_self.shape[0], Ws.shape[1]), dtype=torch.float32,
+                                 device=gu.device)
+            ops.gemm(gu, Ws.detach().t().contiguous(), out=g_self[:M])
             if h_self.shape[0] > M:
-                R[M:, :d_s].zero_()
-            g_self, g_agg = R[:, :d_s], R[:M, d_s:]
-        elif need[0] or need[1]:
-            W = Ws if need[0] else Wn
-            g = ops.gemm(gu, W.detach().t().contiguous())
-            if need[0] and h_self.shape[0] > M:
-                full = torch.zeros((h_self.shape[0], g.shape[1]), dtype=g.dtype,
-                                   device=g.device)
-                full[:M] = g
-                g = full
-            g_self, g_agg = (g, None) if need[0] else (None, g)
+                g_self[M:].zero_()
+        if need[1]:
+            g_agg = ops.gemm(gu, Wn.detach().t().contiguous())
         g_Ws = ops.gemm_tn(gu, hs.contiguous()) if need[2] else None
         g_Wn = ops.gemm_tn(gu, agg.contiguous()) if need[3] else None
         return g_self, g_agg, g_Ws, g_Wn, None, None

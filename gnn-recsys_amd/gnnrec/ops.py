@@ -274,9 +274,11 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
          a2_deg: Optional[torch.Tensor] = None, a2_mode: int = _lib.A2_NONE,
          attn_vec: Optional[torch.Tensor] = None,
          attn_state: Optional[torch.Tensor] = None,
-         bias_nonempty: Optional[torch.Tensor] = None) -> torch.Tensor:
+         bias_nonempty: Optional[torch.Tensor] = None,
+         row_norm: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias [+ bias_nonempty where
-    a2_deg > 0]).  W are nn.Linear weights [N, K]."""
+    a2_deg > 0]).  W are nn.Linear weights [N, K].  row_norm [M] (with l2norm, N <=
+    GEMM_ROW_N): receives each row's norm before the normalisation (training)."""
     lib = _lib.load()
     _dev(A1, "A1", torch.float32)
     _dev(W1, "W1", torch.float32)
@@ -315,6 +317,10 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
             raise ValueError(f"out must be [{M}, {N}]")
     ldo = _rowmajor(out, "out")
     av, ast = _attn_args(accum, attn_vec, attn_state, M, N)
+    if row_norm is not None:
+        _dev(row_norm, "row_norm", torch.float32)
+        if not l2norm or N > GEMM_ROW_N or row_norm.numel() != M or not row_norm.is_contiguous():
+            raise ValueError(f"row_norm needs l2norm, N <= {GEMM_ROW_N} and a contiguous [{M}]")
     if N > GEMM_ROW_N and (l2norm or av is not None):
         # the row norm / attention score needs the whole row: GEMM (bias, ReLU, sigmoid)
         # into a scratch table, then one row-epilogue pass into out
@@ -324,10 +330,10 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
                                           float(out_div), ptr(av), ptr(ast), ptr(out), ldo,
                                           stream_ptr(A1.device)), "gnnrec_row_epilogue_f32")
         return out
-    rc = lib.gnnrec_gemm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2), ptr(a2_deg),
-                             a2_mode, ptr(bias), ptr(bias_nonempty), M, N, epi, ACCUM[accum],
-                             float(out_div),
-                             ptr(av), ptr(ast), ptr(out), ldo, stream_ptr(A1.device))
+    rc = lib.gnnrec_gemm_rownorm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2),
+                                     ptr(a2_deg), a2_mode, ptr(bias), ptr(bias_nonempty), M, N,
+                                     epi, ACCUM[accum], float(out_div), ptr(av), ptr(ast),
+                                     ptr(out), ldo, ptr(row_norm), stream_ptr(A1.device))
     check(rc, "gnnrec_gemm_f32")
     return out
 
@@ -433,10 +439,11 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
 
 
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
-            accumulate: bool = False) -> torch.Tensor:
-    """f2 weight gradient: out [M,N] (+)= Aᵀ B for A [K,M], B [K,N] (dW = dYᵀ X).
+            accumulate: bool = False, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """f2 weight gradient: out [M,N] (+)= Aᵀ B for A [K,M], B [K,N] (dW = dYᵀ X); with
+    colsum [M], also colsum (+)= Σ_k A[k] (the bias gradient) from the same pass.
 
-    Deterministic split-K MFMA (gnnrec_gemm_tn_f32)."""
+    Deterministic split-K MFMA (gnnrec_gemm_tn_bias_f32)."""
     lib = _lib.load()
     _dev(A, "A", torch.float32)
     _dev(B, "B", torch.float32)
@@ -453,13 +460,36 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None
         _dev(out, "out", torch.float32)
         if tuple(out.shape) != (M, N):
             raise ValueError(f"out must be [{M}, {N}]")
+    if colsum is not None:
+        _dev(colsum, "colsum", torch.float32)
+        if colsum.numel() != M or not colsum.is_contiguous():
+            raise ValueError(f"colsum must be a contiguous [{M}] tensor")
     ldc = _rowmajor(out, "out")
     nbytes = lib.gnnrec_gemm_tn_workspace_bytes(K, M, N)
     ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=A.device)
-    check(lib.gnnrec_gemm_tn_f32(ptr(A), lda, ptr(B), ldb, K, M, N, ptr(out), ldc,
-                                 int(accumulate), ptr(ws), stream_ptr(A.device)),
-          "gnnrec_gemm_tn_f32")
+    check(lib.gnnrec_gemm_tn_bias_f32(ptr(A), lda, ptr(B), ldb, K, M, N, ptr(out), ldc,
+                                      ptr(colsum), int(accumulate), ptr(ws),
+                                      stream_ptr(A.device)), "gnnrec_gemm_tn_bias_f32")
     return out
+
+
+def act_backward_normed(z: torch.Tensor, row_norm: torch.Tensor, gz: torch.Tensor,
+                        relu: bool = True) -> torch.Tensor:
+    """f2: gradient through relu?+L2 norm from the normalised output z and the row norms
+    gemm(..., l2norm=True, row_norm=...) wrote (gnnrec_act_backward_normed_f32)."""
+    lib = _lib.load()
+    _dev(z, "z", torch.float32)
+    _dev(gz, "gz", torch.float32)
+    _dev(row_norm, "row_norm", torch.float32)
+    n, d = z.shape
+    if tuple(gz.shape) != (n, d) or row_norm.numel() != n:
+        raise ValueError("act_backward_normed: shape mismatch")
+    gu = torch.empty((n, d), dtype=torch.float32, device=z.device)
+    check(lib.gnnrec_act_backward_normed_f32(ptr(z), _rowmajor(z, "z"), ptr(row_norm.contiguous()),
+                                             ptr(gz), _rowmajor(gz, "gz"), n, d, int(relu),
+                                             ptr(gu), d, stream_ptr(z.device)),
+          "gnnrec_act_backward_normed_f32")
+    return gu
 
 
 def act_backward(u: torch.Tensor, gz: torch.Tensor, relu: bool, l2norm: bool,

@@ -155,6 +155,14 @@ int gnnrec_gemm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
                     float out_div,
                     const float* attn_vec, float* attn_state,
                     float* out, int64_t ldo, void* stream);
+/* Same; with the L2NORM epilogue, row_norm[M] (nullable) receives each row's norm before
+ * the normalisation (0 for a zero row) — what the training backward needs besides z. */
+int gnnrec_gemm_rownorm_f32(const float* A1, int64_t lda1, int64_t K1, const float* W1,
+                            const float* A2, int64_t lda2, int64_t K2, const float* W2,
+                            const int32_t* a2_deg, int a2_mode, const float* bias,
+                            const float* bias_nonempty, int64_t M, int64_t N, int epilogue,
+                            int accum, float out_div, const float* attn_vec, float* attn_state,
+                            float* out, int64_t ldo, float* row_norm, void* stream);
 
 /* ---- a1+a3 fused: aggregation with the projection in its epilogue -----------
  * out[v] (accum)= epi( H[v] W_self^T + agg(v) W_neigh^T ),  agg(v) = reduce over v's
@@ -247,12 +255,23 @@ int64_t gnnrec_gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t N);
 int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K,
                        int64_t M, int64_t N, float* C, int64_t ldc, int accumulate,
                        float* workspace, void* stream);
+/* Same, plus colsum[M] (+)= sum_k A[k, :] (the bias gradient db = column sums of dY),
+ * accumulated from the A tiles the GEMM already stages (no separate reduction pass). */
+int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K,
+                            int64_t M, int64_t N, float* C, int64_t ldc, float* colsum,
+                            int accumulate, float* workspace, void* stream);
 /* gu = d/du of z = norm?(relu?(u)) applied to gz, flags = GNNREC_EPI_RELU|GNNREC_EPI_L2NORM
  * (norm: z = a / ||a||, rows with ||a|| == 0 unchanged — the zero-guarded norm of
  * src/model.py:231-235).  u: the pre-activation rows [n_rows, d]. */
 int gnnrec_act_backward_f32(const float* u, int64_t ldu, const float* gz, int64_t ldg,
                             int64_t n_rows, int64_t d, int flags, float* gu, int64_t ldo,
                             void* stream);
+/* The same Jacobian from the NORMALISED output z = a / |a| (a = relu?(u)) and the row
+ * norms |a| that gnnrec_gemm_rownorm_f32 wrote: gu = mask (gz - z (z.gz)) / |a| (gz for
+ * |a| == 0), mask = [z > 0] when relu — the training forward keeps z, not u. */
+int gnnrec_act_backward_normed_f32(const float* z, int64_t ldz, const float* row_norm,
+                                   const float* gz, int64_t ldg, int64_t n_rows, int64_t d,
+                                   int relu, float* gu, int64_t ldo, void* stream);
 
 /* f2: source-major transpose of a dst-major CSR block (training backward of a1; the
  * reference's DGL update_all backward, src/model.py:161-167).  indptr_t[n_src+1] (int64),

@@ -439,6 +439,16 @@ def test_gemm_tn_matches_fp64(K, M, N):
                                atol=tol)
     # deterministic: same bits twice
     assert torch.equal(ops.gemm_tn(A, B), out)
+    # bias gradient (column sums of A) from the same pass, store and accumulate
+    cs = torch.empty(M, device="cuda")
+    out2 = ops.gemm_tn(A, B, colsum=cs)
+    assert torch.equal(out2, out)
+    np.testing.assert_allclose(cs.cpu().numpy(), A.double().sum(0).cpu().numpy(), rtol=1e-4,
+                               atol=tol)
+    cs0 = cs.clone()
+    ops.gemm_tn(A, B, out=out2, accumulate=True, colsum=cs)
+    np.testing.assert_allclose(cs.cpu().numpy(), (2 * cs0.double()).cpu().numpy(), rtol=1e-5,
+                               atol=tol)
 
 
 @pytest.mark.parametrize("relu,l2", [(True, False), (False, True), (True, True)])
@@ -458,6 +468,31 @@ def test_act_backward_matches_autograd(relu, l2):
     (ref,) = torch.autograd.grad(z, x, gz)
     got = ops.act_backward(u, gz, relu=relu, l2norm=l2)
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_gemm_row_norm_and_normed_act_backward():
+    """Training keeps z = relu(u)/|relu(u)| and the row norms from one GEMM launch; the
+    Jacobian from (z, norms) equals the one from u."""
+    from gnnrec import ops
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(9)
+    M, K, N = 1000, 256, 128
+    A = torch.randn(M, K, device="cuda", generator=gen)
+    A[7] = 0.0
+    W = torch.randn(N, K, device="cuda", generator=gen) * 0.05
+    W[:, :] -= 0.02  # some rows fully negative after relu -> zero rows
+    nrm = torch.empty(M, device="cuda")
+    z = ops.gemm(A, W, relu=True, l2norm=True, row_norm=nrm)
+    u = ops.gemm(A, W)
+    y = torch.relu(u)
+    np.testing.assert_allclose(nrm.cpu().numpy(), y.norm(dim=1).cpu().numpy(), rtol=1e-5,
+                               atol=1e-6)
+    assert torch.equal(z, ops.gemm(A, W, relu=True, l2norm=True))  # same bits as inference
+    gz = torch.randn(M, N, device="cuda", generator=gen)
+    ref = ops.act_backward(u, gz, relu=True, l2norm=True)
+    got = ops.act_backward_normed(z, nrm, gz, relu=True)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    assert not got[7].any()
 
 
 def test_cosine_backward_matches_autograd():
@@ -1022,13 +1057,18 @@ def test_reference_wide_dims_match_oracle(hidden, out, agg, hagg):
                                                                (300, 1, 9, False, True),
                                                                (1000, 777, 40, True, True),
                                                                (5000, 70000, 12, True, False),
-                                                               (2000, 3000, 0, False, True)])
+                                                               (2000, 3000, 0, False, True),
+                                                               (200000, 6000, 20, False, True),
+                                                               (100000, 50, -1, False, True)])
 def test_csr_transpose_bit_exact(n_dst, n_src, max_deg, weighted, mean):
     """Source-major transpose of a block: stable (ascending edge id per source row), the
     weights carried along (· 1/deg for mean) — bit-exact vs a numpy stable sort."""
     from gnnrec import ops
     rng = np.random.default_rng(n_dst + n_src)
-    deg = rng.integers(0, max_deg + 1, n_dst)
+    if max_deg < 0:  # mostly empty rows: more dst rows than three edge slots hold
+        deg = (rng.random(n_dst) < 0.05).astype(np.int64)
+    else:
+        deg = rng.integers(0, max_deg + 1, n_dst)
     indptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
     E = int(indptr[-1])
     idx = rng.integers(0, n_src, E).astype(np.int32)
