@@ -15,10 +15,18 @@ after sampling as DGL's BlockSampler does), then per node type the sources
 are relabelled by mark/scan/compact (dst prefix first, new ids ascending).
 There are no DataLoader worker processes, no pinned host copies and no
 per-batch host->device transfer of blocks (reference run.py:104-107, 338-339).
-`num_workers` / `pin_memory` are accepted and ignored.
+`num_workers > 0` (the reference's asynchronous DataLoader workers) samples
+ahead instead: one host thread builds the next batches on a second HIP stream
+while the caller's stream runs the training step, and each batch is handed over
+through a stream event (at most `num_workers` batches in flight).  Sampling in
+that thread draws from the CUDA generator concurrently with the caller, so the
+batch sequence is reproducible only when the caller draws no random numbers
+(dropout 0).  `pin_memory` is accepted and ignored.
 """
 from __future__ import annotations
 
+import queue
+import threading
 from typing import Dict, List, Optional
 
 import torch
@@ -194,6 +202,85 @@ def _batches(n: int, batch_size: int, shuffle: bool, drop_last: bool, device):
         yield order[i:i + batch_size]
 
 
+def _tensors(obj, out):
+    """Every tensor reachable from a loader item (dicts, tuples, lists, blocks, graphs)."""
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _tensors(v, out)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _tensors(v, out)
+    elif isinstance(obj, (Block, PairGraph)):
+        _tensors(vars(obj), out)
+    return out
+
+
+class _Prefetch:
+    """Runs a batch iterator in a host thread on its own HIP stream, `depth` batches ahead.
+    Each batch is handed over with an event the consumer's stream waits on, and every
+    tensor in it is recorded on the consumer's stream (so the caching allocator does not
+    recycle it under work the consumer queued)."""
+
+    _END = object()
+
+    def __init__(self, make_iter, depth: int, device):
+        self.device = device
+        self.stream = torch.cuda.Stream(device=device)
+        self.q = queue.Queue(maxsize=max(1, depth))
+        self.stop = threading.Event()
+        self.thread = threading.Thread(target=self._run, args=(make_iter,), daemon=True)
+        self.thread.start()
+
+    def _put(self, x):
+        while not self.stop.is_set():
+            try:
+                self.q.put(x, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _run(self, make_iter):
+        try:
+            with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+                for item in make_iter():
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                    if not self._put((item, ev)):
+                        return
+            self._put(self._END)
+        except BaseException as exc:  # surfaced in the consumer
+            self._put(exc)
+
+    def __iter__(self):
+        try:
+            while True:
+                x = self.q.get()
+                if x is self._END:
+                    return
+                if isinstance(x, BaseException):
+                    raise x
+                item, ev = x
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                for t in _tensors(item, []):
+                    if t.is_cuda:
+                        t.record_stream(cur)
+                yield item
+        finally:
+            self.stop.set()
+
+
+def _maybe_prefetch(loader, make_iter):
+    n = int(getattr(loader, "num_workers", 0) or 0)
+    dev = loader.g.device
+    if n > 0 and dev.type == "cuda":
+        return iter(_Prefetch(make_iter, n, dev))
+    return make_iter()
+
+
 def _split_by_type(idx, flat_ids, type_starts, n_types):
     """Batch positions -> per-type id slices, batch order kept within a type; one readback."""
     ty = torch.bucketize(idx, type_starts[1:], right=True)
@@ -230,12 +317,16 @@ class NodeDataLoader:
         self.flat_ids = torch.cat(ids) if ids else torch.zeros(0, dtype=torch.int64, device=dev)
         self.type_starts = _type_starts(ids, dev)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+        self.num_workers = num_workers
 
     def __len__(self):
         n = self.flat_ids.numel()
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
+        return _maybe_prefetch(self, self._iter_batches)
+
+    def _iter_batches(self):
         for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
                             self.drop_last, self.g.device):
             parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
@@ -273,6 +364,7 @@ class EdgeDataLoader:
         self.flat_ids = torch.cat(ids)
         self.type_starts = _type_starts(ids, dev)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
+        self.num_workers = num_workers
 
     def __len__(self):
         n = self.flat_ids.numel()
@@ -314,6 +406,9 @@ class EdgeDataLoader:
         return node_ids, pos_l, neg_l
 
     def __iter__(self):
+        return _maybe_prefetch(self, self._iter_batches)
+
+    def _iter_batches(self):
         g = self.g
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
         for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,

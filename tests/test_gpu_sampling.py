@@ -275,3 +275,55 @@ def test_reversed_gather_backward_matches_atomic(monkeypatch):
             np.testing.assert_allclose(grads[0].cpu().numpy(), grads[1].cpu().numpy(), rtol=1e-5,
                                        atol=1e-5)
             assert torch.equal(grads[1], grads[2])
+
+
+def _flat(item):
+    from gnnrec.sampling import _tensors
+    return [t for t in _tensors(item, []) if t.is_cuda]
+
+
+@pytest.mark.parametrize("workers", [1, 3])
+def test_prefetching_loaders_match_synchronous(workers):
+    """num_workers > 0 samples ahead on a second stream: same batches, bit for bit (the
+    consumer draws no random numbers), tensors usable on the caller's stream, a training
+    step runs on them, and breaking out of the loop early does not hang."""
+    from gnnrec import nn as gnn
+    from gnnrec.sampling import (EdgeDataLoader, MultiLayerNeighborSampler, NodeDataLoader,
+                                 negative_sampler)
+    g, _ = _graph()
+
+    def edge_loader(nw):
+        torch.manual_seed(7)
+        return EdgeDataLoader(g, {BUYS: torch.arange(400), CLICKS: torch.arange(500)},
+                              MultiLayerNeighborSampler([3, 2], seed=5),
+                              exclude='reverse_types',
+                              reverse_etypes={'buys': 'bought-by', 'bought-by': 'buys',
+                                              'clicks': 'clicked-by', 'clicked-by': 'clicks'},
+                              negative_sampler=negative_sampler.Uniform(4), batch_size=64,
+                              shuffle=True, num_workers=nw)
+
+    def node_loader(nw):
+        torch.manual_seed(8)
+        return NodeDataLoader(g, {"user": torch.arange(60), "item": torch.arange(40)},
+                              MultiLayerNeighborSampler([3, 2], seed=6), batch_size=16,
+                              shuffle=True, num_workers=nw)
+
+    for make in (edge_loader, node_loader):
+        ref = [[t.clone() for t in _flat(item)] for item in make(0)]
+        got = [[t.clone() for t in _flat(item)] for item in make(workers)]
+        assert len(ref) == len(got) > 1
+        for a, b in zip(ref, got):
+            assert len(a) == len(b)
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
+    model = _model(g).train()
+    opt = torch.optim.Adam(model.parameters(), lr=0.01)
+    for step, (_, pos_g, neg_g, blocks) in enumerate(edge_loader(workers)):
+        _, ps, ns = model(blocks, blocks[0].srcdata['features'], pos_g, neg_g, True)
+        loss = gnn.max_margin_loss(ps, ns, 0.266, 4, True, pos_g.edata['recency'])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        assert torch.isfinite(loss)
+        if step == 3:
+            break  # the sampling thread stops instead of blocking on a full queue

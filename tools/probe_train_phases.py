@@ -59,7 +59,28 @@ def main():
                        "edges": {ce[1]: b.num_edges(ce) for ce in b.canonical_etypes}}
                       for b in blocks]
     ph["total"] = sum(ph.values())
-    print(json.dumps({"ms": ph, "blocks": shapes}, indent=1))
+    # whole steps without phase syncs, synchronous loader vs sampling ahead on a side stream
+    free = {}
+    for nw in (0, 2):
+        el.num_workers = nw
+        it2 = iter(el)
+
+        def step():
+            _, pos_g, neg_g, blocks = next(it2)
+            _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+            loss = gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            return loss.item()
+        for _ in range(3):
+            step()
+        t0 = t()
+        for _ in range(n):
+            step()
+        free[f"num_workers={nw}"] = (t() - t0) * 1e3 / n
+        del it2
+    print(json.dumps({"ms": ph, "step_ms": free, "blocks": shapes}, indent=1))
 
 
 if __name__ == "__main__":
