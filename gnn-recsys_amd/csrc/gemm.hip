@@ -387,6 +387,9 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt_barrier() {
   static_assert(N >= 0 && N <= 15, "vmcnt immediate");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
@@ -440,61 +443,179 @@ __global__ __launch_bounds__(256, (BN > 128 ? 1 : GEMM_WAVES_PER_SIMD)) void gem
   }
   const int64_t my_row = m0 + wave * 32 + r;  // the A row this lane's fragments come from
 
+  // both operand pairs (A1,W1) then (A2,W2) as ONE stream of K tiles, so the DMA of the
+  // first A2 tile overlaps the last A1 tile's MFMAs (no pipeline restart between segments)
+  const int nk1 = (int)(g.K1 / BK), nk = nk1 + (int)(g.K2 / BK);
+  float rowdiv2 = 1.f;
+  bool rowzero2 = false;
+  if (g.K2 > 0 && g.a2_mode != GNNREC_A2_NONE) {
+    const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
+    if (g.a2_mode == GNNREC_A2_DIV_DEG) rowdiv2 = (float)(dg > 0 ? dg : 1);
+    else rowzero2 = dg == 0;
+  }
+  auto issue = [&](int kt, int buf) {
+    const bool s2 = kt >= nk1;
+    const float* A = s2 ? g.A2 : g.A1;
+    const float* W = s2 ? g.W2 : g.W1;
+    const int64_t K = s2 ? g.K2 : g.K1;
+    const int64_t lda = s2 ? g.lda2 : g.lda1;
+    const int64_t k0 = (int64_t)(s2 ? kt - nk1 : kt) * BK;
+    float* base = smem + buf * TILE;
+#pragma unroll
+    for (int q = 0; q < AI; ++q)
+      dma16(A + a_row[q] * lda + k0 + a_chk[q], base + (wave * AI + q) * 256);
+#pragma unroll
+    for (int q = 0; q < WI; ++q)
+      dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK + (wave * WI + q) * 256);
+  };
+  if (nk > 0) issue(0, 0);
 #pragma unroll 1
-  for (int seg = 0; seg < 2; ++seg) {
-    const float* A = seg ? g.A2 : g.A1;
-    const float* W = seg ? g.W2 : g.W1;
-    const int64_t K = seg ? g.K2 : g.K1;
-    const int64_t lda = seg ? g.lda2 : g.lda1;
-    if (K == 0) continue;
-    const int mode = seg ? g.a2_mode : GNNREC_A2_NONE;
-    float rowdiv = 1.f;
-    bool rowzero = false;
-    if (mode != GNNREC_A2_NONE) {
-      const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
-      if (mode == GNNREC_A2_DIV_DEG) rowdiv = (float)(dg > 0 ? dg : 1);
-      else rowzero = dg == 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, buf ^ 1);
+      wait_vmcnt_barrier<AI + WI>();  // this wave's tile-kt DMA landed; all waves past it
+    } else {
+      wait_vmcnt_barrier<0>();
     }
-    auto issue = [&](int64_t k0, int buf) {
-      float* base = smem + buf * TILE;
+    const bool s2 = kt >= nk1;
+    const bool divide = s2 && g.a2_mode == GNNREC_A2_DIV_DEG;
+    const bool zero = s2 && rowzero2;
+    const float* As = smem + buf * TILE + (wave * 32 + r) * BK;
+    const float* Ws = smem + buf * TILE + BM * BK + r * BK;
 #pragma unroll
-      for (int q = 0; q < AI; ++q)
-        dma16(A + a_row[q] * lda + k0 + a_chk[q], base + (wave * AI + q) * 256);
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int pc = ((h * 4 + s4) ^ sw) * 4;
+      f32x4 a = *reinterpret_cast<const f32x4*>(As + pc);
+      if (divide) a = a / rowdiv2;
+      else if (zero) a = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 b[NT];
 #pragma unroll
-      for (int q = 0; q < WI; ++q)
-        dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK + (wave * WI + q) * 256);
-    };
-    const int nk = (int)(K / BK);
-    issue(0, 0);
-#pragma unroll 1
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < nk) {
-        issue((int64_t)(kt + 1) * BK, buf ^ 1);
-        wait_vmcnt_barrier<AI + WI>();  // this wave's tile-kt DMA landed; all waves past it
-      } else {
-        wait_vmcnt_barrier<0>();
-      }
-      const float* As = smem + buf * TILE + (wave * 32 + r) * BK;
-      const float* Ws = smem + buf * TILE + BM * BK + r * BK;
+      for (int t = 0; t < NT; ++t)
+        b[t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK + pc);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int pc = ((h * 4 + s4) ^ sw) * 4;
-        f32x4 a = *reinterpret_cast<const f32x4*>(As + pc);
-        if (mode == GNNREC_A2_DIV_DEG) a = a / rowdiv;
-        else if (rowzero) a = f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 b[NT];
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          b[t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK + pc);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
+  }
+  gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
+}
+
+// ---- the same with 16-deep K tiles (short-K shapes) --------------------------------
+// Half the LDS of the 32-deep kernel (2 x 16 KB at BN=128), so three blocks share a CU
+// (three waves per SIMD): one block's DMA prologue and store epilogue overlap the others'
+// MFMAs, which is where a K=128..256 GEMM loses its time.  LDS image per wave-instruction:
+// 16 rows x 64 B; 16-B chunk j of tile row R sits at chunk j ^ ((R >> 2) & 3), so the 16
+// rows a 16-lane ds_read_b128 group touches map to 16 distinct 4-bank slots.
+constexpr int BK16 = 16;
+
+template <int BN>
+constexpr int glds16_smem_floats() {
+  return 2 * (BM + BN) * BK16 > smem_floats<BN>() ? 2 * (BM + BN) * BK16 : smem_floats<BN>();
+}
+
+template <int BN>
+__global__ __launch_bounds__(256, 3) void gemm_f32_glds16_kernel(GemmArgs g) {
+  constexpr int NT = BN / 32;
+  constexpr int AI = BM * BK16 * 4 / 1024 / 4;   // A-tile DMA instructions per wave (2)
+  constexpr int WI = BN * BK16 * 4 / 1024 / 4;   // W-tile DMA instructions per wave (BN/64)
+  constexpr int TILE = (BM + BN) * BK16;
+  static_assert(WI >= 1, "BN >= 64");
+  __shared__ __attribute__((aligned(16))) float smem[glds16_smem_floats<BN>()];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int sw = (r >> 2) & 3;
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+
+  // DMA source rows of this lane (tile row R = instr*16 + lane/4, physical chunk lane%4)
+  int64_t a_row[AI], w_row[WI];
+  int a_chk[AI], w_chk[WI];
+#pragma unroll
+  for (int q = 0; q < AI; ++q) {
+    const int R = (wave * AI + q) * 16 + (lane >> 2);
+    const int64_t gm = m0 + R;
+    a_row[q] = gm < g.M ? gm : g.M - 1;
+    a_chk[q] = ((lane & 3) ^ ((R >> 2) & 3)) * 4;
+  }
+#pragma unroll
+  for (int q = 0; q < WI; ++q) {
+    const int R = (wave * WI + q) * 16 + (lane >> 2);
+    const int64_t gn = n0 + R;
+    w_row[q] = gn < g.N ? gn : g.N - 1;
+    w_chk[q] = ((lane & 3) ^ ((R >> 2) & 3)) * 4;
+  }
+  const int64_t my_row = m0 + wave * 32 + r;
+
+  // both operand pairs (A1,W1) then (A2,W2) as ONE stream of K tiles, so the DMA of the
+  // first A2 tile overlaps the last A1 tile's MFMAs (no pipeline restart between segments)
+  const int nk1 = (int)(g.K1 / BK16), nk = nk1 + (int)(g.K2 / BK16);
+  float rowdiv2 = 1.f;
+  bool rowzero2 = false;
+  if (g.K2 > 0 && g.a2_mode != GNNREC_A2_NONE) {
+    const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
+    if (g.a2_mode == GNNREC_A2_DIV_DEG) rowdiv2 = (float)(dg > 0 ? dg : 1);
+    else rowzero2 = dg == 0;
+  }
+  auto issue = [&](int kt, int buf) {
+    const bool s2 = kt >= nk1;
+    const float* A = s2 ? g.A2 : g.A1;
+    const float* W = s2 ? g.W2 : g.W1;
+    const int64_t K = s2 ? g.K2 : g.K1;
+    const int64_t lda = s2 ? g.lda2 : g.lda1;
+    const int64_t k0 = (int64_t)(s2 ? kt - nk1 : kt) * BK16;
+    float* base = smem + buf * TILE;
+#pragma unroll
+    for (int q = 0; q < AI; ++q)
+      dma16(A + a_row[q] * lda + k0 + a_chk[q], base + (wave * AI + q) * 256);
+#pragma unroll
+    for (int q = 0; q < WI; ++q)
+      dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK16 + (wave * WI + q) * 256);
+  };
+  if (nk > 0) issue(0, 0);
+#pragma unroll 1
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, buf ^ 1);
+      wait_vmcnt_barrier<AI + WI>();  // this wave's tile-kt DMA landed; all waves past it
+    } else {
+      wait_vmcnt_barrier<0>();
+    }
+    const bool s2 = kt >= nk1;
+    const bool divide = s2 && g.a2_mode == GNNREC_A2_DIV_DEG;
+    const bool zero = s2 && rowzero2;
+    const float* As = smem + buf * TILE + (wave * 32 + r) * BK16;
+    const float* Ws = smem + buf * TILE + BM * BK16 + r * BK16;
+#pragma unroll
+    for (int s4 = 0; s4 < 2; ++s4) {
+      const int pc = ((h * 2 + s4) ^ sw) * 4;
+      f32x4 a = *reinterpret_cast<const f32x4*>(As + pc);
+      if (divide) a = a / rowdiv2;
+      else if (zero) a = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 b[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        b[t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK16 + pc);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
   }
   gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
 }
@@ -508,6 +629,20 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
     const char* e = getenv("GNNREC_GEMM_DMA");
     return !(e && e[0] == '0');
   }();
+  // 16-deep K tiles (three blocks per CU) for 128-column outputs: +5-10 % at K = 128..256
+  // (tools/bench_gemm_k.py); GNNREC_GEMM_BK16=0 keeps the 32-deep kernel
+  static const bool use_bk16 = [] {
+    const char* e = getenv("GNNREC_GEMM_BK16");
+    return !(e && e[0] == '0');
+  }();
+  if constexpr (BN == 128) {
+    const bool fast16 = g.vecA1 && g.vecW1 && g.K1 % BK16 == 0 &&
+                        (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK16 == 0));
+    if (fast16 && use_dma && use_bk16) {
+      hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN>), grid, dim3(256), 0, s, g);
+      return check_launch("gnnrec_gemm_f32");
+    }
+  }
   if (fast && use_dma) hipLaunchKernelGGL((gemm_f32_glds_kernel<BN>), grid, dim3(256), 0, s, g);
   else if (fast) hipLaunchKernelGGL((gemm_f32_kernel<BN, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gemm_f32_kernel<BN, false>), grid, dim3(256), 0, s, g);
