@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--segments", type=int, default=8,
                     help="source-range tiles of the user->item relation (0: none; "
                          "deterministic mode needs a power of two divisible by the GPU count)")
+    ap.add_argument("--concurrency", default="auto",
+                    help="row-kernel schedule: 'auto' (static at one rank; 16 CUs reserved + "
+                         "work queue beside RCCL at several) or 'R,Q' (R reserved CUs, Q=1 queue)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-scale", type=float, default=0.1,
                     help="fraction of the graph used for the bounded CPU-baseline sample")
@@ -226,8 +229,12 @@ def main():
     model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
                           args.aggregator, "cos", args.hetero, True).to(dev).eval()
     ex = Exchange()
+    conc = None
+    if args.concurrency != "auto":
+        r, q = args.concurrency.split(",")
+        conc = (int(r), bool(int(q)))
     runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap,
-                                  deterministic=det)
+                                  deterministic=det, concurrency=conc)
     timers = EventTimers()
     runner.timers = timers
     torch.cuda.synchronize()
@@ -299,7 +306,12 @@ def main():
                                       else ""),
                        "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
                        "output": "partitioned (each rank keeps the user and item rows it owns)",
-                       "overlap": not args.no_overlap},
+                       "overlap": not args.no_overlap,
+                       "row_schedule": ("static" if not runner.concurrency or
+                                        not runner.concurrency[1] else "queue")
+                                       + (f", {runner.concurrency[0]} CUs reserved"
+                                          if runner.concurrency and runner.concurrency[0]
+                                          else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

@@ -1,0 +1,108 @@
+// Host side of the row queue (rowq.hpp) and the concurrency knobs of the row kernels,
+// plus a diagnostic kernel that holds CUs the way a collective kernel does.
+#include "common.hpp"
+#include "rowq.hpp"
+
+#include <atomic>
+#include <mutex>
+
+namespace gnnrec {
+namespace {
+
+constexpr int kMaxDevices = 64;
+constexpr unsigned kRqSlots = 1024;  // launches that may be in flight on one device at once
+
+std::atomic<int> g_reserve{0};
+std::atomic<int> g_dynamic{1};  // the queue is the default schedule
+std::mutex g_mu;
+unsigned* g_ring[kMaxDevices] = {};
+std::atomic<unsigned> g_next[kMaxDevices];
+int g_cus[kMaxDevices] = {};
+
+int current_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev >= 0 && dev < kMaxDevices ? dev : 0;
+}
+
+// `ticks` of the wall clock with the launch's dynamic LDS allocated: the residency of a
+// collective kernel beside the row kernels (tools/probe_comm_overlap.py)
+__global__ void hold_kernel(int64_t ticks, float* sink) {
+  extern __shared__ float lds[];
+  lds[threadIdx.x] = (float)threadIdx.x;
+  __syncthreads();
+  const uint64_t t0 = wall_clock64();
+  float acc = 0.f;
+  while ((int64_t)(wall_clock64() - t0) < ticks) {
+    acc += lds[(threadIdx.x + 1) % blockDim.x];
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (acc < 0.f) sink[threadIdx.x] = acc;  // never taken: keeps the loop's loads
+}
+
+}  // namespace
+
+int device_cus() {
+  const int dev = current_device();
+  if (g_cus[dev] == 0) {
+    int n = 0;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_cus[dev] = n > 0 ? n : 256;
+  }
+  return g_cus[dev];
+}
+
+int cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
+
+unsigned* rowq_slot() {
+  if (!g_dynamic.load(std::memory_order_relaxed)) return nullptr;
+  const int dev = current_device();
+  if (g_ring[dev] == nullptr) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ring[dev] == nullptr) {
+      unsigned* p = nullptr;
+      const size_t bytes = (size_t)kRqSlots * kRqSlotWords * sizeof(unsigned);
+      if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;  // static schedule instead
+      if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+      }
+      g_ring[dev] = p;
+    }
+  }
+  const unsigned i = g_next[dev].fetch_add(1, std::memory_order_relaxed) % kRqSlots;
+  return g_ring[dev] + (size_t)i * kRqSlotWords;
+}
+
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+extern "C" int gnnrec_set_concurrency(int reserve_cus, int dynamic) {
+  GNNREC_REQUIRE(reserve_cus >= 0 && reserve_cus < 1024,
+                 "gnnrec_set_concurrency: reserve_cus %d out of range", reserve_cus);
+  g_reserve.store(reserve_cus);
+  g_dynamic.store(dynamic ? 1 : 0);
+  return GNNREC_OK;
+}
+
+extern "C" int gnnrec_get_concurrency(int* reserve_cus, int* dynamic) {
+  GNNREC_REQUIRE(reserve_cus && dynamic, "gnnrec_get_concurrency: null pointer");
+  *reserve_cus = g_reserve.load();
+  *dynamic = g_dynamic.load();
+  return GNNREC_OK;
+}
+
+extern "C" int gnnrec_hold_cus(int blocks, int threads, int lds_bytes, int64_t usec,
+                               float* sink, void* stream) {
+  GNNREC_REQUIRE(blocks > 0 && blocks <= 4096 && threads >= 64 && threads <= 1024 &&
+                     threads % 64 == 0 && lds_bytes >= threads * 4 && lds_bytes <= 64 * 1024 &&
+                     usec >= 0 && usec <= 1000000 && sink,
+                 "gnnrec_hold_cus: bad arguments");
+  int khz = 0;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, current_device());
+  const int64_t ticks = usec * (int64_t)(khz > 0 ? khz : 100000) / 1000;
+  hipLaunchKernelGGL(hold_kernel, dim3(blocks), dim3(threads), (size_t)lds_bytes,
+                     as_stream(stream), ticks, sink);
+  return check_launch("gnnrec_hold_cus");
+}

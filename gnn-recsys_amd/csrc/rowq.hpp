@@ -1,0 +1,83 @@
+// Dynamic row distribution for the long-running row kernels (spmm_csr_kernel, the fused
+// spmm_project_kernel) when they share the chip with another kernel — in a multi-rank
+// pass, RCCL's collective kernels launched on their own stream beside the aggregation.
+//
+// Why: those kernels hand out rows statically (grid-stride), and the fused one keeps one
+// block per CU with all 160 KiB of its LDS.  A collective kernel dispatched first holds
+// some CUs; the fused blocks bound to those CUs start only when it ends and then still
+// owe their whole static share, so the launch ends one collective later (the exchange is
+// serialised, not overlapped).  With a queue, a late block simply takes fewer rows.
+//
+// Shape: the rows are cut into 8 contiguous ranges, one per XCD; a wave dequeues chunks of
+// `ch` rows from its own XCD's head (agent-scope atomic, ≈1 µs; ≈30 dequeues/µs per head
+// at C4 shapes, under the ≈88/µs a single word sustains) and, once that range is drained,
+// from the other heads in turn, so every wave reaches every head's end and exits.  The
+// next ticket is requested before the current chunk runs.  Which wave reduces a row does
+// not change how it is reduced: outputs stay bitwise identical to the static schedule.
+//
+// Slots: every launch takes the next slot of a per-device ring (host side, rowq.hip); the
+// last block to finish resets the slot's heads, so the next user finds zeros without a
+// memset.  A slot holds 8 heads + 1 exit counter, each on its own 128-B line.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gnnrec {
+
+constexpr int kRqHeads = 8;
+constexpr int kRqStride = 32;  // uint32 words per head: 128-B lines
+constexpr int kRqSlotWords = (kRqHeads + 1) * kRqStride;
+
+// host (rowq.hip)
+unsigned* rowq_slot();  // next slot of the current device's ring, or nullptr (static mode)
+int device_cus();       // CUs of the current device
+int cu_reserve();       // CUs the row kernels leave free for concurrent kernels
+
+__device__ inline int xcc_id() {
+  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): size-1 in [15:11], offset [10:6], id 20
+  return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kRqHeads - 1);
+}
+
+// lane 0 draws a ticket; the value is read (broadcast) only when the chunk is claimed
+__device__ inline unsigned rq_take(unsigned* head) {
+  unsigned t = 0;
+  if ((threadIdx.x & 63) == 0)
+    t = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return t;
+}
+
+// f(r0, r1) for chunks [r0, r1) of [0, n) until every head is drained (wave-uniform)
+template <class F>
+__device__ inline void rq_for_each(unsigned* q, int64_t n, int ch, F&& f) {
+  int h = xcc_id();
+  for (int visit = 0; visit < kRqHeads; ++visit, h = (h + 1) & (kRqHeads - 1)) {
+    const int64_t lo = n * h / kRqHeads, hi = n * (h + 1) / kRqHeads;
+    if (lo >= hi) continue;
+    unsigned* head = q + h * kRqStride;
+    unsigned t = rq_take(head);
+    while (true) {
+      const int64_t r0 = lo + (int64_t)__shfl(t, 0) * ch;
+      if (r0 >= hi) break;
+      t = rq_take(head);  // the next ticket is in flight while this chunk runs
+      f(r0, r0 + ch < hi ? r0 + ch : hi);
+    }
+  }
+}
+
+// end of a queued launch: after every wave of the block has left rq_for_each, one lane
+// counts the block out; the last block of the grid zeroes the slot for its next user
+__device__ inline void rq_finish(unsigned* q) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
+    unsigned* done = q + kRqHeads * kRqStride;
+    if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        nblk - 1) {
+      for (int h = 0; h < kRqHeads; ++h)
+        __hip_atomic_store(q + h * kRqStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace gnnrec

@@ -22,28 +22,31 @@
 // workspace, then combined per row in chunk order (deterministic two-phase).
 #include "common.hpp"
 #include "gather.hpp"
+#include "rowq.hpp"
 #include <cmath>
 #include <cstdlib>
 
 namespace gnnrec {
 namespace {
 
+// rows per queue ticket of the row kernel (rowq.hpp): ≈70 µs of one wave's gather at C4
+constexpr int kRowChunk = 2;
+
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
-    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg) {
+    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq) {
   const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
   const int col = blockIdx.y * (LPR * VEC) + (lane % LPR) * VEC;
   const bool colok = col < d;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
-  const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_dst; row += wstride) {
+  auto one_row = [&](int64_t row) {
     const int64_t beg = indptr[row];
     const int64_t end = indptr[row + 1];
-    if (end - beg > max_deg) continue;  // heavy row: reduced by the chunk kernels
+    if (end - beg > max_deg) return;  // heavy row: reduced by the chunk kernels
     Frag<VEC> acc;
 #pragma unroll
     for (int v = 0; v < VEC; ++v) acc.v[v] = init;
@@ -55,7 +58,17 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
       if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(acc, out + row * ldo + col);
       store_frag<VEC>(out + row * ldo + col, acc);
     }
+  };
+  if (rq != nullptr) {  // queued rows (one column slice: the launcher checks gridDim.y == 1)
+    rq_for_each(rq, n_dst, kRowChunk, [&](int64_t r0, int64_t r1) {
+      for (int64_t row = r0; row < r1; ++row) one_row(row);
+    });
+    rq_finish(rq);
+    return;
   }
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_dst; row += wstride)
+    one_row(row);
 }
 
 // phase 1 of heavy rows: one wave per chunk of `split` edges -> raw partial in ws[chunk]
@@ -143,7 +156,9 @@ inline int64_t blocks_per_cu() {
 
 inline unsigned grid_waves(int64_t units) {
   int64_t blocks = (units + 3) / 4;
-  const int64_t max_blocks = 256 * blocks_per_cu();
+  // CUs reserved for concurrent kernels (gnnrec_set_concurrency) come off the grid
+  const int cus = device_cus() - cu_reserve();
+  const int64_t max_blocks = (int64_t)(cus > 8 ? cus : 8) * blocks_per_cu();
   if (blocks > max_blocks) blocks = max_blocks;
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
@@ -155,9 +170,12 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
   const int eni = a.flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
   const int64_t max_deg = a.n_heavy > 0 ? a.split : INT64_MAX;
+  const unsigned grid = grid_waves(a.n_dst);
+  // the queue pays off on long launches only (≥ 8 rows per wave of the grid)
+  unsigned* rq = slices == 1 && a.n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot() : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
-                     dim3(grid_waves(a.n_dst), slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
-                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg);
+                     dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
+                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                        dim3(grid_waves(a.n_chunks), slices), dim3(256), 0, s, a.indptr, a.indices,

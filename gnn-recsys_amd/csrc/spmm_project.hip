@@ -20,6 +20,7 @@
 // ds_read_b64) + per wave ROWS × (agg, self) row slots read back as broadcasts.
 #include "common.hpp"
 #include "gather.hpp"
+#include "rowq.hpp"
 #include <cstdlib>
 
 namespace gnnrec {
@@ -28,6 +29,7 @@ namespace {
 constexpr int kPD = 128;       // d_neigh = d_self = N
 constexpr int kPWaves = 16;    // waves per block (one persistent block per CU)
 constexpr int kPRows = 2;      // rows per wave per iteration (halves the LDS weight reads)
+constexpr int kPChunk = 4;     // rows per queue ticket (rowq.hpp): two iterations, ≈60 µs at C4
 
 template <int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
@@ -37,7 +39,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const float* __restrict__ WnT, const float* __restrict__ bias,
     const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
     const float* __restrict__ attn_vec, float* __restrict__ attn_state,
-    float* __restrict__ out, int64_t ldo) {
+    float* __restrict__ out, int64_t ldo, unsigned* rq) {
   __shared__ float Ws[kPD * kPD];
   __shared__ float Wn[kPD * kPD];
   __shared__ float slots[kPWaves][kPRows][2][kPD];
@@ -61,13 +63,13 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
   const float a0 = attn ? attn_vec[j0] : 0.f, a1 = attn ? attn_vec[j0 + 1] : 0.f;
 
-  for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
-       row0 += stride) {
+  // rows [row0, row0 + kPRows) of this wave, those at or past `lim` skipped
+  auto step = [&](int64_t row0, int64_t lim) {
     bool nonempty[kPRows];
 #pragma unroll
     for (int r = 0; r < kPRows; ++r) {
       const int64_t row = row0 + r;
-      const bool valid = row < n_dst;  // uniform per wave
+      const bool valid = row < lim;  // uniform per wave
       float4 hs = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid && grp == 1) hs = *reinterpret_cast<const float4*>(H + row * ldh + col);
       Frag<VEC> acc;
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) e += __shfl_xor(e, off);
         float mnew = e, snew = 1.f, cnew = 1.f;
-        if (row < n_dst && accum != GNNREC_ACC_ATTN_FIRST) {
+        if (row < lim && accum != GNNREC_ACC_ATTN_FIRST) {
           const float2 st = reinterpret_cast<const float2*>(attn_state)[row];
           mnew = fmaxf(st.x, e);
           keep = expf(st.x - mnew);
@@ -157,12 +159,12 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
           snew = st.y * keep + cnew;
         }
         if (accum == GNNREC_ACC_ATTN_LAST) nrm_attn = 1.f / snew;
-        if (row < n_dst && lane == 0)
+        if (row < lim && lane == 0)
           reinterpret_cast<float2*>(attn_state)[row] = make_float2(mnew, snew);
         y0 *= cnew;
         y1 *= cnew;
       }
-      if (row >= n_dst) continue;
+      if (row >= lim) continue;
       float2* p = reinterpret_cast<float2*>(out + row * ldo + j0);
       if (attn) {
         if (accum != GNNREC_ACC_ATTN_FIRST) {
@@ -188,10 +190,19 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
       }
       *p = make_float2(y0, y1);
     }
-  }
-}
+  };
 
-int g_num_cus = 0;
+  if (rq != nullptr) {  // rows from the queue: blocks that start late take fewer
+    rq_for_each(rq, n_dst, kPChunk, [&](int64_t r0, int64_t r1) {
+      for (int64_t row0 = r0; row0 < r1; row0 += kPRows) step(row0, r1);
+    });
+    rq_finish(rq);
+    return;
+  }
+  for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
+       row0 += stride)
+    step(row0, n_dst);
+}
 
 }  // namespace
 }  // namespace gnnrec
@@ -225,15 +236,13 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
                      ldx % 4 == 0 && ldh % 4 == 0 && ldo % 2 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                  "gnnrec_spmm_project_f32: X/H/W need 16-B aligned rows, out 8-B");
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
+  // one persistent block per CU, minus the CUs reserved for concurrent kernels
   const int64_t per_block = (int64_t)kPWaves * kPRows;
   int64_t blocks = (n_dst + per_block - 1) / per_block;
-  if (blocks > g_num_cus) blocks = g_num_cus;
+  const int64_t cus = device_cus() - cu_reserve();
+  if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
+  // queued rows when every wave has several tickets of work
+  unsigned* rq = n_dst >= blocks * kPWaves * kPChunk * 4 ? rowq_slot() : nullptr;
   const dim3 grid((unsigned)blocks), block(kPWaves * 64);
   hipStream_t s = as_stream(stream);
   static const int unroll = [] {  // gather wave-instructions in flight per lane (tuning knob)
@@ -243,7 +252,7 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
 #define GNNREC_SPP_ONE(R, W, U)                                                              \
   hipLaunchKernelGGL((spmm_project_kernel<R, W, U>), grid, block, 0, s, indptr, indices, ew, X, \
                      ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum, \
-                     out_div, attn_vec, attn_state, out, ldo)
+                     out_div, attn_vec, attn_state, out, ldo, rq)
 #define GNNREC_SPP(R, W)                                  \
   do {                                                    \
     if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \

@@ -212,6 +212,9 @@ class GraphShard:
         return out
 
 
+RESERVE_CUS = 16  # of 256: room for RCCL's channel blocks beside the aggregation
+
+
 class ShardedFullGraphPass:
     """Layer-wise full-graph ConvModel pass over a GraphShard (one rank's view).
 
@@ -231,7 +234,7 @@ class ShardedFullGraphPass:
 
     def __init__(self, model, shard: GraphShard, exchange: Optional[Exchange] = None,
                  ops_backend=None, overlap: bool = True, fold_embedding: bool = True,
-                 deterministic: bool = False):
+                 deterministic: bool = False, concurrency=None):
         self.model = model
         # deterministic: outputs bitwise independent of the world size (needs a shard built
         # with `segments`): replicated-type sums are per-segment partials folded in a fixed
@@ -257,6 +260,17 @@ class ShardedFullGraphPass:
         self._ready = {}     # id(table) -> event on the side stream producing it
         self.side = (torch.cuda.Stream(device=shard.device)
                      if overlap and shard.device.type == 'cuda' else None)
+        # (reserve_cus, dynamic) of the row kernels (ops.set_concurrency) during the pass:
+        # rows come from the device work queue (each XCD on its own contiguous range; C4
+        # one GPU 149 -> 144 ms), and with several ranks RESERVE_CUS CUs stay free so
+        # RCCL's kernels find room, while aggregation blocks that start behind one take
+        # fewer rows instead of ending the launch a collective late
+        # (tools/probe_comm_overlap.py).  Default on HIP devices: (0, True) at one rank,
+        # (RESERVE_CUS, True) at several with overlap on.
+        if concurrency is None and shard.device.type == 'cuda':
+            concurrency = (RESERVE_CUS if self.ex.ws > 1 and self.side is not None else 0,
+                           True)
+        self.concurrency = concurrency
         self.timers = None  # optional callable(tag) -> context manager (bench)
         self.fused = set()  # relations whose aggregation ran with the projection fused
         self._last, self._replicate_last = False, True
@@ -296,6 +310,13 @@ class ShardedFullGraphPass:
         {ptype: [n_own, out]} and the replicated types as full padded tables, or — with
         replicate_output=False — as this rank's own row block of them (own_slice), so the
         last layer's all-gather is skipped and every type's output stays partitioned."""
+        mode = getattr(self.ops, 'concurrency', None)
+        if self.concurrency is None or mode is None:
+            return self._run(feats, embedding_layer, replicate_output)
+        with mode(*self.concurrency):
+            return self._run(feats, embedding_layer, replicate_output)
+
+    def _run(self, feats, embedding_layer, replicate_output):
         m, O, sh = self.model, self.ops, self.shard
         self._replicate_last = replicate_output
         if embedding_layer is None:

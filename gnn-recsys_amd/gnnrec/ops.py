@@ -7,6 +7,8 @@ an error.
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
 import os
 
 from typing import Optional
@@ -53,6 +55,48 @@ def _rowmajor(t: torch.Tensor, name: str) -> int:
         raise ValueError(f"{name} must have unit column stride")
     return max(t.stride(0), t.shape[1], 1)
 
+
+def set_concurrency(reserve_cus: int = 0, dynamic: bool = False) -> None:
+    """Process-wide mode of the row kernels (spmm, spmm_project) for launches that share
+    the chip with kernels on other streams (gnnrec_set_concurrency): leave `reserve_cus`
+    CUs free, and hand rows out through a device work queue when `dynamic`."""
+    check(_lib.load().gnnrec_set_concurrency(int(reserve_cus), int(bool(dynamic))),
+          "gnnrec_set_concurrency")
+
+
+def get_concurrency():
+    """(reserve_cus, dynamic) currently in force."""
+    r, d = ctypes.c_int(), ctypes.c_int()
+    check(_lib.load().gnnrec_get_concurrency(ctypes.byref(r), ctypes.byref(d)),
+          "gnnrec_get_concurrency")
+    return r.value, bool(d.value)
+
+
+@contextlib.contextmanager
+def concurrency(reserve_cus: int, dynamic: bool = True):
+    """set_concurrency for the launches enqueued inside the block, restored after."""
+    old = get_concurrency()
+    set_concurrency(reserve_cus, dynamic)
+    try:
+        yield
+    finally:
+        set_concurrency(*old)
+
+
+def hold_cus(blocks: int, usec: int, threads: int = 256, lds_bytes: int = 16384,
+             stream=None) -> None:
+    """Diagnostic: `blocks` workgroups holding `lds_bytes` of LDS each stay resident for
+    `usec` µs on `stream` (default: current) — a collective kernel's footprint."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    sink = _hold_sink.get(dev.index)
+    if sink is None:
+        sink = _hold_sink[dev.index] = torch.empty(1024, dtype=torch.float32, device=dev)
+    s = (stream if stream is not None else torch.cuda.current_stream(dev)).cuda_stream
+    check(_lib.load().gnnrec_hold_cus(int(blocks), int(threads), int(lds_bytes), int(usec),
+                                      ptr(sink), s), "gnnrec_hold_cus")
+
+
+_hold_sink = {}
 
 DEFAULT_SPLIT = 2048  # edges per chunk for rows split across wavefronts
 

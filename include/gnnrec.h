@@ -91,6 +91,29 @@ extern "C" {
 int gnnrec_version(void);
 const char* gnnrec_last_error(void);
 
+/* Concurrency mode of the long-running row kernels (gnnrec_spmm_csr_f32 and its
+ * _split / _planned forms, gnnrec_spmm_project_f32) when they share the chip with
+ * kernels on other streams — RCCL's collectives in a multi-rank pass:
+ *   reserve_cus  CUs the launches leave free (grids sized for CUs - reserve_cus);
+ *   dynamic      1: rows are handed out by a device work queue (one head per XCD,
+ *                then the other heads in turn) instead of a static grid-stride, so
+ *                blocks that start late, behind a collective, take fewer rows.
+ * The queue also keeps each XCD on a contiguous eighth of the rows (one range per
+ * XCD), which is faster alone (C4 fused launch 36.7 -> 34.7 ms).  Outputs are bitwise
+ * identical in every mode.  Process-wide, read at launch time; default (0, 1).  The
+ * first queued launch on a device allocates its queue ring (1.2 MB, hipMalloc +
+ * memset, synchronous, once). */
+int gnnrec_set_concurrency(int reserve_cus, int dynamic);
+int gnnrec_get_concurrency(int* reserve_cus, int* dynamic);
+
+/* Diagnostic (no reference counterpart): `blocks` workgroups of `threads` threads,
+ * each holding `lds_bytes` of LDS, stay resident for `usec` microseconds on
+ * `stream` — a stand-in for a collective kernel's residency when measuring how the
+ * row kernels share the chip with one (tools/probe_comm_overlap.py).  sink:
+ * >= threads floats, never written in practice. */
+int gnnrec_hold_cus(int blocks, int threads, int lds_bytes, int64_t usec, float* sink,
+                    void* stream);
+
 /* ---- a1: gather + aggregate over a dst-major CSR (K1-K3) ----------------
  * out[v, :] = reduce_{e in [indptr[v], indptr[v+1])} X[indices[e], :] * (ew ? ew[e] : 1)
  * MEAN divides the sum by max(deg,1); MAX of an empty row is 0 (or -inf with
