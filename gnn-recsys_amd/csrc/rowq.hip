@@ -4,6 +4,7 @@
 #include "rowq.hpp"
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 
 namespace gnnrec {
@@ -13,7 +14,11 @@ constexpr int kMaxDevices = 64;
 constexpr unsigned kRqSlots = 1024;  // launches that may be in flight on one device at once
 
 std::atomic<int> g_reserve{0};
-std::atomic<int> g_dynamic{1};  // the queue is the default schedule
+// the queue is the default schedule; GNNREC_ROWQ=0 makes the static grid-stride the default
+std::atomic<int> g_dynamic{[] {
+  const char* e = getenv("GNNREC_ROWQ");
+  return e && e[0] == '0' ? 0 : 1;
+}()};
 std::mutex g_mu;
 unsigned* g_ring[kMaxDevices] = {};
 std::atomic<unsigned> g_next[kMaxDevices];

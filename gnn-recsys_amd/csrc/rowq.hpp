@@ -11,8 +11,8 @@
 // Shape: the rows are cut into 8 contiguous ranges, one per XCD; a wave dequeues chunks of
 // `ch` rows from its own XCD's head (agent-scope atomic, ≈1 µs; ≈30 dequeues/µs per head
 // at C4 shapes, under the ≈88/µs a single word sustains) and, once that range is drained,
-// from the other heads in turn, so every wave reaches every head's end and exits.  The
-// next ticket is requested before the current chunk runs.  Which wave reduces a row does
+// from the other heads (all 8 read at once), so every wave sees every head drained and
+// exits.  The next ticket is requested before the current chunk runs.  Which wave reduces a row does
 // not change how it is reduced: outputs stay bitwise identical to the static schedule.
 //
 // Slots: every launch takes the next slot of a per-device ring (host side, rowq.hip); the
@@ -46,21 +46,42 @@ __device__ inline unsigned rq_take(unsigned* head) {
   return t;
 }
 
-// f(r0, r1) for chunks [r0, r1) of [0, n) until every head is drained (wave-uniform)
+// tickets of head h until its range is drained: f(r0, r1) per chunk (wave-uniform)
+template <class F>
+__device__ inline void rq_drain(unsigned* q, int64_t n, int ch, int h, F& f) {
+  const int64_t lo = n * h / kRqHeads, hi = n * (h + 1) / kRqHeads;
+  if (lo >= hi) return;
+  unsigned* head = q + h * kRqStride;
+  unsigned t = rq_take(head);
+  while (true) {
+    const int64_t r0 = lo + (int64_t)__shfl(t, 0) * ch;
+    if (r0 >= hi) return;
+    t = rq_take(head);  // the next ticket is in flight while this chunk runs
+    f(r0, r0 + ch < hi ? r0 + ch : hi);
+  }
+}
+
+// f(r0, r1) for chunks [r0, r1) of [0, n) until every head is drained (wave-uniform):
+// the wave's own XCD's head first, then, with lanes 0..7 reading all heads in one
+// instruction, the next head (after its own) that still has rows — one round trip per
+// steal instead of one per head, which short launches feel
 template <class F>
 __device__ inline void rq_for_each(unsigned* q, int64_t n, int ch, F&& f) {
-  int h = xcc_id();
-  for (int visit = 0; visit < kRqHeads; ++visit, h = (h + 1) & (kRqHeads - 1)) {
-    const int64_t lo = n * h / kRqHeads, hi = n * (h + 1) / kRqHeads;
-    if (lo >= hi) continue;
-    unsigned* head = q + h * kRqStride;
-    unsigned t = rq_take(head);
-    while (true) {
-      const int64_t r0 = lo + (int64_t)__shfl(t, 0) * ch;
-      if (r0 >= hi) break;
-      t = rq_take(head);  // the next ticket is in flight while this chunk runs
-      f(r0, r0 + ch < hi ? r0 + ch : hi);
+  const int home = xcc_id();
+  rq_drain(q, n, ch, home, f);
+  const int lane = threadIdx.x & 63;
+  while (true) {
+    bool open = false;
+    if (lane < kRqHeads) {
+      const int64_t lo = n * lane / kRqHeads, hi = n * (lane + 1) / kRqHeads;
+      const unsigned v =
+          __hip_atomic_load(q + lane * kRqStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      open = lo + (int64_t)v * ch < hi;
     }
+    uint64_t m = __ballot(open) & ((1ull << kRqHeads) - 1);
+    if (m == 0) return;
+    m = ((m >> (home + 1)) | (m << (kRqHeads - 1 - home))) & ((1ull << kRqHeads) - 1);
+    rq_drain(q, n, ch, (home + 1 + __builtin_ctzll(m)) & (kRqHeads - 1), f);
   }
 }
 

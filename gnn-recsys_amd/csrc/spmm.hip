@@ -29,14 +29,26 @@
 namespace gnnrec {
 namespace {
 
-// rows per queue ticket of the row kernel (rowq.hpp): ≈70 µs of one wave's gather at C4
-constexpr int kRowChunk = 2;
+// rows per queue ticket of the row kernel (rowq.hpp): 0 = about kRqTicketEdges edges per
+// ticket from the CSR's mean degree (C4 tiles: 4 rows ≈ 140 µs of one wave; minibatch
+// blocks at 7-10 edges/row: 25-36 rows, so the ticket round trip stays amortised);
+// GNNREC_RQ_CHUNK > 0 fixes it (tuning)
+constexpr int64_t kRqTicketEdges = 256;
+inline int row_chunk() {
+  static const int v = [] {
+    const char* e = getenv("GNNREC_RQ_CHUNK");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 64 ? x : 0;
+  }();
+  return v;
+}
 
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
-    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq) {
+    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq,
+    int rq_ch) {
   const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
@@ -60,7 +72,12 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     }
   };
   if (rq != nullptr) {  // queued rows (one column slice: the launcher checks gridDim.y == 1)
-    rq_for_each(rq, n_dst, kRowChunk, [&](int64_t r0, int64_t r1) {
+    if (rq_ch <= 0) {
+      const int64_t avg = (indptr[n_dst] - indptr[0]) / n_dst;
+      const int64_t c = kRqTicketEdges / (avg > 0 ? avg : 1);
+      rq_ch = (int)(c < 1 ? 1 : c > 64 ? 64 : c);
+    }
+    rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
       for (int64_t row = r0; row < r1; ++row) one_row(row);
     });
     rq_finish(rq);
@@ -175,7 +192,7 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   unsigned* rq = slices == 1 && a.n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot() : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
-                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq);
+                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk());
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                        dim3(grid_waves(a.n_chunks), slices), dim3(256), 0, s, a.indptr, a.indices,

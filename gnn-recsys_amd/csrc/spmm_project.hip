@@ -29,7 +29,16 @@ namespace {
 constexpr int kPD = 128;       // d_neigh = d_self = N
 constexpr int kPWaves = 16;    // waves per block (one persistent block per CU)
 constexpr int kPRows = 2;      // rows per wave per iteration (halves the LDS weight reads)
-constexpr int kPChunk = 4;     // rows per queue ticket (rowq.hpp): two iterations, ≈60 µs at C4
+// rows per queue ticket (rowq.hpp): two iterations, ≈60 µs at C4; GNNREC_RQ_CHUNK_FUSED
+// overrides (tuning; rounded up to a multiple of kPRows)
+inline int fused_chunk() {
+  static const int v = [] {
+    const char* e = getenv("GNNREC_RQ_CHUNK_FUSED");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 4;
+  }();
+  return v;
+}
 
 template <int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
@@ -39,7 +48,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const float* __restrict__ WnT, const float* __restrict__ bias,
     const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
     const float* __restrict__ attn_vec, float* __restrict__ attn_state,
-    float* __restrict__ out, int64_t ldo, unsigned* rq) {
+    float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
   __shared__ float Ws[kPD * kPD];
   __shared__ float Wn[kPD * kPD];
   __shared__ float slots[kPWaves][kPRows][2][kPD];
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   };
 
   if (rq != nullptr) {  // rows from the queue: blocks that start late take fewer
-    rq_for_each(rq, n_dst, kPChunk, [&](int64_t r0, int64_t r1) {
+    rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
       for (int64_t row0 = r0; row0 < r1; row0 += kPRows) step(row0, r1);
     });
     rq_finish(rq);
@@ -242,7 +251,8 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   const int64_t cus = device_cus() - cu_reserve();
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
   // queued rows when every wave has several tickets of work
-  unsigned* rq = n_dst >= blocks * kPWaves * kPChunk * 4 ? rowq_slot() : nullptr;
+  const int rq_ch = fused_chunk();
+  unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot() : nullptr;
   const dim3 grid((unsigned)blocks), block(kPWaves * 64);
   hipStream_t s = as_stream(stream);
   static const int unroll = [] {  // gather wave-instructions in flight per lane (tuning knob)
@@ -252,7 +262,7 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
 #define GNNREC_SPP_ONE(R, W, U)                                                              \
   hipLaunchKernelGGL((spmm_project_kernel<R, W, U>), grid, block, 0, s, indptr, indices, ew, X, \
                      ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum, \
-                     out_div, attn_vec, attn_state, out, ldo, rq)
+                     out_div, attn_vec, attn_state, out, ldo, rq, rq_ch)
 #define GNNREC_SPP(R, W)                                  \
   do {                                                    \
     if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \
