@@ -327,3 +327,29 @@ def test_prefetching_loaders_match_synchronous(workers):
         assert torch.isfinite(loss)
         if step == 3:
             break  # the sampling thread stops instead of blocking on a full queue
+
+
+def test_fanout_sampler_is_uniform():
+    """the HIP fanout sampler picks every in-edge of a row with equal
+    probability — chi-square over in-row positions (2000 users of in-degree 40, fanout 5,
+    four sampler seeds), exactly `fanout` distinct in-edges per seed."""
+    from scipy.stats import chi2
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    n_u, n_i, deg, fan = 2000, 997, 40, 5
+    dst = np.repeat(np.arange(n_u), deg)           # edge e = u * deg + j: j-th in-edge of u
+    src = np.arange(n_u * deg) % n_i
+    g = HeteroGraph({BOUGHT: (torch.from_numpy(src), torch.from_numpy(dst))},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    counts = np.zeros(deg)
+    for seed in range(4):
+        b = MultiLayerNeighborSampler([fan], seed=seed).sample_blocks(
+            g, {"user": torch.arange(n_u, device=DEV)})[0]
+        indptr, _, eids = b._rels[BOUGHT]
+        ip, e = indptr.cpu().numpy(), eids.cpu().numpy()
+        assert (np.diff(ip) == fan).all()
+        for r in range(0, n_u, 97):
+            assert len(set(e[ip[r]:ip[r + 1]].tolist())) == fan
+        counts += np.bincount(e - np.repeat(np.arange(n_u), fan) * deg, minlength=deg)
+    exp = counts.sum() / deg
+    assert chi2.sf(float(((counts - exp) ** 2 / exp).sum()), deg - 1) > 1e-4

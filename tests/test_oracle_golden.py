@@ -101,3 +101,29 @@ def test_lstm_edge_fails_like_the_reference():
     with pytest.raises(AttributeError):
         oracle.conv_layer(g, ("user", "buys", "item"), a["x_neigh"], a["x_self"], {},
                           "lstm_edge", True)
+
+
+def _position_chi2(counts):
+    from scipy.stats import chi2
+    exp = counts.sum() / counts.size
+    stat = float(((counts - exp) ** 2 / exp).sum())
+    return chi2.sf(stat, counts.size - 1)
+
+
+def test_fanout_sampler_restatement_is_uniform():
+    """the fanout sampler (Floyd's algorithm over a counter hash; the HIP
+    sampler is bit-exact to this restatement, tests/test_gpu_sampling.py) picks every
+    in-edge of a row with equal probability: chi-square over in-row positions, 2000 rows
+    of degree 40, fanout 5, four sampler keys; and exactly `fanout` distinct edges per row."""
+    n_rows, deg, fan = 2000, 40, 5
+    indptr = np.arange(n_rows + 1, dtype=np.int64) * deg
+    indices = np.arange(n_rows * deg, dtype=np.int64) % 997
+    eids = np.arange(n_rows * deg, dtype=np.int64)
+    counts = np.zeros(deg)
+    for key in range(4):
+        ip, _, eid = oracle.sample_neighbors(indptr, indices, eids, np.arange(n_rows), fan, key=key)
+        assert (np.diff(ip) == fan).all()
+        rows = np.repeat(np.arange(n_rows), fan)
+        assert all(len(set(eid[ip[r]:ip[r + 1]].tolist())) == fan for r in range(0, n_rows, 97))
+        counts += np.bincount(eid - rows * deg, minlength=deg)
+    assert _position_chi2(counts) > 1e-4
