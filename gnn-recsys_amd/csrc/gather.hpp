@@ -38,16 +38,21 @@ __device__ __forceinline__ float combine(float a, float b) {
 }
 
 // Per-lane partial reduction of edges [beg, end) (lane group grp takes k % NPI == grp).
-template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
+// PRE: the first 64 indices of the range were loaded by the caller (lane k holds
+// indices[beg + k]) — a row kernel prefetches them for row i+1 while row i gathers.
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL, bool PRE = false>
 __device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
                                              const int32_t* __restrict__ indices,
                                              const float* __restrict__ ew,
                                              const float* __restrict__ X, int64_t ldx, int col,
-                                             bool colok, int lane, int grp, Frag<VEC>& acc) {
+                                             bool colok, int lane, int grp, Frag<VEC>& acc,
+                                             int pre_idx = 0) {
   constexpr int NPI = kWave / LPR;
   for (int64_t base = beg; base < end; base += 64) {
     const int cnt = (int)((end - base) < 64 ? (end - base) : 64);
-    const int myidx = lane < cnt ? indices[base + lane] : 0;
+    int myidx;
+    if (PRE && base == beg) myidx = pre_idx;
+    else myidx = lane < cnt ? indices[base + lane] : 0;
     float myw = 0.f;
     if constexpr (WEIGHTED) myw = lane < cnt ? ew[base + lane] : 0.f;
     for (int j = 0; j < cnt; j += NPI * UNROLL) {

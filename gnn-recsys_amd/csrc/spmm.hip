@@ -77,8 +77,37 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
       const int64_t c = kRqTicketEdges / (avg > 0 ? avg : 1);
       rq_ch = (int)(c < 1 ? 1 : c > 64 ? 64 : c);
     }
+    // a ticket's row bounds come from one coalesced indptr load, and the next row's first
+    // 64 indices are requested before the current row gathers: of the indptr -> indices ->
+    // source-row chain only the last link stays exposed at a row boundary
     rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
-      for (int64_t row = r0; row < r1; ++row) one_row(row);
+      const int nr = (int)(r1 - r0);  // <= 64
+      const int64_t ipl = lane < nr ? indptr[r0 + lane] : 0;
+      const int64_t ip_end = indptr[r1];
+      auto bound = [&](int k) { return k < nr ? __shfl(ipl, k) : ip_end; };
+      int64_t beg = bound(0), end = bound(1);
+      int nidx = lane < end - beg ? indices[beg + lane] : 0;
+      for (int k = 0; k < nr; ++k) {
+        const int idx = nidx;
+        const int64_t nbeg = end, nend = k + 1 < nr ? bound(k + 2) : end;
+        if (k + 1 < nr) nidx = lane < nend - nbeg ? indices[nbeg + lane] : 0;
+        if (end - beg <= max_deg) {  // heavy rows: reduced by the chunk kernels
+          Frag<VEC> acc;
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc.v[v] = init;
+          gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(
+              beg, end, indices, ew, X, ldx, col, colok, lane, grp, acc, idx);
+          combine_groups<LPR, VEC, REDUCE>(acc);
+          finalize<VEC, REDUCE>(acc, end - beg, empty_neginf);
+          const int64_t row = r0 + k;
+          if (grp == 0 && colok) {
+            if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(acc, out + row * ldo + col);
+            store_frag<VEC>(out + row * ldo + col, acc);
+          }
+        }
+        beg = nbeg;
+        end = nend;
+      }
     });
     rq_finish(rq);
     return;
@@ -182,7 +211,10 @@ inline unsigned grid_waves(int64_t units) {
 
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
 int launch_all(const SpmmArgs& a, hipStream_t s) {
-  constexpr int UNROLL = (VEC == 4) ? 4 : 2;
+#ifndef GNNREC_SPMM_UNROLL
+#define GNNREC_SPMM_UNROLL 4
+#endif
+  constexpr int UNROLL = (VEC == 4) ? GNNREC_SPMM_UNROLL : 2;
   const int cols_per_slice = LPR * VEC;
   const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
   const int eni = a.flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
