@@ -96,6 +96,53 @@ __global__ __launch_bounds__(256) void add_f32_kernel(const float* __restrict__ 
     out[i] = a[i] + b[i];
 }
 
+// Whole fixed pairwise tree ((p0+p1)+(p2+p3))+... over NP = 2/4/8 tables in one pass:
+// every input read once and one write, instead of NP-1 add launches that re-read and
+// re-write the intermediate sums (the same additions in the same order: bitwise equal)
+struct TreeParts {
+  const float4* p[8];
+};
+template <int NP>
+__global__ __launch_bounds__(256) void tree_sum_f32x4_kernel(TreeParts parts,
+                                                             float4* __restrict__ out,
+                                                             int64_t n4) {
+  constexpr int U = NP >= 8 ? 2 : 4;  // 16 x 16 B in flight per lane
+  const int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
+  float4 x[U][NP];
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n4) {
+#pragma unroll
+      for (int j = 0; j < NP; ++j) x[k][j] = parts.p[j][i];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const int64_t i = base + k * 256;
+    if (i < n4) {
+#pragma unroll
+      for (int w = 1; w < NP; w <<= 1) {
+#pragma unroll
+        for (int j = 0; j < NP; j += 2 * w)
+          x[k][j] = make_float4(x[k][j].x + x[k][j + w].x, x[k][j].y + x[k][j + w].y,
+                                x[k][j].z + x[k][j + w].z, x[k][j].w + x[k][j + w].w);
+      }
+      out[i] = x[k][0];
+    }
+  }
+}
+
+template <int NP>
+void launch_tree(const float* const* parts, int64_t n4, float* out, hipStream_t s) {
+  constexpr int U = NP >= 8 ? 2 : 4;
+  TreeParts tp{};
+  for (int j = 0; j < NP; ++j) tp.p[j] = reinterpret_cast<const float4*>(parts[j]);
+  const int64_t blocks = (n4 + 256 * U - 1) / (256 * U);
+  hipLaunchKernelGGL(tree_sum_f32x4_kernel<NP>, dim3((unsigned)blocks), dim3(256), 0, s, tp,
+                     reinterpret_cast<float4*>(out), n4);
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -120,4 +167,29 @@ extern "C" int gnnrec_add_f32(const float* a, const float* b, float* out, int64_
     hipLaunchKernelGGL(add_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, out, n);
   }
   return check_launch("gnnrec_add_f32");
+}
+
+extern "C" int gnnrec_tree_sum_f32(const float* const* parts, int n_parts, int64_t n, float* out,
+                                   void* stream) {
+  GNNREC_REQUIRE(n >= 0, "gnnrec_tree_sum_f32: negative size");
+  GNNREC_REQUIRE(n_parts == 2 || n_parts == 4 || n_parts == 8,
+                 "gnnrec_tree_sum_f32: n_parts=%d (2, 4 or 8)", n_parts);
+  if (n == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(parts && out, "gnnrec_tree_sum_f32: null pointer");
+  uintptr_t al = reinterpret_cast<uintptr_t>(out);
+  for (int j = 0; j < n_parts; ++j) {
+    GNNREC_REQUIRE(parts[j], "gnnrec_tree_sum_f32: null part %d", j);
+    al |= reinterpret_cast<uintptr_t>(parts[j]);
+  }
+  hipStream_t s = as_stream(stream);
+  GNNREC_REQUIRE((al & 15u) == 0 && n % 4 == 0,
+                 "gnnrec_tree_sum_f32: tables must be 16-B aligned with n %% 4 == 0");
+  const int64_t n4 = n / 4;
+  GNNREC_REQUIRE(n4 / 512 < (int64_t(1) << 31), "gnnrec_tree_sum_f32: n too large");
+  switch (n_parts) {
+    case 2: launch_tree<2>(parts, n4, out, s); break;
+    case 4: launch_tree<4>(parts, n4, out, s); break;
+    default: launch_tree<8>(parts, n4, out, s); break;
+  }
+  return check_launch("gnnrec_tree_sum_f32");
 }

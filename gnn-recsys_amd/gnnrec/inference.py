@@ -609,11 +609,18 @@ class ShardedFullGraphPass:
 
 
 def _tree_sum(parts: List[torch.Tensor], O) -> torch.Tensor:
-    """Pairwise tree ((p0+p1)+(p2+p3))+... over a power-of-two list, in order (in place
-    into the left operand: one add kernel per node)."""
+    """Pairwise tree ((p0+p1)+(p2+p3))+... over a power-of-two list, in order, in place into
+    the left operand: subtrees of up to 8 leaves folded by one tree_sum_ kernel each (every
+    table read once; the same additions as one add kernel per node, bitwise)."""
     parts = [p.contiguous() for p in parts]
+    tree = getattr(O, "tree_sum_", None)
+    aligned = all(p.data_ptr() % 16 == 0 and p.numel() % 4 == 0 for p in parts)
     while len(parts) > 1:
-        parts = [O.add_(parts[i], parts[i + 1]) for i in range(0, len(parts), 2)]
+        g = min(8, len(parts))
+        if tree is not None and aligned:
+            parts = [tree(parts[i:i + g]) for i in range(0, len(parts), g)]
+        else:
+            parts = [O.add_(parts[i], parts[i + 1]) for i in range(0, len(parts), 2)]
     return parts[0]
 
 

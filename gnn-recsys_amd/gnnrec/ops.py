@@ -278,6 +278,25 @@ def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return a
 
 
+def tree_sum_(parts) -> torch.Tensor:
+    """parts[0] = ((p0+p1)+(p2+p3))+... over 2, 4 or 8 same-shape contiguous fp32 tables in
+    one kernel pass (gnnrec_tree_sum_f32): the same additions, in the same order, as
+    pairwise add_ launches level by level; returns parts[0]."""
+    lib = _lib.load()
+    n = len(parts)
+    if n not in (2, 4, 8):
+        raise ValueError("tree_sum_: 2, 4 or 8 tables")
+    a = parts[0]
+    for p in parts:
+        _dev(p, "part", torch.float32)
+        if p.shape != a.shape or not p.is_contiguous():
+            raise ValueError("tree_sum_: operands must be contiguous and of one shape")
+    arr = (ctypes.c_void_p * n)(*[ptr(p) for p in parts])
+    check(lib.gnnrec_tree_sum_f32(arr, n, a.numel(), ptr(a), stream_ptr(a.device)),
+          "gnnrec_tree_sum_f32")
+    return a
+
+
 def l2_normalize_rows(y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = y / ‖y‖ per row, rows with ‖y‖ == 0 unchanged (src/model.py:230-235), one
     wave per row (gnnrec_row_epilogue_f32)."""

@@ -319,6 +319,13 @@ int gnnrec_csr_from_keys(const int32_t* keys, int64_t n_edges, int64_t n_rows, v
  * deterministic pass's fixed pairwise tree over source-range partial tables. */
 int gnnrec_add_f32(const float* a, const float* b, float* out, int64_t n, void* stream);
 
+/* out[i] = ((p0[i]+p1[i])+(p2[i]+p3[i]))+... over n_parts = 2, 4 or 8 tables of n floats in
+ * one pass (out may alias any part; 16-B aligned, n % 4 == 0): a whole level-by-level fold of
+ * the fixed pairwise tree, bitwise equal to n_parts-1 gnnrec_add_f32 launches.  `parts` is a
+ * host array of device pointers. */
+int gnnrec_tree_sum_f32(const float* const* parts, int n_parts, int64_t n, float* out,
+                        void* stream);
+
 /* Row epilogue for projections wider than one GEMM block (N > 256): out (accum)=
  * l2norm?(z) row by row, accum / out_div / attention as gnnrec_gemm_f32.  z holds the
  * GEMM result with bias and ReLU already applied (the reference's hidden 384 / 512 with

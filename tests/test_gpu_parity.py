@@ -1116,3 +1116,28 @@ def test_spmm_accumulate_tiles_equal_whole_relation(reduce, split):
         np.testing.assert_allclose(out.cpu().numpy(), whole.cpu().numpy(), rtol=1e-5, atol=1e-4)
     with pytest.raises(ValueError):
         ops.spmm(_t(indptr), _t(idx), X, "max", out=out, accumulate=True)
+
+
+@pytest.mark.parametrize("n_parts", [2, 4, 8])
+@pytest.mark.parametrize("n", [4, 1000, 262_148])
+def test_tree_sum_equals_pairwise_adds(n_parts, n):
+    """gnnrec_tree_sum_f32 folds the deterministic pass's fixed pairwise tree in one pass:
+    bitwise equal to the level-by-level add_ launches (and to numpy's same-order fp32 sums),
+    in place into the first table."""
+    from gnnrec import ops
+    rng = np.random.default_rng(n_parts * 7 + n)
+    host = [(rng.standard_normal(n) * 10.0 ** rng.integers(-3, 4)).astype(np.float32)
+            for _ in range(n_parts)]
+    ref = [h.copy() for h in host]
+    while len(ref) > 1:
+        ref = [ref[i] + ref[i + 1] for i in range(0, len(ref), 2)]
+    pair = [_t(h) for h in host]
+    while len(pair) > 1:
+        pair = [ops.add_(pair[i], pair[i + 1]) for i in range(0, len(pair), 2)]
+    parts = [_t(h) for h in host]
+    got = ops.tree_sum_(parts)
+    assert got.data_ptr() == parts[0].data_ptr()
+    assert torch.equal(got, pair[0])
+    np.testing.assert_array_equal(got.cpu().numpy(), ref[0])
+    with pytest.raises(ValueError):
+        ops.tree_sum_(parts[:3] if n_parts >= 4 else parts[:1])
