@@ -412,6 +412,7 @@ class ShardedFullGraphPass:
         for T, ces in active.items():
             if T == sh.ptype:
                 continue
+            tree_rels = []
             for ce in ces:
                 mod = hconv.mods[ce[1]]
                 preagg, weighted, reduce = mod._plan_rel(ce)
@@ -419,7 +420,7 @@ class ShardedFullGraphPass:
                 msg = self._message(mod, ce, h, preagg)
                 can_fuse = getattr(O, 'can_spmm_project', None)
                 if self.deterministic and reduce in ('sum', 'mean'):
-                    partials[ce] = self._tree_partial(rs, msg, weighted, reduce)
+                    tree_rels.append((ce, rs, msg, weighted, reduce))
                     continue
                 if rs.segs is not None and reduce != 'lstm':
                     # source-range tiles: each tile gathers from a slice of the source table
@@ -458,27 +459,42 @@ class ShardedFullGraphPass:
                 own, work = self.ex.reduce_scatter_rows(part, 'max' if reduce == 'max' else 'sum',
                                                         async_op=self.overlap)
                 partials[ce] = (own, work, reduce)
+            partials.update(self._tree_partials(tree_rels))
         return partials
 
-    def _tree_partial(self, rs, msg, weighted, reduce):
-        """Σ over this relation's segments in one fixed pairwise tree: the rank folds its
+    def _tree_partials(self, rels):
+        """Σ over each relation's segments in one fixed pairwise tree: the rank folds its
         own contiguous block of segments (a subtree), the all-to-all hands every owner the
         P subtree roots of its rows in rank order, and the owner folds those.  The tree is
-        the same at every world size dividing the segment count."""
+        the same at every world size dividing the segment count.
+
+        Relations into one destination type (C5: clicks and buys into items) run their
+        tiles interleaved, tile j of every relation before tile j+1, so a relation's tile
+        finds the source slice the previous relation's tile j just gathered from still
+        partly in the Infinity Cache; each relation's result is unchanged (same kernels,
+        same inputs)."""
         # the tree's leaf pairs are formed in the kernel (tile 2i+1 accumulated onto tile 2i:
         # the same single add), the upper levels by _tree_sum
-        parts = []
-        for j, (ip, ix, w) in enumerate(rs.segs):
-            ew = w if weighted else None
-            with self._time('spmm_tile'):
-                if j % 2 == 0:
-                    parts.append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew))
-                else:
-                    self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[-1],
-                                  accumulate=True)
-        blocks, work = self.ex.all_to_all_rows(_tree_sum(parts, self.ops),
-                                               async_op=self.overlap)
-        return blocks, work, reduce, 'tree'  # the owner's fold waits for the exchange
+        parts = {ce: [] for ce, *_ in rels}
+        n_seg = max((len(rs.segs) for _, rs, *_ in rels), default=0)
+        for j in range(n_seg):
+            for ce, rs, msg, weighted, _ in rels:
+                if j >= len(rs.segs):
+                    continue
+                ip, ix, w = rs.segs[j]
+                ew = w if weighted else None
+                with self._time('spmm_tile'):
+                    if j % 2 == 0:
+                        parts[ce].append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew))
+                    else:
+                        self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[ce][-1],
+                                      accumulate=True)
+        out = {}
+        for ce, rs, msg, weighted, reduce in rels:
+            blocks, work = self.ex.all_to_all_rows(_tree_sum(parts[ce], self.ops),
+                                                   async_op=self.overlap)
+            out[ce] = (blocks, work, reduce, 'tree')  # the owner's fold waits for the exchange
+        return out
 
     def _local(self, hconv, h, active, out):
         """item->user style relations: dst rows owned here; GEMMs on the side stream."""
