@@ -328,8 +328,7 @@ class ShardedFullGraphPass:
                 if mod is None or nt not in h:
                     continue
                 W, b, x = mod.proj_feats.weight, mod.proj_feats.bias, h[nt]
-                if nt == sh.ptype and self.fold_embedding and m.layers and \
-                        self._foldable(m.layers[0], h, nt, W):
+                if self.fold_embedding and m.layers and self._foldable(m.layers[0], h, nt, W):
                     self._fold[nt] = (W.detach(), b.detach())
                     self._folded_types.add(nt)
                     continue  # h[nt] stays the raw features
@@ -348,8 +347,9 @@ class ShardedFullGraphPass:
         return h
 
     def _foldable(self, hconv, h, nt, W_emb) -> bool:
-        """The partitioned type's NodeEmbedding folds into every first-layer relation that
-        touches nt: as the destination (W_self·W_e, bias W_self·b_e — fused kernel or GEMM
+        """A node type's NodeEmbedding (the partitioned users, and the replicated items,
+        whose 1M-row embedding GEMM every rank would otherwise repeat) folds into every
+        first-layer relation that touches nt: as the destination (W_self·W_e, bias W_self·b_e — fused kernel or GEMM
         alike) and as the source when the reducer is linear in the source rows and adds one
         b_e per non-empty row: mean, no fc_preagg (non-linear), no edge weights (they would
         scale b_e).  Needs the HIP backend (bias_nonempty) and W_e square at the fused width.
@@ -547,15 +547,26 @@ class ShardedFullGraphPass:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
                 akw = self._attn(hconv, T, sh.n_own, o.device)
 
-            Ws, Wn, bias, _ = self._folded(mod, ce)  # the source side is never folded here
+            Ws, Wn, bias, bias_ne = self._folded(mod, ce)
+            # a folded source-side embedding adds W_n b_e on rows that have neighbours
+            fkw = {} if bias_ne is None else {'bias_nonempty': bias_ne,
+                                              'a2_deg': self._local_deg(rs)}
 
-            def proj(Ws=Ws, Wn=Wn, bias=bias, mod=mod, a=a, acc=acc, div=div, o=o, akw=akw):
+            def proj(Ws=Ws, Wn=Wn, bias=bias, mod=mod, a=a, acc=acc, div=div, o=o, akw=akw,
+                     fkw=fkw):
                 O.gemm(self_rows, Ws, a, Wn, bias, relu=True, l2norm=bool(mod.norm), accum=acc,
-                       out_div=div, out=o, **akw)
+                       out_div=div, out=o, **akw, **fkw)
             ev = self._on_side(proj, self_rows, a, o, *akw.values())
         out[T] = o
         if ev is not None:
             self._ready[id(o)] = ev
+
+    @staticmethod
+    def _local_deg(rs):
+        """int32 in-degrees of a locally owned relation's rows (cached on the relation)."""
+        if getattr(rs, '_deg_i32', None) is None:
+            rs._deg_i32 = (rs.indptr[1:] - rs.indptr[:-1]).to(torch.int32)
+        return rs._deg_i32
 
     def _owned(self, hconv, h, active, partials, out):
         """owners project their replicated rows, then all-gather the table."""
