@@ -125,6 +125,44 @@ def main():
     del g, loader, fl, it, blocks
     torch.cuda.empty_cache()
 
+    # ---- C2: one training step (2 conv layers 'mean', d=64, fanout [10,10], cosine head) --
+    def train_steps(g, model, K, label):
+        opt = torch.optim.Adam(model.parameters(), lr=0.005)
+        el = EdgeDataLoader(g, {BUYS: torch.arange(50_000_000)},
+                            MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
+                            reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
+                            negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
+                            shuffle=True)
+        for nw in (0, 2):  # num_workers=2: the next batches are sampled on a second stream
+            el.num_workers = nw
+            it = iter(el)
+
+            def step():
+                _, pos_g, neg_g, blocks = next(it)
+                _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+                loss = gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                return loss.item()
+
+            for _ in range(2):
+                step()
+            ts, _ = sync_time(lambda: [step() for _ in range(10)])
+            res[f"{label}, num_workers={nw}"] = {"ms_per_step": ts / 10 * 1e3,
+                                                 "pos_edges_per_s": 1024 * 10 / ts}
+            del it
+
+    g = c2_graph(64, dev)
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
+                          "mean", "cos", "sum", True).to(dev)
+    for K in (10, 2500):
+        train_steps(g, model, K, f"C2 training step (fanout [10,10], 1024 pos x {K} neg, "
+                                 f"mean d=64)")
+    del g, model
+    torch.cuda.empty_cache()
+
     # ---- C3: heads kernels + one training step --------------------------------------------
     g = c2_graph(128, dev)
     E_pos, K = 1024, 2500
@@ -150,31 +188,7 @@ def main():
 
     model = gnn.ConvModel(g, 3, {"user": 128, "item": 128, "hidden": 128, "out": 128}, True,
                           0.0, "mean_nn", "cos", "sum", True).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=0.005)
-    el = EdgeDataLoader(g, {BUYS: torch.arange(50_000_000)}, MultiLayerNeighborSampler([10, 10]),
-                        exclude="reverse_types", reverse_etypes={"buys": "bought-by",
-                                                                  "bought-by": "buys"},
-                        negative_sampler=negative_sampler.Uniform(K), batch_size=E_pos,
-                        shuffle=True)
-    for nw in (0, 2):  # num_workers=2: the next batches are sampled on a second stream
-        el.num_workers = nw
-        it = iter(el)
-
-        def step():
-            _, pos_g, neg_g, blocks = next(it)
-            _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
-            loss = gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            return loss.item()
-
-        for _ in range(2):
-            step()
-        ts, _ = sync_time(lambda: [step() for _ in range(10)])
-        res[f"C3 training step (fanout [10,10], 1024 pos x 2500 neg, mean_nn d=128), "
-            f"num_workers={nw}"] = {"ms_per_step": ts / 10 * 1e3}
-        del it
+    train_steps(g, model, K, "C3 training step (fanout [10,10], 1024 pos x 2500 neg, mean_nn d=128)")
     print(json.dumps(res, indent=1), flush=True)
 
 
