@@ -75,21 +75,36 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   // rows [row0, row0 + kPRows) of this wave, those at or past `lim` skipped
   auto step = [&](int64_t row0, int64_t lim) {
     bool nonempty[kPRows];
+    // both rows' bounds (one load), first 64 indices and self rows are requested before
+    // either row gathers: the second row's indptr -> indices chain hides under the first
+    // row's gather (it is the fixed per-row cost that low-degree relations feel)
+    const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);  // valid rows, >= 1
+    const int64_t ipl = lane <= nv ? indptr[row0 + lane] : 0;
+    int64_t rb[kPRows + 1];
+#pragma unroll
+    for (int r = 0; r <= kPRows; ++r) rb[r] = __shfl(ipl, r <= nv ? r : nv);
+    int pidx[kPRows];
+    float4 hsr[kPRows];
 #pragma unroll
     for (int r = 0; r < kPRows; ++r) {
-      const int64_t row = row0 + r;
-      const bool valid = row < lim;  // uniform per wave
-      float4 hs = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid && grp == 1) hs = *reinterpret_cast<const float4*>(H + row * ldh + col);
+      const bool valid = r < nv;  // uniform per wave
+      pidx[r] = valid && lane < rb[r + 1] - rb[r] ? indices[rb[r] + lane] : 0;
+      hsr[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (valid && grp == 1) hsr[r] = *reinterpret_cast<const float4*>(H + (row0 + r) * ldh + col);
+    }
+#pragma unroll
+    for (int r = 0; r < kPRows; ++r) {
+      const bool valid = r < nv;  // uniform per wave
+      const float4 hs = hsr[r];
       Frag<VEC> acc;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc.v[v] = init;
       int64_t deg = 0;
       if (valid) {
-        const int64_t beg = indptr[row], end = indptr[row + 1];
+        const int64_t beg = rb[r], end = rb[r + 1];
         deg = end - beg;
-        gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL>(beg, end, indices, ew, X, ldx, col, true,
-                                                         lane, grp, acc);
+        gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(beg, end, indices, ew, X, ldx,
+                                                               col, true, lane, grp, acc, pidx[r]);
       }
       combine_groups<LPR, VEC, REDUCE>(acc);
       finalize<VEC, REDUCE>(acc, deg, 0);
