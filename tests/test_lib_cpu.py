@@ -49,8 +49,16 @@ def test_argument_validation_without_a_gpu():
     rc = lib.gnnrec_gemm_f32(None, 4, 0, None, None, 1, 0, None, None, 0, None, None, 10, 8, 0,
                              _lib.ACC_ATTN, 0.0, None, None, ctypes.c_void_p(16), 8, None)
     assert rc != 0 and b"attention" in lib.gnnrec_last_error()
+    # the deterministic tree's fold: 2, 4 or 8 tables, 16-B aligned
+    parts = (ctypes.c_void_p * 3)(16, 32, 48)
+    rc = lib.gnnrec_tree_sum_f32(parts, 3, 8, ctypes.c_void_p(16), None)
+    assert rc != 0 and b"n_parts=3" in lib.gnnrec_last_error()
+    parts = (ctypes.c_void_p * 2)(16, 36)
+    rc = lib.gnnrec_tree_sum_f32(parts, 2, 8, ctypes.c_void_p(16), None)
+    assert rc != 0 and b"aligned" in lib.gnnrec_last_error()
     # empty problems are no-ops that succeed without touching memory
     assert lib.gnnrec_spmm_csr_f32(None, None, None, None, 4, 0, 4, 1, 0, None, 4, None) == 0
+    assert lib.gnnrec_tree_sum_f32(parts, 2, 0, None, None) == 0
 
 
 def test_ops_refuse_cpu_tensors():
