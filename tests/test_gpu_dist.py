@@ -155,3 +155,81 @@ def test_source_tiles_match_single_process(agg, hetero, d):
     for _, users, items in res:
         np.testing.assert_allclose(users, ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(items, ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+def _digest(t):
+    """Bit-pattern checksum of a large table, on the device: Σ v_i·(2i+1) and Σ v_i·(2i+1)²
+    (mod 2^64) over the int32 views v_i — any single changed bit changes both sums."""
+    v = t.contiguous().view(torch.int32).reshape(-1).to(torch.int64)
+    w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) * 2 + 1
+    return int((v * w).sum()), int((v * (w * w)).sum()), v.numel()
+
+
+def _c4_pass(rank, world, users, items, edges):
+    """The bench's default pass (deterministic, 8 source tiles, partitioned output) on this
+    rank's shard: (own user range, user digest, own item block range, item digest)."""
+    from gnnrec import nn as gnn
+    from gnnrec.dist import Exchange
+    from gnnrec.inference import ShardedFullGraphPass
+    from gnnrec.synth import GraphMeta, bipartite_shard, node_features
+    dev, d = torch.device("cuda", 0), 128
+    sh = bipartite_shard(users, items, edges, rank, world, dev, segments=8)
+    feats = {"user": node_features(users, d, 0, dev, slice(sh.p_lo, sh.p_hi)),
+             "item": torch.zeros((sh.padded_rows("item"), d), device=dev)}
+    feats["item"][:items] = node_features(items, d, 1, dev)
+    torch.manual_seed(0)
+    model = gnn.ConvModel(GraphMeta(sh.canonical_etypes, ["item", "user"]), 3,
+                          {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
+                          "cos", "sum", True).to(dev).eval()
+    with torch.no_grad():
+        out = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True).run(
+            feats, replicate_output=False)
+    S = sh.shard_rows["item"]
+    lo, hi = rank * S, min((rank + 1) * S, items)
+    return (sh.p_lo, sh.p_hi, _digest(out["user"]), lo, hi, _digest(out["item"][: hi - lo]),
+            out)
+
+
+def _c4_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank,) + _c4_pass(rank, world, *C4)[:6])
+    finally:
+        dist.destroy_process_group()
+
+
+C4 = (10_000_000, 1_000_000, 500_000_000)
+
+
+def test_c4_full_size_pass_bitwise_at_two_ranks():
+    """SURVEY §8e at BASELINE.json's full C4 size (10M users x 1M items x 500M edges per
+    direction, d=128, the bench's default deterministic pass): at P = 2 (gloo
+    transport, both ranks on one GPU; more ranks sharing one GPU, each regenerating the
+    500M-edge stream and exchanging 512 MB tables through host memory, exceed a test's
+    time budget — the small-graph tests above cover P = 4 bitwise, and 8 on CPU gloo) every rank produces exactly the bits of its user range
+    and item block that the single-process pass produces (device checksum of every owned
+    table)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    res = []
+    for world in (2,):
+        q, port = ctx.Queue(), _port()
+        procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
+        try:
+            for p in procs:
+                p.start()
+            res += [(world,) + q.get(timeout=80) for _ in range(world)]
+            for p in procs:
+                p.join(timeout=30)
+                assert p.exitcode == 0
+        finally:
+            for p in procs:  # the workers this test started, if a failure left them running
+                if p.is_alive():
+                    p.kill()
+    out = _c4_pass(0, 1, *C4)[6]
+    for world, rank, ulo, uhi, udig, ilo, ihi, idig in res:
+        assert _digest(out["user"][ulo:uhi]) == udig, f"P={world} rank {rank}: user rows differ"
+        assert _digest(out["item"][ilo:ihi]) == idig, f"P={world} rank {rank}: item rows differ"
