@@ -30,10 +30,11 @@ namespace gnnrec {
 namespace {
 
 // rows per queue ticket of the row kernel (rowq.hpp): 0 = about kRqTicketEdges edges per
-// ticket from the CSR's mean degree (C4 tiles: 4 rows ≈ 140 µs of one wave; minibatch
-// blocks at 7-10 edges/row: 25-36 rows, so the ticket round trip stays amortised);
+// ticket from the CSR's mean degree (C4 tiles: 8 rows ≈ 280 µs of one wave, 0.5 % faster
+// than 4; minibatch blocks at 7-10 edges/row: 51-64 rows, so the ticket round trip stays
+// amortised);
 // GNNREC_RQ_CHUNK > 0 fixes it (tuning)
-constexpr int64_t kRqTicketEdges = 256;
+constexpr int64_t kRqTicketEdges = 512;
 inline int row_chunk() {
   static const int v = [] {
     const char* e = getenv("GNNREC_RQ_CHUNK");

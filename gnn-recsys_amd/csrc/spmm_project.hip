@@ -29,13 +29,13 @@ namespace {
 constexpr int kPD = 128;       // d_neigh = d_self = N
 constexpr int kPWaves = 16;    // waves per block (one persistent block per CU)
 constexpr int kPRows = 2;      // rows per wave per iteration (halves the LDS weight reads)
-// rows per queue ticket (rowq.hpp): two iterations, ≈60 µs at C4; GNNREC_RQ_CHUNK_FUSED
+// rows per queue ticket (rowq.hpp): four iterations, ≈120 µs at C4; GNNREC_RQ_CHUNK_FUSED
 // overrides (tuning; rounded up to a multiple of kPRows)
 inline int fused_chunk() {
   static const int v = [] {
     const char* e = getenv("GNNREC_RQ_CHUNK_FUSED");
     const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 4;
+    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 8;
   }();
   return v;
 }
