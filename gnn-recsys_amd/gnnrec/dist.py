@@ -52,6 +52,17 @@ class Exchange:
         self.ws = world()
         self.rk = rank()
         self.backend = dist.get_backend(group) if is_initialized() else None
+        # a group created without an explicit backend reports e.g. 'cpu:gloo,cuda:nccl'
+        self._rccl = self.backend is not None and "nccl" in str(self.backend)
+        self.path = None  # 'rccl' | 'emulated' once the first collective has run
+
+    def _fast(self, t: torch.Tensor) -> bool:
+        """RCCL's reduce-scatter / all-gather-into / all-to-all for device tensors on an
+        nccl (RCCL) group; the gloo emulation otherwise (CPU tests, gloo rehearsals)."""
+        fast = self._rccl and t.is_cuda
+        if self.path is None:
+            self.path = "rccl" if fast else "emulated"
+        return fast
 
     def reduce_scatter_rows(self, full: torch.Tensor, op: str, async_op: bool = False):
         """full [P·S, d] partial on every rank -> (own [S, d], work|None)."""
@@ -59,7 +70,7 @@ class Exchange:
             return full, None
         S = full.shape[0] // self.ws
         rop = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
-        if self.backend == "nccl":
+        if self._fast(full):
             out = torch.empty((S,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
             work = dist.reduce_scatter_tensor(out, full, op=rop, group=self.group,
                                               async_op=async_op)
@@ -73,7 +84,7 @@ class Exchange:
             if out.data_ptr() != own.data_ptr():
                 out.copy_(own)
             return out, None
-        if self.backend == "nccl":
+        if self._fast(own):
             work = dist.all_gather_into_tensor(out, own.contiguous(), group=self.group,
                                                async_op=async_op)
             return out, work
@@ -92,7 +103,7 @@ class Exchange:
         if self.ws == 1:
             return full.view(shape), None
         out = torch.empty_like(full)
-        if self.backend == "nccl":
+        if self._fast(full):
             work = dist.all_to_all_single(out, full.contiguous(), group=self.group,
                                           async_op=async_op)
             return out.view(shape), work

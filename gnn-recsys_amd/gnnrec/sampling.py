@@ -228,6 +228,11 @@ class _Prefetch:
     def __init__(self, make_iter, depth: int, device):
         self.device = device
         self.stream = torch.cuda.Stream(device=device)
+        # the producer starts after everything the consumer has queued, which includes the
+        # tail of any earlier loader's producer (its __iter__ ends with the consumer stream
+        # waiting on it): a sampler shared by several loaders (reference sampling.py:153-241
+        # passes one to all five) never has two producers on its relabel scratch and masks
+        self.stream.wait_stream(torch.cuda.current_stream(device))
         self.q = queue.Queue(maxsize=max(1, depth))
         self.stop = threading.Event()
         self.thread = threading.Thread(target=self._run, args=(make_iter,), daemon=True)
@@ -270,7 +275,11 @@ class _Prefetch:
                         t.record_stream(cur)
                 yield item
         finally:
+            # an early exit (break, exception) must not leave the producer running: stop it,
+            # wait for its host side, and order its queued kernels before the consumer's
             self.stop.set()
+            self.thread.join()
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
 
 def _maybe_prefetch(loader, make_iter):
@@ -353,8 +362,12 @@ class EdgeDataLoader:
         self.exclude = exclude
         if exclude not in (None, 'reverse_types', 'self'):
             raise NotImplementedError(f"exclude={exclude!r}")
+        # the reference passes the same four-type map for every graph (src/sampling.py:180-181);
+        # pairs naming a type this graph lacks (a clicks-only graph) cannot occur in a batch
+        names = {ce[1] for ce in self.g.canonical_etypes} | set(self.g.canonical_etypes)
         self.reverse_etypes = {self.g.to_canonical_etype(k): self.g.to_canonical_etype(v)
-                               for k, v in (reverse_etypes or {}).items()}
+                               for k, v in (reverse_etypes or {}).items()
+                               if k in names and v in names}
         self.negative_sampler = negative_sampler
         dev = g.device
         if not isinstance(eids, dict):

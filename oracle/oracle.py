@@ -16,6 +16,8 @@ Layers (each function cites the reference code it restates):
       model_full_graph ConvModel.get_repr on one batch holding every node,
                        preceded by NodeEmbedding (src/model.py:371-421,
                        src/train/run.py:340-348)
+      model_blocks     the same over sampled blocks (BlockGraph), dst-prefix slicing
+                       as DGL's HeteroGraphConv (src/model.py:415-421,459-465)
       cosine_prediction / predicting_module / max_margin_loss
                        (src/model.py:317-327, 290-305, 256-271, 473-533)
       to_block         DGL to_block relabel, ascending new-src order
@@ -206,18 +208,22 @@ def conv_layer(graph: Graph, ce, h_neigh, h_self, w: dict, aggregator_type: str,
 
 
 def hetero_conv(graph: Graph, h: Dict[str, np.ndarray], layer_w: Dict[str, dict],
-                aggregator_type: str, norm: bool, aggregator_hetero: str):
+                aggregator_type: str, norm: bool, aggregator_hetero: str,
+                h_dst: Optional[Dict[str, np.ndarray]] = None):
     """DGL 0.5.2 HeteroGraphConv (restated) around ConvLayer (src/model.py:384-406).
 
     Relations with no edges, or whose src/dst type has no input, are skipped;
-    outputs of the active relations are stacked per dst type and reduced."""
+    outputs of the active relations are stacked per dst type and reduced.
+    h_dst: the destination inputs when they are not h itself (a block: DGL slices the
+    dst prefix of every src table, h[:number_of_dst_nodes])."""
+    hd = h if h_dst is None else h_dst
     outs: Dict[str, list] = {}
     for ce in graph.canonical_etypes:
         s, rel, d = ce
-        if graph.num_edges(ce) == 0 or s not in h or d not in h:
+        if graph.num_edges(ce) == 0 or s not in h or d not in hd:
             continue
         outs.setdefault(d, []).append(
-            conv_layer(graph, ce, h[s], h[d], layer_w[rel], aggregator_type, norm))
+            conv_layer(graph, ce, h[s], hd[d], layer_w[rel], aggregator_type, norm))
     res = {}
     for nt, lst in outs.items():
         st = np.stack(lst, 0)
@@ -274,6 +280,53 @@ def model_full_graph(graph: Graph, feats: Dict[str, np.ndarray], sd: Dict[str, n
                 h[nt] = linear(h[nt], W, b)
     for lw in layers:
         h = hetero_conv(graph, h, lw, aggregator_type, norm, aggregator_hetero)
+    return h
+
+
+class BlockGraph:
+    """A sampled block (DGL to_block output) as conv_layer reads it: per relation the
+    dst-major CSR over LOCAL ids with the GLOBAL eid of every edge, and per node type the
+    dst-prefix length.  `occurrence` holds the full graph's per-eid edge data (the
+    `*_edge` aggregators read it through the block's eids, src/model.py:173,186,199)."""
+
+    def __init__(self, rels: Dict[Tuple[str, str, str], tuple], num_dst: Dict[str, int],
+                 occurrence: Optional[dict] = None):
+        self.rels = {ce: (np.asarray(ip, np.int64), np.asarray(ix, np.int32),
+                          np.asarray(e, np.int64)) for ce, (ip, ix, e) in rels.items()}
+        self.canonical_etypes = list(self.rels)
+        self.num_dst = dict(num_dst)
+        self.occurrence = dict(occurrence or {})
+
+    def csr(self, ce):
+        return self.rels[ce]
+
+    def num_edges(self, ce):
+        return self.rels[ce][1].size
+
+
+def embed_inputs(feats: Dict[str, np.ndarray], sd: Dict[str, np.ndarray]):
+    """NodeEmbedding per node type (src/model.py:19-24, applied at :459-463)."""
+    embed = split_state_dict(sd)[0]
+    h = {nt: np.asarray(v, np.float32) for nt, v in feats.items()}
+    for nt in ("user", "item", "sport"):
+        if nt in h and nt in embed:
+            W, b = embed[nt]
+            h[nt] = linear(h[nt], W, b)
+    return h
+
+
+def model_blocks(blocks, feats: Dict[str, np.ndarray], sd: Dict[str, np.ndarray],
+                 aggregator_type: str, aggregator_hetero: str, norm: bool,
+                 embedding_layer: bool):
+    """ConvModel.forward's representation half over sampled blocks (src/model.py:459-465:
+    NodeEmbedding, then get_repr :415-421 — layer i on blocks[i]); each block's dst inputs
+    are the dst prefix of its src tables, as DGL's HeteroGraphConv slices them."""
+    _, layers, _ = split_state_dict(sd)
+    h = embed_inputs(feats, sd) if embedding_layer else \
+        {nt: np.asarray(v, np.float32) for nt, v in feats.items()}
+    for block, lw in zip(blocks, layers):
+        h_dst = {nt: h[nt][: block.num_dst[nt]] for nt in h if nt in block.num_dst}
+        h = hetero_conv(block, h, lw, aggregator_type, norm, aggregator_hetero, h_dst)
     return h
 
 

@@ -329,6 +329,42 @@ def test_prefetching_loaders_match_synchronous(workers):
             break  # the sampling thread stops instead of blocking on a full queue
 
 
+def test_shared_sampler_across_loaders_after_early_exit():
+    """The reference hands ONE sampler to all five loaders (src/sampling.py:153-241) and
+    main_train.py runs them with num_workers=4: leaving a prefetching edge loader early and
+    starting a node loader on the same sampler (same relabel scratch and masks) must give
+    the node loader's synchronous blocks bit for bit — the first producer is joined and its
+    stream ordered before the second starts."""
+    from gnnrec.sampling import (EdgeDataLoader, MultiLayerFullNeighborSampler, NodeDataLoader,
+                                 negative_sampler)
+    g, _ = _graph(n_u=300, n_i=200, e_b=6000, e_c=6000)
+
+    def node_items(nw, sampler):
+        torch.manual_seed(8)
+        loader = NodeDataLoader(g, {"user": torch.arange(300), "item": torch.arange(200)},
+                                sampler, batch_size=16, shuffle=True, num_workers=nw)
+        return [[t.clone() for t in _flat(item)] for item in loader]
+
+    ref = node_items(0, MultiLayerFullNeighborSampler(2))
+    shared = MultiLayerFullNeighborSampler(2)
+    for _ in range(3):
+        el = EdgeDataLoader(g, {BUYS: torch.arange(6000), CLICKS: torch.arange(6000)}, shared,
+                            exclude='reverse_types',
+                            reverse_etypes={'buys': 'bought-by', 'bought-by': 'buys',
+                                            'clicks': 'clicked-by', 'clicked-by': 'clicks'},
+                            negative_sampler=negative_sampler.Uniform(4), batch_size=256,
+                            shuffle=True, num_workers=4)
+        for step, _item in enumerate(el):
+            if step == 1:
+                break
+        got = node_items(3, shared)
+        assert len(ref) == len(got)
+        for a, b in zip(ref, got):
+            assert len(a) == len(b)
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
+
+
 def test_fanout_sampler_is_uniform():
     """the HIP fanout sampler picks every in-edge of a row with equal
     probability — chi-square over in-row positions (2000 users of in-degree 40, fanout 5,

@@ -127,3 +127,69 @@ def test_fanout_sampler_restatement_is_uniform():
         assert all(len(set(eid[ip[r]:ip[r + 1]].tolist())) == fan for r in range(0, n_rows, 97))
         counts += np.bincount(eid - rows * deg, minlength=deg)
     assert _position_chi2(counts) > 1e-4
+
+
+def _full_blocks(g, n_blocks):
+    """the reference's golden run passes the full graph as every block (make_golden.py:176)"""
+    rels = {ce: g.csr(ce) for ce in g.canonical_etypes}
+    return [oracle.BlockGraph(rels, g.num_nodes, g.occurrence) for _ in range(n_blocks)]
+
+
+@pytest.mark.parametrize("name", MODEL)
+def test_model_blocks_on_full_blocks_matches_reference(name):
+    """oracle.model_blocks (get_repr over blocks, dst-prefix slicing) with the full graph as
+    every block, as the golden run feeds the reference, reproduces the reference's h."""
+    meta = CASES[name]
+    a = golden_io.load(name)
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = oracle.Graph(num_nodes, edges, occ)
+    feats = {k[5:]: v for k, v in a.items() if k.startswith("feat/")}
+    sd = golden_io.state_dict(a)
+    n_blocks = meta["n_layers"] - 1 if meta["embedding_layer"] else meta["n_layers"]
+    h = oracle.model_blocks(_full_blocks(g, n_blocks), feats, sd, meta["aggregator_type"],
+                            meta["aggregator_hetero"], meta["norm"], meta["embedding_layer"])
+    ref_h = {k[2:]: v for k, v in a.items() if k.startswith("h/")}
+    assert set(h) == set(ref_h)
+    for nt in ref_h:
+        np.testing.assert_allclose(h[nt], ref_h[nt], rtol=RTOL, atol=ATOL)
+
+
+def test_model_blocks_prefix_block_equals_full_graph_rows():
+    """A one-layer block over a seed subset (full in-neighbourhoods, sources = dst prefix +
+    new ids ascending) gives the seeds' rows of the one-layer full-graph model."""
+    name = next(k for k in MODEL if CASES[k]["aggregator_type"] == "mean_nn_edge")
+    meta = CASES[name]
+    a = golden_io.load(name)
+    num_nodes, edges, occ = golden_io.graph_parts(a)
+    g = oracle.Graph(num_nodes, edges, occ)
+    feats = {k[5:]: v for k, v in a.items() if k.startswith("feat/")}
+    sd = {k: v for k, v in golden_io.state_dict(a).items() if not k.startswith("layers.1")
+          and not k.startswith("layers.2")}
+    full = oracle.model_full_graph(g, feats, sd, meta["aggregator_type"],
+                                   meta["aggregator_hetero"], meta["norm"],
+                                   meta["embedding_layer"])
+    rng = np.random.default_rng(0)
+    seeds = {nt: np.sort(rng.choice(n, max(1, n // 3), replace=False))
+             for nt, n in num_nodes.items() if n > 0}
+    rels, picked = {}, {}
+    for ce in g.canonical_etypes:
+        ip, ix, e = g.csr(ce)
+        s = seeds.get(ce[2], np.zeros(0, np.int64))
+        oip, osrc, oe = oracle.sample_neighbors(ip, ix, e, s, -1)
+        rels[ce] = [oip, osrc, oe]
+        picked.setdefault(ce[0], []).append(ce)
+    src_feats = {}
+    for nt in num_nodes:
+        pref = seeds.get(nt, np.zeros(0, np.int64))
+        nodes, locs = oracle.to_block_relabel(pref, [rels[ce][1] for ce in picked.get(nt, [])])
+        for ce, loc in zip(picked.get(nt, []), locs):
+            rels[ce][1] = loc
+        if nodes.size:
+            src_feats[nt] = feats[nt][nodes]
+    blk = oracle.BlockGraph({ce: tuple(r) for ce, r in rels.items()},
+                            {nt: v.size for nt, v in seeds.items()}, occ)
+    h = oracle.model_blocks([blk], src_feats, sd, meta["aggregator_type"],
+                            meta["aggregator_hetero"], meta["norm"], meta["embedding_layer"])
+    for nt, v in seeds.items():
+        if nt in full:
+            np.testing.assert_allclose(h[nt], full[nt][v], rtol=RTOL, atol=ATOL)
