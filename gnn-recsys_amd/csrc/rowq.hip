@@ -20,8 +20,13 @@ std::atomic<int> g_dynamic{[] {
   return e && e[0] == '0' ? 0 : 1;
 }()};
 std::mutex g_mu;
-unsigned* g_ring[kMaxDevices] = {};
+std::atomic<unsigned*> g_ring[kMaxDevices] = {};
 std::atomic<unsigned> g_next[kMaxDevices];
+// completion event of each slot's last launch: a slot whose previous launch (possibly on
+// another stream) has not finished is not handed out again — that launch gets the static
+// schedule instead of sharing heads with a running grid
+hipEvent_t* g_done[kMaxDevices] = {};
+std::atomic<long long> g_queued{0}, g_busy{0};  // launches given a slot / refused one
 int g_cus[kMaxDevices] = {};
 
 int current_device() {
@@ -59,24 +64,44 @@ int device_cus() {
 
 int cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
 
-unsigned* rowq_slot() {
+unsigned* rowq_slot(hipStream_t stream, int* ticket) {
+  *ticket = -1;
+  (void)stream;
   if (!g_dynamic.load(std::memory_order_relaxed)) return nullptr;
   const int dev = current_device();
-  if (g_ring[dev] == nullptr) {
+  unsigned* ring = g_ring[dev].load(std::memory_order_acquire);
+  if (ring == nullptr) {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_ring[dev] == nullptr) {
-      unsigned* p = nullptr;
+    ring = g_ring[dev].load(std::memory_order_relaxed);
+    if (ring == nullptr) {
       const size_t bytes = (size_t)kRqSlots * kRqSlotWords * sizeof(unsigned);
-      if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;  // static schedule instead
-      if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(p);
+      if (hipMalloc(&ring, bytes) != hipSuccess) return nullptr;  // static schedule instead
+      hipEvent_t* ev = new hipEvent_t[kRqSlots]();
+      bool ok = hipMemset(ring, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+      for (unsigned i = 0; ok && i < kRqSlots; ++i)
+        ok = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess;
+      if (!ok) {
+        (void)hipFree(ring);
         return nullptr;
       }
-      g_ring[dev] = p;
+      g_done[dev] = ev;
+      g_ring[dev].store(ring, std::memory_order_release);
     }
   }
   const unsigned i = g_next[dev].fetch_add(1, std::memory_order_relaxed) % kRqSlots;
-  return g_ring[dev] + (size_t)i * kRqSlotWords;
+  // never recorded -> hipSuccess; still running -> hipErrorNotReady: skip the queue
+  if (hipEventQuery(g_done[dev][i]) != hipSuccess) {
+    g_busy.fetch_add(1, std::memory_order_relaxed);
+    return nullptr;
+  }
+  g_queued.fetch_add(1, std::memory_order_relaxed);
+  *ticket = (int)i;
+  return ring + (size_t)i * kRqSlotWords;
+}
+
+void rowq_launched(int ticket, hipStream_t stream) {
+  if (ticket < 0) return;
+  (void)hipEventRecord(g_done[current_device()][ticket], stream);
 }
 
 }  // namespace gnnrec
@@ -95,6 +120,13 @@ extern "C" int gnnrec_get_concurrency(int* reserve_cus, int* dynamic) {
   GNNREC_REQUIRE(reserve_cus && dynamic, "gnnrec_get_concurrency: null pointer");
   *reserve_cus = g_reserve.load();
   *dynamic = g_dynamic.load();
+  return GNNREC_OK;
+}
+
+extern "C" int gnnrec_rowq_stats(int64_t* queued, int64_t* busy) {
+  GNNREC_REQUIRE(queued && busy, "gnnrec_rowq_stats: null pointer");
+  *queued = g_queued.load();
+  *busy = g_busy.load();
   return GNNREC_OK;
 }
 

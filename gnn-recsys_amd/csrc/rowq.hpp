@@ -17,7 +17,8 @@
 //
 // Slots: every launch takes the next slot of a per-device ring (host side, rowq.hip); the
 // last block to finish resets the slot's heads, so the next user finds zeros without a
-// memset.  A slot holds 8 heads + 1 exit counter, each on its own 128-B line.
+// memset.  An event per slot records its launch's completion: a slot whose last launch
+// (on any stream) is still running is not reused — that launch runs the static schedule.  A slot holds 8 heads + 1 exit counter, each on its own 128-B line.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -29,7 +30,10 @@ constexpr int kRqStride = 32;  // uint32 words per head: 128-B lines
 constexpr int kRqSlotWords = (kRqHeads + 1) * kRqStride;
 
 // host (rowq.hip)
-unsigned* rowq_slot();  // next slot of the current device's ring, or nullptr (static mode)
+// next slot of the current device's ring, or nullptr (static mode, or the slot's previous
+// launch still running); after launching with a slot, rowq_launched(ticket, stream)
+unsigned* rowq_slot(hipStream_t stream, int* ticket);
+void rowq_launched(int ticket, hipStream_t stream);
 int device_cus();       // CUs of the current device
 int cu_reserve();       // CUs the row kernels leave free for concurrent kernels
 

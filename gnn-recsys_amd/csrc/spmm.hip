@@ -222,10 +222,13 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   const int64_t max_deg = a.n_heavy > 0 ? a.split : INT64_MAX;
   const unsigned grid = grid_waves(a.n_dst);
   // the queue pays off on long launches only (≥ 8 rows per wave of the grid)
-  unsigned* rq = slices == 1 && a.n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot() : nullptr;
+  int ticket = -1;
+  unsigned* rq =
+      slices == 1 && a.n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot(s, &ticket) : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
                      a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk());
+  rowq_launched(ticket, s);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                        dim3(grid_waves(a.n_chunks), slices), dim3(256), 0, s, a.indptr, a.indices,

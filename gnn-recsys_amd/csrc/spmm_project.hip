@@ -267,9 +267,10 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
   // queued rows when every wave has several tickets of work
   const int rq_ch = fused_chunk();
-  unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot() : nullptr;
-  const dim3 grid((unsigned)blocks), block(kPWaves * 64);
   hipStream_t s = as_stream(stream);
+  int ticket = -1;
+  unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
+  const dim3 grid((unsigned)blocks), block(kPWaves * 64);
   static const int unroll = [] {  // gather wave-instructions in flight per lane (tuning knob)
     const char* e = getenv("GNNREC_SPP_UNROLL");
     return e ? atoi(e) : 4;
@@ -295,5 +296,6 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   }
 #undef GNNREC_SPP
 #undef GNNREC_SPP_ONE
+  rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_project_f32");
 }

@@ -10,7 +10,9 @@
 // One 256-thread block per row: every thread keeps a sorted top-K of its
 // strided columns in registers (insertions are rare after the first few
 // hundred columns), then k rounds of a block-wide argmax over the 256 list
-// heads emit the result.  The exclusion list (already-bought items, a CSR over
+// heads emit the result.  k > 64 (the reference's --k has no bound,
+// main_inference.py:198) runs in passes of up to 64 columns: pass p keeps only
+// candidates ordered after the last result of pass p-1 (the row's "floor").  The exclusion list (already-bought items, a CSR over
 // rows) is staged in LDS, sorted, and binary-searched only for candidates that
 // would enter a thread's list.
 #include "common.hpp"
@@ -30,7 +32,7 @@ template <int KMAX>
 __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
     const float* __restrict__ S, int64_t ld, int64_t n_rows, int64_t n_cols, int k,
     const int64_t* __restrict__ ex_ptr, const int64_t* __restrict__ ex_idx,
-    float* __restrict__ out_v, int64_t* __restrict__ out_i, bool vec) {
+    float* __restrict__ out_v, int64_t* __restrict__ out_i, int64_t ldo, int col0, bool vec) {
   __shared__ int64_t excl[kMaxExcl];
   __shared__ float red_v[kTopkThreads / 64];
   __shared__ int64_t red_i[kTopkThreads / 64];
@@ -39,6 +41,19 @@ __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
   const int64_t row = blockIdx.x;
   if (row >= n_rows) return;
   const float* srow = S + row * ld;
+  out_v += row * ldo + col0;
+  out_i += row * ldo + col0;
+  // floor: the previous pass's last result; candidates must come after it
+  float fl_v = INFINITY;
+  int64_t fl_i = -1;
+  if (col0 > 0) {
+    fl_v = out_v[-1];
+    fl_i = out_i[-1];
+    if (fl_i < 0) {  // the previous pass ran out of columns: so does this one
+      for (int r = tid; r < k; r += kTopkThreads) { out_v[r] = -INFINITY; out_i[r] = -1; }
+      return;
+    }
+  }
 
   // stage and sort (odd-even transposition over LDS) the exclusion list
   int64_t n_ex = 0, ex0 = 0;
@@ -78,6 +93,7 @@ __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
   int64_t thr_i = INT64_MAX;  // register array: a runtime index would spill it to scratch)
   auto offer = [&](float v, int64_t c) {
     if (!better(v, c, thr_v, thr_i)) return;
+    if (col0 > 0 && !better(fl_v, fl_i, v, c)) return;
     if (n_ex && excluded(c)) return;
     // insert (unrolled bubble from the tail)
     float cv = v;
@@ -151,8 +167,8 @@ __global__ __launch_bounds__(kTopkThreads) void topk_rows_kernel(
     if (tid == 0) {
       for (int w = 1; w < kTopkThreads / 64; ++w)
         if (better(red_v[w], red_i[w], bv, bi)) { bv = red_v[w]; bi = red_i[w]; bt = red_t[w]; }
-      out_v[row * k + r] = bv;
-      out_i[row * k + r] = (bi == INT64_MAX) ? -1 : bi;
+      out_v[r] = bv;
+      out_i[r] = (bi == INT64_MAX) ? -1 : bi;
       red_t[0] = bt;
     }
     __syncthreads();
@@ -170,8 +186,8 @@ extern "C" int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_r
                                     int64_t* out_idx, void* stream) {
   using namespace gnnrec;
   GNNREC_REQUIRE(n_rows >= 0 && n_cols >= 0, "gnnrec_topk_rows_f32: negative size");
-  GNNREC_REQUIRE(k >= 1 && k <= 64, "gnnrec_topk_rows_f32: k must be in [1, 64] (got %lld)",
-                 (long long)k);
+  GNNREC_REQUIRE(k >= 1 && k <= (int64_t)1 << 20,
+                 "gnnrec_topk_rows_f32: k must be in [1, 2^20] (got %lld)", (long long)k);
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(scores && out_vals && out_idx && ld >= n_cols,
                  "gnnrec_topk_rows_f32: bad pointers / ld");
@@ -180,14 +196,20 @@ extern "C" int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_r
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)n_rows);
   const bool vec = aligned16(scores) && ld % 4 == 0;
-  if (k <= 16)
-    hipLaunchKernelGGL((topk_rows_kernel<16>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
-  else if (k <= 32)
-    hipLaunchKernelGGL((topk_rows_kernel<32>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
-  else
-    hipLaunchKernelGGL((topk_rows_kernel<64>), grid, dim3(kTopkThreads), 0, s, scores, ld, n_rows,
-                       n_cols, (int)k, exclude_indptr, exclude_indices, out_vals, out_idx, vec);
+  for (int64_t c0 = 0; c0 < k; c0 += 64) {  // passes of <= 64 columns, each after the last
+    const int kk = (int)(k - c0 < 64 ? k - c0 : 64);
+    if (kk <= 16)
+      hipLaunchKernelGGL((topk_rows_kernel<16>), grid, dim3(kTopkThreads), 0, s, scores, ld,
+                         n_rows, n_cols, kk, exclude_indptr, exclude_indices, out_vals, out_idx,
+                         k, (int)c0, vec);
+    else if (kk <= 32)
+      hipLaunchKernelGGL((topk_rows_kernel<32>), grid, dim3(kTopkThreads), 0, s, scores, ld,
+                         n_rows, n_cols, kk, exclude_indptr, exclude_indices, out_vals, out_idx,
+                         k, (int)c0, vec);
+    else
+      hipLaunchKernelGGL((topk_rows_kernel<64>), grid, dim3(kTopkThreads), 0, s, scores, ld,
+                         n_rows, n_cols, kk, exclude_indptr, exclude_indices, out_vals, out_idx,
+                         k, (int)c0, vec);
+  }
   return check_launch("gnnrec_topk_rows_f32");
 }

@@ -45,6 +45,7 @@ SIGNATURES = {
     "gnnrec_last_error": (ctypes.c_char_p, []),
     "gnnrec_set_concurrency": (_INT, [_INT, _INT]),
     "gnnrec_get_concurrency": (_INT, [_P, _P]),
+    "gnnrec_rowq_stats": (_INT, [_P, _P]),
     "gnnrec_hold_cus": (_INT, [_INT, _INT, _INT, _I64, _P, _P]),
     "gnnrec_spmm_csr_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64, _P]),
     "gnnrec_spmm_csr_split_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,

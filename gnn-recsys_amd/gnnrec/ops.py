@@ -72,6 +72,13 @@ def get_concurrency():
     return r.value, bool(d.value)
 
 
+def rowq_stats():
+    """(queued launches, launches refused a busy ring slot) since the library loaded."""
+    q, b = ctypes.c_int64(), ctypes.c_int64()
+    check(_lib.load().gnnrec_rowq_stats(ctypes.byref(q), ctypes.byref(b)), "gnnrec_rowq_stats")
+    return q.value, b.value
+
+
 @contextlib.contextmanager
 def concurrency(reserve_cus: int, dynamic: bool = True):
     """set_concurrency for the launches enqueued inside the block, restored after."""

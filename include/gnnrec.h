@@ -106,6 +106,11 @@ const char* gnnrec_last_error(void);
 int gnnrec_set_concurrency(int reserve_cus, int dynamic);
 int gnnrec_get_concurrency(int* reserve_cus, int* dynamic);
 
+/* Diagnostic counters of the row queue since the library loaded: launches that ran
+ * queued, and launches that fell back to the static schedule because their ring slot's
+ * previous launch (on any stream) had not completed yet. */
+int gnnrec_rowq_stats(int64_t* queued, int64_t* busy);
+
 /* Diagnostic (no reference counterpart): `blocks` workgroups of `threads` threads,
  * each holding `lds_bytes` of LDS, stay resident for `usec` microseconds on
  * `stream` — a stand-in for a collective kernel's residency when measuring how the
@@ -257,10 +262,12 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
 
 /* ---- f1: recommendation top-k --------------------------------------------
  * For each row r of scores[n_rows, n_cols] (leading dimension ld): the k
- * (1..64) best columns ordered by (score desc, column asc), skipping the
+ * (1..2^20) best columns ordered by (score desc, column asc), skipping the
  * columns listed in exclude_indices[exclude_indptr[r] .. exclude_indptr[r+1])
  * (already-bought items; both pointers may be NULL).  Rows with fewer than k
- * eligible columns are padded with (-inf, -1).
+ * eligible columns are padded with (-inf, -1).  out_vals/out_idx: [n_rows, k].
+ * k > 64 streams the rows once per 64 results (reference --k is unbounded,
+ * main_inference.py:198). 
  * Replaces the per-user argsort / filter loop of src/metrics.py:52-77. */
 int gnnrec_topk_rows_f32(const float* scores, int64_t ld, int64_t n_rows, int64_t n_cols,
                          int64_t k, const int64_t* exclude_indptr, const int64_t* exclude_indices,

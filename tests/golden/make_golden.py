@@ -223,10 +223,13 @@ def gen_metrics_cases(ref, manifest):
     import importlib
     sys.path.insert(0, REF)
     ref_metrics = importlib.import_module("src.metrics")
-    cases = [("recs_cos", "cos", False), ("recs_cos_pop", "cos", True), ("recs_nn", "nn", False)]
-    for case_no, (name, pred, pop) in enumerate(cases):
+    # k=100 (> the 64 results of one top-k pass): the reference's --k is unbounded
+    cases = [("recs_cos", "cos", False, 10), ("recs_cos_pop", "cos", True, 10),
+             ("recs_nn", "nn", False, 10), ("recs_cos_k100", "cos", False, 100),
+             ("recs_nn_k100", "nn", False, 100)]
+    for case_no, (name, pred, pop, k) in enumerate(cases):
         rng = np.random.default_rng(500 + case_no)
-        n_u, n_i, d, k = 40, 300, 16, 10
+        n_u, n_i, d = 40, 300, 16
         hu = rng.standard_normal((n_u, d)).astype(np.float32)
         hi = rng.standard_normal((n_i, d)).astype(np.float32)
         popularity = rng.random(n_i).astype(np.float32)

@@ -99,11 +99,16 @@ def test_queue_ring_wraps(static_mode):
     X = torch.randn(n_src, d, device="cuda")
     ref = ops.spmm(indptr, indices, X, "sum")
     outs = []
+    q0, b0 = ops.rowq_stats()
     with ops.concurrency(0, True):
         for i in range(1100):
             o = ops.spmm(indptr, indices, X, "sum")
             if i % 100 == 99:
                 outs.append(o)
     torch.cuda.synchronize()
+    q1, b1 = ops.rowq_stats()
+    # every launch either ran queued or, when its slot's previous launch was still in
+    # flight, statically; fresh slots are always granted
+    assert (q1 - q0) + (b1 - b0) == 1100 and q1 - q0 >= 1024
     for o in outs:
         assert torch.equal(ref, o)

@@ -73,6 +73,29 @@ def test_topk_rows_edge_cases():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [64, 65, 100, 200, 3000, 3010])
+def test_topk_rows_beyond_one_pass(k):
+    """k > 64 runs in passes of 64 (each keeps only columns after the previous pass's
+    last result): the same order as a full (score desc, column asc) sort, ties across a
+    pass boundary included, exclusions honoured, rows that run out padded with -1."""
+    from gnnrec.recs import topk_rows
+    rng = np.random.default_rng(k)
+    S = rng.integers(-40, 40, (4, 3000)).astype(np.float32)  # many ties
+    ex_ptr = torch.tensor([0, 0, 500, 500, 500], device="cuda")
+    ex = rng.choice(3000, 500, replace=False).astype(np.int64)
+    vals, idx = topk_rows(torch.from_numpy(S).cuda(), k, ex_ptr, torch.from_numpy(ex).cuda())
+    idx, vals = idx.cpu().numpy(), vals.cpu().numpy()
+    for r in range(4):
+        cols = np.arange(3000)
+        if r == 1:
+            cols = np.setdiff1d(cols, ex)
+        ref = cols[np.lexsort((cols, -S[r, cols]))][:k]
+        np.testing.assert_array_equal(idx[r, : ref.size], ref)
+        np.testing.assert_array_equal(vals[r, : ref.size], S[r, ref])
+        assert (idx[r, ref.size:] == -1).all()
+
+
+@pytest.mark.gpu
 def test_inference_ondemand_end_to_end(tmp_path):
     """graph file -> ConvModel -> full-graph embeddings -> top-k, vs the oracle composition."""
     from gnnrec import nn as gnn
