@@ -1,0 +1,276 @@
+// f3 — COO -> CSR construction on the device: a stable LSD radix sort of the row keys.
+//
+// Reference: create_graph / dgl.heterograph (src/builder.py:377-383) and the reverse
+// relations of src/utils_data.py:204-238, whose in-CSR DGL builds when update_all first
+// runs; the CSR keeps the edges of a row in edge-id order.  Here: per pass of 8 key bits
+// (3 passes for up to 16M rows),
+//   radix_hist    one 256-thread block per 2048-edge tile counts the tile's digits,
+//                 stored digit-major [256][tiles];
+//   scan          exclusive scan of that table (gnnrec_exclusive_scan_i32): the first
+//                 output position of every (digit, tile);
+//   radix_scatter each wave ranks its 512 edges, 64 at a time, by digit: 8 ballots give
+//                 the lanes holding the same digit, mbcnt the rank among them, and an LDS
+//                 counter per (wave, digit) the edges of earlier rounds — so equal digits
+//                 keep their input order (stable), then writes key and value at
+//                 tile offset + earlier waves' counts + rank.
+// The final pass writes the CSR directly (indices = src[e], eids = e), and the row
+// pointers come from the sorted keys' run boundaries.  Bytes per edge per pass: 4 (hist)
+// + 8 read + 8 written (scatter); C4's 500M-edge relation sorts in 3 passes.
+#include "common.hpp"
+#include "csrsort.hpp"
+
+namespace gnnrec {
+namespace {
+
+constexpr int kRT = 256;                 // threads per tile block
+constexpr int kRRounds = 8;              // 64-edge rounds per wave
+constexpr int kRTile = kRT * kRRounds;   // edges per tile
+constexpr int kDigits = 256;
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+inline int key_passes(int64_t n_rows) {
+  int b = 1;
+  while (b < 32 && (int64_t(1) << b) < n_rows) ++b;
+  return (b + 7) / 8;
+}
+
+inline unsigned tile_grid(int64_t n_tiles) {
+  int64_t g = n_tiles < 256 * 16 ? n_tiles : 256 * 16;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+template <class K>
+__global__ __launch_bounds__(kRT) void radix_hist_kernel(const K* __restrict__ keys, int64_t E,
+                                                         int shift, int64_t n_tiles,
+                                                         int32_t* __restrict__ hist) {
+  __shared__ int cnt[kDigits];
+  const int tid = threadIdx.x;
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    cnt[tid] = 0;
+    __syncthreads();
+    const int64_t base = t * kRTile;
+#pragma unroll
+    for (int j = 0; j < kRRounds; ++j) {
+      const int64_t i = base + j * kRT + tid;
+      if (i < E) atomicAdd(&cnt[((uint32_t)keys[i] >> shift) & (kDigits - 1)], 1);
+    }
+    __syncthreads();
+    hist[(int64_t)tid * n_tiles + t] = cnt[tid];
+    __syncthreads();
+  }
+}
+
+// MODE 0: keys_out / vals_out; MODE 1: keys_out + the CSR gather (idx_out, eid_out)
+template <class K, bool VIN, int MODE>
+__global__ __launch_bounds__(kRT) void radix_scatter_kernel(
+    const K* __restrict__ keys, const int32_t* __restrict__ vals, int64_t E, int shift,
+    int64_t n_tiles, const int64_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
+    int32_t* __restrict__ vals_out, const int64_t* __restrict__ src,
+    int32_t* __restrict__ idx_out, int64_t* __restrict__ eid_out) {
+  __shared__ int cnt[kRT / kWave][kDigits];
+  __shared__ int64_t pos[kRT / kWave][kDigits];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
+  for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    for (int i = tid; i < (kRT / kWave) * kDigits; i += kRT) cnt[i / kDigits][i % kDigits] = 0;
+    __syncthreads();
+    const int64_t base = t * kRTile + (int64_t)w * (kRRounds * kWave);
+    uint32_t kk[kRRounds];
+    int32_t vv[kRRounds];
+    uint32_t dr[kRRounds];  // digit << 16 | rank among the wave's edges of that digit
+#pragma unroll
+    for (int j = 0; j < kRRounds; ++j) {
+      const int64_t i = base + j * kWave + lane;
+      const bool act = i < E;
+      const uint32_t k = act ? (uint32_t)keys[i] : 0u;
+      kk[j] = k;
+      vv[j] = act ? (VIN ? vals[i] : (int32_t)i) : 0;
+      const uint32_t d = (k >> shift) & (kDigits - 1);
+      uint64_t peers = __ballot(act);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      const unsigned r = __builtin_amdgcn_mbcnt_hi(
+          (unsigned)(peers >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)peers, 0u));
+      // every lane of a digit reads the wave's running count, then the lowest one adds the
+      // round's count (one wave: the LDS sees the read before the write)
+      const int old = act ? cnt[w][d] : 0;
+      if (act && r == 0) cnt[w][d] = old + __popcll(peers);
+      dr[j] = (d << 16) | (uint32_t)(old + (int)r);
+    }
+    __syncthreads();
+    {  // per digit: the tile's first position, then each wave's after the earlier waves'
+      const int d = tid;
+      int64_t run = offs[(int64_t)d * n_tiles + t];
+#pragma unroll
+      for (int ww = 0; ww < kRT / kWave; ++ww) {
+        pos[ww][d] = run;
+        run += cnt[ww][d];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRRounds; ++j) {
+      const int64_t i = base + j * kWave + lane;
+      if (i >= E) continue;
+      const int64_t p = pos[w][dr[j] >> 16] + (dr[j] & 0xffff);
+      if (keys_out) keys_out[p] = kk[j];
+      if (MODE == 0) {
+        vals_out[p] = vv[j];
+      } else {
+        idx_out[p] = (int32_t)src[vv[j]];
+        eid_out[p] = vv[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// row_ptr[r] = first sorted position with key >= r (run boundaries, one write per row)
+__global__ __launch_bounds__(256) void row_bounds_kernel(const uint32_t* __restrict__ keys,
+                                                         int64_t E, int64_t n_rows,
+                                                         int64_t* __restrict__ row_ptr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= E; k += stride) {
+    // clamped: an out-of-range key (a caller bug) leaves wrong rows, never a wild write
+    const int64_t prev = k > 0 ? min((int64_t)keys[k - 1], n_rows) : -1;
+    const int64_t cur = k < E ? min((int64_t)keys[k], n_rows) : n_rows;
+    for (int64_t r = prev + 1; r <= cur; ++r) row_ptr[r] = k;
+  }
+}
+
+__global__ __launch_bounds__(256) void zero_rows_kernel(int64_t* __restrict__ p, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0;
+}
+
+inline unsigned flat_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 256 * 16) b = 256 * 16;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+template <class K>
+void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64_t n_tiles,
+                 int32_t* hist, int64_t* offs, void* scan_ws, uint32_t* k_out, int32_t* v_out,
+                 const CsrGather* g, hipStream_t s) {
+  const unsigned grid = tile_grid(n_tiles);
+  hipLaunchKernelGGL(radix_hist_kernel<K>, dim3(grid), dim3(kRT), 0, s, keys, E, shift, n_tiles,
+                     hist);
+  (void)gnnrec_exclusive_scan_i32(hist, (int64_t)kDigits * n_tiles, offs, scan_ws, s);
+  const int64_t* src = g ? g->src : nullptr;
+  int32_t* idx = g ? g->idx_out : nullptr;
+  int64_t* eid = g ? g->eid_out : nullptr;
+#define GNNREC_SCATTER(VIN, MODE)                                                            \
+  hipLaunchKernelGGL((radix_scatter_kernel<K, VIN, MODE>), dim3(grid), dim3(kRT), 0, s, keys, \
+                     vals, E, shift, n_tiles, offs, k_out, v_out, src, idx, eid)
+  if (g) {
+    if (vals) GNNREC_SCATTER(true, 1);
+    else GNNREC_SCATTER(false, 1);
+  } else {
+    if (vals) GNNREC_SCATTER(true, 0);
+    else GNNREC_SCATTER(false, 0);
+  }
+#undef GNNREC_SCATTER
+}
+
+}  // namespace
+
+size_t radix_ws_bytes(int64_t E, int64_t n_rows) {
+  (void)n_rows;
+  if (E <= 0) return 0;
+  const int64_t n_tiles = (E + kRTile - 1) / kRTile;
+  const int64_t n_hist = kDigits * n_tiles;
+  return 4 * align_up((size_t)E * 4)                            // two (key, value) buffers
+         + align_up((size_t)n_hist * 4)                         // per-tile digit counts
+         + align_up((size_t)(n_hist + 1) * 8)                   // their scan
+         + align_up((size_t)gnnrec_scan_workspace_bytes(n_hist));
+}
+
+int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, int64_t E,
+                    int64_t n_rows, uint32_t* keys_out, int32_t* vals_out, const CsrGather* g,
+                    int64_t* row_ptr, void* ws, size_t ws_bytes, hipStream_t s) {
+  GNNREC_REQUIRE(E >= 0 && E < (int64_t(1) << 31) && n_rows >= 0 && n_rows < (int64_t(1) << 31),
+                 "radix sort: %lld keys / %lld rows exceed the int32 range", (long long)E,
+                 (long long)n_rows);
+  if (E == 0) {
+    if (row_ptr)
+      hipLaunchKernelGGL(zero_rows_kernel, dim3(flat_grid(n_rows + 1)), dim3(256), 0, s, row_ptr,
+                         n_rows + 1);
+    return check_launch("radix sort");
+  }
+  GNNREC_REQUIRE(keys_in && ws && (g || vals_out) && (!row_ptr || keys_out),
+                 "radix sort: null pointer");
+  GNNREC_REQUIRE(ws_bytes >= radix_ws_bytes(E, n_rows), "radix sort: workspace %zu < %zu bytes",
+                 ws_bytes, radix_ws_bytes(E, n_rows));
+  const int64_t n_tiles = (E + kRTile - 1) / kRTile;
+  const int64_t n_hist = kDigits * n_tiles;
+  char* p = static_cast<char*>(ws);
+  const size_t slot = align_up((size_t)E * 4);
+  uint32_t* kb[2] = {reinterpret_cast<uint32_t*>(p), reinterpret_cast<uint32_t*>(p + slot)};
+  int32_t* vb[2] = {reinterpret_cast<int32_t*>(p + 2 * slot),
+                    reinterpret_cast<int32_t*>(p + 3 * slot)};
+  int32_t* hist = reinterpret_cast<int32_t*>(p + 4 * slot);
+  int64_t* offs = reinterpret_cast<int64_t*>(p + 4 * slot + align_up((size_t)n_hist * 4));
+  void* scan_ws = p + 4 * slot + align_up((size_t)n_hist * 4) + align_up((size_t)(n_hist + 1) * 8);
+  const int passes = key_passes(n_rows);
+  for (int ps = 0; ps < passes; ++ps) {
+    const bool last = ps == passes - 1;
+    uint32_t* k_out = last ? keys_out : kb[ps & 1];
+    int32_t* v_out = last ? vals_out : vb[ps & 1];
+    const CsrGather* gg = last ? g : nullptr;
+    if (ps == 0) {
+      if (keys64)
+        launch_pass(static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles, hist, offs,
+                    scan_ws, k_out, v_out, gg, s);
+      else
+        launch_pass(static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles, hist, offs,
+                    scan_ws, k_out, v_out, gg, s);
+    } else {
+      launch_pass(kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, 8 * ps, n_tiles, hist, offs, scan_ws,
+                  k_out, v_out, gg, s);
+    }
+  }
+  if (row_ptr)
+    hipLaunchKernelGGL(row_bounds_kernel, dim3(flat_grid(E + 1)), dim3(256), 0, s, keys_out, E,
+                       n_rows, row_ptr);
+  return check_launch("radix sort");
+}
+
+}  // namespace gnnrec
+
+extern "C" size_t gnnrec_csr_build_workspace_bytes(int64_t n_edges, int64_t n_dst) {
+  using namespace gnnrec;
+  if (n_edges <= 0) return 0;
+  return align_up((size_t)n_edges * 4) + radix_ws_bytes(n_edges, n_dst);
+}
+
+extern "C" int gnnrec_csr_build(const int64_t* src, const int64_t* dst, int64_t n_edges,
+                                int64_t n_dst, void* workspace, size_t workspace_bytes,
+                                int64_t* indptr, int32_t* indices, int64_t* eids,
+                                void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_edges >= 0 && n_dst >= 0, "gnnrec_csr_build: negative size");
+  GNNREC_REQUIRE(indptr, "gnnrec_csr_build: null indptr");
+  hipStream_t s = as_stream(stream);
+  if (n_edges == 0)
+    return radix_sort_rows(nullptr, true, nullptr, 0, n_dst, nullptr, nullptr, nullptr, indptr,
+                           nullptr, 0, s);
+  GNNREC_REQUIRE(n_dst > 0, "gnnrec_csr_build: %lld edges into 0 rows", (long long)n_edges);
+  GNNREC_REQUIRE(src && dst && indices && eids && workspace, "gnnrec_csr_build: null pointer");
+  const size_t need = gnnrec_csr_build_workspace_bytes(n_edges, n_dst);
+  GNNREC_REQUIRE(workspace_bytes >= need, "gnnrec_csr_build: workspace %zu < %zu bytes",
+                 workspace_bytes, need);
+  char* p = static_cast<char*>(workspace);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(p);  // sorted dst ids (for the row pointers)
+  const size_t slot = align_up((size_t)n_edges * 4);
+  CsrGather g;
+  g.src = src;
+  g.idx_out = indices;
+  g.eid_out = eids;
+  return radix_sort_rows(dst, true, nullptr, n_edges, n_dst, keys, nullptr, &g, indptr, p + slot,
+                         workspace_bytes - slot, s);
+}

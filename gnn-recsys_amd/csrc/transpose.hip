@@ -4,34 +4,19 @@
 // source rows is the same sum with the roles swapped: grad_X[u] = Σ_{e: src_e = u}
 // w_e · g[dst_e].  Scattering that with float atomics is capped by the L2 atomic units
 // (≈0.32 T float atomics/s measured, tools/bench_spmm_bwd.py), well below what a gather
-// moves; transposing the block once (stable LSD radix sort of the int32 source ids, then
-// a bounds pass) turns it into the same bandwidth-bound gather as the forward, and the
+// moves; transposing the block once (the library's stable LSD radix sort of the int32
+// source ids, csrsort.hip) turns it into the same bandwidth-bound gather as the forward, and the
 // stable order (ascending edge id inside each source row) makes the gradient bitwise
 // repeatable.  Reference: DGL's backward of update_all(copy_u, mean/sum) used by
 // ConvLayer training (src/model.py:161-167, src/train/run.py:136-138).
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include "common.hpp"
+#include "csrsort.hpp"
 
 namespace gnnrec {
 namespace {
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
-
-inline unsigned key_bits(int64_t n_src) {
-  unsigned b = 0;
-  while (b < 32 && (int64_t(1) << b) < n_src) ++b;
-  return b < 1 ? 1 : b;
-}
-
-size_t sort_temp_bytes(int64_t E, int64_t n_src, hipStream_t s) {
-  size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                            (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)E, 0,
-                            key_bits(n_src), s);
-  return bytes;
-}
 
 // one wave per dst row: edge id, dst id and the per-edge weight (ew · 1/deg for mean)
 __global__ __launch_bounds__(256) void edge_rows_kernel(const int64_t* __restrict__ indptr,
@@ -113,37 +98,19 @@ inline unsigned flat_grid(int64_t n) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
-__global__ __launch_bounds__(256) void iota_kernel(int32_t* __restrict__ out, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
-    out[k] = (int32_t)k;
-}
-
-// stable sort of row keys: perm = edge ids ordered by (key, edge id); indptr[n_rows+1].
-// Scratch: [values | sorted keys | radix temp]; values = 0..E-1 written here unless the
-// caller supplies them (eid_ready), in which case the first slot is free for perm.
+// stable sort of row keys: perm = edge ids ordered by (key, edge id) — eid_ready's values
+// when given, else the identity — and indptr[n_rows+1].  Scratch: [free slot | sorted keys |
+// radix scratch].
 int sort_rows(const int32_t* keys_in, int64_t E, int64_t n_rows, char* p, size_t bytes,
               int64_t* indptr, int32_t* perm, int32_t* eid_ready, hipStream_t s) {
   const size_t slot = align_up((size_t)E * 4);
-  int32_t* eid = eid_ready ? eid_ready : reinterpret_cast<int32_t*>(p);
-  int32_t* keys = reinterpret_cast<int32_t*>(p + slot);
-  void* temp = p + 2 * slot;
-  size_t temp_bytes = bytes - 2 * slot;
-  if (!eid_ready)
-    hipLaunchKernelGGL(iota_kernel, dim3(flat_grid(E)), dim3(256), 0, s, eid, E);
-  if (hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys, eid, perm,
-                                               (unsigned)E, 0, key_bits(n_rows), s);
-      e != hipSuccess) {
-    set_error("radix sort failed: %s", hipGetErrorString(e));
-    return GNNREC_EHIP;
-  }
-  hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_rows + 1)), dim3(256), 0, s, keys, E,
-                     n_rows, indptr);
-  return GNNREC_OK;
+  uint32_t* keys = reinterpret_cast<uint32_t*>(p + slot);
+  return radix_sort_rows(keys_in, false, eid_ready, E, n_rows, keys, perm, nullptr, indptr,
+                         p + 2 * slot, bytes - 2 * slot, s);
 }
 
 size_t sort_rows_bytes(int64_t E, int64_t n_rows) {
-  return 2 * align_up((size_t)E * 4) + align_up(sort_temp_bytes(E, n_rows, nullptr));
+  return 2 * align_up((size_t)E * 4) + radix_ws_bytes(E, n_rows);
 }
 
 }  // namespace
@@ -191,15 +158,10 @@ extern "C" int gnnrec_csr_transpose(const int64_t* indptr, const int32_t* indice
     size_t temp_bytes = need - 2 * slot - deg_bytes;
     hipLaunchKernelGGL(edge_dst_kernel, dim3(flat_grid(n_dst * 16)), dim3(256), 0, s, indptr,
                        n_dst, mean, dst_of, inv_deg);
-    if (hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, indices, keys, dst_of,
-                                                 indices_t, (unsigned)n_edges, 0,
-                                                 key_bits(n_src), s);
-        e != hipSuccess) {
-      set_error("radix sort failed: %s", hipGetErrorString(e));
-      return GNNREC_EHIP;
-    }
-    hipLaunchKernelGGL(bounds_kernel, dim3(flat_grid(n_src + 1)), dim3(256), 0, s, keys,
-                       n_edges, n_src, indptr_t);
+    const int rc = radix_sort_rows(indices, false, dst_of, n_edges, n_src,
+                                   reinterpret_cast<uint32_t*>(keys), indices_t, nullptr,
+                                   indptr_t, temp, temp_bytes, s);
+    if (rc != GNNREC_OK) return rc;
     if (mean)
       hipLaunchKernelGGL(row_weight_kernel, dim3(flat_grid(n_edges)), dim3(256), 0, s, indices_t,
                          inv_deg, n_edges, ew_t);

@@ -25,6 +25,8 @@ from typing import Dict, Iterable, Optional, Tuple
 
 import torch
 
+from . import ops
+
 NID = "_ID"
 EID = "_ID"
 CEType = Tuple[str, str, str]
@@ -81,16 +83,20 @@ class _MultiTypeData:
 
 
 def build_csr(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
-    """dst-major CSR with in-row order = eid order.  -> indptr, indices(int32), eids."""
-    dev = dst.device
-    if dst.numel() == 0:
-        return (torch.zeros(n_dst + 1, dtype=torch.int64, device=dev),
-                torch.zeros(0, dtype=torch.int32, device=dev),
-                torch.zeros(0, dtype=torch.int64, device=dev))
+    """dst-major CSR with in-row order = eid order.  -> indptr, indices(int32), eids.
+
+    Row f3 (reference src/builder.py:377-383 -> dgl.heterograph, whose in-CSR keeps the
+    edges of a row in edge-id order): on a HIP device the library's stable radix sort of
+    the dst ids (gnnrec_csr_build).  A graph still held in host memory (assembled on the
+    CPU before .to(device), as the reference builds its graphs) gets the same CSR from a
+    host stable sort; nothing on the device path falls back to it."""
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64, device=src.device)
+    if dst.device.type == 'cuda':
+        return ops.csr_build(src, dst, n_dst)
     order = torch.argsort(dst, stable=True)
-    counts = torch.bincount(dst, minlength=n_dst)
-    indptr = torch.zeros(n_dst + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(counts, 0, out=indptr[1:])
+    indptr = torch.zeros(n_dst + 1, dtype=torch.int64)
+    torch.cumsum(torch.bincount(dst, minlength=n_dst), 0, out=indptr[1:])
     return indptr, src[order].to(torch.int32), order
 
 

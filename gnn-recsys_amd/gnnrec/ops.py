@@ -254,6 +254,30 @@ def csr_transpose(indptr: torch.Tensor, indices: torch.Tensor, n_src: int,
     return ip_t, ix_t, w_t
 
 
+def csr_build(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
+    """dst-major CSR of the COO relation (src, dst) with in-row order = edge id
+    (gnnrec_csr_build: stable radix sort of the dst ids on the device).
+    -> (indptr int64 [n_dst+1], indices int32 = src ids, eids int64)."""
+    lib = _lib.load()
+    _dev(dst, "dst", torch.int64)
+    _dev(src, "src", torch.int64)
+    if src.shape != dst.shape or src.dim() != 1:
+        raise ValueError("csr_build: src and dst must be 1-D tensors of one length")
+    dev, E = dst.device, dst.numel()
+    if E and n_dst <= 0:
+        raise ValueError(f"csr_build: {E} edges into {n_dst} rows")
+    src, dst = src.contiguous(), dst.contiguous()
+    indptr = torch.empty(n_dst + 1, dtype=torch.int64, device=dev)
+    indices = torch.empty(E, dtype=torch.int32, device=dev)
+    eids = torch.empty(E, dtype=torch.int64, device=dev)
+    nbytes = int(lib.gnnrec_csr_build_workspace_bytes(E, n_dst))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    check(lib.gnnrec_csr_build(ptr(src), ptr(dst), E, n_dst, ptr(ws), nbytes, ptr(indptr),
+                               ptr(indices), ptr(eids), stream_ptr(dev)), "gnnrec_csr_build")
+    indptr._gnnrec_nnz = E
+    return indptr, indices, eids
+
+
 def csr_from_keys(keys: torch.Tensor, n_rows: int):
     """Rows of a COO list: -> (indptr int64 [n_rows+1], perm int32 [E]) with perm the edge
     ids grouped by keys[e] (ascending edge id inside a row).  keys: int32/int64 in [0, n_rows)."""

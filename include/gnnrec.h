@@ -322,6 +322,20 @@ size_t gnnrec_csr_from_keys_workspace_bytes(int64_t n_edges, int64_t n_rows);
 int gnnrec_csr_from_keys(const int32_t* keys, int64_t n_edges, int64_t n_rows, void* workspace,
                          size_t workspace_bytes, int64_t* indptr, int32_t* perm, void* stream);
 
+/* ---- f3: graph construction ----------------------------------------------
+ * dst-major CSR of a COO relation (src[e], dst[e]) e = 0..n_edges-1, in-row order =
+ * edge id (DGL's in-CSR of a heterograph built by dgl.heterograph, reference
+ * src/builder.py:377-383, reverse relations src/utils_data.py:204-238; the reverse
+ * relation's CSR is the same call with src and dst swapped).  indptr[n_dst+1] (int64),
+ * indices[n_edges] = src[e] narrowed to int32, eids[n_edges] (int64).  Every dst id must
+ * lie in [0, n_dst); n_edges, n_dst < 2^31.  A stable LSD radix sort of the dst ids
+ * (8 bits per pass, own kernels, no vendor sort): 3 passes for up to 16M rows.  Workspace
+ * from gnnrec_csr_build_workspace_bytes (≈ 20 B per edge). */
+size_t gnnrec_csr_build_workspace_bytes(int64_t n_edges, int64_t n_dst);
+int gnnrec_csr_build(const int64_t* src, const int64_t* dst, int64_t n_edges, int64_t n_dst,
+                     void* workspace, size_t workspace_bytes, int64_t* indptr, int32_t* indices,
+                     int64_t* eids, void* stream);
+
 /* out[i] = a[i] + b[i] over n floats (out may alias a or b): the upper levels of the
  * deterministic pass's fixed pairwise tree over source-range partial tables. */
 int gnnrec_add_f32(const float* a, const float* b, float* out, int64_t n, void* stream);

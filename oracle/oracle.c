@@ -15,6 +15,10 @@
  *                           max of an empty row = 0.
  *   oracle_synth_edges      the benchmark generator (gnn-recsys_amd/csrc/synth.hip),
  *                           bit for bit.
+ *   oracle_csr_from_coo     the in-CSR DGL builds for a relation of dgl.heterograph
+ *                           (reference src/builder.py:377-383): rows by dst, in-row
+ *                           order = edge id.  A stable counting sort: thread t owns a
+ *                           contiguous dst range and scans every edge in eid order.
  *   oracle_sample_*         DGL MultiLayer{Full,}NeighborSampler frontier +
  *                           exclusion (reference src/sampling.py:153-161): all
  *                           in-edges, or `fanout` of them by Floyd's algorithm on
@@ -178,5 +182,38 @@ void oracle_sample_fill(const int64_t* indptr, const int64_t* indices, const int
         ++o;
       }
     }
+  }
+}
+
+/* dst-major CSR of (src, dst), in-row order = edge id.  indptr[n_dst+1], indices[E] (src
+ * narrowed to int32), eids[E].  dst must lie in [0, n_dst). */
+void oracle_csr_from_coo(const int64_t* src, const int64_t* dst, int64_t E, int64_t n_dst,
+                         int64_t* indptr, int32_t* indices, int64_t* eids) {
+  memset(indptr, 0, sizeof(int64_t) * (size_t)(n_dst + 1));
+#pragma omp parallel
+  {
+#ifdef _OPENMP
+    const int nt = omp_get_num_threads(), t = omp_get_thread_num();
+#else
+    const int nt = 1, t = 0;
+#endif
+    const int64_t lo = n_dst * t / nt, hi = n_dst * (t + 1) / nt;
+    for (int64_t e = 0; e < E; ++e)
+      if (dst[e] >= lo && dst[e] < hi) ++indptr[dst[e] + 1];
+#pragma omp barrier
+#pragma omp single
+    for (int64_t r = 0; r < n_dst; ++r) indptr[r + 1] += indptr[r];
+    /* implicit barrier after single: every row's start is known */
+    int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(hi > lo ? hi - lo : 1));
+    for (int64_t r = lo; r < hi; ++r) cur[r - lo] = indptr[r];
+    for (int64_t e = 0; e < E; ++e) {
+      const int64_t d = dst[e];
+      if (d >= lo && d < hi) {
+        const int64_t p = cur[d - lo]++;
+        indices[p] = (int32_t)src[e];
+        eids[p] = e;
+      }
+    }
+    free(cur);
   }
 }

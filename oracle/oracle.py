@@ -61,6 +61,8 @@ def lib():
         L.oracle_sample_count.restype = None
         L.oracle_sample_fill.argtypes = [P, P, P, P, P, I64, I64, U64, P, P, P]
         L.oracle_sample_fill.restype = None
+        L.oracle_csr_from_coo.argtypes = [P, P, I64, I64, P, P, P]
+        L.oracle_csr_from_coo.restype = None
         L.oracle_hash3.argtypes = [U64, U64, U64]
         L.oracle_hash3.restype = U64
         L.oracle_num_threads.restype = INT
@@ -85,6 +87,19 @@ def csr_from_coo(src: np.ndarray, dst: np.ndarray, n_dst: int):
     return indptr, src[order].astype(np.int32), order.astype(np.int64)
 
 
+def csr_from_coo_c(src: np.ndarray, dst: np.ndarray, n_dst: int):
+    """csr_from_coo through oracle.c's parallel stable counting sort (large graphs: the
+    numpy argsort above is single-threaded).  Same outputs, bit for bit."""
+    src = np.ascontiguousarray(src, np.int64)
+    dst = np.ascontiguousarray(dst, np.int64)
+    E = src.size
+    indptr = np.empty(n_dst + 1, np.int64)
+    indices = np.empty(E, np.int32)
+    eids = np.empty(E, np.int64)
+    lib().oracle_csr_from_coo(_p(src), _p(dst), E, n_dst, _p(indptr), _p(indices), _p(eids))
+    return indptr, indices, eids
+
+
 class Graph:
     """Heterograph restated: COO per canonical etype (reverse relations share
     the forward eid order, reference src/utils_data.py:205-238)."""
@@ -101,7 +116,8 @@ class Graph:
     def csr(self, ce):
         if ce not in self._csr:
             s, d = self.edges[ce]
-            self._csr[ce] = csr_from_coo(s, d, self.num_nodes[ce[2]])
+            build = csr_from_coo_c if s.size > (1 << 20) else csr_from_coo
+            self._csr[ce] = build(s, d, self.num_nodes[ce[2]])
         return self._csr[ce]
 
     def num_edges(self, ce):

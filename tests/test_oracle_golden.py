@@ -193,3 +193,15 @@ def test_model_blocks_prefix_block_equals_full_graph_rows():
     for nt, v in seeds.items():
         if nt in full:
             np.testing.assert_allclose(h[nt], full[nt][v], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("E,n_dst", [(0, 5), (1, 1), (1000, 7), (200_000, 50_000),
+                                     (3_000_000, 1000)])
+def test_csr_from_coo_c_equals_numpy_restatement(E, n_dst):
+    """oracle.c's parallel counting sort (large graphs, CPU baseline, row f3's checker)
+    gives the numpy stable-argsort CSR bit for bit, empty rows included."""
+    rng = np.random.default_rng(E)
+    src = rng.integers(0, 1 << 30, E)
+    dst = rng.integers(0, n_dst, E) if E else np.zeros(0, np.int64)
+    for a, b in zip(oracle.csr_from_coo_c(src, dst, n_dst), oracle.csr_from_coo(src, dst, n_dst)):
+        np.testing.assert_array_equal(a, b)
