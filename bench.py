@@ -62,8 +62,9 @@ def parse():
                     help="row-kernel schedule: 'auto' (static at one rank; 16 CUs reserved + "
                          "work queue beside RCCL at several) or 'R,Q' (R reserved CUs, Q=1 queue)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-scale", type=float, default=0.1,
-                    help="fraction of the graph used for the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=float, default=1 / 32,
+                    help="fraction of each relation's destination rows the bounded CPU "
+                         "baseline aggregates (over the full-size tables and edge stream)")
     return ap.parse_args()
 
 
@@ -123,70 +124,180 @@ def launch_bytes(shard, d, fused, deterministic):
     return out
 
 
-def pmc_traffic(args, world, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x2 for gfx950's half-counted wide reads + WRITE_SIZE, KB -> B), for
-    the default single-GPU C4 workload they were collected on; None otherwise."""
+CSRC = os.path.join(ROOT, "gnn-recsys_amd", "csrc")
+
+
+def csrc_digest() -> str:
+    """sha256 (16 hex) of the HIP sources and build flags the library is compiled from: ties
+    a committed PMC profile to the kernels that produced it."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".hpp", ".cpp", ".h")) or f == "Makefile":
+            h.update(f.encode())
+            h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def default_workload(args) -> bool:
+    return (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
+            args.config, args.hetero, args.mode, args.segments) == (
+                10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4", "sum",
+                "deterministic", 8)
+
+
+def pmc_traffic(args, world):
+    """{bench tag: HBM bytes per launch} from the newest committed rocprofv3 PMC
+    passes (profiles/<tag>_pmc_{fetch,write}.csv + <tag>_pmc_meta.json): FETCH_SIZE x2 (gfx950
+    counts half the bytes of wide reads) + WRITE_SIZE, KB -> B.  Only for the default
+    single-GPU C4 workload the passes ran on, and only if the HIP sources hash to the
+    `csrc_sha` the profile was taken with; otherwise ({}, reason)."""
     import csv
-    default = (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
-               args.config, args.mode, args.segments) == (10_000_000, 1_000_000, 500_000_000,
-                                                          128, 0.0, "mean", "c4",
-                                                          "deterministic", 8)
-    f = os.path.join(ROOT, "profiles", "r01_c4_pmc_fetch.csv")
-    w = os.path.join(ROOT, "profiles", "r01_c4_pmc_write.csv")
-    if world != 1 or not default or not (os.path.exists(f) and os.path.exists(w)):
-        return None
-    tot, n = 0.0, 0
-    for path, scale in ((f, 2.0), (w, 1.0)):
-        for r in csv.DictReader(open(path)):
-            if kernel in r["Kernel_Name"]:
-                tot += float(r["Counter_Value"]) * 1024 * scale
-                n += scale == 2.0
-    return tot / n if n else None
+    import glob
+    metas = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_meta.json")))
+    if world != 1 or not default_workload(args):
+        return {}, "not the profiled workload"
+    if not metas:
+        return {}, "no PMC profile"
+    meta = json.load(open(metas[-1]))
+    tag = os.path.basename(metas[-1])[: -len("_pmc_meta.json")]
+    if meta.get("csrc_sha") != csrc_digest():
+        return {}, f"stale: {tag} profiled csrc {meta.get('csrc_sha')}, now {csrc_digest()}"
+    out = {}
+    for t, kernel in meta["kernels"].items():  # bench tag -> kernel-name substring
+        tot, n = 0.0, 0
+        for kind, scale in (("fetch", 2.0), ("write", 1.0)):
+            path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{kind}.csv")
+            for r in csv.DictReader(open(path)):
+                if kernel in r["Kernel_Name"]:
+                    tot += float(r["Counter_Value"]) * 1024 * scale
+                    n += kind == "fetch"
+        if n:
+            out[t] = tot / n
+    return out, f"{tag} (csrc {meta['csrc_sha']})"
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(args, d):
-    """Bounded sample of the same workload on the host cores: the oracle's C/OpenMP
-    restatement of DGL 0.5's CPU SpMM + numpy fp32 GEMMs (kind 'port')."""
+    """The same workload on the host cores, timed on a bounded row sample.
+
+    Full-size inputs — the whole user and item tables (C4: 5.1 GB + 512 MB fp32) and the
+    same generated edge stream — and the destination rows [0, f·N) of both relations (f =
+    --cpu-sample): every sampled row gathers its full in-neighbourhood from the full table,
+    so the cache behaviour is the workload's, not a small graph's.  Timed per pass: the
+    NodeEmbedding of f of the nodes, then L=2 ConvLayers 'mean' over both sampled
+    relations (hetero sum over one relation per type is the identity).
+      kind 'port': the oracle (C/OpenMP restatement of DGL 0.5's CPU SpMM + numpy fp32
+        GEMMs, reference src/model.py:143-148,226-235);
+      'index_add_value': torch CPU, edge-chunked index_add_ + matmul (the second data point
+        SURVEY §8d asks for).
+    Rate = sampled edges aggregated / time."""
     import numpy as np
 
     sys.path.insert(0, ROOT)
     from oracle import oracle
 
-    U = max(1000, int(args.users * args.cpu_scale))
-    I = max(100, int(args.items * args.cpu_scale))
-    E = max(1000, int(args.edges * args.cpu_scale))
-    u, i = oracle.synth_edges(11, 0, E, U, I)
-    g = oracle.Graph({"user": U, "item": I},
-                     {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)})
-    for ce in g.canonical_etypes:
-        g.csr(ce)
-    rng = np.random.default_rng(0)
-    feats = {"user": rng.standard_normal((U, d), dtype=np.float32),
-             "item": rng.standard_normal((I, d), dtype=np.float32)}
+    U, I, E, f = args.users, args.items, args.edges, args.cpu_sample
+    Us, Is = max(1, int(U * f)), max(1, int(I * f))
+    t_setup = time.perf_counter()
+    # sampled CSRs: bought-by rows = users [0, Us) (sources: items), buys rows = items [0, Is)
+    su, du, si, di = [], [], [], []
+    chunk = 1 << 26
+    for e0 in range(0, E, chunk):
+        u, i = oracle.synth_edges(11, e0, min(chunk, E - e0), U, I)
+        m = u < Us
+        su.append(i[m]); du.append(u[m])
+        m = i < Is
+        si.append(u[m]); di.append(i[m])
+    ce_u, ce_i = ("item", "bought-by", "user"), ("user", "buys", "item")
+    csr = {ce_u: oracle.csr_from_coo_c(np.concatenate(su), np.concatenate(du), Us),
+           ce_i: oracle.csr_from_coo_c(np.concatenate(si), np.concatenate(di), Is)}
+    del su, du, si, di
+    X = {"user": oracle.fill_f32(1, (U, d)), "item": oracle.fill_f32(2, (I, d))}
     torch.manual_seed(0)
-    sd = {}
-    for nt in ("user", "item"):
-        lin = torch.nn.Linear(d, d)
-        sd[f"{nt}_embed.proj_feats.weight"] = lin.weight.detach().numpy()
-        sd[f"{nt}_embed.proj_feats.bias"] = lin.bias.detach().numpy()
-    for layer in range(2):
-        for rel in ("buys", "bought-by"):
-            for w in ("fc_self", "fc_neigh"):
-                t = torch.empty(d, d)
-                torch.nn.init.xavier_uniform_(t, gain=torch.nn.init.calculate_gain("relu"))
-                sd[f"layers.{layer}.mods.{rel}.{w}.weight"] = t.numpy()
-    reps, t_tot = 0, 0.0
-    while reps < 2 or (t_tot < 10.0 and reps < 5):
-        t0 = time.perf_counter()
-        oracle.model_full_graph(g, feats, sd, args.aggregator, "sum", True, True)
-        t_tot += time.perf_counter() - t0
-        reps += 1
-    edges = 2 * 2 * E
-    return {"value": edges * reps / t_tot, "unit": "edges/s", "cores": oracle.num_threads(),
-            "kind": "port",
-            "sample": f"{U} users x {I} items x {E} edges ({args.cpu_scale:g} of the workload, "
-                      f"same mean degrees), same model, {reps} passes, {t_tot:.1f} s"}
+    w = {}
+    for rel in ("buys", "bought-by"):
+        w[rel] = {}
+        for name in ("fc_self.weight", "fc_neigh.weight"):
+            t = torch.empty(d, d)
+            torch.nn.init.xavier_uniform_(t, gain=torch.nn.init.calculate_gain("relu"))
+            w[rel][name] = t.numpy()
+    emb = {nt: (oracle.fill_f32(3, (d, d)) * 0.1, oracle.fill_f32(4, (d,))) for nt in X}
+    t_setup = time.perf_counter() - t_setup
+
+    class Sample:  # what oracle.conv_layer reads of a graph: the CSR of the relation
+        occurrence = {}
+
+        @staticmethod
+        def csr(ce):
+            return csr[ce]
+
+    edges = sum(int(c[0][-1]) for c in csr.values()) * 2  # L=2 layers
+    rows = {"user": Us, "item": Is}
+
+    def port_pass():
+        for nt in X:  # the NodeEmbedding share of the sampled rows
+            oracle.linear(X[nt][: rows[nt]], *emb[nt])
+        for _ in range(2):
+            for ce in (ce_u, ce_i):
+                oracle.conv_layer(Sample, ce, X[ce[0]], X[ce[2]][: rows[ce[2]]],
+                                  w[ce[1]], "mean", True)
+
+    tX = {nt: torch.from_numpy(x) for nt, x in X.items()}
+    tcsr = {}
+    for ce, (ip, ix, _) in csr.items():
+        ipt = torch.from_numpy(ip)
+        deg = ipt[1:] - ipt[:-1]
+        tcsr[ce] = (torch.repeat_interleave(torch.arange(deg.numel()), deg),
+                    torch.from_numpy(ix).long(), deg.clamp(min=1).float().unsqueeze(1))
+    tw = {rel: {k: torch.from_numpy(v) for k, v in ww.items()} for rel, ww in w.items()}
+    temb = {nt: (torch.from_numpy(a), torch.from_numpy(b)) for nt, (a, b) in emb.items()}
+
+    def torch_pass():
+        for nt in tX:
+            torch.nn.functional.linear(tX[nt][: rows[nt]], *temb[nt])
+        for _ in range(2):
+            for ce in (ce_u, ce_i):
+                dst, src, deg = tcsr[ce]
+                agg = torch.zeros((rows[ce[2]], d))
+                for k in range(0, src.numel(), 1 << 22):
+                    agg.index_add_(0, dst[k:k + (1 << 22)], tX[ce[0]][src[k:k + (1 << 22)]])
+                agg /= deg
+                z = torch.relu(tX[ce[2]][: rows[ce[2]]] @ tw[ce[1]]["fc_self.weight"].t()
+                               + agg @ tw[ce[1]]["fc_neigh.weight"].t())
+                n = z.norm(dim=1, keepdim=True)
+                z / torch.where(n == 0, torch.ones_like(n), n)
+
+    def timed(fn, budget=8.0, warm=True):
+        if warm:
+            fn()  # page faults, thread pools
+        reps, tot = 0, 0.0
+        while reps < 1 or (tot < budget and reps < 5):
+            t0 = time.perf_counter()
+            fn()
+            tot += time.perf_counter() - t0
+            reps += 1
+        return edges * reps / tot, reps, tot
+
+    cores = oracle.num_threads()
+    torch.set_num_threads(cores)
+    port, reps, tot = timed(port_pass)
+    alt, _, _ = timed(torch_pass, budget=4.0, warm=False)
+    wl = "C4" if default_workload(args) else "custom"
+    return {"value": port, "unit": "edges/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(), "index_add_value": alt, "config": wl,
+            "sample": f"{wl} full-size tables ({U}x{d} + {I}x{d} fp32) and edge stream; dst rows "
+                      f"[0,{f:g}N) of both relations = {edges // 2} edges/layer; 2 layers, "
+                      f"{reps} passes, {tot:.1f} s (setup {t_setup:.0f} s)"}
 
 
 def main():
@@ -259,22 +370,44 @@ def main():
     edges_per_step = 2 * sum(rs.global_edges for rs in shard.rels.values())  # L=2 layers
     value = edges_per_step * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-    # roofline of the aggregation kernels: the fused gather+projection launch when the pass
-    # has one (C4: the user side, ~half the pass), else the busiest tag; the other
-    # aggregation kernel (C4: the item side's source-range tiles) is reported beside it
+
+    # roofline of the aggregation kernels (SURVEY §8d d4 bytes per launch ÷ the launch's
+    # HIP-event time): the headline is the kernel with the most time per pass (C4: the
+    # user->item source tiles, 16 launches, about half the pass; the fused item->user
+    # launches the other half); every other aggregation kernel rides along as flat
+    # `<field>_<tag>` keys so a flat record parser keeps them
     per_tag = launch_bytes(shard, d, runner.fused, det)
-    ran = [t for t in per_tag if timers.mean_ms(t)[1]]
-
-    def line(t):
+    stats = {}
+    for t in per_tag:
         ms, n = timers.mean_ms(t)
-        b = per_tag[t][0] / per_tag[t][1]  # bytes per layer / launches per layer
-        return ms, n, b, b / (ms * 1e-3) / 1e9
+        if n:
+            b = per_tag[t][0] / per_tag[t][1]  # bytes per layer / launches per layer
+            stats[t] = {"launch_ms": ms, "launches_timed": n, "bytes_per_launch": b,
+                        "achieved": b / (ms * 1e-3) / 1e9, "ms_per_pass": ms * n / args.steps}
+    traffic, traffic_src = pmc_traffic(args, world)
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None, "traffic": None}
+    if stats:
+        order = sorted(stats, key=lambda t: -stats[t]["ms_per_pass"])
+        head = order[0]
+        st = stats[head]
+        roof.update(achieved=st["achieved"], frac=st["achieved"] / HBM_PEAK_GBS,
+                    traffic=traffic.get(head),
+                    kernel=KERNELS[head][1], bytes_per_launch=st["bytes_per_launch"],
+                    launch_ms=st["launch_ms"], launches_timed=st["launches_timed"],
+                    share_of_step=st["ms_per_pass"] / ms_step, traffic_src=traffic_src)
+        for t in order[1:]:
+            o = stats[t]
+            roof.update({f"frac_{t}": o["achieved"] / HBM_PEAK_GBS, f"achieved_{t}": o["achieved"],
+                         f"launch_ms_{t}": o["launch_ms"], f"launches_{t}": o["launches_timed"],
+                         f"bytes_per_launch_{t}": o["bytes_per_launch"],
+                         f"share_of_step_{t}": o["ms_per_pass"] / ms_step,
+                         f"traffic_{t}": traffic.get(t)})
 
-    tag = "spmm_project" if "spmm_project" in ran else max(
-        ran, key=lambda t: timers.mean_ms(t)[0] * timers.mean_ms(t)[1]) if ran else "spmm"
-    spmm_ms, n_launch, bytes_per_launch, achieved = line(tag) if ran else (None, 0, None, None)
-    others = {t: dict(zip(("launch_ms", "launches_timed", "bytes_per_launch", "achieved"),
-                          line(t)), kernel=KERNELS[t][1]) for t in ran if t != tag}
+    diag = None
+    if world > 1:
+        diag = multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
+                                     ms_step)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
@@ -285,47 +418,77 @@ def main():
                    "sample": f"failed: {exc!r}"}
 
     if rank == 0:
+        wl = (args.config.upper() if (args.users, args.items, args.edges) ==
+              (10_000_000, 1_000_000, 500_000_000) else "custom")
+        cfg = {"workload": f"{wl}: {args.users / 1e6:g}M users x {args.items / 1e6:g}M items, "
+                           f"{args.edges / 1e6:g}M edges/dir, embed + 2 SAGE '{args.aggregator}'"
+                           f", hetero {args.hetero}, d={d}"
+                           + (" (80/20 clicks/buys)" if args.config == "c5" else "")
+                           + (f", zipf {args.zipf}" if args.zipf else ""),
+               "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
+               "mode": ("deterministic (bitwise equal at 1/2/4/8 GPUs)" if det else "fast"),
+               "source_tiles": shard.segments or 0, "partition": shard.balance,
+               "output": "partitioned (each rank keeps the user and item rows it owns)",
+               "overlap": not args.no_overlap,
+               "row_schedule": ("static" if not runner.concurrency or
+                                not runner.concurrency[1] else "queue")
+                               + (f", {runner.concurrency[0]} CUs reserved"
+                                  if runner.concurrency and runner.concurrency[0] else "")}
+        if diag is not None:
+            cfg.update(diag)
         rec = {
             "metric": "edges aggregated/sec, full-graph embed pass, d=128",
             "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (counter-hash graph seed 11, N(0,1) features, xavier weights)",
-            "config": {"workload": (args.config.upper() if (args.users, args.items, args.edges) ==
-                                    (10_000_000, 1_000_000, 500_000_000) else "custom")
-                                   + f" full-graph embed pass: {args.users} users x {args.items} "
-                                   f"items, {args.edges} edges/direction"
-                                   + (" (80% clicks / 20% buys, 4 relations)"
-                                      if args.config == "c5" else "")
-                                   + f", NodeEmbedding + L=2 ConvLayer '{args.aggregator}', "
-                                     f"hetero {args.hetero}, norm, d={d}"
-                                   + (f", item zipf s={args.zipf}" if args.zipf else "")
-                                   + (f", {shard.segments} source tiles" if shard.segments
-                                      else "")
-                                   + (", deterministic (bitwise equal at 1/2/4/8 GPUs)" if det
-                                      else ""),
-                       "edges_per_step": edges_per_step, "parallelism": f"graph{world}",
-                       "output": "partitioned (each rank keeps the user and item rows it owns)",
-                       "overlap": not args.no_overlap,
-                       "row_schedule": ("static" if not runner.concurrency or
-                                        not runner.concurrency[1] else "queue")
-                                       + (f", {runner.concurrency[0]} CUs reserved"
-                                          if runner.concurrency and runner.concurrency[0]
-                                          else "")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": pmc_traffic(args, world, KERNELS[tag][0]),
-                         "kernel": KERNELS[tag][1],
-                         "bytes_per_launch": bytes_per_launch, "launch_ms": spmm_ms,
-                         "launches_timed": n_launch,
-                         "other_kernels": {t: dict(o, frac=o["achieved"] / HBM_PEAK_GBS)
-                                           for t, o in others.items()}},
-            "cpu_baseline": cpu,
+            "config": cfg, "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev, ms_step):
+    """Self-diagnosis of a P > 1 run (every rank takes part; rank 0 reports):
+      rank_compute_ms  each rank's share of the pass with the same kernels and concurrency
+                       but an exchange that moves nothing (gnnrec.dist.ComputeOnlyExchange);
+      comm_ms          one pass's collectives issued alone, back to back (RecordingExchange
+                       replay), and comm_bytes_per_rank the bytes each rank sends;
+      overlap_frac     the share of comm_ms hidden under compute:
+                       (max rank_compute + comm − step) / comm, clamped to [0, 1]."""
+    from gnnrec.dist import ComputeOnlyExchange, RecordingExchange
+    from gnnrec.inference import ShardedFullGraphPass
+
+    world = ex.ws
+    rec = RecordingExchange(ex)
+    runner.ex = rec
+    runner.run(feats, replicate_output=False)
+    torch.cuda.synchronize()
+    runner.ex = ex
+    comm_ms = rec.replay_ms(dev)
+    null = ShardedFullGraphPass(model, shard, ComputeOnlyExchange(world, ex.rk),
+                                overlap=not args.no_overlap, deterministic=det, concurrency=conc)
+    reps = max(2, min(args.steps, 5))
+    null.run(feats, replicate_output=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        null.run(feats, replicate_output=False)
+    torch.cuda.synchronize()
+    mine = (time.perf_counter() - t0) / reps * 1e3
+    t = torch.tensor([mine, float(shard.local_edge_count())], dtype=torch.float64, device=dev)
+    allr = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(allr, t)
+    compute = [float(a[0]) for a in allr]
+    edges = [int(a[1]) for a in allr]
+    overlap = None
+    if comm_ms > 0:
+        overlap = max(0.0, min(1.0, (max(compute) + comm_ms - ms_step) / comm_ms))
+    return {"backend": str(ex.backend), "collective_path": rec.path, "ranks_seen": world,
+            "rank_compute_ms": [round(c, 2) for c in compute], "rank_edges": edges,
+            "comm_ms": comm_ms, "comm_bytes_per_rank": rec.bytes_sent(),
+            "collectives_per_pass": len(rec.calls), "overlap_frac": overlap}
 
 
 if __name__ == "__main__":

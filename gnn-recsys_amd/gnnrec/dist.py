@@ -39,6 +39,30 @@ def even_ranges(n: int, parts: int) -> List[int]:
     return [(n * p) // parts for p in range(parts + 1)]
 
 
+def degree_ranges(weight: torch.Tensor, parts: int) -> List[int]:
+    """Boundaries b[0..parts] of a contiguous split of [0, n) balanced by cumulative weight
+    ("contiguous global-id ranges balanced by cumulative in-degree"): b[p] is
+    the first id whose exclusive prefix weight reaches p·W/parts.  `weight` is a per-node
+    int tensor (callers pass in-degree summed over relations + 1, so a row's fixed cost
+    counts and zero-degree ranges still split).  Integer arithmetic only: every rank that
+    computes it from the same degrees gets the same boundaries."""
+    n = int(weight.numel())
+    if n == 0 or parts == 1:
+        return [0] + [n] * parts if n else [0] * (parts + 1)
+    c = torch.cumsum(weight.to(torch.int64), 0)
+    W = int(c[-1])
+    if W <= 0:
+        return even_ranges(n, parts)
+    t = torch.tensor([(W * p) // parts for p in range(1, parts)], dtype=torch.int64,
+                     device=c.device)
+    # exclusive prefix of id j is c[j-1]: first j with c[j-1] >= t is searchsorted(c, t) + 1
+    inner = (torch.searchsorted(c, t) + 1).clamp_(max=n).tolist()
+    b = [0] + [int(x) for x in inner] + [n]
+    for p in range(1, parts + 1):  # monotone even with ties
+        b[p] = max(b[p], b[p - 1])
+    return b
+
+
 def padded_shard(n: int, parts: int) -> int:
     """Rows per rank of a replicated table padded to parts·S rows."""
     return (n + parts - 1) // parts if n else 0
@@ -124,3 +148,111 @@ class Exchange:
         t = torch.tensor([x], dtype=torch.float64, device=device)
         self.all_reduce_(t, "max")
         return float(t.item())
+
+
+class ComputeOnlyExchange:
+    """An Exchange of world size P that moves nothing: each collective returns this rank's
+    own data in the right shape.  Runs a rank's share of the pass with the same kernels,
+    launch order and concurrency settings as the real one, minus the communication
+    (bench.py's per-rank compute time at P > 1; tools/probe_rank_work.py)."""
+
+    def __init__(self, ws: int, rk: int = 0):
+        self.ws, self.rk, self.backend, self.group, self.path = ws, rk, None, None, "none"
+
+    def reduce_scatter_rows(self, full, op, async_op=False):
+        S = full.shape[0] // self.ws
+        return full[self.rk * S:(self.rk + 1) * S], None
+
+    def all_to_all_rows(self, full, async_op=False):
+        S = full.shape[0] // self.ws
+        return full.view((self.ws, S) + tuple(full.shape[1:])), None
+
+    def all_gather_rows(self, own, out, async_op=False):
+        S = own.shape[0]
+        out[self.rk * S:(self.rk + 1) * S].copy_(own)
+        return out, None
+
+    def all_reduce_(self, t, op="sum"):
+        return t
+
+    def max_scalar(self, x, device):
+        return x
+
+
+class RecordingExchange:
+    """Wraps an Exchange and records every collective of a pass: (kind, shape, dtype, op)
+    plus the bytes this rank sends (all-to-all / reduce-scatter: (P−1)/P of the table;
+    all-gather: (P−1)·own).  `replay_ms` times the same collectives alone, back to back,
+    on fresh tensors: the communication a pass would cost with nothing to overlap."""
+
+    def __init__(self, inner: Exchange):
+        self.inner = inner
+        self.ws, self.rk, self.group = inner.ws, inner.rk, inner.group
+        self.backend = inner.backend
+        self.calls = []
+
+    @property
+    def path(self):
+        return self.inner.path
+
+    def _rec(self, kind, t, op=None, sent=0):
+        self.calls.append((kind, tuple(t.shape), t.dtype, op, int(sent)))
+
+    def reduce_scatter_rows(self, full, op, async_op=False):
+        self._rec("reduce_scatter", full, op,
+                  full.numel() * full.element_size() * (self.ws - 1) // self.ws)
+        return self.inner.reduce_scatter_rows(full, op, async_op)
+
+    def all_to_all_rows(self, full, async_op=False):
+        self._rec("all_to_all", full, None,
+                  full.numel() * full.element_size() * (self.ws - 1) // self.ws)
+        return self.inner.all_to_all_rows(full, async_op)
+
+    def all_gather_rows(self, own, out, async_op=False):
+        self._rec("all_gather", out, None,
+                  own.numel() * own.element_size() * (self.ws - 1))
+        return self.inner.all_gather_rows(own, out, async_op)
+
+    def all_reduce_(self, t, op="sum"):
+        return self.inner.all_reduce_(t, op)
+
+    def max_scalar(self, x, device):
+        return self.inner.max_scalar(x, device)
+
+    def bytes_sent(self) -> int:
+        return sum(c[4] for c in self.calls)
+
+    def replay_ms(self, device, reps: int = 3) -> float:
+        """Mean wall ms of one pass's collectives issued alone (synchronous, in order)."""
+        if self.ws == 1 or not self.calls:
+            return 0.0
+        bufs = []
+        for kind, shape, dtype, op, _ in self.calls:
+            full = torch.zeros(shape, dtype=dtype, device=device)
+            if kind == "all_gather":
+                own = full[: shape[0] // self.ws].clone()
+                bufs.append((kind, own, full, op))
+            else:
+                bufs.append((kind, full, None, op))
+
+        def once():
+            for kind, a, b, op in bufs:
+                if kind == "reduce_scatter":
+                    self.inner.reduce_scatter_rows(a, op)
+                elif kind == "all_to_all":
+                    self.inner.all_to_all_rows(a)
+                else:
+                    self.inner.all_gather_rows(a, b)
+
+        import time
+        once()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        dist.barrier(group=self.group)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            once()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        dist.barrier(group=self.group)
+        return (time.perf_counter() - t0) / reps * 1e3

@@ -30,7 +30,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import _lib, ops
-from .dist import Exchange, even_ranges, padded_shard
+from .dist import Exchange, degree_ranges, even_ranges, padded_shard
 from .graph import HeteroGraph, build_csr
 
 
@@ -92,11 +92,18 @@ class GraphShard:
     """This rank's share of a heterograph for the sharded full-graph pass."""
 
     def __init__(self, rank: int, world: int, ptype: str, num_nodes: Dict[str, int],
-                 canonical_etypes: List[tuple], device, segments: Optional[int] = None):
+                 canonical_etypes: List[tuple], device, segments: Optional[int] = None,
+                 ptype_weight: Optional[torch.Tensor] = None):
         """segments: split every 'partial' relation's edges into this many fixed key ranges
         (source id of the partitioned type, else edge id), `segments // world` per rank, so
         ShardedFullGraphPass(deterministic=True) sums the same partials in the same tree at
-        any world size dividing `segments` (bitwise-equal outputs at P=1/2/4/8)."""
+        any world size dividing `segments` (bitwise-equal outputs at P=1/2/4/8).
+
+        ptype_weight: per-node weight of the partitioned type (its in-degree summed over
+        relations, + 1): the contiguous id ranges are then balanced by cumulative weight
+         instead of by node count.  With `segments`, the segment key ranges are
+        the weight-balanced ones and every rank's range is the union of its segments, so the
+        boundaries still nest at every world size."""
         if segments is not None and (segments < world or segments % world or
                                      segments & (segments - 1)):
             raise ValueError(f"segments={segments} must be a power of two and a multiple of "
@@ -106,8 +113,20 @@ class GraphShard:
         self.num_nodes = dict(num_nodes)
         self.canonical_etypes = list(canonical_etypes)
         self.device = torch.device(device)
-        b = even_ranges(num_nodes[ptype], world)
-        self.p_lo, self.p_hi = b[rank], b[rank + 1]
+        n_p = num_nodes[ptype]
+        if ptype_weight is not None and ptype_weight.numel() != n_p:
+            raise ValueError(f"ptype_weight has {ptype_weight.numel()} entries for {n_p} nodes")
+        split = (lambda parts: degree_ranges(ptype_weight, parts)) if ptype_weight is not None \
+            else (lambda parts: even_ranges(n_p, parts))
+        self.balance = "degree" if ptype_weight is not None else "count"
+        if segments is not None:
+            self.seg_bounds = split(segments)
+            k = segments // world
+            self.bounds = [self.seg_bounds[r * k] for r in range(world + 1)]
+        else:
+            self.seg_bounds = None
+            self.bounds = split(world)
+        self.p_lo, self.p_hi = self.bounds[rank], self.bounds[rank + 1]
         self.shard_rows = {nt: padded_shard(n, world) for nt, n in num_nodes.items()
                            if nt != ptype}
         self.rels: Dict[tuple, RelShard] = {}
@@ -161,7 +180,7 @@ class GraphShard:
             # edge split of from_graph); each segment's rows keep the edges' input order
             k = self.segments // self.world
             if s_t == self.ptype:
-                key, bounds = src, even_ranges(self.num_nodes[self.ptype], self.segments)
+                key, bounds = src, self.seg_bounds
             else:
                 key, bounds = eid, even_ranges(global_edges, self.segments)
             segs = []
@@ -176,11 +195,19 @@ class GraphShard:
 
     @classmethod
     def from_graph(cls, g: HeteroGraph, rank: int, world: int, ptype: str = 'user', device=None,
-                   weight_field: Optional[str] = 'occurrence', segments: Optional[int] = None):
-        """Shard a full HeteroGraph held by every rank (tests / moderate graphs)."""
+                   weight_field: Optional[str] = 'occurrence', segments: Optional[int] = None,
+                   balance: str = 'degree'):
+        """Shard a full HeteroGraph held by every rank (tests / moderate graphs).
+        balance: 'degree' (ranges balanced by the partitioned type's in-degree over all
+        relations + 1) or 'count' (equal node counts)."""
         dev = device if device is not None else g.device
+        weight = None
+        if balance == 'degree':
+            weight = ptype_in_degree(g, ptype)
+        elif balance != 'count':
+            raise ValueError(f"balance must be 'degree' or 'count', not {balance!r}")
         sh = cls(rank, world, ptype, {nt: g.num_nodes(nt) for nt in g.ntypes},
-                 g.canonical_etypes, dev, segments)
+                 g.canonical_etypes, dev, segments, weight)
         for ce in g.canonical_etypes:
             s, d = g.all_edges(etype=ce)
             E = s.numel()
@@ -210,6 +237,17 @@ class GraphShard:
                 t[: x.shape[0]] = x.to(self.device)
                 out[nt] = t
         return out
+
+
+def ptype_in_degree(g: HeteroGraph, ptype: str) -> torch.Tensor:
+    """In-degree of every `ptype` node summed over the relations into it, + 1 (the
+    partition weight of GraphShard: a row costs its edges plus its own read/write)."""
+    w = torch.ones(g.num_nodes(ptype), dtype=torch.int64, device=g.device)
+    for ce in g.canonical_etypes:
+        if ce[2] == ptype:
+            _, d = g.all_edges(etype=ce)
+            w += torch.bincount(d, minlength=w.numel())
+    return w
 
 
 RESERVE_CUS = 16  # of 256: room for RCCL's channel blocks beside the aggregation
@@ -687,13 +725,12 @@ def gather_partitioned(shard: GraphShard, rows: torch.Tensor, exchange: Exchange
     if exchange.ws == 1:
         return rows
     import torch.distributed as dist
-    n = shard.num_nodes[shard.ptype]
-    S = padded_shard(n, exchange.ws)
+    b = shard.bounds
+    S = max(b[r + 1] - b[r] for r in range(exchange.ws))
     pad = torch.zeros((S, rows.shape[1]), dtype=rows.dtype, device=rows.device)
     pad[: rows.shape[0]] = rows
     parts = [torch.empty_like(pad) for _ in range(exchange.ws)]
     dist.all_gather(parts, pad, group=exchange.group)
-    b = even_ranges(n, exchange.ws)
     return torch.cat([parts[r][: b[r + 1] - b[r]] for r in range(exchange.ws)], 0)
 
 

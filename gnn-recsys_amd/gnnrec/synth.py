@@ -43,18 +43,32 @@ def bipartite_shard(n_users: int, n_items: int, n_edges: int, rank: int, world: 
                     seed: int = 11, zipf_s: float = 0.0, chunk: int = 1 << 26,
                     occurrence: bool = False,
                     split=(("buys", "bought-by", 1.0),),
-                    segments: Optional[int] = None) -> GraphShard:
+                    segments: Optional[int] = None, balance: str = "degree") -> GraphShard:
     """This rank's GraphShard of the synthetic user->item graph (+ reverse relations).
 
     `split` assigns consecutive eid ranges of the generated edge stream to relations
     (e.g. C5: clicks 80 % / buys 20 %); eids are per relation, reverse relations share
-    the forward eid order."""
+    the forward eid order.  balance='degree' partitions users by cumulative in-degree
+    (one extra pass over the regenerated edge stream counts it), 'count' by
+    user count."""
     dev = torch.device(device)
     pairs = relation_pairs(split)
     etypes = [ce for f, r, _ in pairs for ce in (f, r)]
-    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, etypes, dev,
-                    segments)
     cdf = zipf_cdf(n_items, zipf_s, dev) if zipf_s > 0 else None
+    weight = None
+    if balance == "degree" and (world > 1 or segments is not None):
+        # (at one rank too when segmented: the segment ranges must not depend on P)
+        # every relation's edges are incident to one user (its reverse lands on it)
+        weight = torch.ones(n_users, dtype=torch.int64, device=dev)
+        for e0 in range(0, n_edges, chunk):
+            u, _ = ops.synth_edges(seed, e0, min(chunk, n_edges - e0), n_users, n_items, dev,
+                                   cdf)
+            weight += torch.bincount(u, minlength=n_users)
+            del u
+    elif balance not in ("degree", "count"):
+        raise ValueError(f"balance must be 'degree' or 'count', not {balance!r}")
+    sh = GraphShard(rank, world, "user", {"user": n_users, "item": n_items}, etypes, dev,
+                    segments, weight)
     bounds = [0]
     for _, _, frac in pairs:
         bounds.append(min(n_edges, bounds[-1] + int(round(frac * n_edges))))

@@ -19,6 +19,9 @@
  *                           (reference src/builder.py:377-383): rows by dst, in-row
  *                           order = edge id.  A stable counting sort: thread t owns a
  *                           contiguous dst range and scans every edge in eid order.
+ *   oracle_fill_f32         uniform [-1, 1) fp32 table (xorshift per 4 K chunk) (the CPU
+ *                           baseline's full-size feature tables; values do not change
+ *                           the amount of work, and numpy's generator is single-threaded)
  *   oracle_sample_*         DGL MultiLayer{Full,}NeighborSampler frontier +
  *                           exclusion (reference src/sampling.py:153-161): all
  *                           in-edges, or `fanout` of them by Floyd's algorithm on
@@ -113,6 +116,21 @@ void oracle_synth_edges(uint64_t seed, int64_t e0, int64_t n, int64_t n_u, int64
         else lo = mid + 1;
       }
       it[k] = (int32_t)lo;
+    }
+  }
+}
+
+void oracle_fill_f32(uint64_t seed, int64_t n, float* out) {
+  const int64_t chunks = (n + 4095) / 4096;
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < chunks; ++c) {  /* xorshift64* per 4096-element chunk */
+    uint64_t x = mix64(seed ^ mix64((uint64_t)c)) | 1u;
+    const int64_t end = (c + 1) * 4096 < n ? (c + 1) * 4096 : n;
+    for (int64_t k = c * 4096; k < end; ++k) {
+      x ^= x >> 12;
+      x ^= x << 25;
+      x ^= x >> 27;
+      out[k] = (float)((x * 0x2545F4914F6CDD1Dull) >> 40) * (2.0f / 16777216.0f) - 1.0f;
     }
   }
 }

@@ -63,6 +63,8 @@ def lib():
         L.oracle_sample_fill.restype = None
         L.oracle_csr_from_coo.argtypes = [P, P, I64, I64, P, P, P]
         L.oracle_csr_from_coo.restype = None
+        L.oracle_fill_f32.argtypes = [U64, I64, P]
+        L.oracle_fill_f32.restype = None
         L.oracle_hash3.argtypes = [U64, U64, U64]
         L.oracle_hash3.restype = U64
         L.oracle_num_threads.restype = INT
@@ -443,6 +445,13 @@ def synth_edges(seed: int, e0: int, n: int, n_u: int, n_i: int, cdf=None):
         cdf = np.ascontiguousarray(cdf, np.float64)
     lib().oracle_synth_edges(seed, e0, n, n_u, n_i, _p(cdf), _p(u), _p(i))
     return u, i
+
+
+def fill_f32(seed: int, shape) -> np.ndarray:
+    """uniform [-1, 1) fp32 array (OpenMP; bench.py's CPU-baseline feature tables)."""
+    out = np.empty(shape, np.float32)
+    lib().oracle_fill_f32(seed, out.size, _p(out))
+    return out
 
 
 def zipf_cdf(n: int, s: float) -> np.ndarray:
