@@ -97,21 +97,25 @@ class EventTimers:
 KERNELS = {
     "spmm_project": ("spmm_project_kernel", "gnnrec spmm_project_kernel (gather + segmented "
                      "mean + fused SAGE projection, ReLU, L2 norm)"),
+    "spmm_project_mfma": ("spmm_project_mfma_kernel", "gnnrec spmm_project_mfma_kernel (gather "
+                          "+ mean of 32-row tiles, SAGE projection on fp32 MFMA, ReLU, L2 norm)"),
     "spmm_tile": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented sum of one "
                   "source-range tile, accumulated in place)"),
     "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
 }
 
 
-def launch_bytes(shard, d, fused, deterministic):
+def launch_bytes(shard, d, runner, deterministic):
     """Algorithmic bytes per layer and launches per layer of each aggregation kernel tag
     (SURVEY §8d row d4): per edge d*4 (fp32 source row) + 4 (int32 index); per dst row 8
     (int64 indptr) + d*4 (write), + d*4 for the h_self row when the projection is fused
     into the launch, + d*4 for the partial read back when a tile accumulates in place."""
     out = {}
     for ce, rs in shard.rels.items():
-        if ce in fused:
-            tag, b, n = "spmm_project", rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + 8 * d), 1
+        if ce in runner.fused:
+            avg = rs.global_edges / max(shard.num_nodes[ce[2]], 1) if deterministic else None
+            tag = runner._fused_tag(rs, avg)
+            b, n = rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + 8 * d), 1
         elif rs.segs is not None:
             tag, b, n = "spmm_tile", 0, len(rs.segs)
             for j, (ip, ix, _) in enumerate(rs.segs):
@@ -376,7 +380,7 @@ def main():
     # user->item source tiles, 16 launches, about half the pass; the fused item->user
     # launches the other half); every other aggregation kernel rides along as flat
     # `<field>_<tag>` keys so a flat record parser keeps them
-    per_tag = launch_bytes(shard, d, runner.fused, det)
+    per_tag = launch_bytes(shard, d, runner, det)
     stats = {}
     for t in per_tag:
         ms, n = timers.mean_ms(t)

@@ -89,6 +89,48 @@ __device__ inline void rq_for_each(unsigned* q, int64_t n, int ch, F&& f) {
   }
 }
 
+// The same walk as rq_for_each as a cursor, for kernels whose whole block consumes one
+// chunk at a time (one wave draws, the block processes): rq_next returns the next chunk
+// [r0, r1) of [0, n) or false once every head is drained.  Wave-uniform; call rq_begin
+// once, then rq_next until it returns false.
+struct RqCursor {
+  int home, h;
+  unsigned t;
+};
+
+__device__ inline void rq_begin(RqCursor& c, unsigned* q) {
+  c.home = xcc_id();
+  c.h = c.home;
+  c.t = rq_take(q + c.h * kRqStride);
+}
+
+__device__ inline bool rq_next(RqCursor& c, unsigned* q, int64_t n, int ch, int64_t& r0,
+                               int64_t& r1) {
+  const int lane = threadIdx.x & 63;
+  while (true) {
+    const int64_t lo = n * c.h / kRqHeads, hi = n * (c.h + 1) / kRqHeads;
+    const int64_t s = lo + (int64_t)__shfl(c.t, 0) * ch;
+    if (s < hi) {
+      c.t = rq_take(q + c.h * kRqStride);  // in flight while this chunk runs
+      r0 = s;
+      r1 = s + ch < hi ? s + ch : hi;
+      return true;
+    }
+    bool open = false;  // head c.h drained: the next head after home that has rows
+    if (lane < kRqHeads) {
+      const int64_t l2 = n * lane / kRqHeads, h2 = n * (lane + 1) / kRqHeads;
+      const unsigned v =
+          __hip_atomic_load(q + lane * kRqStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      open = l2 + (int64_t)v * ch < h2;
+    }
+    uint64_t m = __ballot(open) & ((1ull << kRqHeads) - 1);
+    if (m == 0) return false;
+    m = ((m >> (c.home + 1)) | (m << (kRqHeads - 1 - c.home))) & ((1ull << kRqHeads) - 1);
+    c.h = (c.home + 1 + __builtin_ctzll(m)) & (kRqHeads - 1);
+    c.t = rq_take(q + c.h * kRqStride);
+  }
+}
+
 // end of a queued launch: after every wave of the block has left rq_for_each, one lane
 // counts the block out; the last block of the grid zeroes the slot for its next user
 __device__ inline void rq_finish(unsigned* q) {

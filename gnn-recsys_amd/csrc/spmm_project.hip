@@ -40,6 +40,82 @@ inline int fused_chunk() {
   return v;
 }
 
+// The per-row epilogue both fused kernels share: lane = output columns j0, j0+1 of `row`
+// (y = the projected pre-activation incl. bias): ReLU, zero-guarded L2 norm over the 64
+// lanes, the cross-relation accumulate (store / add / max / online-softmax attention),
+// out_div, one float2 store per lane.  `valid` (wave-uniform) is false for padding rows
+// past the range end: they take part in the shuffles, store nothing.
+struct EpiArgs {
+  bool relu, l2, attn;
+  int accum;
+  float out_div, a0, a1;
+  float* attn_state;
+  float* out;
+  int64_t ldo;
+  int j0;
+};
+
+__device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool valid,
+                                             float y0, float y1) {
+  if (e.relu) {
+    y0 = fmaxf(y0, 0.f);
+    y1 = fmaxf(y1, 0.f);
+  }
+  if (e.l2) {
+    float ss = y0 * y0 + y1 * y1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) ss += __shfl_xor(ss, off);
+    float nrm = sqrtf(ss);
+    if (nrm == 0.f) nrm = 1.f;
+    y0 = y0 / nrm;
+    y1 = y1 / nrm;
+  }
+  float keep = 0.f, nrm_attn = 1.f;
+  if (e.attn) {  // online softmax over relations, score s = a . y (row-uniform)
+    float sc = y0 * e.a0 + y1 * e.a1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) sc += __shfl_xor(sc, off);
+    float mnew = sc, snew = 1.f, cnew = 1.f;
+    if (valid && e.accum != GNNREC_ACC_ATTN_FIRST) {
+      const float2 st = reinterpret_cast<const float2*>(e.attn_state)[row];
+      mnew = fmaxf(st.x, sc);
+      keep = expf(st.x - mnew);
+      cnew = expf(sc - mnew);
+      snew = st.y * keep + cnew;
+    }
+    if (e.accum == GNNREC_ACC_ATTN_LAST) nrm_attn = 1.f / snew;
+    if (valid && (threadIdx.x & 63) == 0)
+      reinterpret_cast<float2*>(e.attn_state)[row] = make_float2(mnew, snew);
+    y0 *= cnew;
+    y1 *= cnew;
+  }
+  if (!valid) return;
+  float2* p = reinterpret_cast<float2*>(e.out + row * e.ldo + e.j0);
+  if (e.attn) {
+    if (e.accum != GNNREC_ACC_ATTN_FIRST) {
+      const float2 o = *p;
+      y0 = o.x * keep + y0;
+      y1 = o.y * keep + y1;
+    }
+    y0 *= nrm_attn;
+    y1 *= nrm_attn;
+  } else if (e.accum != GNNREC_ACC_STORE) {
+    const float2 o = *p;
+    if (e.accum == GNNREC_ACC_ADD) {
+      y0 = o.x + y0;
+      y1 = o.y + y1;
+    } else {
+      y0 = fmaxf(o.x, y0);
+      y1 = fmaxf(o.y, y1);
+    }
+  }
+  if (e.out_div > 0.f) {
+    y0 = y0 / e.out_div;
+    y1 = y1 / e.out_div;
+  }
+  *p = make_float2(y0, y1);
+}
+
 template <int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
@@ -71,6 +147,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   const float c0 = bias_ne ? bias_ne[j0] : 0.f, c1 = bias_ne ? bias_ne[j0 + 1] : 0.f;
   const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
   const float a0 = attn ? attn_vec[j0] : 0.f, a1 = attn ? attn_vec[j0 + 1] : 0.f;
+  const EpiArgs ep{relu, l2, attn, accum, out_div, a0, a1, attn_state, out, ldo, j0};
 
   // rows [row0, row0 + kPRows) of this wave, those at or past `lim` skipped
   auto step = [&](int64_t row0, int64_t lim) {
@@ -153,67 +230,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free for the next rows
 
 #pragma unroll
-    for (int r = 0; r < kPRows; ++r) {
-      const int64_t row = row0 + r;
-      float y0 = z[r][0], y1 = z[r][1];
-      if (relu) {
-        y0 = fmaxf(y0, 0.f);
-        y1 = fmaxf(y1, 0.f);
-      }
-      if (l2) {
-        float ss = y0 * y0 + y1 * y1;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) ss += __shfl_xor(ss, off);
-        float nrm = sqrtf(ss);
-        if (nrm == 0.f) nrm = 1.f;
-        y0 = y0 / nrm;
-        y1 = y1 / nrm;
-      }
-      float keep = 0.f, nrm_attn = 1.f;
-      if (attn) {  // online softmax over relations, score e = a . y (row-uniform)
-        float e = y0 * a0 + y1 * a1;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) e += __shfl_xor(e, off);
-        float mnew = e, snew = 1.f, cnew = 1.f;
-        if (row < lim && accum != GNNREC_ACC_ATTN_FIRST) {
-          const float2 st = reinterpret_cast<const float2*>(attn_state)[row];
-          mnew = fmaxf(st.x, e);
-          keep = expf(st.x - mnew);
-          cnew = expf(e - mnew);
-          snew = st.y * keep + cnew;
-        }
-        if (accum == GNNREC_ACC_ATTN_LAST) nrm_attn = 1.f / snew;
-        if (row < lim && lane == 0)
-          reinterpret_cast<float2*>(attn_state)[row] = make_float2(mnew, snew);
-        y0 *= cnew;
-        y1 *= cnew;
-      }
-      if (row >= lim) continue;
-      float2* p = reinterpret_cast<float2*>(out + row * ldo + j0);
-      if (attn) {
-        if (accum != GNNREC_ACC_ATTN_FIRST) {
-          const float2 o = *p;
-          y0 = o.x * keep + y0;
-          y1 = o.y * keep + y1;
-        }
-        y0 *= nrm_attn;
-        y1 *= nrm_attn;
-      } else if (accum != GNNREC_ACC_STORE) {
-        const float2 o = *p;
-        if (accum == GNNREC_ACC_ADD) {
-          y0 = o.x + y0;
-          y1 = o.y + y1;
-        } else {
-          y0 = fmaxf(o.x, y0);
-          y1 = fmaxf(o.y, y1);
-        }
-      }
-      if (out_div > 0.f) {
-        y0 = y0 / out_div;
-        y1 = y1 / out_div;
-      }
-      *p = make_float2(y0, y1);
-    }
+    for (int r = 0; r < kPRows; ++r) epilogue_row(ep, row0 + r, row0 + r < lim, z[r][0], z[r][1]);
   };
 
   if (rq != nullptr) {  // rows from the queue: blocks that start late take fewer
@@ -226,6 +243,212 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
   for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
        row0 += stride)
     step(row0, n_dst);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// The same fused operation for LOW-DEGREE relations, projection on the MFMA.
+//
+// Why: the VALU kernel above re-reads both 64 KiB weight matrices from LDS for every 2
+// rows, a fixed per-row cost that the gather hides at C4's 50 edges/row but that bounds
+// a 10-edges/row relation (C5 bought-by: 18.0 ms fused vs 7.6 ms gather + 7.1 ms GEMM).
+// Here a block of 8 waves owns 32-row tiles: the waves gather 4 rows each (the same
+// gather_range / xor tree as spmm_csr_kernel, so the aggregate is bit-identical) into an
+// LDS tile A = [h_self | agg] (32 × 256 fp32), then 32×128 = A · [W_self | W_neigh]ᵀ
+// runs as v_mfma_f32_32x32x2_f32: wave w owns output columns 32·(w&3) and K half (w>>2)
+// (W_self or W_neigh), i.e. 64 B operands per lane, re-read from L2 per tile by buffer
+// loads (held across the gather they would spill: 128 VGPRs is the budget at two 8-wave
+// blocks per CU) — the weights cross the CU once per 32 rows instead of once per 2.  Each
+// lane half h of an MFMA consumes k ∈ [64h, 64h+64) of its K half (a fixed permutation of
+// the summation order; vectorised ds_read_b128 of A).  The two K halves meet in LDS, then
+// each wave finishes 4 rows with the shared epilogue.  Two blocks per CU (≈ 67 KiB LDS
+// each; HIP's second launch-bounds argument is waves per SIMD), so one block's MFMA phase
+// runs under the other's gather.
+//
+// Measured (C5 bought-by, 10M rows × 10 edges, tools/probe_c5.py): 13.1 ms, vs 18.0 ms
+// for the VALU kernel and 7.6 + 7.1 ms for gather + GEMM launched back to back.  A
+// variant splitting the block into 8 gather waves and 8 MFMA waves (weights resident in
+// the MFMA waves' registers, one barrier per pipelined step) took 17–22 ms: its timing
+// builds put the gather side alone at 17.9 ms and the MFMA side alone at 7.4 ms — 8
+// gathering waves per CU cannot keep HBM busy at 10 edges per row.  So the sharded pass,
+// which can run the GEMM on a second stream under the next relation's HBM-bound gather,
+// keeps gather + GEMM for such relations; this kernel serves the module path
+// (nn.ConvLayer), where the two would run back to back.
+#ifndef GNNREC_SPM_U
+#define GNNREC_SPM_U 4  // gather wave-instructions in flight per lane
+#endif
+constexpr int kMT = 32;                  // rows per tile
+constexpr int kMWaves = 8;               // waves per block
+constexpr int kMRows = kMT / kMWaves;    // rows gathered per wave per tile
+constexpr int kALd = 2 * kPD + 4;        // A tile row stride (floats): conflict-free b128 reads
+constexpr int kCLd = kPD + 8;            // C tile row stride: the two lane halves' stores
+                                         // land on disjoint banks
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int REDUCE, bool WEIGHTED, int UNROLL>
+__global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx,
+    const float* __restrict__ H, int64_t ldh, const float* __restrict__ WsT,
+    const float* __restrict__ WnT, const float* __restrict__ bias,
+    const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
+    const float* __restrict__ attn_vec, float* __restrict__ attn_state,
+    float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
+  __shared__ float As[kMT * kALd];
+  __shared__ float Cs[2][kMT * kCLd];
+  __shared__ int nes[kMT];
+  __shared__ int64_t blk_r[2];
+
+  constexpr int LPR = 32, VEC = 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = lane / LPR;
+  const int li = lane & 31, bh = lane >> 5;
+  const int col = li * VEC;
+  const int j0 = 2 * lane;
+  const int cb = wave & 3, kh = wave >> 2;
+  const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
+  const bool attn = accum >= GNNREC_ACC_ATTN_FIRST;
+  const float a0 = attn ? attn_vec[j0] : 0.f, a1 = attn ? attn_vec[j0 + 1] : 0.f;
+  const EpiArgs ep{(epilogue & GNNREC_EPI_RELU) != 0, (epilogue & GNNREC_EPI_L2NORM) != 0,
+                   attn, accum, out_div, a0, a1, attn_state, out, ldo, j0};
+
+  // B operands: lane supplies Wᵀ[k][n], k = 64·bh + i of this wave's K half, n = 32·cb + li.
+  // Buffer loads: one 32-bit per-lane offset plus an immediate row offset, instead of 64
+  // hoisted 64-bit addresses (which the compiler spills)
+  const float* WTb = kh ? WnT : WsT;
+  const uint64_t wbase = ((uint64_t)__builtin_amdgcn_readfirstlane(
+                              (unsigned)((uintptr_t)WTb >> 32)) << 32) |
+                         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)WTb);
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wbase), 0,
+                                                       kPD * kPD * 4, 0x00020000);
+  const int wvoff = ((64 * bh) * kPD + 32 * cb + li) * 4;
+
+  // one tile: rows [t0, min(t0 + kMT, lim)); every wave of the block takes part
+  auto tile = [&](int64_t t0, int64_t lim) __attribute__((always_inline)) {
+    const int64_t rbase = t0 + wave * kMRows;
+    const int64_t left = lim - rbase;
+    const int nv = (int)(left <= 0 ? 0 : left < kMRows ? left : kMRows);
+    // the 4 rows' bounds in one load; each row's first 64 indices are requested before
+    // the previous row gathers, the self rows (two per instruction) a row pair ahead
+    // (nv == 0: rows past the range end — nothing is read, the tile rows stay zero)
+    const int64_t ipl = nv > 0 && lane <= nv ? indptr[rbase + lane] : 0;
+    auto bound = [&](int r) { return __shfl(ipl, r <= nv ? r : nv); };
+    auto first_idx = [&](int r) {
+      const int64_t b = bound(r), e = bound(r + 1);
+      return r < nv && lane < e - b ? indices[b + lane] : 0;
+    };
+    auto self_rows = [&](int q) {  // lanes of half bh: self row 2q + bh
+      const int rl = 2 * q + bh;
+      return rl < nv ? *reinterpret_cast<const float4*>(H + (rbase + rl) * ldh + col)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    int pidx = first_idx(0);
+    float4 hs = self_rows(0);
+#pragma unroll
+    for (int r = 0; r < kMRows; ++r) {
+      const int pnext = r + 1 < kMRows ? first_idx(r + 1) : 0;
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = init;
+      int64_t deg = 0;
+      if (r < nv) {
+        const int64_t beg = bound(r), end = bound(r + 1);
+        deg = end - beg;
+        gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(beg, end, indices, ew, X, ldx,
+                                                               col, true, lane, grp, acc, pidx);
+      }
+      combine_groups<LPR, VEC, REDUCE>(acc);
+      finalize<VEC, REDUCE>(acc, deg, 0);
+      const int rl = wave * kMRows + r;
+      if (grp == 0)
+        *reinterpret_cast<float4*>(&As[rl * kALd + kPD + col]) =
+            make_float4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
+      if (lane == 0) nes[rl] = deg > 0;
+      if (r % 2 == 0) {  // the self-row pair of rows r, r+1 has landed: park it
+        *reinterpret_cast<float4*>(&As[(wave * kMRows + r + bh) * kALd + col]) = hs;
+        if (r + 2 < kMRows) hs = self_rows(r / 2 + 1);
+      }
+      pidx = pnext;
+    }
+    __syncthreads();
+
+    // C_kh[32 × 32 block cb] = A[:, K half kh] · Wᵀ[K half kh, block cb]
+    float bw[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+      bw[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wrsrc, wvoff, i * kPD * 4, 0));
+    f32x16 c;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) c[v] = 0.f;
+    const float* ap = As + li * kALd + kh * kPD + 64 * bh;
+#pragma unroll
+    for (int i = 0; i < 64; i += 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(ap + i);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], bw[i], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], bw[i + 1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], bw[i + 2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], bw[i + 3], c, 0, 0, 0);
+    }
+    // D map of the 32x32 MFMA: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 h
+    float* cp = Cs[kh] + 32 * cb + li;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) cp[((v & 3) + 8 * (v >> 2) + 4 * bh) * kCLd] = c[v];
+    __syncthreads();
+
+#pragma unroll
+    for (int r = 0; r < kMRows; ++r) {
+      const int rl = wave * kMRows + r;
+      const float2 s2 = *reinterpret_cast<const float2*>(&Cs[0][rl * kCLd + j0]);
+      const float2 n2 = *reinterpret_cast<const float2*>(&Cs[1][rl * kCLd + j0]);
+      float z0 = s2.x + n2.x, z1 = s2.y + n2.y;
+      if (bias) {
+        z0 = bias[j0] + z0;
+        z1 = bias[j0 + 1] + z1;
+      }
+      if (bias_ne && nes[rl]) {
+        z0 = bias_ne[j0] + z0;
+        z1 = bias_ne[j0 + 1] + z1;
+      }
+      epilogue_row(ep, rbase + r, r < nv, z0, z1);
+    }
+    __syncthreads();  // As / Cs / nes free for the next tile
+  };
+
+  // chunks of rows come from the queue (blocks that start late, behind another kernel,
+  // take fewer) or, statically, one tile at a time from this block's XCD's contiguous
+  // eighth of the tiles (blocks are dispatched round-robin over the 8, so each XCD's L2
+  // sees contiguous indptr / H / out rows); wave 0 draws and publishes each chunk, and
+  // the whole block processes it — one call site of the tile body
+  RqCursor cur;
+  if (rq != nullptr && wave == 0) rq_begin(cur, rq);
+  const int64_t tiles = (n_dst + kMT - 1) / kMT;
+  const int xcd = blockIdx.x % kRqHeads;
+  const int64_t per = (int64_t)(gridDim.x - xcd + kRqHeads - 1) / kRqHeads;  // blocks on xcd
+  int64_t st = tiles * xcd / kRqHeads + blockIdx.x / kRqHeads;
+  const int64_t st_hi = tiles * (xcd + 1) / kRqHeads;
+  while (true) {
+    if (wave == 0) {
+      int64_t r0 = -1, r1 = 0;
+      if (rq != nullptr) {
+        if (!rq_next(cur, rq, n_dst, rq_ch, r0, r1)) r0 = -1;
+      } else if (st < st_hi) {
+        r0 = st * kMT;
+        r1 = r0 + kMT < n_dst ? r0 + kMT : n_dst;
+        st += per;
+      }
+      if (lane == 0) {
+        blk_r[0] = r0;
+        blk_r[1] = r1;
+      }
+    }
+    __syncthreads();
+    const int64_t r0 = blk_r[0], r1 = blk_r[1];
+    if (r0 < 0) break;
+    for (int64_t t0 = r0; t0 < r1; t0 += kMT) tile(t0, r1);  // ends with a barrier
+  }
+  if (rq != nullptr) rq_finish(rq);
 }
 
 }  // namespace
@@ -298,4 +521,65 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
 #undef GNNREC_SPP_ONE
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_project_f32");
+}
+
+extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t* indices,
+                                            const float* ew, const float* X, int64_t ldx,
+                                            const float* H, int64_t ldh, const float* W_selfT,
+                                            const float* W_neighT, const float* bias,
+                                            const float* bias_nonempty, int64_t n_dst,
+                                            int64_t d, int reduce, int epilogue, int accum,
+                                            float out_div, const float* attn_vec,
+                                            float* attn_state, float* out, int64_t ldo,
+                                            void* stream) {
+  GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project_mfma_f32: only d = %d (got %lld)", kPD,
+                 (long long)d);
+  GNNREC_REQUIRE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN ||
+                     reduce == GNNREC_REDUCE_MAX,
+                 "gnnrec_spmm_project_mfma_f32: unknown reduce %d", reduce);
+  GNNREC_REQUIRE((epilogue & ~(GNNREC_EPI_RELU | GNNREC_EPI_L2NORM)) == 0,
+                 "gnnrec_spmm_project_mfma_f32: epilogue must be RELU|L2NORM");
+  GNNREC_REQUIRE(accum >= GNNREC_ACC_STORE && accum <= GNNREC_ACC_ATTN_LAST,
+                 "gnnrec_spmm_project_mfma_f32: unknown accumulate mode %d", accum);
+  GNNREC_REQUIRE(accum < GNNREC_ACC_ATTN_FIRST || (attn_vec && attn_state),
+                 "gnnrec_spmm_project_mfma_f32: attention accumulation needs attn_vec, "
+                 "attn_state");
+  GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project_mfma_f32: negative n_dst");
+  if (n_dst == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(indptr && X && H && W_selfT && W_neighT && out,
+                 "gnnrec_spmm_project_mfma_f32: null pointer");
+  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(W_selfT) && aligned16(W_neighT) &&
+                     ldx % 4 == 0 && ldh % 4 == 0 && ldo % 2 == 0 &&
+                     (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
+                 "gnnrec_spmm_project_mfma_f32: X/H/W need 16-B aligned rows, out 8-B");
+  // two persistent 8-wave blocks per CU, minus the CUs reserved for concurrent kernels
+  const int64_t tiles = (n_dst + kMT - 1) / kMT;
+  const int64_t cus = device_cus() - cu_reserve();
+  int64_t blocks = 2 * (cus > 8 ? cus : 8);
+  if (blocks > tiles) blocks = tiles;
+  static const int rq_ch = [] {  // rows per queue ticket (whole tiles)
+    const char* e = getenv("GNNREC_RQ_CHUNK_MFMA");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 16 ? x * kMT : 2 * kMT;
+  }();
+  hipStream_t s = as_stream(stream);
+  int ticket = -1;
+  unsigned* rq = n_dst >= blocks * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
+  const dim3 grid((unsigned)blocks), block(kMWaves * 64);
+#define GNNREC_SPM(R, W)                                                                      \
+  hipLaunchKernelGGL((spmm_project_mfma_kernel<R, W, GNNREC_SPM_U>), grid, block, 0, s, indptr, \
+                     indices, ew, X, ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty,       \
+                     n_dst, epilogue, accum, out_div, attn_vec, attn_state, out, ldo, rq, rq_ch)
+  if (ew) {
+    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, true);
+    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, true);
+    else GNNREC_SPM(GNNREC_REDUCE_MAX, true);
+  } else {
+    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, false);
+    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, false);
+    else GNNREC_SPM(GNNREC_REDUCE_MAX, false);
+  }
+#undef GNNREC_SPM
+  rowq_launched(ticket, s);
+  return check_launch("gnnrec_spmm_project_mfma_f32");
 }

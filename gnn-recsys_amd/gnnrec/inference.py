@@ -588,7 +588,7 @@ class ShardedFullGraphPass:
             avg = (rs.global_edges / max(sh.num_nodes[T], 1)) if self.deterministic else None
             if reduce != 'lstm' and can_fuse is not None and can_fuse(
                     rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight,
-                    avg_deg=avg):
+                    avg_deg=avg, gemm_overlaps=self.side is not None):
                 # aggregation and projection in one launch on the main stream: the self rows
                 # must be ready here (they may come from the side stream)
                 self_rows = self._get(h, T)
@@ -600,11 +600,12 @@ class ShardedFullGraphPass:
                                     device=msg.device)
                     akw = self._attn(hconv, T, sh.n_own, o.device)
                 Ws, Wn, bias, bias_ne = self._folded(mod, ce)
-                with self._time('spmm_project'):
+                vkw = {} if avg is None else {'avg_deg': avg}  # same kernel on every rank
+                with self._time(self._fused_tag(rs, avg)):
                     O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                    rs.weights if weighted else None, relu=True,
                                    l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,
-                                   bias=bias, bias_nonempty=bias_ne, **akw)
+                                   bias=bias, bias_nonempty=bias_ne, **akw, **vkw)
                 self.fused.add(ce)
                 continue
             with self._time('spmm'):
@@ -629,6 +630,12 @@ class ShardedFullGraphPass:
         out[T] = o
         if ev is not None:
             self._ready[id(o)] = ev
+
+    def _fused_tag(self, rs, avg):
+        """timer tag of a fused launch: 'spmm_project' (VALU kernel) or 'spmm_project_mfma'."""
+        fv = getattr(self.ops, 'fused_variant', None)
+        return 'spmm_project_mfma' if fv is not None and fv(rs.indptr, avg) == 'mfma' \
+            else 'spmm_project'
 
     @staticmethod
     def _local_deg(rs):
@@ -657,7 +664,7 @@ class ShardedFullGraphPass:
                         o = torch.empty((self_rows.shape[0], mod._out_feats),
                                         dtype=torch.float32, device=msg.device)
                     Ws, Wn, bias, bias_ne = self._folded(mod, ce)
-                    with self._time('spmm_project'):
+                    with self._time(self._fused_tag(rs, None)):
                         O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                        rs.weights if weighted else None, relu=True,
                                        l2norm=bool(mod.norm), accum=acc, out_div=div, out=o,

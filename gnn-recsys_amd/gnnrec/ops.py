@@ -437,10 +437,14 @@ GEMM_ROW_N = 256  # widest output row gnnrec_gemm_f32 normalises / attends in on
 
 
 def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT,
-                     avg_deg: Optional[float] = None) -> bool:
-    """True when the fused aggregation+projection kernel applies (shapes, alignment, no
+                     avg_deg: Optional[float] = None, gemm_overlaps: bool = False) -> bool:
+    """True when a fused aggregation+projection kernel applies (shapes, alignment, no
     heavy rows, GPU tensors; GNNREC_FUSED=0 disables it).  avg_deg: edges per row to judge
-    the degree threshold by (default: this CSR's own)."""
+    the degree threshold by (default: this CSR's own).  gemm_overlaps: the caller can run
+    an unfused projection GEMM on a second stream under other HBM-bound work (the sharded
+    pass) — then low-degree CSRs, whose fused kernel is the MFMA one, stay unfused: the
+    overlapped GEMM costs less than the MFMA kernel's extra time over the bare gather
+    (C5 bought-by: 13.1 ms fused vs 7.6 ms gather + a 7.1 ms GEMM on the side stream)."""
     if os.environ.get("GNNREC_FUSED", "1") == "0":
         return False
     D = FUSED_D
@@ -456,16 +460,32 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
             return False
     if split and split_plan(indptr, split) is not None:
         return False
-    # the in-kernel projection reads both weight matrices from LDS once per 2 rows
-    # (64 KiB/row): below ~24 edges per row that LDS traffic, not the gather, bounds the
-    # launch (C5 bought-by, 10 edges/row: fused 20.3 ms vs spmm 8.1 + GEMM 7.7 ms)
-    if avg_deg is not None:
-        return avg_deg >= FUSED_MIN_DEG
-    n = indptr.numel() - 1
-    return n == 0 or _nnz(indptr) >= FUSED_MIN_DEG * n
+    # below FUSED_MIN_DEG edges per row the VALU kernel's per-row weight reads bound it and
+    # the MFMA variant takes the relation (C5 bought-by, 10 edges/row: VALU-fused 18.0 ms,
+    # MFMA-fused 13.1 ms, spmm 7.6 + GEMM 7.1 ms back to back); GNNREC_FUSED_MFMA=0 keeps
+    # aggregation + GEMM there
+    if os.environ.get("GNNREC_FUSED_MFMA", "1") == "0" or gemm_overlaps:
+        return fused_variant(indptr, avg_deg) == "valu"
+    return True
 
 
 FUSED_MIN_DEG = 24
+
+
+def fused_variant(indptr, avg_deg: Optional[float] = None) -> str:
+    """'valu' (gnnrec_spmm_project_f32: weights in LDS, read once per 2 rows — bound by
+    the gather from FUSED_MIN_DEG edges per row up) or 'mfma' (gnnrec_spmm_project_mfma_f32:
+    32-row tiles through fp32 MFMA, weights read once per 32 rows — low degrees).  avg_deg:
+    the edges per row to decide by (the sharded pass passes the GLOBAL average so every
+    rank picks the same kernel); default this CSR's own.  GNNREC_FUSED_VARIANT=valu|mfma
+    forces one (tuning, tests)."""
+    forced = os.environ.get("GNNREC_FUSED_VARIANT", "auto")
+    if forced in ("valu", "mfma"):
+        return forced
+    if avg_deg is None:
+        n = indptr.numel() - 1
+        avg_deg = _nnz(indptr) / n if n else float(FUSED_MIN_DEG)
+    return "valu" if avg_deg >= FUSED_MIN_DEG else "mfma"
 
 
 def _nnz(indptr: torch.Tensor) -> int:
@@ -486,9 +506,12 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                  out: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
                  bias_nonempty: Optional[torch.Tensor] = None,
                  attn_vec: Optional[torch.Tensor] = None,
-                 attn_state: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 attn_state: Optional[torch.Tensor] = None,
+                 avg_deg: Optional[float] = None, variant: Optional[str] = None) -> torch.Tensor:
     """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ + bias
-    + [deg > 0]·bias_nonempty), d = 128."""
+    + [deg > 0]·bias_nonempty), d = 128.  variant 'valu' | 'mfma' (default: fused_variant
+    of avg_deg) picks the kernel; both give the same aggregate bits, the projection's
+    fp32 summation order differs."""
     lib = _lib.load()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
@@ -522,7 +545,11 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
     bias_nonempty = None if bias_nonempty is None else bias_nonempty.detach().contiguous()
     av, ast = _attn_args(accum, attn_vec, attn_state, n_dst, D)
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
-    check(lib.gnnrec_spmm_project_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
+    variant = variant or fused_variant(indptr, avg_deg)
+    if variant not in ("valu", "mfma"):
+        raise ValueError(f"spmm_project variant must be 'valu' or 'mfma', not {variant!r}")
+    fn = lib.gnnrec_spmm_project_mfma_f32 if variant == "mfma" else lib.gnnrec_spmm_project_f32
+    check(fn(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
                                       _rowmajor(X, "X"), ptr(H), _rowmajor(H, "H"), ptr(WsT),
                                       ptr(WnT), ptr(bias), ptr(bias_nonempty), n_dst,
                                       X.shape[1], REDUCE[reduce], epi,

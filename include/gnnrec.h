@@ -212,6 +212,19 @@ int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices, const
                             int epilogue, int accum, float out_div, const float* attn_vec,
                             float* attn_state, float* out, int64_t ldo, void* stream);
 
+/* The same operation with the projection on the MFMA, for low-degree CSRs (callers
+ * pick it below ~24 edges per row): 32-row tiles, [h_self | agg] staged in LDS and
+ * multiplied by the register-resident weights with v_mfma_f32_32x32x2_f32, so the
+ * weights are read once per 32 rows.  Same arguments, contract and aggregate bits as
+ * gnnrec_spmm_project_f32; the projection's summation order differs (fp32 rounding). */
+int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t* indices,
+                                 const float* ew, const float* X, int64_t ldx, const float* H,
+                                 int64_t ldh, const float* W_selfT, const float* W_neighT,
+                                 const float* bias, const float* bias_nonempty, int64_t n_dst,
+                                 int64_t d, int reduce, int epilogue, int accum, float out_div,
+                                 const float* attn_vec, float* attn_state, float* out,
+                                 int64_t ldo, void* stream);
+
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >
  * Replaces CosinePrediction.forward, src/model.py:317-327. */

@@ -65,12 +65,16 @@ def test_spmm_queue_bitwise(static_mode, d, reduce, weighted, hold):
     assert torch.equal(ref, out)
 
 
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
 @pytest.mark.parametrize("accum", ["store", "add", "attn"])
 @pytest.mark.parametrize("hold", [False, True])
-def test_spmm_project_queue_bitwise(static_mode, accum, hold):
+def test_spmm_project_queue_bitwise(static_mode, accum, hold, variant):
+    """(mfma: whole 32-row tiles per ticket, drawn by one wave for the block.)  Row counts
+    large enough for the launch to take the queue at 16 reserved CUs (VALU: ≥ 240 blocks ×
+    16 waves × 8-row tickets × 4; MFMA: ≥ 480 blocks × 64-row tickets × 4)."""
     from gnnrec import ops
-    n_dst, n_src, d = 120_000, 30_000, 128
-    indptr, indices = _csr(n_dst, n_src, 40, 2)
+    n_dst, n_src, d = (200_000, 30_000, 128) if variant == "valu" else (300_000, 30_000, 128)
+    indptr, indices = _csr(n_dst, n_src, 40 if variant == "valu" else 16, 2)
     X = torch.randn(n_src, d, device="cuda")
     H = torch.randn(n_dst, d, device="cuda")
     Ws, Wn = torch.randn(d, d, device="cuda") * 0.1, torch.randn(d, d, device="cuda") * 0.1
@@ -84,9 +88,11 @@ def test_spmm_project_queue_bitwise(static_mode, accum, hold):
         if accum == "attn":
             kw = {"attn_vec": av, "attn_state": st0.clone()}
         ops.spmm_project(indptr, indices, X, H, Ws, Wn, "mean", relu=True, l2norm=True,
-                         accum=accum, out=o, **kw)
+                         accum=accum, out=o, variant=variant, **kw)
         return o
+    q0, _ = ops.rowq_stats()
     ref, out = _both(run, hold)
+    assert ops.rowq_stats()[0] > q0  # the concurrent launch did take the queue
     assert torch.equal(ref, out)
 
 

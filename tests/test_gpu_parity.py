@@ -662,10 +662,13 @@ def test_lstm_layer_matches_torch_lstm_and_trains():
 
 
 # ------------------------------------------- a1+a3 fused aggregate + project ---
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
 @pytest.mark.parametrize("reduce", ["mean", "max", "sum"])
 @pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("epi", ["relu_norm", "relu"])
-def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
+def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi, variant):
+    """Both fused kernels (VALU matvec with LDS weights; 32-row tiles through fp32 MFMA)
+    against the oracle and the unfused path; 3001 rows: a ragged last MFMA tile."""
     from gnnrec import ops
     import zlib
     rng = np.random.default_rng(zlib.crc32(f"{reduce}{weighted}{epi}".encode()))
@@ -691,7 +694,7 @@ def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
     g = [_t(indptr), _t(indices.astype(np.int32)), _t(X), _t(H), _t(Ws), _t(Wn)]
     w = None if ew is None else _t(ew)
     assert ops.can_spmm_project(g[0], g[2], g[3], g[4], g[5])
-    got = ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2)
+    got = ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2, variant=variant)
     # unnormalised sums over 700-edge rows reach |z| ~ 1e2: fp32 cancellation in a
     # 256-term dot product is relative to that scale, not to the (small) result
     atol = ATOL * max(1.0, float(np.abs(ref).max()))
@@ -702,10 +705,12 @@ def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi):
     unf = ops.gemm(g[3], g[4], a, g[5], relu=True, l2norm=l2)
     np.testing.assert_allclose(got.cpu().numpy(), unf.cpu().numpy(), rtol=RTOL, atol=atol)
     # deterministic
-    assert torch.equal(ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2), got)
+    assert torch.equal(ops.spmm_project(*g, reduce, w, relu=True, l2norm=l2, variant=variant),
+                       got)
 
 
-def test_spmm_project_accumulate_modes_and_strides():
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
+def test_spmm_project_accumulate_modes_and_strides(variant):
     from gnnrec import ops
     rng = np.random.default_rng(77)
     n_dst, n_src, d = 500, 400, 128
@@ -723,7 +728,8 @@ def test_spmm_project_accumulate_modes_and_strides():
     for mode, fn in (("add", lambda o: o + z), ("max", lambda o: np.maximum(o, z))):
         out = _t(base)[:, :d]
         ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), Xt, _t(H), _t(Ws), _t(Wn),
-                         "mean", None, relu=True, l2norm=True, accum=mode, out_div=2.0, out=out)
+                         "mean", None, relu=True, l2norm=True, accum=mode, out_div=2.0, out=out,
+                         variant=variant)
         np.testing.assert_allclose(out.cpu().numpy(), fn(base[:, :d]) / 2.0, rtol=RTOL, atol=ATOL)
 
 
@@ -865,17 +871,60 @@ def test_gather_rows_any_dtype_and_stride():
     assert ops.gather_rows(cases[0], idx[:0]).shape == (0, 128)
 
 
-def test_fused_dispatch_skips_low_degree_csr():
-    """Below FUSED_MIN_DEG edges per row the in-kernel projection is LDS-bound: such CSRs
-    take the aggregation + GEMM path."""
+def test_fused_dispatch_picks_mfma_below_min_degree(monkeypatch):
+    """Below FUSED_MIN_DEG edges per row the VALU kernel's per-row LDS weight reads bound
+    it: such CSRs take the MFMA variant (GNNREC_FUSED_MFMA=0: aggregation + GEMM)."""
     from gnnrec import ops
     d = 128
     X, H = torch.zeros(10, d, device=DEV), torch.zeros(100, d, device=DEV)
     W = torch.zeros(d, d, device=DEV)
     sparse = torch.arange(0, 1001, 10, device=DEV)        # 100 rows x 10 edges
     dense = torch.arange(0, 100 * 30 + 1, 30, device=DEV)  # 100 rows x 30 edges
+    assert ops.can_spmm_project(sparse, X, H, W, W)
+    assert ops.can_spmm_project(dense, X, H, W, W)
+    assert ops.fused_variant(sparse) == "mfma" and ops.fused_variant(dense) == "valu"
+    assert ops.fused_variant(dense, avg_deg=10.0) == "mfma"  # the global average decides
+    monkeypatch.setenv("GNNREC_FUSED_MFMA", "0")
     assert not ops.can_spmm_project(sparse, X, H, W, W)
     assert ops.can_spmm_project(dense, X, H, W, W)
+
+
+@pytest.mark.parametrize("deg", [4, 10, 16])
+def test_c5_scale_low_degree_fused_mfma_vs_oracle(deg):
+    """A C5 bought-by-shaped relation (10M user rows, `deg` edges each from a 1M-row item
+    table, d=128) through the MFMA fused kernel: 1000 sampled rows against the oracle,
+    bitwise run-to-run, and the VALU kernel agreeing within fp32 rounding."""
+    from gnnrec import ops
+    from gnnrec.graph import build_csr
+    n_u, n_i, d = 10_000_000, 1_000_000, 128
+    E = n_u * deg
+    u, i = ops.synth_edges(13, 0, E, n_u, n_i, DEV)
+    indptr, idx, _ = build_csr(i.long(), u.long(), n_u)
+    del u, i
+    assert ops.fused_variant(indptr) == "mfma"
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(deg)
+    X = torch.randn(n_i, d, device=DEV, generator=gen)
+    H = torch.randn(n_u, d, device=DEV, generator=gen)
+    Ws = torch.randn(d, d, device=DEV, generator=gen) * 0.08
+    Wn = torch.randn(d, d, device=DEV, generator=gen) * 0.08
+    a = ops.spmm_project(indptr, idx, X, H, Ws, Wn, "mean", None, relu=True, l2norm=True)
+    assert torch.equal(a, ops.spmm_project(indptr, idx, X, H, Ws, Wn, "mean", None, relu=True,
+                                           l2norm=True))
+    rows = torch.cat([torch.arange(0, 40, device=DEV), torch.arange(n_u - 40, n_u, device=DEV),
+                      torch.randint(0, n_u, (920,), device=DEV, generator=gen)])
+    sub_ip, sub_idx = _sub_csr(indptr, idx, rows)
+    agg = oracle.spmm_csr(sub_ip, sub_idx, X.cpu().numpy(), "mean")
+    ref = oracle.l2_normalize_rows_guarded(oracle.relu(
+        oracle.linear(H[rows].cpu().numpy(), Ws.cpu().numpy()) +
+        oracle.linear(agg, Wn.cpu().numpy())))
+    np.testing.assert_allclose(a[rows].cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    v = ops.spmm_project(indptr, idx, X, H, Ws, Wn, "mean", None, relu=True, l2norm=True,
+                         variant="valu")
+    np.testing.assert_allclose(a.cpu().numpy()[::997], v.cpu().numpy()[::997], rtol=RTOL,
+                               atol=ATOL)
+    del indptr, idx, X, H, a, v
+    torch.cuda.empty_cache()
 
 
 def _sub_csr(indptr, idx, rows):

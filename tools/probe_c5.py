@@ -36,14 +36,22 @@ def main():
         n = rs.indptr.numel() - 1
         deg = (rs.indptr[1:] - rs.indptr[:-1])
         out = torch.empty(n, d, device=dev)
-        ms = t(lambda: ops.spmm_project(rs.indptr, rs.indices, X[ce[0]], X[ce[2]][:n], W, W,
-                                        "mean", None, relu=True, l2norm=True, out=out))
-        ms2 = t(lambda: ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean"))
         E = int(rs.indptr[-1])
-        print(f"{ce}: rows {n} edges {E} deg max {int(deg.max())} mean {E / n:.1f} "
-              f"fused {ms:.2f} ms ({E * 516 / ms / 1e9:.2f} TB/s) spmm {ms2:.2f} ms "
-              f"split_plan {'yes' if ops.split_plan(rs.indptr) is not None else 'no'}",
-              flush=True)
+        res = {}
+        for v in ("valu", "mfma"):
+            res[v] = t(lambda: ops.spmm_project(rs.indptr, rs.indices, X[ce[0]], X[ce[2]][:n], W,
+                                                W, "mean", None, relu=True, l2norm=True, out=out,
+                                                variant=v))
+        agg = ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean")
+        res["spmm"] = t(lambda: ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean", out=agg))
+        res["gemm"] = t(lambda: ops.gemm(X[ce[2]][:n], W, agg, W, relu=True, l2norm=True,
+                                         out=out))
+        alg = E * 516 + n * 1032  # fused: per edge row + index, per row indptr + self + out
+        print(f"{ce}: rows {n} edges {E} deg max {int(deg.max())} mean {E / n:.1f} | "
+              + " ".join(f"{k} {ms:.2f} ms" for k, ms in res.items())
+              + f" | fused valu {alg / res['valu'] / 1e9:.2f} TB/s, mfma "
+              f"{alg / res['mfma'] / 1e9:.2f} TB/s (algorithmic) | split_plan "
+              f"{'yes' if ops.split_plan(rs.indptr) is not None else 'no'}", flush=True)
 
 
 if __name__ == "__main__":
