@@ -512,19 +512,30 @@ __global__ __launch_bounds__(256, (BN > 128 ? 1 : GEMM_WAVES_PER_SIMD)) void gem
 // rows a 16-lane ds_read_b128 group touches map to 16 distinct 4-bank slots.
 constexpr int BK16 = 16;
 
-template <int BN>
+//
+// S stages (S−1 tiles in flight while one is consumed): a 16-deep tile is only 2048 MFMA
+// cycles per wave, shorter than an HBM round trip, so with two stages each block waited
+// on its DMA about as long as it computed (MFMA busy ≈56 % at M=1M, K=256, N=128).
+template <int BN, int S>
 constexpr int glds16_smem_floats() {
-  return 2 * (BM + BN) * BK16 > smem_floats<BN>() ? 2 * (BM + BN) * BK16 : smem_floats<BN>();
+  return S * (BM + BN) * BK16 > smem_floats<BN>() ? S * (BM + BN) * BK16 : smem_floats<BN>();
 }
 
-template <int BN>
-__global__ __launch_bounds__(256, 3) void gemm_f32_glds16_kernel(GemmArgs g) {
+// waves per SIMD the S-stage kernel is built for: LDS allows 3 blocks per CU up to 3 stages
+template <int S>
+constexpr int glds16_waves() {
+  return S <= 3 ? 3 : 2;
+}
+
+template <int BN, int S>
+__global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel(GemmArgs g) {
   constexpr int NT = BN / 32;
   constexpr int AI = BM * BK16 * 4 / 1024 / 4;   // A-tile DMA instructions per wave (2)
   constexpr int WI = BN * BK16 * 4 / 1024 / 4;   // W-tile DMA instructions per wave (BN/64)
   constexpr int TILE = (BM + BN) * BK16;
   static_assert(WI >= 1, "BN >= 64");
-  __shared__ __attribute__((aligned(16))) float smem[glds16_smem_floats<BN>()];
+  static_assert(S >= 2 && S <= 4, "stages");
+  __shared__ __attribute__((aligned(16))) float smem[glds16_smem_floats<BN, S>()];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -584,36 +595,45 @@ __global__ __launch_bounds__(256, 3) void gemm_f32_glds16_kernel(GemmArgs g) {
     for (int q = 0; q < WI; ++q)
       dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK16 + (wave * WI + q) * 256);
   };
-  if (nk > 0) issue(0, 0);
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j)
+    if (j < nk) issue(j, j);
 #pragma unroll 1
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) {
-      issue(kt + 1, buf ^ 1);
-      wait_vmcnt_barrier<AI + WI>();  // this wave's tile-kt DMA landed; all waves past it
-    } else {
-      wait_vmcnt_barrier<0>();
-    }
+    const int buf = kt % S;
+    if (kt + S - 1 < nk) issue(kt + S - 1, (kt + S - 1) % S);
+    // this wave's tile-kt DMA landed (the younger tiles may still fly); all waves past it
+    const int ahead = nk - 1 - kt < S - 1 ? nk - 1 - kt : S - 1;
+    if (ahead >= 3) wait_vmcnt_barrier<3 * (AI + WI)>();
+    else if (ahead == 2) wait_vmcnt_barrier<2 * (AI + WI)>();
+    else if (ahead == 1) wait_vmcnt_barrier<AI + WI>();
+    else wait_vmcnt_barrier<0>();
     const bool s2 = kt >= nk1;
     const bool divide = s2 && g.a2_mode == GNNREC_A2_DIV_DEG;
     const bool zero = s2 && rowzero2;
     const float* As = smem + buf * TILE + (wave * 32 + r) * BK16;
     const float* Ws = smem + buf * TILE + BM * BK16 + r * BK16;
+    // both halves' fragments are requested before the first MFMA: the second half's LDS
+    // latency hides under the first half's 16 MFMAs (one lgkmcnt wait per half, not a
+    // full drain before each)
+    f32x4 a[2], b[2][NT];
 #pragma unroll
     for (int s4 = 0; s4 < 2; ++s4) {
       const int pc = ((h * 2 + s4) ^ sw) * 4;
-      f32x4 a = *reinterpret_cast<const f32x4*>(As + pc);
-      if (divide) a = a / rowdiv2;
-      else if (zero) a = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 b[NT];
+      a[s4] = *reinterpret_cast<const f32x4*>(As + pc);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        b[t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK16 + pc);
+        b[s4][t] = *reinterpret_cast<const f32x4*>(Ws + t * 32 * BK16 + pc);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 2; ++s4) {
+      if (divide) a[s4] = a[s4] / rowdiv2;
+      else if (zero) a[s4] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[t][s], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s4][s], b[s4][t][s], acc[t], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
   }
@@ -639,7 +659,14 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
     const bool fast16 = g.vecA1 && g.vecW1 && g.K1 % BK16 == 0 &&
                         (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK16 == 0));
     if (fast16 && use_dma && use_bk16) {
-      hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN>), grid, dim3(256), 0, s, g);
+      static const int stages = [] {  // GNNREC_GEMM_STAGES: tuning knob
+        const char* e = getenv("GNNREC_GEMM_STAGES");
+        const int x = e ? atoi(e) : 3;
+        return x >= 2 && x <= 4 ? x : 3;
+      }();
+      if (stages == 2) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 2>), grid, dim3(256), 0, s, g);
+      else if (stages == 4) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 4>), grid, dim3(256), 0, s, g);
+      else hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3>), grid, dim3(256), 0, s, g);
       return check_launch("gnnrec_gemm_f32");
     }
   }
