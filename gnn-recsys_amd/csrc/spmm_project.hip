@@ -424,10 +424,14 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
   RqCursor cur;
   if (rq != nullptr && wave == 0) rq_begin(cur, rq);
   const int64_t tiles = (n_dst + kMT - 1) / kMT;
-  const int xcd = blockIdx.x % kRqHeads;
-  const int64_t per = (int64_t)(gridDim.x - xcd + kRqHeads - 1) / kRqHeads;  // blocks on xcd
-  int64_t st = tiles * xcd / kRqHeads + blockIdx.x / kRqHeads;
-  const int64_t st_hi = tiles * (xcd + 1) / kRqHeads;
+  // a grid of fewer than 8 blocks (small relations) leaves some XCDs without a block: then
+  // a plain block-strided walk, so no eighth of the tiles is left without an owner
+  const bool by_xcd = gridDim.x >= (unsigned)kRqHeads;
+  const int xcd = by_xcd ? blockIdx.x % kRqHeads : 0;
+  const int64_t per = by_xcd ? (int64_t)(gridDim.x - xcd + kRqHeads - 1) / kRqHeads  // blocks on xcd
+                             : (int64_t)gridDim.x;
+  int64_t st = by_xcd ? tiles * xcd / kRqHeads + blockIdx.x / kRqHeads : (int64_t)blockIdx.x;
+  const int64_t st_hi = by_xcd ? tiles * (xcd + 1) / kRqHeads : tiles;
   while (true) {
     if (wave == 0) {
       int64_t r0 = -1, r1 = 0;

@@ -1,0 +1,858 @@
+// torch_ops.cpp — TORCH_LIBRARY(gnnrec) over the C ABI of libgnnrec.so (include/gnnrec.h).
+//
+// Every op is a thin, validated wrapper of one C-ABI entry point: device pointers and the
+// current HIP stream of the operand's device in, the library's status out (GNNREC_EINVAL
+// -> ValueError, anything else -> RuntimeError with gnnrec_last_error()).  Outputs are
+// preallocated by the caller and declared mutable in the schema (Tensor(a!)), the same
+// contract as the C ABI, so torch.compile functionalises them (auto_functionalize).  The
+// Meta kernel of each op is the same function: on meta /
+// fake tensors it runs the shape checks and returns before the launch, which is all that
+// shape inference of an op with mutated outputs needs.
+//
+// Reference call sites these ops serve (the nn.Module drop-ins in gnnrec/nn.py):
+//   spmm_csr*, spmm_project, gemm   <- ConvLayer.forward src/model.py:143-208,226-235
+//   sddmm_cos                       <- CosinePrediction.forward src/model.py:317-327
+//   edge_mlp                        <- PredictingModule.forward src/model.py:290-305
+//   sample_*, scan, relabel ops     <- dgl samplers / to_block, src/sampling.py:153-161
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gnnrec.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+void ck(int rc, const char* what) {
+  if (rc == GNNREC_OK) return;
+  const char* msg = gnnrec_last_error();
+  TORCH_CHECK_VALUE(rc != GNNREC_EINVAL, what, ": ", msg);
+  TORCH_CHECK(false, what, ": ", msg, " (status ", rc, ")");
+}
+
+void* stream_of(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+// device operand (or meta/fake during tracing) of the given dtype
+void dev(const Tensor& t, const char* name, c10::ScalarType dt) {
+  TORCH_CHECK_VALUE(t.is_cuda() || t.is_meta(), name,
+                    " must be a HIP device tensor (gnnrec has no CPU path), got ", t.device());
+  TORCH_CHECK_VALUE(t.scalar_type() == dt, name, " must be ", dt, ", got ", t.scalar_type());
+}
+void dev(const optional<Tensor>& t, const char* name, c10::ScalarType dt) {
+  if (t.has_value() && t->defined()) dev(*t, name, dt);
+}
+
+bool has(const optional<Tensor>& t) { return t.has_value() && t->defined(); }
+
+template <typename T>
+T* p(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+T* p(const optional<Tensor>& t) { return has(t) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
+
+// leading dimension of a 2-D row-major operand (unit column stride)
+int64_t ld(const Tensor& t, const char* name) {
+  TORCH_CHECK_VALUE(t.dim() == 2, name, " must be 2-D, got ", t.sizes());
+  TORCH_CHECK_VALUE(t.stride(1) == 1 || t.size(1) <= 1, name, " must have unit column stride");
+  return std::max<int64_t>({t.stride(0), t.size(1), 1});
+}
+
+bool meta(const Tensor& t) { return t.is_meta(); }
+
+// ---------------------------------------------------------------- a1 aggregation
+void spmm_csr(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+              const Tensor& X, int64_t reduce, int64_t flags, Tensor& out) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(X, "X", at::kFloat);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t n_dst = indptr.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d,
+                    "], got ", out.sizes());
+  const int64_t ldx = ld(X, "X"), ldo = ld(out, "out");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew), p<float>(X), ldx,
+                         n_dst, d, (int)reduce, (int)flags, p<float>(out), ldo, stream_of(X)),
+     "gnnrec_spmm_csr_f32");
+}
+
+void spmm_csr_split(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+                    const Tensor& X, int64_t reduce, int64_t flags, int64_t split,
+                    const Tensor& heavy, const Tensor& chunk_ptr, const Tensor& chunk_row,
+                    int64_t n_chunks, Tensor& out, Tensor& ws) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(X, "X", at::kFloat);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(heavy, "heavy_rows", at::kLong);
+  dev(chunk_ptr, "chunk_ptr", at::kLong);
+  dev(chunk_row, "chunk_row", at::kLong);
+  dev(out, "out", at::kFloat);
+  dev(ws, "workspace", at::kFloat);
+  const int64_t n_dst = indptr.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d, "]");
+  TORCH_CHECK_VALUE(ws.numel() >= n_chunks * d, "workspace must hold n_chunks x d floats");
+  const int64_t ldx = ld(X, "X"), ldo = ld(out, "out");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  ck(gnnrec_spmm_csr_split_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew), p<float>(X),
+                               ldx, n_dst, d, (int)reduce, (int)flags, p<float>(out), ldo, split,
+                               p<int64_t>(heavy), heavy.numel(), p<int64_t>(chunk_ptr),
+                               p<int64_t>(chunk_row), n_chunks, p<float>(ws), stream_of(X)),
+     "gnnrec_spmm_csr_split_f32");
+}
+
+void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor& plan) {
+  dev(indptr, "indptr", at::kLong);
+  dev(plan, "plan", at::kLong);
+  if (meta(indptr)) return;
+  const c10::DeviceGuard g(indptr.device());
+  ck(gnnrec_spmm_plan_build(p<int64_t>(indptr), indptr.numel() - 1, split, cap_h,
+                            p<int64_t>(plan), stream_of(indptr)),
+     "gnnrec_spmm_plan_build");
+}
+
+void spmm_csr_planned(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+                      const Tensor& X, int64_t reduce, int64_t flags, int64_t split,
+                      const Tensor& plan, int64_t cap_h, int64_t cap_c, Tensor& out, Tensor& ws) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(X, "X", at::kFloat);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(plan, "plan", at::kLong);
+  dev(out, "out", at::kFloat);
+  dev(ws, "workspace", at::kFloat);
+  const int64_t n_dst = indptr.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d, "]");
+  TORCH_CHECK_VALUE(ws.numel() >= cap_c * d, "workspace must hold cap_c x d floats");
+  const int64_t ldx = ld(X, "X"), ldo = ld(out, "out");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew),
+                                 p<float>(X), ldx, n_dst, d, (int)reduce, (int)flags,
+                                 p<float>(out), ldo, split, p<int64_t>(plan), cap_h, cap_c,
+                                 p<float>(ws), stream_of(X)),
+     "gnnrec_spmm_csr_planned_f32");
+}
+
+void spmm_backward(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+                   const Tensor& grad_out, const optional<Tensor>& X,
+                   const optional<Tensor>& out, int64_t reduce, Tensor& grad_X) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(grad_out, "grad_out", at::kFloat);
+  dev(X, "X", at::kFloat);
+  dev(out, "out", at::kFloat);
+  dev(grad_X, "grad_X", at::kFloat);
+  const int64_t n_dst = grad_out.size(0), d = grad_out.size(1);
+  const int64_t ldg = ld(grad_out, "grad_out"), ldgx = ld(grad_X, "grad_X");
+  const int64_t ldx = has(X) ? ld(*X, "X") : 0, ldo = has(out) ? ld(*out, "out") : 0;
+  if (meta(grad_out)) return;
+  const c10::DeviceGuard g(grad_out.device());
+  ck(gnnrec_spmm_backward_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew),
+                              p<float>(grad_out), ldg, p<float>(X), ldx, p<float>(out), ldo,
+                              n_dst, d, (int)reduce, p<float>(grad_X), ldgx, stream_of(grad_out)),
+     "gnnrec_spmm_backward_f32");
+}
+
+// ---------------------------------------------------------------- a2-a4 projections
+void gemm(const Tensor& A1, const Tensor& W1, const optional<Tensor>& A2,
+          const optional<Tensor>& W2, const optional<Tensor>& a2_deg, int64_t a2_mode,
+          const optional<Tensor>& bias, const optional<Tensor>& bias_nonempty, int64_t epilogue,
+          int64_t accum, double out_div, const optional<Tensor>& attn_vec,
+          const optional<Tensor>& attn_state, Tensor& out, const optional<Tensor>& row_norm) {
+  dev(A1, "A1", at::kFloat);
+  dev(W1, "W1", at::kFloat);
+  dev(A2, "A2", at::kFloat);
+  dev(W2, "W2", at::kFloat);
+  dev(a2_deg, "a2_deg", at::kInt);
+  dev(bias, "bias", at::kFloat);
+  dev(bias_nonempty, "bias_nonempty", at::kFloat);
+  dev(attn_vec, "attn_vec", at::kFloat);
+  dev(attn_state, "attn_state", at::kFloat);
+  dev(out, "out", at::kFloat);
+  dev(row_norm, "row_norm", at::kFloat);
+  const int64_t M = A1.size(0), K1 = A1.size(1), N = W1.size(0);
+  TORCH_CHECK_VALUE(W1.size(1) == K1 && W1.is_contiguous(), "W1 must be a contiguous [N, ", K1, "]");
+  const int64_t lda1 = ld(A1, "A1");
+  int64_t K2 = 0, lda2 = 1;
+  if (has(A2)) {
+    TORCH_CHECK_VALUE(has(W2) && A2->size(0) == M && W2->size(0) == N &&
+                          W2->size(1) == A2->size(1) && W2->is_contiguous(),
+                      "A2/W2 shape mismatch");
+    K2 = A2->size(1);
+    lda2 = ld(*A2, "A2");
+  }
+  TORCH_CHECK_VALUE(out.size(0) == M && out.size(1) == N, "out must be [", M, ", ", N, "]");
+  const int64_t ldo = ld(out, "out");
+  if (meta(A1)) return;
+  const c10::DeviceGuard g(A1.device());
+  ck(gnnrec_gemm_rownorm_f32(p<float>(A1), lda1, K1, p<float>(W1), p<float>(A2), lda2, K2,
+                             p<float>(W2), p<int32_t>(a2_deg), (int)a2_mode, p<float>(bias),
+                             p<float>(bias_nonempty), M, N, (int)epilogue, (int)accum,
+                             (float)out_div, p<float>(attn_vec), p<float>(attn_state),
+                             p<float>(out), ldo, p<float>(row_norm), stream_of(A1)),
+     "gnnrec_gemm_f32");
+}
+
+void row_epilogue(const Tensor& z, int64_t l2norm, int64_t accum, double out_div,
+                  const optional<Tensor>& attn_vec, const optional<Tensor>& attn_state,
+                  Tensor& out) {
+  dev(z, "z", at::kFloat);
+  dev(attn_vec, "attn_vec", at::kFloat);
+  dev(attn_state, "attn_state", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t M = z.size(0), N = z.size(1);
+  TORCH_CHECK_VALUE(out.size(0) == M && out.size(1) == N, "out must be [", M, ", ", N, "]");
+  const int64_t ldz = ld(z, "z"), ldo = ld(out, "out");
+  if (meta(z)) return;
+  const c10::DeviceGuard g(z.device());
+  ck(gnnrec_row_epilogue_f32(p<float>(z), ldz, M, N, (int)l2norm, (int)accum, (float)out_div,
+                             p<float>(attn_vec), p<float>(attn_state), p<float>(out), ldo,
+                             stream_of(z)),
+     "gnnrec_row_epilogue_f32");
+}
+
+void spmm_project(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+                  const Tensor& X, const Tensor& H, const Tensor& W_selfT, const Tensor& W_neighT,
+                  const optional<Tensor>& bias, const optional<Tensor>& bias_nonempty,
+                  int64_t reduce, int64_t epilogue, int64_t accum, double out_div,
+                  const optional<Tensor>& attn_vec, const optional<Tensor>& attn_state,
+                  bool mfma, Tensor& out) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(X, "X", at::kFloat);
+  dev(H, "H", at::kFloat);
+  dev(W_selfT, "W_selfT", at::kFloat);
+  dev(W_neighT, "W_neighT", at::kFloat);
+  dev(bias, "bias", at::kFloat);
+  dev(bias_nonempty, "bias_nonempty", at::kFloat);
+  dev(attn_vec, "attn_vec", at::kFloat);
+  dev(attn_state, "attn_state", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t n_dst = indptr.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(H.size(0) >= n_dst, "H has ", H.size(0), " rows, the CSR ", n_dst,
+                    " destinations");
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d, "]");
+  TORCH_CHECK_VALUE(W_selfT.is_contiguous() && W_neighT.is_contiguous(),
+                    "transposed weights must be contiguous");
+  const int64_t ldx = ld(X, "X"), ldh = ld(H, "H"), ldo = ld(out, "out");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  auto fn = mfma ? gnnrec_spmm_project_mfma_f32 : gnnrec_spmm_project_f32;
+  ck(fn(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew), p<float>(X), ldx, p<float>(H), ldh,
+        p<float>(W_selfT), p<float>(W_neighT), p<float>(bias), p<float>(bias_nonempty), n_dst, d,
+        (int)reduce, (int)epilogue, (int)accum, (float)out_div, p<float>(attn_vec),
+        p<float>(attn_state), p<float>(out), ldo, stream_of(X)),
+     mfma ? "gnnrec_spmm_project_mfma_f32" : "gnnrec_spmm_project_f32");
+}
+
+// ---------------------------------------------------------------- a7 / a8 heads
+void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
+               Tensor& out) {
+  dev(src, "src", at::kLong);
+  dev(dst, "dst", at::kLong);
+  dev(Hs, "Hs", at::kFloat);
+  dev(Hd, "Hd", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t E = src.numel();
+  TORCH_CHECK_VALUE(dst.numel() == E && out.numel() == E, "src/dst/out length mismatch");
+  TORCH_CHECK_VALUE(Hs.size(1) == Hd.size(1), "endpoint feature sizes differ");
+  TORCH_CHECK_VALUE(src.is_contiguous() && dst.is_contiguous(), "src/dst must be contiguous");
+  const int64_t lds = ld(Hs, "Hs"), ldd = ld(Hd, "Hd");
+  if (meta(Hs)) return;
+  const c10::DeviceGuard g(Hs.device());
+  ck(gnnrec_sddmm_cos_f32(p<int64_t>(src), p<int64_t>(dst), E, p<float>(Hs), lds, p<float>(Hd),
+                          ldd, Hs.size(1), p<float>(out), stream_of(Hs)),
+     "gnnrec_sddmm_cos_f32");
+}
+
+void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
+                        const Tensor& grad, const optional<Tensor>& gHs,
+                        const optional<Tensor>& gHd, Tensor& ws) {
+  dev(src, "src", at::kLong);
+  dev(dst, "dst", at::kLong);
+  dev(Hs, "Hs", at::kFloat);
+  dev(Hd, "Hd", at::kFloat);
+  dev(grad, "grad", at::kFloat);
+  dev(gHs, "gHs", at::kFloat);
+  dev(gHd, "gHd", at::kFloat);
+  const int64_t E = src.numel(), d = Hs.size(1);
+  TORCH_CHECK_VALUE(dst.numel() == E && grad.numel() == E, "src/dst/grad length mismatch");
+  TORCH_CHECK_VALUE(Hd.size(1) == d, "endpoint feature sizes differ");
+  const int64_t lds = ld(Hs, "Hs"), ldd = ld(Hd, "Hd");
+  if (meta(Hs)) return;
+  const c10::DeviceGuard g(Hs.device());
+  ck(gnnrec_sddmm_cos_backward_f32(p<int64_t>(src), p<int64_t>(dst), E, p<float>(Hs), lds,
+                                   Hs.size(0), p<float>(Hd), ldd, Hd.size(0), d, p<float>(grad),
+                                   p<float>(gHs), p<float>(gHd), ws.data_ptr(), ws.nbytes(),
+                                   stream_of(Hs)),
+     "gnnrec_sddmm_cos_backward_f32");
+}
+
+void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tensor& Q,
+              const Tensor& W2, const Tensor& b2, const Tensor& w3, const Tensor& b3,
+              Tensor& out) {
+  dev(src, "src", at::kLong);
+  dev(dst, "dst", at::kLong);
+  for (auto* t : {&P, &Q, &W2, &b2, &w3, &b3}) dev(*t, "edge_mlp operand", at::kFloat);
+  dev(out, "out", at::kFloat);
+  TORCH_CHECK_VALUE(P.size(1) == 128 && Q.size(1) == 128 && W2.size(0) == 32 && W2.size(1) == 128,
+                    "edge_mlp expects the reference's 128/32 hidden sizes");
+  TORCH_CHECK_VALUE(P.is_contiguous() && Q.is_contiguous() && W2.is_contiguous(),
+                    "edge_mlp operands must be contiguous");
+  const int64_t E = src.numel();
+  TORCH_CHECK_VALUE(dst.numel() == E && out.numel() == E, "src/dst/out length mismatch");
+  if (meta(P)) return;
+  const c10::DeviceGuard g(P.device());
+  ck(gnnrec_edge_mlp_f32(p<int64_t>(src), p<int64_t>(dst), E, p<float>(P), p<float>(Q),
+                         p<float>(W2), p<float>(b2), p<float>(w3), p<float>(b3), p<float>(out),
+                         stream_of(P)),
+     "gnnrec_edge_mlp_f32");
+}
+
+// ---------------------------------------------------------------- a9 sampler / relabel
+void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tensor>& excluded,
+                  const Tensor& seeds, int64_t fanout, int64_t seed_key, Tensor& counts) {
+  dev(indptr, "indptr", at::kLong);
+  dev(eids, "eids", at::kLong);
+  dev(excluded, "excluded", at::kByte);
+  dev(seeds, "seeds", at::kLong);
+  dev(counts, "counts", at::kLong);
+  TORCH_CHECK_VALUE(counts.numel() >= seeds.numel(), "counts shorter than seeds");
+  if (meta(seeds)) return;
+  const c10::DeviceGuard g(seeds.device());
+  ck(gnnrec_sample_count(p<int64_t>(indptr), p<int64_t>(eids), p<uint8_t>(excluded),
+                         p<int64_t>(seeds), seeds.numel(), fanout, (uint64_t)seed_key,
+                         p<int64_t>(counts), stream_of(seeds)),
+     "gnnrec_sample_count");
+}
+
+void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids,
+                 const optional<Tensor>& excluded, const Tensor& seeds, int64_t fanout,
+                 int64_t seed_key, const Tensor& out_indptr, Tensor& out_src, Tensor& out_eid) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(eids, "eids", at::kLong);
+  dev(excluded, "excluded", at::kByte);
+  dev(seeds, "seeds", at::kLong);
+  dev(out_indptr, "out_indptr", at::kLong);
+  dev(out_src, "out_src", at::kLong);
+  dev(out_eid, "out_eid", at::kLong);
+  TORCH_CHECK_VALUE(out_indptr.numel() >= seeds.numel() + 1, "out_indptr shorter than seeds + 1");
+  if (meta(seeds)) return;
+  const c10::DeviceGuard g(seeds.device());
+  ck(gnnrec_sample_fill(p<int64_t>(indptr), p<int32_t>(indices), p<int64_t>(eids),
+                        p<uint8_t>(excluded), p<int64_t>(seeds), seeds.numel(), fanout,
+                        (uint64_t)seed_key, p<int64_t>(out_indptr), p<int64_t>(out_src),
+                        p<int64_t>(out_eid), stream_of(seeds)),
+     "gnnrec_sample_fill");
+}
+
+void exclusive_scan(const Tensor& x, Tensor& out, Tensor& ws) {
+  dev(out, "out", at::kLong);
+  TORCH_CHECK_VALUE(x.is_cuda() || x.is_meta(), "x must be a HIP device tensor");
+  TORCH_CHECK_VALUE(x.scalar_type() == at::kLong || x.scalar_type() == at::kInt,
+                    "exclusive_scan supports int32/int64");
+  TORCH_CHECK_VALUE(x.is_contiguous() && out.numel() == x.numel() + 1,
+                    "exclusive_scan: contiguous x [n] and out [n+1]");
+  if (meta(x)) return;
+  const c10::DeviceGuard g(x.device());
+  if (x.scalar_type() == at::kLong)
+    ck(gnnrec_exclusive_scan_i64(p<int64_t>(x), x.numel(), p<int64_t>(out), ws.data_ptr(),
+                                 stream_of(x)),
+       "gnnrec_exclusive_scan_i64");
+  else
+    ck(gnnrec_exclusive_scan_i32(p<int32_t>(x), x.numel(), p<int64_t>(out), ws.data_ptr(),
+                                 stream_of(x)),
+       "gnnrec_exclusive_scan_i32");
+}
+
+void mark_ids(const Tensor& ids, const Tensor& prefix_pos, Tensor& mark) {
+  dev(ids, "ids", at::kLong);
+  dev(prefix_pos, "prefix_pos", at::kLong);
+  dev(mark, "mark", at::kInt);
+  if (meta(ids)) return;
+  const c10::DeviceGuard g(ids.device());
+  ck(gnnrec_mark_ids(p<int64_t>(ids), ids.numel(), p<int64_t>(prefix_pos), p<int32_t>(mark),
+                     stream_of(ids)),
+     "gnnrec_mark_ids");
+}
+
+void relabel_ids(const Tensor& ids, const Tensor& prefix_pos, const Tensor& rank, int64_t n_prefix,
+                 Tensor& local) {
+  dev(ids, "ids", at::kLong);
+  dev(prefix_pos, "prefix_pos", at::kLong);
+  dev(rank, "rank", at::kLong);
+  dev(local, "local", at::kLong);
+  TORCH_CHECK_VALUE(local.numel() >= ids.numel(), "local shorter than ids");
+  if (meta(ids)) return;
+  const c10::DeviceGuard g(ids.device());
+  ck(gnnrec_relabel_ids(p<int64_t>(ids), ids.numel(), p<int64_t>(prefix_pos), p<int64_t>(rank),
+                        n_prefix, p<int64_t>(local), stream_of(ids)),
+     "gnnrec_relabel_ids");
+}
+
+void compact_marked(const Tensor& mark, const Tensor& rank, Tensor& out_ids) {
+  dev(mark, "mark", at::kInt);
+  dev(rank, "rank", at::kLong);
+  dev(out_ids, "out_ids", at::kLong);
+  if (meta(mark)) return;
+  const c10::DeviceGuard g(mark.device());
+  ck(gnnrec_compact_marked(p<int32_t>(mark), p<int64_t>(rank), mark.numel(), p<int64_t>(out_ids),
+                           stream_of(mark)),
+     "gnnrec_compact_marked");
+}
+
+void set_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
+  dev(prefix, "prefix", at::kLong);
+  dev(prefix_pos, "prefix_pos", at::kLong);
+  if (meta(prefix)) return;
+  const c10::DeviceGuard g(prefix.device());
+  ck(gnnrec_set_prefix_pos(p<int64_t>(prefix), prefix.numel(), p<int64_t>(prefix_pos),
+                           stream_of(prefix)),
+     "gnnrec_set_prefix_pos");
+}
+
+void clear_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
+  dev(prefix, "prefix", at::kLong);
+  dev(prefix_pos, "prefix_pos", at::kLong);
+  if (meta(prefix)) return;
+  const c10::DeviceGuard g(prefix.device());
+  ck(gnnrec_clear_prefix_pos(p<int64_t>(prefix), prefix.numel(), p<int64_t>(prefix_pos),
+                             stream_of(prefix)),
+     "gnnrec_clear_prefix_pos");
+}
+
+// ---------------------------------------------------------------- f1 top-k
+void topk_rows(const Tensor& scores, int64_t k, const optional<Tensor>& exclude_indptr,
+               const optional<Tensor>& exclude_indices, Tensor& out_vals, Tensor& out_idx) {
+  dev(scores, "scores", at::kFloat);
+  dev(exclude_indptr, "exclude_indptr", at::kLong);
+  dev(exclude_indices, "exclude_indices", at::kLong);
+  dev(out_vals, "out_vals", at::kFloat);
+  dev(out_idx, "out_idx", at::kLong);
+  const int64_t n_rows = scores.size(0), n_cols = scores.size(1);
+  TORCH_CHECK_VALUE(out_vals.numel() == n_rows * k && out_idx.numel() == n_rows * k,
+                    "out_vals / out_idx must be [n_rows, k]");
+  const int64_t lds = ld(scores, "scores");
+  if (meta(scores)) return;
+  const c10::DeviceGuard g(scores.device());
+  ck(gnnrec_topk_rows_f32(p<float>(scores), lds, n_rows, n_cols, k, p<int64_t>(exclude_indptr),
+                          p<int64_t>(exclude_indices), p<float>(out_vals), p<int64_t>(out_idx),
+                          stream_of(scores)),
+     "gnnrec_topk_rows_f32");
+}
+
+// ---------------------------------------------------------------- f2 training
+void gemm_tn(const Tensor& A, const Tensor& B, const optional<Tensor>& colsum, bool accumulate,
+             Tensor& out, Tensor& ws) {
+  dev(A, "A", at::kFloat);
+  dev(B, "B", at::kFloat);
+  dev(colsum, "colsum", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
+  TORCH_CHECK_VALUE(B.size(0) == K, "gemm_tn: A and B differ in K");
+  TORCH_CHECK_VALUE(out.size(0) == M && out.size(1) == N, "out must be [", M, ", ", N, "]");
+  const int64_t lda = ld(A, "A"), ldb = ld(B, "B"), ldc = ld(out, "out");
+  if (meta(A)) return;
+  const c10::DeviceGuard g(A.device());
+  ck(gnnrec_gemm_tn_bias_f32(p<float>(A), lda, p<float>(B), ldb, K, M, N, p<float>(out), ldc,
+                             p<float>(colsum), (int)accumulate, p<float>(ws), stream_of(A)),
+     "gnnrec_gemm_tn_bias_f32");
+}
+
+void act_backward(const Tensor& u, const Tensor& gz, int64_t flags, Tensor& out) {
+  dev(u, "u", at::kFloat);
+  dev(gz, "gz", at::kFloat);
+  dev(out, "out", at::kFloat);
+  TORCH_CHECK_VALUE(u.sizes() == gz.sizes() && u.sizes() == out.sizes(),
+                    "act_backward: u / gz / out shapes differ");
+  const int64_t ldu = ld(u, "u"), ldg = ld(gz, "gz"), ldo = ld(out, "out");
+  if (meta(u)) return;
+  const c10::DeviceGuard g(u.device());
+  ck(gnnrec_act_backward_f32(p<float>(u), ldu, p<float>(gz), ldg, u.size(0), u.size(1),
+                             (int)flags, p<float>(out), ldo, stream_of(u)),
+     "gnnrec_act_backward_f32");
+}
+
+void act_backward_normed(const Tensor& z, const Tensor& row_norm, const Tensor& gz, bool relu,
+                         Tensor& out) {
+  dev(z, "z", at::kFloat);
+  dev(row_norm, "row_norm", at::kFloat);
+  dev(gz, "gz", at::kFloat);
+  dev(out, "out", at::kFloat);
+  TORCH_CHECK_VALUE(z.sizes() == gz.sizes() && z.sizes() == out.sizes() &&
+                        row_norm.numel() == z.size(0) && row_norm.is_contiguous(),
+                    "act_backward_normed: shape mismatch");
+  const int64_t ldz = ld(z, "z"), ldg = ld(gz, "gz"), ldo = ld(out, "out");
+  if (meta(z)) return;
+  const c10::DeviceGuard g(z.device());
+  ck(gnnrec_act_backward_normed_f32(p<float>(z), ldz, p<float>(row_norm), p<float>(gz), ldg,
+                                    z.size(0), z.size(1), (int)relu, p<float>(out), ldo,
+                                    stream_of(z)),
+     "gnnrec_act_backward_normed_f32");
+}
+
+void csr_transpose(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
+                   int64_t n_src, int64_t n_edges, bool mean, Tensor& ws, Tensor& indptr_t,
+                   Tensor& indices_t, const optional<Tensor>& ew_t) {
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(ew, "edge_weight", at::kFloat);
+  dev(indptr_t, "indptr_t", at::kLong);
+  dev(indices_t, "indices_t", at::kInt);
+  dev(ew_t, "ew_t", at::kFloat);
+  TORCH_CHECK_VALUE(indices.numel() >= n_edges, "csr_transpose: indices shorter than the edge count");
+  TORCH_CHECK_VALUE(indptr_t.numel() == n_src + 1 && indices_t.numel() >= n_edges,
+                    "csr_transpose: output sizes");
+  if (meta(indptr)) return;
+  const c10::DeviceGuard g(indptr.device());
+  ck(gnnrec_csr_transpose(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew),
+                          indptr.numel() - 1, n_src, n_edges, (int)mean, ws.data_ptr(), ws.nbytes(),
+                          p<int64_t>(indptr_t), p<int32_t>(indices_t), p<float>(ew_t),
+                          stream_of(indptr)),
+     "gnnrec_csr_transpose");
+}
+
+void csr_from_keys(const Tensor& keys, int64_t n_rows, Tensor& ws, Tensor& indptr, Tensor& perm) {
+  dev(keys, "keys", at::kInt);
+  dev(indptr, "indptr", at::kLong);
+  dev(perm, "perm", at::kInt);
+  TORCH_CHECK_VALUE(keys.is_contiguous() && indptr.numel() == n_rows + 1 &&
+                        perm.numel() == keys.numel(),
+                    "csr_from_keys: output sizes");
+  if (meta(keys)) return;
+  const c10::DeviceGuard g(keys.device());
+  ck(gnnrec_csr_from_keys(p<int32_t>(keys), keys.numel(), n_rows, ws.data_ptr(), ws.nbytes(),
+                          p<int64_t>(indptr), p<int32_t>(perm), stream_of(keys)),
+     "gnnrec_csr_from_keys");
+}
+
+// ---------------------------------------------------------------- f3 graph construction
+void csr_build(const Tensor& src, const Tensor& dst, int64_t n_dst, Tensor& ws, Tensor& indptr,
+               Tensor& indices, Tensor& eids) {
+  dev(src, "src", at::kLong);
+  dev(dst, "dst", at::kLong);
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(eids, "eids", at::kLong);
+  const int64_t E = dst.numel();
+  TORCH_CHECK_VALUE(src.numel() == E && src.is_contiguous() && dst.is_contiguous(),
+                    "csr_build: src and dst must be contiguous 1-D tensors of one length");
+  TORCH_CHECK_VALUE(indptr.numel() == n_dst + 1 && indices.numel() == E && eids.numel() == E,
+                    "csr_build: output sizes");
+  if (meta(dst)) return;
+  const c10::DeviceGuard g(dst.device());
+  ck(gnnrec_csr_build(p<int64_t>(src), p<int64_t>(dst), E, n_dst, ws.data_ptr(), ws.nbytes(),
+                      p<int64_t>(indptr), p<int32_t>(indices), p<int64_t>(eids), stream_of(dst)),
+     "gnnrec_csr_build");
+}
+
+// ---------------------------------------------------------------- sharded-pass helpers
+void add_(Tensor& a, const Tensor& b) {
+  dev(a, "a", at::kFloat);
+  dev(b, "b", at::kFloat);
+  TORCH_CHECK_VALUE(a.sizes() == b.sizes() && a.is_contiguous() && b.is_contiguous(),
+                    "add_: operands must be contiguous and of one shape");
+  if (meta(a)) return;
+  const c10::DeviceGuard g(a.device());
+  ck(gnnrec_add_f32(p<float>(a), p<float>(b), p<float>(a), a.numel(), stream_of(a)),
+     "gnnrec_add_f32");
+}
+
+void tree_sum_(Tensor& a, at::TensorList rest) {
+  dev(a, "part", at::kFloat);
+  const int n = (int)rest.size() + 1;
+  TORCH_CHECK_VALUE(n == 2 || n == 4 || n == 8, "tree_sum_: 2, 4 or 8 tables");
+  TORCH_CHECK_VALUE(a.is_contiguous(), "tree_sum_: operands must be contiguous");
+  for (const Tensor& t : rest) {
+    dev(t, "part", at::kFloat);
+    TORCH_CHECK_VALUE(t.sizes() == a.sizes() && t.is_contiguous(),
+                      "tree_sum_: operands must be contiguous and of one shape");
+  }
+  if (meta(a)) return;
+  std::vector<const float*> parts{p<float>(a)};
+  for (const Tensor& t : rest) parts.push_back(p<float>(t));
+  const c10::DeviceGuard g(a.device());
+  ck(gnnrec_tree_sum_f32(parts.data(), n, a.numel(), p<float>(a), stream_of(a)),
+     "gnnrec_tree_sum_f32");
+}
+
+// ---------------------------------------------------------------- f4 LSTM reducer
+void lstm_step(const Tensor& P, const Tensor& indptr, const Tensor& indices, const Tensor& order,
+               int64_t t, int64_t n_act, const Tensor& h_in, Tensor& h_out, Tensor& c,
+               const Tensor& W_hhT, Tensor& out) {
+  dev(P, "P", at::kFloat);
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(order, "order", at::kLong);
+  dev(h_in, "h_in", at::kFloat);
+  dev(h_out, "h_out", at::kFloat);
+  dev(c, "c", at::kFloat);
+  dev(W_hhT, "W_hhT", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t d = h_in.size(1);
+  TORCH_CHECK_VALUE(W_hhT.size(0) == d && W_hhT.size(1) == 4 * d && W_hhT.is_contiguous(),
+                    "W_hhT must be a contiguous [d, 4d]");
+  const int64_t ldp = ld(P, "P"), ldo = ld(out, "out");
+  if (meta(P)) return;
+  const c10::DeviceGuard g(P.device());
+  ck(gnnrec_lstm_step_f32(p<float>(P), ldp, p<int64_t>(indptr), p<int32_t>(indices),
+                          p<int64_t>(order), t, n_act, p<float>(h_in), p<float>(h_out),
+                          p<float>(c), d, p<float>(W_hhT), p<float>(out), ldo, stream_of(P)),
+     "gnnrec_lstm_step_f32");
+}
+
+// ---------------------------------------------------------------- a10 row gather
+void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
+  dev(idx, "idx", at::kLong);
+  TORCH_CHECK_VALUE(src.is_cuda() || src.is_meta(), "src: expected a device tensor (there is no CPU path)");
+  TORCH_CHECK_VALUE(src.dim() >= 1 && out.dim() == src.dim() && out.scalar_type() == src.scalar_type(),
+                    "gather_rows: out must match src's dtype and rank");
+  TORCH_CHECK_VALUE(idx.is_contiguous() && out.size(0) == idx.numel() && out.is_contiguous(),
+                    "gather_rows: contiguous idx [n] and out [n, ...]");
+  const int64_t es = src.element_size();
+  int64_t row_elems = 1;
+  for (int64_t k = 1; k < src.dim(); ++k) {
+    TORCH_CHECK_VALUE(out.size(k) == src.size(k), "gather_rows: row shapes differ");
+    row_elems *= src.size(k);
+  }
+  const int64_t row_bytes = es * row_elems;
+  if (meta(src)) return;
+  const c10::DeviceGuard g(src.device());
+  ck(gnnrec_gather_rows(src.data_ptr(), src.stride(0) * es, p<int64_t>(idx), idx.numel(),
+                        row_bytes, out.data_ptr(), row_bytes, stream_of(src)),
+     "gnnrec_gather_rows");
+}
+
+// ---------------------------------------------------------------- f2 loss
+void margin_loss(const Tensor& pos, const Tensor& neg, int64_t K, double delta,
+                 const optional<Tensor>& mask, const optional<Tensor>& recency, Tensor& g_pos,
+                 Tensor& g_neg, Tensor& partial) {
+  dev(pos, "pos_score", at::kFloat);
+  dev(neg, "neg_score", at::kFloat);
+  dev(mask, "negative_mask", at::kFloat);
+  dev(g_pos, "g_pos", at::kFloat);
+  dev(g_neg, "g_neg", at::kFloat);
+  dev(partial, "partial", at::kFloat);
+  const int64_t n_pos = pos.numel();
+  TORCH_CHECK_VALUE(neg.numel() == n_pos * K, "neg must hold n_pos x K scores");
+  TORCH_CHECK_VALUE(pos.is_contiguous() && neg.is_contiguous(), "scores must be contiguous");
+  int rec_i64 = 0;
+  if (has(recency)) {
+    TORCH_CHECK_VALUE(recency->scalar_type() == at::kLong || recency->scalar_type() == at::kFloat,
+                      "recency must be float32 or int64");
+    rec_i64 = recency->scalar_type() == at::kLong;
+  }
+  if (meta(pos)) return;
+  const c10::DeviceGuard g(pos.device());
+  ck(gnnrec_margin_loss_f32(p<float>(pos), p<float>(neg), n_pos, K, (float)delta, p<float>(mask),
+                            has(recency) ? recency->data_ptr() : nullptr, rec_i64, p<float>(g_pos),
+                            p<float>(g_neg), p<float>(partial), partial.numel(), stream_of(pos)),
+     "gnnrec_margin_loss_f32");
+}
+
+void sum_scaled(const Tensor& x, double scale, Tensor& out) {
+  dev(x, "x", at::kFloat);
+  dev(out, "out", at::kFloat);
+  if (meta(x)) return;
+  const c10::DeviceGuard g(x.device());
+  ck(gnnrec_sum_scaled_f32(p<float>(x), x.numel(), (float)scale, p<float>(out), stream_of(x)),
+     "gnnrec_sum_scaled_f32");
+}
+
+// ---------------------------------------------------------------- synthetic generator
+void synth_edges(int64_t seed, int64_t e0, int64_t n_u, int64_t n_i,
+                 const optional<Tensor>& zipf_cdf, Tensor& u, Tensor& i) {
+  dev(zipf_cdf, "zipf_cdf", at::kDouble);
+  dev(u, "u", at::kInt);
+  dev(i, "i", at::kInt);
+  TORCH_CHECK_VALUE(u.numel() == i.numel(), "u and i must have one length");
+  if (meta(u)) return;
+  const c10::DeviceGuard g(u.device());
+  ck(gnnrec_synth_edges((uint64_t)seed, e0, u.numel(), n_u, n_i, p<double>(zipf_cdf),
+                        p<int32_t>(u), p<int32_t>(i), stream_of(u)),
+     "gnnrec_synth_edges");
+}
+
+void hold_cus(int64_t blocks, int64_t threads, int64_t lds_bytes, int64_t usec, Tensor& sink) {
+  dev(sink, "sink", at::kFloat);
+  TORCH_CHECK_VALUE(sink.numel() >= threads, "sink must hold >= threads floats");
+  if (meta(sink)) return;
+  const c10::DeviceGuard g(sink.device());
+  ck(gnnrec_hold_cus((int)blocks, (int)threads, (int)lds_bytes, usec, p<float>(sink),
+                     stream_of(sink)),
+     "gnnrec_hold_cus");
+}
+
+// ---------------------------------------------------------------- host-only queries
+int64_t version() { return gnnrec_version(); }
+void set_concurrency(int64_t reserve_cus, bool dynamic) {
+  ck(gnnrec_set_concurrency((int)reserve_cus, (int)dynamic), "gnnrec_set_concurrency");
+}
+std::tuple<int64_t, int64_t> get_concurrency() {
+  int r = 0, d = 0;
+  ck(gnnrec_get_concurrency(&r, &d), "gnnrec_get_concurrency");
+  return {r, d};
+}
+std::tuple<int64_t, int64_t> rowq_stats() {
+  int64_t q = 0, b = 0;
+  ck(gnnrec_rowq_stats(&q, &b), "gnnrec_rowq_stats");
+  return {q, b};
+}
+int64_t scan_workspace_bytes(int64_t n) { return gnnrec_scan_workspace_bytes(n); }
+int64_t gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t N) {
+  return gnnrec_gemm_tn_workspace_bytes(K, M, N);
+}
+int64_t csr_transpose_workspace_bytes(int64_t E, int64_t n_src) {
+  return (int64_t)gnnrec_csr_transpose_workspace_bytes(E, n_src);
+}
+int64_t csr_from_keys_workspace_bytes(int64_t E, int64_t n_rows) {
+  return (int64_t)gnnrec_csr_from_keys_workspace_bytes(E, n_rows);
+}
+int64_t csr_build_workspace_bytes(int64_t E, int64_t n_dst) {
+  return (int64_t)gnnrec_csr_build_workspace_bytes(E, n_dst);
+}
+int64_t sddmm_cos_backward_workspace_bytes(int64_t E, int64_t n_src, int64_t n_dst, int64_t d) {
+  return (int64_t)gnnrec_sddmm_cos_backward_workspace_bytes(E, n_src, n_dst, d);
+}
+int64_t margin_loss_blocks(int64_t n_pos) { return gnnrec_margin_loss_blocks(n_pos); }
+
+}  // namespace
+
+// Schemas: mutated outputs are annotated (a!) so functionalisation knows what each op
+// writes; every launch op returns ().
+TORCH_LIBRARY(gnnrec, m) {
+  m.def("spmm_csr(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, int reduce, "
+        "int flags, Tensor(a!) out) -> ()");
+  m.def("spmm_csr_split(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, "
+        "int reduce, int flags, int split, Tensor heavy_rows, Tensor chunk_ptr, "
+        "Tensor chunk_row, int n_chunks, Tensor(a!) out, Tensor(b!) workspace) -> ()");
+  m.def("spmm_plan_build(Tensor indptr, int split, int cap_h, Tensor(a!) plan) -> ()");
+  m.def("spmm_csr_planned(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, "
+        "int reduce, int flags, int split, Tensor plan, int cap_h, int cap_c, Tensor(a!) out, "
+        "Tensor(b!) workspace) -> ()");
+  m.def("spmm_backward(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor grad_out, "
+        "Tensor? X, Tensor? out, int reduce, Tensor(a!) grad_X) -> ()");
+  m.def("gemm(Tensor A1, Tensor W1, Tensor? A2, Tensor? W2, Tensor? a2_deg, int a2_mode, "
+        "Tensor? bias, Tensor? bias_nonempty, int epilogue, int accum, float out_div, "
+        "Tensor? attn_vec, Tensor(b!)? attn_state, Tensor(a!) out, Tensor(c!)? row_norm) -> ()");
+  m.def("row_epilogue(Tensor z, int l2norm, int accum, float out_div, Tensor? attn_vec, "
+        "Tensor(b!)? attn_state, Tensor(a!) out) -> ()");
+  m.def("spmm_project(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, Tensor H, "
+        "Tensor W_selfT, Tensor W_neighT, Tensor? bias, Tensor? bias_nonempty, int reduce, "
+        "int epilogue, int accum, float out_div, Tensor? attn_vec, Tensor(b!)? attn_state, "
+        "bool mfma, Tensor(a!) out) -> ()");
+  m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
+  m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
+        "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");
+  m.def("edge_mlp(Tensor src, Tensor dst, Tensor P, Tensor Q, Tensor W2, Tensor b2, Tensor w3, "
+        "Tensor b3, Tensor(a!) out) -> ()");
+  m.def("sample_count(Tensor indptr, Tensor eids, Tensor? excluded, Tensor seeds, int fanout, "
+        "int seed_key, Tensor(a!) counts) -> ()");
+  m.def("sample_fill(Tensor indptr, Tensor indices, Tensor eids, Tensor? excluded, Tensor seeds, "
+        "int fanout, int seed_key, Tensor out_indptr, Tensor(a!) out_src, Tensor(b!) out_eid) -> ()");
+  m.def("exclusive_scan(Tensor x, Tensor(a!) out, Tensor(b!) workspace) -> ()");
+  m.def("mark_ids(Tensor ids, Tensor prefix_pos, Tensor(a!) mark) -> ()");
+  m.def("relabel_ids(Tensor ids, Tensor prefix_pos, Tensor rank, int n_prefix, "
+        "Tensor(a!) local) -> ()");
+  m.def("compact_marked(Tensor mark, Tensor rank, Tensor(a!) out_ids) -> ()");
+  m.def("set_prefix_pos(Tensor prefix, Tensor(a!) prefix_pos) -> ()");
+  m.def("clear_prefix_pos(Tensor prefix, Tensor(a!) prefix_pos) -> ()");
+  m.def("topk_rows(Tensor scores, int k, Tensor? exclude_indptr, Tensor? exclude_indices, "
+        "Tensor(a!) out_vals, Tensor(b!) out_idx) -> ()");
+  m.def("gemm_tn(Tensor A, Tensor B, Tensor(b!)? colsum, bool accumulate, Tensor(a!) out, "
+        "Tensor(c!) workspace) -> ()");
+  m.def("act_backward(Tensor u, Tensor gz, int flags, Tensor(a!) out) -> ()");
+  m.def("act_backward_normed(Tensor z, Tensor row_norm, Tensor gz, bool relu, "
+        "Tensor(a!) out) -> ()");
+  m.def("csr_transpose(Tensor indptr, Tensor indices, Tensor? edge_weight, int n_src, "
+        "int n_edges, bool mean, Tensor(a!) workspace, Tensor(b!) indptr_t, "
+        "Tensor(c!) indices_t, Tensor(d!)? ew_t) -> ()");
+  m.def("csr_from_keys(Tensor keys, int n_rows, Tensor(a!) workspace, Tensor(b!) indptr, "
+        "Tensor(c!) perm) -> ()");
+  m.def("csr_build(Tensor src, Tensor dst, int n_dst, Tensor(a!) workspace, Tensor(b!) indptr, "
+        "Tensor(c!) indices, Tensor(d!) eids) -> ()");
+  m.def("add_(Tensor(a!) a, Tensor b) -> ()");
+  m.def("tree_sum_(Tensor(a!) a, Tensor[] rest) -> ()");
+  m.def("lstm_step(Tensor P, Tensor indptr, Tensor indices, Tensor order, int t, int n_act, "
+        "Tensor h_in, Tensor(a!) h_out, Tensor(b!) c, Tensor W_hhT, Tensor(c!) out) -> ()");
+  m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("margin_loss(Tensor pos, Tensor neg, int K, float delta, Tensor? mask, Tensor? recency, "
+        "Tensor(a!) g_pos, Tensor(b!) g_neg, Tensor(c!) partial) -> ()");
+  m.def("sum_scaled(Tensor x, float scale, Tensor(a!) out) -> ()");
+  m.def("synth_edges(int seed, int e0, int n_u, int n_i, Tensor? zipf_cdf, Tensor(a!) u, "
+        "Tensor(b!) i) -> ()");
+  m.def("hold_cus(int blocks, int threads, int lds_bytes, int usec, Tensor(a!) sink) -> ()");
+  // host-only entry points (no tensors: one catch-all kernel each)
+  m.def("version() -> int", &version);
+  m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);
+  m.def("get_concurrency() -> (int, int)", &get_concurrency);
+  m.def("rowq_stats() -> (int, int)", &rowq_stats);
+  m.def("scan_workspace_bytes(int n) -> int", &scan_workspace_bytes);
+  m.def("gemm_tn_workspace_bytes(int K, int M, int N) -> int", &gemm_tn_workspace_bytes);
+  m.def("csr_transpose_workspace_bytes(int n_edges, int n_src) -> int",
+        &csr_transpose_workspace_bytes);
+  m.def("csr_from_keys_workspace_bytes(int n_edges, int n_rows) -> int",
+        &csr_from_keys_workspace_bytes);
+  m.def("csr_build_workspace_bytes(int n_edges, int n_dst) -> int", &csr_build_workspace_bytes);
+  m.def("sddmm_cos_backward_workspace_bytes(int n_edges, int n_src, int n_dst, int d) -> int",
+        &sddmm_cos_backward_workspace_bytes);
+  m.def("margin_loss_blocks(int n_pos) -> int", &margin_loss_blocks);
+}
+
+#define GNNREC_IMPLS(m)                                  \
+  m.impl("spmm_csr", &spmm_csr);                         \
+  m.impl("spmm_csr_split", &spmm_csr_split);             \
+  m.impl("spmm_plan_build", &spmm_plan_build);           \
+  m.impl("spmm_csr_planned", &spmm_csr_planned);         \
+  m.impl("spmm_backward", &spmm_backward);               \
+  m.impl("gemm", &gemm);                                 \
+  m.impl("row_epilogue", &row_epilogue);                 \
+  m.impl("spmm_project", &spmm_project);                 \
+  m.impl("sddmm_cos", &sddmm_cos);                       \
+  m.impl("sddmm_cos_backward", &sddmm_cos_backward);     \
+  m.impl("edge_mlp", &edge_mlp);                         \
+  m.impl("sample_count", &sample_count);                 \
+  m.impl("sample_fill", &sample_fill);                   \
+  m.impl("exclusive_scan", &exclusive_scan);             \
+  m.impl("mark_ids", &mark_ids);                         \
+  m.impl("relabel_ids", &relabel_ids);                   \
+  m.impl("compact_marked", &compact_marked);             \
+  m.impl("set_prefix_pos", &set_prefix_pos);             \
+  m.impl("clear_prefix_pos", &clear_prefix_pos);         \
+  m.impl("topk_rows", &topk_rows);                       \
+  m.impl("gemm_tn", &gemm_tn);                           \
+  m.impl("act_backward", &act_backward);                 \
+  m.impl("act_backward_normed", &act_backward_normed);   \
+  m.impl("csr_transpose", &csr_transpose);               \
+  m.impl("csr_from_keys", &csr_from_keys);               \
+  m.impl("csr_build", &csr_build);                       \
+  m.impl("add_", &add_);                                 \
+  m.impl("tree_sum_", &tree_sum_);                       \
+  m.impl("lstm_step", &lstm_step);                       \
+  m.impl("gather_rows", &gather_rows);                   \
+  m.impl("margin_loss", &margin_loss);                   \
+  m.impl("sum_scaled", &sum_scaled);                     \
+  m.impl("synth_edges", &synth_edges);                   \
+  m.impl("hold_cus", &hold_cus)
+
+// HIP tensors dispatch under the CUDA key in ROCm PyTorch.
+TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) { GNNREC_IMPLS(m); }
+// Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
+TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }
+// CPU tensors: the same functions refuse them in their first operand check (ValueError:
+// "must be a HIP device tensor") — there is no CPU path, and the error says so.
+TORCH_LIBRARY_IMPL(gnnrec, CPU, m) { GNNREC_IMPLS(m); }

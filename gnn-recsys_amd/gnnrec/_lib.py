@@ -135,9 +135,38 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+TORCH_LIB_PATH = os.environ.get("GNNREC_TORCH_LIB", os.path.join(_HERE, "libgnnrec_torch.so"))
+_ops = None
+
+
+def torch_ops():
+    """torch.ops.gnnrec: the TORCH_LIBRARY(gnnrec) registration (csrc/torch_ops.cpp) over
+    the C ABI, loaded after libgnnrec.so itself.  The product path launches every kernel
+    through it; ctypes (load()) stays the C-ABI test path.  GnnrecLibraryError if absent."""
+    global _ops
+    if _ops is not None:
+        return _ops
+    load()
+    if not os.path.exists(TORCH_LIB_PATH):
+        raise GnnrecLibraryError(f"libgnnrec_torch.so not found at {TORCH_LIB_PATH}; build it "
+                                 f"with `make -C gnn-recsys_amd/csrc`. There is no fallback path.")
+    try:
+        torch.ops.load_library(TORCH_LIB_PATH)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        raise GnnrecLibraryError(f"failed to load {TORCH_LIB_PATH}: {exc}") from exc
+    _ops = torch.ops.gnnrec
+    return _ops
+
+
+def i64(v: int) -> int:
+    """A 64-bit unsigned key (RNG seeds) as the signed int a torch schema `int` carries."""
+    v &= 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
 def available() -> bool:
     try:
-        load()
+        torch_ops()
         return True
     except GnnrecLibraryError:
         return False

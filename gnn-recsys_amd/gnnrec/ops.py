@@ -1,14 +1,15 @@
-"""Torch-facing wrappers over the gnnrec C ABI (include/gnnrec.h).
+"""Torch-facing wrappers over the gnnrec ops (include/gnnrec.h, registered with the torch
+dispatcher as torch.ops.gnnrec.* by csrc/torch_ops.cpp).
 
-Each function validates shapes/dtypes/devices on the host, allocates the output
-with torch (device memory plumbing only) and launches the HIP kernel on the
-current HIP stream.  There is no fallback: a missing library or a CPU tensor is
-an error.
+Each function validates shapes/dtypes/devices on the host, allocates the output with
+torch (device memory plumbing only) and launches the HIP kernel through its
+torch.ops.gnnrec op on the current HIP stream, so the launches are visible to the
+dispatcher, to torch.compile (meta kernels, functionalised outputs) and to HIP-graph
+capture.  There is no fallback: a missing library or a CPU tensor is an error.
 """
 from __future__ import annotations
 
 import contextlib
-import ctypes
 import os
 
 from typing import Optional
@@ -16,7 +17,11 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import check, ptr, stream_ptr
+
+
+def _T():
+    """torch.ops.gnnrec (loads libgnnrec.so + libgnnrec_torch.so on first use)."""
+    return _lib.torch_ops()
 
 REDUCE = {"sum": _lib.REDUCE_SUM, "mean": _lib.REDUCE_MEAN, "max": _lib.REDUCE_MAX}
 ACCUM = {"store": _lib.ACC_STORE, "add": _lib.ACC_ADD, "max": _lib.ACC_MAX,
@@ -40,7 +45,7 @@ def _attn_args(accum, attn_vec, attn_state, n_rows, n_cols):
 
 
 def _dev(t: torch.Tensor, name: str, dtype=None) -> None:
-    if not t.is_cuda:
+    if not (t.is_cuda or t.is_meta):  # meta: shape tracing, the ops launch nothing
         raise ValueError(f"{name} must be a HIP device tensor (got {t.device}); "
                          f"gnnrec has no CPU path")
     if dtype is not None and t.dtype != dtype:
@@ -60,23 +65,19 @@ def set_concurrency(reserve_cus: int = 0, dynamic: bool = False) -> None:
     """Process-wide mode of the row kernels (spmm, spmm_project) for launches that share
     the chip with kernels on other streams (gnnrec_set_concurrency): leave `reserve_cus`
     CUs free, and hand rows out through a device work queue when `dynamic`."""
-    check(_lib.load().gnnrec_set_concurrency(int(reserve_cus), int(bool(dynamic))),
-          "gnnrec_set_concurrency")
+    _T().set_concurrency(int(reserve_cus), bool(dynamic))
 
 
 def get_concurrency():
     """(reserve_cus, dynamic) currently in force."""
-    r, d = ctypes.c_int(), ctypes.c_int()
-    check(_lib.load().gnnrec_get_concurrency(ctypes.byref(r), ctypes.byref(d)),
-          "gnnrec_get_concurrency")
-    return r.value, bool(d.value)
+    r, d = _T().get_concurrency()
+    return r, bool(d)
 
 
 def rowq_stats():
     """(queued launches, launches refused a busy ring slot) since the library loaded."""
-    q, b = ctypes.c_int64(), ctypes.c_int64()
-    check(_lib.load().gnnrec_rowq_stats(ctypes.byref(q), ctypes.byref(b)), "gnnrec_rowq_stats")
-    return q.value, b.value
+    q, b = _T().rowq_stats()
+    return q, b
 
 
 @contextlib.contextmanager
@@ -98,9 +99,8 @@ def hold_cus(blocks: int, usec: int, threads: int = 256, lds_bytes: int = 16384,
     sink = _hold_sink.get(dev.index)
     if sink is None:
         sink = _hold_sink[dev.index] = torch.empty(1024, dtype=torch.float32, device=dev)
-    s = (stream if stream is not None else torch.cuda.current_stream(dev)).cuda_stream
-    check(_lib.load().gnnrec_hold_cus(int(blocks), int(threads), int(lds_bytes), int(usec),
-                                      ptr(sink), s), "gnnrec_hold_cus")
+    with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(dev)):
+        _T().hold_cus(int(blocks), int(threads), int(lds_bytes), int(usec), sink)
 
 
 _hold_sink = {}
@@ -145,9 +145,7 @@ def _device_plan(indptr: torch.Tensor, split: int):
     if cap_h > 0:
         cap_c = E // split + cap_h
         pl = torch.empty(2 + cap_h + cap_h + 1 + cap_c, dtype=torch.int64, device=indptr.device)
-        check(_lib.load().gnnrec_spmm_plan_build(ptr(indptr), n_dst, split, cap_h, ptr(pl),
-                                                 stream_ptr(indptr.device)),
-              "gnnrec_spmm_plan_build")
+        _T().spmm_plan_build(indptr, split, cap_h, pl)
         res = (pl, cap_h, cap_c)
     try:
         indptr._gnnrec_dev_plan = (split, res)
@@ -167,7 +165,7 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
     accumulate: out[v] = out[v] (+ | max) that (source-range tiles of one relation; max
     needs empty_neginf so rows without edges in the tile leave out unchanged).
     """
-    lib = _lib.load()
+    T = _T()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
     _dev(X, "X", torch.float32)
@@ -175,7 +173,7 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
         raise KeyError(f"Aggregator reduce {reduce} not recognized.")
     n_dst = indptr.numel() - 1
     d = X.shape[1]
-    ldx = _rowmajor(X, "X")
+    _rowmajor(X, "X")
     if edge_weight is not None:
         _dev(edge_weight, "edge_weight", torch.float32)
         if edge_weight.numel() != indices.numel():
@@ -189,7 +187,7 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
         _dev(out, "out", torch.float32)
         if tuple(out.shape) != (n_dst, d):
             raise ValueError(f"out must be [{n_dst}, {d}]")
-    ldo = _rowmajor(out, "out")
+    _rowmajor(out, "out")
     flags = _lib.SPMM_EMPTY_NEGINF if empty_neginf else 0
     if accumulate:
         if reduce == "max" and not empty_neginf:
@@ -202,26 +200,18 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
         if dplan is not None:
             pl, cap_h, cap_c = dplan
             ws = torch.empty((cap_c, d), dtype=torch.float32, device=X.device)
-            check(lib.gnnrec_spmm_csr_planned_f32(
-                ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx, n_dst, d,
-                REDUCE[reduce], flags, ptr(out), ldo, split, ptr(pl), cap_h, cap_c, ptr(ws),
-                stream_ptr(X.device)), "gnnrec_spmm_csr_planned_f32")
+            T.spmm_csr_planned(indptr, indices, edge_weight, X, REDUCE[reduce], flags, split, pl,
+                               cap_h, cap_c, out, ws)
             return out
         split = None  # no row can exceed split
     plan = split_plan(indptr, split) if split else None
     if plan is None:
-        rc = lib.gnnrec_spmm_csr_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx,
-                                     n_dst, d, REDUCE[reduce], flags, ptr(out), ldo,
-                                     stream_ptr(X.device))
-        check(rc, "gnnrec_spmm_csr_f32")
+        T.spmm_csr(indptr, indices, edge_weight, X, REDUCE[reduce], flags, out)
         return out
     heavy, chunk_ptr, chunk_row, n_chunks = plan
     ws = torch.empty((n_chunks, d), dtype=torch.float32, device=X.device)
-    rc = lib.gnnrec_spmm_csr_split_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X), ldx,
-                                       n_dst, d, REDUCE[reduce], flags, ptr(out), ldo, split,
-                                       ptr(heavy), heavy.numel(), ptr(chunk_ptr), ptr(chunk_row),
-                                       n_chunks, ptr(ws), stream_ptr(X.device))
-    check(rc, "gnnrec_spmm_csr_split_f32")
+    T.spmm_csr_split(indptr, indices, edge_weight, X, REDUCE[reduce], flags, split, heavy,
+                     chunk_ptr, chunk_row, n_chunks, out, ws)
     return out
 
 
@@ -231,7 +221,7 @@ def csr_transpose(indptr: torch.Tensor, indices: torch.Tensor, n_src: int,
     """Source-major CSR of a dst-major block (stable: ascending edge id per source row).
     -> (indptr_t int64 [n_src+1], indices_t int32 = dst rows, ew_t float32 or None), where
     ew_t = edge_weight (· 1/deg(dst) when mean) in the transposed order."""
-    lib = _lib.load()
+    T = _T()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
     dev = indptr.device
@@ -245,11 +235,9 @@ def csr_transpose(indptr: torch.Tensor, indices: torch.Tensor, n_src: int,
     ip_t = torch.empty(n_src + 1, dtype=torch.int64, device=dev)
     ix_t = torch.empty(E, dtype=torch.int32, device=dev)
     w_t = torch.empty(E, dtype=torch.float32, device=dev) if (edge_weight is not None or mean) else None
-    nbytes = int(lib.gnnrec_csr_transpose_workspace_bytes(E, n_src))
+    nbytes = int(T.csr_transpose_workspace_bytes(E, n_src))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-    check(lib.gnnrec_csr_transpose(ptr(indptr), ptr(indices), ptr(edge_weight), n_dst, n_src, E,
-                                   int(mean), ptr(ws), nbytes, ptr(ip_t), ptr(ix_t), ptr(w_t),
-                                   stream_ptr(dev)), "gnnrec_csr_transpose")
+    T.csr_transpose(indptr, indices, edge_weight, n_src, E, bool(mean), ws, ip_t, ix_t, w_t)
     ip_t._gnnrec_nnz = E
     return ip_t, ix_t, w_t
 
@@ -258,7 +246,7 @@ def csr_build(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
     """dst-major CSR of the COO relation (src, dst) with in-row order = edge id
     (gnnrec_csr_build: stable radix sort of the dst ids on the device).
     -> (indptr int64 [n_dst+1], indices int32 = src ids, eids int64)."""
-    lib = _lib.load()
+    T = _T()
     _dev(dst, "dst", torch.int64)
     _dev(src, "src", torch.int64)
     if src.shape != dst.shape or src.dim() != 1:
@@ -270,10 +258,9 @@ def csr_build(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
     indptr = torch.empty(n_dst + 1, dtype=torch.int64, device=dev)
     indices = torch.empty(E, dtype=torch.int32, device=dev)
     eids = torch.empty(E, dtype=torch.int64, device=dev)
-    nbytes = int(lib.gnnrec_csr_build_workspace_bytes(E, n_dst))
+    nbytes = int(T.csr_build_workspace_bytes(E, n_dst))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-    check(lib.gnnrec_csr_build(ptr(src), ptr(dst), E, n_dst, ptr(ws), nbytes, ptr(indptr),
-                               ptr(indices), ptr(eids), stream_ptr(dev)), "gnnrec_csr_build")
+    T.csr_build(src, dst, n_dst, ws, indptr, indices, eids)
     indptr._gnnrec_nnz = E
     return indptr, indices, eids
 
@@ -281,7 +268,7 @@ def csr_build(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
 def csr_from_keys(keys: torch.Tensor, n_rows: int):
     """Rows of a COO list: -> (indptr int64 [n_rows+1], perm int32 [E]) with perm the edge
     ids grouped by keys[e] (ascending edge id inside a row).  keys: int32/int64 in [0, n_rows)."""
-    lib = _lib.load()
+    T = _T()
     if keys.dtype != torch.int32:
         keys = keys.to(torch.int32)
     _dev(keys, "keys", torch.int32)
@@ -289,23 +276,20 @@ def csr_from_keys(keys: torch.Tensor, n_rows: int):
     dev, E = keys.device, keys.numel()
     ip = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
     perm = torch.empty(E, dtype=torch.int32, device=dev)
-    nbytes = int(lib.gnnrec_csr_from_keys_workspace_bytes(E, n_rows))
+    nbytes = int(T.csr_from_keys_workspace_bytes(E, n_rows))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-    check(lib.gnnrec_csr_from_keys(ptr(keys), E, n_rows, ptr(ws), nbytes, ptr(ip), ptr(perm),
-                                   stream_ptr(dev)), "gnnrec_csr_from_keys")
+    T.csr_from_keys(keys, n_rows, ws, ip, perm)
     ip._gnnrec_nnz = E
     return ip, perm
 
 
 def add_(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a += b (same shape, contiguous fp32) with the library's add kernel; returns a."""
-    lib = _lib.load()
     _dev(a, "a", torch.float32)
     _dev(b, "b", torch.float32)
     if a.shape != b.shape or not (a.is_contiguous() and b.is_contiguous()):
         raise ValueError("add_: operands must be contiguous and of one shape")
-    check(lib.gnnrec_add_f32(ptr(a), ptr(b), ptr(a), a.numel(), stream_ptr(a.device)),
-          "gnnrec_add_f32")
+    _T().add_(a, b)
     return a
 
 
@@ -313,7 +297,6 @@ def tree_sum_(parts) -> torch.Tensor:
     """parts[0] = ((p0+p1)+(p2+p3))+... over 2, 4 or 8 same-shape contiguous fp32 tables in
     one kernel pass (gnnrec_tree_sum_f32): the same additions, in the same order, as
     pairwise add_ launches level by level; returns parts[0]."""
-    lib = _lib.load()
     n = len(parts)
     if n not in (2, 4, 8):
         raise ValueError("tree_sum_: 2, 4 or 8 tables")
@@ -322,42 +305,31 @@ def tree_sum_(parts) -> torch.Tensor:
         _dev(p, "part", torch.float32)
         if p.shape != a.shape or not p.is_contiguous():
             raise ValueError("tree_sum_: operands must be contiguous and of one shape")
-    arr = (ctypes.c_void_p * n)(*[ptr(p) for p in parts])
-    check(lib.gnnrec_tree_sum_f32(arr, n, a.numel(), ptr(a), stream_ptr(a.device)),
-          "gnnrec_tree_sum_f32")
+    _T().tree_sum_(a, list(parts[1:]))
     return a
 
 
 def l2_normalize_rows(y: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = y / ‖y‖ per row, rows with ‖y‖ == 0 unchanged (src/model.py:230-235), one
     wave per row (gnnrec_row_epilogue_f32)."""
-    lib = _lib.load()
     _dev(y, "y", torch.float32)
     M, N = y.shape
-    ldy = _rowmajor(y, "y")
+    _rowmajor(y, "y")
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=y.device)
-    check(lib.gnnrec_row_epilogue_f32(ptr(y), ldy, M, N, 1, ACCUM["store"], 0.0, 0, 0, ptr(out),
-                                      _rowmajor(out, "out"), stream_ptr(y.device)),
-          "gnnrec_row_epilogue_f32")
+    _T().row_epilogue(y, 1, ACCUM["store"], 0.0, None, None, out)
     return out
 
 
 def spmm_backward(indptr, indices, grad_out, reduce, edge_weight=None, X=None, out=None,
                   grad_X=None, n_src=None):
     """Gradient of spmm w.r.t. its source rows (accumulated into grad_X, created if None)."""
-    lib = _lib.load()
     _dev(grad_out, "grad_out", torch.float32)
     n_dst, d = grad_out.shape
     if grad_X is None:
         grad_X = torch.zeros((n_src, d), dtype=torch.float32, device=grad_out.device)
     grad_out = grad_out.contiguous()
-    rc = lib.gnnrec_spmm_backward_f32(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(grad_out),
-                                      d, ptr(X), 0 if X is None else _rowmajor(X, "X"), ptr(out),
-                                      0 if out is None else _rowmajor(out, "out"), n_dst, d,
-                                      REDUCE[reduce], ptr(grad_X), _rowmajor(grad_X, "grad_X"),
-                                      stream_ptr(grad_out.device))
-    check(rc, "gnnrec_spmm_backward_f32")
+    _T().spmm_backward(indptr, indices, edge_weight, grad_out, X, out, REDUCE[reduce], grad_X)
     return grad_X
 
 
@@ -373,32 +345,30 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
     """a2/a3/a4: out (accum)= epi(A1 W1ᵀ + T(A2) W2ᵀ + bias [+ bias_nonempty where
     a2_deg > 0]).  W are nn.Linear weights [N, K].  row_norm [M] (with l2norm, N <=
     GEMM_ROW_N): receives each row's norm before the normalisation (training)."""
-    lib = _lib.load()
+    T = _T()
     _dev(A1, "A1", torch.float32)
     _dev(W1, "W1", torch.float32)
     M, K1 = A1.shape
     N = W1.shape[0]
     if W1.shape[1] != K1:
         raise ValueError(f"W1 shape {tuple(W1.shape)} does not match A1 K={K1}")
-    W1 = W1.contiguous()
-    lda1 = _rowmajor(A1, "A1")
-    K2, lda2 = 0, 1
+    W1 = W1.detach().contiguous()
+    _rowmajor(A1, "A1")
     if A2 is not None:
         _dev(A2, "A2", torch.float32)
         _dev(W2, "W2", torch.float32)
         if A2.shape[0] != M or W2.shape[0] != N or W2.shape[1] != A2.shape[1]:
             raise ValueError("A2/W2 shape mismatch")
-        K2 = A2.shape[1]
-        lda2 = _rowmajor(A2, "A2")
-        W2 = W2.contiguous()
+        _rowmajor(A2, "A2")
+        W2 = W2.detach().contiguous()
     if bias is not None:
         _dev(bias, "bias", torch.float32)
-        bias = bias.contiguous()
+        bias = bias.detach().contiguous()
     if a2_mode != _lib.A2_NONE or bias_nonempty is not None:
         _dev(a2_deg, "a2_deg", torch.int32)
     if bias_nonempty is not None:
         _dev(bias_nonempty, "bias_nonempty", torch.float32)
-        bias_nonempty = bias_nonempty.contiguous()
+        bias_nonempty = bias_nonempty.detach().contiguous()
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0) | (
         _lib.EPI_SIGMOID if sigmoid else 0)
     if out is None:
@@ -409,7 +379,7 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
         _dev(out, "out", torch.float32)
         if tuple(out.shape) != (M, N):
             raise ValueError(f"out must be [{M}, {N}]")
-    ldo = _rowmajor(out, "out")
+    _rowmajor(out, "out")
     av, ast = _attn_args(accum, attn_vec, attn_state, M, N)
     if row_norm is not None:
         _dev(row_norm, "row_norm", torch.float32)
@@ -420,15 +390,10 @@ def gemm(A1: torch.Tensor, W1: torch.Tensor, A2: Optional[torch.Tensor] = None,
         # into a scratch table, then one row-epilogue pass into out
         z = gemm(A1, W1, A2, W2, bias, relu=relu, sigmoid=sigmoid, a2_deg=a2_deg,
                  a2_mode=a2_mode, bias_nonempty=bias_nonempty)
-        check(lib.gnnrec_row_epilogue_f32(ptr(z), N, M, N, int(l2norm), ACCUM[accum],
-                                          float(out_div), ptr(av), ptr(ast), ptr(out), ldo,
-                                          stream_ptr(A1.device)), "gnnrec_row_epilogue_f32")
+        T.row_epilogue(z, int(l2norm), ACCUM[accum], float(out_div), av, ast, out)
         return out
-    rc = lib.gnnrec_gemm_rownorm_f32(ptr(A1), lda1, K1, ptr(W1), ptr(A2), lda2, K2, ptr(W2),
-                                     ptr(a2_deg), a2_mode, ptr(bias), ptr(bias_nonempty), M, N,
-                                     epi, ACCUM[accum], float(out_div), ptr(av), ptr(ast),
-                                     ptr(out), ldo, ptr(row_norm), stream_ptr(A1.device))
-    check(rc, "gnnrec_gemm_f32")
+    T.gemm(A1, W1, A2, W2, a2_deg, a2_mode, bias, bias_nonempty, epi, ACCUM[accum],
+           float(out_div), av, ast, out, row_norm)
     return out
 
 
@@ -448,7 +413,8 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
     if os.environ.get("GNNREC_FUSED", "1") == "0":
         return False
     D = FUSED_D
-    if not (X.is_cuda and H.is_cuda and X.dim() == 2 and H.dim() == 2):
+    if not ((X.is_cuda or X.is_meta) and (H.is_cuda or H.is_meta) and X.dim() == 2
+            and H.dim() == 2):
         return False
     if X.shape[1] != D or H.shape[1] != D or tuple(W_self.shape) != (D, D) or \
             tuple(W_neigh.shape) != (D, D):
@@ -456,7 +422,11 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
     if X.dtype != torch.float32 or H.dtype != torch.float32:
         return False
     for t in (X, H):
-        if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        if t.stride(1) != 1 or t.stride(0) % 4:
+            return False
+        # 16-B aligned rows; torch.compile's fake tensors have no address (there the
+        # library's own alignment check is what refuses a misaligned view, loudly)
+        if not torch.compiler.is_compiling() and t.data_ptr() % 16:
             return False
     if split and split_plan(indptr, split) is not None:
         return False
@@ -512,7 +482,6 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
     + [deg > 0]·bias_nonempty), d = 128.  variant 'valu' | 'mfma' (default: fused_variant
     of avg_deg) picks the kernel; both give the same aggregate bits, the projection's
     fp32 summation order differs."""
-    lib = _lib.load()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
     _dev(X, "X", torch.float32)
@@ -548,14 +517,12 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
     variant = variant or fused_variant(indptr, avg_deg)
     if variant not in ("valu", "mfma"):
         raise ValueError(f"spmm_project variant must be 'valu' or 'mfma', not {variant!r}")
-    fn = lib.gnnrec_spmm_project_mfma_f32 if variant == "mfma" else lib.gnnrec_spmm_project_f32
-    check(fn(ptr(indptr), ptr(indices), ptr(edge_weight), ptr(X),
-                                      _rowmajor(X, "X"), ptr(H), _rowmajor(H, "H"), ptr(WsT),
-                                      ptr(WnT), ptr(bias), ptr(bias_nonempty), n_dst,
-                                      X.shape[1], REDUCE[reduce], epi,
-                                      ACCUM[accum], float(out_div), ptr(av), ptr(ast), ptr(out),
-                                      _rowmajor(out, "out"), stream_ptr(X.device)),
-          "gnnrec_spmm_project_f32")
+    _rowmajor(X, "X")
+    _rowmajor(H, "H")
+    _rowmajor(out, "out")
+    _T().spmm_project(indptr, indices, edge_weight, X, H, WsT, WnT, bias, bias_nonempty,
+                      REDUCE[reduce], epi, ACCUM[accum], float(out_div), av, ast,
+                      variant == "mfma", out)
     return out
 
 
@@ -565,14 +532,15 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None
     colsum [M], also colsum (+)= Σ_k A[k] (the bias gradient) from the same pass.
 
     Deterministic split-K MFMA (gnnrec_gemm_tn_bias_f32)."""
-    lib = _lib.load()
+    T = _T()
     _dev(A, "A", torch.float32)
     _dev(B, "B", torch.float32)
     K, M = A.shape
     if B.shape[0] != K:
         raise ValueError(f"gemm_tn: A {tuple(A.shape)} and B {tuple(B.shape)} differ in K")
     N = B.shape[1]
-    lda, ldb = _rowmajor(A, "A"), _rowmajor(B, "B")
+    _rowmajor(A, "A")
+    _rowmajor(B, "B")
     if out is None:
         if accumulate:
             raise ValueError("accumulating gemm_tn needs an out tensor")
@@ -585,12 +553,10 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None
         _dev(colsum, "colsum", torch.float32)
         if colsum.numel() != M or not colsum.is_contiguous():
             raise ValueError(f"colsum must be a contiguous [{M}] tensor")
-    ldc = _rowmajor(out, "out")
-    nbytes = lib.gnnrec_gemm_tn_workspace_bytes(K, M, N)
+    _rowmajor(out, "out")
+    nbytes = T.gemm_tn_workspace_bytes(K, M, N)
     ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=A.device)
-    check(lib.gnnrec_gemm_tn_bias_f32(ptr(A), lda, ptr(B), ldb, K, M, N, ptr(out), ldc,
-                                      ptr(colsum), int(accumulate), ptr(ws),
-                                      stream_ptr(A.device)), "gnnrec_gemm_tn_bias_f32")
+    T.gemm_tn(A, B, colsum, bool(accumulate), out, ws)
     return out
 
 
@@ -598,7 +564,6 @@ def act_backward_normed(z: torch.Tensor, row_norm: torch.Tensor, gz: torch.Tenso
                         relu: bool = True) -> torch.Tensor:
     """f2: gradient through relu?+L2 norm from the normalised output z and the row norms
     gemm(..., l2norm=True, row_norm=...) wrote (gnnrec_act_backward_normed_f32)."""
-    lib = _lib.load()
     _dev(z, "z", torch.float32)
     _dev(gz, "gz", torch.float32)
     _dev(row_norm, "row_norm", torch.float32)
@@ -606,17 +571,13 @@ def act_backward_normed(z: torch.Tensor, row_norm: torch.Tensor, gz: torch.Tenso
     if tuple(gz.shape) != (n, d) or row_norm.numel() != n:
         raise ValueError("act_backward_normed: shape mismatch")
     gu = torch.empty((n, d), dtype=torch.float32, device=z.device)
-    check(lib.gnnrec_act_backward_normed_f32(ptr(z), _rowmajor(z, "z"), ptr(row_norm.contiguous()),
-                                             ptr(gz), _rowmajor(gz, "gz"), n, d, int(relu),
-                                             ptr(gu), d, stream_ptr(z.device)),
-          "gnnrec_act_backward_normed_f32")
+    _T().act_backward_normed(z, row_norm.contiguous(), gz, bool(relu), gu)
     return gu
 
 
 def act_backward(u: torch.Tensor, gz: torch.Tensor, relu: bool, l2norm: bool,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """f2: gradient through z = norm?(relu?(u)) (zero-guarded row norm) for pre-activation u."""
-    lib = _lib.load()
     _dev(u, "u", torch.float32)
     _dev(gz, "gz", torch.float32)
     if gz.shape != u.shape:
@@ -626,9 +587,7 @@ def act_backward(u: torch.Tensor, gz: torch.Tensor, relu: bool, l2norm: bool,
     if out is None:
         out = torch.empty_like(u)
     flags = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
-    check(lib.gnnrec_act_backward_f32(ptr(u), _rowmajor(u, "u"), ptr(gz), _rowmajor(gz, "gz"), n,
-                                      d, flags, ptr(out), _rowmajor(out, "out"),
-                                      stream_ptr(u.device)), "gnnrec_act_backward_f32")
+    _T().act_backward(u, gz, flags, out)
     return out
 
 
@@ -661,7 +620,7 @@ def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """f4: per destination, nn.LSTM over its in-neighbour rows of X in CSR (edge) order ->
     final hidden state [n_dst, d]; 0 for zero in-degree (ConvLayer._lstm_reducer)."""
-    lib = _lib.load()
+    T = _T()
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
     d = W_hh.shape[1]
@@ -678,21 +637,17 @@ def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh,
          torch.empty((plan.n_rows, d), dtype=torch.float32, device=X.device)]
     c = torch.zeros((plan.n_rows, d), dtype=torch.float32, device=X.device)
     WT = W_hh.detach().t().contiguous()
-    s = stream_ptr(X.device)
     for t, n_act in enumerate(plan.n_active):
-        check(lib.gnnrec_lstm_step_f32(ptr(P), P.stride(0), ptr(indptr), ptr(indices),
-                                       ptr(plan.order), t, n_act, ptr(h[t % 2]),
-                                       ptr(h[(t + 1) % 2]), ptr(c), d, ptr(WT), ptr(out),
-                                       out.stride(0), s), "gnnrec_lstm_step_f32")
+        T.lstm_step(P, indptr, indices, plan.order, t, n_act, h[t % 2], h[(t + 1) % 2], c, WT,
+                    out)
     return out
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """a10: src[idx] along dim 0 for a device tensor of any dtype whose rows are contiguous
     (node features into blocks[0].srcdata, edge data into blocks)."""
-    lib = _lib.load()
     _dev(idx, "idx", torch.int64)
-    if not src.is_cuda:
+    if not (src.is_cuda or src.is_meta):
         raise ValueError("src: expected a device tensor (there is no CPU path)")
     if src.dim() == 0:
         raise ValueError("src: expected at least one dimension")
@@ -700,21 +655,13 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     if not (row.is_contiguous() and (src.dim() == 1 or src.stride(0) >= row.numel())):
         src = src.contiguous()
     out = torch.empty((idx.numel(),) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-    es = src.element_size()
-    row_elems = 1
-    for n in src.shape[1:]:
-        row_elems *= n
-    row_bytes = es * row_elems
-    idx = idx.contiguous()
-    check(lib.gnnrec_gather_rows(ptr(src), src.stride(0) * es, ptr(idx), idx.numel(), row_bytes,
-                                 ptr(out), row_bytes, stream_ptr(src.device)), "gnnrec_gather_rows")
+    _T().gather_rows(src, idx.contiguous(), out)
     return out
 
 
 def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
               Hd: torch.Tensor) -> torch.Tensor:
     """a7: cosine of the L2-normalised endpoint rows, one value per edge -> [E]."""
-    lib = _lib.load()
     _dev(src, "src", torch.int64)
     _dev(dst, "dst", torch.int64)
     _dev(Hs, "Hs", torch.float32)
@@ -725,10 +672,9 @@ def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
     if Hs.shape[1] != Hd.shape[1]:
         raise ValueError("endpoint feature sizes differ")
     out = torch.empty(E, dtype=torch.float32, device=Hs.device)
-    rc = lib.gnnrec_sddmm_cos_f32(ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(Hs),
-                                  _rowmajor(Hs, "Hs"), ptr(Hd), _rowmajor(Hd, "Hd"), Hs.shape[1],
-                                  ptr(out), stream_ptr(Hs.device))
-    check(rc, "gnnrec_sddmm_cos_f32")
+    _rowmajor(Hs, "Hs")
+    _rowmajor(Hd, "Hd")
+    _T().sddmm_cos(src.contiguous(), dst.contiguous(), Hs, Hd, out)
     return out
 
 
@@ -736,7 +682,7 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
                        grad: torch.Tensor, need_src: bool = True, need_dst: bool = True):
     """f2: gradients of sddmm_cos w.r.t. Hs and Hd given dL/dcos [E] -> (gHs|None, gHd|None),
     one library call (key sort, planned weighted gather, normalisation Jacobian)."""
-    lib = _lib.load()
+    T = _T()
     _dev(src, "src", torch.int64)
     _dev(dst, "dst", torch.int64)
     _dev(Hs, "Hs", torch.float32)
@@ -750,12 +696,10 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
     n_s, n_d = Hs.shape[0], Hd.shape[0]
     gHs = torch.empty((n_s, d), dtype=torch.float32, device=Hs.device) if need_src else None
     gHd = torch.empty((n_d, d), dtype=torch.float32, device=Hs.device) if need_dst else None
-    nbytes = int(lib.gnnrec_sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d))
+    nbytes = int(T.sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=Hs.device)
-    check(lib.gnnrec_sddmm_cos_backward_f32(
-        ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(Hs), _rowmajor(Hs, "Hs"), n_s,
-        ptr(Hd), _rowmajor(Hd, "Hd"), n_d, d, ptr(grad.contiguous()), ptr(gHs), ptr(gHd),
-        ptr(ws), nbytes, stream_ptr(Hs.device)), "gnnrec_sddmm_cos_backward_f32")
+    T.sddmm_cos_backward(src.contiguous(), dst.contiguous(), Hs, Hd, grad.contiguous(), gHs, gHd,
+                         ws)
     return gHs, gHd
 
 
@@ -763,9 +707,9 @@ def margin_loss(parts, delta: float):
     """f2: max_margin_loss forward + unscaled gradients for a list of etype parts
     [(pos [E], neg [E*K], K, mask|None, recency|None)] -> (loss 0-d tensor, N_total,
     [(g_pos, g_neg)]).  Gradients are d(sum of scores)/d(score); the loss is the mean."""
-    lib = _lib.load()
+    T = _T()
     dev = parts[0][0].device
-    blocks = [int(lib.gnnrec_margin_loss_blocks(p[0].numel())) for p in parts]
+    blocks = [int(T.margin_loss_blocks(p[0].numel())) for p in parts]
     partial = torch.empty(sum(blocks), dtype=torch.float32, device=dev)
     grads, off, total = [], 0, 0
     for (pos, neg, K, mask, rec), nb in zip(parts, blocks):
@@ -778,89 +722,70 @@ def margin_loss(parts, delta: float):
             mask = mask.to(device=dev, dtype=torch.float32).contiguous()
             if mask.numel() != neg.numel():
                 raise ValueError("negative_mask must have one value per negative score")
-        rec_i64 = 0
         if rec is not None:
             rec = rec.to(dev).reshape(-1)
-            if rec.dtype == torch.int64:
-                rec_i64 = 1
-            elif rec.dtype != torch.float32:
+            if rec.dtype not in (torch.int64, torch.float32):
                 rec = rec.float()
             rec = rec.contiguous()
             if rec.numel() != n_pos:
                 raise ValueError("recency must have one value per positive edge")
         g_pos = torch.empty_like(pos)
         g_neg = torch.empty_like(neg)
-        check(lib.gnnrec_margin_loss_f32(ptr(pos.contiguous()), ptr(neg.contiguous()), n_pos, K,
-                                         float(delta), ptr(mask), ptr(rec), rec_i64, ptr(g_pos),
-                                         ptr(g_neg), ptr(partial[off:]), nb, stream_ptr(dev)),
-              "gnnrec_margin_loss_f32")
+        T.margin_loss(pos.contiguous(), neg.contiguous(), K, float(delta), mask, rec, g_pos,
+                      g_neg, partial[off:off + nb])
         grads.append((g_pos, g_neg))
         off += nb
         total += neg.numel()
     loss = torch.empty((), dtype=torch.float32, device=dev)
-    check(lib.gnnrec_sum_scaled_f32(ptr(partial), partial.numel(),
-                                    1.0 / total if total else float('nan'), ptr(loss),
-                                    stream_ptr(dev)), "gnnrec_sum_scaled_f32")
+    T.sum_scaled(partial, 1.0 / total if total else float('nan'), loss)
     return loss, total, grads
 
 
 def edge_mlp(src: torch.Tensor, dst: torch.Tensor, P: torch.Tensor, Q: torch.Tensor,
              W2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor) -> torch.Tensor:
     """a8 tail: sigmoid(w3·relu(W2·relu(P[src]+Q[dst]) + b2) + b3) -> [E]."""
-    lib = _lib.load()
     for t, n in ((P, "P"), (Q, "Q"), (W2, "W2"), (b2, "b2"), (w3, "w3"), (b3, "b3")):
         _dev(t, n, torch.float32)
     _dev(src, "src", torch.int64)
     _dev(dst, "dst", torch.int64)
     if P.shape[1] != 128 or Q.shape[1] != 128 or tuple(W2.shape) != (32, 128):
         raise ValueError("edge_mlp expects the reference's 128/32 hidden sizes")
-    P, Q, W2 = P.contiguous(), Q.contiguous(), W2.contiguous()
+    P, Q, W2 = P.contiguous(), Q.contiguous(), W2.detach().contiguous()
     E = src.numel()
     out = torch.empty(E, dtype=torch.float32, device=P.device)
-    rc = lib.gnnrec_edge_mlp_f32(ptr(src.contiguous()), ptr(dst.contiguous()), E, ptr(P), ptr(Q),
-                                 ptr(W2), ptr(b2.contiguous()), ptr(w3.contiguous()),
-                                 ptr(b3.contiguous()), ptr(out), stream_ptr(P.device))
-    check(rc, "gnnrec_edge_mlp_f32")
+    _T().edge_mlp(src.contiguous(), dst.contiguous(), P, Q, W2, b2.detach().contiguous(),
+                  w3.detach().contiguous(), b3.detach().contiguous(), out)
     return out
 
 
 def synth_edges(seed: int, e0: int, n: int, n_u: int, n_i: int, device,
                 zipf_cdf: Optional[torch.Tensor] = None):
     """Counter-hash bipartite edges [e0, e0+n) -> (u int32 [n], i int32 [n])."""
-    lib = _lib.load()
     u = torch.empty(n, dtype=torch.int32, device=device)
     i = torch.empty(n, dtype=torch.int32, device=device)
     if zipf_cdf is not None:
         _dev(zipf_cdf, "zipf_cdf", torch.float64)
-    rc = lib.gnnrec_synth_edges(seed & 0xFFFFFFFFFFFFFFFF, e0, n, n_u, n_i, ptr(zipf_cdf), ptr(u),
-                                ptr(i), stream_ptr(u.device))
-    check(rc, "gnnrec_synth_edges")
+    _T().synth_edges(_lib.i64(seed), e0, n_u, n_i, zipf_cdf, u, i)
     return u, i
 
 
 def exclusive_scan(x: torch.Tensor) -> torch.Tensor:
     """[n] int32/int64 -> [n+1] int64 exclusive prefix sums (last = total)."""
-    lib = _lib.load()
+    T = _T()
     _dev(x, "x")
+    if x.dtype not in (torch.int64, torch.int32):
+        raise ValueError("exclusive_scan supports int32/int64")
     n = x.numel()
     out = torch.empty(n + 1, dtype=torch.int64, device=x.device)
-    ws = torch.empty(max(1, (lib.gnnrec_scan_workspace_bytes(n) + 7) // 8), dtype=torch.int64,
+    ws = torch.empty(max(1, (T.scan_workspace_bytes(n) + 7) // 8), dtype=torch.int64,
                      device=x.device)
-    x = x.contiguous()
-    if x.dtype == torch.int64:
-        rc = lib.gnnrec_exclusive_scan_i64(ptr(x), n, ptr(out), ptr(ws), stream_ptr(x.device))
-    elif x.dtype == torch.int32:
-        rc = lib.gnnrec_exclusive_scan_i32(ptr(x), n, ptr(out), ptr(ws), stream_ptr(x.device))
-    else:
-        raise ValueError("exclusive_scan supports int32/int64")
-    check(rc, "gnnrec_exclusive_scan")
+    T.exclusive_scan(x.contiguous(), out, ws)
     return out
 
 
 def sample_count(indptr, eids, seeds, fanout: int, seed_key: int = 0,
                  excluded: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a9 phase 1: per-seed sampled in-edge counts -> out_indptr [n_seeds+1] (device)."""
-    lib = _lib.load()
     for t, n in ((indptr, "indptr"), (eids, "eids"), (seeds, "seeds")):
         _dev(t, n, torch.int64)
     if excluded is not None:
@@ -868,9 +793,7 @@ def sample_count(indptr, eids, seeds, fanout: int, seed_key: int = 0,
     n = seeds.numel()
     fan = -1 if fanout is None or fanout < 0 else int(fanout)
     counts = torch.empty(n, dtype=torch.int64, device=seeds.device)
-    check(lib.gnnrec_sample_count(ptr(indptr), ptr(eids), ptr(excluded), ptr(seeds), n, fan,
-                                  seed_key & 0xFFFFFFFFFFFFFFFF, ptr(counts),
-                                  stream_ptr(seeds.device)), "gnnrec_sample_count")
+    _T().sample_count(indptr, eids, excluded, seeds, fan, _lib.i64(seed_key), counts)
     return exclusive_scan(counts)
 
 
@@ -879,16 +802,13 @@ def sample_fill(indptr, indices, eids, seeds, fanout: int, seed_key: int, out_in
     """a9 phase 2: copy the sampled edges at out_indptr offsets -> (src ids, eids).
 
     indices: the CSR's int32 source ids (graph.in_csr); outputs are int64."""
-    lib = _lib.load()
     _dev(indices, "indices", torch.int32)
     n = seeds.numel()
     fan = -1 if fanout is None or fanout < 0 else int(fanout)
     out_src = torch.empty(total, dtype=torch.int64, device=seeds.device)
     out_eid = torch.empty(total, dtype=torch.int64, device=seeds.device)
-    check(lib.gnnrec_sample_fill(ptr(indptr), ptr(indices), ptr(eids), ptr(excluded), ptr(seeds),
-                                 n, fan, seed_key & 0xFFFFFFFFFFFFFFFF, ptr(out_indptr),
-                                 ptr(out_src), ptr(out_eid), stream_ptr(seeds.device)),
-          "gnnrec_sample_fill")
+    _T().sample_fill(indptr, indices, eids, excluded, seeds, fan, _lib.i64(seed_key), out_indptr,
+                     out_src, out_eid)
     return out_src, out_eid
 
 
@@ -920,33 +840,26 @@ class Relabeler:
 
     def begin(self, prefix: torch.Tensor, id_lists):
         """set the prefix map, mark new ids, scan -> rank (device; rank[-1] = n_new)."""
-        lib = _lib.load()
-        s = stream_ptr(prefix.device)
-        check(lib.gnnrec_set_prefix_pos(ptr(prefix), prefix.numel(), ptr(self.prefix_pos), s),
-              "set_prefix")
+        T = _T()
+        T.set_prefix_pos(prefix, self.prefix_pos)
         for ids in id_lists:
-            check(lib.gnnrec_mark_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(self.mark),
-                                      s), "mark_ids")
+            T.mark_ids(ids, self.prefix_pos, self.mark)
         return exclusive_scan(self.mark)
 
     def finish(self, prefix: torch.Tensor, id_lists, rank: torch.Tensor, n_new: int):
         """compact the new ids, relabel every list, reset the scratch."""
-        lib = _lib.load()
-        s = stream_ptr(prefix.device)
+        T = _T()
         n_p = prefix.numel()
         src_nodes = torch.empty(n_p + n_new, dtype=torch.int64, device=prefix.device)
         src_nodes[:n_p] = prefix
         if n_new:
-            check(lib.gnnrec_compact_marked(ptr(self.mark), ptr(rank), self.n_nodes,
-                                            ptr(src_nodes[n_p:]), s), "compact")
+            T.compact_marked(self.mark, rank, src_nodes[n_p:])
         locals_ = []
         for ids in id_lists:
             loc = torch.empty(ids.numel(), dtype=torch.int64, device=prefix.device)
-            check(lib.gnnrec_relabel_ids(ptr(ids), ids.numel(), ptr(self.prefix_pos), ptr(rank),
-                                         n_p, ptr(loc), s), "relabel")
+            T.relabel_ids(ids, self.prefix_pos, rank, n_p, loc)
             locals_.append(loc)
-        check(lib.gnnrec_clear_prefix_pos(ptr(prefix), n_p, ptr(self.prefix_pos), s),
-              "clear_prefix")
+        T.clear_prefix_pos(prefix, self.prefix_pos)
         if n_new:
             self.mark.index_fill_(0, src_nodes[n_p:], 0)
         return src_nodes, locals_
@@ -957,3 +870,11 @@ class Relabeler:
         Returns (src_nodes [n_p + n_new] global ids, [local ids per list])."""
         rank = self.begin(prefix, id_lists)
         return self.finish(prefix, id_lists, rank, int(rank[-1].item()))
+
+
+# load the library at import (outside any torch.compile trace); if it is missing, every op
+# raises GnnrecLibraryError when called — there is no fallback
+try:
+    _lib.torch_ops()
+except _lib.GnnrecLibraryError:
+    pass

@@ -19,7 +19,6 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import check, ptr, stream_ptr
 
 
 def create_ground_truth(users, items):
@@ -39,14 +38,10 @@ def create_already_bought(g, bought_eids, etype='buys'):
 
 def topk_rows(scores: torch.Tensor, k: int, exclude_indptr=None, exclude_indices=None):
     """Per row: k best columns by (score desc, column asc), excluded columns skipped."""
-    lib = _lib.load()
     n_rows, n_cols = scores.shape
     vals = torch.empty((n_rows, k), dtype=torch.float32, device=scores.device)
     idx = torch.empty((n_rows, k), dtype=torch.int64, device=scores.device)
-    rc = lib.gnnrec_topk_rows_f32(ptr(scores), scores.stride(0), n_rows, n_cols, k,
-                                  ptr(exclude_indptr), ptr(exclude_indices), ptr(vals), ptr(idx),
-                                  stream_ptr(scores.device))
-    check(rc, "gnnrec_topk_rows_f32")
+    _lib.torch_ops().topk_rows(scores, k, exclude_indptr, exclude_indices, vals, idx)
     return vals, idx
 
 

@@ -733,6 +733,32 @@ def test_spmm_project_accumulate_modes_and_strides(variant):
         np.testing.assert_allclose(out.cpu().numpy(), fn(base[:, :d]) / 2.0, rtol=RTOL, atol=ATOL)
 
 
+@pytest.mark.parametrize("variant", ["valu", "mfma"])
+@pytest.mark.parametrize("n_dst", [1, 31, 33, 65, 200, 257, 300])
+def test_spmm_project_small_relations_cover_every_row(n_dst, variant):
+    """Relations of 1..10 MFMA tiles launch fewer blocks than the chip has XCDs: every
+    row must still be produced (the MFMA kernel's XCD-contiguous static walk once left
+    the tiles of block-less XCDs unwritten — tests/test_gpu_fuzz.py seed 4, 65 items)."""
+    from gnnrec import ops
+    rng = np.random.default_rng(n_dst)
+    n_src, d = 90, 128
+    deg = rng.integers(0, 25, n_dst)
+    dst = np.repeat(np.arange(n_dst), deg)
+    src = rng.integers(0, n_src, dst.size)
+    indptr, indices, _ = oracle.csr_from_coo(src, dst, n_dst)
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    agg = oracle.spmm_csr(indptr, indices, X, "mean")
+    ref = oracle.l2_normalize_rows_guarded(oracle.relu(oracle.linear(H, Ws) +
+                                                       oracle.linear(agg, Wn)))
+    out = torch.full((n_dst, d), float("nan"), device=DEV)  # unwritten rows stay NaN
+    ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), _t(X), _t(H), _t(Ws), _t(Wn),
+                     "mean", None, relu=True, l2norm=True, out=out, variant=variant)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+
+
 def test_fused_sharded_pass_equals_modules_bitwise():
     """d=128 models run the fused kernel in both the module path and the sharded pass:
     at P=1 the two are bitwise identical and match the oracle."""
