@@ -88,6 +88,16 @@ class RelShard:
         return int(self.indices.numel())
 
 
+def _planned(indptr: torch.Tensor) -> torch.Tensor:
+    """A shard CSR with its heavy-row plan computed once, at setup (one host readback):
+    the pass then launches the plain aggregation kernel when no row is heavy, instead of
+    the device-planned form's plan / chunk / combine launches on every pass (C5: 32 extra
+    launches per layer, ≈1.5 ms)."""
+    if indptr.is_cuda:
+        ops.split_plan(indptr)
+    return indptr
+
+
 class GraphShard:
     """This rank's share of a heterograph for the sharded full-graph pass."""
 
@@ -164,7 +174,7 @@ class GraphShard:
             rows = dst - self.p_lo
             indptr, indices, order = build_csr(src, rows, self.n_own)
             w = None if weights is None else weights[order].float().contiguous()
-            self.rels[ce] = RelShard(ce, 'local_dst', indptr.to(dev), indices.to(dev),
+            self.rels[ce] = RelShard(ce, 'local_dst', _planned(indptr.to(dev)), indices.to(dev),
                                      None if w is None else w.to(dev), self.n_own, global_edges)
             return
         src_loc = src - self.p_lo if s_t == self.ptype else src
@@ -188,8 +198,8 @@ class GraphShard:
                 sel = (key >= bounds[sg]) & (key < bounds[sg + 1])
                 ip, ix, od = build_csr(src_loc[sel], dst[sel], n_rows)
                 ws = None if weights is None else weights[sel][od].float().contiguous().to(dev)
-                segs.append((ip.to(dev), ix.to(dev), ws))
-        self.rels[ce] = RelShard(ce, 'partial', indptr.to(dev), indices.to(dev),
+                segs.append((_planned(ip.to(dev)), ix.to(dev), ws))
+        self.rels[ce] = RelShard(ce, 'partial', _planned(indptr.to(dev)), indices.to(dev),
                                  None if w is None else w.to(dev), n_rows, global_edges,
                                  deg[self.own_slice(d_t)].contiguous().to(dev), segs)
 
