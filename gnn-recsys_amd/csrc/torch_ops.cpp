@@ -697,6 +697,108 @@ void hold_cus(int64_t blocks, int64_t threads, int64_t lds_bytes, int64_t usec, 
      "gnnrec_hold_cus");
 }
 
+// ---------------------------------------------------------------- a9 one sampled layer
+// The whole of one block layer of BlockSampler.sample_blocks (gnnrec/sampling.py) issued
+// from C++: per relation count -> scan; ONE host read of the sampled edge counts; fills;
+// per node type the to_block relabel (prefix map, marks of the new sources, scan); ONE
+// host read of the new-source counts; compaction, relabel of every relation's sources,
+// scratch reset.  The same kernels in the same order with the same keys as the Python
+// form it replaces (bitwise the same blocks), minus ≈ 40 Python-level launches per layer
+// (the C2 step's sampler spent 1.5 ms of host time per batch on them).
+//   relations r: CSR (indptr, indices int32, eids), optional exclusion mask, source / dst
+//   node-type index, fanout (-1 = all), RNG key; node types t: the seeds (dst prefix) and
+//   the Relabeler scratch (prefix_pos int64 [n_t] = -1, mark int32 [n_t] = 0, restored on
+//   exit).  Returns per relation (out indptr, local src int32, eids), per type the src
+//   node ids (prefix first), and the edge counts.
+Tensor exclusive_scan_new(const Tensor& x) {
+  const int64_t n = x.numel();
+  Tensor out = at::empty({n + 1}, x.options().dtype(at::kLong));
+  Tensor ws = at::empty({std::max<int64_t>(1, (gnnrec_scan_workspace_bytes(n) + 7) / 8)},
+                        x.options().dtype(at::kLong));
+  exclusive_scan(x, out, ws);
+  return out;
+}
+
+std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>,
+           std::vector<int64_t>>
+sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids,
+             const c10::List<optional<Tensor>>& masks, at::IntArrayRef src_type,
+             at::IntArrayRef dst_type, at::IntArrayRef fanouts, at::IntArrayRef keys,
+             at::TensorList seeds, at::TensorList prefix_pos, at::TensorList marks) {
+  const size_t R = indptrs.size(), NT = seeds.size();
+  TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && masks.size() == R &&
+                        src_type.size() == R && dst_type.size() == R && fanouts.size() == R &&
+                        keys.size() == R,
+                    "sample_layer: one entry per relation in every relation list");
+  TORCH_CHECK_VALUE(prefix_pos.size() == NT && marks.size() == NT,
+                    "sample_layer: one seed list and one scratch pair per node type");
+  for (size_t r = 0; r < R; ++r)
+    TORCH_CHECK_VALUE(src_type[r] >= 0 && (size_t)src_type[r] < NT && dst_type[r] >= 0 &&
+                          (size_t)dst_type[r] < NT,
+                      "sample_layer: node-type index out of range");
+  TORCH_CHECK_VALUE(NT > 0, "sample_layer: no node types");
+  const c10::DeviceGuard g(seeds[0].device());
+  // counts -> out indptr per relation
+  std::vector<Tensor> o_ip(R), o_src(R), o_eid(R), src_loc(R), src_nid(NT);
+  for (size_t r = 0; r < R; ++r) {
+    const Tensor& sd = seeds[dst_type[r]];
+    Tensor counts = at::empty({sd.numel()}, sd.options().dtype(at::kLong));
+    const optional<Tensor> m = masks.get(r);
+    sample_count(indptrs[r], eids[r], m, sd, fanouts[r], keys[r], counts);
+    o_ip[r] = exclusive_scan_new(counts);
+  }
+  std::vector<int64_t> totals(R, 0);
+  if (R) {
+    std::vector<Tensor> last;
+    for (size_t r = 0; r < R; ++r) last.push_back(o_ip[r].narrow(0, o_ip[r].numel() - 1, 1));
+    const Tensor t = at::cat(last).to(at::kCPU);  // the layer's one size readback
+    for (size_t r = 0; r < R; ++r) totals[r] = t.data_ptr<int64_t>()[r];
+  }
+  for (size_t r = 0; r < R; ++r) {
+    const Tensor& sd = seeds[dst_type[r]];
+    o_src[r] = at::empty({totals[r]}, sd.options().dtype(at::kLong));
+    o_eid[r] = at::empty({totals[r]}, sd.options().dtype(at::kLong));
+    const optional<Tensor> m = masks.get(r);
+    sample_fill(indptrs[r], indices[r], eids[r], m, sd, fanouts[r], keys[r], o_ip[r], o_src[r],
+                o_eid[r]);
+  }
+  // relabel: per node type, mark the new sources and scan
+  std::vector<Tensor> rank(NT);
+  for (size_t t = 0; t < NT; ++t) {
+    Tensor pp = prefix_pos[t], mk = marks[t];
+    set_prefix_pos(seeds[t], pp);
+    for (size_t r = 0; r < R; ++r)
+      if ((size_t)src_type[r] == t) mark_ids(o_src[r], pp, mk);
+    rank[t] = exclusive_scan_new(mk);
+  }
+  std::vector<int64_t> n_new(NT, 0);
+  {
+    std::vector<Tensor> last;
+    for (size_t t = 0; t < NT; ++t) last.push_back(rank[t].narrow(0, rank[t].numel() - 1, 1));
+    const Tensor c = at::cat(last).to(at::kCPU);  // the layer's second size readback
+    for (size_t t = 0; t < NT; ++t) n_new[t] = c.data_ptr<int64_t>()[t];
+  }
+  for (size_t t = 0; t < NT; ++t) {
+    Tensor pp = prefix_pos[t], mk = marks[t];
+    const Tensor& pre = seeds[t];
+    const int64_t n_p = pre.numel();
+    Tensor nodes = at::empty({n_p + n_new[t]}, pre.options().dtype(at::kLong));
+    nodes.narrow(0, 0, n_p).copy_(pre);
+    Tensor fresh = nodes.narrow(0, n_p, n_new[t]);
+    if (n_new[t]) compact_marked(mk, rank[t], fresh);
+    for (size_t r = 0; r < R; ++r) {
+      if ((size_t)src_type[r] != t) continue;
+      Tensor loc = at::empty({o_src[r].numel()}, pre.options().dtype(at::kLong));
+      relabel_ids(o_src[r], pp, rank[t], n_p, loc);
+      src_loc[r] = loc.to(at::kInt);
+    }
+    clear_prefix_pos(pre, pp);
+    if (n_new[t]) mk.index_fill_(0, fresh, 0);
+    src_nid[t] = nodes;
+  }
+  return {o_ip, src_loc, o_eid, src_nid, totals};
+}
+
 // ---------------------------------------------------------------- host-only queries
 int64_t version() { return gnnrec_version(); }
 void set_concurrency(int64_t reserve_cus, bool dynamic) {
@@ -796,6 +898,10 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("synth_edges(int seed, int e0, int n_u, int n_i, Tensor? zipf_cdf, Tensor(a!) u, "
         "Tensor(b!) i) -> ()");
   m.def("hold_cus(int blocks, int threads, int lds_bytes, int usec, Tensor(a!) sink) -> ()");
+  m.def("sample_layer(Tensor[] indptrs, Tensor[] indices, Tensor[] eids, Tensor?[] masks, "
+        "int[] src_type, int[] dst_type, int[] fanouts, int[] keys, Tensor[] seeds, "
+        "Tensor(a!)[] prefix_pos, Tensor(b!)[] marks) -> "
+        "(Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, Tensor[] src_nid, int[] n_edges)");
   // host-only entry points (no tensors: one catch-all kernel each)
   m.def("version() -> int", &version);
   m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);
@@ -850,7 +956,10 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("hold_cus", &hold_cus)
 
 // HIP tensors dispatch under the CUDA key in ROCm PyTorch.
-TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) { GNNREC_IMPLS(m); }
+TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) {
+  GNNREC_IMPLS(m);
+  m.impl("sample_layer", &sample_layer);  // data-dependent sizes: device only, no meta form
+}
 // Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
 TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }
 // CPU tensors: the same functions refuse them in their first operand check (ValueError:

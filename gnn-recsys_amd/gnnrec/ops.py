@@ -825,6 +825,19 @@ def sample_neighbors(indptr, indices, eids, seeds, fanout: int, seed_key: int = 
     return out_indptr, out_src, out_eid
 
 
+def sample_layer(indptrs, indices, eids, masks, src_type, dst_type, fanouts, keys, seeds,
+                 prefix_pos, marks):
+    """a9, one block layer in one call (gnnrec::sample_layer): sampled in-edges of every
+    relation's seeds + the to_block relabel of every node type, two host size reads.
+    -> ([out_indptr], [local src int32], [eids], [src node ids per type], [edge counts])."""
+    for t in list(indptrs) + list(eids) + list(seeds) + list(prefix_pos):
+        _dev(t, "sample_layer operand", torch.int64)
+    fans = [-1 if f is None or f < 0 else int(f) for f in fanouts]
+    return _T().sample_layer(list(indptrs), list(indices), list(eids), list(masks),
+                             list(src_type), list(dst_type), fans, [_lib.i64(k) for k in keys],
+                             list(seeds), list(prefix_pos), list(marks))
+
+
 class Relabeler:
     """Per-node-type scratch for to_block relabelling (mark array + prefix map).
 

@@ -118,7 +118,35 @@ class BlockSampler:
 
     def _one_block(self, g, seeds, block_id, masks) -> Block:
         """One layer: counts of every relation, ONE size readback, fills; then the
-        new-source marks of every node type, ONE size readback, compaction/relabel."""
+        new-source marks of every node type, ONE size readback, compaction/relabel —
+        issued from C++ by the gnnrec::sample_layer op (same kernels, same order, same
+        keys as _one_block_py, which stays as the readable form)."""
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        ces = list(g.canonical_etypes)
+        nts = list(g.ntypes)
+        tix = {nt: i for i, nt in enumerate(nts)}
+        csrs = [g.in_csr_global(ce) for ce in ces]
+        fans = [self._fanout(block_id, ce) for ce in ces]
+        rel = [self._relabeler(g, nt) for nt in nts]
+        o_ip, src_loc, o_eid, src_nid, totals = ops.sample_layer(
+            [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
+            [masks.get(ce, (None,))[0] for ce in ces], [tix[ce[0]] for ce in ces],
+            [tix[ce[2]] for ce in ces], fans,
+            [_mix(self.seed, self._calls, block_id, r) for r in range(len(ces))],
+            [seeds.get(nt, empty) for nt in nts], [r.prefix_pos for r in rel],
+            [r.mark for r in rel])
+        rels = {}
+        for r, ce in enumerate(ces):
+            ip = o_ip[r]
+            ip._gnnrec_nnz = int(totals[r])  # edge count known on the host: no later readback
+            if fans[r] is not None and 0 <= fans[r] <= ops.DEFAULT_SPLIT:
+                ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows possible
+            rels[ce] = (ip, src_loc[r], o_eid[r])
+        num_dst = {nt: int(seeds.get(nt, empty).numel()) for nt in nts}
+        return Block(dict(zip(nts, src_nid)), num_dst, rels)
+
+    def _one_block_py(self, g, seeds, block_id, masks) -> Block:
+        """_one_block issued from Python, op by op (the reference form of the C++ op)."""
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
         plan = []
         for r_idx, ce in enumerate(g.canonical_etypes):

@@ -389,3 +389,37 @@ def test_fanout_sampler_is_uniform():
         counts += np.bincount(e - np.repeat(np.arange(n_u), fan) * deg, minlength=deg)
     exp = counts.sum() / deg
     assert chi2.sf(float(((counts - exp) ** 2 / exp).sum()), deg - 1) > 1e-4
+
+
+@pytest.mark.parametrize("fanouts", [None, [3, 2], [{"buys": 2, "bought-by": 4}, 1]])
+def test_cpp_sample_layer_equals_python_form(fanouts):
+    """gnnrec::sample_layer (the layer issued from C++) builds the same blocks, bit for bit,
+    as the op-by-op Python form it replaces: seeds of both types, a type with no seeds,
+    exclusion masks, full and fanout sampling, per-relation fanouts."""
+    from gnnrec.sampling import MultiLayerFullNeighborSampler, MultiLayerNeighborSampler
+    g, edges = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    mk = (lambda: MultiLayerFullNeighborSampler(2)) if fanouts is None else \
+        (lambda: MultiLayerNeighborSampler(fanouts, seed=9))
+    seed_sets = [{"user": torch.arange(0, 300, 5, device=DEV),
+                  "item": torch.tensor([3, 1, 77, 5], device=DEV)},
+                 {"item": torch.arange(0, 120, 3, device=DEV)}]
+    for seeds in seed_sets:
+        for excl in (None, {BUYS: torch.arange(0, 4000, 3, device=DEV)}):
+            blocks = []
+            for impl in ("_one_block", "_one_block_py"):
+                s = mk()
+                masks = {}
+                if excl:
+                    for ce, e in excl.items():
+                        m = s._mask(g, ce)
+                        m[e] = 1
+                        masks[ce] = (m, e)
+                blocks.append(getattr(s, impl)(g, seeds, 1, masks))
+            a, b = blocks
+            assert a.canonical_etypes == b.canonical_etypes and a._num_dst == b._num_dst
+            for nt in a.ntypes:
+                assert torch.equal(a._src[nt]["_ID"], b._src[nt]["_ID"]), nt
+            for ce in a.canonical_etypes:
+                for x, y in zip(a._rels[ce], b._rels[ce]):
+                    assert x.dtype == y.dtype and torch.equal(x, y), ce
+                assert a._rels[ce][0]._gnnrec_nnz == b._rels[ce][0]._gnnrec_nnz
