@@ -13,6 +13,36 @@ struct Frag {
   float v[VEC];
 };
 
+// Streams read or written once per launch (CSR indices / indptr, self rows, outputs and
+// partials) vs the gathered source table, which should keep the caches: with
+// GNNREC_NT_STREAM=1 (default) the streams use non-temporal loads / stores: C4 pass 143.0 -> 142.3
+// ms in an alternating A/B (tools/micro/bench_ab.sh; tiles 4.45 -> 4.42 ms, fused 34.58 -> 34.45).
+#ifndef GNNREC_NT_STREAM
+#define GNNREC_NT_STREAM 1
+#endif
+typedef float f32x4s __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (GNNREC_NT_STREAM) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+__device__ __forceinline__ float4 ld_stream4(const float* p) {
+  if constexpr (GNNREC_NT_STREAM) {
+    const f32x4s t = __builtin_nontemporal_load(reinterpret_cast<const f32x4s*>(p));
+    return make_float4(t[0], t[1], t[2], t[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+__device__ __forceinline__ void st_stream4(float* p, float a, float b, float c, float d) {
+  if constexpr (GNNREC_NT_STREAM) {
+    const f32x4s t = {a, b, c, d};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4s*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+  }
+}
+
 template <int VEC>
 __device__ __forceinline__ void load_frag(Frag<VEC>& f, const float* p) {
   if constexpr (VEC == 4) {
@@ -26,7 +56,7 @@ __device__ __forceinline__ void load_frag(Frag<VEC>& f, const float* p) {
 template <int VEC>
 __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   if constexpr (VEC == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
+    st_stream4(p, f.v[0], f.v[1], f.v[2], f.v[3]);
   } else {
     *p = f.v[0];
   }
@@ -52,9 +82,9 @@ __device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
     const int cnt = (int)((end - base) < 64 ? (end - base) : 64);
     int myidx;
     if (PRE && base == beg) myidx = pre_idx;
-    else myidx = lane < cnt ? indices[base + lane] : 0;
+    else myidx = lane < cnt ? ld_stream(indices + base + lane) : 0;
     float myw = 0.f;
-    if constexpr (WEIGHTED) myw = lane < cnt ? ew[base + lane] : 0.f;
+    if constexpr (WEIGHTED) myw = lane < cnt ? ld_stream(ew + base + lane) : 0.f;
     for (int j = 0; j < cnt; j += NPI * UNROLL) {
       Frag<VEC> val[UNROLL];
       bool ok[UNROLL];
@@ -101,7 +131,12 @@ __device__ __forceinline__ void combine_groups(Frag<VEC>& acc) {
 template <int VEC, int REDUCE>
 __device__ __forceinline__ void accumulate_into(Frag<VEC>& acc, const float* p) {
   Frag<VEC> o;
-  load_frag<VEC>(o, p);
+  if constexpr (VEC == 4) {
+    const float4 t = ld_stream4(p);
+    o.v[0] = t.x; o.v[1] = t.y; o.v[2] = t.z; o.v[3] = t.w;
+  } else {
+    load_frag<VEC>(o, p);
+  }
 #pragma unroll
   for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(o.v[v], acc.v[v]);
 }

@@ -83,15 +83,15 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     // source-row chain only the last link stays exposed at a row boundary
     rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
       const int nr = (int)(r1 - r0);  // <= 64
-      const int64_t ipl = lane < nr ? indptr[r0 + lane] : 0;
+      const int64_t ipl = lane < nr ? ld_stream(indptr + r0 + lane) : 0;
       const int64_t ip_end = indptr[r1];
       auto bound = [&](int k) { return k < nr ? __shfl(ipl, k) : ip_end; };
       int64_t beg = bound(0), end = bound(1);
-      int nidx = lane < end - beg ? indices[beg + lane] : 0;
+      int nidx = lane < end - beg ? ld_stream(indices + beg + lane) : 0;
       for (int k = 0; k < nr; ++k) {
         const int idx = nidx;
         const int64_t nbeg = end, nend = k + 1 < nr ? bound(k + 2) : end;
-        if (k + 1 < nr) nidx = lane < nend - nbeg ? indices[nbeg + lane] : 0;
+        if (k + 1 < nr) nidx = lane < nend - nbeg ? ld_stream(indices + nbeg + lane) : 0;
         if (end - beg <= max_deg) {  // heavy rows: reduced by the chunk kernels
           Frag<VEC> acc;
 #pragma unroll

@@ -113,7 +113,12 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool
     y0 = y0 / e.out_div;
     y1 = y1 / e.out_div;
   }
-  *p = make_float2(y0, y1);
+  if constexpr (GNNREC_NT_STREAM) {
+    typedef float f32x2s __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(f32x2s{y0, y1}, reinterpret_cast<f32x2s*>(p));
+  } else {
+    *p = make_float2(y0, y1);
+  }
 }
 
 template <int REDUCE, bool WEIGHTED, int UNROLL>
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
     // either row gathers: the second row's indptr -> indices chain hides under the first
     // row's gather (it is the fixed per-row cost that low-degree relations feel)
     const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);  // valid rows, >= 1
-    const int64_t ipl = lane <= nv ? indptr[row0 + lane] : 0;
+    const int64_t ipl = lane <= nv ? ld_stream(indptr + row0 + lane) : 0;
     int64_t rb[kPRows + 1];
 #pragma unroll
     for (int r = 0; r <= kPRows; ++r) rb[r] = __shfl(ipl, r <= nv ? r : nv);
@@ -165,9 +170,9 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 #pragma unroll
     for (int r = 0; r < kPRows; ++r) {
       const bool valid = r < nv;  // uniform per wave
-      pidx[r] = valid && lane < rb[r + 1] - rb[r] ? indices[rb[r] + lane] : 0;
+      pidx[r] = valid && lane < rb[r + 1] - rb[r] ? ld_stream(indices + rb[r] + lane) : 0;
       hsr[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid && grp == 1) hsr[r] = *reinterpret_cast<const float4*>(H + (row0 + r) * ldh + col);
+      if (valid && grp == 1) hsr[r] = ld_stream4(H + (row0 + r) * ldh + col);
     }
 #pragma unroll
     for (int r = 0; r < kPRows; ++r) {
