@@ -167,7 +167,21 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
       Frag<VEC> acc;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc.v[v] = init;
-      for (int64_t c = chunk_ptr[h]; c < chunk_ptr[h + 1]; ++c) {
+      // chunk partials in chunk order; 16 loads in flight ahead of the (ordered) adds: a
+      // Zipf head row has thousands of chunks per tile, and one load per add made its
+      // combine a 0.87 ms latency chain (C4 --zipf 1.0, 16 launches per pass)
+      const int64_t c_end = chunk_ptr[h + 1];
+      int64_t c = chunk_ptr[h];
+      for (; c + 16 <= c_end; c += 16) {
+        Frag<VEC> p[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) load_frag<VEC>(p[u], ws + (c + u) * (int64_t)d + col);
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc.v[v] = combine<REDUCE>(acc.v[v], p[u].v[v]);
+      }
+      for (; c < c_end; ++c) {
         Frag<VEC> p;
         load_frag<VEC>(p, ws + c * (int64_t)d + col);
 #pragma unroll
