@@ -88,14 +88,23 @@ class RelShard:
         return int(self.indices.numel())
 
 
-def _planned(indptr: torch.Tensor) -> torch.Tensor:
+def _planned(indptr: torch.Tensor, split: int = ops.DEFAULT_SPLIT) -> torch.Tensor:
     """A shard CSR with its heavy-row plan computed once, at setup (one host readback):
     the pass then launches the plain aggregation kernel when no row is heavy, instead of
     the device-planned form's plan / chunk / combine launches on every pass (C5: 32 extra
     launches per layer, ≈1.5 ms)."""
     if indptr.is_cuda:
-        ops.split_plan(indptr)
+        ops.split_plan(indptr, split)
     return indptr
+
+
+# Source-range tiles are reduced by the plain aggregation kernel, never by the fused one, so
+# their heavy rows can be chunked finer than the fused kernel's eligibility threshold
+# (DEFAULT_SPLIT): one wave per 512 edges instead of per 2048 spreads a Zipf head over 4x
+# the waves — C4 --zipf 1.0 pass 164.2 -> 142.6 ms (split 256: 146.3, 1024: 149.1); the
+# uniform configs have no tile row that long.  Every rank uses the same split, so the
+# deterministic tree stays bitwise P-invariant.
+TILE_SPLIT = 512
 
 
 class GraphShard:
@@ -198,7 +207,7 @@ class GraphShard:
                 sel = (key >= bounds[sg]) & (key < bounds[sg + 1])
                 ip, ix, od = build_csr(src_loc[sel], dst[sel], n_rows)
                 ws = None if weights is None else weights[sel][od].float().contiguous().to(dev)
-                segs.append((_planned(ip.to(dev)), ix.to(dev), ws))
+                segs.append((_planned(ip.to(dev), TILE_SPLIT), ix.to(dev), ws))
         self.rels[ce] = RelShard(ce, 'partial', _planned(indptr.to(dev)), indices.to(dev),
                                  None if w is None else w.to(dev), n_rows, global_edges,
                                  deg[self.own_slice(d_t)].contiguous().to(dev), segs)
@@ -509,7 +518,8 @@ class ShardedFullGraphPass:
                     for j, (ip, ix, w) in enumerate(rs.segs):
                         with self._time('spmm_tile'):
                             O.spmm(ip, ix, msg, op, edge_weight=w if weighted else None,
-                                   empty_neginf=op == 'max', out=part, accumulate=j > 0)
+                                   empty_neginf=op == 'max', out=part, accumulate=j > 0,
+                                   split=TILE_SPLIT)
                     own, work = self.ex.reduce_scatter_rows(part, op, async_op=self.overlap)
                     partials[ce] = (own, work, reduce)
                     continue
@@ -563,10 +573,11 @@ class ShardedFullGraphPass:
                 ew = w if weighted else None
                 with self._time('spmm_tile'):
                     if j % 2 == 0:
-                        parts[ce].append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew))
+                        parts[ce].append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew,
+                                                       split=TILE_SPLIT))
                     else:
                         self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[ce][-1],
-                                      accumulate=True)
+                                      accumulate=True, split=TILE_SPLIT)
         out = {}
         for ce, rs, msg, weighted, reduce in rels:
             blocks, work = self.ex.all_to_all_rows(_tree_sum(parts[ce], self.ops),

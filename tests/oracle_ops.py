@@ -11,7 +11,7 @@ from oracle import oracle
 
 
 def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_neginf=False,
-         accumulate=False):
+         accumulate=False, split=None):  # split: the HIP op's heavy-row chunking (no-op here)
     ip = indptr.cpu().numpy()
     res = oracle.spmm_csr(ip, indices.cpu().numpy(), X.detach().cpu().numpy(), reduce,
                           None if edge_weight is None else edge_weight.cpu().numpy())
