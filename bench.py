@@ -101,6 +101,8 @@ KERNELS = {
                           "+ mean of 32-row tiles, SAGE projection on fp32 MFMA, ReLU, L2 norm)"),
     "spmm_tile": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented sum of one "
                   "source-range tile, accumulated in place)"),
+    "spmm_tile2": ("spmm_csr2_kernel", "gnnrec spmm_csr2_kernel (gather + segmented sums of two "
+                   "relations' source-range tiles from one table in one launch)"),
     "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
 }
 
@@ -111,8 +113,15 @@ def launch_bytes(shard, d, runner, deterministic):
     (int64 indptr) + d*4 (write), + d*4 for the h_self row when the projection is fused
     into the launch, + d*4 for the partial read back when a tile accumulates in place."""
     out = {}
+    paired = {c: pair for pair in runner.tile_pairs for c in pair}
     for ce, rs in shard.rels.items():
-        if ce in runner.fused:
+        if ce in paired:  # both relations' tile bytes, one launch per segment for the pair
+            tag, b = "spmm_tile2", 0
+            n = len(rs.segs) if ce == paired[ce][0] else 0
+            for j, (ip, ix, _) in enumerate(rs.segs):
+                acc = (j % 2 == 1) if deterministic else j > 0
+                b += ix.numel() * (d * 4 + 4) + rs.n_rows * (8 + 4 * d * (2 if acc else 1))
+        elif ce in runner.fused:
             avg = rs.global_edges / max(shard.num_nodes[ce[2]], 1) if deterministic else None
             tag = runner._fused_tag(rs, avg)
             b, n = rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + 8 * d), 1

@@ -224,11 +224,11 @@ inline unsigned grid_waves(int64_t units) {
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
 
-template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
-int launch_all(const SpmmArgs& a, hipStream_t s) {
 #ifndef GNNREC_SPMM_UNROLL
 #define GNNREC_SPMM_UNROLL 4
 #endif
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
+int launch_all(const SpmmArgs& a, hipStream_t s) {
   constexpr int UNROLL = (VEC == 4) ? GNNREC_SPMM_UNROLL : 2;
   const int cols_per_slice = LPR * VEC;
   const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
@@ -254,6 +254,94 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
                        a.out, a.ldo, eni, a.counts);
   }
   return check_launch("gnnrec_spmm_csr_f32");
+}
+
+// ---- two relations into one destination type, one launch ----------------------------
+// C5's user->item relations (clicks: 50 edges per item row and source tile, buys: 12.5)
+// gather from the same user slice into separate partial tables.  Launched apart, the
+// low-degree relation's tiles are bound by their per-row latency chain (1.2-1.36 ms for
+// 12.5M edges); here every queue ticket takes rows [r0, r1) of relation A and then the
+// same rows of relation B, so the short rows run beside long ones on every wave.  Each
+// relation's rows are reduced exactly as by spmm_csr_kernel (bitwise the same partials).
+// No heavy-row split (callers check both CSRs are plan-free), one column slice (d <= 256).
+struct Csr2 {
+  const int64_t* indptr[2];
+  const int32_t* indices[2];
+  const float* ew[2];
+  float* out[2];
+};
+
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
+__global__ __launch_bounds__(256) void spmm_csr2_kernel(Csr2 c, const float* __restrict__ X,
+                                                        int64_t ldx, int64_t n_dst, int d,
+                                                        int64_t ldo, int flags, unsigned* rq,
+                                                        int rq_ch) {
+  const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / LPR;
+  const int col = (lane % LPR) * VEC;
+  const bool colok = col < d;
+  const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
+  // rows [r0, r1) of relation rel: the queued row loop of spmm_csr_kernel
+  auto rows = [&](const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                  const float* __restrict__ ew, float* __restrict__ out, int64_t r0,
+                  int64_t r1) __attribute__((always_inline)) {
+    const int nr = (int)(r1 - r0);  // <= 64
+    const int64_t ipl = lane < nr ? ld_stream(indptr + r0 + lane) : 0;
+    const int64_t ip_end = indptr[r1];
+    auto bound = [&](int k) { return k < nr ? __shfl(ipl, k) : ip_end; };
+    int64_t beg = bound(0), end = bound(1);
+    int nidx = lane < end - beg ? ld_stream(indices + beg + lane) : 0;
+    for (int k = 0; k < nr; ++k) {
+      const int idx = nidx;
+      const int64_t nbeg = end, nend = k + 1 < nr ? bound(k + 2) : end;
+      if (k + 1 < nr) nidx = lane < nend - nbeg ? ld_stream(indices + nbeg + lane) : 0;
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = init;
+      gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(beg, end, indices, ew, X, ldx, col,
+                                                             colok, lane, grp, acc, idx);
+      combine_groups<LPR, VEC, REDUCE>(acc);
+      finalize<VEC, REDUCE>(acc, end - beg, empty_neginf);
+      const int64_t row = r0 + k;
+      if (grp == 0 && colok) {
+        if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(acc, out + row * ldo + col);
+        store_frag<VEC>(out + row * ldo + col, acc);
+      }
+      beg = nbeg;
+      end = nend;
+    }
+  };
+  auto both = [&](int64_t r0, int64_t r1) __attribute__((always_inline)) {
+    rows(c.indptr[0], c.indices[0], c.ew[0], c.out[0], r0, r1);
+    rows(c.indptr[1], c.indices[1], c.ew[1], c.out[1], r0, r1);
+  };
+  if (rq != nullptr) {
+    if (rq_ch <= 0) {  // ≈ kRqTicketEdges edges of both relations per ticket
+      const int64_t e = c.indptr[0][n_dst] - c.indptr[0][0] + c.indptr[1][n_dst] - c.indptr[1][0];
+      const int64_t avg = e / n_dst, ch = kRqTicketEdges / (avg > 0 ? avg : 1);
+      rq_ch = (int)(ch < 1 ? 1 : ch > 64 ? 64 : ch);
+    }
+    rq_for_each(rq, n_dst, rq_ch, both);
+    rq_finish(rq);
+    return;
+  }
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n_dst; row += wstride)
+    both(row, row + 1);
+}
+
+template <int LPR, int REDUCE, bool WEIGHTED>
+int launch_csr2(const Csr2& c, const float* X, int64_t ldx, int64_t n_dst, int d, int64_t ldo,
+                int flags, hipStream_t s) {
+  const unsigned grid = grid_waves(n_dst);
+  int ticket = -1;
+  unsigned* rq = n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot(s, &ticket) : nullptr;
+  hipLaunchKernelGGL((spmm_csr2_kernel<LPR, 4, REDUCE, WEIGHTED, GNNREC_SPMM_UNROLL>),
+                     dim3(grid), dim3(256), 0, s, c, X, ldx, n_dst, d, ldo, flags, rq,
+                     row_chunk());
+  rowq_launched(ticket, s);
+  return check_launch("gnnrec_spmm_csr2_f32");
 }
 
 template <int VEC, int REDUCE, bool WEIGHTED>
@@ -557,4 +645,48 @@ extern "C" int gnnrec_spmm_backward_f32(const int64_t* indptr, const int32_t* in
 #undef GNNREC_BWD_W
 #undef GNNREC_BWD_NC
   return check_launch("gnnrec_spmm_backward_f32");
+}
+
+extern "C" int gnnrec_spmm_csr2_f32(const int64_t* indptr_a, const int32_t* indices_a,
+                                    const float* ew_a, const int64_t* indptr_b,
+                                    const int32_t* indices_b, const float* ew_b, const float* X,
+                                    int64_t ldx, int64_t n_dst, int64_t d, int reduce, int flags,
+                                    float* out_a, float* out_b, int64_t ldo, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_dst >= 0 && d >= 0, "gnnrec_spmm_csr2_f32: negative size");
+  GNNREC_REQUIRE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN ||
+                     reduce == GNNREC_REDUCE_MAX,
+                 "gnnrec_spmm_csr2_f32: unknown reduce %d", reduce);
+  GNNREC_REQUIRE((ew_a == nullptr) == (ew_b == nullptr),
+                 "gnnrec_spmm_csr2_f32: edge weights on both relations or on neither");
+  if (n_dst == 0 || d == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(indptr_a && indptr_b && X && out_a && out_b, "gnnrec_spmm_csr2_f32: null pointer");
+  GNNREC_REQUIRE(d % 4 == 0 && d <= 256 && ldx % 4 == 0 && ldo % 4 == 0 && ldx >= d && ldo >= d &&
+                     aligned16(X) && aligned16(out_a) && aligned16(out_b),
+                 "gnnrec_spmm_csr2_f32: needs d %% 4 == 0, d <= 256 and 16-B aligned rows");
+  Csr2 c{{indptr_a, indptr_b}, {indices_a, indices_b}, {ew_a, ew_b}, {out_a, out_b}};
+  hipStream_t s = as_stream(stream);
+  const int eni = flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
+  int lpr = 4;
+  while (lpr < d / 4 && lpr < 64) lpr <<= 1;
+#define GNNREC_CSR2(L)                                                                        \
+  do {                                                                                        \
+    const bool w = ew_a != nullptr;                                                           \
+    if (reduce == GNNREC_REDUCE_SUM)                                                          \
+      return w ? launch_csr2<L, GNNREC_REDUCE_SUM, true>(c, X, ldx, n_dst, (int)d, ldo, eni, s)  \
+               : launch_csr2<L, GNNREC_REDUCE_SUM, false>(c, X, ldx, n_dst, (int)d, ldo, eni, s); \
+    if (reduce == GNNREC_REDUCE_MEAN)                                                         \
+      return w ? launch_csr2<L, GNNREC_REDUCE_MEAN, true>(c, X, ldx, n_dst, (int)d, ldo, eni, s) \
+               : launch_csr2<L, GNNREC_REDUCE_MEAN, false>(c, X, ldx, n_dst, (int)d, ldo, eni, s); \
+    return w ? launch_csr2<L, GNNREC_REDUCE_MAX, true>(c, X, ldx, n_dst, (int)d, ldo, eni, s)    \
+             : launch_csr2<L, GNNREC_REDUCE_MAX, false>(c, X, ldx, n_dst, (int)d, ldo, eni, s);  \
+  } while (0)
+  switch (lpr) {
+    case 4: GNNREC_CSR2(4);
+    case 8: GNNREC_CSR2(8);
+    case 16: GNNREC_CSR2(16);
+    case 32: GNNREC_CSR2(32);
+    default: GNNREC_CSR2(64);
+  }
+#undef GNNREC_CSR2
 }

@@ -111,6 +111,33 @@ void spmm_csr_split(const Tensor& indptr, const Tensor& indices, const optional<
      "gnnrec_spmm_csr_split_f32");
 }
 
+void spmm_csr2(const Tensor& indptr_a, const Tensor& indices_a, const optional<Tensor>& ew_a,
+               const Tensor& indptr_b, const Tensor& indices_b, const optional<Tensor>& ew_b,
+               const Tensor& X, int64_t reduce, int64_t flags, Tensor& out_a, Tensor& out_b) {
+  dev(indptr_a, "indptr_a", at::kLong);
+  dev(indices_a, "indices_a", at::kInt);
+  dev(ew_a, "ew_a", at::kFloat);
+  dev(indptr_b, "indptr_b", at::kLong);
+  dev(indices_b, "indices_b", at::kInt);
+  dev(ew_b, "ew_b", at::kFloat);
+  dev(X, "X", at::kFloat);
+  dev(out_a, "out_a", at::kFloat);
+  dev(out_b, "out_b", at::kFloat);
+  const int64_t n_dst = indptr_a.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1, "spmm_csr2: the relations' row counts differ");
+  TORCH_CHECK_VALUE(out_a.size(0) == n_dst && out_a.size(1) == d && out_b.sizes() == out_a.sizes(),
+                    "out_a / out_b must be [", n_dst, ", ", d, "]");
+  const int64_t ldx = ld(X, "X"), ldo = ld(out_a, "out_a");
+  TORCH_CHECK_VALUE(ld(out_b, "out_b") == ldo, "out_a and out_b must share a row stride");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  ck(gnnrec_spmm_csr2_f32(p<int64_t>(indptr_a), p<int32_t>(indices_a), p<float>(ew_a),
+                          p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b), p<float>(X),
+                          ldx, n_dst, d, (int)reduce, (int)flags, p<float>(out_a), p<float>(out_b),
+                          ldo, stream_of(X)),
+     "gnnrec_spmm_csr2_f32");
+}
+
 void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor& plan) {
   dev(indptr, "indptr", at::kLong);
   dev(plan, "plan", at::kLong);
@@ -843,6 +870,9 @@ TORCH_LIBRARY(gnnrec, m) {
         "int reduce, int flags, int split, Tensor heavy_rows, Tensor chunk_ptr, "
         "Tensor chunk_row, int n_chunks, Tensor(a!) out, Tensor(b!) workspace) -> ()");
   m.def("spmm_plan_build(Tensor indptr, int split, int cap_h, Tensor(a!) plan) -> ()");
+  m.def("spmm_csr2(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, Tensor indptr_b, "
+        "Tensor indices_b, Tensor? ew_b, Tensor X, int reduce, int flags, Tensor(a!) out_a, "
+        "Tensor(b!) out_b) -> ()");
   m.def("spmm_csr_planned(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, "
         "int reduce, int flags, int split, Tensor plan, int cap_h, int cap_c, Tensor(a!) out, "
         "Tensor(b!) workspace) -> ()");
@@ -923,6 +953,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("spmm_csr", &spmm_csr);                         \
   m.impl("spmm_csr_split", &spmm_csr_split);             \
   m.impl("spmm_plan_build", &spmm_plan_build);           \
+  m.impl("spmm_csr2", &spmm_csr2);                       \
   m.impl("spmm_csr_planned", &spmm_csr_planned);         \
   m.impl("spmm_backward", &spmm_backward);               \
   m.impl("gemm", &gemm);                                 \

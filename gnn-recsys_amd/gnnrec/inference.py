@@ -25,6 +25,7 @@ collectives overlap the user-side aggregation (async RCCL work handles).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -336,6 +337,7 @@ class ShardedFullGraphPass:
         self.timers = None  # optional callable(tag) -> context manager (bench)
         self.capture = None  # optional list: every layer's output tables are appended (tests)
         self.fused = set()  # relations whose aggregation ran with the projection fused
+        self.tile_pairs = set()  # (relation a, relation b) whose tiles ran as one launch
         self._last, self._replicate_last = False, True
 
     def _get(self, h, nt):
@@ -565,8 +567,25 @@ class ShardedFullGraphPass:
         # the same single add), the upper levels by _tree_sum
         parts = {ce: [] for ce, *_ in rels}
         n_seg = max((len(rs.segs) for _, rs, *_ in rels), default=0)
+        pairs = self._tile_pairs(rels)
         for j in range(n_seg):
-            for ce, rs, msg, weighted, _ in rels:
+            for item in pairs:
+                if len(item) == 2:  # two relations, one launch per tile (gnnrec_spmm_csr2_f32)
+                    (ca, ra, msg, weighted, _), (cb, rb, *_r) = item
+                    self.tile_pairs.add((ca, cb))
+                    sa, sb = ra.segs[j], rb.segs[j]
+                    csr_a = (sa[0], sa[1], sa[2] if weighted else None)
+                    csr_b = (sb[0], sb[1], sb[2] if weighted else None)
+                    with self._time('spmm_tile2'):
+                        if j % 2 == 0:
+                            pa, pb = self.ops.spmm2(csr_a, csr_b, msg, 'sum')
+                            parts[ca].append(pa)
+                            parts[cb].append(pb)
+                        else:
+                            self.ops.spmm2(csr_a, csr_b, msg, 'sum', out_a=parts[ca][-1],
+                                           out_b=parts[cb][-1], accumulate=True)
+                    continue
+                ce, rs, msg, weighted, _ = item[0]
                 if j >= len(rs.segs):
                     continue
                 ip, ix, w = rs.segs[j]
@@ -583,6 +602,37 @@ class ShardedFullGraphPass:
             blocks, work = self.ex.all_to_all_rows(_tree_sum(parts[ce], self.ops),
                                                    async_op=self.overlap)
             out[ce] = (blocks, work, reduce, 'tree')  # the owner's fold waits for the exchange
+        return out
+
+    def _tile_pairs(self, rels):
+        """Relations of one destination type grouped for the tile launches: two relations
+        that gather from the same table with the same segments and no heavy tile rows run as
+        one launch per tile (ops.spmm2: C5's clicks and buys); the rest alone.  Each pair's
+        partials are bitwise those of separate launches."""
+        pair_ok = getattr(self.ops, 'spmm2', None) is not None and \
+            os.environ.get("GNNREC_TILE_PAIRS", "1") != "0"
+        out, used = [], set()
+        for i, a in enumerate(rels):
+            if i in used:
+                continue
+            used.add(i)
+            for k in range(i + 1, len(rels)):
+                b = rels[k]
+                if not pair_ok or k in used or b[2] is not a[2] or b[3] != a[3] or \
+                        b[1].n_rows != a[1].n_rows or len(b[1].segs) != len(a[1].segs) or \
+                        a[2].shape[1] > 256 or a[2].shape[1] % 4:
+                    continue
+                segs = a[1].segs + b[1].segs
+                if any(not sg[0].is_cuda or ops.split_plan(sg[0], TILE_SPLIT) is not None
+                       for sg in segs):
+                    continue
+                if a[3] and any(sg[2] is None for sg in segs):
+                    continue
+                used.add(k)
+                out.append((a, b))
+                break
+            else:
+                out.append((a,))
         return out
 
     def _local(self, hconv, h, active, out):

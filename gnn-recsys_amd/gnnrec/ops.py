@@ -215,6 +215,36 @@ def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: s
     return out
 
 
+def spmm2(csr_a, csr_b, X: torch.Tensor, reduce: str = "sum", out_a=None, out_b=None,
+          accumulate: bool = False, empty_neginf: bool = False):
+    """a1 for two relations into one destination type in one launch (gnnrec_spmm_csr2_f32):
+    csr_* = (indptr, indices int32, edge_weight|None) over the same n_dst rows, both gathering
+    from X -> (out_a, out_b), each bitwise what spmm() gives for that relation.  No heavy-row
+    split: callers use it only for CSRs without heavy rows (split_plan(...) is None)."""
+    (ip_a, ix_a, w_a), (ip_b, ix_b, w_b) = csr_a, csr_b
+    for t, n in ((ip_a, "indptr_a"), (ip_b, "indptr_b")):
+        _dev(t, n, torch.int64)
+    _dev(X, "X", torch.float32)
+    if reduce not in REDUCE:
+        raise KeyError(f"Aggregator reduce {reduce} not recognized.")
+    if (w_a is None) != (w_b is None):
+        raise ValueError("spmm2: edge weights on both relations or on neither")
+    n_dst, d = ip_a.numel() - 1, X.shape[1]
+    if accumulate and (out_a is None or out_b is None):
+        raise ValueError("spmm2: accumulate needs out_a and out_b")
+    if out_a is None:
+        out_a = torch.empty((n_dst, d), dtype=torch.float32, device=X.device)
+    if out_b is None:
+        out_b = torch.empty((n_dst, d), dtype=torch.float32, device=X.device)
+    if accumulate and reduce == "max" and not empty_neginf:
+        raise ValueError("spmm2: max accumulation needs empty_neginf")
+    flags = (_lib.SPMM_EMPTY_NEGINF if empty_neginf else 0) | (_lib.SPMM_ACCUM if accumulate else 0)
+    _T().spmm_csr2(ip_a, ix_a, None if w_a is None else w_a.contiguous(), ip_b, ix_b,
+                   None if w_b is None else w_b.contiguous(), X, REDUCE[reduce], flags, out_a,
+                   out_b)
+    return out_a, out_b
+
+
 def csr_transpose(indptr: torch.Tensor, indices: torch.Tensor, n_src: int,
                   edge_weight: Optional[torch.Tensor] = None, mean: bool = False,
                   n_edges: Optional[int] = None):

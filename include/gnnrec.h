@@ -157,6 +157,20 @@ int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices, c
                                 const int64_t* plan, int64_t cap_h, int64_t cap_c,
                                 float* workspace, void* stream);
 
+/* Two relations into one destination type in one launch: out_a[v] = reduce over relation
+ * A's in-edges of v, out_b[v] likewise over relation B, both gathering from the same source
+ * table X (C5's clicks and buys source tiles: the 12.5-edges-per-row relation runs beside
+ * the 50-edges-per-row one on every wave instead of as its own latency-bound launch).  Each
+ * output row is bitwise what gnnrec_spmm_csr_f32 computes for that relation; reduce / flags
+ * apply to both.  No heavy-row split (callers route CSRs with rows above their split
+ * threshold to gnnrec_spmm_csr_split_f32); d % 4 == 0, d <= 256, 16-B aligned rows; ew_a and
+ * ew_b both given or both NULL.  Replaces two update_all calls of one HeteroGraphConv
+ * layer, src/model.py:143-208,384-406. */
+int gnnrec_spmm_csr2_f32(const int64_t* indptr_a, const int32_t* indices_a, const float* ew_a,
+                         const int64_t* indptr_b, const int32_t* indices_b, const float* ew_b,
+                         const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
+                         int flags, float* out_a, float* out_b, int64_t ldo, void* stream);
+
 /* Gradient of gnnrec_spmm_csr_f32 w.r.t. X (training):
  * grad_X[indices[e]] += (ew ? ew[e] : 1) * grad_out[v] (/ deg for MEAN); for MAX the
  * gradient of each column goes to the first edge whose message equals out[v]

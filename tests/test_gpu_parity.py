@@ -1216,3 +1216,45 @@ def test_tree_sum_equals_pairwise_adds(n_parts, n):
     np.testing.assert_array_equal(got.cpu().numpy(), ref[0])
     with pytest.raises(ValueError):
         ops.tree_sum_(parts[:3] if n_parts >= 4 else parts[:1])
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("n_dst", [37, 200_000])
+def test_spmm2_equals_two_launches_bitwise(reduce, weighted, n_dst):
+    """gnnrec_spmm_csr2_f32 (two relations into one destination type, one launch; static
+    walk for small grids, row queue for large ones) gives each relation exactly the bits of
+    its own gnnrec_spmm_csr_f32 launch, stored and accumulated, and matches the oracle."""
+    from gnnrec import ops
+    rng = np.random.default_rng(n_dst + len(reduce) + weighted)
+    n_src, d = 3000, 128
+    csrs, ref_in = [], []
+    for deg_hi in (90, 20):  # a 'clicks'-like and a 'buys'-like relation
+        deg = rng.integers(0, deg_hi, n_dst)
+        dst = np.repeat(np.arange(n_dst), deg)
+        src = rng.integers(0, n_src, dst.size)
+        perm = rng.permutation(dst.size)
+        indptr, indices, eids = oracle.csr_from_coo(src[perm], dst[perm], n_dst)
+        ew = rng.integers(1, 9, dst.size).astype(np.float32)[eids] if weighted else None
+        csrs.append((_t(indptr), _t(indices.astype(np.int32)), None if ew is None else _t(ew)))
+        ref_in.append((indptr, indices, ew))
+    X = _t(rng.standard_normal((n_src, d)).astype(np.float32))
+    a, b = ops.spmm2(csrs[0], csrs[1], X, reduce, empty_neginf=reduce == "max")
+    for got, (ip, ix, w) in zip((a, b), csrs):
+        assert torch.equal(got, ops.spmm(ip, ix, X, reduce, edge_weight=w,
+                                         empty_neginf=reduce == "max"))
+    # accumulate onto existing partials: the same bits as two accumulating launches
+    base = [torch.randn(n_dst, d, device=DEV) for _ in range(2)]
+    a2, b2 = ops.spmm2(csrs[0], csrs[1], X, reduce, out_a=base[0].clone(), out_b=base[1].clone(),
+                       accumulate=True, empty_neginf=reduce == "max")
+    for got, (ip, ix, w), o in zip((a2, b2), csrs, base):
+        exp = ops.spmm(ip, ix, X, reduce, edge_weight=w, out=o.clone(), accumulate=True,
+                       empty_neginf=reduce == "max")
+        assert torch.equal(got, exp)
+    if n_dst < 1000:
+        ip, ix, w = ref_in[1]
+        ref = oracle.spmm_csr(ip, ix, X.cpu().numpy(), reduce, w)
+        got = b.cpu().numpy()
+        if reduce == "max":
+            got[(ip[1:] - ip[:-1]) == 0] = 0.0  # empty rows stay -inf with empty_neginf
+        np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)

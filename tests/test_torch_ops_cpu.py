@@ -23,7 +23,7 @@ RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_t
            "gnnrec_row_epilogue_f32": "row_epilogue", "gnnrec_add_f32": "add_",
            "gnnrec_tree_sum_f32": "tree_sum_", "gnnrec_spmm_csr_f32": "spmm_csr",
            "gnnrec_spmm_csr_split_f32": "spmm_csr_split",
-           "gnnrec_spmm_csr_planned_f32": "spmm_csr_planned",
+           "gnnrec_spmm_csr_planned_f32": "spmm_csr_planned", "gnnrec_spmm_csr2_f32": "spmm_csr2",
            "gnnrec_spmm_backward_f32": "spmm_backward",
            "gnnrec_spmm_project_f32": "spmm_project", "gnnrec_sddmm_cos_f32": "sddmm_cos",
            "gnnrec_sddmm_cos_backward_f32": "sddmm_cos_backward",
