@@ -362,6 +362,13 @@ def main():
     timers = EventTimers()
     runner.timers = timers
     torch.cuda.synchronize()
+    # the graph build's temporaries (edge streams, CSR sort workspaces: ~20 B per edge) sit in
+    # the caching allocator; hand them back so the pass's own tables never meet a full pool
+    # (an allocation that finds none frees the whole cache under a device sync: 2 s stalls)
+    torch.cuda.empty_cache()
+    if os.environ.get("GNNREC_BENCH_MEMINFO"):
+        print(f"[bench] allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "
+              f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
 
     for _ in range(args.warmup):
         out = runner.run(feats, replicate_output=False)
@@ -377,6 +384,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("GNNREC_BENCH_MEMINFO"):
+        print(f"[bench] after the timed passes: allocated "
+              f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "
+              f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB, peak "
+              f"{torch.cuda.max_memory_reserved() / 2**30:.1f} GiB, alloc retries "
+              f"{torch.cuda.memory_stats().get('num_alloc_retries', 0)}", file=sys.stderr,
+              flush=True)
     elapsed = ex.max_scalar(elapsed, dev)
     del out
 

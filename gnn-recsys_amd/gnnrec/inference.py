@@ -107,6 +107,8 @@ def _planned(indptr: torch.Tensor, split: int = ops.DEFAULT_SPLIT) -> torch.Tens
 # deterministic tree stays bitwise P-invariant.
 TILE_SPLIT = 512
 
+_SCRATCH = os.environ.get("GNNREC_SCRATCH", "1") != "0"  # reuse scratch tables across passes
+
 
 class GraphShard:
     """This rank's share of a heterograph for the sharded full-graph pass."""
@@ -338,7 +340,27 @@ class ShardedFullGraphPass:
         self.capture = None  # optional list: every layer's output tables are appended (tests)
         self.fused = set()  # relations whose aggregation ran with the projection fused
         self.tile_pairs = set()  # (relation a, relation b) whose tiles ran as one launch
+        self._pool = {}  # scratch tables reused across passes (_scratch)
+        self._scratch_ev = {}  # scratch key -> event of the side-stream work reading it
         self._last, self._replicate_last = False, True
+
+    def _scratch(self, key, shape, device):
+        """A per-runner scratch table reused by every pass (tile partials, unfused
+        aggregates): the pass allocates the same shapes every time, and tables that the
+        side-stream GEMMs read (record_stream) would otherwise park freed blocks in the
+        caching allocator until that stream catches up, growing the pool by tens of GB per
+        pass and stalling on fresh hipMallocs (C5: reserved 17 -> 175 GiB over 10 passes, 2 s
+        host stalls).  Reuse is ordered by the pass itself: a partial is read by the tree and
+        the exchange, which the owner's GEMM waits for, before the next layer's tiles write
+        it; an aggregate is read by the side-stream GEMM whose output the next layer waits
+        for before it reaches the same relation."""
+        if not _SCRATCH:
+            return torch.empty(shape, dtype=torch.float32, device=device)
+        t = self._pool.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.device != torch.device(device):
+            t = torch.empty(shape, dtype=torch.float32, device=device)
+            self._pool[key] = t
+        return t
 
     def _get(self, h, nt):
         w = self._pending.pop(id(h[nt]), None)
@@ -515,8 +537,7 @@ class ShardedFullGraphPass:
                     # source-range tiles: each tile gathers from a slice of the source table
                     # small enough to stay in the Infinity Cache; accumulated in place
                     op = 'max' if reduce == 'max' else 'sum'
-                    part = torch.empty((rs.n_rows, msg.shape[1]), dtype=torch.float32,
-                                       device=msg.device)
+                    part = self._scratch(('part', ce), (rs.n_rows, msg.shape[1]), msg.device)
                     for j, (ip, ix, w) in enumerate(rs.segs):
                         with self._time('spmm_tile'):
                             O.spmm(ip, ix, msg, op, edge_weight=w if weighted else None,
@@ -578,7 +599,11 @@ class ShardedFullGraphPass:
                     csr_b = (sb[0], sb[1], sb[2] if weighted else None)
                     with self._time('spmm_tile2'):
                         if j % 2 == 0:
-                            pa, pb = self.ops.spmm2(csr_a, csr_b, msg, 'sum')
+                            shp = (ra.n_rows, msg.shape[1])
+                            pa, pb = self.ops.spmm2(
+                                csr_a, csr_b, msg, 'sum',
+                                out_a=self._scratch(('tile', ca, j), shp, msg.device),
+                                out_b=self._scratch(('tile', cb, j), shp, msg.device))
                             parts[ca].append(pa)
                             parts[cb].append(pb)
                         else:
@@ -592,8 +617,10 @@ class ShardedFullGraphPass:
                 ew = w if weighted else None
                 with self._time('spmm_tile'):
                     if j % 2 == 0:
-                        parts[ce].append(self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew,
-                                                       split=TILE_SPLIT))
+                        parts[ce].append(self.ops.spmm(
+                            ip, ix, msg, 'sum', edge_weight=ew, split=TILE_SPLIT,
+                            out=self._scratch(('tile', ce, j), (rs.n_rows, msg.shape[1]),
+                                              msg.device)))
                     else:
                         self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[ce][-1],
                                       accumulate=True, split=TILE_SPLIT)
@@ -680,9 +707,14 @@ class ShardedFullGraphPass:
                 self.fused.add(ce)
                 continue
             with self._time('spmm'):
+                ev_prev = self._scratch_ev.pop(('agg', ce), None)
+                if ev_prev is not None:  # the last side-stream GEMM that read this scratch
+                    torch.cuda.current_stream(self.shard.device).wait_event(ev_prev)
                 a = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm') if reduce == 'lstm' else
                      O.spmm(rs.indptr, rs.indices, msg, reduce,
-                            edge_weight=rs.weights if weighted else None))
+                            edge_weight=rs.weights if weighted else None,
+                            out=self._scratch(('agg', ce), (rs.n_rows, msg.shape[1]),
+                                              msg.device)))
             if o is None:
                 o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32, device=a.device)
                 akw = self._attn(hconv, T, sh.n_own, o.device)
@@ -698,6 +730,8 @@ class ShardedFullGraphPass:
                        out_div=div, out=o, **akw, **fkw)
             ev = self._on_side(proj, self_rows, a, o, *akw.values(), *fkw.values(),
                                *(t for t in (Ws, Wn, bias) if t is not None))
+            if ev is not None:
+                self._scratch_ev[('agg', ce)] = ev
         out[T] = o
         if ev is not None:
             self._ready[id(o)] = ev
