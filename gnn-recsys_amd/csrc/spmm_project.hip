@@ -270,29 +270,55 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 // each; HIP's second launch-bounds argument is waves per SIMD), so one block's MFMA phase
 // runs under the other's gather.
 //
-// Measured (C5 bought-by, 10M rows × 10 edges, tools/probe_c5.py): 13.1 ms, vs 18.0 ms
-// for the VALU kernel and 7.6 + 7.1 ms for gather + GEMM launched back to back.  A
+// The gather runs the wave's 4 rows in lockstep (all 4 rows' index loads, then steps of
+// 2·LU neighbours of every row), so a 10-edge row does not pay its own index -> row round
+// trips; the W operands stream from L2 in chunks of 16 under the MFMAs.
+//
+// PRE (W_neighT = NULL): the source rows arrive already projected (Y = X·W_neighᵀ, linear
+// reductions only), the neighbour term is their aggregate, read from the A tile in the
+// epilogue, and the 8 waves split the self half's K = 128 (two 32-row·32-col partials).
+//
+// Measured (C5 bought-by, 10M rows × 10 edges, tools/probe_c5.py, one box): 12.8–13.1 ms
+// (13.1 with the rows gathered one after another), PRE 10.6 ms + 0.38 ms for the 1M-row
+// source projection; 18.0 ms for the VALU kernel; 7.6 + 7.1 ms for gather + GEMM launched
+// back to back.  Timing builds (GNNREC_SPM_PHASE): the GEMM phase alone (no neighbour
+// loads) takes 7.3–7.8 ms — the fp32 MFMA at ≈0.6 of its peak, as in the plain GEMM
+// (profiles/r02_gemm_experiments.md) — so the two phases overlap by ≈2 ms only.  Not kept
+// (same session A/B): 64-row tiles (C in the A tile's LDS, 12.6–12.7 ms, within noise of
+// 32), all 64 W operands up front (14.7 vs 13.1 ms once the lockstep gather holds its
+// registers), three blocks per CU at 80 VGPRs (16.4 ms: spills), LU = 4 (spills).  A
 // variant splitting the block into 8 gather waves and 8 MFMA waves (weights resident in
-// the MFMA waves' registers, one barrier per pipelined step) took 17–22 ms: its timing
-// builds put the gather side alone at 17.9 ms and the MFMA side alone at 7.4 ms — 8
-// gathering waves per CU cannot keep HBM busy at 10 edges per row.  So the sharded pass,
-// which can run the GEMM on a second stream under the next relation's HBM-bound gather,
-// keeps gather + GEMM for such relations; this kernel serves the module path
-// (nn.ConvLayer), where the two would run back to back.
+// the MFMA waves' registers, one barrier per pipelined step) took 17–22 ms: 8 gathering
+// waves per CU cannot keep HBM busy at 10 edges per row.  The sharded pass fuses such a
+// relation only in the PRE form (else gather + GEMM on the side stream).
 #ifndef GNNREC_SPM_U
-#define GNNREC_SPM_U 4  // gather wave-instructions in flight per lane
+#define GNNREC_SPM_U 4  // gather wave-instructions in flight per lane (rows > 64 edges)
+#endif
+#ifndef GNNREC_SPM_PHASE
+#define GNNREC_SPM_PHASE 0  // timing builds only: 1 = gather phase alone, 2 = GEMM phase alone
+#endif
+#ifndef GNNREC_SPM_LU
+#define GNNREC_SPM_LU 2  // lockstep gather: steps of 2·LU neighbours of 4 rows at once
+#endif
+#ifndef GNNREC_SPM_WC
+#define GNNREC_SPM_WC 16  // W operands per chunk (64: all loaded up front)
+#endif
+#ifndef GNNREC_SPM_EU
+#define GNNREC_SPM_EU 4  // epilogue rows unrolled
 #endif
 constexpr int kMT = 32;                  // rows per tile
+constexpr int kMB = kMT / 32;            // 32-row MFMA blocks per tile
 constexpr int kMWaves = 8;               // waves per block
 constexpr int kMRows = kMT / kMWaves;    // rows gathered per wave per tile
 constexpr int kALd = 2 * kPD + 4;        // A tile row stride (floats): conflict-free b128 reads
 constexpr int kCLd = kPD + 8;            // C tile row stride: the two lane halves' stores
                                          // land on disjoint banks
+constexpr int kALds = kMT * kALd;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int REDUCE, bool WEIGHTED, int UNROLL>
+template <int REDUCE, bool WEIGHTED, int UNROLL, bool PRE>
 __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx,
@@ -301,10 +327,12 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
     const float* __restrict__ bias_ne, int64_t n_dst, int epilogue, int accum, float out_div,
     const float* __restrict__ attn_vec, float* __restrict__ attn_state,
     float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
-  __shared__ float As[kMT * kALd];
-  __shared__ float Cs[2][kMT * kCLd];
+  __shared__ float lds[kALds + 2 * kMT * kCLd];
   __shared__ int nes[kMT];
   __shared__ int64_t blk_r[2];
+  float* const As = lds;
+  float* const Cs0 = lds + kALds;
+  float* const Cs1 = Cs0 + kMT * kCLd;
 
   constexpr int LPR = 32, VEC = 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -319,95 +347,184 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
   const EpiArgs ep{(epilogue & GNNREC_EPI_RELU) != 0, (epilogue & GNNREC_EPI_L2NORM) != 0,
                    attn, accum, out_div, a0, a1, attn_state, out, ldo, j0};
 
-  // B operands: lane supplies Wᵀ[k][n], k = 64·bh + i of this wave's K half, n = 32·cb + li.
+  // B operands: lane supplies Wᵀ[k][n], k = 64·bh + i of this wave's K half, n = 32·cb + li
+  // (PRE: the self half alone, split over the two wave halves: k = 64·kh + 32·bh + i).
   // Buffer loads: one 32-bit per-lane offset plus an immediate row offset, instead of 64
   // hoisted 64-bit addresses (which the compiler spills)
-  const float* WTb = kh ? WnT : WsT;
+  constexpr int kKL = PRE ? 32 : 64;  // K per lane half
+  const float* WTb = (kh && !PRE) ? WnT : WsT;
   const uint64_t wbase = ((uint64_t)__builtin_amdgcn_readfirstlane(
                               (unsigned)((uintptr_t)WTb >> 32)) << 32) |
                          (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)WTb);
   const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wbase), 0,
                                                        kPD * kPD * 4, 0x00020000);
-  const int wvoff = ((64 * bh) * kPD + 32 * cb + li) * 4;
+  const int wvoff = ((PRE ? 64 * kh + 32 * bh : 64 * bh) * kPD + 32 * cb + li) * 4;
 
   // one tile: rows [t0, min(t0 + kMT, lim)); every wave of the block takes part
   auto tile = [&](int64_t t0, int64_t lim) __attribute__((always_inline)) {
     const int64_t rbase = t0 + wave * kMRows;
     const int64_t left = lim - rbase;
     const int nv = (int)(left <= 0 ? 0 : left < kMRows ? left : kMRows);
-    // the 4 rows' bounds in one load; each row's first 64 indices are requested before
-    // the previous row gathers, the self rows (two per instruction) a row pair ahead
-    // (nv == 0: rows past the range end — nothing is read, the tile rows stay zero)
+    // the rows' bounds in one load (nv == 0: rows past the range end — nothing is read,
+    // the tile rows stay zero); self rows two per instruction, after the gather
     const int64_t ipl = nv > 0 && lane <= nv ? indptr[rbase + lane] : 0;
     auto bound = [&](int r) { return __shfl(ipl, r <= nv ? r : nv); };
-    auto first_idx = [&](int r) {
-      const int64_t b = bound(r), e = bound(r + 1);
-      return r < nv && lane < e - b ? indices[b + lane] : 0;
-    };
     auto self_rows = [&](int q) {  // lanes of half bh: self row 2q + bh
       const int rl = 2 * q + bh;
       return rl < nv ? *reinterpret_cast<const float4*>(H + (rbase + rl) * ldh + col)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
     };
-    int pidx = first_idx(0);
-    float4 hs = self_rows(0);
+    // Lockstep gather, 4 rows at a time: their bounds and first 64 indices are requested up
+    // front, then every step issues the loads of all 4 rows (4·LU·2 source rows in flight
+    // per wave), so a 10-edge row does not pay its own index -> row round trips.  Each
+    // row's neighbours are still summed by group in gather_range's order
+    // (k = j + u·NPI + grp, ascending — the same sequence for any LU): the same aggregate
+    // bits.  Rows with more than 64 edges take gather_range row by row.
+    constexpr int NPI = kWave / LPR, U = GNNREC_SPM_LU, kLR = 4;
 #pragma unroll
-    for (int r = 0; r < kMRows; ++r) {
-      const int pnext = r + 1 < kMRows ? first_idx(r + 1) : 0;
-      Frag<VEC> acc;
+    for (int g = 0; g < kMRows; g += kLR) {
+      int ridx[kLR];
+      float rwt[kLR];
+      int dg[kLR];
+      int dmax = 0;
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) acc.v[v] = init;
-      int64_t deg = 0;
-      if (r < nv) {
-        const int64_t beg = bound(r), end = bound(r + 1);
-        deg = end - beg;
-        gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(beg, end, indices, ew, X, ldx,
-                                                               col, true, lane, grp, acc, pidx);
+      for (int r = 0; r < kLR; ++r) {
+        const int64_t b = bound(g + r);
+        dg[r] = g + r < nv ? (int)(bound(g + r + 1) - b) : 0;
+#if GNNREC_SPM_PHASE == 2
+        dg[r] = 0;
+#endif
+        ridx[r] = lane < dg[r] ? ld_stream(indices + b + lane) : 0;
+        rwt[r] = 0.f;
+        if constexpr (WEIGHTED) rwt[r] = lane < dg[r] ? ld_stream(ew + b + lane) : 0.f;
+        dmax = dg[r] > dmax ? dg[r] : dmax;
       }
-      combine_groups<LPR, VEC, REDUCE>(acc);
-      finalize<VEC, REDUCE>(acc, deg, 0);
-      const int rl = wave * kMRows + r;
-      if (grp == 0)
-        *reinterpret_cast<float4*>(&As[rl * kALd + kPD + col]) =
-            make_float4(acc.v[0], acc.v[1], acc.v[2], acc.v[3]);
-      if (lane == 0) nes[rl] = deg > 0;
-      if (r % 2 == 0) {  // the self-row pair of rows r, r+1 has landed: park it
-        *reinterpret_cast<float4*>(&As[(wave * kMRows + r + bh) * kALd + col]) = hs;
-        if (r + 2 < kMRows) hs = self_rows(r / 2 + 1);
+      Frag<VEC> acc[kLR];
+#pragma unroll
+      for (int r = 0; r < kLR; ++r)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[r].v[v] = init;
+      if (dmax <= 64) {
+        for (int j = 0; j < dmax; j += NPI * U) {
+          Frag<VEC> val[kLR][U];
+          bool ok[kLR][U];
+#pragma unroll
+          for (int r = 0; r < kLR; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int k = j + u * NPI + grp;
+              ok[r][u] = k < dg[r];
+              const int src = __shfl(ridx[r], k & 63);
+              if (ok[r][u]) {
+                load_frag<VEC>(val[r][u], X + (int64_t)src * ldx + col);
+              } else {
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) val[r][u].v[v] = 0.f;
+              }
+            }
+#pragma unroll
+          for (int r = 0; r < kLR; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              float w = 1.f;
+              if constexpr (WEIGHTED) w = __shfl(rwt[r], (j + u * NPI + grp) & 63);
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) {
+                const float m = WEIGHTED ? val[r][u].v[v] * w : val[r][u].v[v];
+                if constexpr (REDUCE == GNNREC_REDUCE_MAX) {
+                  if (ok[r][u]) acc[r].v[v] = fmaxf(acc[r].v[v], m);
+                } else {
+                  acc[r].v[v] += m;
+                }
+              }
+            }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < kLR; ++r)
+          if (g + r < nv)
+            gather_range<LPR, VEC, REDUCE, WEIGHTED, UNROLL, true>(
+                bound(g + r), bound(g + r + 1), indices, ew, X, ldx, col, true, lane, grp,
+                acc[r], ridx[r]);
       }
-      pidx = pnext;
+#pragma unroll
+      for (int r = 0; r < kLR; ++r) {
+        combine_groups<LPR, VEC, REDUCE>(acc[r]);
+        finalize<VEC, REDUCE>(acc[r], dg[r], 0);
+        const int rl = wave * kMRows + g + r;
+        if (grp == 0)
+          *reinterpret_cast<float4*>(&As[rl * kALd + kPD + col]) =
+              make_float4(acc[r].v[0], acc[r].v[1], acc[r].v[2], acc[r].v[3]);
+        if (lane == 0) nes[rl] = dg[r] > 0;
+      }
     }
+#pragma unroll
+    for (int q = 0; q < kMRows / 2; ++q)
+      *reinterpret_cast<float4*>(&As[(wave * kMRows + 2 * q + bh) * kALd + col]) = self_rows(q);
     __syncthreads();
 
-    // C_kh[32 × 32 block cb] = A[:, K half kh] · Wᵀ[K half kh, block cb]
-    float bw[64];
+    // C_kh[rows 32·b.., 32 × 32 block cb] = A[:, K half kh] · Wᵀ[K half kh, block cb], the
+    // W operands loaded once for the tile's kMB row blocks
+    // W operands stream in 4 chunks of 16 (double-buffered, the next chunk's loads in
+    // flight under this chunk's MFMAs) instead of 64 live registers
+    constexpr int kWC = GNNREC_SPM_WC;
+    float bw[2][kWC];
+    auto load_w = [&](float* dst, int i0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 64; ++i)
-      bw[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wrsrc, wvoff, i * kPD * 4, 0));
-    f32x16 c;
+      for (int i = 0; i < kWC; ++i)
+        dst[i] = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(wrsrc, wvoff, (i0 + i) * kPD * 4, 0));
+    };
+    f32x16 c[kMB];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) c[v] = 0.f;
-    const float* ap = As + li * kALd + kh * kPD + 64 * bh;
+    for (int b = 0; b < kMB; ++b)
 #pragma unroll
-    for (int i = 0; i < 64; i += 4) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(ap + i);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], bw[i], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], bw[i + 1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], bw[i + 2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], bw[i + 3], c, 0, 0, 0);
+      for (int v = 0; v < 16; ++v) c[b][v] = 0.f;
+    const float* ap = As + li * kALd + (PRE ? 64 * kh + 32 * bh : kh * kPD + 64 * bh);
+#if GNNREC_SPM_PHASE == 1
+    if (nv < 0)
+#endif
+    {
+      load_w(bw[0], 0);
+#pragma unroll
+      for (int ch = 0; ch < kKL / kWC; ++ch) {
+        if (ch + 1 < kKL / kWC) load_w(bw[(ch + 1) & 1], (ch + 1) * kWC);
+        __builtin_amdgcn_sched_barrier(0);
+        const float* w = bw[ch & 1];
+#pragma unroll
+        for (int i = 0; i < kWC; i += 4) {
+#pragma unroll
+          for (int b = 0; b < kMB; ++b) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(ap + 32 * b * kALd + ch * kWC + i);
+            c[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], w[i], c[b], 0, 0, 0);
+            c[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], w[i + 1], c[b], 0, 0, 0);
+            c[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], w[i + 2], c[b], 0, 0, 0);
+            c[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], w[i + 3], c[b], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     // D map of the 32x32 MFMA: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 h
-    float* cp = Cs[kh] + 32 * cb + li;
+    float* cp = (kh ? Cs1 : Cs0) + 32 * cb + li;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) cp[((v & 3) + 8 * (v >> 2) + 4 * bh) * kCLd] = c[v];
+    for (int b = 0; b < kMB; ++b)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        cp[(32 * b + (v & 3) + 8 * (v >> 2) + 4 * bh) * kCLd] = c[b][v];
     __syncthreads();
 
-#pragma unroll
+#pragma unroll GNNREC_SPM_EU
     for (int r = 0; r < kMRows; ++r) {
       const int rl = wave * kMRows + r;
-      const float2 s2 = *reinterpret_cast<const float2*>(&Cs[0][rl * kCLd + j0]);
-      const float2 n2 = *reinterpret_cast<const float2*>(&Cs[1][rl * kCLd + j0]);
+      const float2 s2 = *reinterpret_cast<const float2*>(&Cs0[rl * kCLd + j0]);
+      const float2 n2 = *reinterpret_cast<const float2*>(&Cs1[rl * kCLd + j0]);
       float z0 = s2.x + n2.x, z1 = s2.y + n2.y;
+      if constexpr (PRE) {  // + the aggregate of the pre-projected rows
+        const float2 g2 = *reinterpret_cast<const float2*>(&As[rl * kALd + kPD + j0]);
+        z0 += g2.x;
+        z1 += g2.y;
+      }
       if (bias) {
         z0 = bias[j0] + z0;
         z1 = bias[j0 + 1] + z1;
@@ -486,8 +603,9 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
                  "gnnrec_spmm_project_f32: attention accumulation needs attn_vec, attn_state");
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(indptr && X && H && W_selfT && W_neighT && out,
-                 "gnnrec_spmm_project_f32: null pointer");
+  GNNREC_REQUIRE(W_neighT, "gnnrec_spmm_project_f32: W_neighT = NULL (pre-projected source "
+                           "rows) is gnnrec_spmm_project_mfma_f32's form");
+  GNNREC_REQUIRE(indptr && X && H && W_selfT && out, "gnnrec_spmm_project_f32: null pointer");
   GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(W_selfT) && aligned16(W_neighT) &&
                      ldx % 4 == 0 && ldh % 4 == 0 && ldo % 2 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
@@ -555,11 +673,17 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
                  "attn_state");
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project_mfma_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(indptr && X && H && W_selfT && W_neighT && out,
+  GNNREC_REQUIRE(indptr && X && H && W_selfT && out,
                  "gnnrec_spmm_project_mfma_f32: null pointer");
-  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(W_selfT) && aligned16(W_neighT) &&
-                     ldx % 4 == 0 && ldh % 4 == 0 && ldo % 2 == 0 &&
-                     (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
+  // W_neighT == NULL: X holds pre-projected source rows (X·W_neighᵀ), the neighbour half
+  // is their aggregate itself — linear reductions only
+  const bool pre = W_neighT == nullptr;
+  GNNREC_REQUIRE(!pre || reduce != GNNREC_REDUCE_MAX,
+                 "gnnrec_spmm_project_mfma_f32: pre-projected rows (W_neighT = NULL) need a "
+                 "sum or mean reduce");
+  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(W_selfT) &&
+                     (pre || aligned16(W_neighT)) && ldx % 4 == 0 && ldh % 4 == 0 &&
+                     ldo % 2 == 0 && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                  "gnnrec_spmm_project_mfma_f32: X/H/W need 16-B aligned rows, out 8-B");
   // two persistent 8-wave blocks per CU, minus the CUs reserved for concurrent kernels
   const int64_t tiles = (n_dst + kMT - 1) / kMT;
@@ -575,18 +699,27 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
   const dim3 grid((unsigned)blocks), block(kMWaves * 64);
-#define GNNREC_SPM(R, W)                                                                      \
-  hipLaunchKernelGGL((spmm_project_mfma_kernel<R, W, GNNREC_SPM_U>), grid, block, 0, s, indptr, \
-                     indices, ew, X, ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty,       \
-                     n_dst, epilogue, accum, out_div, attn_vec, attn_state, out, ldo, rq, rq_ch)
-  if (ew) {
-    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, true);
-    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, true);
-    else GNNREC_SPM(GNNREC_REDUCE_MAX, true);
+#define GNNREC_SPM(R, W, P)                                                                     \
+  hipLaunchKernelGGL((spmm_project_mfma_kernel<R, W, GNNREC_SPM_U, P>), grid, block, 0, s,      \
+                     indptr, indices, ew, X, ldx, H, ldh, W_selfT, W_neighT, bias,              \
+                     bias_nonempty, n_dst, epilogue, accum, out_div, attn_vec, attn_state, out, \
+                     ldo, rq, rq_ch)
+  if (pre) {
+    if (ew) {
+      if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, true, true);
+      else GNNREC_SPM(GNNREC_REDUCE_MEAN, true, true);
+    } else {
+      if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, false, true);
+      else GNNREC_SPM(GNNREC_REDUCE_MEAN, false, true);
+    }
+  } else if (ew) {
+    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, true, false);
+    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, true, false);
+    else GNNREC_SPM(GNNREC_REDUCE_MAX, true, false);
   } else {
-    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, false);
-    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, false);
-    else GNNREC_SPM(GNNREC_REDUCE_MAX, false);
+    if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPM(GNNREC_REDUCE_SUM, false, false);
+    else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPM(GNNREC_REDUCE_MEAN, false, false);
+    else GNNREC_SPM(GNNREC_REDUCE_MAX, false, false);
   }
 #undef GNNREC_SPM
   rowq_launched(ticket, s);

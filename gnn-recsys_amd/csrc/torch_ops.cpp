@@ -251,11 +251,11 @@ void row_epilogue(const Tensor& z, int64_t l2norm, int64_t accum, double out_div
 }
 
 void spmm_project(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
-                  const Tensor& X, const Tensor& H, const Tensor& W_selfT, const Tensor& W_neighT,
-                  const optional<Tensor>& bias, const optional<Tensor>& bias_nonempty,
-                  int64_t reduce, int64_t epilogue, int64_t accum, double out_div,
-                  const optional<Tensor>& attn_vec, const optional<Tensor>& attn_state,
-                  bool mfma, Tensor& out) {
+                  const Tensor& X, const Tensor& H, const Tensor& W_selfT,
+                  const optional<Tensor>& W_neighT, const optional<Tensor>& bias,
+                  const optional<Tensor>& bias_nonempty, int64_t reduce, int64_t epilogue,
+                  int64_t accum, double out_div, const optional<Tensor>& attn_vec,
+                  const optional<Tensor>& attn_state, bool mfma, Tensor& out) {
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(ew, "edge_weight", at::kFloat);
@@ -272,8 +272,10 @@ void spmm_project(const Tensor& indptr, const Tensor& indices, const optional<Te
   TORCH_CHECK_VALUE(H.size(0) >= n_dst, "H has ", H.size(0), " rows, the CSR ", n_dst,
                     " destinations");
   TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d, "]");
-  TORCH_CHECK_VALUE(W_selfT.is_contiguous() && W_neighT.is_contiguous(),
+  TORCH_CHECK_VALUE(W_selfT.is_contiguous() && (!has(W_neighT) || W_neighT->is_contiguous()),
                     "transposed weights must be contiguous");
+  TORCH_CHECK_VALUE(has(W_neighT) || mfma, "pre-projected source rows (W_neighT None) need the "
+                    "mfma variant");
   const int64_t ldx = ld(X, "X"), ldh = ld(H, "H"), ldo = ld(out, "out");
   if (meta(X)) return;
   const c10::DeviceGuard g(X.device());
@@ -884,7 +886,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("row_epilogue(Tensor z, int l2norm, int accum, float out_div, Tensor? attn_vec, "
         "Tensor(b!)? attn_state, Tensor(a!) out) -> ()");
   m.def("spmm_project(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, Tensor H, "
-        "Tensor W_selfT, Tensor W_neighT, Tensor? bias, Tensor? bias_nonempty, int reduce, "
+        "Tensor W_selfT, Tensor? W_neighT, Tensor? bias, Tensor? bias_nonempty, int reduce, "
         "int epilogue, int accum, float out_div, Tensor? attn_vec, Tensor(b!)? attn_state, "
         "bool mfma, Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");

@@ -684,9 +684,16 @@ class ShardedFullGraphPass:
             msg = self._message(mod, ce, h, preagg)
             acc, div = hconv.accum_mode(j, R)
             avg = (rs.global_edges / max(sh.num_nodes[T], 1)) if self.deterministic else None
+            # a pre-projected low-degree relation fuses even beside a side stream: its
+            # MFMA runs the self half only (C5 bought-by: 10.6 + 0.4 ms vs 7.6 ms gather +
+            # a 7 ms GEMM contending with the tiles for HBM); GNNREC_PRE_FUSE_PASS=0 keeps
+            # gather + side-stream GEMM there
+            pre = reduce != 'lstm' and getattr(O, 'preproject_pays', None) is not None and \
+                O.preproject_pays(msg.shape[0], rs.n_rows, reduce) and \
+                os.environ.get("GNNREC_PRE_FUSE_PASS", "1") != "0"
             if reduce != 'lstm' and can_fuse is not None and can_fuse(
                     rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight,
-                    avg_deg=avg, gemm_overlaps=self.side is not None):
+                    avg_deg=avg, gemm_overlaps=self.side is not None and not pre):
                 # aggregation and projection in one launch on the main stream: the self rows
                 # must be ready here (they may come from the side stream)
                 self_rows = self._get(h, T)
@@ -699,6 +706,11 @@ class ShardedFullGraphPass:
                     akw = self._attn(hconv, T, sh.n_own, o.device)
                 Ws, Wn, bias, bias_ne = self._folded(mod, ce)
                 vkw = {} if avg is None else {'avg_deg': avg}  # same kernel on every rank
+                if O.fused_preprojects(rs.indptr, msg, self_rows, reduce, avg):
+                    with self._time('preproject'):
+                        msg = O.preproject(msg, Wn, out=self._scratch(
+                            ('pre', ce), (msg.shape[0], Wn.shape[0]), msg.device))
+                    Wn = None
                 with self._time(self._fused_tag(rs, avg)):
                     O.spmm_project(rs.indptr, rs.indices, msg, self_rows, Ws, Wn, reduce,
                                    rs.weights if weighted else None, relu=True,

@@ -157,8 +157,12 @@ class ConvLayer(nn.Module):
         m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
         if reduce != 'lstm' and ops.can_spmm_project(graph.indptr, m, h_self, self.fc_self.weight,
                                                      self.fc_neigh.weight):
+            Wn = self.fc_neigh.weight
+            if ops.fused_preprojects(graph.indptr, m, h_self, reduce):
+                # few source rows: project them first, the kernel runs the self half only
+                m, Wn = ops.preproject(m, Wn), None
             return ops.spmm_project(graph.indptr, graph.indices, m, h_self, self.fc_self.weight,
-                                    self.fc_neigh.weight, reduce, ew, relu=True,
+                                    Wn, reduce, ew, relu=True,
                                     l2norm=bool(self.norm), accum=accum, out_div=out_div,
                                     out=out, attn_vec=av, attn_state=ast)
         agg = self.aggregate(graph.indptr, graph.indices, m, reduce, ew)

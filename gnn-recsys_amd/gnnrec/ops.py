@@ -469,6 +469,13 @@ def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAU
     return True
 
 
+def fused_preprojects(indptr, X, H, reduce: str, avg_deg: Optional[float] = None) -> bool:
+    """A fused launch that can_spmm_project accepted runs the pre-projected form: the MFMA
+    variant, a linear reduce and a source table at most half the destination count."""
+    return fused_variant(indptr, avg_deg) == "mfma" and preproject_pays(
+        X.shape[0], indptr.numel() - 1, reduce)
+
+
 FUSED_MIN_DEG = 24
 
 
@@ -511,7 +518,12 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
     """a1+a3 fused: out (accum)= epi(H W_selfᵀ + reduce_e X[src_e] W_neighᵀ + bias
     + [deg > 0]·bias_nonempty), d = 128.  variant 'valu' | 'mfma' (default: fused_variant
     of avg_deg) picks the kernel; both give the same aggregate bits, the projection's
-    fp32 summation order differs."""
+    fp32 summation order differs.
+
+    W_neigh None: X holds pre-projected source rows (preproject(X, W_neigh)) and the
+    neighbour term is reduce_e X[src_e] itself (sum / mean only; the mfma kernel, which
+    then runs only the self half on the MFMA).  The same value up to fp32 rounding: the
+    projection is applied before the (linear) reduction instead of after it."""
     _dev(indptr, "indptr", torch.int64)
     _dev(indices, "indices", torch.int32)
     _dev(X, "X", torch.float32)
@@ -531,10 +543,17 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
         _dev(out, "out", torch.float32)
         if tuple(out.shape) != (n_dst, D):
             raise ValueError(f"out must be [{n_dst}, {D}], got {tuple(out.shape)}")
-    if tuple(W_self.shape) != (D, D) or tuple(W_neigh.shape) != (D, D):
+    if tuple(W_self.shape) != (D, D) or (W_neigh is not None
+                                         and tuple(W_neigh.shape) != (D, D)):
         raise ValueError(f"spmm_project needs {D}x{D} weights")
+    if W_neigh is None:
+        if reduce not in ("sum", "mean"):
+            raise ValueError("pre-projected source rows (W_neigh None) need reduce sum or mean")
+        if variant not in (None, "mfma"):
+            raise ValueError("pre-projected source rows (W_neigh None) run on the mfma kernel")
+        variant = "mfma"
     WsT = W_self.detach().t().contiguous()
-    WnT = W_neigh.detach().t().contiguous()
+    WnT = None if W_neigh is None else W_neigh.detach().t().contiguous()
     for t, name in ((bias, "bias"), (bias_nonempty, "bias_nonempty")):
         if t is not None:
             _dev(t, name, torch.float32)
@@ -554,6 +573,25 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                       REDUCE[reduce], epi, ACCUM[accum], float(out_div), av, ast,
                       variant == "mfma", out)
     return out
+
+
+def preproject_pays(n_src: int, n_dst: int, reduce: str) -> bool:
+    """Project a low-degree relation's source rows ahead of the reduction (spmm_project
+    with W_neigh=None) when the reduction is linear and the source type has at most half
+    as many rows as the destination: the MFMA then runs the self half only (C5 bought-by,
+    1M items -> 10M users: fused 13.0 -> 10.6 ms + 0.38 ms for the 1M-row projection).
+    GNNREC_PREPROJECT=0 disables it."""
+    if os.environ.get("GNNREC_PREPROJECT", "1") == "0":
+        return False
+    return reduce in ("sum", "mean") and 2 * n_src <= n_dst
+
+
+def preproject(X: torch.Tensor, W_neigh: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Y = X W_neighᵀ: a relation's source rows projected ahead of its (linear) reduction,
+    for spmm_project(..., W_neigh=None).  Worth it where the source type has fewer rows
+    than the destination (C5 item -> user: 1M projected rows instead of 10M aggregates)."""
+    return gemm(X, W_neigh, out=out)
 
 
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -230,7 +230,12 @@ int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* indices, const
  * pick it below ~24 edges per row): 32-row tiles, [h_self | agg] staged in LDS and
  * multiplied by the register-resident weights with v_mfma_f32_32x32x2_f32, so the
  * weights are read once per 32 rows.  Same arguments, contract and aggregate bits as
- * gnnrec_spmm_project_f32; the projection's summation order differs (fp32 rounding). */
+ * gnnrec_spmm_project_f32; the projection's summation order differs (fp32 rounding).
+ * W_neighT == NULL (reduce SUM / MEAN only): X holds pre-projected source rows
+ * (X W_neigh^T, e.g. from gnnrec_gemm_f32) and the neighbour term is agg(v) itself —
+ * the projection moved ahead of the linear reduction (equal up to fp32 rounding), worth
+ * it where the source type has fewer rows than the destination.  gnnrec_spmm_project_f32
+ * rejects a NULL W_neighT (GNNREC_EINVAL). */
 int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t* indices,
                                  const float* ew, const float* X, int64_t ldx, const float* H,
                                  int64_t ldh, const float* W_selfT, const float* W_neighT,

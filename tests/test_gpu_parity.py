@@ -709,6 +709,49 @@ def test_spmm_project_matches_oracle_and_unfused(reduce, weighted, epi, variant)
                        got)
 
 
+@pytest.mark.parametrize("reduce", ["sum", "mean"])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("accum", ["store", "add"])
+def test_spmm_project_preprojected_matches_oracle(reduce, weighted, accum):
+    """W_neigh=None: the source rows are projected first (ops.preproject) and the MFMA
+    kernel aggregates them, running only the self half of the projection — against the
+    oracle's aggregate-then-project ConvLayer (reference src/model.py:143-208), so within
+    fp32 rounding, not bitwise; with bias, bias_nonempty, empty rows and a 700-edge row."""
+    from gnnrec import ops
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"pre{reduce}{weighted}{accum}".encode()))
+    n_dst, n_src, d = 3001, 1700, 128
+    deg = rng.integers(0, 40, n_dst)
+    deg[:4] = [0, 1, 2, 700]
+    dst = np.repeat(np.arange(n_dst), deg)
+    src = rng.integers(0, n_src, dst.size)
+    indptr, indices, eids = oracle.csr_from_coo(src, dst, n_dst)
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(d).astype(np.float32) * 0.1
+    bne = rng.standard_normal(d).astype(np.float32) * 0.1
+    ew = rng.integers(1, 9, dst.size).astype(np.float32)[eids] if weighted else None
+    agg = oracle.spmm_csr(indptr, indices, X, reduce, ew)
+    z = oracle.linear(H, Ws) + oracle.linear(agg, Wn) + b + (np.diff(indptr) > 0)[:, None] * bne
+    z = oracle.l2_normalize_rows_guarded(oracle.relu(z))
+    base = rng.standard_normal((n_dst, d)).astype(np.float32)
+    ref = base + z if accum == "add" else z
+    Y = ops.preproject(_t(X), _t(Wn))
+    out = _t(base)
+    ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), Y, _t(H), _t(Ws), None, reduce,
+                     None if ew is None else _t(ew), relu=True, l2norm=True, accum=accum,
+                     out=out, bias=_t(b), bias_nonempty=_t(bne))
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    with pytest.raises(ValueError):
+        ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), Y, _t(H), _t(Ws), None,
+                         "max")
+    with pytest.raises(ValueError):
+        ops.spmm_project(_t(indptr), _t(indices.astype(np.int32)), Y, _t(H), _t(Ws), None,
+                         reduce, variant="valu")
+
+
 @pytest.mark.parametrize("variant", ["valu", "mfma"])
 def test_spmm_project_accumulate_modes_and_strides(variant):
     from gnnrec import ops
@@ -949,7 +992,11 @@ def test_c5_scale_low_degree_fused_mfma_vs_oracle(deg):
                          variant="valu")
     np.testing.assert_allclose(a.cpu().numpy()[::997], v.cpu().numpy()[::997], rtol=RTOL,
                                atol=ATOL)
-    del indptr, idx, X, H, a, v
+    # the pre-projected form (1M item rows projected, the MFMA runs the self half only)
+    p = ops.spmm_project(indptr, idx, ops.preproject(X, Wn), H, Ws, None, "mean", None,
+                         relu=True, l2norm=True)
+    np.testing.assert_allclose(p[rows].cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    del indptr, idx, X, H, a, v, p
     torch.cuda.empty_cache()
 
 

@@ -32,16 +32,28 @@ def main():
     d = 128
     X = {"user": torch.randn(10_000_000, d, device=dev), "item": torch.randn(1_000_000, d, device=dev)}
     W = torch.randn(d, d, device=dev) * 0.1
+    only = os.environ.get("PROBE_REL")  # e.g. bought-by
     for ce, rs in sh.rels.items():
+        if only and ce[1] != only:
+            continue
         n = rs.indptr.numel() - 1
         deg = (rs.indptr[1:] - rs.indptr[:-1])
         out = torch.empty(n, d, device=dev)
         E = int(rs.indptr[-1])
         res = {}
-        for v in ("valu", "mfma"):
+        for v in [v for v in os.environ.get("PROBE_VARIANTS", "valu,mfma,pre").split(",")
+                  if v in ("valu", "mfma")]:
             res[v] = t(lambda: ops.spmm_project(rs.indptr, rs.indices, X[ce[0]], X[ce[2]][:n], W,
                                                 W, "mean", None, relu=True, l2norm=True, out=out,
                                                 variant=v))
+        if "pre" in os.environ.get("PROBE_VARIANTS", "valu,mfma,pre").split(","):
+            # pre-projected source rows: the fused launch runs the self half on the MFMA
+            Y = ops.preproject(X[ce[0]], W)
+            res["pre"] = t(lambda: ops.spmm_project(rs.indptr, rs.indices, Y, X[ce[2]][:n], W,
+                                                    None, "mean", None, relu=True, l2norm=True,
+                                                    out=out))
+            res["preproj"] = t(lambda: ops.preproject(X[ce[0]], W, out=Y))
+            del Y
         agg = ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean")
         res["spmm"] = t(lambda: ops.spmm(rs.indptr, rs.indices, X[ce[0]], "mean", out=agg))
         res["gemm"] = t(lambda: ops.gemm(X[ce[2]][:n], W, agg, W, relu=True, l2norm=True,
@@ -49,8 +61,9 @@ def main():
         alg = E * 516 + n * 1032  # fused: per edge row + index, per row indptr + self + out
         print(f"{ce}: rows {n} edges {E} deg max {int(deg.max())} mean {E / n:.1f} | "
               + " ".join(f"{k} {ms:.2f} ms" for k, ms in res.items())
-              + f" | fused valu {alg / res['valu'] / 1e9:.2f} TB/s, mfma "
-              f"{alg / res['mfma'] / 1e9:.2f} TB/s (algorithmic) | split_plan "
+              + " | fused " + ", ".join(f"{v} {alg / res[v] / 1e9:.2f} TB/s" for v in
+                                         ("valu", "mfma", "pre") if v in res)
+              + " (algorithmic) | split_plan "
               f"{'yes' if ops.split_plan(rs.indptr) is not None else 'no'}", flush=True)
 
 
