@@ -104,6 +104,9 @@ KERNELS = {
     "spmm_tile2": ("spmm_csr2_kernel", "gnnrec spmm_csr2_kernel (gather + segmented sums of two "
                    "relations' source-range tiles from one table in one launch)"),
     "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
+    "spmm_project2": ("spmm_project2_kernel", "gnnrec spmm_project2_kernel (two pre-projected "
+                      "relations' gathers + means into one dst row, both SAGE self projections, "
+                      "ReLU, L2 norm, cross-relation sum)"),
 }
 
 
@@ -114,8 +117,12 @@ def launch_bytes(shard, d, runner, deterministic):
     into the launch, + d*4 for the partial read back when a tile accumulates in place."""
     out = {}
     paired = {c: pair for pair in runner.tile_pairs for c in pair}
+    fused2 = {c: pair for pair in getattr(runner, 'pair_fused', ()) for c in pair}
     for ce, rs in shard.rels.items():
-        if ce in paired:  # both relations' tile bytes, one launch per segment for the pair
+        if ce in fused2:  # one launch for both: their edges, 2 indptr, the h_self row + output
+            tag, n = "spmm_project2", 1 if ce == fused2[ce][0] else 0
+            b = rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + (8 * d if n else 0))
+        elif ce in paired:  # both relations' tile bytes, one launch per segment for the pair
             tag, b = "spmm_tile2", 0
             n = len(rs.segs) if ce == paired[ce][0] else 0
             for j, (ip, ix, _) in enumerate(rs.segs):

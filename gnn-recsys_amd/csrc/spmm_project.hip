@@ -22,6 +22,7 @@
 #include "gather.hpp"
 #include "rowq.hpp"
 #include <cstdlib>
+#include <type_traits>
 
 namespace gnnrec {
 namespace {
@@ -55,13 +56,13 @@ struct EpiArgs {
   int j0;
 };
 
-__device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool valid,
-                                             float y0, float y1) {
-  if (e.relu) {
+// ReLU and the zero-guarded row L2 norm over the wave's 64 lanes (2 columns per lane)
+__device__ __forceinline__ void activate(bool relu, bool l2, float& y0, float& y1) {
+  if (relu) {
     y0 = fmaxf(y0, 0.f);
     y1 = fmaxf(y1, 0.f);
   }
-  if (e.l2) {
+  if (l2) {
     float ss = y0 * y0 + y1 * y1;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) ss += __shfl_xor(ss, off);
@@ -70,6 +71,11 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool
     y0 = y0 / nrm;
     y1 = y1 / nrm;
   }
+}
+
+__device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool valid,
+                                             float y0, float y1) {
+  activate(e.relu, e.l2, y0, y1);
   float keep = 0.f, nrm_attn = 1.f;
   if (e.attn) {  // online softmax over relations, score s = a . y (row-uniform)
     float sc = y0 * e.a0 + y1 * e.a1;
@@ -724,4 +730,243 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
 #undef GNNREC_SPM
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_project_mfma_f32");
+}
+
+// ---------------------------------------------------------------------------------------
+// Two pre-projected relations into one destination type in one launch:
+//   out[v] = combine( epi(h[v]·W_aᵀ + agg_a(v) + b_a [+ bne_a]),
+//                     epi(h[v]·W_bᵀ + agg_b(v) + b_b [+ bne_b]) ) / out_div
+// agg_r = sum / mean over relation r's in-edges of Y_r = X_r·W_neigh,rᵀ (pre-projected
+// source rows), combine = + (HeteroGraphConv sum / mean) or max.  For C5's user side
+// (clicked-by, 40 edges/row, and bought-by, 10 edges/row, both from the 1M-row item
+// table): the h_self row is read once instead of twice, the output written once instead
+// of stored and read-modified-written, and the two gathers share the waves — the
+// launch streams 50 source rows per destination row and stays HBM-bound.  The self
+// halves of both relations are the 2 × 128×128 matvec per row (the same VALU work per
+// row as the single-relation kernel's W_self + W_neigh), both W_selfᵀ resident in LDS.
+// The aggregates never touch LDS: the wave's float4-per-lane fragment is turned into
+// this lane's two output columns by four shuffles.
+namespace gnnrec {
+namespace {
+
+#ifndef GNNREC_SPP2_U
+#define GNNREC_SPP2_U 4  // gather wave-instructions in flight per lane
+#endif
+
+struct PreRel {
+  const int64_t* indptr;
+  const int32_t* indices;
+  const float* ew;
+  const float* Y;
+  int64_t ldy;
+  const float* bias_ne;
+  int mean;
+};
+
+template <bool WA, bool WB>
+__global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
+    PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
+    const float* __restrict__ WaT, const float* __restrict__ WbT,
+    const float* __restrict__ bias_a, const float* __restrict__ bias_b, int64_t n_dst,
+    int epilogue, int combine_max, float out_div, float* __restrict__ out, int64_t ldo,
+    unsigned* rq, int rq_ch) {
+  __shared__ float Wa[kPD * kPD];
+  __shared__ float Wb[kPD * kPD];
+  __shared__ float slots[kPWaves][kPRows][kPD];
+  for (int i = threadIdx.x; i < kPD * kPD / 4; i += kPWaves * 64) {
+    reinterpret_cast<float4*>(Wa)[i] = reinterpret_cast<const float4*>(WaT)[i];
+    reinterpret_cast<float4*>(Wb)[i] = reinterpret_cast<const float4*>(WbT)[i];
+  }
+  __syncthreads();
+
+  constexpr int LPR = 32, VEC = 4, U = GNNREC_SPP2_U;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = lane / LPR;
+  const int col = (lane % LPR) * VEC;
+  const int j0 = 2 * lane;
+  const bool relu = epilogue & GNNREC_EPI_RELU;
+  const bool l2 = epilogue & GNNREC_EPI_L2NORM;
+  const int64_t stride = (int64_t)gridDim.x * kPWaves * kPRows;
+  const float ba0 = bias_a ? bias_a[j0] : 0.f, ba1 = bias_a ? bias_a[j0 + 1] : 0.f;
+  const float bb0 = bias_b ? bias_b[j0] : 0.f, bb1 = bias_b ? bias_b[j0 + 1] : 0.f;
+  const float ca0 = ra.bias_ne ? ra.bias_ne[j0] : 0.f, ca1 = ra.bias_ne ? ra.bias_ne[j0 + 1] : 0.f;
+  const float cb0 = rb.bias_ne ? rb.bias_ne[j0] : 0.f, cb1 = rb.bias_ne ? rb.bias_ne[j0 + 1] : 0.f;
+
+  // a relation's bounds and first 64 indices of rows [row0, row0 + nv) (both relations'
+  // are requested before either gathers: B's indptr -> indices chain hides under A's rows)
+  struct Heads {
+    int64_t rbd[kPRows + 1];
+    int pidx[kPRows];
+  };
+  auto heads = [&](const PreRel& r, int64_t row0, int nv, Heads& h) __attribute__((always_inline)) {
+    const int64_t ipl = lane <= nv ? ld_stream(r.indptr + row0 + lane) : 0;
+#pragma unroll
+    for (int i = 0; i <= kPRows; ++i) h.rbd[i] = __shfl(ipl, i <= nv ? i : nv);
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i)
+      h.pidx[i] = i < nv && lane < h.rbd[i + 1] - h.rbd[i] ? ld_stream(r.indices + h.rbd[i] + lane)
+                                                            : 0;
+  };
+  // the aggregate of relation `r` for rows [row0, row0 + nv) into this lane's columns
+  // j0, j0 + 1 (g), and whether each row has an in-edge
+  auto gather_rel = [&](const PreRel& r, auto weighted, const Heads& h, int nv,
+                        float (&g)[kPRows][2], bool (&ne)[kPRows]) __attribute__((always_inline)) {
+    constexpr bool W = decltype(weighted)::value;
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
+      int64_t deg = 0;
+      if (i < nv) {
+        deg = h.rbd[i + 1] - h.rbd[i];
+        gather_range<LPR, VEC, GNNREC_REDUCE_SUM, W, U, true>(h.rbd[i], h.rbd[i + 1], r.indices,
+                                                              r.ew, r.Y, r.ldy, col, true, lane,
+                                                              grp, acc, h.pidx[i]);
+      }
+      combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc);
+      if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc, deg, 0);
+      ne[i] = deg > 0;
+      // lane L takes columns 2L, 2L+1 = components 2(L&1), 2(L&1)+1 of lane L/2's fragment
+      const int sl = lane >> 1;
+      const float x0 = __shfl(acc.v[0], sl), x1 = __shfl(acc.v[1], sl);
+      const float x2 = __shfl(acc.v[2], sl), x3 = __shfl(acc.v[3], sl);
+      g[i][0] = (lane & 1) ? x2 : x0;
+      g[i][1] = (lane & 1) ? x3 : x1;
+    }
+  };
+
+  auto step = [&](int64_t row0, int64_t lim) {
+    const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);  // valid rows, >= 1
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {  // self rows into this wave's slots first
+      const float4 hs = i < nv && grp == 0 ? ld_stream4(H + (row0 + i) * ldh + col)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (grp == 0) *reinterpret_cast<float4*>(&slots[wave][i][col]) = hs;
+    }
+    float ga[kPRows][2], gb[kPRows][2];
+    bool nea[kPRows], neb[kPRows];
+    Heads ha, hb;
+    heads(ra, row0, nv, ha);
+    heads(rb, row0, nv, hb);
+    gather_rel(ra, std::integral_constant<bool, WA>{}, ha, nv, ga, nea);
+    gather_rel(rb, std::integral_constant<bool, WB>{}, hb, nv, gb, neb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    float za[kPRows][2], zb[kPRows][2];
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      za[i][0] = ba0 + (nea[i] ? ca0 : 0.f);
+      za[i][1] = ba1 + (nea[i] ? ca1 : 0.f);
+      zb[i][0] = bb0 + (neb[i] ? cb0 : 0.f);
+      zb[i][1] = bb1 + (neb[i] ? cb1 : 0.f);
+    }
+#pragma unroll 2
+    for (int k = 0; k < kPD; k += 4) {
+      float4 s4[kPRows];
+#pragma unroll
+      for (int i = 0; i < kPRows; ++i) s4[i] = *reinterpret_cast<const float4*>(&slots[wave][i][k]);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float2 wa = *reinterpret_cast<const float2*>(&Wa[(k + kk) * kPD + j0]);
+        const float2 wb = *reinterpret_cast<const float2*>(&Wb[(k + kk) * kPD + j0]);
+#pragma unroll
+        for (int i = 0; i < kPRows; ++i) {
+          const float s = kk == 0 ? s4[i].x : kk == 1 ? s4[i].y : kk == 2 ? s4[i].z : s4[i].w;
+          za[i][0] = fmaf(s, wa.x, za[i][0]);
+          za[i][1] = fmaf(s, wa.y, za[i][1]);
+          zb[i][0] = fmaf(s, wb.x, zb[i][0]);
+          zb[i][1] = fmaf(s, wb.y, zb[i][1]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free for the next rows
+
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      float ya0 = za[i][0] + ga[i][0], ya1 = za[i][1] + ga[i][1];
+      float yb0 = zb[i][0] + gb[i][0], yb1 = zb[i][1] + gb[i][1];
+      activate(relu, l2, ya0, ya1);
+      activate(relu, l2, yb0, yb1);
+      float y0 = combine_max ? fmaxf(ya0, yb0) : ya0 + yb0;
+      float y1 = combine_max ? fmaxf(ya1, yb1) : ya1 + yb1;
+      if (out_div > 0.f) {
+        y0 = y0 / out_div;
+        y1 = y1 / out_div;
+      }
+      if (i < nv) {
+        typedef float f32x2s __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(f32x2s{y0, y1},
+                                    reinterpret_cast<f32x2s*>(out + (row0 + i) * ldo + j0));
+      }
+    }
+  };
+
+  if (rq != nullptr) {
+    rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
+      for (int64_t row0 = r0; row0 < r1; row0 += kPRows) step(row0, r1);
+    });
+    rq_finish(rq);
+    return;
+  }
+  for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
+       row0 += stride)
+    step(row0, n_dst);
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_spmm_project2_f32(
+    const int64_t* indptr_a, const int32_t* indices_a, const float* ew_a, const float* Ya,
+    int64_t ldya, int reduce_a, const float* bias_nonempty_a, const int64_t* indptr_b,
+    const int32_t* indices_b, const float* ew_b, const float* Yb, int64_t ldyb, int reduce_b,
+    const float* bias_nonempty_b, const float* H, int64_t ldh, const float* W_self_aT,
+    const float* W_self_bT, const float* bias_a, const float* bias_b, int64_t n_dst, int64_t d,
+    int epilogue, int combine, float out_div, float* out, int64_t ldo, void* stream) {
+  GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project2_f32: only d = %d (got %lld)", kPD,
+                 (long long)d);
+  GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
+                     (reduce_b == GNNREC_REDUCE_SUM || reduce_b == GNNREC_REDUCE_MEAN),
+                 "gnnrec_spmm_project2_f32: pre-projected relations reduce by sum or mean");
+  GNNREC_REQUIRE((epilogue & ~(GNNREC_EPI_RELU | GNNREC_EPI_L2NORM)) == 0,
+                 "gnnrec_spmm_project2_f32: epilogue must be RELU|L2NORM");
+  GNNREC_REQUIRE(combine == GNNREC_ACC_ADD || combine == GNNREC_ACC_MAX,
+                 "gnnrec_spmm_project2_f32: combine must be GNNREC_ACC_ADD or GNNREC_ACC_MAX");
+  GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project2_f32: negative n_dst");
+  if (n_dst == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(indptr_a && Ya && indptr_b && Yb && H && W_self_aT && W_self_bT && out,
+                 "gnnrec_spmm_project2_f32: null pointer");
+  GNNREC_REQUIRE(aligned16(Ya) && aligned16(Yb) && aligned16(H) && aligned16(W_self_aT) &&
+                     aligned16(W_self_bT) && ldya % 4 == 0 && ldyb % 4 == 0 && ldh % 4 == 0 &&
+                     ldo % 2 == 0 && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
+                 "gnnrec_spmm_project2_f32: Y/H/W need 16-B aligned rows, out 8-B");
+  const int64_t per_block = (int64_t)kPWaves * kPRows;
+  int64_t blocks = (n_dst + per_block - 1) / per_block;
+  const int64_t cus = device_cus() - cu_reserve();
+  if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
+  const int rq_ch = fused_chunk();
+  hipStream_t s = as_stream(stream);
+  int ticket = -1;
+  unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
+  const dim3 grid((unsigned)blocks), block(kPWaves * 64);
+  const PreRel a{indptr_a, indices_a, ew_a, Ya, ldya, bias_nonempty_a,
+                 reduce_a == GNNREC_REDUCE_MEAN};
+  const PreRel b{indptr_b, indices_b, ew_b, Yb, ldyb, bias_nonempty_b,
+                 reduce_b == GNNREC_REDUCE_MEAN};
+  const int cmax = combine == GNNREC_ACC_MAX;
+#define GNNREC_SPP2(WA_, WB_)                                                                  \
+  hipLaunchKernelGGL((spmm_project2_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,       \
+                     W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, cmax, out_div, out, \
+                     ldo, rq, rq_ch)
+  if (ew_a) {
+    if (ew_b) GNNREC_SPP2(true, true);
+    else GNNREC_SPP2(true, false);
+  } else {
+    if (ew_b) GNNREC_SPP2(false, true);
+    else GNNREC_SPP2(false, false);
+  }
+#undef GNNREC_SPP2
+  rowq_launched(ticket, s);
+  return check_launch("gnnrec_spmm_project2_f32");
 }

@@ -287,6 +287,50 @@ void spmm_project(const Tensor& indptr, const Tensor& indices, const optional<Te
      mfma ? "gnnrec_spmm_project_mfma_f32" : "gnnrec_spmm_project_f32");
 }
 
+void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const optional<Tensor>& ew_a,
+                   const Tensor& Ya, int64_t reduce_a, const optional<Tensor>& bias_nonempty_a,
+                   const Tensor& indptr_b, const Tensor& indices_b, const optional<Tensor>& ew_b,
+                   const Tensor& Yb, int64_t reduce_b, const optional<Tensor>& bias_nonempty_b,
+                   const Tensor& H, const Tensor& W_self_aT, const Tensor& W_self_bT,
+                   const optional<Tensor>& bias_a, const optional<Tensor>& bias_b,
+                   int64_t epilogue, int64_t combine, double out_div, Tensor& out) {
+  dev(indptr_a, "indptr_a", at::kLong);
+  dev(indices_a, "indices_a", at::kInt);
+  dev(ew_a, "ew_a", at::kFloat);
+  dev(Ya, "Ya", at::kFloat);
+  dev(bias_nonempty_a, "bias_nonempty_a", at::kFloat);
+  dev(indptr_b, "indptr_b", at::kLong);
+  dev(indices_b, "indices_b", at::kInt);
+  dev(ew_b, "ew_b", at::kFloat);
+  dev(Yb, "Yb", at::kFloat);
+  dev(bias_nonempty_b, "bias_nonempty_b", at::kFloat);
+  dev(H, "H", at::kFloat);
+  dev(W_self_aT, "W_self_aT", at::kFloat);
+  dev(W_self_bT, "W_self_bT", at::kFloat);
+  dev(bias_a, "bias_a", at::kFloat);
+  dev(bias_b, "bias_b", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t n_dst = indptr_a.numel() - 1, d = Ya.size(1);
+  TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1,
+                    "spmm_project2: the relations' row counts differ");
+  TORCH_CHECK_VALUE(Yb.size(1) == d && H.size(0) >= n_dst, "spmm_project2: Yb / H shapes");
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d,
+                    "]");
+  TORCH_CHECK_VALUE(W_self_aT.is_contiguous() && W_self_bT.is_contiguous(),
+                    "transposed weights must be contiguous");
+  const int64_t ldya = ld(Ya, "Ya"), ldyb = ld(Yb, "Yb"), ldh = ld(H, "H"), ldo = ld(out, "out");
+  if (meta(Ya)) return;
+  const c10::DeviceGuard g(Ya.device());
+  ck(gnnrec_spmm_project2_f32(p<int64_t>(indptr_a), p<int32_t>(indices_a), p<float>(ew_a),
+                              p<float>(Ya), ldya, (int)reduce_a, p<float>(bias_nonempty_a),
+                              p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b),
+                              p<float>(Yb), ldyb, (int)reduce_b, p<float>(bias_nonempty_b),
+                              p<float>(H), ldh, p<float>(W_self_aT), p<float>(W_self_bT),
+                              p<float>(bias_a), p<float>(bias_b), n_dst, d, (int)epilogue,
+                              (int)combine, (float)out_div, p<float>(out), ldo, stream_of(Ya)),
+     "gnnrec_spmm_project2_f32");
+}
+
 // ---------------------------------------------------------------- a7 / a8 heads
 void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                Tensor& out) {
@@ -889,6 +933,11 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor W_selfT, Tensor? W_neighT, Tensor? bias, Tensor? bias_nonempty, int reduce, "
         "int epilogue, int accum, float out_div, Tensor? attn_vec, Tensor(b!)? attn_state, "
         "bool mfma, Tensor(a!) out) -> ()");
+  m.def("spmm_project2(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, Tensor Ya, int reduce_a, "
+        "Tensor? bias_nonempty_a, Tensor indptr_b, Tensor indices_b, Tensor? ew_b, Tensor Yb, "
+        "int reduce_b, Tensor? bias_nonempty_b, Tensor H, Tensor W_self_aT, Tensor W_self_bT, "
+        "Tensor? bias_a, Tensor? bias_b, int epilogue, int combine, float out_div, "
+        "Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
         "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");
@@ -961,6 +1010,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("gemm", &gemm);                                 \
   m.impl("row_epilogue", &row_epilogue);                 \
   m.impl("spmm_project", &spmm_project);                 \
+  m.impl("spmm_project2", &spmm_project2);               \
   m.impl("sddmm_cos", &sddmm_cos);                       \
   m.impl("sddmm_cos_backward", &sddmm_cos_backward);     \
   m.impl("edge_mlp", &edge_mlp);                         \

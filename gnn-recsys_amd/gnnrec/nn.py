@@ -25,6 +25,7 @@ gradients are computed by the Functions in gnnrec/autograd.py.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -125,6 +126,21 @@ class ConvLayer(nn.Module):
         """Reference ConvLayer.forward(graph, (h_neigh, h_self)) -> z [n_dst, out_feats]."""
         return self._run(graph, x, None, 'store', 0.0)
 
+    def _pre_plan(self, graph, x):
+        """Inference: (message, reduce, edge weight) when this relation can run pre-projected
+        inside a two-relation launch (ops.spmm_project2) — a linear reduce, the fused
+        shapes, a source table at most half the destination count; else None."""
+        h_neigh, h_self = x
+        preagg, weighted, reduce = self._plan(graph)
+        if reduce not in ('sum', 'mean') or self._dropout_active() or \
+                not ops.preproject_pays(h_neigh.shape[0], graph.n_dst, reduce):
+            return None
+        m = ops.gemm(h_neigh, self.fc_preagg.weight, relu=True) if preagg else h_neigh
+        if not ops.can_spmm_project(graph.indptr, m, h_self, self.fc_self.weight,
+                                    self.fc_neigh.weight):
+            return None
+        return m, reduce, (self._edge_weight(graph) if weighted else None)
+
     def _dropout_active(self) -> bool:
         return self.training and self.dropout_fn.p > 0
 
@@ -207,6 +223,34 @@ class HeteroGraphConv(nn.Module):
         div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
         return acc, div
 
+    def _pair(self, g, ces, src_inputs, h_dst, out) -> bool:
+        """Inference, exactly two relations into one type, both pre-projectable
+        (ConvLayer._pre_plan): one ops.spmm_project2 launch with the sum / mean / max
+        combine inside (the sharded pass's _pair does the same).  GNNREC_PAIR_FUSE=0
+        disables it."""
+        if self.aggregate not in ('sum', 'mean', 'max') or \
+                os.environ.get("GNNREC_PAIR_FUSE", "1") == "0":
+            return False
+        mods = [self.mods[ce[1]] for ce in ces]
+        if bool(mods[0].norm) != bool(mods[1].norm):
+            return False
+        plans = []
+        for mod, ce in zip(mods, ces):
+            p = mod._pre_plan(g.rel_graph(ce), (src_inputs[ce[0]], h_dst))
+            if p is None:
+                return False
+            plans.append(p)
+        rels = []
+        for mod, ce, (m, reduce, ew) in zip(mods, ces, plans):
+            rg = g.rel_graph(ce)
+            rels.append((rg.indptr, rg.indices, ops.preproject(m, mod.fc_neigh.weight), reduce,
+                         ew, None))
+        combine, div = _pair_combine(self.aggregate)
+        ops.spmm_project2(rels[0], rels[1], h_dst, mods[0].fc_self.weight,
+                          mods[1].fc_self.weight, relu=True, l2norm=bool(mods[0].norm),
+                          combine=combine, out_div=div, out=out)
+        return True
+
     def forward(self, g, inputs):
         if isinstance(inputs, tuple):
             src_inputs, dst_inputs = inputs
@@ -258,6 +302,9 @@ class HeteroGraphConv(nn.Module):
             out = torch.empty((n_dst, out_feats), dtype=torch.float32,
                               device=dst_inputs[dtype].device)
             R = len(ces)
+            if R == 2 and self._pair(g, ces, src_inputs, dst_inputs[dtype], out):
+                rsts[dtype] = out
+                continue
             attn = None
             if self.aggregate == 'attention':
                 attn = (self.attn[dtype], torch.empty((n_dst, 2), dtype=torch.float32,
@@ -268,6 +315,10 @@ class HeteroGraphConv(nn.Module):
                                       out, accum, div, attn)
             rsts[dtype] = out
         return rsts
+
+
+def _pair_combine(aggregate: str):
+    return ('max' if aggregate == 'max' else 'add'), (2.0 if aggregate == 'mean' else 0.0)
 
 
 class PredictingLayer(nn.Module):

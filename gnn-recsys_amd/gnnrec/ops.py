@@ -575,6 +575,54 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
     return out
 
 
+def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None, *,
+                  relu: bool = True, l2norm: bool = False, combine: str = "add",
+                  out_div: float = 0.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Two pre-projected relations into one destination type in one launch
+    (gnnrec_spmm_project2_f32): out = combine(epi(H W_self_aᵀ + agg_a + bias_a
+    [+ bias_nonempty_a]), epi(... b ...)) / out_div.  rel_r = (indptr, indices, Y,
+    reduce, edge_weight, bias_nonempty) with Y = preproject(X_r, W_neigh_r); reduce sum
+    or mean; combine 'add' (HeteroGraphConv sum, mean with out_div=2) or 'max'."""
+    D = FUSED_D
+    args = []
+    n_dst = rel_a[0].numel() - 1
+    for name, (indptr, indices, Y, reduce, ew, bne) in (("a", rel_a), ("b", rel_b)):
+        _dev(indptr, f"indptr_{name}", torch.int64)
+        _dev(indices, f"indices_{name}", torch.int32)
+        _dev(Y, f"Y{name}", torch.float32)
+        _rowmajor(Y, f"Y{name}")
+        if reduce not in ("sum", "mean"):
+            raise ValueError("spmm_project2: pre-projected relations reduce by sum or mean")
+        if indptr.numel() - 1 != n_dst:
+            raise ValueError("spmm_project2: the relations' row counts differ")
+        if ew is not None:
+            _dev(ew, f"ew_{name}", torch.float32)
+            ew = ew.contiguous()
+        if bne is not None:
+            _dev(bne, f"bias_nonempty_{name}", torch.float32)
+            bne = bne.detach().contiguous()
+        args += [indptr, indices, ew, Y, REDUCE[reduce], bne]
+    _dev(H, "H", torch.float32)
+    _rowmajor(H, "H")
+    if combine not in ("add", "max"):
+        raise ValueError(f"spmm_project2: combine must be 'add' or 'max', not {combine!r}")
+    for W in (W_self_a, W_self_b):
+        if tuple(W.shape) != (D, D):
+            raise ValueError(f"spmm_project2 needs {D}x{D} weights")
+    if out is None:
+        out = torch.empty((n_dst, D), dtype=torch.float32, device=H.device)
+    else:
+        _dev(out, "out", torch.float32)
+        _rowmajor(out, "out")
+    bias_a = None if bias_a is None else bias_a.detach().contiguous()
+    bias_b = None if bias_b is None else bias_b.detach().contiguous()
+    epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
+    _T().spmm_project2(*args, H, W_self_a.detach().t().contiguous(),
+                       W_self_b.detach().t().contiguous(), bias_a, bias_b, epi,
+                       ACCUM[combine], float(out_div), out)
+    return out
+
+
 def preproject_pays(n_src: int, n_dst: int, reduce: str) -> bool:
     """Project a low-degree relation's source rows ahead of the reduction (spmm_project
     with W_neigh=None) when the reduction is linear and the source type has at most half

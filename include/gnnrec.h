@@ -244,6 +244,28 @@ int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t* indices,
                                  const float* attn_vec, float* attn_state, float* out,
                                  int64_t ldo, void* stream);
 
+/* Two pre-projected relations into one destination type in one launch (HeteroGraphConv
+ * with exactly two relations into the type, both reduced by sum / mean — C5's clicked-by
+ * and bought-by into users):
+ *   out[v] = combine( epi(H[v] W_self_a^T + agg_a(v) + bias_a [+ bias_nonempty_a]),
+ *                     epi(H[v] W_self_b^T + agg_b(v) + bias_b [+ bias_nonempty_b]) ) / out_div
+ * agg_r = reduce_r over relation r's in-edges of Y_r[indices_r[e]] (* ew_r[e]), Y_r the
+ * source rows already multiplied by W_neigh,r^T; combine GNNREC_ACC_ADD (sum; mean with
+ * out_div = 2) or GNNREC_ACC_MAX; out_div <= 0: none.  Both CSRs have n_dst rows.  The
+ * self row is read once and the output written once.  d = 128; alignment as
+ * gnnrec_spmm_project_f32.  Equal to the two single-relation launches up to fp32 rounding
+ * (the projection's summation order).  Replaces two ConvLayer.forward calls + the
+ * HeteroGraphConv aggregate, src/model.py:143-235,384-406. */
+int gnnrec_spmm_project2_f32(const int64_t* indptr_a, const int32_t* indices_a,
+                             const float* ew_a, const float* Ya, int64_t ldya, int reduce_a,
+                             const float* bias_nonempty_a, const int64_t* indptr_b,
+                             const int32_t* indices_b, const float* ew_b, const float* Yb,
+                             int64_t ldyb, int reduce_b, const float* bias_nonempty_b,
+                             const float* H, int64_t ldh, const float* W_self_aT,
+                             const float* W_self_bT, const float* bias_a, const float* bias_b,
+                             int64_t n_dst, int64_t d, int epilogue, int combine, float out_div,
+                             float* out, int64_t ldo, void* stream);
+
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >
  * Replaces CosinePrediction.forward, src/model.py:317-327. */

@@ -362,7 +362,10 @@ def test_full_size_pass_layers_match_oracle(full_shard, hetero):
     runner.run(feats, replicate_output=False)
     torch.cuda.synchronize()
     assert len(runner.capture) == 2
-    assert runner.fused, "the C4/C5 pass must run the fused aggregate+project kernel"
+    assert runner.fused or runner.pair_fused, \
+        "the C4/C5 pass must run a fused aggregate+project kernel"
+    if config == "c5" and hetero == "sum":  # clicked-by + bought-by as one launch
+        assert len(runner.pair_fused) == 1
     h1, h2 = runner.capture
     _layer_rows_vs_oracle(model, 0, feats, h1, lists, rows, hetero, raw_feats=True)
     _layer_rows_vs_oracle(model, 1, h1, h2, lists, rows, hetero)

@@ -752,6 +752,56 @@ def test_spmm_project_preprojected_matches_oracle(reduce, weighted, accum):
                          reduce, variant="valu")
 
 
+@pytest.mark.parametrize("combine", ["add", "mean", "max"])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_project2_two_relations_match_oracle(combine, weighted):
+    """Two pre-projected relations into one destination type in one launch against the
+    oracle's two ConvLayers + HeteroGraphConv sum / mean / max (reference
+    src/model.py:143-235,384-406): reduce mean for one relation and sum for the other,
+    empty rows, a 700-edge row, biases; within fp32 rounding."""
+    from gnnrec import ops
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"dual{combine}{weighted}".encode()))
+    n_dst, n_src, d = 2999, 900, 128
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    rels, zs, targs = [], [], []
+    for r, (reduce, hi) in enumerate((("mean", 60), ("sum", 12))):
+        deg = rng.integers(0, hi, n_dst)
+        deg[:3] = [0, 700, 1] if r == 0 else [0, 2, 0]
+        dst = np.repeat(np.arange(n_dst), deg)
+        src = rng.integers(0, n_src, dst.size)
+        indptr, indices, eids = oracle.csr_from_coo(src, dst, n_dst)
+        X = rng.standard_normal((n_src, d)).astype(np.float32)
+        Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+        Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+        b = rng.standard_normal(d).astype(np.float32) * 0.1
+        bne = rng.standard_normal(d).astype(np.float32) * 0.1
+        ew = rng.integers(1, 5, dst.size).astype(np.float32)[eids] if weighted else None
+        agg = oracle.spmm_csr(indptr, indices, X, reduce, ew)
+        z = oracle.linear(H, Ws) + oracle.linear(agg, Wn) + b + \
+            (np.diff(indptr) > 0)[:, None] * bne
+        zs.append(oracle.l2_normalize_rows_guarded(oracle.relu(z)))
+        Y = ops.preproject(_t(X), _t(Wn))
+        rels.append((_t(indptr), _t(indices.astype(np.int32)), Y, reduce,
+                     None if ew is None else _t(ew), _t(bne)))
+        targs.append((_t(Ws), _t(b)))
+    if combine == "max":
+        ref, kw = np.maximum(zs[0], zs[1]), dict(combine="max")
+    elif combine == "mean":
+        ref, kw = (zs[0] + zs[1]) / 2, dict(combine="add", out_div=2.0)
+    else:
+        ref, kw = zs[0] + zs[1], dict(combine="add")
+    out = ops.spmm_project2(rels[0], rels[1], _t(H), targs[0][0], targs[1][0], targs[0][1],
+                            targs[1][1], relu=True, l2norm=True, **kw)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    again = ops.spmm_project2(rels[0], rels[1], _t(H), targs[0][0], targs[1][0], targs[0][1],
+                              targs[1][1], relu=True, l2norm=True, **kw)
+    assert torch.equal(out, again)
+    with pytest.raises(ValueError):
+        ops.spmm_project2(rels[0], rels[1][:3] + ("max",) + rels[1][4:], _t(H), targs[0][0],
+                          targs[1][0])
+
+
 @pytest.mark.parametrize("variant", ["valu", "mfma"])
 def test_spmm_project_accumulate_modes_and_strides(variant):
     from gnnrec import ops
@@ -837,6 +887,50 @@ def test_fused_sharded_pass_equals_modules_bitwise():
     runner = ShardedFullGraphPass(model, shard)
     h3 = runner.run(lf)
     assert runner.fused == set(shard.canonical_etypes)
+    for nt in ref:
+        np.testing.assert_allclose(h3[nt][: ref[nt].shape[0]].cpu().numpy(), ref[nt], rtol=RTOL,
+                                   atol=ATOL)
+
+
+@pytest.mark.parametrize("hetero", ["sum", "mean", "max"])
+def test_pair_launch_modules_and_pass_match_oracle(hetero):
+    """Two item->user relations from a table of at most half the users (the C5 shape,
+    small): HeteroGraphConv and the sharded pass both run them as ONE pre-projected
+    spmm_project2 launch — bitwise the same at P=1 — and match the oracle's two
+    ConvLayers + sum / mean / max; the folded-embedding pass agrees within fp32 rounding."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    rng = np.random.default_rng(11)
+    n_u, n_i, d = 900, 300, 128
+    edges = {}
+    for (fwd, rev), E in ((("clicks", "clicked-by"), 24000), (("buys", "bought-by"), 5000)):
+        u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+        edges[("user", fwd, "item")] = (u, i)
+        edges[("item", rev, "user")] = (i, u)
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in edges.items()},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    feats = {"user": rng.standard_normal((n_u, d)).astype(np.float32),
+             "item": rng.standard_normal((n_i, d)).astype(np.float32)}
+    for nt, f in feats.items():
+        g.nodes[nt].data["features"] = _t(f)
+    torch.manual_seed(1)
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
+                          "cos", hetero, True).to(DEV).eval()
+    h1 = full_graph_embeddings(g, model)
+    shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
+    lf = shard.local_features(g.ndata["features"])
+    runner = ShardedFullGraphPass(model, shard, fold_embedding=False)
+    h2 = runner.run(lf)
+    assert runner.pair_fused == {(("item", "clicked-by", "user"), ("item", "bought-by", "user"))}
+    for nt in h1:
+        assert torch.equal(h1[nt], h2[nt][: h1[nt].shape[0]]), nt
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    ref = oracle.model_full_graph(oracle.Graph({"user": n_u, "item": n_i}, edges), feats, sd,
+                                  "mean", hetero, True, True)
+    for nt in ref:
+        np.testing.assert_allclose(h1[nt].cpu().numpy(), ref[nt], rtol=RTOL, atol=ATOL)
+    h3 = ShardedFullGraphPass(model, shard).run(lf)
     for nt in ref:
         np.testing.assert_allclose(h3[nt][: ref[nt].shape[0]].cpu().numpy(), ref[nt], rtol=RTOL,
                                    atol=ATOL)

@@ -67,5 +67,39 @@ def main():
               f"{'yes' if ops.split_plan(rs.indptr) is not None else 'no'}", flush=True)
 
 
+def dual():
+    """C5's two item->user relations (clicked-by 40 edges/row, bought-by 10) as one
+    pre-projected launch (ops.spmm_project2) vs the pass's two launches."""
+    dev = torch.device("cuda")
+    split = (("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2))
+    sh = bipartite_shard(10_000_000, 1_000_000, 500_000_000, 0, 1, dev, split=split)
+    d = 128
+    Xu, Xi = torch.randn(10_000_000, d, device=dev), torch.randn(1_000_000, d, device=dev)
+    W = [torch.randn(d, d, device=dev) * 0.1 for _ in range(4)]
+    ra, rb = sh.rels[("item", "clicked-by", "user")], sh.rels[("item", "bought-by", "user")]
+    Ya, Yb = ops.preproject(Xi, W[1]), ops.preproject(Xi, W[3])
+    out = torch.empty(10_000_000, d, device=dev)
+    res = {}
+    res["dual"] = t(lambda: ops.spmm_project2((ra.indptr, ra.indices, Ya, "mean", None, None),
+                                              (rb.indptr, rb.indices, Yb, "mean", None, None),
+                                              Xu, W[0], W[2], relu=True, l2norm=True,
+                                              out=out))
+
+    def two():
+        ops.spmm_project(ra.indptr, ra.indices, Xi, Xu, W[0], W[1], "mean", None, relu=True,
+                         l2norm=True, out=out)
+        ops.spmm_project(rb.indptr, rb.indices, Yb, Xu, W[2], None, "mean", None, relu=True,
+                         l2norm=True, accum="add", out=out)
+    res["two"] = t(two)
+    E = int(ra.indptr[-1]) + int(rb.indptr[-1])
+    alg = E * 516 + 10_000_000 * (16 + 1024)
+    print("user side (clicked-by + bought-by): " + " ".join(f"{k} {v:.2f} ms" for k, v in
+                                                             res.items())
+          + f" | dual {alg / res['dual'] / 1e9:.2f} TB/s (algorithmic)", flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("PROBE_DUAL") == "1":
+        dual()
+        sys.exit(0)
     main()
