@@ -945,7 +945,14 @@ extern "C" int gnnrec_spmm_project2_f32(
   int64_t blocks = (n_dst + per_block - 1) / per_block;
   const int64_t cus = device_cus() - cu_reserve();
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
-  const int rq_ch = fused_chunk();
+  // rows per queue ticket: 16 (C5 user side, one session: 38.4–38.8 ms at 8, 37.4 at 16,
+  // 37.5 at 32 — within the kernel's ±1 ms run-to-run spread); GNNREC_RQ_CHUNK_FUSED2
+  // overrides
+  static const int rq_ch = [] {
+    const char* e = getenv("GNNREC_RQ_CHUNK_FUSED2");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 16;
+  }();
   hipStream_t s = as_stream(stream);
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
