@@ -168,13 +168,16 @@ def default_workload(args) -> bool:
 
 def pmc_traffic(args, world):
     """{bench tag: HBM bytes per launch} from the newest committed rocprofv3 PMC
-    passes (profiles/<tag>_pmc_{fetch,write}.csv + <tag>_pmc_meta.json): FETCH_SIZE x2 (gfx950
+    passes of the default workload (profiles/<tag>_pmc_{fetch,write}.csv +
+    <tag>_pmc_meta.json with empty bench_args): FETCH_SIZE x2 (gfx950
     counts half the bytes of wide reads) + WRITE_SIZE, KB -> B.  Only for the default
     single-GPU C4 workload the passes ran on, and only if the HIP sources hash to the
     `csrc_sha` the profile was taken with; otherwise ({}, reason)."""
     import csv
     import glob
-    metas = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_meta.json")))
+    # the passes taken on the default workload (no extra bench arguments); newest last
+    metas = [m for m in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_meta.json")))
+             if not json.load(open(m)).get("bench_args")]
     if world != 1 or not default_workload(args):
         return {}, "not the profiled workload"
     if not metas:
