@@ -17,7 +17,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _build(agg, hetero, d=32):
+def _build(agg, hetero, d=32, two_rel=False):
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     rng = np.random.default_rng(0)
@@ -25,7 +25,7 @@ def _build(agg, hetero, d=32):
     u = rng.integers(0, n_u, E)
     i = rng.integers(0, n_i, E)
     rels = {("user", "buys", "item"): (u, i), ("item", "bought-by", "user"): (i, u)}
-    if hetero == "attention":  # a second relation per dst type (sparser: the GEMM path)
+    if hetero == "attention" or two_rel:  # a second relation per dst type (sparser)
         Ec = E // 3
         uc, ic = rng.integers(0, n_u, Ec), rng.integers(0, n_i, Ec)
         rels[("user", "clicks", "item")] = (uc, ic)
@@ -43,7 +43,7 @@ def _build(agg, hetero, d=32):
     return g, feats, model
 
 
-def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None):
+def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None, two_rel=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -51,11 +51,14 @@ def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None):
     try:
         from gnnrec.dist import Exchange
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
-        g, feats, model = _build(agg, hetero, d)
+        g, feats, model = _build(agg, hetero, d, two_rel)
         ex = Exchange()
         sh = GraphShard.from_graph(g, rank, world, "user", device="cuda", segments=segments)
         det = segments is not None if det is None else det
-        out = ShardedFullGraphPass(model, sh, ex, deterministic=det).run(sh.local_features(feats))
+        runner = ShardedFullGraphPass(model, sh, ex, deterministic=det)
+        out = runner.run(sh.local_features(feats))
+        if two_rel and hetero != "attention":  # both item->user relations in one launch
+            assert len(runner.pair_fused) == 1, runner.pair_fused
         users = gather_partitioned(sh, out["user"], ex)
         q.put((rank, users.cpu().numpy(), out["item"][:700].cpu().numpy()))
     finally:
@@ -109,6 +112,41 @@ def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
         port = _port()
         procs = [ctx.Process(target=_worker, args=(r, world, port, agg, hetero, d, q, 8))
                  for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+        for rank, users, items in res:
+            assert np.array_equal(users, base[0]), f"P={world} rank {rank}: users differ"
+            assert np.array_equal(items, base[1]), f"P={world} rank {rank}: items differ"
+
+
+@pytest.mark.parametrize("hetero", ["sum", "mean"])
+def test_deterministic_pair_launch_bitwise_across_world_sizes(hetero):
+    """Two item->user relations (the C5 shape, small) run as ONE pre-projected
+    spmm_project2 launch on every rank — the choice is made from the global user count —
+    so deterministic mode stays bitwise identical at P = 1, 2 and 4."""
+    import torch.multiprocessing as mp
+    from gnnrec.dist import Exchange
+    from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    g, feats, model = _build("mean", hetero, 128, two_rel=True)
+    with torch.no_grad():
+        ref = full_graph_embeddings(g, model, feats)
+    sh = GraphShard.from_graph(g, 0, 1, "user", device="cuda", segments=8)
+    runner = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True)
+    one = runner.run(sh.local_features(feats))
+    assert len(runner.pair_fused) == 1
+    base = (one["user"].cpu().numpy(), one["item"][:700].cpu().numpy())
+    np.testing.assert_allclose(base[0], ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(base[1], ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+    ctx = mp.get_context("spawn")
+    for world in (2, 4):
+        q = ctx.Queue()
+        port = _port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, "mean", hetero, 128, q, 8, None,
+                                                   True)) for r in range(world)]
         for p in procs:
             p.start()
         res = [q.get(timeout=300) for _ in range(world)]
