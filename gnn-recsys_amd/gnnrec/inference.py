@@ -284,10 +284,13 @@ class ShardedFullGraphPass:
             MFMA-bound and run concurrently with the HBM-bound aggregation of
             the other relation (events order every hand-off);
       RCCL  reduce-scatter / all-gather, issued async_op=True.
-    Order per layer: at world size 1, user-dst aggregation first so its GEMM
-    overlaps the item-dst aggregation; with several ranks, partial aggregation
-    first so the reduce-scatter overlaps the user-dst aggregation and the
-    all-gather overlaps the next layer's partial aggregation.
+    Order per layer: partial aggregation (the item-dst tiles) first.  At world size 1
+    the items' tree + projection GEMMs then go to the side stream under the user-dst
+    launch (C5 157.8 -> 157.0 ms, C4 -0.1 ms: the persistent user-side launch holds every
+    CU, so the GEMM blocks mostly find room only between launches; reserving CUs for them
+    costs the HBM-bound launch more — 32 CUs: C5 160.7 ms); GNNREC_OWNED_SIDE=0 restores
+    user-side-first on one stream.  With several ranks the reduce-scatter overlaps the
+    user-dst aggregation and the all-gather the next layer's partial aggregation.
 
     `ops_backend` defaults to the HIP ops (gnnrec.ops); tests on CPU ranks
     inject a checker backend with the same signatures."""
@@ -363,6 +366,11 @@ class ShardedFullGraphPass:
             self._pool[key] = t
         return t
 
+    def _par(self) -> int:
+        """Scratch set of this layer's replicated-type partials: alternating by layer when
+        the previous layer's tree + GEMMs may still read theirs on the side stream."""
+        return self._layer_idx % 2 if getattr(self, '_owned_side', False) else 0
+
     def _get(self, h, nt):
         w = self._pending.pop(id(h[nt]), None)
         if w is not None:
@@ -431,7 +439,13 @@ class ShardedFullGraphPass:
                     h[nt] = y
                 else:
                     h[nt] = O.gemm(x, W, bias=b)
+        # one rank with a side stream: the replicated type's tree + projection GEMMs run on
+        # the side stream under the partitioned type's (HBM-bound) aggregation of the same
+        # layer; the tile partials then alternate between two scratch sets by layer parity
+        self._owned_side = self.ex.ws == 1 and self.side is not None and \
+            os.environ.get("GNNREC_OWNED_SIDE", "1") != "0"
         for i, layer in enumerate(m.layers):
+            self._layer_idx = i
             self._last = i == len(m.layers) - 1
             h = self._layer(layer, h)
             if self.capture is not None:
@@ -538,7 +552,8 @@ class ShardedFullGraphPass:
                     # source-range tiles: each tile gathers from a slice of the source table
                     # small enough to stay in the Infinity Cache; accumulated in place
                     op = 'max' if reduce == 'max' else 'sum'
-                    part = self._scratch(('part', ce), (rs.n_rows, msg.shape[1]), msg.device)
+                    part = self._scratch(('part', ce, self._par()), (rs.n_rows, msg.shape[1]),
+                                         msg.device)
                     for j, (ip, ix, w) in enumerate(rs.segs):
                         with self._time('spmm_tile'):
                             O.spmm(ip, ix, msg, op, edge_weight=w if weighted else None,
@@ -603,8 +618,10 @@ class ShardedFullGraphPass:
                             shp = (ra.n_rows, msg.shape[1])
                             pa, pb = self.ops.spmm2(
                                 csr_a, csr_b, msg, 'sum',
-                                out_a=self._scratch(('tile', ca, j), shp, msg.device),
-                                out_b=self._scratch(('tile', cb, j), shp, msg.device))
+                                out_a=self._scratch(('tile', ca, j, self._par()), shp,
+                                                    msg.device),
+                                out_b=self._scratch(('tile', cb, j, self._par()), shp,
+                                                    msg.device))
                             parts[ca].append(pa)
                             parts[cb].append(pb)
                         else:
@@ -620,8 +637,8 @@ class ShardedFullGraphPass:
                     if j % 2 == 0:
                         parts[ce].append(self.ops.spmm(
                             ip, ix, msg, 'sum', edge_weight=ew, split=TILE_SPLIT,
-                            out=self._scratch(('tile', ce, j), (rs.n_rows, msg.shape[1]),
-                                              msg.device)))
+                            out=self._scratch(('tile', ce, j, self._par()),
+                                              (rs.n_rows, msg.shape[1]), msg.device)))
                     else:
                         self.ops.spmm(ip, ix, msg, 'sum', edge_weight=ew, out=parts[ce][-1],
                                       accumulate=True, split=TILE_SPLIT)
@@ -872,9 +889,32 @@ class ShardedFullGraphPass:
                 self._pending[id(table)] = work
             out[T] = table
 
+    def _owned_on_side(self, hconv, h, active, partials, out):
+        """_owned on the side stream (one rank): ordered after the tiles queued on main,
+        its outputs handed to later main-stream readers by an event (_get)."""
+        main = torch.cuda.current_stream(self.shard.device)
+        self.side.wait_stream(main)
+        produced = {}
+        with torch.cuda.stream(self.side):
+            self._owned(hconv, h, active, partials, produced)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        for T, t in produced.items():
+            t.record_stream(main)  # read on main later: not recycled under it
+            self._ready[id(t)] = ev
+            out[T] = t
+
     def _layer(self, hconv, h):
         active = self._active(hconv, h)
         out = {}
+        if self._owned_side:
+            # tiles (main) -> tree + GEMMs of the replicated type (side) under the
+            # partitioned type's launch (main), whose inputs are the previous layer's
+            partials = self._partials(hconv, h, active)
+            self._owned_on_side(hconv, h, active, partials, out)
+            self._local(hconv, h, active, out)
+            self._fold.clear()
+            return out
         if self.ex.ws > 1:
             partials = self._partials(hconv, h, active)
             self._local(hconv, h, active, out)
