@@ -90,7 +90,7 @@ class BlockSampler:
             for ce, eids in exclude_eids.items():
                 ce = g.to_canonical_etype(ce)
                 m = self._mask(g, ce)
-                m[eids] = 1
+                m.index_fill_(0, eids, 1)  # (m[eids] = 1 copies the scalar: a host sync)
                 masks[ce] = (m, eids)
         blocks = []
         try:
@@ -101,7 +101,7 @@ class BlockSampler:
                          if block.number_of_src_nodes(nt) > 0}
         finally:
             for ce, (m, eids) in masks.items():
-                m[eids] = 0
+                m.index_fill_(0, eids, 0)
         # copy edge data into every block and node data into the input block (DGL copies
         # features at block creation; the reference reads blocks[0].srcdata['features'])
         for b in blocks:
@@ -319,7 +319,10 @@ def _maybe_prefetch(loader, make_iter):
 
 
 def _split_by_type(idx, flat_ids, type_starts, n_types):
-    """Batch positions -> per-type id slices, batch order kept within a type; one readback."""
+    """Batch positions -> per-type id slices, batch order kept within a type; one readback
+    (none for a single edge type: the reference's training loaders batch one type)."""
+    if n_types == 1:
+        return [flat_ids[idx]]
     ty = torch.bucketize(idx, type_starts[1:], right=True)
     order = torch.argsort(ty, stable=True)
     ids = flat_ids[idx[order]]
