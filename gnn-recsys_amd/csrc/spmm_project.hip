@@ -737,7 +737,8 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
 //   out[v] = combine( epi(h[v]·W_aᵀ + agg_a(v) + b_a [+ bne_a]),
 //                     epi(h[v]·W_bᵀ + agg_b(v) + b_b [+ bne_b]) ) / out_div
 // agg_r = sum / mean over relation r's in-edges of Y_r = X_r·W_neigh,rᵀ (pre-projected
-// source rows), combine = + (HeteroGraphConv sum / mean) or max.  For C5's user side
+// source rows), combine = + (HeteroGraphConv sum / mean), max, or the per-relation
+// attention softmax of s_r = a·y_r (the build-defined C5 aggregate).  For C5's user side
 // (clicked-by, 40 edges/row, and bought-by, 10 edges/row, both from the 1M-row item
 // table): the h_self row is read once instead of twice, the output written once instead
 // of stored and read-modified-written, and the two gathers share the waves — the
@@ -768,7 +769,8 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
     PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
     const float* __restrict__ WaT, const float* __restrict__ WbT,
     const float* __restrict__ bias_a, const float* __restrict__ bias_b, int64_t n_dst,
-    int epilogue, int combine_max, float out_div, float* __restrict__ out, int64_t ldo,
+    int epilogue, int combine, const float* __restrict__ attn_vec, float out_div,
+    float* __restrict__ out, int64_t ldo,
     unsigned* rq, int rq_ch) {
   __shared__ float Wa[kPD * kPD];
   __shared__ float Wb[kPD * kPD];
@@ -791,6 +793,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
   const float bb0 = bias_b ? bias_b[j0] : 0.f, bb1 = bias_b ? bias_b[j0 + 1] : 0.f;
   const float ca0 = ra.bias_ne ? ra.bias_ne[j0] : 0.f, ca1 = ra.bias_ne ? ra.bias_ne[j0 + 1] : 0.f;
   const float cb0 = rb.bias_ne ? rb.bias_ne[j0] : 0.f, cb1 = rb.bias_ne ? rb.bias_ne[j0 + 1] : 0.f;
+  const float at0 = attn_vec ? attn_vec[j0] : 0.f, at1 = attn_vec ? attn_vec[j0 + 1] : 0.f;
 
   // a relation's bounds and first 64 indices of rows [row0, row0 + nv) (both relations'
   // are requested before either gathers: B's indptr -> indices chain hides under A's rows)
@@ -888,8 +891,30 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
       float yb0 = zb[i][0] + gb[i][0], yb1 = zb[i][1] + gb[i][1];
       activate(relu, l2, ya0, ya1);
       activate(relu, l2, yb0, yb1);
-      float y0 = combine_max ? fmaxf(ya0, yb0) : ya0 + yb0;
-      float y1 = combine_max ? fmaxf(ya1, yb1) : ya1 + yb1;
+      float y0, y1;
+      if (combine == GNNREC_ACC_MAX) {
+        y0 = fmaxf(ya0, yb0);
+        y1 = fmaxf(ya1, yb1);
+      } else if (combine == GNNREC_ACC_ATTN_LAST) {
+        // softmax over the two relations of s_r = a·y_r, in the order of the single-relation
+        // launches' online form: a first (max s_a, sum 1), then b rescales and normalises
+        float sa = ya0 * at0 + ya1 * at1, sb = yb0 * at0 + yb1 * at1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          sa += __shfl_xor(sa, off);
+          sb += __shfl_xor(sb, off);
+        }
+        const float mnew = fmaxf(sa, sb);
+        const float keep = expf(sa - mnew), cnew = expf(sb - mnew);
+        const float nrm = 1.f / (1.f * keep + cnew);
+        y0 = ya0 * keep + yb0 * cnew;
+        y1 = ya1 * keep + yb1 * cnew;
+        y0 *= nrm;
+        y1 *= nrm;
+      } else {
+        y0 = ya0 + yb0;
+        y1 = ya1 + yb1;
+      }
       if (out_div > 0.f) {
         y0 = y0 / out_div;
         y1 = y1 / out_div;
@@ -923,7 +948,8 @@ extern "C" int gnnrec_spmm_project2_f32(
     const int32_t* indices_b, const float* ew_b, const float* Yb, int64_t ldyb, int reduce_b,
     const float* bias_nonempty_b, const float* H, int64_t ldh, const float* W_self_aT,
     const float* W_self_bT, const float* bias_a, const float* bias_b, int64_t n_dst, int64_t d,
-    int epilogue, int combine, float out_div, float* out, int64_t ldo, void* stream) {
+    int epilogue, int combine, const float* attn_vec, float out_div, float* out, int64_t ldo,
+    void* stream) {
   GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project2_f32: only d = %d (got %lld)", kPD,
                  (long long)d);
   GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
@@ -931,8 +957,11 @@ extern "C" int gnnrec_spmm_project2_f32(
                  "gnnrec_spmm_project2_f32: pre-projected relations reduce by sum or mean");
   GNNREC_REQUIRE((epilogue & ~(GNNREC_EPI_RELU | GNNREC_EPI_L2NORM)) == 0,
                  "gnnrec_spmm_project2_f32: epilogue must be RELU|L2NORM");
-  GNNREC_REQUIRE(combine == GNNREC_ACC_ADD || combine == GNNREC_ACC_MAX,
-                 "gnnrec_spmm_project2_f32: combine must be GNNREC_ACC_ADD or GNNREC_ACC_MAX");
+  GNNREC_REQUIRE(combine == GNNREC_ACC_ADD || combine == GNNREC_ACC_MAX ||
+                     combine == GNNREC_ACC_ATTN_LAST,
+                 "gnnrec_spmm_project2_f32: combine must be GNNREC_ACC_ADD, _MAX or _ATTN_LAST");
+  GNNREC_REQUIRE((combine == GNNREC_ACC_ATTN_LAST) == (attn_vec != nullptr),
+                 "gnnrec_spmm_project2_f32: attn_vec goes with combine GNNREC_ACC_ATTN_LAST");
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_project2_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
   GNNREC_REQUIRE(indptr_a && Ya && indptr_b && Yb && H && W_self_aT && W_self_bT && out,
@@ -961,11 +990,10 @@ extern "C" int gnnrec_spmm_project2_f32(
                  reduce_a == GNNREC_REDUCE_MEAN};
   const PreRel b{indptr_b, indices_b, ew_b, Yb, ldyb, bias_nonempty_b,
                  reduce_b == GNNREC_REDUCE_MEAN};
-  const int cmax = combine == GNNREC_ACC_MAX;
 #define GNNREC_SPP2(WA_, WB_)                                                                  \
   hipLaunchKernelGGL((spmm_project2_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,       \
-                     W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, cmax, out_div, out, \
-                     ldo, rq, rq_ch)
+                     W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine, attn_vec,  \
+                     out_div, out, ldo, rq, rq_ch)
   if (ew_a) {
     if (ew_b) GNNREC_SPP2(true, true);
     else GNNREC_SPP2(true, false);

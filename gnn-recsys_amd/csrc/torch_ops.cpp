@@ -293,7 +293,8 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
                    const Tensor& Yb, int64_t reduce_b, const optional<Tensor>& bias_nonempty_b,
                    const Tensor& H, const Tensor& W_self_aT, const Tensor& W_self_bT,
                    const optional<Tensor>& bias_a, const optional<Tensor>& bias_b,
-                   int64_t epilogue, int64_t combine, double out_div, Tensor& out) {
+                   int64_t epilogue, int64_t combine, const optional<Tensor>& attn_vec,
+                   double out_div, Tensor& out) {
   dev(indptr_a, "indptr_a", at::kLong);
   dev(indices_a, "indices_a", at::kInt);
   dev(ew_a, "ew_a", at::kFloat);
@@ -309,6 +310,7 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
   dev(W_self_bT, "W_self_bT", at::kFloat);
   dev(bias_a, "bias_a", at::kFloat);
   dev(bias_b, "bias_b", at::kFloat);
+  dev(attn_vec, "attn_vec", at::kFloat);
   dev(out, "out", at::kFloat);
   const int64_t n_dst = indptr_a.numel() - 1, d = Ya.size(1);
   TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1,
@@ -327,7 +329,8 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
                               p<float>(Yb), ldyb, (int)reduce_b, p<float>(bias_nonempty_b),
                               p<float>(H), ldh, p<float>(W_self_aT), p<float>(W_self_bT),
                               p<float>(bias_a), p<float>(bias_b), n_dst, d, (int)epilogue,
-                              (int)combine, (float)out_div, p<float>(out), ldo, stream_of(Ya)),
+                              (int)combine, p<float>(attn_vec), (float)out_div, p<float>(out),
+                              ldo, stream_of(Ya)),
      "gnnrec_spmm_project2_f32");
 }
 
@@ -936,8 +939,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("spmm_project2(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, Tensor Ya, int reduce_a, "
         "Tensor? bias_nonempty_a, Tensor indptr_b, Tensor indices_b, Tensor? ew_b, Tensor Yb, "
         "int reduce_b, Tensor? bias_nonempty_b, Tensor H, Tensor W_self_aT, Tensor W_self_bT, "
-        "Tensor? bias_a, Tensor? bias_b, int epilogue, int combine, float out_div, "
-        "Tensor(a!) out) -> ()");
+        "Tensor? bias_a, Tensor? bias_b, int epilogue, int combine, Tensor? attn_vec, "
+        "float out_div, Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
         "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");

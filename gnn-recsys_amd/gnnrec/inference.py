@@ -775,12 +775,13 @@ class ShardedFullGraphPass:
         spmm_project2 launch reads each user row once and writes it once (C5 user side
         39.0 ms vs 41.0 ms for the two fused launches).  GNNREC_PAIR_FUSE=0 disables it.
         In deterministic mode the decision uses the global user count (same on every
-        rank); the HeteroGraphConv combine runs in the kernel (sum, mean as /2, max)."""
+        rank); the HeteroGraphConv combine runs in the kernel (sum, mean as /2, max, the
+        attention softmax over the two relations)."""
         sh, O = self.shard, self.ops
         T = sh.ptype
         if getattr(O, 'spmm_project2', None) is None or \
                 os.environ.get("GNNREC_PAIR_FUSE", "1") == "0" or \
-                hconv.aggregate not in ('sum', 'mean', 'max'):
+                hconv.aggregate not in ('sum', 'mean', 'max', 'attention'):
             return False
         n_dec = sh.num_nodes[T] if self.deterministic else sh.n_own
         plan = []
@@ -814,11 +815,13 @@ class ShardedFullGraphPass:
         mod = plan[0][0]
         o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
                         device=self_rows.device)
+        from .nn import _pair_combine
+        combine, div = _pair_combine(hconv.aggregate)
         with self._time('spmm_project2'):
             O.spmm_project2(rels[0], rels[1], self_rows, Wself[0], Wself[1], biases[0],
-                            biases[1], relu=True, l2norm=bool(mod.norm),
-                            combine='max' if hconv.aggregate == 'max' else 'add',
-                            out_div=2.0 if hconv.aggregate == 'mean' else 0.0, out=o)
+                            biases[1], relu=True, l2norm=bool(mod.norm), combine=combine,
+                            out_div=div, out=o,
+                            attn_vec=hconv.attn[T] if combine == 'attention' else None)
         self.pair_fused.add((ces[0], ces[1]))
         out[T] = o
         return True

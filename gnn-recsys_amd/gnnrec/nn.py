@@ -228,7 +228,7 @@ class HeteroGraphConv(nn.Module):
         (ConvLayer._pre_plan): one ops.spmm_project2 launch with the sum / mean / max
         combine inside (the sharded pass's _pair does the same).  GNNREC_PAIR_FUSE=0
         disables it."""
-        if self.aggregate not in ('sum', 'mean', 'max') or \
+        if self.aggregate not in ('sum', 'mean', 'max', 'attention') or \
                 os.environ.get("GNNREC_PAIR_FUSE", "1") == "0":
             return False
         mods = [self.mods[ce[1]] for ce in ces]
@@ -246,9 +246,11 @@ class HeteroGraphConv(nn.Module):
             rels.append((rg.indptr, rg.indices, ops.preproject(m, mod.fc_neigh.weight), reduce,
                          ew, None))
         combine, div = _pair_combine(self.aggregate)
+        dtype = ces[0][2]
         ops.spmm_project2(rels[0], rels[1], h_dst, mods[0].fc_self.weight,
                           mods[1].fc_self.weight, relu=True, l2norm=bool(mods[0].norm),
-                          combine=combine, out_div=div, out=out)
+                          combine=combine, out_div=div, out=out,
+                          attn_vec=self.attn[dtype] if combine == 'attention' else None)
         return True
 
     def forward(self, g, inputs):
@@ -318,7 +320,10 @@ class HeteroGraphConv(nn.Module):
 
 
 def _pair_combine(aggregate: str):
-    return ('max' if aggregate == 'max' else 'add'), (2.0 if aggregate == 'mean' else 0.0)
+    """(spmm_project2 combine, out_div) of a HeteroGraphConv aggregate over two relations."""
+    if aggregate in ('max', 'attention'):
+        return aggregate, 0.0
+    return 'add', (2.0 if aggregate == 'mean' else 0.0)
 
 
 class PredictingLayer(nn.Module):

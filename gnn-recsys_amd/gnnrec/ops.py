@@ -577,12 +577,14 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
 
 def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None, *,
                   relu: bool = True, l2norm: bool = False, combine: str = "add",
-                  out_div: float = 0.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out_div: float = 0.0, out: Optional[torch.Tensor] = None,
+                  attn_vec: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Two pre-projected relations into one destination type in one launch
     (gnnrec_spmm_project2_f32): out = combine(epi(H W_self_aᵀ + agg_a + bias_a
     [+ bias_nonempty_a]), epi(... b ...)) / out_div.  rel_r = (indptr, indices, Y,
     reduce, edge_weight, bias_nonempty) with Y = preproject(X_r, W_neigh_r); reduce sum
-    or mean; combine 'add' (HeteroGraphConv sum, mean with out_div=2) or 'max'."""
+    or mean; combine 'add' (HeteroGraphConv sum, mean with out_div=2), 'max', or
+    'attention' with attn_vec [d] (softmax over the two relations of attn_vec·y_r)."""
     D = FUSED_D
     args = []
     n_dst = rel_a[0].numel() - 1
@@ -604,8 +606,16 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
         args += [indptr, indices, ew, Y, REDUCE[reduce], bne]
     _dev(H, "H", torch.float32)
     _rowmajor(H, "H")
-    if combine not in ("add", "max"):
-        raise ValueError(f"spmm_project2: combine must be 'add' or 'max', not {combine!r}")
+    if combine not in ("add", "max", "attention"):
+        raise ValueError(f"spmm_project2: combine must be 'add', 'max' or 'attention', "
+                         f"not {combine!r}")
+    if (combine == "attention") != (attn_vec is not None):
+        raise ValueError("spmm_project2: attn_vec goes with combine='attention'")
+    if attn_vec is not None:
+        _dev(attn_vec, "attn_vec", torch.float32)
+        if attn_vec.numel() != D:
+            raise ValueError(f"attn_vec must have {D} entries")
+        attn_vec = attn_vec.detach().contiguous()
     for W in (W_self_a, W_self_b):
         if tuple(W.shape) != (D, D):
             raise ValueError(f"spmm_project2 needs {D}x{D} weights")
@@ -619,7 +629,8 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
     _T().spmm_project2(*args, H, W_self_a.detach().t().contiguous(),
                        W_self_b.detach().t().contiguous(), bias_a, bias_b, epi,
-                       ACCUM[combine], float(out_div), out)
+                       ACCUM["attn_last" if combine == "attention" else combine], attn_vec,
+                       float(out_div), out)
     return out
 
 

@@ -251,7 +251,9 @@ int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t* indices,
  *                     epi(H[v] W_self_b^T + agg_b(v) + bias_b [+ bias_nonempty_b]) ) / out_div
  * agg_r = reduce_r over relation r's in-edges of Y_r[indices_r[e]] (* ew_r[e]), Y_r the
  * source rows already multiplied by W_neigh,r^T; combine GNNREC_ACC_ADD (sum; mean with
- * out_div = 2) or GNNREC_ACC_MAX; out_div <= 0: none.  Both CSRs have n_dst rows.  The
+ * out_div = 2), GNNREC_ACC_MAX, or GNNREC_ACC_ATTN_LAST with attn_vec [d] (out = the
+ * softmax over r of attn_vec . y_r weighting the y_r; attn_vec NULL otherwise); out_div <= 0:
+ * none.  Both CSRs have n_dst rows.  The
  * self row is read once and the output written once.  d = 128; alignment as
  * gnnrec_spmm_project_f32.  Equal to the two single-relation launches up to fp32 rounding
  * (the projection's summation order).  Replaces two ConvLayer.forward calls + the
@@ -263,8 +265,9 @@ int gnnrec_spmm_project2_f32(const int64_t* indptr_a, const int32_t* indices_a,
                              int64_t ldyb, int reduce_b, const float* bias_nonempty_b,
                              const float* H, int64_t ldh, const float* W_self_aT,
                              const float* W_self_bT, const float* bias_a, const float* bias_b,
-                             int64_t n_dst, int64_t d, int epilogue, int combine, float out_div,
-                             float* out, int64_t ldo, void* stream);
+                             int64_t n_dst, int64_t d, int epilogue, int combine,
+                             const float* attn_vec, float out_div, float* out, int64_t ldo,
+                             void* stream);
 
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >

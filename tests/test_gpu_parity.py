@@ -752,7 +752,7 @@ def test_spmm_project_preprojected_matches_oracle(reduce, weighted, accum):
                          reduce, variant="valu")
 
 
-@pytest.mark.parametrize("combine", ["add", "mean", "max"])
+@pytest.mark.parametrize("combine", ["add", "mean", "max", "attention"])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_project2_two_relations_match_oracle(combine, weighted):
     """Two pre-projected relations into one destination type in one launch against the
@@ -785,7 +785,14 @@ def test_spmm_project2_two_relations_match_oracle(combine, weighted):
         rels.append((_t(indptr), _t(indices.astype(np.int32)), Y, reduce,
                      None if ew is None else _t(ew), _t(bne)))
         targs.append((_t(Ws), _t(b)))
-    if combine == "max":
+    if combine == "attention":  # softmax over the two relations of a . z_r, per row
+        a = rng.standard_normal(d).astype(np.float32)
+        sc = np.stack([z @ a for z in zs])
+        w = np.exp(sc - sc.max(0))
+        w /= w.sum(0)
+        ref, kw = w[0][:, None] * zs[0] + w[1][:, None] * zs[1], dict(combine="attention",
+                                                                     attn_vec=_t(a))
+    elif combine == "max":
         ref, kw = np.maximum(zs[0], zs[1]), dict(combine="max")
     elif combine == "mean":
         ref, kw = (zs[0] + zs[1]) / 2, dict(combine="add", out_div=2.0)
@@ -892,7 +899,7 @@ def test_fused_sharded_pass_equals_modules_bitwise():
                                    atol=ATOL)
 
 
-@pytest.mark.parametrize("hetero", ["sum", "mean", "max"])
+@pytest.mark.parametrize("hetero", ["sum", "mean", "max", "attention"])
 def test_pair_launch_modules_and_pass_match_oracle(hetero):
     """Two item->user relations from a table of at most half the users (the C5 shape,
     small): HeteroGraphConv and the sharded pass both run them as ONE pre-projected
@@ -1172,8 +1179,10 @@ def test_attention_hetero_aggregate_matches_oracle(d, dense):
     shard = GraphShard.from_graph(g, 0, 1, "user", device=DEV)
     runner = ShardedFullGraphPass(model, shard)
     h2 = runner.run(shard.local_features(g.ndata["features"]))
-    if d == 128 and dense:
-        assert runner.fused == set(shard.canonical_etypes)
+    if d == 128 and dense:  # every relation fused; the two into users as one pair launch
+        assert runner.fused | {c for p in runner.pair_fused for c in p} == \
+            set(shard.canonical_etypes)
+        assert len(runner.pair_fused) == 1
     h3 = model.embed(g.ndata["features"])  # autograd path (parameters require grad)
     for layer in model.layers:
         h3 = layer(g, h3)
