@@ -297,6 +297,9 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 // the MFMA waves' registers, one barrier per pipelined step) took 17–22 ms: 8 gathering
 // waves per CU cannot keep HBM busy at 10 edges per row.  The sharded pass fuses such a
 // relation only in the PRE form (else gather + GEMM on the side stream).
+#ifndef GNNREC_SPP_UDEF
+#define GNNREC_SPP_UDEF 4  // the VALU kernel's default gather unroll (GNNREC_SPP_UNROLL=2|8 env)
+#endif
 #ifndef GNNREC_SPM_U
 #define GNNREC_SPM_U 4  // gather wave-instructions in flight per lane (rows > 64 edges)
 #endif
@@ -639,7 +642,7 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   do {                                                    \
     if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \
     else if (unroll == 2) GNNREC_SPP_ONE(R, W, 2);        \
-    else GNNREC_SPP_ONE(R, W, 4);                         \
+    else GNNREC_SPP_ONE(R, W, GNNREC_SPP_UDEF);           \
   } while (0)
   if (ew) {
     if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPP(GNNREC_REDUCE_SUM, true);
