@@ -263,6 +263,7 @@ __global__ void mark_ids_kernel(const int64_t* __restrict__ ids, int64_t n,
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t id = ids[i];
+  if (id < 0) return;  // unused capacity of a bounded sample buffer
   if (prefix_pos[id] < 0) mark[id] = 1;  // benign race: all writers store 1
 }
 
@@ -273,6 +274,10 @@ __global__ void relabel_kernel(const int64_t* __restrict__ ids, int64_t n,
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t id = ids[i];
+  if (id < 0) {  // unused capacity of a bounded sample buffer
+    local[i] = -1;
+    return;
+  }
   const int64_t p = prefix_pos[id];
   local[i] = p >= 0 ? p : n_prefix + rank[id];
 }

@@ -814,6 +814,13 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
                       "sample_layer: node-type index out of range");
   TORCH_CHECK_VALUE(NT > 0, "sample_layer: no node types");
   const c10::DeviceGuard g(seeds[0].device());
+  // Bounded fanouts (every relation samples at most fanout >= 0 in-edges per seed): the
+  // fills write into capacity-sized buffers (seeds x fanout, unused tail = -1, which the
+  // mark / relabel kernels skip) and the new-source scan runs before any size is known,
+  // so the layer's edge counts and new-node counts come back in ONE readback.  Unbounded
+  // (full-neighbour) layers read the edge counts first to size the fills (two readbacks).
+  bool bounded = true;
+  for (size_t r = 0; r < R; ++r) bounded = bounded && fanouts[r] >= 0;
   // counts -> out indptr per relation
   std::vector<Tensor> o_ip(R), o_src(R), o_eid(R), src_loc(R), src_nid(NT);
   for (size_t r = 0; r < R; ++r) {
@@ -824,16 +831,23 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
     o_ip[r] = exclusive_scan_new(counts);
   }
   std::vector<int64_t> totals(R, 0);
-  if (R) {
+  auto read_totals = [&](std::vector<Tensor> extra) {  // one device -> host copy
     std::vector<Tensor> last;
     for (size_t r = 0; r < R; ++r) last.push_back(o_ip[r].narrow(0, o_ip[r].numel() - 1, 1));
-    const Tensor t = at::cat(last).to(at::kCPU);  // the layer's one size readback
+    for (auto& t : extra) last.push_back(t);
+    const Tensor t = at::cat(last).to(at::kCPU);
     for (size_t r = 0; r < R; ++r) totals[r] = t.data_ptr<int64_t>()[r];
-  }
+    std::vector<int64_t> rest;
+    for (size_t i = R; i < last.size(); ++i) rest.push_back(t.data_ptr<int64_t>()[i]);
+    return rest;
+  };
+  if (R && !bounded) read_totals({});  // the unbounded layer's first readback
   for (size_t r = 0; r < R; ++r) {
     const Tensor& sd = seeds[dst_type[r]];
-    o_src[r] = at::empty({totals[r]}, sd.options().dtype(at::kLong));
-    o_eid[r] = at::empty({totals[r]}, sd.options().dtype(at::kLong));
+    const int64_t cap = bounded ? sd.numel() * fanouts[r] : totals[r];
+    o_src[r] = bounded ? at::full({cap}, -1, sd.options().dtype(at::kLong))
+                       : at::empty({cap}, sd.options().dtype(at::kLong));
+    o_eid[r] = at::empty({cap}, sd.options().dtype(at::kLong));
     const optional<Tensor> m = masks.get(r);
     sample_fill(indptrs[r], indices[r], eids[r], m, sd, fanouts[r], keys[r], o_ip[r], o_src[r],
                 o_eid[r]);
@@ -847,31 +861,71 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
       if ((size_t)src_type[r] == t) mark_ids(o_src[r], pp, mk);
     rank[t] = exclusive_scan_new(mk);
   }
+  // local source ids and (bounded) the fresh nodes, before any count is on the host
+  std::vector<Tensor> nodes(NT);
+  auto relabel_all = [&](size_t t) {
+    Tensor pp = prefix_pos[t];
+    const int64_t n_p = seeds[t].numel();
+    for (size_t r = 0; r < R; ++r) {
+      if ((size_t)src_type[r] != t) continue;
+      Tensor loc = at::empty({o_src[r].numel()}, seeds[t].options().dtype(at::kLong));
+      relabel_ids(o_src[r], pp, rank[t], n_p, loc);
+      src_loc[r] = loc;
+    }
+  };
   std::vector<int64_t> n_new(NT, 0);
-  {
+  if (bounded) {
+    for (size_t t = 0; t < NT; ++t) {
+      const Tensor& pre = seeds[t];
+      const int64_t n_p = pre.numel();
+      int64_t cap = 0;  // new sources of type t: at most the sampled edges from it
+      for (size_t r = 0; r < R; ++r)
+        if ((size_t)src_type[r] == t) cap += o_src[r].numel();
+      cap = std::min(cap, marks[t].numel());
+      nodes[t] = at::empty({n_p + cap}, pre.options().dtype(at::kLong));
+      nodes[t].narrow(0, 0, n_p).copy_(pre);
+      if (cap) {
+        Tensor tail = nodes[t].narrow(0, n_p, cap);
+        compact_marked(marks[t], rank[t], tail);
+      }
+      relabel_all(t);
+    }
+    std::vector<Tensor> last;
+    for (size_t t = 0; t < NT; ++t) last.push_back(rank[t].narrow(0, rank[t].numel() - 1, 1));
+    const std::vector<int64_t> nn = read_totals(last);  // the layer's one size readback
+    for (size_t t = 0; t < NT; ++t) n_new[t] = nn[t];
+    for (size_t r = 0; r < R; ++r) {
+      o_src[r] = o_src[r].narrow(0, 0, totals[r]);
+      o_eid[r] = o_eid[r].narrow(0, 0, totals[r]);
+    }
+  } else {
     std::vector<Tensor> last;
     for (size_t t = 0; t < NT; ++t) last.push_back(rank[t].narrow(0, rank[t].numel() - 1, 1));
     const Tensor c = at::cat(last).to(at::kCPU);  // the layer's second size readback
     for (size_t t = 0; t < NT; ++t) n_new[t] = c.data_ptr<int64_t>()[t];
+    for (size_t t = 0; t < NT; ++t) {
+      const Tensor& pre = seeds[t];
+      const int64_t n_p = pre.numel();
+      nodes[t] = at::empty({n_p + n_new[t]}, pre.options().dtype(at::kLong));
+      nodes[t].narrow(0, 0, n_p).copy_(pre);
+      if (n_new[t]) {
+        Tensor fresh = nodes[t].narrow(0, n_p, n_new[t]);
+        compact_marked(marks[t], rank[t], fresh);
+      }
+      relabel_all(t);
+    }
   }
   for (size_t t = 0; t < NT; ++t) {
-    Tensor pp = prefix_pos[t], mk = marks[t];
     const Tensor& pre = seeds[t];
     const int64_t n_p = pre.numel();
-    Tensor nodes = at::empty({n_p + n_new[t]}, pre.options().dtype(at::kLong));
-    nodes.narrow(0, 0, n_p).copy_(pre);
-    Tensor fresh = nodes.narrow(0, n_p, n_new[t]);
-    if (n_new[t]) compact_marked(mk, rank[t], fresh);
-    for (size_t r = 0; r < R; ++r) {
-      if ((size_t)src_type[r] != t) continue;
-      Tensor loc = at::empty({o_src[r].numel()}, pre.options().dtype(at::kLong));
-      relabel_ids(o_src[r], pp, rank[t], n_p, loc);
-      src_loc[r] = loc.to(at::kInt);
-    }
+    Tensor fresh = nodes[t].narrow(0, n_p, n_new[t]);
+    Tensor pp = prefix_pos[t], mk = marks[t];
     clear_prefix_pos(pre, pp);
     if (n_new[t]) mk.index_fill_(0, fresh, 0);
-    src_nid[t] = nodes;
+    src_nid[t] = bounded ? nodes[t].narrow(0, 0, n_p + n_new[t]) : nodes[t];
   }
+  for (size_t r = 0; r < R; ++r)
+    src_loc[r] = src_loc[r].narrow(0, 0, totals[r]).to(at::kInt);
   return {o_ip, src_loc, o_eid, src_nid, totals};
 }
 

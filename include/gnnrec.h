@@ -307,7 +307,8 @@ int gnnrec_exclusive_scan_i32(const int32_t* in, int64_t n, int64_t* out, void* 
                               void* stream);
 /* relabel (DGL to_block): mark[id] = 1 for every id in ids (global), then
  * after a scan of mark, local[i] = n_prefix + rank(ids[i]) unless ids[i] is
- * one of the dst-prefix nodes (prefix_pos[id] >= 0), which keep their slot. */
+ * one of the dst-prefix nodes (prefix_pos[id] >= 0), which keep their slot.  Negative ids
+ * (the unused tail of a capacity-sized sample buffer) are skipped: no mark, local = -1. */
 int gnnrec_mark_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos, int32_t* mark,
                     void* stream);
 int gnnrec_relabel_ids(const int64_t* ids, int64_t n, const int64_t* prefix_pos,
