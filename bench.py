@@ -147,15 +147,20 @@ def launch_bytes(shard, d, runner, deterministic):
 CSRC = os.path.join(ROOT, "gnn-recsys_amd", "csrc")
 
 
+# the sources of the kernels whose HBM traffic the PMC passes measure (the aggregation
+# launches and what they include) plus the build flags
+PMC_SOURCES = ("spmm.hip", "spmm_project.hip", "gemm.hip", "rowq.hip", "gather.hpp", "rowq.hpp",
+               "common.hpp", "Makefile")
+
+
 def csrc_digest() -> str:
-    """sha256 (16 hex) of the HIP sources and build flags the library is compiled from: ties
-    a committed PMC profile to the kernels that produced it."""
+    """sha256 (16 hex) of the sources and build flags the profiled kernels are compiled
+    from (PMC_SOURCES): ties a committed PMC profile to the kernels that produced it."""
     import hashlib
     h = hashlib.sha256()
-    for f in sorted(os.listdir(CSRC)):
-        if f.endswith((".hip", ".hpp", ".cpp", ".h")) or f == "Makefile":
-            h.update(f.encode())
-            h.update(open(os.path.join(CSRC, f), "rb").read())
+    for f in sorted(PMC_SOURCES):
+        h.update(f.encode())
+        h.update(open(os.path.join(CSRC, f), "rb").read())
     return h.hexdigest()[:16]
 
 
