@@ -81,6 +81,18 @@ def test_meta_kernels_check_shapes():
     with pytest.raises(ValueError, match="unit column stride"):
         T.sddmm_cos(_meta(3, dtype=torch.int64), _meta(3, dtype=torch.int64), _meta(4, 8).t(),
                     _meta(8, 4), _meta(3))
+    # two pre-projected relations into one type: row counts must agree
+    i64, i32 = torch.int64, torch.int32
+    ra = (_meta(6, dtype=i64), _meta(20, dtype=i32), None, _meta(9, 128), 1, None)
+    rb = (_meta(6, dtype=i64), _meta(7, dtype=i32), None, _meta(9, 128), 0, None)
+    W = _meta(128, 128)
+    T.spmm_project2(*ra, *rb, _meta(5, 128), W, W, None, None, 3, 1, None, 0.0, _meta(5, 128))
+    with pytest.raises(ValueError, match="row counts differ"):
+        T.spmm_project2(*ra, _meta(7, dtype=i64), *rb[1:], _meta(5, 128), W, W, None, None, 3, 1,
+                        None, 0.0, _meta(5, 128))
+    with pytest.raises(ValueError, match="out must be"):
+        T.spmm_project2(*ra, *rb, _meta(5, 128), W, W, None, None, 3, 1, None, 0.0,
+                        _meta(4, 128))
 
 
 def test_cpu_tensors_are_refused():
@@ -104,16 +116,18 @@ def _meta_rel(n_src, n_dst, E):
                     n_dst)
 
 
-@pytest.mark.parametrize("d,agg", [(128, "mean"), (64, "mean_nn"), (128, "pool_nn")])
-def test_compile_convlayer_forward_fullgraph(d, agg):
+@pytest.mark.parametrize("d,agg,n_src,deg", [(128, "mean", 50, 30), (64, "mean_nn", 50, 30),
+                                             (128, "pool_nn", 50, 30), (128, "mean", 15, 10)])
+def test_compile_convlayer_forward_fullgraph(d, agg, n_src, deg):
     """torch.compile(fullgraph=True) of the drop-in ConvLayer.forward in eval mode: every
-    launch is a torch.ops.gnnrec op with a meta kernel, nothing breaks the graph."""
+    launch is a torch.ops.gnnrec op with a meta kernel, nothing breaks the graph (the last
+    case: a small source table at 10 edges/row, projected before the reduction)."""
     import torch._dynamo
     from gnnrec import nn as gnn
     torch._dynamo.reset()
     layer = gnn.ConvLayer((d, d), d, 0.0, agg, True).eval().to("meta")
-    g = _meta_rel(50, 40, 40 * 30)
-    x = (_meta(50, d), _meta(40, d))
+    g = _meta_rel(n_src, 40, 40 * deg)
+    x = (_meta(n_src, d), _meta(40, d))
     compiled = torch.compile(layer, fullgraph=True, backend="aot_eager")
     with torch.no_grad():
         z = compiled(g, x)
@@ -129,7 +143,7 @@ def test_compile_convlayer_forward_fullgraph(d, agg):
     with torch.no_grad():
         torch.compile(layer, fullgraph=True, backend=backend)(g, x)
     want = {"spmm_project"} if d == 128 else {"spmm_csr", "gemm"}  # fused at d = 128
-    if agg != "mean":
+    if agg != "mean" or n_src * 2 <= 40:  # fc_preagg on the sources / their pre-projection
         want.add("gemm")  # fc_preagg + ReLU on the source table
     assert want <= ops_seen, ops_seen
 
