@@ -753,6 +753,11 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
 namespace gnnrec {
 namespace {
 
+#ifndef GNNREC_SPP2_WAVES
+#define GNNREC_SPP2_WAVES 16  // waves per (one-per-CU) block: 12 waves at U = 8-10 took 59.5 ms,
+#endif                        // 8 waves at U = 12-16 75 ms (vs 38.2): the wave count, not the
+                              // loads in flight per wave, sets this kernel's rate
+constexpr int kP2Waves = GNNREC_SPP2_WAVES;
 #ifndef GNNREC_SPP2_U
 #define GNNREC_SPP2_U 5  // gather wave-instructions in flight per lane (C5: 5 beats 4 by ≈0.6 ms; 6 and 8 slow down)
 #endif
@@ -768,7 +773,7 @@ struct PreRel {
 };
 
 template <bool WA, bool WB>
-__global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
+__global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_kernel(
     PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
     const float* __restrict__ WaT, const float* __restrict__ WbT,
     const float* __restrict__ bias_a, const float* __restrict__ bias_b, int64_t n_dst,
@@ -777,8 +782,8 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
     unsigned* rq, int rq_ch) {
   __shared__ float Wa[kPD * kPD];
   __shared__ float Wb[kPD * kPD];
-  __shared__ float slots[kPWaves][kPRows][kPD];
-  for (int i = threadIdx.x; i < kPD * kPD / 4; i += kPWaves * 64) {
+  __shared__ float slots[kP2Waves][kPRows][kPD];
+  for (int i = threadIdx.x; i < kPD * kPD / 4; i += kP2Waves * 64) {
     reinterpret_cast<float4*>(Wa)[i] = reinterpret_cast<const float4*>(WaT)[i];
     reinterpret_cast<float4*>(Wb)[i] = reinterpret_cast<const float4*>(WbT)[i];
   }
@@ -791,7 +796,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
   const int j0 = 2 * lane;
   const bool relu = epilogue & GNNREC_EPI_RELU;
   const bool l2 = epilogue & GNNREC_EPI_L2NORM;
-  const int64_t stride = (int64_t)gridDim.x * kPWaves * kPRows;
+  const int64_t stride = (int64_t)gridDim.x * kP2Waves * kPRows;
   const float ba0 = bias_a ? bias_a[j0] : 0.f, ba1 = bias_a ? bias_a[j0 + 1] : 0.f;
   const float bb0 = bias_b ? bias_b[j0] : 0.f, bb1 = bias_b ? bias_b[j0 + 1] : 0.f;
   const float ca0 = ra.bias_ne ? ra.bias_ne[j0] : 0.f, ca1 = ra.bias_ne ? ra.bias_ne[j0 + 1] : 0.f;
@@ -937,7 +942,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project2_kernel(
     rq_finish(rq);
     return;
   }
-  for (int64_t row0 = ((int64_t)blockIdx.x * kPWaves + wave) * kPRows; row0 < n_dst;
+  for (int64_t row0 = ((int64_t)blockIdx.x * kP2Waves + wave) * kPRows; row0 < n_dst;
        row0 += stride)
     step(row0, n_dst);
 }
@@ -973,7 +978,7 @@ extern "C" int gnnrec_spmm_project2_f32(
                      aligned16(W_self_bT) && ldya % 4 == 0 && ldyb % 4 == 0 && ldh % 4 == 0 &&
                      ldo % 2 == 0 && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                  "gnnrec_spmm_project2_f32: Y/H/W need 16-B aligned rows, out 8-B");
-  const int64_t per_block = (int64_t)kPWaves * kPRows;
+  const int64_t per_block = (int64_t)kP2Waves * kPRows;
   int64_t blocks = (n_dst + per_block - 1) / per_block;
   const int64_t cus = device_cus() - cu_reserve();
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
@@ -987,8 +992,8 @@ extern "C" int gnnrec_spmm_project2_f32(
   }();
   hipStream_t s = as_stream(stream);
   int ticket = -1;
-  unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
-  const dim3 grid((unsigned)blocks), block(kPWaves * 64);
+  unsigned* rq = n_dst >= blocks * kP2Waves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
+  const dim3 grid((unsigned)blocks), block(kP2Waves * 64);
   const PreRel a{indptr_a, indices_a, ew_a, Ya, ldya, bias_nonempty_a,
                  reduce_a == GNNREC_REDUCE_MEAN};
   const PreRel b{indptr_b, indices_b, ew_b, Yb, ldyb, bias_nonempty_b,
