@@ -235,6 +235,42 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const T* in, int
   if (blockIdx.x == n_tiles - 1 && threadIdx.x == kScanBlock - 1) out[n] = sums[n_tiles];
 }
 
+// arrays of up to kScan1Tile entries (the sampler's per-seed counts, the radix sort's digit
+// tables of a block CSR): one launch of one 1024-thread block instead of three
+constexpr int kScan1Block = 1024;
+constexpr int kScan1Items = 16;
+constexpr int64_t kScan1Tile = (int64_t)kScan1Block * kScan1Items;
+
+template <typename T>
+__global__ __launch_bounds__(kScan1Block) void scan_one_block_kernel(const T* in, int64_t n,
+                                                                    int64_t* out) {
+  __shared__ int64_t sh[kScan1Block];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)t * kScan1Items;
+  int64_t vals[kScan1Items];
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kScan1Items; ++j) {
+    vals[j] = base + j < n ? (int64_t)in[base + j] : 0;
+    s += vals[j];
+  }
+  sh[t] = s;
+  __syncthreads();  // (in may alias out: every read above precedes the writes below)
+  for (int off = 1; off < kScan1Block; off <<= 1) {
+    const int64_t y = t >= off ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  int64_t run = sh[t] - s;
+#pragma unroll
+  for (int j = 0; j < kScan1Items; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += vals[j];
+  }
+  if (t == kScan1Block - 1) out[n] = run;  // the total
+}
+
 template <typename T>
 int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStream_t s) {
   GNNREC_REQUIRE(n >= 0, "scan: negative n");
@@ -245,6 +281,10 @@ int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStr
       return GNNREC_EHIP;
     }
     return GNNREC_OK;
+  }
+  if (n <= kScan1Tile) {
+    hipLaunchKernelGGL(scan_one_block_kernel<T>, dim3(1), dim3(kScan1Block), 0, s, in, n, out);
+    return check_launch("gnnrec_exclusive_scan");
   }
   GNNREC_REQUIRE(workspace != nullptr, "scan: null workspace");
   const int64_t n_tiles = (n + kScanTile - 1) / kScanTile;

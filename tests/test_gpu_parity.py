@@ -333,11 +333,13 @@ def test_sampler_bit_exact_vs_oracle(fanout, exclude):
 def test_relabel_and_scan_bit_exact():
     from gnnrec import ops
     rng = np.random.default_rng(4)
-    for n in (0, 1, 5, 2047, 2048, 2049, 100_000):
-        x = rng.integers(0, 50, n).astype(np.int64)
-        got = ops.exclusive_scan(_t(x)).cpu().numpy()
-        ref = np.concatenate([[0], np.cumsum(x)])
-        np.testing.assert_array_equal(got, ref)
+    # one-block path up to 16384 entries, three-kernel path above; int64 and int32 inputs
+    for n in (0, 1, 5, 2047, 2048, 2049, 16383, 16384, 16385, 100_000):
+        for dt in (np.int64, np.int32):
+            x = rng.integers(0, 50, n).astype(dt)
+            got = ops.exclusive_scan(_t(x)).cpu().numpy()
+            ref = np.concatenate([[0], np.cumsum(x.astype(np.int64))])
+            np.testing.assert_array_equal(got, ref)
     N = 5000
     prefix = rng.choice(N, 200, replace=False).astype(np.int64)
     lists = [rng.integers(0, N, 3000).astype(np.int64), rng.integers(0, N, 10).astype(np.int64)]
