@@ -203,15 +203,17 @@ def _digest(t):
     return int((v * w).sum()), int((v * (w * w)).sum()), v.numel()
 
 
-def _c4_pass(rank, world, users, items, edges):
+def _c4_pass(rank, world, users, items, edges, split=None):
     """The bench's default pass (deterministic, 8 source tiles, partitioned output) on this
-    rank's shard: (own user range, user digest, own item block range, item digest)."""
+    rank's shard: (own user range, user digest, own item block range, item digest).
+    split: C5's relation split (4 relations; the item->user pair runs as one launch)."""
     from gnnrec import nn as gnn
     from gnnrec.dist import Exchange
     from gnnrec.inference import ShardedFullGraphPass
     from gnnrec.synth import GraphMeta, bipartite_shard, node_features
     dev, d = torch.device("cuda", 0), 128
-    sh = bipartite_shard(users, items, edges, rank, world, dev, segments=8)
+    kw = {} if split is None else {"split": split}
+    sh = bipartite_shard(users, items, edges, rank, world, dev, segments=8, **kw)
     feats = {"user": node_features(users, d, 0, dev, slice(sh.p_lo, sh.p_hi)),
              "item": torch.zeros((sh.padded_rows("item"), d), device=dev)}
     feats["item"][:items] = node_features(items, d, 1, dev)
@@ -219,24 +221,29 @@ def _c4_pass(rank, world, users, items, edges):
     model = gnn.ConvModel(GraphMeta(sh.canonical_etypes, ["item", "user"]), 3,
                           {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
                           "cos", "sum", True).to(dev).eval()
+    runner = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True)
     with torch.no_grad():
-        out = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True).run(
-            feats, replicate_output=False)
+        out = runner.run(feats, replicate_output=False)
+    if split is not None:
+        assert len(runner.pair_fused) == 1, runner.pair_fused
     S = sh.shard_rows["item"]
     lo, hi = rank * S, min((rank + 1) * S, items)
     return (sh.p_lo, sh.p_hi, _digest(out["user"]), lo, hi, _digest(out["item"][: hi - lo]),
             out)
 
 
-def _c4_worker(rank, world, port, q):
+def _c4_worker(rank, world, port, q, split=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank,) + _c4_pass(rank, world, *C4)[:6])
+        q.put((rank,) + _c4_pass(rank, world, *C4, split=split)[:6])
     finally:
         dist.destroy_process_group()
+
+
+C5_SPLIT = (("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2))
 
 
 C4 = (10_000_000, 1_000_000, 500_000_000)
@@ -271,3 +278,29 @@ def test_c4_full_size_pass_bitwise_at_two_ranks():
     for world, rank, ulo, uhi, udig, ilo, ihi, idig in res:
         assert _digest(out["user"][ulo:uhi]) == udig, f"P={world} rank {rank}: user rows differ"
         assert _digest(out["item"][ilo:ihi]) == idig, f"P={world} rank {rank}: item rows differ"
+
+
+def test_c5_full_size_pass_bitwise_at_two_ranks():
+    """The same at C5 (the C4 graph split 80/20 into clicks and buys, four relations): the
+    item->user pair runs as one pre-projected launch on every rank, decided from the global
+    user count, so the two ranks reproduce the single-process bits."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q, port, world = ctx.Queue(), _port(), 2
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q, C5_SPLIT))
+             for r in range(world)]
+    try:
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=120) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=30)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    out = _c4_pass(0, 1, *C4, split=C5_SPLIT)[6]
+    for rank, ulo, uhi, udig, ilo, ihi, idig in res:
+        assert _digest(out["user"][ulo:uhi]) == udig, f"rank {rank}: user rows differ"
+        assert _digest(out["item"][ilo:ihi]) == idig, f"rank {rank}: item rows differ"
