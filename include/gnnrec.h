@@ -19,6 +19,10 @@
  *                                 (DGL gspmm -> _CAPI_DGLKernelSpMM)
  *   - gnnrec_spmm_project_f32  <- the two above fused for d = 128 (update_all +
  *                                 fc_self/fc_neigh + relu + norm in one launch)
+ *   - gnnrec_spmm_project_mfma_f32 / gnnrec_spmm_project2_f32 <- the same for
+ *                                 low-degree CSRs, pre-projected source rows, and
+ *                                 two relations + the HeteroGraphConv aggregate
+ *                                 (src/model.py:384-406) in one launch
  *   - gnnrec_gemm_f32          <- nn.Linear fc_self/fc_neigh/fc_preagg +
  *                                 relu + zero-guarded L2 norm + HeteroGraphConv
  *                                 aggregate, src/model.py:98-102,151,226-235,
