@@ -345,7 +345,7 @@ def main():
             dist.init_process_group(backend)
 
     from gnnrec import nn as gnn
-    from gnnrec.dist import Exchange
+    from gnnrec.dist import AsyncEmulatedExchange, Exchange
     from gnnrec.inference import ShardedFullGraphPass
     from gnnrec.synth import GraphMeta, bipartite_shard, node_features
 
@@ -367,7 +367,11 @@ def main():
     meta = GraphMeta(shard.canonical_etypes, ["item", "user"])
     model = gnn.ConvModel(meta, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
                           args.aggregator, "cos", args.hetero, True).to(dev).eval()
+    # RCCL when the group is nccl; a gloo rehearsal (GNNREC_DIST_BACKEND=gloo) exchanges
+    # through the async emulation, so the pass waits on real work handles as under RCCL
     ex = Exchange()
+    if world > 1 and not ex._rccl:
+        ex = AsyncEmulatedExchange(delay_us=0)
     conc = None
     if args.concurrency != "auto":
         r, q = args.concurrency.split(",")
@@ -509,6 +513,7 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
     torch.cuda.synchronize()
     runner.ex = ex
     comm_ms = rec.replay_ms(dev)
+    per_kind = rec.replay_by_kind(dev)
     null = ShardedFullGraphPass(model, shard, ComputeOnlyExchange(world, ex.rk),
                                 overlap=not args.no_overlap, deterministic=det, concurrency=conc)
     reps = max(2, min(args.steps, 5))
@@ -530,7 +535,31 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
     return {"backend": str(ex.backend), "collective_path": rec.path, "ranks_seen": world,
             "rank_compute_ms": [round(c, 2) for c in compute], "rank_edges": edges,
             "comm_ms": comm_ms, "comm_bytes_per_rank": rec.bytes_sent(),
-            "collectives_per_pass": len(rec.calls), "overlap_frac": overlap}
+            "collectives_per_pass": len(rec.calls), "overlap_frac": overlap,
+            # per collective kind, replayed alone: ms per call, bytes each rank sends per
+            # call, and bus bandwidth = those bytes / time (nccl-tests' busbw: algbw x
+            # (P-1)/P) — against ~153 GB/s per xGMI link, 7 links per GPU
+            "comm_by_kind": {k: {"ms": round(v["ms"], 3), "calls_per_pass": v["calls"],
+                                 "bytes_sent": v["bytes"],
+                                 "busbw_GBs": None if v["busbw_GBs"] is None else round(v["busbw_GBs"], 1)}
+                             for k, v in per_kind.items()},
+            "rccl": rccl_environment(ex)}
+
+
+def rccl_environment(ex):
+    """What decides RCCL's algorithm for this run: its version and every NCCL_* / RCCL_* /
+    HSA_* variable set in the environment (none set = RCCL's defaults)."""
+    env = {k: v for k, v in sorted(os.environ.items())
+           if k.startswith(("NCCL_", "RCCL_", "HSA_ENABLE_IPC", "HSA_FORCE_FINE"))}
+    ver = None
+    if ex._rccl:
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as exc:  # a diagnostic never fails the bench
+            ver = f"unknown ({exc!r})"
+    return {"version": ver, "env": env, "defaults": not any(
+        k.startswith(("NCCL_", "RCCL_")) for k in env)}
 
 
 if __name__ == "__main__":

@@ -66,8 +66,14 @@ int cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
 
 unsigned* rowq_slot(hipStream_t stream, int* ticket) {
   *ticket = -1;
-  (void)stream;
   if (!g_dynamic.load(std::memory_order_relaxed)) return nullptr;
+  // a launch captured into a hipGraph would replay with its slot baked in and no
+  // completion check, so an eager launch could take the same slot while the replay runs
+  // (two grids on one set of heads skip or repeat rows): captured launches get the static
+  // schedule
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
+    return nullptr;
   const int dev = current_device();
   unsigned* ring = g_ring[dev].load(std::memory_order_acquire);
   if (ring == nullptr) {

@@ -40,11 +40,33 @@ void* stream_of(const Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.device().index()).stream();
 }
 
+// Every device operand of one op must sit on ONE device: the guard and the stream come from
+// one of them, and a pointer into another GPU's memory would fault in the kernel instead of
+// raising.  Each op opens a OneDevice scope; dev()/same_dev() compare every operand with
+// the first one seen in it.
+thread_local bool g_op_dev_set = false;
+thread_local c10::Device g_op_device{c10::DeviceType::CPU};
+struct OneDevice {
+  OneDevice() { g_op_dev_set = false; }
+  ~OneDevice() { g_op_dev_set = false; }
+};
+void same_dev(const Tensor& t, const char* name) {
+  if (!t.defined() || !t.is_cuda()) return;
+  if (!g_op_dev_set) {
+    g_op_device = t.device();
+    g_op_dev_set = true;
+    return;
+  }
+  TORCH_CHECK_VALUE(t.device() == g_op_device, name, " is on ", t.device(),
+                    " but the op's other operands are on ", g_op_device);
+}
+
 // device operand (or meta/fake during tracing) of the given dtype
 void dev(const Tensor& t, const char* name, c10::ScalarType dt) {
   TORCH_CHECK_VALUE(t.is_cuda() || t.is_meta(), name,
                     " must be a HIP device tensor (gnnrec has no CPU path), got ", t.device());
   TORCH_CHECK_VALUE(t.scalar_type() == dt, name, " must be ", dt, ", got ", t.scalar_type());
+  same_dev(t, name);
 }
 void dev(const optional<Tensor>& t, const char* name, c10::ScalarType dt) {
   if (t.has_value() && t->defined()) dev(*t, name, dt);
@@ -69,6 +91,7 @@ bool meta(const Tensor& t) { return t.is_meta(); }
 // ---------------------------------------------------------------- a1 aggregation
 void spmm_csr(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
               const Tensor& X, int64_t reduce, int64_t flags, Tensor& out) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(X, "X", at::kFloat);
@@ -89,6 +112,7 @@ void spmm_csr_split(const Tensor& indptr, const Tensor& indices, const optional<
                     const Tensor& X, int64_t reduce, int64_t flags, int64_t split,
                     const Tensor& heavy, const Tensor& chunk_ptr, const Tensor& chunk_row,
                     int64_t n_chunks, Tensor& out, Tensor& ws) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(X, "X", at::kFloat);
@@ -114,6 +138,7 @@ void spmm_csr_split(const Tensor& indptr, const Tensor& indices, const optional<
 void spmm_csr2(const Tensor& indptr_a, const Tensor& indices_a, const optional<Tensor>& ew_a,
                const Tensor& indptr_b, const Tensor& indices_b, const optional<Tensor>& ew_b,
                const Tensor& X, int64_t reduce, int64_t flags, Tensor& out_a, Tensor& out_b) {
+  const OneDevice one_device_;
   dev(indptr_a, "indptr_a", at::kLong);
   dev(indices_a, "indices_a", at::kInt);
   dev(ew_a, "ew_a", at::kFloat);
@@ -139,6 +164,7 @@ void spmm_csr2(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
 }
 
 void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor& plan) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(plan, "plan", at::kLong);
   if (meta(indptr)) return;
@@ -151,6 +177,7 @@ void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor&
 void spmm_csr_planned(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
                       const Tensor& X, int64_t reduce, int64_t flags, int64_t split,
                       const Tensor& plan, int64_t cap_h, int64_t cap_c, Tensor& out, Tensor& ws) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(X, "X", at::kFloat);
@@ -174,6 +201,7 @@ void spmm_csr_planned(const Tensor& indptr, const Tensor& indices, const optiona
 void spmm_backward(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
                    const Tensor& grad_out, const optional<Tensor>& X,
                    const optional<Tensor>& out, int64_t reduce, Tensor& grad_X) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(ew, "edge_weight", at::kFloat);
@@ -198,6 +226,7 @@ void gemm(const Tensor& A1, const Tensor& W1, const optional<Tensor>& A2,
           const optional<Tensor>& bias, const optional<Tensor>& bias_nonempty, int64_t epilogue,
           int64_t accum, double out_div, const optional<Tensor>& attn_vec,
           const optional<Tensor>& attn_state, Tensor& out, const optional<Tensor>& row_norm) {
+  const OneDevice one_device_;
   dev(A1, "A1", at::kFloat);
   dev(W1, "W1", at::kFloat);
   dev(A2, "A2", at::kFloat);
@@ -235,6 +264,7 @@ void gemm(const Tensor& A1, const Tensor& W1, const optional<Tensor>& A2,
 void row_epilogue(const Tensor& z, int64_t l2norm, int64_t accum, double out_div,
                   const optional<Tensor>& attn_vec, const optional<Tensor>& attn_state,
                   Tensor& out) {
+  const OneDevice one_device_;
   dev(z, "z", at::kFloat);
   dev(attn_vec, "attn_vec", at::kFloat);
   dev(attn_state, "attn_state", at::kFloat);
@@ -256,6 +286,7 @@ void spmm_project(const Tensor& indptr, const Tensor& indices, const optional<Te
                   const optional<Tensor>& bias_nonempty, int64_t reduce, int64_t epilogue,
                   int64_t accum, double out_div, const optional<Tensor>& attn_vec,
                   const optional<Tensor>& attn_state, bool mfma, Tensor& out) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(ew, "edge_weight", at::kFloat);
@@ -295,6 +326,7 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
                    const optional<Tensor>& bias_a, const optional<Tensor>& bias_b,
                    int64_t epilogue, int64_t combine, const optional<Tensor>& attn_vec,
                    double out_div, Tensor& out) {
+  const OneDevice one_device_;
   dev(indptr_a, "indptr_a", at::kLong);
   dev(indices_a, "indices_a", at::kInt);
   dev(ew_a, "ew_a", at::kFloat);
@@ -337,6 +369,7 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
 // ---------------------------------------------------------------- a7 / a8 heads
 void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                Tensor& out) {
+  const OneDevice one_device_;
   dev(src, "src", at::kLong);
   dev(dst, "dst", at::kLong);
   dev(Hs, "Hs", at::kFloat);
@@ -357,6 +390,7 @@ void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Ten
 void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                         const Tensor& grad, const optional<Tensor>& gHs,
                         const optional<Tensor>& gHd, Tensor& ws) {
+  const OneDevice one_device_;
   dev(src, "src", at::kLong);
   dev(dst, "dst", at::kLong);
   dev(Hs, "Hs", at::kFloat);
@@ -380,6 +414,7 @@ void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, 
 void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tensor& Q,
               const Tensor& W2, const Tensor& b2, const Tensor& w3, const Tensor& b3,
               Tensor& out) {
+  const OneDevice one_device_;
   dev(src, "src", at::kLong);
   dev(dst, "dst", at::kLong);
   for (auto* t : {&P, &Q, &W2, &b2, &w3, &b3}) dev(*t, "edge_mlp operand", at::kFloat);
@@ -401,6 +436,7 @@ void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tenso
 // ---------------------------------------------------------------- a9 sampler / relabel
 void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tensor>& excluded,
                   const Tensor& seeds, int64_t fanout, int64_t seed_key, Tensor& counts) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(eids, "eids", at::kLong);
   dev(excluded, "excluded", at::kByte);
@@ -418,6 +454,7 @@ void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tenso
 void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids,
                  const optional<Tensor>& excluded, const Tensor& seeds, int64_t fanout,
                  int64_t seed_key, const Tensor& out_indptr, Tensor& out_src, Tensor& out_eid) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(eids, "eids", at::kLong);
@@ -437,6 +474,7 @@ void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids
 }
 
 void exclusive_scan(const Tensor& x, Tensor& out, Tensor& ws) {
+  const OneDevice one_device_;
   dev(out, "out", at::kLong);
   TORCH_CHECK_VALUE(x.is_cuda() || x.is_meta(), "x must be a HIP device tensor");
   TORCH_CHECK_VALUE(x.scalar_type() == at::kLong || x.scalar_type() == at::kInt,
@@ -456,6 +494,7 @@ void exclusive_scan(const Tensor& x, Tensor& out, Tensor& ws) {
 }
 
 void mark_ids(const Tensor& ids, const Tensor& prefix_pos, Tensor& mark) {
+  const OneDevice one_device_;
   dev(ids, "ids", at::kLong);
   dev(prefix_pos, "prefix_pos", at::kLong);
   dev(mark, "mark", at::kInt);
@@ -468,6 +507,7 @@ void mark_ids(const Tensor& ids, const Tensor& prefix_pos, Tensor& mark) {
 
 void relabel_ids(const Tensor& ids, const Tensor& prefix_pos, const Tensor& rank, int64_t n_prefix,
                  Tensor& local) {
+  const OneDevice one_device_;
   dev(ids, "ids", at::kLong);
   dev(prefix_pos, "prefix_pos", at::kLong);
   dev(rank, "rank", at::kLong);
@@ -481,6 +521,7 @@ void relabel_ids(const Tensor& ids, const Tensor& prefix_pos, const Tensor& rank
 }
 
 void compact_marked(const Tensor& mark, const Tensor& rank, Tensor& out_ids) {
+  const OneDevice one_device_;
   dev(mark, "mark", at::kInt);
   dev(rank, "rank", at::kLong);
   dev(out_ids, "out_ids", at::kLong);
@@ -492,6 +533,7 @@ void compact_marked(const Tensor& mark, const Tensor& rank, Tensor& out_ids) {
 }
 
 void set_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
+  const OneDevice one_device_;
   dev(prefix, "prefix", at::kLong);
   dev(prefix_pos, "prefix_pos", at::kLong);
   if (meta(prefix)) return;
@@ -502,6 +544,7 @@ void set_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
 }
 
 void clear_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
+  const OneDevice one_device_;
   dev(prefix, "prefix", at::kLong);
   dev(prefix_pos, "prefix_pos", at::kLong);
   if (meta(prefix)) return;
@@ -514,6 +557,7 @@ void clear_prefix_pos(const Tensor& prefix, Tensor& prefix_pos) {
 // ---------------------------------------------------------------- f1 top-k
 void topk_rows(const Tensor& scores, int64_t k, const optional<Tensor>& exclude_indptr,
                const optional<Tensor>& exclude_indices, Tensor& out_vals, Tensor& out_idx) {
+  const OneDevice one_device_;
   dev(scores, "scores", at::kFloat);
   dev(exclude_indptr, "exclude_indptr", at::kLong);
   dev(exclude_indices, "exclude_indices", at::kLong);
@@ -534,6 +578,7 @@ void topk_rows(const Tensor& scores, int64_t k, const optional<Tensor>& exclude_
 // ---------------------------------------------------------------- f2 training
 void gemm_tn(const Tensor& A, const Tensor& B, const optional<Tensor>& colsum, bool accumulate,
              Tensor& out, Tensor& ws) {
+  const OneDevice one_device_;
   dev(A, "A", at::kFloat);
   dev(B, "B", at::kFloat);
   dev(colsum, "colsum", at::kFloat);
@@ -550,6 +595,7 @@ void gemm_tn(const Tensor& A, const Tensor& B, const optional<Tensor>& colsum, b
 }
 
 void act_backward(const Tensor& u, const Tensor& gz, int64_t flags, Tensor& out) {
+  const OneDevice one_device_;
   dev(u, "u", at::kFloat);
   dev(gz, "gz", at::kFloat);
   dev(out, "out", at::kFloat);
@@ -565,6 +611,7 @@ void act_backward(const Tensor& u, const Tensor& gz, int64_t flags, Tensor& out)
 
 void act_backward_normed(const Tensor& z, const Tensor& row_norm, const Tensor& gz, bool relu,
                          Tensor& out) {
+  const OneDevice one_device_;
   dev(z, "z", at::kFloat);
   dev(row_norm, "row_norm", at::kFloat);
   dev(gz, "gz", at::kFloat);
@@ -584,6 +631,7 @@ void act_backward_normed(const Tensor& z, const Tensor& row_norm, const Tensor& 
 void csr_transpose(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
                    int64_t n_src, int64_t n_edges, bool mean, Tensor& ws, Tensor& indptr_t,
                    Tensor& indices_t, const optional<Tensor>& ew_t) {
+  const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(ew, "edge_weight", at::kFloat);
@@ -603,6 +651,7 @@ void csr_transpose(const Tensor& indptr, const Tensor& indices, const optional<T
 }
 
 void csr_from_keys(const Tensor& keys, int64_t n_rows, Tensor& ws, Tensor& indptr, Tensor& perm) {
+  const OneDevice one_device_;
   dev(keys, "keys", at::kInt);
   dev(indptr, "indptr", at::kLong);
   dev(perm, "perm", at::kInt);
@@ -619,6 +668,7 @@ void csr_from_keys(const Tensor& keys, int64_t n_rows, Tensor& ws, Tensor& indpt
 // ---------------------------------------------------------------- f3 graph construction
 void csr_build(const Tensor& src, const Tensor& dst, int64_t n_dst, Tensor& ws, Tensor& indptr,
                Tensor& indices, Tensor& eids) {
+  const OneDevice one_device_;
   dev(src, "src", at::kLong);
   dev(dst, "dst", at::kLong);
   dev(indptr, "indptr", at::kLong);
@@ -638,6 +688,7 @@ void csr_build(const Tensor& src, const Tensor& dst, int64_t n_dst, Tensor& ws, 
 
 // ---------------------------------------------------------------- sharded-pass helpers
 void add_(Tensor& a, const Tensor& b) {
+  const OneDevice one_device_;
   dev(a, "a", at::kFloat);
   dev(b, "b", at::kFloat);
   TORCH_CHECK_VALUE(a.sizes() == b.sizes() && a.is_contiguous() && b.is_contiguous(),
@@ -649,6 +700,7 @@ void add_(Tensor& a, const Tensor& b) {
 }
 
 void tree_sum_(Tensor& a, at::TensorList rest) {
+  const OneDevice one_device_;
   dev(a, "part", at::kFloat);
   const int n = (int)rest.size() + 1;
   TORCH_CHECK_VALUE(n == 2 || n == 4 || n == 8, "tree_sum_: 2, 4 or 8 tables");
@@ -670,6 +722,7 @@ void tree_sum_(Tensor& a, at::TensorList rest) {
 void lstm_step(const Tensor& P, const Tensor& indptr, const Tensor& indices, const Tensor& order,
                int64_t t, int64_t n_act, const Tensor& h_in, Tensor& h_out, Tensor& c,
                const Tensor& W_hhT, Tensor& out) {
+  const OneDevice one_device_;
   dev(P, "P", at::kFloat);
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
@@ -693,8 +746,11 @@ void lstm_step(const Tensor& P, const Tensor& indptr, const Tensor& indices, con
 
 // ---------------------------------------------------------------- a10 row gather
 void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
+  const OneDevice one_device_;
   dev(idx, "idx", at::kLong);
   TORCH_CHECK_VALUE(src.is_cuda() || src.is_meta(), "src: expected a device tensor (there is no CPU path)");
+  same_dev(src, "src");
+  same_dev(out, "out");
   TORCH_CHECK_VALUE(src.dim() >= 1 && out.dim() == src.dim() && out.scalar_type() == src.scalar_type(),
                     "gather_rows: out must match src's dtype and rank");
   TORCH_CHECK_VALUE(idx.is_contiguous() && out.size(0) == idx.numel() && out.is_contiguous(),
@@ -704,6 +760,14 @@ void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
   for (int64_t k = 1; k < src.dim(); ++k) {
     TORCH_CHECK_VALUE(out.size(k) == src.size(k), "gather_rows: row shapes differ");
     row_elems *= src.size(k);
+  }
+  // rows are copied as flat byte runs: within a row the elements must be contiguous
+  int64_t inner = 1;
+  for (int64_t k = src.dim() - 1; k >= 1; --k) {
+    TORCH_CHECK_VALUE(src.size(k) <= 1 || src.stride(k) == inner,
+                      "gather_rows: src rows must be contiguous (stride ", src.stride(k),
+                      " in dim ", k, ")");
+    inner *= src.size(k);
   }
   const int64_t row_bytes = es * row_elems;
   if (meta(src)) return;
@@ -717,6 +781,7 @@ void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
 void margin_loss(const Tensor& pos, const Tensor& neg, int64_t K, double delta,
                  const optional<Tensor>& mask, const optional<Tensor>& recency, Tensor& g_pos,
                  Tensor& g_neg, Tensor& partial) {
+  const OneDevice one_device_;
   dev(pos, "pos_score", at::kFloat);
   dev(neg, "neg_score", at::kFloat);
   dev(mask, "negative_mask", at::kFloat);
@@ -741,6 +806,7 @@ void margin_loss(const Tensor& pos, const Tensor& neg, int64_t K, double delta,
 }
 
 void sum_scaled(const Tensor& x, double scale, Tensor& out) {
+  const OneDevice one_device_;
   dev(x, "x", at::kFloat);
   dev(out, "out", at::kFloat);
   if (meta(x)) return;
@@ -752,6 +818,7 @@ void sum_scaled(const Tensor& x, double scale, Tensor& out) {
 // ---------------------------------------------------------------- synthetic generator
 void synth_edges(int64_t seed, int64_t e0, int64_t n_u, int64_t n_i,
                  const optional<Tensor>& zipf_cdf, Tensor& u, Tensor& i) {
+  const OneDevice one_device_;
   dev(zipf_cdf, "zipf_cdf", at::kDouble);
   dev(u, "u", at::kInt);
   dev(i, "i", at::kInt);
@@ -764,6 +831,7 @@ void synth_edges(int64_t seed, int64_t e0, int64_t n_u, int64_t n_i,
 }
 
 void hold_cus(int64_t blocks, int64_t threads, int64_t lds_bytes, int64_t usec, Tensor& sink) {
+  const OneDevice one_device_;
   dev(sink, "sink", at::kFloat);
   TORCH_CHECK_VALUE(sink.numel() >= threads, "sink must hold >= threads floats");
   if (meta(sink)) return;
@@ -787,6 +855,7 @@ void hold_cus(int64_t blocks, int64_t threads, int64_t lds_bytes, int64_t usec, 
 //   exit).  Returns per relation (out indptr, local src int32, eids), per type the src
 //   node ids (prefix first), and the edge counts.
 Tensor exclusive_scan_new(const Tensor& x) {
+  const OneDevice one_device_;
   const int64_t n = x.numel();
   Tensor out = at::empty({n + 1}, x.options().dtype(at::kLong));
   Tensor ws = at::empty({std::max<int64_t>(1, (gnnrec_scan_workspace_bytes(n) + 7) / 8)},
@@ -801,6 +870,7 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
              const c10::List<optional<Tensor>>& masks, at::IntArrayRef src_type,
              at::IntArrayRef dst_type, at::IntArrayRef fanouts, at::IntArrayRef keys,
              at::TensorList seeds, at::TensorList prefix_pos, at::TensorList marks) {
+  const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = seeds.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && masks.size() == R &&
                         src_type.size() == R && dst_type.size() == R && fanouts.size() == R &&
@@ -932,32 +1002,40 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
 // ---------------------------------------------------------------- host-only queries
 int64_t version() { return gnnrec_version(); }
 void set_concurrency(int64_t reserve_cus, bool dynamic) {
+  const OneDevice one_device_;
   ck(gnnrec_set_concurrency((int)reserve_cus, (int)dynamic), "gnnrec_set_concurrency");
 }
 std::tuple<int64_t, int64_t> get_concurrency() {
+  const OneDevice one_device_;
   int r = 0, d = 0;
   ck(gnnrec_get_concurrency(&r, &d), "gnnrec_get_concurrency");
   return {r, d};
 }
 std::tuple<int64_t, int64_t> rowq_stats() {
+  const OneDevice one_device_;
   int64_t q = 0, b = 0;
   ck(gnnrec_rowq_stats(&q, &b), "gnnrec_rowq_stats");
   return {q, b};
 }
 int64_t scan_workspace_bytes(int64_t n) { return gnnrec_scan_workspace_bytes(n); }
 int64_t gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t N) {
+  const OneDevice one_device_;
   return gnnrec_gemm_tn_workspace_bytes(K, M, N);
 }
 int64_t csr_transpose_workspace_bytes(int64_t E, int64_t n_src) {
+  const OneDevice one_device_;
   return (int64_t)gnnrec_csr_transpose_workspace_bytes(E, n_src);
 }
 int64_t csr_from_keys_workspace_bytes(int64_t E, int64_t n_rows) {
+  const OneDevice one_device_;
   return (int64_t)gnnrec_csr_from_keys_workspace_bytes(E, n_rows);
 }
 int64_t csr_build_workspace_bytes(int64_t E, int64_t n_dst) {
+  const OneDevice one_device_;
   return (int64_t)gnnrec_csr_build_workspace_bytes(E, n_dst);
 }
 int64_t sddmm_cos_backward_workspace_bytes(int64_t E, int64_t n_src, int64_t n_dst, int64_t d) {
+  const OneDevice one_device_;
   return (int64_t)gnnrec_sddmm_cos_backward_workspace_bytes(E, n_src, n_dst, d);
 }
 int64_t margin_loss_blocks(int64_t n_pos) { return gnnrec_margin_loss_blocks(n_pos); }

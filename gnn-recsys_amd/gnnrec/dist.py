@@ -150,6 +150,175 @@ class Exchange:
         return float(t.item())
 
 
+class _StreamWork:
+    """The work handle RCCL returns, restated for the emulation: the collective completes
+    on its own stream, and wait() makes the CURRENT stream wait for that completion (the
+    host blocks only until the transport thread has queued the copy-out, as a torch RCCL
+    work's wait() blocks only until the collective is enqueued)."""
+
+    def __init__(self, fut, device):
+        self._fut, self._dev = fut, device
+
+    def wait(self, timeout=None):
+        ev = self._fut.result()
+        torch.cuda.current_stream(self._dev).wait_event(ev)
+        return True
+
+    def is_completed(self) -> bool:
+        return self._fut.done() and self._fut.result().query()
+
+
+class AsyncEmulatedExchange(Exchange):
+    """The RCCL exchange's asynchrony without RCCL (gloo transport): what a one-GPU box and
+    the CPU tests can run of the multi-GPU pass's ordering (the pool gives one GPU per job,
+    so RCCL itself only runs in the driver's 8-GPU bench).
+
+    Device tensors: every collective is issued like an async RCCL one —
+      * a copy-in stream waits for the issuing stream, runs a delay kernel holding
+        `hold_blocks` CUs for `delay_us` µs (gnnrec_hold_cus: a collective kernel's
+        residency and latency), then copies the input to pinned host memory — so the input
+        is read LATE, and a producer that overwrites it before waiting on the work races;
+      * one transport thread (FIFO: the same collective order on every rank) runs the gloo
+        collective on the host copies, then queues on a copy-out stream another delay and
+        the copy of the result into the device output, and records the completion event;
+      * the work's wait() makes the current stream wait for that event — so a reader that
+        skips the wait reads the output before it arrives.
+    CPU tensors: gloo's own async_op works (a transport thread per group).
+
+    Every collective returns a work (never None): `works_issued` counts them and
+    `sync_calls` counts the collectives asked for synchronously (async_op=False)."""
+
+    def __init__(self, group=None, delay_us: int = 500, hold_blocks: int = 16):
+        super().__init__(group)
+        if self._rccl:
+            raise ValueError("AsyncEmulatedExchange emulates RCCL on a gloo group; this group "
+                             "is RCCL already: use Exchange")
+        self.path = "emulated-async"
+        self.delay_us, self.hold_blocks = int(delay_us), int(hold_blocks)
+        self.works_issued = 0
+        self.sync_calls = 0
+        self._streams = None
+        self._pool = None
+        # the transport thread's collectives go through their own gloo group, so they never
+        # interleave with collectives the main thread issues on the default one
+        self._tgroup = dist.new_group(backend="gloo") if self.ws > 1 else None
+
+    def _fast(self, t):
+        return False
+
+    # ---- device tensors: copy-in (main thread) -> gloo (transport thread) -> copy-out ----
+    def _dev_setup(self, dev):
+        if self._streams is None:
+            import concurrent.futures
+            self._dev = dev
+            self._streams = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+            self._pool = concurrent.futures.ThreadPoolExecutor(
+                max_workers=1, thread_name_prefix="gnnrec-exchange",
+                initializer=torch.cuda.set_device, initargs=(dev,))
+
+    def _delay(self, stream):
+        if self.delay_us > 0:
+            from . import ops
+            ops.hold_cus(self.hold_blocks, self.delay_us, stream=stream)
+
+    def _issue(self, src: torch.Tensor, out: torch.Tensor, transport, async_op: bool):
+        """src (device) -> transport(h_in, h_out) on host copies -> out (device)."""
+        dev = src.device
+        self._dev_setup(dev)
+        s_in, s_out = self._streams
+        cur = torch.cuda.current_stream(dev)
+        s_in.wait_stream(cur)
+        with torch.cuda.stream(s_in):
+            self._delay(s_in)
+            h_in = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            h_in.copy_(src, non_blocking=True)
+            ev_in = torch.cuda.Event()
+            ev_in.record(s_in)
+        src.record_stream(s_in)
+        out.record_stream(s_out)
+        h_out = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+
+        def job():
+            ev_in.synchronize()
+            transport(h_in, h_out)
+            with torch.cuda.stream(s_out):
+                self._delay(s_out)
+                out.copy_(h_out, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s_out)
+            return ev
+
+        work = _StreamWork(self._pool.submit(job), dev)
+        self.works_issued += 1
+        if not async_op:
+            self.sync_calls += 1
+            work.wait()
+            return None
+        return work
+
+    def reduce_scatter_rows(self, full, op, async_op=False):
+        if self.ws == 1:
+            return full, None
+        S = full.shape[0] // self.ws
+        rop = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+        out = torch.empty((S,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+        if full.is_cuda:
+            def transport(h_in, h_out):
+                dist.reduce_scatter_tensor(h_out, h_in, op=rop, group=self._tgroup)
+            return out, self._issue(full, out, transport, async_op)
+        work = dist.reduce_scatter_tensor(out, full.contiguous(), op=rop, group=self._tgroup,
+                                          async_op=True)
+        return out, self._cpu(work, async_op)
+
+    def all_gather_rows(self, own, out, async_op=False):
+        if self.ws == 1:
+            return super().all_gather_rows(own, out, async_op)
+        own = own.contiguous()
+        if own.is_cuda:
+            def transport(h_in, h_out):
+                dist.all_gather_into_tensor(h_out, h_in, group=self._tgroup)
+            return out, self._issue(own, out, transport, async_op)
+        work = dist.all_gather_into_tensor(out, own, group=self._tgroup, async_op=True)
+        return out, self._cpu(work, async_op)
+
+    def all_to_all_rows(self, full, async_op=False):
+        S = full.shape[0] // self.ws
+        shape = (self.ws, S) + tuple(full.shape[1:])
+        if self.ws == 1:
+            return full.view(shape), None
+        full = full.contiguous()
+        out = torch.empty_like(full)
+        if full.is_cuda:
+            def transport(h_in, h_out):
+                dist.all_to_all_single(h_out, h_in, group=self._tgroup)
+            return out.view(shape), self._issue(full, out, transport, async_op)
+        work = dist.all_to_all_single(out, full, group=self._tgroup, async_op=True)
+        return out.view(shape), self._cpu(work, async_op)
+
+    def _cpu(self, work, async_op):
+        self.works_issued += 1
+        if not async_op:
+            self.sync_calls += 1
+            work.wait()
+            return None
+        return work
+
+    def all_reduce_(self, t, op="sum"):
+        self.drain()
+        return super().all_reduce_(t, op)
+
+    def drain(self):
+        """Block until every issued device collective has queued its copy-out."""
+        if self._pool is not None:
+            self._pool.submit(lambda: None).result()
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+            self._streams = None
+
+
 class ComputeOnlyExchange:
     """An Exchange of world size P that moves nothing: each collective returns this rank's
     own data in the right shape.  Runs a rank's share of the pass with the same kernels,
@@ -244,6 +413,25 @@ class RecordingExchange:
                 else:
                     self.inner.all_gather_rows(a, b)
 
+        return self._timed(once, device, reps)
+
+    def replay_by_kind(self, device, reps: int = 3) -> dict:
+        """Per collective kind, that kind's calls of one pass replayed alone:
+        {kind: {'ms': per call, 'calls': per pass, 'bytes': sent per call, 'busbw_GBs'}}."""
+        if self.ws == 1 or not self.calls:
+            return {}
+        out = {}
+        for kind in sorted({c[0] for c in self.calls}):
+            calls = [c for c in self.calls if c[0] == kind]
+            sub = RecordingExchange(self.inner)
+            sub.calls = calls
+            ms = sub.replay_ms(device, reps) / len(calls)
+            sent = sum(c[4] for c in calls) / len(calls)
+            out[kind] = {"ms": ms, "calls": len(calls), "bytes": int(sent),
+                         "busbw_GBs": sent / (ms * 1e-3) / 1e9 if ms > 0 else None}
+        return out
+
+    def _timed(self, once, device, reps):
         import time
         once()
         if device.type == "cuda":

@@ -340,6 +340,7 @@ class ShardedFullGraphPass:
                            True)
         self.concurrency = concurrency
         self.timers = None  # optional callable(tag) -> context manager (bench)
+        self.side_delay_us = 0  # tests: a delay kernel ahead of every side-stream task
         self.capture = None  # optional list: every layer's output tables are appended (tests)
         self.fused = set()  # relations whose aggregation ran with the projection fused
         self.pair_fused = set()  # (ce_a, ce_b) run as one pre-projected two-relation launch
@@ -372,13 +373,38 @@ class ShardedFullGraphPass:
         return self._layer_idx % 2 if getattr(self, '_owned_side', False) else 0
 
     def _get(self, h, nt):
-        w = self._pending.pop(id(h[nt]), None)
+        """h[nt], ready for reading on the CURRENT stream.  A table is produced either by a
+        collective (its work handle in _pending) or on the side stream (its event in
+        _ready), and may be read on both streams — at one rank the replicated table is read
+        by the side stream's tree + GEMMs and by main's item->user launch — so readiness is
+        never consumed by the first reader: a waited work becomes an event recorded on the
+        stream that waited, kept in _ready for every later reader (until the layer that
+        reads the table is done, _prune_ready)."""
+        t = h[nt]
+        key = id(t)
+        cur = torch.cuda.current_stream(self.shard.device) if t.is_cuda else None
+        ev = self._ready.get(key)
+        if ev is not None and cur is not None:
+            cur.wait_event(ev)
+        w = self._pending.pop(key, None)
         if w is not None:
             w.wait()
-        ev = self._ready.pop(id(h[nt]), None)
-        if ev is not None:
-            torch.cuda.current_stream(self.shard.device).wait_event(ev)
-        return h[nt]
+            if cur is not None:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                self._ready[key] = ev
+        return t
+
+    def _prune_ready(self, h):
+        """Drop readiness of tables no longer in h (a freed table's id can be reused)."""
+        live = {id(t) for t in h.values()}
+        self._ready = {k: v for k, v in self._ready.items() if k in live}
+
+    def _side_delay(self):
+        """Test hook (side_delay_us): hold the side stream before its work, so a reader
+        that skips a wait on it reads the table before it is written."""
+        if self.side_delay_us and self.side is not None:
+            self.ops.hold_cus(8, self.side_delay_us, stream=self.side)
 
     def _time(self, tag):
         import contextlib
@@ -394,6 +420,7 @@ class ShardedFullGraphPass:
         for t in tensors:  # keep the allocator from recycling them under the side stream
             t.record_stream(self.side)
         with torch.cuda.stream(self.side):
+            self._side_delay()
             fn()
             ev = torch.cuda.Event()
             ev.record(self.side)
@@ -448,6 +475,7 @@ class ShardedFullGraphPass:
             self._layer_idx = i
             self._last = i == len(m.layers) - 1
             h = self._layer(layer, h)
+            self._prune_ready(h)
             if self.capture is not None:
                 for nt in list(h):
                     self._get(h, nt)
@@ -796,12 +824,15 @@ class ShardedFullGraphPass:
             plan.append((mod, ce, rs, preagg, weighted, reduce))
         if bool(plan[0][0].norm) != bool(plan[1][0].norm):
             return False
-        self_rows = self._get(h, T)
-        msgs = [self._message(mod, ce, h, preagg) for mod, ce, _, preagg, _, _ in plan]
-        for (mod, ce, rs, _, _, _), msg in zip(plan, msgs):
-            if not O.can_spmm_project(rs.indptr, msg, self_rows, mod.fc_self.weight,
+        # eligibility from the tables' shapes and layouts before anything is launched or
+        # waited for (a message is the source table itself, or fc_preagg's fresh output of
+        # the same shape): a refused pair costs no GEMM and no main-stream wait
+        for mod, ce, rs, _, _, _ in plan:
+            if not O.can_spmm_project(rs.indptr, h[ce[0]], h[T], mod.fc_self.weight,
                                       mod.fc_neigh.weight):
                 return False
+        self_rows = self._get(h, T)
+        msgs = [self._message(mod, ce, h, preagg) for mod, ce, _, preagg, _, _ in plan]
         rels, Wself, biases = [], [], []
         for (mod, ce, rs, _, weighted, reduce), msg in zip(plan, msgs):
             Ws, Wn, bias, bias_ne = self._folded(mod, ce)
@@ -899,6 +930,7 @@ class ShardedFullGraphPass:
         self.side.wait_stream(main)
         produced = {}
         with torch.cuda.stream(self.side):
+            self._side_delay()
             self._owned(hconv, h, active, partials, produced)
             ev = torch.cuda.Event()
             ev.record(self.side)

@@ -394,11 +394,19 @@ class EdgeDataLoader:
         if exclude not in (None, 'reverse_types', 'self'):
             raise NotImplementedError(f"exclude={exclude!r}")
         # the reference passes the same four-type map for every graph (src/sampling.py:180-181);
-        # pairs naming a type this graph lacks (a clicks-only graph) cannot occur in a batch
+        # a pair naming two types this graph lacks (clicks / clicked-by on a buys-only graph)
+        # cannot occur in a batch and is dropped.  A pair with ONE side known is a typo that
+        # would silently switch reverse-edge exclusion off for the known relation (its
+        # reverse edges would leak into the sampled blocks): that raises
         names = {ce[1] for ce in self.g.canonical_etypes} | set(self.g.canonical_etypes)
-        self.reverse_etypes = {self.g.to_canonical_etype(k): self.g.to_canonical_etype(v)
-                               for k, v in (reverse_etypes or {}).items()
-                               if k in names and v in names}
+        self.reverse_etypes = {}
+        for k, v in (reverse_etypes or {}).items():
+            if (k in names) != (v in names):
+                bad = v if k in names else k
+                raise KeyError(f"reverse_etypes pair {k!r}: {v!r} names {bad!r}, which is not a "
+                               f"relation of this graph ({sorted(n for n in names if isinstance(n, str))})")
+            if k in names:
+                self.reverse_etypes[self.g.to_canonical_etype(k)] = self.g.to_canonical_etype(v)
         self.negative_sampler = negative_sampler
         dev = g.device
         if not isinstance(eids, dict):

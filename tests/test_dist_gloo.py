@@ -31,10 +31,11 @@ def _worker(rank, world, port, case, q):
     try:
         import oracle_ops
         from gnnrec import nn as gnn
-        from gnnrec.dist import Exchange
+        from gnnrec.dist import AsyncEmulatedExchange, Exchange
         from gnnrec.graph import HeteroGraph
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
 
+        case, _, xk = case.partition("~")  # "~sync": the synchronous gloo Exchange
         case, _, det = case.partition("#")  # "#det": deterministic segment mode, "#seg": tiles
         seg, part, det = det == "seg", det == "part", det == "det"
         case, _, hetero = case.partition("@")  # "@attention": build-defined hetero mode
@@ -55,12 +56,16 @@ def _worker(rank, world, port, case, q):
                               strict=not hetero)
         _set_attention(model)
         model.eval()
-        ex = Exchange()
+        # default: every collective async with a real work handle (gloo's own async works),
+        # as RCCL issues them; "~sync": the blocking emulation
+        ex = Exchange() if xk == "sync" else AsyncEmulatedExchange()
         shard = GraphShard.from_graph(g, rank, world, "user", device="cpu",
                                       segments=8 if (det or seg) else None)
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
         p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
         out = p.run(shard.local_features(feats), replicate_output=not part)
+        if xk != "sync" and world > 1:  # the pass asked for every collective async
+            assert ex.works_issued > 0 and ex.sync_calls == 0, (ex.works_issued, ex.sync_calls)
         users = gather_partitioned(shard, out["user"], ex)
         res = {"user": users.numpy()}
         for nt in out:
@@ -101,6 +106,7 @@ def _run(case, world):
 
 @pytest.mark.parametrize("case,world", [
     ("model_bip_mean_sum_emb", 2),
+    ("model_bip_mean_sum_emb~sync", 2),
     ("model_het_meannnedge_mean_emb", 2),
     ("model_het_pooledge_sum_noemb_nn", 2),
     ("model_het_meanedge_max_emb", 4),
@@ -112,6 +118,7 @@ def _run(case, world):
     ("model_het_meannnedge_mean_emb#det", 2),
     ("model_het_mean_sum_skip@attention#det", 4),
     ("model_het_meanedge_max_emb#det", 8),
+    ("model_het_meanedge_max_emb#det~sync", 4),
     ("model_het_meannnedge_mean_emb#seg", 1),
     ("model_het_meanedge_max_emb#seg", 2),
     ("model_het_mean_sum_skip#part", 4),
@@ -120,7 +127,7 @@ def test_sharded_pass_matches_single_process_oracle(case, world):
     """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a
     fixed tree and exchanged all-to-all; its bitwise independence of the world size is
     checked on the GPU, tests/test_gpu_dist.py, where the arithmetic is the product's.)"""
-    name, _, hetero = case.split("#")[0].partition("@")
+    name, _, hetero = case.split("~")[0].split("#")[0].partition("@")
     meta = dict(golden_io.manifest()[name])
     a = golden_io.load(name)
     num_nodes, edges, occ = golden_io.graph_parts(a)

@@ -1,6 +1,12 @@
 """Two ranks on ONE GPU (gloo transport, HIP kernels for all arithmetic): the sharded
 full-graph pass must reproduce the single-process GPU pass.  (RCCL itself needs
-one GPU per rank; the collectives' nccl forms run in the driver's multi-GPU bench.)"""
+one GPU per rank; the collectives' nccl forms run in the driver's multi-GPU bench.)
+
+The ranks exchange through gnnrec.dist.AsyncEmulatedExchange: every collective is issued
+async and returns a work handle, its input is read late on a copy-in stream behind a delay
+kernel and its output lands late on a copy-out stream — the ordering RCCL imposes — so the
+pass's waits (inference.py: the owner's work.wait() before the projection, the pending
+all-gather waited by _get, scratch reuse across passes) are exercised, not bypassed."""
 import os
 import socket
 
@@ -43,24 +49,38 @@ def _build(agg, hetero, d=32, two_rel=False):
     return g, feats, model
 
 
-def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None, two_rel=False):
+def _async_exchange():
+    from gnnrec.dist import AsyncEmulatedExchange
+    return AsyncEmulatedExchange(delay_us=2000)
+
+
+def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None, two_rel=False,
+            passes=2):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from gnnrec.dist import Exchange
         from gnnrec.inference import GraphShard, ShardedFullGraphPass, gather_partitioned
         g, feats, model = _build(agg, hetero, d, two_rel)
-        ex = Exchange()
+        ex = _async_exchange()
         sh = GraphShard.from_graph(g, rank, world, "user", device="cuda", segments=segments)
         det = segments is not None if det is None else det
         runner = ShardedFullGraphPass(model, sh, ex, deterministic=det)
-        out = runner.run(sh.local_features(feats))
+        x = sh.local_features(feats)
+        res = []
+        for _ in range(passes):  # back to back: the scratch tables are reused across passes
+            out = runner.run(x)
+            res.append((out["user"].clone(), out["item"][:700].clone()))
+        assert ex.works_issued >= 2 * passes and ex.sync_calls == 0, \
+            (ex.works_issued, ex.sync_calls)
+        for u, i in res[1:]:
+            assert torch.equal(u, res[0][0]) and torch.equal(i, res[0][1]), "passes differ"
         if two_rel and hetero != "attention":  # both item->user relations in one launch
             assert len(runner.pair_fused) == 1, runner.pair_fused
-        users = gather_partitioned(sh, out["user"], ex)
-        q.put((rank, users.cpu().numpy(), out["item"][:700].cpu().numpy()))
+        users = gather_partitioned(sh, res[0][0], ex)
+        q.put((rank, users.cpu().numpy(), res[0][1].cpu().numpy()))
+        ex.close()
     finally:
         dist.destroy_process_group()
 
@@ -203,10 +223,12 @@ def _digest(t):
     return int((v * w).sum()), int((v * (w * w)).sum()), v.numel()
 
 
-def _c4_pass(rank, world, users, items, edges, split=None):
+def _c4_pass(rank, world, users, items, edges, split=None, ex=None, passes=1):
     """The bench's default pass (deterministic, 8 source tiles, partitioned output) on this
     rank's shard: (own user range, user digest, own item block range, item digest).
-    split: C5's relation split (4 relations; the item->user pair runs as one launch)."""
+    split: C5's relation split (4 relations; the item->user pair runs as one launch).
+    passes: back-to-back runs (scratch reuse across passes); every one must give the same
+    digests."""
     from gnnrec import nn as gnn
     from gnnrec.dist import Exchange
     from gnnrec.inference import ShardedFullGraphPass
@@ -221,15 +243,19 @@ def _c4_pass(rank, world, users, items, edges, split=None):
     model = gnn.ConvModel(GraphMeta(sh.canonical_etypes, ["item", "user"]), 3,
                           {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, "mean",
                           "cos", "sum", True).to(dev).eval()
-    runner = ShardedFullGraphPass(model, sh, Exchange(), deterministic=True)
-    with torch.no_grad():
-        out = runner.run(feats, replicate_output=False)
-    if split is not None:
-        assert len(runner.pair_fused) == 1, runner.pair_fused
+    runner = ShardedFullGraphPass(model, sh, ex if ex is not None else Exchange(),
+                                  deterministic=True)
     S = sh.shard_rows["item"]
     lo, hi = rank * S, min((rank + 1) * S, items)
-    return (sh.p_lo, sh.p_hi, _digest(out["user"]), lo, hi, _digest(out["item"][: hi - lo]),
-            out)
+    digs = []
+    for _ in range(passes):
+        with torch.no_grad():
+            out = runner.run(feats, replicate_output=False)
+        digs.append((_digest(out["user"]), _digest(out["item"][: hi - lo])))
+    assert all(dg == digs[0] for dg in digs), f"rank {rank}: back-to-back passes differ {digs}"
+    if split is not None:
+        assert len(runner.pair_fused) == 1, runner.pair_fused
+    return (sh.p_lo, sh.p_hi, digs[0][0], lo, hi, digs[0][1], out)
 
 
 def _c4_worker(rank, world, port, q, split=None):
@@ -238,7 +264,12 @@ def _c4_worker(rank, world, port, q, split=None):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank,) + _c4_pass(rank, world, *C4, split=split)[:6])
+        ex = _async_exchange()
+        r = _c4_pass(rank, world, *C4, split=split, ex=ex, passes=3)[:6]
+        # per pass: layer 1 all-to-all + all-gather, layer 2 all-to-all (partitioned output)
+        assert ex.works_issued >= 3 * 3 and ex.sync_calls == 0, (ex.works_issued, ex.sync_calls)
+        q.put((rank,) + r)
+        ex.close()
     finally:
         dist.destroy_process_group()
 
@@ -266,7 +297,7 @@ def test_c4_full_size_pass_bitwise_at_two_ranks():
         try:
             for p in procs:
                 p.start()
-            res += [(world,) + q.get(timeout=80) for _ in range(world)]
+            res += [(world,) + q.get(timeout=240) for _ in range(world)]
             for p in procs:
                 p.join(timeout=30)
                 assert p.exitcode == 0
@@ -292,7 +323,7 @@ def test_c5_full_size_pass_bitwise_at_two_ranks():
     try:
         for p in procs:
             p.start()
-        res = [q.get(timeout=120) for _ in range(world)]
+        res = [q.get(timeout=240) for _ in range(world)]
         for p in procs:
             p.join(timeout=30)
             assert p.exitcode == 0
