@@ -274,3 +274,54 @@ extern "C" int gnnrec_csr_build(const int64_t* src, const int64_t* dst, int64_t 
   return radix_sort_rows(dst, true, nullptr, n_edges, n_dst, keys, nullptr, &g, indptr, p + slot,
                          workspace_bytes - slot, s);
 }
+
+// K10 — has_edges_between (reference src/train/run.py:95-101,160-166: the false-negative
+// mask of the training loss, 1024 x K negative pairs per batch against the validation
+// graph).  The membership CSR is the relation's in-CSR with each row's source ids in
+// ascending order (gnnrec_csr_build over the edges taken in source order: the stable sort
+// keeps that order inside a row), so a query (u, v) is one lower-bound search of row v:
+// ceil(log2(deg + 1)) dependent 4-B loads, one thread per query, ids outside the node
+// ranges answer false.
+namespace gnnrec {
+namespace {
+__global__ __launch_bounds__(256) void has_edges_kernel(const int64_t* __restrict__ indptr,
+                                                        const int32_t* __restrict__ idx,
+                                                        int64_t n_dst, int64_t n_src,
+                                                        const int64_t* __restrict__ u,
+                                                        const int64_t* __restrict__ v, int64_t n,
+                                                        uint8_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t a = __builtin_nontemporal_load(u + i), b = __builtin_nontemporal_load(v + i);
+    uint8_t hit = 0;
+    if (a >= 0 && a < n_src && b >= 0 && b < n_dst) {
+      int64_t lo = indptr[b];
+      const int64_t end = indptr[b + 1];
+      int64_t hi = end;
+      const int32_t key = (int32_t)a;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (idx[mid] < key) lo = mid + 1;
+        else hi = mid;
+      }
+      hit = lo < end && idx[lo] == key;
+    }
+    __builtin_nontemporal_store(hit, out + i);
+  }
+}
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_csr_has_edges(const int64_t* indptr, const int32_t* sorted_indices,
+                                    int64_t n_dst, int64_t n_src, const int64_t* u,
+                                    const int64_t* v, int64_t n, uint8_t* out, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n >= 0 && n_dst >= 0 && n_src >= 0 && n_src < (int64_t(1) << 31),
+                 "gnnrec_csr_has_edges: bad sizes");
+  if (n == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(indptr && u && v && out && (sorted_indices || n_dst == 0),
+                 "gnnrec_csr_has_edges: null pointer");
+  hipLaunchKernelGGL(has_edges_kernel, dim3(flat_grid(n)), dim3(256), 0, as_stream(stream),
+                     indptr, sorted_indices, n_dst, n_src, u, v, n, out);
+  return check_launch("gnnrec_csr_has_edges");
+}

@@ -686,6 +686,27 @@ void csr_build(const Tensor& src, const Tensor& dst, int64_t n_dst, Tensor& ws, 
      "gnnrec_csr_build");
 }
 
+// K10 membership: has_edges_between over a source-sorted in-CSR
+void csr_has_edges(const Tensor& indptr, const Tensor& sorted_indices, int64_t n_src, const Tensor& u,
+               const Tensor& v, Tensor& out) {
+  const OneDevice one_device_;
+  dev(indptr, "indptr", at::kLong);
+  dev(sorted_indices, "sorted_indices", at::kInt);
+  dev(u, "u", at::kLong);
+  dev(v, "v", at::kLong);
+  dev(out, "out", at::kBool);
+  const int64_t n = u.numel();
+  TORCH_CHECK_VALUE(v.numel() == n && out.numel() == n && u.is_contiguous() && v.is_contiguous() &&
+                        out.is_contiguous() && indptr.numel() >= 1,
+                    "has_edges: contiguous u, v, out of one length and a non-empty indptr");
+  if (meta(u)) return;
+  const c10::DeviceGuard g(u.device());
+  ck(gnnrec_csr_has_edges(p<int64_t>(indptr), p<int32_t>(sorted_indices), indptr.numel() - 1,
+                          n_src, p<int64_t>(u), p<int64_t>(v), n,
+                          reinterpret_cast<uint8_t*>(out.data_ptr()), stream_of(u)),
+     "gnnrec_csr_has_edges");
+}
+
 // ---------------------------------------------------------------- sharded-pass helpers
 void add_(Tensor& a, const Tensor& b) {
   const OneDevice one_device_;
@@ -1108,6 +1129,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("lstm_step(Tensor P, Tensor indptr, Tensor indices, Tensor order, int t, int n_act, "
         "Tensor h_in, Tensor(a!) h_out, Tensor(b!) c, Tensor W_hhT, Tensor(c!) out) -> ()");
   m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("csr_has_edges(Tensor indptr, Tensor sorted_indices, int n_src, Tensor u, Tensor v, "
+        "Tensor(a!) out) -> ()");
   m.def("margin_loss(Tensor pos, Tensor neg, int K, float delta, Tensor? mask, Tensor? recency, "
         "Tensor(a!) g_pos, Tensor(b!) g_neg, Tensor(c!) partial) -> ()");
   m.def("sum_scaled(Tensor x, float scale, Tensor(a!) out) -> ()");
@@ -1168,6 +1191,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("tree_sum_", &tree_sum_);                       \
   m.impl("lstm_step", &lstm_step);                       \
   m.impl("gather_rows", &gather_rows);                   \
+  m.impl("csr_has_edges", &csr_has_edges);               \
   m.impl("margin_loss", &margin_loss);                   \
   m.impl("sum_scaled", &sum_scaled);                     \
   m.impl("synth_edges", &synth_edges);                   \

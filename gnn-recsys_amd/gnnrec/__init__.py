@@ -7,13 +7,13 @@ include/gnnrec.h and wrapped here as drop-in replacements for the reference's
 src/model.py modules and DGL loaders.  See DESIGN.md.
 """
 from . import _lib
-from .graph import Block, HeteroGraph, PairGraph, RelGraph, NID, EID  # noqa: F401
+from .graph import Block, HeteroGraph, PairGraph, RelGraph, NID, EID, create_graph  # noqa: F401
 from .nn import (ConvLayer, ConvModel, CosinePrediction, HeteroGraphConv,  # noqa: F401
                  NodeEmbedding, PredictingLayer, PredictingModule, max_margin_loss)
 
 __all__ = ["ConvLayer", "ConvModel", "CosinePrediction", "HeteroGraphConv", "NodeEmbedding",
            "PredictingLayer", "PredictingModule", "max_margin_loss", "HeteroGraph", "Block",
-           "PairGraph", "RelGraph", "NID", "EID"]
+           "PairGraph", "RelGraph", "NID", "EID", "create_graph"]
 
 __version__ = "0.1.0"
 

@@ -88,6 +88,7 @@ SIGNATURES = {
     "gnnrec_csr_from_keys": (_INT, [_P, _I64, _I64, _P, _U64, _P, _P, _P]),
     "gnnrec_csr_build_workspace_bytes": (_U64, [_I64, _I64]),
     "gnnrec_csr_build": (_INT, [_P, _P, _I64, _I64, _P, _U64, _P, _P, _P, _P]),
+    "gnnrec_csr_has_edges": (_INT, [_P, _P, _I64, _I64, _P, _P, _I64, _P, _P]),
     "gnnrec_add_f32": (_INT, [_P, _P, _P, _I64, _P]),
     "gnnrec_tree_sum_f32": (_INT, [_P, _INT, _I64, _P, _P]),
     "gnnrec_row_epilogue_f32": (_INT, [_P, _I64, _I64, _I64, _INT, _INT, _F32, _P, _P, _P, _I64,

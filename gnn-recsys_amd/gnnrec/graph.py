@@ -137,16 +137,36 @@ class HeteroGraph:
     is_block = False
 
     def __init__(self, data_dict: Dict[CEType, Tuple[torch.Tensor, torch.Tensor]],
-                 num_nodes_dict: Dict[str, int], device=None):
+                 num_nodes_dict: Optional[Dict[str, int]] = None, device=None):
+        """data_dict: {(src type, relation, dst type): (src ids, dst ids)} — the reference's
+        `graph_schema` (src/utils_data.py:204-238).  num_nodes_dict: nodes per type; types it
+        omits (all of them when None) get max id + 1 over every relation they appear in,
+        as dgl.heterograph infers them (0 for a type with no edges)."""
         self._coo = {}
         for ce, (s, d) in data_dict.items():
+            if len(ce) != 3:
+                raise ValueError(f"edge type {ce!r} must be a (src type, relation, dst type) "
+                                 f"triple")
             s = torch.as_tensor(s, dtype=torch.int64, device=device)
             d = torch.as_tensor(d, dtype=torch.int64, device=device)
-            if s.shape != d.shape:
-                raise ValueError(f"src/dst length mismatch for {ce}")
+            if s.shape != d.shape or s.dim() != 1:
+                raise ValueError(f"src/dst of {ce} must be 1-D id arrays of one length")
             self._coo[tuple(ce)] = (s, d)
         self.canonical_etypes = list(self._coo.keys())
-        self._num_nodes = dict(num_nodes_dict)
+        self._num_nodes = dict(num_nodes_dict or {})
+        inferred: Dict[str, int] = {}
+        for ce, (s, d) in self._coo.items():
+            for nt, ids in ((ce[0], s), (ce[2], d)):
+                if nt in self._num_nodes:
+                    continue
+                n = int(ids.max()) + 1 if ids.numel() else 0
+                inferred[nt] = max(inferred.get(nt, 0), n)
+        for ce, (s, d) in self._coo.items():  # ids must lie in [0, N)
+            for nt, ids in ((ce[0], s), (ce[2], d)):
+                if nt in self._num_nodes and ids.numel() and not ids.is_meta and (
+                        int(ids.min()) < 0 or int(ids.max()) >= self._num_nodes[nt]):
+                    raise ValueError(f"{ce}: {nt} ids outside [0, {self._num_nodes[nt]})")
+        self._num_nodes.update(inferred)
         for ce in self.canonical_etypes:
             for nt in (ce[0], ce[2]):
                 self._num_nodes.setdefault(nt, 0)
@@ -258,24 +278,30 @@ class HeteroGraph:
         return self.rel_graph(key if isinstance(key, tuple) and len(key) == 3 else key)
 
     def has_edges_between(self, u, v, etype=None) -> torch.Tensor:
-        """Membership of (u[i], v[i]) in relation etype (reference run.py:95-101)."""
+        """Membership of (u[i], v[i]) in relation etype: a bool tensor (reference
+        src/train/run.py:95-101,160-166, the false-negative mask; DGL's has_edges_between).
+        On a HIP device, one binary search per query over the relation's source-sorted
+        in-CSR (gnnrec_csr_has_edges; the CSR is built once by the library's radix sort and
+        cached).  A graph still in host memory answers with a host sort + search."""
         ce = self.to_canonical_etype(etype if etype is not None else self.canonical_etypes[0])
-        indptr, indices, _ = self.in_csr(ce)
-        u = torch.as_tensor(u, dtype=torch.int64, device=indptr.device)
-        v = torch.as_tensor(v, dtype=torch.int64, device=indptr.device)
-        key = self._sorted_keys(ce)
-        q = v * self._num_nodes[ce[0]] + u
+        s, d = self._coo[ce]
+        if s.is_cuda:
+            cache = self._csr_edata.setdefault(("_member",) + ce, {})
+            if "csr" not in cache:
+                cache["csr"] = ops.membership_csr(s, d, self._num_nodes[ce[0]],
+                                                  self._num_nodes[ce[2]])
+            indptr, indices = cache["csr"]
+            return ops.has_edges(indptr, indices, self._num_nodes[ce[0]], u, v)
+        u = torch.as_tensor(u, dtype=torch.int64).reshape(-1)
+        v = torch.as_tensor(v, dtype=torch.int64).reshape(-1)
+        n_src = self._num_nodes[ce[0]]
+        key = torch.sort(d * n_src + s).values
+        ok = (u >= 0) & (u < n_src) & (v >= 0) & (v < self._num_nodes[ce[2]])
+        q = v * n_src + u
         if key.numel() == 0:
             return torch.zeros_like(q, dtype=torch.bool)
         pos = torch.searchsorted(key, q).clamp(max=key.numel() - 1)
-        return key[pos] == q
-
-    def _sorted_keys(self, ce):
-        cache = self._csr_edata.setdefault(("_keys",) + ce, {})
-        if "k" not in cache:
-            s, d = self._coo[ce]
-            cache["k"] = torch.sort(d * self._num_nodes[ce[0]] + s).values
-        return cache["k"]
+        return (key[pos] == q) & ok
 
     def to(self, device):
         g = HeteroGraph({ce: (s.to(device), d.to(device)) for ce, (s, d) in self._coo.items()},
@@ -287,6 +313,15 @@ class HeteroGraph:
             for k, v in f.items():
                 g._edata[ce][k] = v.to(device)
         return g
+
+
+def create_graph(graph_schema: Dict[CEType, Tuple[object, object]], device=None,
+                 num_nodes_dict: Optional[Dict[str, int]] = None) -> HeteroGraph:
+    """Drop-in for the reference's `create_graph(graph_schema)` (src/builder.py:377-383,
+    `dgl.heterograph(graph_schema)`): the relation -> (src ids, dst ids) dict built by
+    DataLoader.graph_schema (src/utils_data.py:204-238, numpy arrays or tensors), node
+    counts inferred per type as max id + 1 unless given."""
+    return HeteroGraph(graph_schema, num_nodes_dict, device=device)
 
 
 class Block:

@@ -295,6 +295,36 @@ def csr_build(src: torch.Tensor, dst: torch.Tensor, n_dst: int):
     return indptr, indices, eids
 
 
+def membership_csr(src: torch.Tensor, dst: torch.Tensor, n_src: int, n_dst: int):
+    """The dst-major CSR of (src, dst) with every row's source ids ascending — what
+    has_edges searches.  Two stable radix sorts of the library (gnnrec_csr_build): by source
+    (edge ids grouped by source), then by destination over the edges in that order, so the
+    second sort's stability leaves each row sorted by source.  -> (indptr, sorted_indices)."""
+    _dev(src, "src", torch.int64)
+    _dev(dst, "dst", torch.int64)
+    if src.numel() == 0:
+        return torch.zeros(n_dst + 1, dtype=torch.int64, device=src.device), \
+            torch.zeros(0, dtype=torch.int32, device=src.device)
+    _, _, by_src = csr_build(dst, src, n_src)
+    indptr, indices, _ = csr_build(gather_rows(src, by_src), gather_rows(dst, by_src), n_dst)
+    return indptr, indices
+
+
+def has_edges(indptr: torch.Tensor, sorted_indices: torch.Tensor, n_src: int,
+              u: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """K10: bool [n], (u[i] -> v[i]) is an edge of the relation whose membership_csr is
+    (indptr, sorted_indices) (gnnrec_csr_has_edges: one binary search per query)."""
+    _dev(indptr, "indptr", torch.int64)
+    u = torch.as_tensor(u, dtype=torch.int64, device=indptr.device).reshape(-1).contiguous()
+    v = torch.as_tensor(v, dtype=torch.int64, device=indptr.device).reshape(-1).contiguous()
+    if u.numel() != v.numel():
+        raise ValueError(f"has_edges: {u.numel()} sources for {v.numel()} destinations")
+    out = torch.empty(u.numel(), dtype=torch.bool, device=indptr.device)
+    if u.numel():
+        _T().csr_has_edges(indptr, sorted_indices, int(n_src), u, v, out)
+    return out
+
+
 def csr_from_keys(keys: torch.Tensor, n_rows: int):
     """Rows of a COO list: -> (indptr int64 [n_rows+1], perm int32 [E]) with perm the edge
     ids grouped by keys[e] (ascending edge id inside a row).  keys: int32/int64 in [0, n_rows)."""

@@ -398,6 +398,16 @@ int gnnrec_csr_build(const int64_t* src, const int64_t* dst, int64_t n_edges, in
                      void* workspace, size_t workspace_bytes, int64_t* indptr, int32_t* indices,
                      int64_t* eids, void* stream);
 
+/* K10 — DGLGraph.has_edges_between(u, v, etype) (reference src/train/run.py:95-101,160-166,
+ * the false-negative mask; DGL 0.5.2 [ext]: `_CAPI_DGLHeteroHasEdgesBetween`): out[i] = 1
+ * when some edge u[i] -> v[i] exists, else 0; ids outside [0, n_src) / [0, n_dst) give 0.
+ * (indptr, sorted_indices) is the relation's dst-major CSR with every row's source ids in
+ * ASCENDING order — gnnrec_csr_build over the edges listed in source order (the stable
+ * sort keeps it inside a row) — and each query is one binary search of its row. */
+int gnnrec_csr_has_edges(const int64_t* indptr, const int32_t* sorted_indices, int64_t n_dst,
+                         int64_t n_src, const int64_t* u, const int64_t* v, int64_t n,
+                         uint8_t* out, void* stream);
+
 /* out[i] = a[i] + b[i] over n floats (out may alias a or b): the upper levels of the
  * deterministic pass's fixed pairwise tree over source-range partial tables. */
 int gnnrec_add_f32(const float* a, const float* b, float* out, int64_t n, void* stream);

@@ -401,6 +401,17 @@ def max_margin_loss(pos, neg, delta, K, use_recency=False, recency=None,
 
 
 # --------------------------------------------------------------- sampler ----
+def has_edges_between(src, dst, n_src: int, n_dst: int, u, v) -> np.ndarray:
+    """valid_graph.has_edges_between(neg_src, neg_dst, etype) of the false-negative mask
+    (reference src/train/run.py:95-101,160-166; DGL 0.5.2 [ext]): bool per query, True when
+    some edge u[i] -> v[i] exists.  Build-defined where DGL raises: ids outside the node
+    ranges answer False.  A set lookup over the relation's (dst, src) keys."""
+    src, dst = np.asarray(src, np.int64), np.asarray(dst, np.int64)
+    u, v = np.asarray(u, np.int64).reshape(-1), np.asarray(v, np.int64).reshape(-1)
+    ok = (u >= 0) & (u < n_src) & (v >= 0) & (v < n_dst)
+    return np.isin(v * n_src + u, dst * n_src + src) & ok
+
+
 def sample_neighbors(indptr, indices, eids, seeds, fanout: int, key: int = 0, excluded=None):
     indptr = np.ascontiguousarray(indptr, np.int64)
     indices = np.ascontiguousarray(indices, np.int64)

@@ -84,3 +84,34 @@ def test_csr_build_c4_size_bit_exact():
             np.testing.assert_array_equal(a.cpu().numpy(), b, err_msg=name)
         del out, ref
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n_src,n_dst,E", [(1, 1, 0), (300, 40, 5000), (40, 300, 5000),
+                                           (100_000, 2_000, 400_000), (3_000, 90_000, 400_000)])
+def test_has_edges_between_matches_oracle(n_src, n_dst, E):
+    """K10 (reference src/train/run.py:95-101): the device membership search against the
+    oracle's set lookup, bit for bit — true edges, multi-edges, random pairs (mostly
+    absent), ids outside the node ranges, one heavy row (a third of the edges)."""
+    from gnnrec.graph import HeteroGraph
+    rng = np.random.default_rng(E + n_src)
+    s = rng.integers(0, n_src, E)
+    d = rng.integers(0, n_dst, E)
+    if E:
+        d[::3] = n_dst // 2
+    ce = ("user", "buys", "item")
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d))},
+                    {"user": n_src, "item": n_dst}, device=DEV)
+    qn = 200_000
+    qu = rng.integers(-2, n_src + 2, qn)
+    qv = rng.integers(-2, n_dst + 2, qn)
+    if E:  # a third of the queries are real edges
+        k = rng.integers(0, E, qn // 3)
+        qu[: qn // 3], qv[: qn // 3] = s[k], d[k]
+    got = g.has_edges_between(torch.from_numpy(qu).to(DEV), torch.from_numpy(qv).to(DEV),
+                              etype="buys")
+    assert got.dtype == torch.bool and got.device.type == "cuda"
+    ref = oracle.has_edges_between(s, d, n_src, n_dst, qu, qv)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    host = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(d))},
+                       {"user": n_src, "item": n_dst})
+    np.testing.assert_array_equal(host.has_edges_between(qu, qv).numpy(), ref)

@@ -42,3 +42,26 @@ def test_round_trip(tmp_path):
         for k, v in g._edata[ce].items():
             assert torch.equal(h.edges[ce].data[k], v)
     assert read_graph(f).num_edges() == g.num_edges()
+
+
+def test_create_graph_infers_node_counts_like_dgl_heterograph():
+    """Reference src/builder.py:377-383: create_graph(graph_schema) = dgl.heterograph(
+    graph_schema), node counts inferred per type as max id + 1 over every relation the
+    type appears in (0 for a type with no edges); given counts are kept and checked."""
+    import pytest
+
+    from gnnrec import create_graph
+    u = np.array([0, 5, 2]), np.array([1, 1, 7])
+    schema = {("user", "buys", "item"): u, ("item", "bought-by", "user"): (u[1], u[0]),
+              ("user", "clicks", "item"): (np.array([9]), np.array([0])),
+              ("sport", "includes", "sport"): (np.zeros(0, np.int64), np.zeros(0, np.int64))}
+    g = create_graph(schema)
+    assert (g.num_nodes("user"), g.num_nodes("item"), g.num_nodes("sport")) == (10, 8, 0)
+    assert g.canonical_etypes == list(schema)
+    assert g.num_edges("buys") == 3 and g.num_edges(("user", "clicks", "item")) == 1
+    g2 = create_graph(schema, num_nodes_dict={"user": 12})
+    assert g2.num_nodes("user") == 12 and g2.num_nodes("item") == 8
+    with pytest.raises(ValueError):
+        create_graph(schema, num_nodes_dict={"user": 5})
+    with pytest.raises(ValueError):
+        create_graph({("user", "buys"): u})
