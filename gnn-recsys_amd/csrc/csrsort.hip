@@ -319,7 +319,7 @@ extern "C" int gnnrec_csr_has_edges(const int64_t* indptr, const int32_t* sorted
   GNNREC_REQUIRE(n >= 0 && n_dst >= 0 && n_src >= 0 && n_src < (int64_t(1) << 31),
                  "gnnrec_csr_has_edges: bad sizes");
   if (n == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(indptr && u && v && out && (sorted_indices || n_dst == 0),
+  GNNREC_REQUIRE(indptr && u && v && out,  // sorted_indices: null for an edgeless relation
                  "gnnrec_csr_has_edges: null pointer");
   hipLaunchKernelGGL(has_edges_kernel, dim3(flat_grid(n)), dim3(256), 0, as_stream(stream),
                      indptr, sorted_indices, n_dst, n_src, u, v, n, out);
