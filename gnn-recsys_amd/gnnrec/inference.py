@@ -513,8 +513,8 @@ class ShardedFullGraphPass:
         plus W_n b_e on rows that have neighbours."""
         Ws, Wn = mod.fc_self.weight, mod.fc_neigh.weight
         fd, fs = self._fold.get(ce[2]), self._fold.get(ce[0])
-        if fd is None and fs is None:
-            return Ws.detach(), Wn.detach(), None, None
+        if fd is None and fs is None:  # the parameters themselves: the ops detach them, and
+            return Ws, Wn, None, None   # their transposes stay cached on them (ops._transposed)
 
         def ver(*ts):
             return tuple((id(t), t._version) for t in ts)

@@ -537,6 +537,29 @@ def _nnz(indptr: torch.Tensor) -> int:
     return v
 
 
+def _transposed(W: torch.Tensor) -> torch.Tensor:
+    """Wᵀ (k-major, contiguous) of a fused kernel's weight, kept on the weight tensor and
+    rebuilt only when the weight changes (its version counter, an optimizer step) — not a
+    transpose-copy kernel per launch inside the pass (C4: two per layer before the fused
+    launch, profiles/r02f_c4_timeline.txt)."""
+    if torch.compiler.is_compiling() or not W.is_cuda:
+        return W.detach().t().contiguous()
+    hit = getattr(W, "_gnnrec_wt", None)
+    key = (W._version, W.data_ptr())
+    cur = torch.cuda.current_stream(W.device)
+    if hit is None or hit[0] != key:
+        ev = torch.cuda.Event()
+        hit = (key, W.detach().t().contiguous(), ev, cur.cuda_stream)
+        ev.record(cur)
+        try:
+            W._gnnrec_wt = hit
+        except (AttributeError, RuntimeError):  # pragma: no cover
+            pass
+    elif hit[3] != cur.cuda_stream:  # made on another stream: ordered after its copy
+        cur.wait_event(hit[2])
+    return hit[1]
+
+
 def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
                  edge_weight: Optional[torch.Tensor] = None, relu: bool = True,
                  l2norm: bool = False, accum: str = "store", out_div: float = 0.0,
@@ -582,8 +605,8 @@ def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
         if variant not in (None, "mfma"):
             raise ValueError("pre-projected source rows (W_neigh None) run on the mfma kernel")
         variant = "mfma"
-    WsT = W_self.detach().t().contiguous()
-    WnT = None if W_neigh is None else W_neigh.detach().t().contiguous()
+    WsT = _transposed(W_self)
+    WnT = None if W_neigh is None else _transposed(W_neigh)
     for t, name in ((bias, "bias"), (bias_nonempty, "bias_nonempty")):
         if t is not None:
             _dev(t, name, torch.float32)
@@ -657,8 +680,8 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
     bias_a = None if bias_a is None else bias_a.detach().contiguous()
     bias_b = None if bias_b is None else bias_b.detach().contiguous()
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
-    _T().spmm_project2(*args, H, W_self_a.detach().t().contiguous(),
-                       W_self_b.detach().t().contiguous(), bias_a, bias_b, epi,
+    _T().spmm_project2(*args, H, _transposed(W_self_a), _transposed(W_self_b), bias_a, bias_b,
+                       epi,
                        ACCUM["attn_last" if combine == "attention" else combine], attn_vec,
                        float(out_div), out)
     return out

@@ -12,8 +12,9 @@
       (n_layers=3: two conv layers, the reference's convention with embedding_layer; and
       n_layers=4: three conv layers).
   C4/C5  the 500M-edge full-graph pass (bench.py's workload; C5 = 80 % clicks / 20 % buys,
-      4 relations, hetero sum and the build-defined attention): every layer of the sharded
-      pass checked on 1000 sampled rows per node type — the layer's GPU inputs for the
+      4 relations, hetero sum and the build-defined attention; C4 with Zipf-1.0 items): every
+      layer of the sharded pass checked on a 1/32 slice of each node type + 1000 random rows
+      (+ the 100 heaviest items under Zipf) — the layer's GPU inputs for the
       sampled rows' in-neighbourhoods go through oracle.hetero_conv and must give the GPU's
       outputs.  The neighbour lists come from re-generating the edge stream (synth_edges,
       bit-exact to the oracle's generator) and filtering it, not from the product's CSR.
@@ -270,12 +271,18 @@ SPLITS = {"c4": (("buys", "bought-by", 1.0),),
           "c5": (("clicks", "clicked-by", 0.8), ("buys", "bought-by", 0.2))}
 
 
-def _neighbour_lists(split, rows_u, rows_i, chunk=1 << 26):
+def _neighbour_lists(split, rows_u, rows_i, chunk=1 << 26, cdf=None):
     """In-edges (eid order) of the sampled user rows (relations item -> user) and item rows
-    (user -> item), from the regenerated edge stream: {ce: (indptr, src global, eids)}."""
+    (user -> item), from the regenerated edge stream: {ce: (indptr, src global, eids)}.
+    cdf: the item Zipf CDF of a skewed stream (bench --zipf)."""
     from gnnrec import ops
     from gnnrec.synth import relation_pairs
     pairs = relation_pairs(split)
+    sel = {}
+    for rows, n in ((rows_u, N_U), (rows_i, N_I)):  # membership tables of the sampled rows
+        m = torch.zeros(n, dtype=torch.bool, device=DEV)
+        m[rows] = True
+        sel[n] = m
     bounds = [0]
     for _, _, frac in pairs:
         bounds.append(min(N_E, bounds[-1] + int(round(frac * N_E))))
@@ -285,17 +292,17 @@ def _neighbour_lists(split, rows_u, rows_i, chunk=1 << 26):
         acc = {fwd: ([], [], []), rev: ([], [], [])}
         for e0 in range(lo, hi, chunk):
             n = min(chunk, hi - e0)
-            u, i = ops.synth_edges(11, e0, n, N_U, N_I, DEV)
+            u, i = ops.synth_edges(11, e0, n, N_U, N_I, DEV, cdf)
             u, i = u.long(), i.long()
             for ce, dst, src, rows in ((rev, u, i, rows_u), (fwd, i, u, rows_i)):
-                m = torch.nonzero(torch.isin(dst, rows)).squeeze(1)
+                m = torch.nonzero(sel[N_U if rows is rows_u else N_I][dst]).squeeze(1)
                 acc[ce][0].append(torch.searchsorted(rows, dst[m]))
                 acc[ce][1].append(src[m])
                 acc[ce][2].append(m + (e0 - lo))
         for ce, (d, s, e) in acc.items():
             d, s, e = (_np(torch.cat(x)) for x in (d, s, e))
-            ip, _, order = oracle.csr_from_coo(np.zeros_like(d), d, (rows_u if ce == rev
-                                                                    else rows_i).numel())
+            ip, _, order = oracle.csr_from_coo_c(np.zeros_like(d), d, (rows_u if ce == rev
+                                                                      else rows_i).numel())
             out[ce] = (ip, s[order], e[order])
     return out
 
@@ -325,18 +332,39 @@ def _layer_rows_vs_oracle(model, layer_idx, h_in, h_out, lists, rows, hetero, ra
         np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL, err_msg=f"layer {layer_idx} {T}")
 
 
-@pytest.fixture(scope="module", params=["c4", "c5"])
+@pytest.fixture(scope="module", params=["c4", "c5", "c4zipf"])
 def full_shard(request):
-    from gnnrec.synth import bipartite_shard, node_features
-    shard = bipartite_shard(N_U, N_I, N_E, 0, 1, torch.device(DEV), split=SPLITS[request.param],
-                            segments=8)
+    """The full-size shard plus the rows checked against the oracle: per node type a
+    contiguous 1/32 slice (312,500 users, 31,250 items — the slice bench.cpu_baseline
+    times) and 1000 random rows; with --zipf 1.0 items also the 100 heaviest, whose
+    ~180M in-edges (the top item ~35M) run through the chunked heavy-row tiles
+    (inference.TILE_SPLIT) and their 16-partial combine."""
+    from gnnrec.synth import bipartite_shard, node_features, zipf_cdf
+    cfg = request.param
+    zipf = 1.0 if cfg == "c4zipf" else 0.0
+    split = SPLITS["c5" if cfg == "c5" else "c4"]
+    shard = bipartite_shard(N_U, N_I, N_E, 0, 1, torch.device(DEV), split=split, segments=8,
+                            zipf_s=zipf)
     feats = {"user": node_features(N_U, D, 0, DEV), "item": node_features(N_I, D, 1, DEV)}
     gen = torch.Generator(device=DEV)
     gen.manual_seed(5)
-    rows = {"user": torch.sort(torch.randperm(N_U, device=DEV, generator=gen)[:1000]).values,
-            "item": torch.sort(torch.randperm(N_I, device=DEV, generator=gen)[:1000]).values}
-    lists = _neighbour_lists(SPLITS[request.param], rows["user"], rows["item"])
-    yield request.param, shard, feats, {nt: _np(v) for nt, v in rows.items()}, lists
+    rows = {}
+    for nt, n in (("user", N_U), ("item", N_I)):
+        # (under Zipf the item ids are popularity ranks: the first 1/32 of them hold ~3/4 of
+        # the edges, so the item slice is taken from the light end there)
+        lo = n - n // 32 if zipf and nt == "item" else 0
+        pick = [torch.arange(lo, lo + n // 32, device=DEV),
+                torch.randperm(n, device=DEV, generator=gen)[:1000]]
+        if zipf and nt == "item":
+            deg = shard.rels[("user", "buys", "item")].deg_own[:N_I].long()
+            pick.append(torch.topk(deg, 100).indices)
+        rows[nt] = torch.unique(torch.cat(pick))  # sorted
+    cdf = zipf_cdf(N_I, zipf, DEV) if zipf else None
+    lists = _neighbour_lists(split, rows["user"], rows["item"], cdf=cdf)
+    if zipf:  # the heavy rows really are in the checked set, with their whole in-edge lists
+        ip = lists[("user", "buys", "item")][0]
+        assert int(np.diff(ip).max()) > 30_000_000
+    yield cfg, shard, feats, {nt: _np(v) for nt, v in rows.items()}, lists
     del shard, feats
     torch.cuda.empty_cache()
 
@@ -348,7 +376,7 @@ def test_full_size_pass_layers_match_oracle(full_shard, hetero):
     from gnnrec.inference import ShardedFullGraphPass
     from gnnrec.synth import GraphMeta
     config, shard, feats, rows, lists = full_shard
-    if config == "c4" and hetero == "attention":
+    if config != "c5" and hetero == "attention":
         pytest.skip("C4 has one relation per destination type: attention == identity weights")
     # degree conservation of the product's CSRs: every edge lands in one row
     for ce, rs in shard.rels.items():

@@ -335,3 +335,49 @@ def test_c5_full_size_pass_bitwise_at_two_ranks():
     for rank, ulo, uhi, udig, ilo, ihi, idig in res:
         assert _digest(out["user"][ulo:uhi]) == udig, f"rank {rank}: user rows differ"
         assert _digest(out["item"][ilo:ihi]) == idig, f"rank {rank}: item rows differ"
+
+
+def _emulation_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gnnrec.dist import AsyncEmulatedExchange
+        ex = AsyncEmulatedExchange(delay_us=30000)
+        own = torch.full((4, 8), float(rank + 1), device="cuda")
+        out = torch.full((8, 8), -1.0, device="cuda")
+        _, work = ex.all_gather_rows(own, out, async_op=True)
+        own.fill_(7.0)  # the collective reads its input late: this write races it
+        early = out.clone()  # no wait: the output has not landed yet
+        work.wait()
+        late = out.clone()
+        full = torch.arange(16.0, device="cuda").view(8, 2) * (rank + 1)
+        blocks, work = ex.all_to_all_rows(full, async_op=True)
+        work.wait()
+        q.put((rank, early.cpu().numpy(), late.cpu().numpy(), blocks.cpu().numpy()))
+        ex.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_async_emulation_lands_late_and_reads_late():
+    """The emulation does what makes it a test of the pass's ordering: a reader that skips
+    work.wait() sees the output before it lands, and the input is read when the collective
+    runs (after its delay), not when it is issued — as under RCCL."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q, port = ctx.Queue(), _port()
+    procs = [ctx.Process(target=_emulation_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, early, late, blocks in res:
+        assert (early == -1).all(), "the output landed before the delay ran out"
+        assert (late == 7.0).all(), "the input was read before the collective ran"
+        for src in range(2):  # block `rank` of every rank's table, in source-rank order
+            want = np.arange(16.0).reshape(8, 2)[rank * 4:(rank + 1) * 4] * (src + 1)
+            np.testing.assert_array_equal(blocks[src], want)
