@@ -37,7 +37,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=1 / 32,
                     help="fraction of each relation's destination rows the bounded CPU "
                          "baseline aggregates (over the full-size tables and edge stream)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 class EventTimers:
@@ -164,33 +164,41 @@ def csrc_digest() -> str:
     return h.hexdigest()[:16]
 
 
-def default_workload(args) -> bool:
+def workload_key(args) -> tuple:
+    """What a PMC profile's bytes depend on: the graph, the model and the pass mode."""
     return (args.users, args.items, args.edges, args.dim, args.zipf, args.aggregator,
-            args.config, args.hetero, args.mode, args.segments) == (
-                10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4", "sum",
-                "deterministic", 8)
+            args.config, args.hetero, args.mode, args.segments)
+
+
+def default_workload(args) -> bool:
+    return workload_key(args) == (10_000_000, 1_000_000, 500_000_000, 128, 0.0, "mean", "c4",
+                                  "sum", "deterministic", 8)
 
 
 def pmc_traffic(args, world):
-    """{bench tag: HBM bytes per launch} from the newest committed rocprofv3 PMC
-    passes of the default workload (profiles/<tag>_pmc_{fetch,write}.csv +
-    <tag>_pmc_meta.json with empty bench_args): FETCH_SIZE x2 (gfx950
-    counts half the bytes of wide reads) + WRITE_SIZE, KB -> B.  Only for the default
-    single-GPU C4 workload the passes ran on, and only if the HIP sources hash to the
-    `csrc_sha` the profile was taken with; otherwise ({}, reason)."""
+    """{bench tag: HBM bytes per launch} from the newest committed rocprofv3 PMC passes of
+    THIS run's workload (profiles/<tag>_pmc_{fetch,write}.csv + <tag>_pmc_meta.json, whose
+    bench_args give the same workload_key: C4 by default, C5 with --config c5, ...):
+    FETCH_SIZE x2 (gfx950 counts half the bytes of wide reads) + WRITE_SIZE, KB -> B.  One
+    GPU only, and only if the HIP sources hash to the `csrc_sha` the profile was taken
+    with; otherwise ({}, reason)."""
     import csv
     import glob
-    # the passes taken on the default workload (no extra bench arguments); newest last
+    if world != 1:
+        return {}, "not the profiled workload (profiles are single-GPU)"
+    mine = workload_key(args)
     metas = [m for m in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_meta.json")))
-             if not json.load(open(m)).get("bench_args")]
-    if world != 1 or not default_workload(args):
-        return {}, "not the profiled workload"
+             if workload_key(parse(json.load(open(m)).get("bench_args", []))) == mine]
     if not metas:
-        return {}, "no PMC profile"
+        return {}, "no PMC profile of this workload"
+    cur = [m for m in metas if json.load(open(m)).get("csrc_sha") == csrc_digest()]
+    if not cur:
+        tag = os.path.basename(metas[-1])[: -len("_pmc_meta.json")]
+        return {}, (f"stale: {tag} profiled csrc {json.load(open(metas[-1])).get('csrc_sha')}, "
+                    f"now {csrc_digest()}")
+    metas = cur  # newest profile of these very kernels
     meta = json.load(open(metas[-1]))
     tag = os.path.basename(metas[-1])[: -len("_pmc_meta.json")]
-    if meta.get("csrc_sha") != csrc_digest():
-        return {}, f"stale: {tag} profiled csrc {meta.get('csrc_sha')}, now {csrc_digest()}"
     out = {}
     for t, kernel in meta["kernels"].items():  # bench tag -> kernel-name substring
         tot, n = 0.0, 0
@@ -417,11 +425,13 @@ def main():
     value = edges_per_step * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
 
-    # roofline of the aggregation kernels (SURVEY §8d d4 bytes per launch ÷ the launch's
-    # HIP-event time): the headline is the kernel with the most time per pass (C4: the
-    # user->item source tiles, 16 launches, about half the pass; the fused item->user
-    # launches the other half); every other aggregation kernel rides along as flat
-    # `<field>_<tag>` keys so a flat record parser keeps them
+    # roofline of the aggregation (SURVEY §8d d4 algorithmic bytes ÷ HIP-event time of the
+    # launches, timed live on the stream they run on).  Headline: every aggregation launch
+    # of a pass COMBINED — their bytes per pass ÷ their summed time per pass — so it cannot
+    # flip between two kernels of near-equal share (C4: the user->item source tiles and the
+    # fused item->user launch, ~half the pass each); every kernel rides along as flat
+    # `<field>_<tag>` keys, and `pass_frac` prices the whole step: aggregation bytes per
+    # step ÷ ms_per_step ÷ peak
     per_tag = launch_bytes(shard, d, runner, det)
     stats = {}
     for t in per_tag:
@@ -429,20 +439,28 @@ def main():
         if n:
             b = per_tag[t][0] / per_tag[t][1]  # bytes per layer / launches per layer
             stats[t] = {"launch_ms": ms, "launches_timed": n, "bytes_per_launch": b,
-                        "achieved": b / (ms * 1e-3) / 1e9, "ms_per_pass": ms * n / args.steps}
+                        "achieved": b / (ms * 1e-3) / 1e9, "ms_per_pass": ms * n / args.steps,
+                        "launches_per_pass": n / args.steps}
     traffic, traffic_src = pmc_traffic(args, world)
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": None, "traffic": None}
     if stats:
         order = sorted(stats, key=lambda t: -stats[t]["ms_per_pass"])
-        head = order[0]
-        st = stats[head]
-        roof.update(achieved=st["achieved"], frac=st["achieved"] / HBM_PEAK_GBS,
-                    traffic=traffic.get(head),
-                    kernel=KERNELS[head][1], bytes_per_launch=st["bytes_per_launch"],
-                    launch_ms=st["launch_ms"], launches_timed=st["launches_timed"],
-                    share_of_step=st["ms_per_pass"] / ms_step, traffic_src=traffic_src)
-        for t in order[1:]:
+        bytes_pass = sum(st["bytes_per_launch"] * st["launches_per_pass"] for st in stats.values())
+        ms_pass = sum(st["ms_per_pass"] for st in stats.values())
+        ach = bytes_pass / (ms_pass * 1e-3) / 1e9
+        tr = None
+        if traffic and all(t in traffic for t in stats):
+            tr = sum(traffic[t] * stats[t]["launches_per_pass"] for t in stats)
+        roof.update(achieved=ach, frac=ach / HBM_PEAK_GBS, traffic=tr,
+                    kernel="every aggregation launch of one pass: " + " + ".join(
+                        f"{stats[t]['launches_per_pass']:g} x {KERNELS[t][0]}" for t in order),
+                    unit_of_work="one pass (achieved and traffic: bytes per pass)",
+                    bytes_per_pass=bytes_pass, kernel_ms_per_pass=ms_pass,
+                    share_of_step=ms_pass / ms_step,
+                    pass_frac=bytes_pass / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    dominant=order[0], traffic_src=traffic_src)
+        for t in order:
             o = stats[t]
             roof.update({f"frac_{t}": o["achieved"] / HBM_PEAK_GBS, f"achieved_{t}": o["achieved"],
                          f"launch_ms_{t}": o["launch_ms"], f"launches_{t}": o["launches_timed"],
