@@ -947,6 +947,306 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_kernel(
     step(row0, n_dst);
 }
 
+// ---- the same launch with each step's row heads prefetched one step ahead ------------
+// The kernel above spends 64 % of its wave cycles parked on s_waitcnt (DESIGN.md §9 item
+// 8): every step of 2 rows opens with two dependent round trips — indptr, then the first
+// indices of both relations — before the first source row can be requested.  Here a wave
+// knows its NEXT row pair while it works on the current one (the static walk, or the row
+// queue's chunk / next ticket), so during step i it
+//   * loads step i+1's bounds (indptr of both relations) into registers right at the start
+//     (they arrive under step i's gathers) and parks them in its LDS area, and
+//   * DMAs step i+1's first 48 indices of every (row, relation) straight into LDS with
+//     global_load_lds (no registers live across the matvec: the earlier register-carried
+//     form spilled to scratch and ran at 73 ms),
+// so step i+1 starts gathering immediately from LDS-resident heads.  A row's later index
+// windows (past 48 edges) load as before.  Summation order per row is unchanged: the
+// aggregate bits equal the kernel above (and spmm_csr_kernel's).
+// LDS: 2 x 64 KiB weights + 16 KiB self-row slots + 16 waves x (4 x 192 B index windows +
+// 48 B bounds) = 156.75 KiB of the CU's 160.
+constexpr int kP2Win = 48;  // prefetched indices per (row, relation)
+
+__device__ __forceinline__ void dma4(const int32_t* src, int32_t* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+#endif
+}
+
+// the row pairs of one wave, in order: the static grid-stride walk, or the row queue's chunks
+struct PairWalk {
+  RqCursor c;
+  int64_t pos, c1;
+  bool queued;
+};
+
+__device__ __forceinline__ bool walk_next(PairWalk& w, unsigned* rq, int64_t n_dst, int rq_ch,
+                                          int64_t stride, int64_t& row0, int64_t& lim) {
+  if (!w.queued) {
+    if (w.pos >= n_dst) return false;
+    row0 = w.pos;
+    lim = n_dst;
+    w.pos += stride;
+    return true;
+  }
+  if (w.pos >= w.c1) {
+    int64_t r0, r1;
+    if (!rq_next(w.c, rq, n_dst, rq_ch, r0, r1)) return false;
+    w.pos = r0;
+    w.c1 = r1;
+  }
+  row0 = w.pos;
+  lim = w.c1;
+  w.pos += kPRows;
+  return true;
+}
+
+template <bool WA, bool WB>
+__global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
+    PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
+    const float* __restrict__ WaT, const float* __restrict__ WbT,
+    const float* __restrict__ bias_a, const float* __restrict__ bias_b, int64_t n_dst,
+    int epilogue, int combine, const float* __restrict__ attn_vec, float out_div,
+    float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
+  __shared__ float Wa[kPD * kPD];
+  __shared__ float Wb[kPD * kPD];
+  __shared__ float slots[kP2Waves][kPRows][kPD];
+  __shared__ int32_t win[kP2Waves][2][kPRows][kP2Win];  // [wave][relation][row] first indices
+  __shared__ int64_t bnd[kP2Waves][2][kPRows + 1];      // [wave][relation] row bounds
+  for (int i = threadIdx.x; i < kPD * kPD / 4; i += kP2Waves * 64) {
+    reinterpret_cast<float4*>(Wa)[i] = reinterpret_cast<const float4*>(WaT)[i];
+    reinterpret_cast<float4*>(Wb)[i] = reinterpret_cast<const float4*>(WbT)[i];
+  }
+  __syncthreads();
+
+  constexpr int LPR = 32, VEC = 4, U = GNNREC_SPP2_U, NPI = kWave / LPR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int grp = lane / LPR;
+  const int col = (lane % LPR) * VEC;
+  const int j0 = 2 * lane;
+  const bool relu = epilogue & GNNREC_EPI_RELU;
+  const bool l2 = epilogue & GNNREC_EPI_L2NORM;
+  const int64_t stride = (int64_t)gridDim.x * kP2Waves * kPRows;
+  const float ba0 = bias_a ? bias_a[j0] : 0.f, ba1 = bias_a ? bias_a[j0 + 1] : 0.f;
+  const float bb0 = bias_b ? bias_b[j0] : 0.f, bb1 = bias_b ? bias_b[j0 + 1] : 0.f;
+  const float ca0 = ra.bias_ne ? ra.bias_ne[j0] : 0.f, ca1 = ra.bias_ne ? ra.bias_ne[j0 + 1] : 0.f;
+  const float cb0 = rb.bias_ne ? rb.bias_ne[j0] : 0.f, cb1 = rb.bias_ne ? rb.bias_ne[j0 + 1] : 0.f;
+  const float at0 = attn_vec ? attn_vec[j0] : 0.f, at1 = attn_vec ? attn_vec[j0 + 1] : 0.f;
+
+  // bounds of rows [row0, row0 + nv) of both relations: lanes 0..nv hold relation a's,
+  // lanes 32..32+nv relation b's (one load instruction each, no wait)
+  auto load_bounds = [&](int64_t row0, int nv) __attribute__((always_inline)) {
+    const int l = lane & 31;
+    const int64_t* ip = lane < 32 ? ra.indptr : rb.indptr;
+    return l <= nv ? ld_stream(ip + row0 + l) : (int64_t)0;
+  };
+  // park them in LDS and DMA the first kP2Win indices of every (row, relation)
+  auto stage_heads = [&](int64_t bv, int nv) __attribute__((always_inline)) {
+    int64_t ba[kPRows + 1], bb[kPRows + 1];
+#pragma unroll
+    for (int i = 0; i <= kPRows; ++i) {
+      ba[i] = __shfl(bv, i <= nv ? i : nv);
+      bb[i] = __shfl(bv, 32 + (i <= nv ? i : nv));
+    }
+    if (lane <= kPRows) {
+      bnd[wave][0][lane] = ba[lane <= nv ? lane : nv];
+      bnd[wave][1][lane] = bb[lane <= nv ? lane : nv];
+    }
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      if (i < nv) {
+        if (lane < ba[i + 1] - ba[i] && lane < kP2Win)
+          dma4(ra.indices + ba[i] + lane, &win[wave][0][i][0]);
+        if (lane < bb[i + 1] - bb[i] && lane < kP2Win)
+          dma4(rb.indices + bb[i] + lane, &win[wave][1][i][0]);
+      }
+    }
+  };
+  // relation r's aggregate of row i (bounds beg, end; its first kP2Win indices in LDS)
+  auto gather_row = [&](const PreRel& r, auto weighted, int64_t beg, int64_t end,
+                        int pre_idx, Frag<VEC>& acc) __attribute__((always_inline)) {
+    constexpr bool W = decltype(weighted)::value;
+    int64_t base = beg;
+    int wlen = kP2Win;
+    while (base < end) {
+      const int cnt = (int)((end - base) < wlen ? (end - base) : wlen);
+      const int myidx = base == beg ? pre_idx : (lane < cnt ? ld_stream(r.indices + base + lane) : 0);
+      float myw = 0.f;
+      if constexpr (W) myw = lane < cnt ? ld_stream(r.ew + base + lane) : 0.f;
+      for (int j = 0; j < cnt; j += NPI * U) {
+        Frag<VEC> val[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = j + u * NPI + grp;
+          ok[u] = k < cnt;
+          const int src = __shfl(myidx, k & 63);
+          if (ok[u]) {
+            load_frag<VEC>(val[u], r.Y + (int64_t)src * r.ldy + col);
+          } else {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float w = 1.f;
+          if constexpr (W) w = __shfl(myw, (j + u * NPI + grp) & 63);
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc.v[v] += W ? val[u].v[v] * w : val[u].v[v];
+        }
+      }
+      base += wlen;
+      wlen = 64;
+    }
+  };
+  // the reduced fragment of a relation's row -> this lane's two output columns
+  auto finish_rel = [&](const PreRel& r, Frag<VEC>& acc, int64_t deg, float (&g)[2])
+      __attribute__((always_inline)) {
+    combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc);
+    if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc, deg, 0);
+    const int sl = lane >> 1;
+    const float x0 = __shfl(acc.v[0], sl), x1 = __shfl(acc.v[1], sl);
+    const float x2 = __shfl(acc.v[2], sl), x3 = __shfl(acc.v[3], sl);
+    g[0] = (lane & 1) ? x2 : x0;
+    g[1] = (lane & 1) ? x3 : x1;
+  };
+
+  PairWalk walk;
+  walk.queued = rq != nullptr;
+  walk.pos = ((int64_t)blockIdx.x * kP2Waves + wave) * kPRows;
+  walk.c1 = 0;
+  if (walk.queued) rq_begin(walk.c, rq);
+  int64_t row0, lim;
+  bool have = walk_next(walk, rq, n_dst, rq_ch, stride, row0, lim);
+  if (have) {  // prologue: the first step's heads, synchronously
+    const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);
+    stage_heads(load_bounds(row0, nv), nv);
+  }
+  while (have) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // heads DMA'd and parked
+    const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);  // valid rows, >= 1
+    int64_t rba[kPRows + 1], rbb[kPRows + 1];
+    int pa[kPRows], pb[kPRows];
+#pragma unroll
+    for (int i = 0; i <= kPRows; ++i) {
+      rba[i] = bnd[wave][0][i];
+      rbb[i] = bnd[wave][1][i];
+    }
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      pa[i] = lane < kP2Win ? win[wave][0][i][lane] : 0;
+      pb[i] = lane < kP2Win ? win[wave][1][i][lane] : 0;
+    }
+    // the next step's bounds, in flight under this step's gathers
+    int64_t nrow0 = 0, nlim = 0;
+    const bool next = walk_next(walk, rq, n_dst, rq_ch, stride, nrow0, nlim);
+    const int nnv = next ? (int)(nlim - nrow0 < kPRows ? nlim - nrow0 : kPRows) : 0;
+    const int64_t nbv = next ? load_bounds(nrow0, nnv) : 0;
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {  // self rows into this wave's slots
+      const float4 hs = i < nv && grp == 0 ? ld_stream4(H + (row0 + i) * ldh + col)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (grp == 0) *reinterpret_cast<float4*>(&slots[wave][i][col]) = hs;
+    }
+    float ga[kPRows][2], gb[kPRows][2];
+    bool nea[kPRows], neb[kPRows];
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
+      const int64_t deg = i < nv ? rba[i + 1] - rba[i] : 0;
+      if (i < nv) gather_row(ra, std::integral_constant<bool, WA>{}, rba[i], rba[i + 1], pa[i], acc);
+      finish_rel(ra, acc, deg, ga[i]);
+      nea[i] = deg > 0;
+    }
+    // this step's index windows are in registers (pa / pb): the next step's land in LDS
+    if (next) stage_heads(nbv, nnv);
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      Frag<VEC> acc;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
+      const int64_t deg = i < nv ? rbb[i + 1] - rbb[i] : 0;
+      if (i < nv) gather_row(rb, std::integral_constant<bool, WB>{}, rbb[i], rbb[i + 1], pb[i], acc);
+      finish_rel(rb, acc, deg, gb[i]);
+      neb[i] = deg > 0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    float za[kPRows][2], zb[kPRows][2];
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      za[i][0] = ba0 + (nea[i] ? ca0 : 0.f);
+      za[i][1] = ba1 + (nea[i] ? ca1 : 0.f);
+      zb[i][0] = bb0 + (neb[i] ? cb0 : 0.f);
+      zb[i][1] = bb1 + (neb[i] ? cb1 : 0.f);
+    }
+#pragma unroll 2
+    for (int k = 0; k < kPD; k += 4) {
+      float4 s4[kPRows];
+#pragma unroll
+      for (int i = 0; i < kPRows; ++i) s4[i] = *reinterpret_cast<const float4*>(&slots[wave][i][k]);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float2 wa = *reinterpret_cast<const float2*>(&Wa[(k + kk) * kPD + j0]);
+        const float2 wb = *reinterpret_cast<const float2*>(&Wb[(k + kk) * kPD + j0]);
+#pragma unroll
+        for (int i = 0; i < kPRows; ++i) {
+          const float sv = kk == 0 ? s4[i].x : kk == 1 ? s4[i].y : kk == 2 ? s4[i].z : s4[i].w;
+          za[i][0] = fmaf(sv, wa.x, za[i][0]);
+          za[i][1] = fmaf(sv, wa.y, za[i][1]);
+          zb[i][0] = fmaf(sv, wb.x, zb[i][0]);
+          zb[i][1] = fmaf(sv, wb.y, zb[i][1]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free for the next rows
+
+#pragma unroll
+    for (int i = 0; i < kPRows; ++i) {
+      float ya0 = za[i][0] + ga[i][0], ya1 = za[i][1] + ga[i][1];
+      float yb0 = zb[i][0] + gb[i][0], yb1 = zb[i][1] + gb[i][1];
+      activate(relu, l2, ya0, ya1);
+      activate(relu, l2, yb0, yb1);
+      float y0, y1;
+      if (combine == GNNREC_ACC_MAX) {
+        y0 = fmaxf(ya0, yb0);
+        y1 = fmaxf(ya1, yb1);
+      } else if (combine == GNNREC_ACC_ATTN_LAST) {
+        float sa = ya0 * at0 + ya1 * at1, sb = yb0 * at0 + yb1 * at1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          sa += __shfl_xor(sa, off);
+          sb += __shfl_xor(sb, off);
+        }
+        const float mnew = fmaxf(sa, sb);
+        const float keep = expf(sa - mnew), cnew = expf(sb - mnew);
+        const float nrm = 1.f / (1.f * keep + cnew);
+        y0 = ya0 * keep + yb0 * cnew;
+        y1 = ya1 * keep + yb1 * cnew;
+        y0 *= nrm;
+        y1 *= nrm;
+      } else {
+        y0 = ya0 + yb0;
+        y1 = ya1 + yb1;
+      }
+      if (out_div > 0.f) {
+        y0 = y0 / out_div;
+        y1 = y1 / out_div;
+      }
+      if (i < nv) {
+        typedef float f32x2s __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(f32x2s{y0, y1},
+                                    reinterpret_cast<f32x2s*>(out + (row0 + i) * ldo + j0));
+      }
+    }
+    row0 = nrow0;
+    lim = nlim;
+    have = next;
+  }
+  if (rq != nullptr) rq_finish(rq);
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -998,10 +1298,22 @@ extern "C" int gnnrec_spmm_project2_f32(
                  reduce_a == GNNREC_REDUCE_MEAN};
   const PreRel b{indptr_b, indices_b, ew_b, Yb, ldyb, bias_nonempty_b,
                  reduce_b == GNNREC_REDUCE_MEAN};
+  // GNNREC_SPP2_PIPE=0: the kernel without the one-step-ahead heads (A/B)
+  static const bool pipe = [] {
+    const char* e = getenv("GNNREC_SPP2_PIPE");
+    return !(e && e[0] == '0');
+  }();
 #define GNNREC_SPP2(WA_, WB_)                                                                  \
-  hipLaunchKernelGGL((spmm_project2_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,       \
-                     W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine, attn_vec,  \
-                     out_div, out, ldo, rq, rq_ch)
+  do {                                                                                         \
+    if (pipe)                                                                                  \
+      hipLaunchKernelGGL((spmm_project2_pipe_kernel<WA_, WB_>), grid, block, 0, s, a, b, H,    \
+                         ldh, W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,  \
+                         attn_vec, out_div, out, ldo, rq, rq_ch);                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((spmm_project2_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,   \
+                         W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,       \
+                         attn_vec, out_div, out, ldo, rq, rq_ch);                              \
+  } while (0)
   if (ew_a) {
     if (ew_b) GNNREC_SPP2(true, true);
     else GNNREC_SPP2(true, false);
