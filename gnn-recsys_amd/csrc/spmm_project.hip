@@ -1159,7 +1159,9 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
       finish_rel(ra, acc, deg, ga[i]);
       nea[i] = deg > 0;
     }
-    // this step's index windows are in registers (pa / pb): the next step's land in LDS
+    // this step's index windows are in registers (pa / pb; their LDS reads retired): the
+    // next step's land in LDS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (next) stage_heads(nbv, nnv);
 #pragma unroll
     for (int i = 0; i < kPRows; ++i) {
