@@ -98,6 +98,34 @@ void oracle_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const fl
   }
 }
 
+/* The same sum / mean with a double accumulator per row (rounded to fp32 once, after the
+ * mean): the exact-arithmetic yardstick for rows so heavy that the sequential fp32 running
+ * sum above stagnates (a Zipf head item with ~35M in-edges of post-ReLU, norm-1 rows: the
+ * running sum reaches ~1e6, whose fp32 ulp exceeds the terms' own size). */
+void oracle_spmm_csr_f64acc(const int64_t* indptr, const int32_t* indices, const float* ew,
+                            const float* X, int64_t ldx, int64_t n_dst, int64_t d, int mean,
+                            float* out, int64_t ldo) {
+#pragma omp parallel
+  {
+    double* acc = (double*)malloc((size_t)d * sizeof(double));
+#pragma omp for schedule(dynamic, 256)
+    for (int64_t v = 0; v < n_dst; ++v) {
+      const int64_t beg = indptr[v], end = indptr[v + 1];
+      for (int64_t c = 0; c < d; ++c) acc[c] = 0.0;
+      for (int64_t e = beg; e < end; ++e) {
+        const float* x = X + (int64_t)indices[e] * ldx;
+        const double w = ew ? (double)ew[e] : 1.0;
+        for (int64_t c = 0; c < d; ++c) acc[c] += (double)x[c] * w;
+      }
+      const int64_t deg = end - beg;
+      const double dd = mean ? (double)(deg > 0 ? deg : 1) : 1.0;
+      float* o = out + v * ldo;
+      for (int64_t c = 0; c < d; ++c) o[c] = (float)(acc[c] / dd);
+    }
+    free(acc);
+  }
+}
+
 void oracle_synth_edges(uint64_t seed, int64_t e0, int64_t n, int64_t n_u, int64_t n_i,
                         const double* cdf, int32_t* u, int32_t* it) {
 #pragma omp parallel for schedule(static)

@@ -30,6 +30,7 @@ structurally instead.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -55,6 +56,8 @@ def lib():
         P, I64, U64, INT = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
         L.oracle_spmm_csr_f32.argtypes = [P, P, P, P, I64, I64, I64, INT, P, I64]
         L.oracle_spmm_csr_f32.restype = None
+        L.oracle_spmm_csr_f64acc.argtypes = [P, P, P, P, I64, I64, I64, INT, P, I64]
+        L.oracle_spmm_csr_f64acc.restype = None
         L.oracle_synth_edges.argtypes = [U64, I64, I64, I64, I64, P, P, P]
         L.oracle_synth_edges.restype = None
         L.oracle_sample_count.argtypes = [P, P, P, P, I64, I64, U64, P]
@@ -127,8 +130,25 @@ class Graph:
 
 
 # ------------------------------------------------------------------- ops ----
+# "f32": DGL 0.5.2's CPU SpMM arithmetic (sequential fp32 running sum per row); "f64": the
+# same sums with a double accumulator, the exact-arithmetic yardstick (accumulate_f64()).
+ACCUMULATE = "f32"
+
+
+@contextlib.contextmanager
+def accumulate_f64():
+    """sum / mean aggregations inside the block accumulate in double (see ACCUMULATE)."""
+    global ACCUMULATE
+    old, ACCUMULATE = ACCUMULATE, "f64"
+    try:
+        yield
+    finally:
+        ACCUMULATE = old
+
+
 def spmm_csr(indptr, indices, X, reduce: str, ew=None) -> np.ndarray:
-    """DGL 0.5.2 CPU SpMM (fp32 accumulator, sequential neighbour order)."""
+    """DGL 0.5.2 CPU SpMM (fp32 accumulator, sequential neighbour order); inside
+    accumulate_f64() sum / mean use a double accumulator instead."""
     X = np.ascontiguousarray(X, np.float32)
     indptr = np.ascontiguousarray(indptr, np.int64)
     indices = np.ascontiguousarray(indices, np.int32)
@@ -138,6 +158,10 @@ def spmm_csr(indptr, indices, X, reduce: str, ew=None) -> np.ndarray:
     if ew is not None:
         ew = np.ascontiguousarray(ew, np.float32)
     red = {"sum": 0, "mean": 1, "max": 2}[reduce]
+    if ACCUMULATE == "f64" and red != 2:
+        lib().oracle_spmm_csr_f64acc(_p(indptr), _p(indices), _p(ew), _p(X), d, n_dst, d, red,
+                                     _p(out), d)
+        return out
     lib().oracle_spmm_csr_f32(_p(indptr), _p(indices), _p(ew), _p(X), d, n_dst, d, red, _p(out), d)
     return out
 
