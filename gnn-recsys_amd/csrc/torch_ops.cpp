@@ -686,6 +686,183 @@ void csr_build(const Tensor& src, const Tensor& dst, int64_t n_dst, Tensor& ws, 
      "gnnrec_csr_build");
 }
 
+// ---------------------------------------------------------------- f2 fused relation
+// One ConvLayer relation of a TRAINING step (sum / mean aggregation), forward and backward
+// each as ONE dispatcher call that issues every launch from C++ (gnnrec/autograd.py
+// SageRelFn): the per-launch Python wrappers and the second autograd node per relation were
+// most of the C2 step's host time (profiles/r03_c2_step_probe.txt).  Same kernels, same
+// order, same values as SpmmFn + SageProjectFn.
+//   forward:  agg = spmm(indptr, indices, m, reduce, ew); z = norm?(relu(h_self[:M] Wsᵀ +
+//             agg Wnᵀ)) with the row norms kept (norm, N <= 256) -> (z, agg, row_norm)
+//   backward: gu = the ReLU / norm Jacobian applied to gz; g_self = gu Ws (whole table,
+//             zero past M); g_m = transposed gather of gu Wn over the source-major CSR (the
+//             mean's 1/deg folded into the edge weights); g_Ws = guᵀ h_self; g_Wn = guᵀ agg
+namespace {
+constexpr int64_t kSplit = 2048;  // ops.DEFAULT_SPLIT: heavy rows of the transposed gather
+
+float* pw(const Tensor& t) { return t.defined() ? p<float>(t) : nullptr; }
+
+Tensor gemm_nt(const Tensor& A, const Tensor& W, const Tensor* A2, const Tensor* W2, int epi,
+               Tensor out, Tensor* row_norm) {
+  const int64_t M = A.size(0), K1 = A.size(1), N = W.size(0);
+  const int64_t K2 = A2 ? A2->size(1) : 0;
+  ck(gnnrec_gemm_rownorm_f32(p<float>(A), ld(A, "A"), K1, p<float>(W), A2 ? p<float>(*A2) : nullptr,
+                             A2 ? ld(*A2, "A2") : 1, K2, W2 ? p<float>(*W2) : nullptr, nullptr,
+                             GNNREC_A2_NONE, nullptr, nullptr, M, N, epi, GNNREC_ACC_STORE, 0.f,
+                             nullptr, nullptr, p<float>(out), ld(out, "out"),
+                             row_norm ? p<float>(*row_norm) : nullptr, stream_of(A)),
+     "gnnrec_gemm_f32");
+  return out;
+}
+
+Tensor weight_grad(const Tensor& gu, const Tensor& X) {  // guᵀ X, split-K MFMA
+  const int64_t K = gu.size(0), M = gu.size(1), N = X.size(1);
+  Tensor out = at::empty({M, N}, gu.options());
+  const int64_t wsb = gnnrec_gemm_tn_workspace_bytes(K, M, N);
+  Tensor ws = at::empty({std::max<int64_t>(wsb / 4, 1)}, gu.options());
+  ck(gnnrec_gemm_tn_bias_f32(p<float>(gu), ld(gu, "gu"), p<float>(X), ld(X, "X"), K, M, N,
+                             p<float>(out), ld(out, "out"), nullptr, 0, p<float>(ws),
+                             stream_of(gu)),
+     "gnnrec_gemm_tn_bias_f32");
+  return out;
+}
+
+// sum gather of X over a CSR whose edge count is known on the host but whose degrees are
+// not (the transposed block): heavy rows planned on the device, as ops.spmm does
+void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const Tensor& X,
+                    int64_t nnz, Tensor& out) {
+  const int64_t n = ip.numel() - 1, d = X.size(1);
+  const int64_t cap_h = std::min<int64_t>(n, nnz / (kSplit + 1));
+  void* s = stream_of(X);
+  if (cap_h <= 0) {
+    ck(gnnrec_spmm_csr_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X), ld(X, "X"), n, d,
+                           GNNREC_REDUCE_SUM, 0, p<float>(out), ld(out, "out"), s),
+       "gnnrec_spmm_csr_f32");
+    return;
+  }
+  const int64_t cap_c = nnz / kSplit + cap_h;
+  Tensor plan = at::empty({2 + cap_h + cap_h + 1 + cap_c}, ip.options());
+  ck(gnnrec_spmm_plan_build(p<int64_t>(ip), n, kSplit, cap_h, p<int64_t>(plan), s),
+     "gnnrec_spmm_plan_build");
+  Tensor wsp = at::empty({cap_c, d}, X.options());
+  ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),
+                                 ld(X, "X"), n, d, GNNREC_REDUCE_SUM, 0, p<float>(out),
+                                 ld(out, "out"), kSplit, p<int64_t>(plan), cap_h, cap_c,
+                                 p<float>(wsp), s),
+     "gnnrec_spmm_csr_planned_f32");
+}
+}  // namespace
+
+std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tensor& h_self,
+                                                    int64_t n_self, const Tensor& Ws,
+                                                    const Tensor& Wn, const Tensor& indptr,
+                                                    const Tensor& indices,
+                                                    const optional<Tensor>& ew, int64_t reduce,
+                                                    bool norm) {
+  const OneDevice one_device_;
+  dev(m, "m", at::kFloat);
+  dev(h_self, "h_self", at::kFloat);
+  dev(Ws, "W_self", at::kFloat);
+  dev(Wn, "W_neigh", at::kFloat);
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(ew, "edge_weight", at::kFloat);
+  TORCH_CHECK_VALUE(reduce == GNNREC_REDUCE_SUM || reduce == GNNREC_REDUCE_MEAN,
+                    "sage_rel_forward: sum or mean");
+  const int64_t M = indptr.numel() - 1, N = Ws.size(0);
+  TORCH_CHECK_VALUE(N <= 256 || !norm, "sage_rel_forward: the row norm needs N <= 256");
+  TORCH_CHECK_VALUE(h_self.size(0) >= M && (n_self == 0 || n_self == M),
+                    "sage_rel_forward: h_self must hold the ", M, " destination rows first");
+  TORCH_CHECK_VALUE(Wn.size(0) == N && Ws.size(1) == h_self.size(1) && Wn.size(1) == m.size(1),
+                    "sage_rel_forward: weight shapes");
+  const Tensor X = m.contiguous(), H = h_self.narrow(0, 0, M).contiguous();
+  const optional<Tensor> ewc = has(ew) ? optional<Tensor>(ew->contiguous()) : ew;
+  const Tensor Wsc = Ws.contiguous(), Wnc = Wn.contiguous();
+  Tensor agg = at::empty({M, m.size(1)}, m.options());
+  Tensor z = at::empty({M, N}, m.options());
+  Tensor nrm = norm ? at::empty({M}, m.options()) : at::empty({0}, m.options());
+  if (meta(m)) return {z, agg, nrm};
+  const c10::DeviceGuard g(m.device());
+  ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), p<float>(X),
+                         ld(X, "m"), M, X.size(1), (int)reduce, 0, p<float>(agg), ld(agg, "agg"),
+                         stream_of(m)),
+     "gnnrec_spmm_csr_f32");
+  gemm_nt(H, Wsc, &agg, &Wnc, GNNREC_EPI_RELU | (norm ? GNNREC_EPI_L2NORM : 0), z,
+          norm ? &nrm : nullptr);
+  return {z, agg, nrm};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
+    const Tensor& gz_in, const Tensor& z, const Tensor& row_norm, const Tensor& h_self,
+    const Tensor& agg, const Tensor& Ws, const Tensor& Wn, const Tensor& indptr,
+    const Tensor& indices, const optional<Tensor>& ew, int64_t reduce, int64_t n_src,
+    int64_t nnz, bool norm, int64_t need) {
+  const OneDevice one_device_;
+  dev(gz_in, "gz", at::kFloat);
+  dev(z, "z", at::kFloat);
+  dev(h_self, "h_self", at::kFloat);
+  dev(agg, "agg", at::kFloat);
+  dev(Ws, "W_self", at::kFloat);
+  dev(Wn, "W_neigh", at::kFloat);
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(ew, "edge_weight", at::kFloat);
+  const int64_t M = z.size(0), N = z.size(1);
+  TORCH_CHECK_VALUE(gz_in.sizes() == z.sizes() && agg.size(0) == M && h_self.size(0) >= M &&
+                        indptr.numel() == M + 1 && (!norm || row_norm.numel() == M),
+                    "sage_rel_backward: shapes");
+  const Tensor gz = gz_in.contiguous();
+  Tensor none = at::empty({0}, z.options());  // outputs not asked for (`need` bits)
+  Tensor g_self = none, g_m = none, g_Ws = none, g_Wn = none;
+  if (meta(z)) {
+    if (need & 1) g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
+    if (need & 2) g_m = at::empty({n_src, Wn.size(1)}, z.options());
+    if (need & 4) g_Ws = at::empty_like(Ws);
+    if (need & 8) g_Wn = at::empty_like(Wn);
+    return {g_self, g_m, g_Ws, g_Wn};
+  }
+  const c10::DeviceGuard g(z.device());
+  void* s = stream_of(z);
+  Tensor gu = at::empty({M, N}, z.options());
+  if (norm) {
+    dev(row_norm, "row_norm", at::kFloat);
+    ck(gnnrec_act_backward_normed_f32(p<float>(z), ld(z, "z"), p<float>(row_norm), p<float>(gz),
+                                      ld(gz, "gz"), M, N, 1, p<float>(gu), N, s),
+       "gnnrec_act_backward_normed_f32");
+  } else {  // z = relu(u): the same mask
+    ck(gnnrec_act_backward_f32(p<float>(z), ld(z, "z"), p<float>(gz), ld(gz, "gz"), M, N,
+                               GNNREC_EPI_RELU, p<float>(gu), N, s),
+       "gnnrec_act_backward_f32");
+  }
+  if (need & 1) {  // gu Ws over the whole source table of the dst type (zero past M)
+    g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
+    Tensor head = g_self.narrow(0, 0, M);
+    gemm_nt(gu, Ws.t().contiguous(), nullptr, nullptr, 0, head, nullptr);
+    if (h_self.size(0) > M) g_self.narrow(0, M, h_self.size(0) - M).zero_();
+  }
+  if (need & 2) {  // transposed gather of g_agg = gu Wn (DGL: the backward of a gSpMM)
+    Tensor g_agg = at::empty({M, Wn.size(1)}, z.options());
+    gemm_nt(gu, Wn.t().contiguous(), nullptr, nullptr, 0, g_agg, nullptr);
+    const bool mean = reduce == GNNREC_REDUCE_MEAN;
+    Tensor ip_t = at::empty({n_src + 1}, indptr.options());
+    Tensor ix_t = at::empty({std::max<int64_t>(nnz, 1)}, indices.options());
+    Tensor w_t;
+    if (has(ew) || mean) w_t = at::empty({std::max<int64_t>(nnz, 1)}, z.options());
+    const size_t wsb = gnnrec_csr_transpose_workspace_bytes(nnz, n_src);
+    Tensor ws = at::empty({(int64_t)std::max<size_t>(wsb, 1)}, indptr.options().dtype(at::kByte));
+    const optional<Tensor> ewc = has(ew) ? optional<Tensor>(ew->contiguous()) : ew;
+    ck(gnnrec_csr_transpose(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), M, n_src, nnz,
+                            (int)mean, ws.data_ptr(), ws.nbytes(), p<int64_t>(ip_t),
+                            p<int32_t>(ix_t), pw(w_t), s),
+       "gnnrec_csr_transpose");
+    g_m = at::empty({n_src, Wn.size(1)}, z.options());
+    gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m);
+  }
+  if (need & 4) g_Ws = weight_grad(gu, h_self.narrow(0, 0, M).contiguous());
+  if (need & 8) g_Wn = weight_grad(gu, agg.contiguous());
+  return {g_self, g_m, g_Ws, g_Wn};
+}
+
 // K10 membership: has_edges_between over a source-sorted in-CSR
 void csr_has_edges(const Tensor& indptr, const Tensor& sorted_indices, int64_t n_src, const Tensor& u,
                const Tensor& v, Tensor& out) {
@@ -1131,6 +1308,13 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
   m.def("csr_has_edges(Tensor indptr, Tensor sorted_indices, int n_src, Tensor u, Tensor v, "
         "Tensor(a!) out) -> ()");
+  m.def("sage_rel_forward(Tensor m, Tensor h_self, int n_self, Tensor W_self, Tensor W_neigh, "
+        "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
+        "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
+        "int reduce, int n_src, int nnz, bool norm, int need) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("margin_loss(Tensor pos, Tensor neg, int K, float delta, Tensor? mask, Tensor? recency, "
         "Tensor(a!) g_pos, Tensor(b!) g_neg, Tensor(c!) partial) -> ()");
   m.def("sum_scaled(Tensor x, float scale, Tensor(a!) out) -> ()");
@@ -1192,6 +1376,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("lstm_step", &lstm_step);                       \
   m.impl("gather_rows", &gather_rows);                   \
   m.impl("csr_has_edges", &csr_has_edges);               \
+  m.impl("sage_rel_forward", &sage_rel_forward);         \
+  m.impl("sage_rel_backward", &sage_rel_backward);       \
   m.impl("margin_loss", &margin_loss);                   \
   m.impl("sum_scaled", &sum_scaled);                     \
   m.impl("synth_edges", &synth_edges);                   \

@@ -188,6 +188,53 @@ class SageProjectFn(torch.autograd.Function):
         return g_self, g_agg, g_Ws, g_Wn, None, None
 
 
+class SageRelFn(torch.autograd.Function):
+    """One sum / mean ConvLayer relation of a training step — SpmmFn and SageProjectFn as
+    ONE autograd node whose forward and backward are each ONE dispatcher call
+    (torch.ops.gnnrec.sage_rel_forward / sage_rel_backward, csrc/torch_ops.cpp), which issue
+    the same launches as the two-node form from C++: the spmm + projection GEMM (row norms
+    kept), and the epilogue Jacobian, self / neighbour input GEMMs, device CSR transpose +
+    transposed gather, and the two split-K weight-gradient GEMMs.  Same values bit for bit;
+    the per-launch Python wrappers and the second node per relation were most of the C2
+    step's host time.  GNNREC_TRAIN_FUSED=0 keeps the two-node form."""
+
+    @staticmethod
+    def forward(ctx, m, h_self, Ws, Wn, indptr, indices, ew, reduce: str, norm: bool,
+                n_self: int = 0):
+        z, agg, nrm = ops._T().sage_rel_forward(m, h_self, n_self, Ws.detach(), Wn.detach(),
+                                                indptr, indices, ew, ops.REDUCE[reduce],
+                                                bool(norm))
+        ctx.save_for_backward(h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew)
+        ctx.reduce, ctx.norm, ctx.n_src = reduce, bool(norm), m.shape[0]
+        ctx.nnz = ops._nnz(indptr)  # sampled blocks carry it: no readback
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        mask = (1 if need[1] else 0) | (2 if need[0] else 0) | (4 if need[2] else 0) | \
+            (8 if need[3] else 0)
+        g_self, g_m, g_Ws, g_Wn = ops._T().sage_rel_backward(
+            gz, z, nrm, h_self, agg, Ws.detach(), Wn.detach(), indptr, indices, ew,
+            ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask)
+        return (g_m if need[0] else None, g_self if need[1] else None,
+                g_Ws if need[2] else None, g_Wn if need[3] else None,
+                None, None, None, None, None, None)
+
+
+def sage_rel_fusable(m, h_self, Wn, reduce: str, norm: bool) -> bool:
+    """SageRelFn applies: a linear reduce, fp32 row-major tables, the row norm within one
+    GEMM block (ops.GEMM_ROW_N)."""
+    if os.environ.get("GNNREC_TRAIN_FUSED", "1") == "0" or reduce not in ("sum", "mean") or \
+            os.environ.get("GNNREC_SPMM_BWD") == "atomic":
+        return False
+    if norm and Wn.shape[0] > ops.GEMM_ROW_N:
+        return False
+    return all(t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(-1) == 1
+               for t in (m, h_self))
+
+
 class CosineFn(torch.autograd.Function):
     """cos_e = <ĥs[src_e], ĥd[dst_e]>; forward = gnnrec_sddmm_cos_f32, backward =
     gnnrec_sddmm_cos_backward_f32 (both reduction sides of the SDDMM backward as weighted

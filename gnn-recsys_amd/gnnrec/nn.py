@@ -161,6 +161,11 @@ class ConvLayer(nn.Module):
         if grad:
             m = ag.LinearFn.apply(h_neigh, self.fc_preagg.weight, None, True, False) \
                 if preagg else h_neigh
+            if ag.sage_rel_fusable(m, h_self, self.fc_neigh.weight, reduce, bool(self.norm)):
+                # one autograd node, one C++ call each way (ag.SageRelFn)
+                return ag.SageRelFn.apply(m, h_self, self.fc_self.weight, self.fc_neigh.weight,
+                                          graph.indptr, graph.indices, ew, reduce,
+                                          bool(self.norm), n_self)
             if reduce == 'lstm':
                 L = self.lstm
                 agg = ag.LstmAggFn.apply(m, L.weight_ih_l0, L.weight_hh_l0, L.bias_ih_l0,

@@ -423,3 +423,47 @@ def test_cpp_sample_layer_equals_python_form(fanouts):
                 for x, y in zip(a._rels[ce], b._rels[ce]):
                     assert x.dtype == y.dtype and torch.equal(x, y), ce
                 assert a._rels[ce][0]._gnnrec_nnz == b._rels[ce][0]._gnnrec_nnz
+
+
+@pytest.mark.parametrize("agg,hetero,norm", [("mean", "sum", True), ("mean_edge", "mean", True),
+                                             ("mean_nn_edge", "sum", False),
+                                             ("mean_nn", "attention", True)])
+def test_fused_training_relation_equals_two_node_form(monkeypatch, agg, hetero, norm):
+    """gnnrec.autograd.SageRelFn (one node and one C++ call each way per relation) gives
+    the loss and every parameter gradient of the SpmmFn + SageProjectFn form bit for bit,
+    on sampled blocks (dst-prefix self tables) and on the full graph."""
+    from gnnrec import nn as gnn
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    g, _ = _graph()
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 5, "item": 6, "hidden": 16, "out": 8}, norm, 0.0, agg,
+                          "cos", hetero, True).to(DEV)
+    loader = EdgeDataLoader(g, {BUYS: torch.arange(400)}, MultiLayerNeighborSampler([4, 4]),
+                            exclude="reverse_types",
+                            reverse_etypes={"buys": "bought-by", "bought-by": "buys",
+                                            "clicks": "clicked-by", "clicked-by": "clicks"},
+                            negative_sampler=negative_sampler.Uniform(3), batch_size=64)
+    _, pos_g, neg_g, blocks = next(iter(loader))
+
+    def grads(fused, full_graph):
+        monkeypatch.setenv("GNNREC_TRAIN_FUSED", "1" if fused else "0")
+        model.zero_grad()
+        if full_graph:
+            h = model.embed(g.ndata["features"])
+            for layer in model.layers:
+                h = layer(g, h)
+            loss = sum((v * v).sum() for v in h.values())
+        else:
+            _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+            loss = gnn.max_margin_loss(ps, ns, 0.266, 3)
+        loss.backward()
+        return loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                               if p.grad is not None}
+
+    for full_graph in (False, True):
+        l1, g1 = grads(True, full_graph)
+        l0, g0 = grads(False, full_graph)
+        assert torch.equal(l1, l0)
+        assert g1.keys() == g0.keys() and len(g1) > 0
+        for n in g1:
+            assert torch.equal(g1[n], g0[n]), n

@@ -170,3 +170,19 @@ def test_compile_heterograph_conv_fullgraph():
         out = torch.compile(conv, fullgraph=True, backend="aot_eager")(
             g, {"user": _meta(500, d), "item": _meta(150, d)})
     assert tuple(out["user"].shape) == (500, d) and tuple(out["item"].shape) == (150, d)
+
+
+def test_sage_rel_ops_meta_shapes():
+    """The fused training relation ops (gnnrec/autograd.py SageRelFn) return the forward's
+    (z, agg, row norms) and the backward's four gradients with the right shapes on meta
+    tensors, and refuse a max reduce."""
+    T = _T()
+    M, n_src, E, d, N = 5, 9, 20, 8, 6
+    ip, ix = _meta(M + 1, dtype=torch.int64), _meta(E, dtype=torch.int32)
+    m, hs, Ws, Wn = _meta(n_src, d), _meta(7, d), _meta(N, d), _meta(N, d)
+    z, agg, nrm = T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 1, True)
+    assert tuple(z.shape) == (M, N) and tuple(agg.shape) == (M, d) and tuple(nrm.shape) == (M,)
+    g = T.sage_rel_backward(z, z, nrm, hs, agg, Ws, Wn, ip, ix, None, 1, n_src, E, True, 15)
+    assert [tuple(t.shape) for t in g] == [(7, d), (n_src, d), (N, d), (N, d)]
+    with pytest.raises(ValueError, match="sum or mean"):
+        T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 2, True)
