@@ -61,39 +61,64 @@ int oracle_num_threads(void) {
 #endif
 }
 
+/* Rows with more in-edges than this are reduced one at a time with the feature columns
+ * split across the threads instead of one thread per row: every column still sums its
+ * edges in the same sequential order (bit-identical), but a Zipf head item's tens of
+ * millions of edges no longer run on one core. */
+#define ORACLE_HEAVY_ROW (1 << 20)
+
+static void row_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                    const float* X, int64_t ldx, int64_t v, int64_t c0, int64_t c1, int reduce,
+                    float* out, int64_t ldo);
+
 /* reduce: 0 sum, 1 mean, 2 max */
 void oracle_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
                          const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
                          float* out, int64_t ldo) {
 #pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t v = 0; v < n_dst; ++v)
+    if (indptr[v + 1] - indptr[v] <= ORACLE_HEAVY_ROW)
+      row_f32(indptr, indices, ew, X, ldx, v, 0, d, reduce, out, ldo);
   for (int64_t v = 0; v < n_dst; ++v) {
+    if (indptr[v + 1] - indptr[v] <= ORACLE_HEAVY_ROW) continue;
+#pragma omp parallel for schedule(static, 1)
+    for (int64_t c0 = 0; c0 < d; c0 += 4)
+      row_f32(indptr, indices, ew, X, ldx, v, c0, c0 + 4 < d ? c0 + 4 : d, reduce, out, ldo);
+  }
+}
+
+/* columns [c0, c1) of row v, DGL's SpMMSumCsr / SpMMCmpCsr order: edges in CSR order */
+static void row_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                    const float* X, int64_t ldx, int64_t v, int64_t c0, int64_t c1, int reduce,
+                    float* out, int64_t ldo) {
+  {
     float* o = out + v * ldo;
     const int64_t beg = indptr[v], end = indptr[v + 1];
     if (reduce == 2) {
-      for (int64_t c = 0; c < d; ++c) o[c] = -INFINITY;
+      for (int64_t c = c0; c < c1; ++c) o[c] = -INFINITY;
     } else {
-      for (int64_t c = 0; c < d; ++c) o[c] = 0.f;
+      for (int64_t c = c0; c < c1; ++c) o[c] = 0.f;
     }
     for (int64_t e = beg; e < end; ++e) {
       const float* x = X + (int64_t)indices[e] * ldx;
       const float w = ew ? ew[e] : 1.f;
       if (reduce == 2) {
-        for (int64_t c = 0; c < d; ++c) {
+        for (int64_t c = c0; c < c1; ++c) {
           const float m = ew ? x[c] * w : x[c];
           o[c] = m > o[c] ? m : o[c];
         }
       } else if (ew) {
-        for (int64_t c = 0; c < d; ++c) o[c] += x[c] * w;
+        for (int64_t c = c0; c < c1; ++c) o[c] += x[c] * w;
       } else {
-        for (int64_t c = 0; c < d; ++c) o[c] += x[c];
+        for (int64_t c = c0; c < c1; ++c) o[c] += x[c];
       }
     }
     const int64_t deg = end - beg;
     if (reduce == 1) {
       const float dd = (float)(deg > 0 ? deg : 1);
-      for (int64_t c = 0; c < d; ++c) o[c] = o[c] / dd;
+      for (int64_t c = c0; c < c1; ++c) o[c] = o[c] / dd;
     } else if (reduce == 2 && deg == 0) {
-      for (int64_t c = 0; c < d; ++c) o[c] = 0.f;
+      for (int64_t c = c0; c < c1; ++c) o[c] = 0.f;
     }
   }
 }
@@ -102,27 +127,38 @@ void oracle_spmm_csr_f32(const int64_t* indptr, const int32_t* indices, const fl
  * mean): the exact-arithmetic yardstick for rows so heavy that the sequential fp32 running
  * sum above stagnates (a Zipf head item with ~35M in-edges of post-ReLU, norm-1 rows: the
  * running sum reaches ~1e6, whose fp32 ulp exceeds the terms' own size). */
+static void row_f64(const int64_t* indptr, const int32_t* indices, const float* ew,
+                    const float* X, int64_t ldx, int64_t v, int64_t c0, int64_t c1, int mean,
+                    float* out, int64_t ldo) {
+  double acc[64];
+  for (int64_t cb = c0; cb < c1; cb += 64) {
+    const int64_t ce = cb + 64 < c1 ? cb + 64 : c1;
+    const int64_t beg = indptr[v], end = indptr[v + 1];
+    for (int64_t c = cb; c < ce; ++c) acc[c - cb] = 0.0;
+    for (int64_t e = beg; e < end; ++e) {
+      const float* x = X + (int64_t)indices[e] * ldx;
+      const double w = ew ? (double)ew[e] : 1.0;
+      for (int64_t c = cb; c < ce; ++c) acc[c - cb] += (double)x[c] * w;
+    }
+    const int64_t deg = end - beg;
+    const double dd = mean ? (double)(deg > 0 ? deg : 1) : 1.0;
+    float* o = out + v * ldo;
+    for (int64_t c = cb; c < ce; ++c) o[c] = (float)(acc[c - cb] / dd);
+  }
+}
+
 void oracle_spmm_csr_f64acc(const int64_t* indptr, const int32_t* indices, const float* ew,
                             const float* X, int64_t ldx, int64_t n_dst, int64_t d, int mean,
                             float* out, int64_t ldo) {
-#pragma omp parallel
-  {
-    double* acc = (double*)malloc((size_t)d * sizeof(double));
-#pragma omp for schedule(dynamic, 256)
-    for (int64_t v = 0; v < n_dst; ++v) {
-      const int64_t beg = indptr[v], end = indptr[v + 1];
-      for (int64_t c = 0; c < d; ++c) acc[c] = 0.0;
-      for (int64_t e = beg; e < end; ++e) {
-        const float* x = X + (int64_t)indices[e] * ldx;
-        const double w = ew ? (double)ew[e] : 1.0;
-        for (int64_t c = 0; c < d; ++c) acc[c] += (double)x[c] * w;
-      }
-      const int64_t deg = end - beg;
-      const double dd = mean ? (double)(deg > 0 ? deg : 1) : 1.0;
-      float* o = out + v * ldo;
-      for (int64_t c = 0; c < d; ++c) o[c] = (float)(acc[c] / dd);
-    }
-    free(acc);
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t v = 0; v < n_dst; ++v)
+    if (indptr[v + 1] - indptr[v] <= ORACLE_HEAVY_ROW)
+      row_f64(indptr, indices, ew, X, ldx, v, 0, d, mean, out, ldo);
+  for (int64_t v = 0; v < n_dst; ++v) {  /* heavy rows: columns across the threads */
+    if (indptr[v + 1] - indptr[v] <= ORACLE_HEAVY_ROW) continue;
+#pragma omp parallel for schedule(static, 1)
+    for (int64_t c0 = 0; c0 < d; c0 += 4)
+      row_f64(indptr, indices, ew, X, ldx, v, c0, c0 + 4 < d ? c0 + 4 : d, mean, out, ldo);
   }
 }
 
