@@ -104,9 +104,10 @@ KERNELS = {
     "spmm_tile2": ("spmm_csr2_kernel", "gnnrec spmm_csr2_kernel (gather + segmented sums of two "
                    "relations' source-range tiles from one table in one launch)"),
     "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
-    "spmm_project2": ("spmm_project2_kernel", "gnnrec spmm_project2_kernel (two pre-projected "
-                      "relations' gathers + means into one dst row, both SAGE self projections, "
-                      "ReLU, L2 norm, cross-relation sum)"),
+    "spmm_project2": ("spmm_project2_pipe_kernel", "gnnrec spmm_project2_pipe_kernel (two "
+                      "pre-projected relations' gathers + means into one dst row, both SAGE self "
+                      "projections, ReLU, L2 norm, cross-relation sum; next rows' heads "
+                      "prefetched)"),
 }
 
 
