@@ -244,6 +244,75 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   }
 }
 
+// The common epilogues with their flags known at compile time — FE = bias | relu << 1 |
+// l2norm << 2 (the SAGE projection: ReLU + row norm; fc_preagg: ReLU; NodeEmbedding: bias),
+// store-only, full 128-column tiles, 16-B aligned output — instead of runtime flags in the
+// unrolled value loops (selects per value: the 1M x 256 x 128 GEMM issued 4.8 non-MFMA VALU
+// instructions per MFMA, profiles/r03_gemm_pmc.md).  The row norm divides once per row and
+// scales by the reciprocal.
+template <int BN, int FE>
+__device__ __forceinline__ void gemm_epilogue_fast(const GemmArgs& g, f32x16 (&acc)[BN / 32],
+                                                   float* smem, int64_t m0, int wave, int lane) {
+  constexpr int NT = BN / 32;
+  constexpr bool BIAS = FE & 1, RELU = FE & 2, L2 = FE & 4;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  float bias_t[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bias_t[t] = BIAS ? g.bias[t * 32 + r] : 0.f;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float x = acc[t][v];
+      if constexpr (BIAS) x += bias_t[t];
+      if constexpr (RELU) x = fmaxf(x, 0.f);
+      acc[t][v] = x;
+      if constexpr (L2) ss = fmaf(x, x, ss);
+    }
+    if constexpr (L2) {
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) ss += __shfl_xor(ss, off);
+      const float nrm = sqrtf(ss);
+      if (g.row_norm && r == 0) {
+        const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        if (row < g.M) g.row_norm[row] = nrm;
+      }
+      const float inv = 1.f / (nrm == 0.f ? 1.f : nrm);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][v] *= inv;
+    }
+  }
+  constexpr int SC = stage_cols<BN>();
+  constexpr int OSTR = SC + 4;
+  constexpr int TPR = SC / 32;
+  float* Ot = smem + wave * 32 * OSTR;
+#pragma unroll
+  for (int round = 0; round < NT / TPR; ++round) {
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int rl = (v & 3) + 8 * (v >> 2) + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < TPR; ++tt) Ot[rl * OSTR + tt * 32 + r] = acc[round * TPR + tt][v];
+    }
+    __syncthreads();
+    constexpr int C4 = SC / 4;
+    constexpr int ITER = 32 * C4 / kWave;
+#pragma unroll
+    for (int q = 0; q < ITER; ++q) {
+      const int flat = q * kWave + lane;
+      const int rl = flat / C4;
+      const int c = (flat % C4) * 4;
+      const int64_t row = m0 + wave * 32 + rl;
+      if (row < g.M)
+        *reinterpret_cast<f32x4*>(g.out + row * g.ldo + round * SC + c) =
+            *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+    }
+  }
+}
+
 template <int BN, bool FAST>
 __global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float smem[smem_floats<BN>()];
@@ -527,7 +596,7 @@ constexpr int glds16_waves() {
   return S <= 3 ? 3 : 2;
 }
 
-template <int BN, int S>
+template <int BN, int S, int FE = -1>
 __global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel(GemmArgs g) {
   constexpr int NT = BN / 32;
   constexpr int AI = BM * BK16 * 4 / 1024 / 4;   // A-tile DMA instructions per wave (2)
@@ -569,31 +638,41 @@ __global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel
     w_chk[q] = ((lane & 3) ^ ((R >> 2) & 3)) * 4;
   }
   const int64_t my_row = m0 + wave * 32 + r;
+  // this lane's DMA source pointers of both operand pairs, formed once (a tile adds k0):
+  // the 64-bit row-offset products are not redone per tile
+  const float* pa[2][AI];
+  const float* pw[2][WI];
+#pragma unroll
+  for (int q = 0; q < AI; ++q) {
+    pa[0][q] = g.A1 + a_row[q] * g.lda1 + a_chk[q];
+    pa[1][q] = g.K2 > 0 ? g.A2 + a_row[q] * g.lda2 + a_chk[q] : pa[0][q];
+  }
+#pragma unroll
+  for (int q = 0; q < WI; ++q) {
+    pw[0][q] = g.W1 + w_row[q] * g.K1 + w_chk[q];
+    pw[1][q] = g.K2 > 0 ? g.W2 + w_row[q] * g.K2 + w_chk[q] : pw[0][q];
+  }
 
   // both operand pairs (A1,W1) then (A2,W2) as ONE stream of K tiles, so the DMA of the
   // first A2 tile overlaps the last A1 tile's MFMAs (no pipeline restart between segments)
   const int nk1 = (int)(g.K1 / BK16), nk = nk1 + (int)(g.K2 / BK16);
-  float rowdiv2 = 1.f;
+  // the mean's 1/deg (GNNREC_A2_DIV_DEG): one division per row, then a multiply per operand
+  // (64 IEEE divisions per lane per launch otherwise: half the VALU of the owned-row GEMM)
+  float rowinv2 = 1.f;
   bool rowzero2 = false;
   if (g.K2 > 0 && g.a2_mode != GNNREC_A2_NONE) {
     const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
-    if (g.a2_mode == GNNREC_A2_DIV_DEG) rowdiv2 = (float)(dg > 0 ? dg : 1);
+    if (g.a2_mode == GNNREC_A2_DIV_DEG) rowinv2 = 1.f / (float)(dg > 0 ? dg : 1);
     else rowzero2 = dg == 0;
   }
   auto issue = [&](int kt, int buf) {
-    const bool s2 = kt >= nk1;
-    const float* A = s2 ? g.A2 : g.A1;
-    const float* W = s2 ? g.W2 : g.W1;
-    const int64_t K = s2 ? g.K2 : g.K1;
-    const int64_t lda = s2 ? g.lda2 : g.lda1;
-    const int64_t k0 = (int64_t)(s2 ? kt - nk1 : kt) * BK16;
+    const int s2 = kt >= nk1;
+    const int k0 = (s2 ? kt - nk1 : kt) * BK16;
     float* base = smem + buf * TILE;
 #pragma unroll
-    for (int q = 0; q < AI; ++q)
-      dma16(A + a_row[q] * lda + k0 + a_chk[q], base + (wave * AI + q) * 256);
+    for (int q = 0; q < AI; ++q) dma16(pa[s2][q] + k0, base + (wave * AI + q) * 256);
 #pragma unroll
-    for (int q = 0; q < WI; ++q)
-      dma16(W + w_row[q] * K + k0 + w_chk[q], base + BM * BK16 + (wave * WI + q) * 256);
+    for (int q = 0; q < WI; ++q) dma16(pw[s2][q] + k0, base + BM * BK16 + (wave * WI + q) * 256);
   };
 #pragma unroll
   for (int j = 0; j < S - 1; ++j)
@@ -627,7 +706,7 @@ __global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel
     }
 #pragma unroll
     for (int s4 = 0; s4 < 2; ++s4) {
-      if (divide) a[s4] = a[s4] / rowdiv2;
+      if (divide) a[s4] = a[s4] * rowinv2;
       else if (zero) a[s4] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -637,7 +716,8 @@ __global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer free for reuse
   }
-  gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
+  if constexpr (FE >= 0) gemm_epilogue_fast<BN, FE>(g, acc, smem, m0, wave, lane);
+  else gemm_epilogue<BN>(g, acc, smem, m0, n0, wave, lane);
 }
 
 template <int BN>
@@ -664,6 +744,28 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
         const int x = e ? atoi(e) : 3;
         return x >= 2 && x <= 4 ? x : 3;
       }();
+      // the compile-time epilogue (gemm_epilogue_fast) for the common flag sets:
+      // GNNREC_GEMM_FAST_EPI=0 keeps the runtime-flag epilogue (A/B)
+      static const bool fast_epi = [] {
+        const char* e = getenv("GNNREC_GEMM_FAST_EPI");
+        return !(e && e[0] == '0');
+      }();
+      const bool sig = g.epilogue & GNNREC_EPI_SIGMOID;
+      const int fe = (g.bias ? 1 : 0) | ((g.epilogue & GNNREC_EPI_RELU) ? 2 : 0) |
+                     ((g.epilogue & GNNREC_EPI_L2NORM) ? 4 : 0);
+      if (fast_epi && stages == 3 && !sig && g.accum == GNNREC_ACC_STORE && !g.bias_ne &&
+          g.N == BN && g.vecO && (g.row_norm == nullptr || (fe & 4))) {
+        switch (fe) {
+          case 0: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 0>), grid, dim3(256), 0, s, g); break;
+          case 1: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 1>), grid, dim3(256), 0, s, g); break;
+          case 2: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 2>), grid, dim3(256), 0, s, g); break;
+          case 3: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 3>), grid, dim3(256), 0, s, g); break;
+          case 6: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 6>), grid, dim3(256), 0, s, g); break;
+          case 7: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 7>), grid, dim3(256), 0, s, g); break;
+          default: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3>), grid, dim3(256), 0, s, g);
+        }
+        return check_launch("gnnrec_gemm_f32");
+      }
       if (stages == 2) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 2>), grid, dim3(256), 0, s, g);
       else if (stages == 4) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 4>), grid, dim3(256), 0, s, g);
       else hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3>), grid, dim3(256), 0, s, g);
