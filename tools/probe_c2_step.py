@@ -4,7 +4,10 @@ Times 20 steps of the C2 shape (2 conv layers 'mean' d=64, fanout [10,10], 1024 
 neg, cosine head, Adam) and counts the kernels one step launches (torch profiler-free: a
 rocprofv3 --kernel-trace of this script gives the per-kernel split).
 
-    python tools/probe_c2_step.py [K]
+    python tools/probe_c2_step.py [K] [num_workers]
+
+GNNREC_SWITCH_INTERVAL=<s>: sys.setswitchinterval for the run (the GIL hand-over period
+between the training thread and a prefetching sampler thread).
 """
 import os
 import sys
@@ -20,6 +23,9 @@ from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    nw = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    if os.environ.get("GNNREC_SWITCH_INTERVAL"):
+        sys.setswitchinterval(float(os.environ["GNNREC_SWITCH_INTERVAL"]))
     dev = torch.device("cuda")
     g = c2_graph(64, dev)
     torch.manual_seed(0)
@@ -30,7 +36,7 @@ def main():
                         exclude="reverse_types", reverse_etypes={"buys": "bought-by",
                                                                   "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
-                        shuffle=True)
+                        shuffle=True, num_workers=nw)
     it = iter(el)
     phases = {"sample": 0.0, "forward": 0.0, "backward": 0.0, "optim": 0.0}
 
@@ -62,7 +68,8 @@ def main():
     host = (time.perf_counter() - t) * 1e3 / n
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t) * 1e3 / n
-    print({"K": K, "wall_ms_per_step": wall, "host_ms_per_step": host,
+    print({"K": K, "num_workers": nw, "switch_interval": sys.getswitchinterval(),
+           "wall_ms_per_step": wall, "host_ms_per_step": host,
            "host_phase_ms": {k: v / n for k, v in phases.items()}}, flush=True)
 
 
