@@ -796,7 +796,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     const Tensor& gz_in, const Tensor& z, const Tensor& row_norm, const Tensor& h_self,
     const Tensor& agg, const Tensor& Ws, const Tensor& Wn, const Tensor& indptr,
     const Tensor& indices, const optional<Tensor>& ew, int64_t reduce, int64_t n_src,
-    int64_t nnz, bool norm, int64_t need) {
+    int64_t nnz, bool norm, int64_t need, const optional<Tensor>& indptr_t_in,
+    const optional<Tensor>& indices_t_in, const optional<Tensor>& w_mean_in) {
   const OneDevice one_device_;
   dev(gz_in, "gz", at::kFloat);
   dev(z, "z", at::kFloat);
@@ -844,23 +845,68 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     Tensor g_agg = at::empty({M, Wn.size(1)}, z.options());
     gemm_nt(gu, Wn.t().contiguous(), nullptr, nullptr, 0, g_agg, nullptr);
     const bool mean = reduce == GNNREC_REDUCE_MEAN;
-    Tensor ip_t = at::empty({n_src + 1}, indptr.options());
-    Tensor ix_t = at::empty({std::max<int64_t>(nnz, 1)}, indices.options());
-    Tensor w_t;
-    if (has(ew) || mean) w_t = at::empty({std::max<int64_t>(nnz, 1)}, z.options());
-    const size_t wsb = gnnrec_csr_transpose_workspace_bytes(nnz, n_src);
-    Tensor ws = at::empty({(int64_t)std::max<size_t>(wsb, 1)}, indptr.options().dtype(at::kByte));
-    const optional<Tensor> ewc = has(ew) ? optional<Tensor>(ew->contiguous()) : ew;
-    ck(gnnrec_csr_transpose(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), M, n_src, nnz,
-                            (int)mean, ws.data_ptr(), ws.nbytes(), p<int64_t>(ip_t),
-                            p<int32_t>(ix_t), pw(w_t), s),
-       "gnnrec_csr_transpose");
+    Tensor ip_t, ix_t, w_t;
+    if (has(indptr_t_in) && !has(ew)) {
+      // the block's source-major CSR, built by the sampler (block_transposes) beside the
+      // block itself: no sort on the training thread
+      TORCH_CHECK_VALUE(indptr_t_in->numel() == n_src + 1 && has(indices_t_in) &&
+                            (!mean || has(w_mean_in)),
+                        "sage_rel_backward: precomputed transpose does not fit the block");
+      ip_t = *indptr_t_in;
+      ix_t = *indices_t_in;
+      if (mean) w_t = *w_mean_in;
+    } else {
+      ip_t = at::empty({n_src + 1}, indptr.options());
+      ix_t = at::empty({std::max<int64_t>(nnz, 1)}, indices.options());
+      if (has(ew) || mean) w_t = at::empty({std::max<int64_t>(nnz, 1)}, z.options());
+      const size_t wsb = gnnrec_csr_transpose_workspace_bytes(nnz, n_src);
+      Tensor ws = at::empty({(int64_t)std::max<size_t>(wsb, 1)},
+                            indptr.options().dtype(at::kByte));
+      const optional<Tensor> ewc = has(ew) ? optional<Tensor>(ew->contiguous()) : ew;
+      ck(gnnrec_csr_transpose(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), M, n_src,
+                              nnz, (int)mean, ws.data_ptr(), ws.nbytes(), p<int64_t>(ip_t),
+                              p<int32_t>(ix_t), pw(w_t), s),
+         "gnnrec_csr_transpose");
+    }
     g_m = at::empty({n_src, Wn.size(1)}, z.options());
     gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m);
   }
   if (need & 4) g_Ws = weight_grad(gu, h_self.narrow(0, 0, M).contiguous());
   if (need & 8) g_Wn = weight_grad(gu, agg.contiguous());
   return {g_self, g_m, g_Ws, g_Wn};
+}
+
+// Every relation's source-major CSR of one sampled block, in one call (the sampler's
+// training side, gnnrec/sampling.py): (indptr_t, dst rows, 1/deg(dst) per edge) per relation,
+// the transposes the aggregation backward gathers over (sage_rel_backward).
+std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>> block_transposes(
+    at::TensorList indptrs, at::TensorList indices, at::IntArrayRef n_src,
+    at::IntArrayRef nnz) {
+  const OneDevice one_device_;
+  const size_t R = indptrs.size();
+  TORCH_CHECK_VALUE(indices.size() == R && n_src.size() == R && nnz.size() == R,
+                    "block_transposes: one entry per relation");
+  std::vector<Tensor> ips(R), ixs(R), ws_(R);
+  for (size_t r = 0; r < R; ++r) {
+    dev(indptrs[r], "indptr", at::kLong);
+    dev(indices[r], "indices", at::kInt);
+    const int64_t E = nnz[r], ns = n_src[r];
+    TORCH_CHECK_VALUE(indices[r].numel() >= E && ns >= 0, "block_transposes: sizes");
+    ips[r] = at::empty({ns + 1}, indptrs[r].options());
+    ixs[r] = at::empty({std::max<int64_t>(E, 1)}, indices[r].options());
+    ws_[r] = at::empty({std::max<int64_t>(E, 1)}, indptrs[r].options().dtype(at::kFloat));
+    if (meta(indptrs[r])) continue;
+    const c10::DeviceGuard g(indptrs[r].device());
+    const size_t wsb = gnnrec_csr_transpose_workspace_bytes(E, ns);
+    Tensor ws = at::empty({(int64_t)std::max<size_t>(wsb, 1)},
+                          indptrs[r].options().dtype(at::kByte));
+    ck(gnnrec_csr_transpose(p<int64_t>(indptrs[r]), p<int32_t>(indices[r]), nullptr,
+                            indptrs[r].numel() - 1, ns, E, 1, ws.data_ptr(), ws.nbytes(),
+                            p<int64_t>(ips[r]), p<int32_t>(ixs[r]), p<float>(ws_[r]),
+                            stream_of(indptrs[r])),
+       "gnnrec_csr_transpose");
+  }
+  return {ips, ixs, ws_};
 }
 
 // K10 membership: has_edges_between over a source-sorted in-CSR
@@ -1313,8 +1359,10 @@ TORCH_LIBRARY(gnnrec, m) {
         "-> (Tensor, Tensor, Tensor)");
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
-        "int reduce, int n_src, int nnz, bool norm, int need) "
-        "-> (Tensor, Tensor, Tensor, Tensor)");
+        "int reduce, int n_src, int nnz, bool norm, int need, Tensor? indptr_t=None, "
+        "Tensor? indices_t=None, Tensor? w_mean=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("block_transposes(Tensor[] indptrs, Tensor[] indices, int[] n_src, int[] nnz) "
+        "-> (Tensor[], Tensor[], Tensor[])");
   m.def("margin_loss(Tensor pos, Tensor neg, int K, float delta, Tensor? mask, Tensor? recency, "
         "Tensor(a!) g_pos, Tensor(b!) g_neg, Tensor(c!) partial) -> ()");
   m.def("sum_scaled(Tensor x, float scale, Tensor(a!) out) -> ()");
@@ -1378,6 +1426,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("csr_has_edges", &csr_has_edges);               \
   m.impl("sage_rel_forward", &sage_rel_forward);         \
   m.impl("sage_rel_backward", &sage_rel_backward);       \
+  m.impl("block_transposes", &block_transposes);         \
   m.impl("margin_loss", &margin_loss);                   \
   m.impl("sum_scaled", &sum_scaled);                     \
   m.impl("synth_edges", &synth_edges);                   \

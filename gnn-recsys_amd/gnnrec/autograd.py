@@ -200,13 +200,15 @@ class SageRelFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, m, h_self, Ws, Wn, indptr, indices, ew, reduce: str, norm: bool,
-                n_self: int = 0):
+                n_self: int = 0, transposed=None):
         z, agg, nrm = ops._T().sage_rel_forward(m, h_self, n_self, Ws.detach(), Wn.detach(),
                                                 indptr, indices, ew, ops.REDUCE[reduce],
                                                 bool(norm))
         ctx.save_for_backward(h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew)
         ctx.reduce, ctx.norm, ctx.n_src = reduce, bool(norm), m.shape[0]
         ctx.nnz = ops._nnz(indptr)  # sampled blocks carry it: no readback
+        # the block's source-major CSR when the sampler built it (unweighted relations)
+        ctx.transposed = transposed if ew is None else None
         return z
 
     @staticmethod
@@ -215,12 +217,13 @@ class SageRelFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         mask = (1 if need[1] else 0) | (2 if need[0] else 0) | (4 if need[2] else 0) | \
             (8 if need[3] else 0)
+        tr = ctx.transposed or (None, None, None)
         g_self, g_m, g_Ws, g_Wn = ops._T().sage_rel_backward(
             gz, z, nrm, h_self, agg, Ws.detach(), Wn.detach(), indptr, indices, ew,
-            ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask)
+            ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask, *tr)
         return (g_m if need[0] else None, g_self if need[1] else None,
                 g_Ws if need[2] else None, g_Wn if need[3] else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def sage_rel_fusable(m, h_self, Wn, reduce: str, norm: bool) -> bool:

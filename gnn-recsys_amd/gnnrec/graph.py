@@ -106,8 +106,12 @@ class RelGraph:
     is_block = True
 
     def __init__(self, cetype: CEType, indptr, indices, n_src: int, n_dst: int,
-                 edata: Optional[dict] = None, eids: Optional[torch.Tensor] = None):
+                 edata: Optional[dict] = None, eids: Optional[torch.Tensor] = None,
+                 transposed: Optional[tuple] = None):
         self.cetype = cetype
+        # (indptr_t, dst rows int32, 1/deg(dst) per edge): the source-major CSR the
+        # aggregation backward gathers over, when the sampler built it with the block
+        self.transposed = transposed
         self.canonical_etypes = [cetype]
         self.indptr = indptr
         self.indices = indices
@@ -340,6 +344,7 @@ class Block:
         self._src = {nt: _FrameDict({NID: src_nid[nt]}) for nt in self.ntypes}
         self._dst = {nt: _FrameDict({NID: src_nid[nt][: num_dst[nt]]}) for nt in self.ntypes}
         self._edata = {ce: _FrameDict({EID: rels[ce][2]}) for ce in self.canonical_etypes}
+        self._t = {}  # ce -> source-major CSR of the relation (sampler, training loaders)
 
     @property
     def srcdata(self):
@@ -368,7 +373,7 @@ class Block:
         indptr, indices, eids = self._rels[ce]
         edata = {k: v for k, v in self._edata[ce].items() if k != EID}
         return RelGraph(ce, indptr, indices, self.number_of_src_nodes(ce[0]), self._num_dst[ce[2]],
-                        edata, eids)
+                        edata, eids, self._t.get(ce))
 
     def __getitem__(self, ce) -> RelGraph:
         return self.rel_graph(ce)
@@ -382,6 +387,7 @@ class Block:
         for ce in self.canonical_etypes:
             for k, v in self._edata[ce].items():
                 b._edata[ce][k] = v.to(device)
+        b._t = {ce: tuple(t.to(device) for t in v) for ce, v in self._t.items()}
         return b
 
 

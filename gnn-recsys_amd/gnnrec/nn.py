@@ -165,7 +165,8 @@ class ConvLayer(nn.Module):
                 # one autograd node, one C++ call each way (ag.SageRelFn)
                 return ag.SageRelFn.apply(m, h_self, self.fc_self.weight, self.fc_neigh.weight,
                                           graph.indptr, graph.indices, ew, reduce,
-                                          bool(self.norm), n_self)
+                                          bool(self.norm), n_self,
+                                          getattr(graph, 'transposed', None))
             if reduce == 'lstm':
                 L = self.lstm
                 agg = ag.LstmAggFn.apply(m, L.weight_ih_l0, L.weight_hh_l0, L.bias_ih_l0,

@@ -81,7 +81,11 @@ class BlockSampler:
         return m
 
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
-                      exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None) -> List[Block]:
+                      exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
+                      transposes: bool = False) -> List[Block]:
+        """transposes: also build every relation's source-major CSR (Block._t), which the
+        training backward gathers over — in the sampling thread (num_workers > 0), off the
+        training thread (EdgeDataLoader, transposed_blocks=True)."""
         self._calls += 1
         seeds = {nt: torch.as_tensor(v, dtype=torch.int64, device=g.device)
                  for nt, v in seed_nodes.items()}
@@ -96,6 +100,8 @@ class BlockSampler:
         try:
             for block_id in reversed(range(self.num_layers)):
                 block = self._one_block(g, seeds, block_id, masks)
+                if transposes:
+                    _add_transposes(block)
                 blocks.insert(0, block)
                 seeds = {nt: block.srcdata[NID][nt] for nt in block.ntypes
                          if block.number_of_src_nodes(nt) > 0}
@@ -183,6 +189,20 @@ class BlockSampler:
             for ce, loc in zip(ces, locs):
                 rels[ce][1] = loc.to(torch.int32)
         return Block(src_nid, num_dst, {ce: tuple(v) for ce, v in rels.items()})
+
+
+def _add_transposes(block: Block) -> None:
+    """Every relation's source-major CSR of the block, one C++ call (ops.block_transposes)."""
+    ces = [ce for ce in block.canonical_etypes if ops._nnz(block._rels[ce][0]) > 0]
+    if not ces:
+        return
+    ips, ixs, ws = ops._T().block_transposes(
+        [block._rels[ce][0] for ce in ces], [block._rels[ce][1] for ce in ces],
+        [block.number_of_src_nodes(ce[0]) for ce in ces],
+        [ops._nnz(block._rels[ce][0]) for ce in ces])
+    for ce, ip, ix, w in zip(ces, ips, ixs, ws):
+        ip._gnnrec_nnz = ops._nnz(block._rels[ce][0])
+        block._t[ce] = (ip, ix, w)
 
 
 class MultiLayerFullNeighborSampler(BlockSampler):
@@ -386,9 +406,12 @@ class EdgeDataLoader:
                  reverse_eids=None, reverse_etypes: Optional[dict] = None,
                  negative_sampler=None, batch_size: int = 1, shuffle: bool = False,
                  drop_last: bool = False, num_workers: int = 0, pin_memory: bool = False,
-                 **kwargs):
+                 transposed_blocks: bool = True, **kwargs):
         self.g = g
         self.g_sampling = g_sampling if g_sampling is not None else g
+        # the training loader's blocks carry their source-major CSRs (built by the sampler,
+        # in the sampling thread when num_workers > 0): the backward sorts nothing
+        self.transposed_blocks = transposed_blocks
         self.sampler = block_sampler
         self.exclude = exclude
         if exclude not in (None, 'reverse_types', 'self'):
@@ -489,7 +512,8 @@ class EdgeDataLoader:
             elif self.exclude == 'self':
                 exclude = dict(batch)
             seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
-            blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude)
+            blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
+                                                transposes=self.transposed_blocks)
             input_nodes = blocks[0].srcdata[NID]
             if self.negative_sampler is None:
                 yield input_nodes, pos_g, blocks
