@@ -577,8 +577,8 @@ def rccl_environment(ex):
             ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
         except Exception as exc:  # a diagnostic never fails the bench
             ver = f"unknown ({exc!r})"
-    return {"version": ver, "env": env, "defaults": not any(
-        k.startswith(("NCCL_", "RCCL_")) for k in env)}
+    return {"version": ver, "env": env, "defaults": not any(  # (logging does not count)
+        k.startswith(("NCCL_", "RCCL_")) and not k.startswith("NCCL_DEBUG") for k in env)}
 
 
 if __name__ == "__main__":
