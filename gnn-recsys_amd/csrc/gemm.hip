@@ -462,6 +462,7 @@ __device__ __forceinline__ void wait_vmcnt_barrier() {
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
   else static_assert(N == 0, "add the vmcnt immediate");
 }
@@ -735,10 +736,17 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
     const char* e = getenv("GNNREC_GEMM_BK16");
     return !(e && e[0] == '0');
   }();
-  if constexpr (BN == 128) {
+  // 64-column outputs (the d = 64 minibatch layers, K = 64..128): the same 3-stage kernel
+  // overlaps one block's DMA prologue and epilogue with the other blocks' MFMAs;
+  // GNNREC_GEMM_BK16_N64=0 keeps the 32-deep kernel there
+  static const bool use_bk16_64 = [] {
+    const char* e = getenv("GNNREC_GEMM_BK16_N64");
+    return !(e && e[0] == '0');
+  }();
+  if constexpr (BN == 128 || BN == 64) {
     const bool fast16 = g.vecA1 && g.vecW1 && g.K1 % BK16 == 0 &&
                         (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK16 == 0));
-    if (fast16 && use_dma && use_bk16) {
+    if (fast16 && use_dma && use_bk16 && (BN == 128 || use_bk16_64)) {
       static const int stages = [] {  // GNNREC_GEMM_STAGES: tuning knob
         const char* e = getenv("GNNREC_GEMM_STAGES");
         const int x = e ? atoi(e) : 3;

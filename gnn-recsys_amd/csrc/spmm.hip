@@ -35,6 +35,12 @@ namespace {
 // amortised);
 // GNNREC_RQ_CHUNK > 0 fixes it (tuning)
 constexpr int64_t kRqTicketEdges = 512;
+// Below 32 rows per wave the static grid-stride wins: the queue's dequeues are bound by
+// the heads' atomic rate (≈88 per µs each), so a short launch either takes few long tickets
+// (a fraction of the waves walk 51-row chains) or many short ones (atomic-bound).  A C2
+// block relation (100k rows x 10 edges, d = 64): 52 µs static vs 127-165 µs queued; 1M rows:
+// 444 µs queued vs 472 static (tools/micro/spmm_one.py, profiles/r03_spmm_rowq.txt).
+constexpr int64_t kRqMinRowsPerWave = 32;
 inline int row_chunk() {
   static const int v = [] {
     const char* e = getenv("GNNREC_RQ_CHUNK");
@@ -42,6 +48,17 @@ inline int row_chunk() {
     return x > 0 && x <= 64 ? x : 0;
   }();
   return v;
+}
+
+// rows per ticket: about kRqTicketEdges edges, but at least 4 tickets per wave of the grid.
+// A minibatch block (100k rows at 10 edges) at 51 rows per ticket fed 1960 of the grid's
+// 8192 waves, each walking its 51 rows one latency chain after another (C2: 130-180 µs per
+// launch); the cap keeps every wave busy.  The reduction of a row does not depend on it.
+__device__ __forceinline__ int ticket_rows(int64_t avg_deg, int64_t n_dst, int64_t waves) {
+  int64_t c = kRqTicketEdges / (avg_deg > 0 ? avg_deg : 1);
+  const int64_t cap = n_dst / (waves * 4);
+  if (c > cap) c = cap;
+  return (int)(c < 1 ? 1 : c > 64 ? 64 : c);
 }
 
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
@@ -75,8 +92,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
   if (rq != nullptr) {  // queued rows (one column slice: the launcher checks gridDim.y == 1)
     if (rq_ch <= 0) {
       const int64_t avg = (indptr[n_dst] - indptr[0]) / n_dst;
-      const int64_t c = kRqTicketEdges / (avg > 0 ? avg : 1);
-      rq_ch = (int)(c < 1 ? 1 : c > 64 ? 64 : c);
+      rq_ch = ticket_rows(avg, n_dst, gridDim.x * 4);
     }
     // a ticket's row bounds come from one coalesced indptr load, and the next row's first
     // 64 indices are requested before the current row gathers: of the indptr -> indices ->
@@ -235,10 +251,11 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   const int eni = a.flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
   const int64_t max_deg = a.n_heavy > 0 ? a.split : INT64_MAX;
   const unsigned grid = grid_waves(a.n_dst);
-  // the queue pays off on long launches only (≥ 8 rows per wave of the grid)
+  // the queue pays off on long launches only (≥ kRqMinRowsPerWave rows per wave of the grid)
   int ticket = -1;
-  unsigned* rq =
-      slices == 1 && a.n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot(s, &ticket) : nullptr;
+  unsigned* rq = slices == 1 && a.n_dst >= (int64_t)grid * 4 * kRqMinRowsPerWave
+                     ? rowq_slot(s, &ticket)
+                     : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
                      a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk());
@@ -319,8 +336,7 @@ __global__ __launch_bounds__(256) void spmm_csr2_kernel(Csr2 c, const float* __r
   if (rq != nullptr) {
     if (rq_ch <= 0) {  // ≈ kRqTicketEdges edges of both relations per ticket
       const int64_t e = c.indptr[0][n_dst] - c.indptr[0][0] + c.indptr[1][n_dst] - c.indptr[1][0];
-      const int64_t avg = e / n_dst, ch = kRqTicketEdges / (avg > 0 ? avg : 1);
-      rq_ch = (int)(ch < 1 ? 1 : ch > 64 ? 64 : ch);
+      rq_ch = ticket_rows(e / n_dst, n_dst, gridDim.x * 4);
     }
     rq_for_each(rq, n_dst, rq_ch, both);
     rq_finish(rq);

@@ -1243,6 +1243,83 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
   return {o_ip, src_loc, o_eid, src_nid, totals};
 }
 
+// EdgeDataLoader's batch head in one call (gnnrec/sampling.py _iter_batches): the batch's
+// positive pairs (find_edges), the uniform negatives (src repeated K times, dst =
+// randint(N_dst) from the default generator — the same draws as negative_sampler.Uniform),
+// and DGL's compact_graphs([pos, neg]) over both (relabel per node type, ONE size
+// readback), returning every pair list in local ids.  The same kernels, generator calls and
+// order as the Python form it replaces (bitwise the same pair graphs), issued from C++ with
+// the GIL released, so a prefetching loader thread leaves the training thread alone.
+//   batch[r]: edge ids of relation r in the batch (empty: not in it); neg_order: the
+//   relations in the order their negatives are drawn (the batch's type order)
+std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>,
+           std::vector<Tensor>>
+edge_batch_pairs(at::TensorList rel_src, at::TensorList rel_dst, at::IntArrayRef src_type,
+                 at::IntArrayRef dst_type, at::TensorList batch, at::IntArrayRef neg_order,
+                 int64_t K, at::IntArrayRef n_nodes, at::TensorList prefix_pos,
+                 at::TensorList marks) {
+  const OneDevice one_device_;
+  const size_t R = rel_src.size(), NT = n_nodes.size();
+  TORCH_CHECK_VALUE(rel_dst.size() == R && src_type.size() == R && dst_type.size() == R &&
+                        batch.size() == R && prefix_pos.size() == NT && marks.size() == NT &&
+                        NT > 0,
+                    "edge_batch_pairs: list lengths");
+  for (size_t r = 0; r < R; ++r)
+    TORCH_CHECK_VALUE(src_type[r] >= 0 && (size_t)src_type[r] < NT && dst_type[r] >= 0 &&
+                          (size_t)dst_type[r] < NT,
+                      "edge_batch_pairs: node-type index out of range");
+  const c10::DeviceGuard g(prefix_pos[0].device());
+  const auto opt = prefix_pos[0].options();  // int64 on the device
+  const Tensor empty = at::empty({0}, opt);
+  std::vector<Tensor> ps(R, empty), pd(R, empty), ns(R, empty), nd(R, empty);
+  for (size_t r = 0; r < R; ++r) {
+    if (batch[r].numel() == 0) continue;
+    ps[r] = rel_src[r].index_select(0, batch[r]);
+    pd[r] = rel_dst[r].index_select(0, batch[r]);
+  }
+  if (K > 0) {
+    for (int64_t r : neg_order) {
+      TORCH_CHECK_VALUE(r >= 0 && (size_t)r < R, "edge_batch_pairs: neg_order out of range");
+      if (batch[r].numel() == 0) continue;
+      ns[r] = ps[r].repeat_interleave(K);
+      nd[r] = at::randint(0, n_nodes[dst_type[r]], {ns[r].numel()}, opt);
+    }
+  }
+  // compact_graphs([pos, neg]): per node type the lists in (pos, neg) x relation order
+  std::vector<std::vector<Tensor*>> lists(NT);
+  for (auto* side : {&ps, &ns})
+    for (size_t r = 0; r < R; ++r) {
+      lists[src_type[r]].push_back(&(*side)[r]);
+      auto& dlist = side == &ps ? pd : nd;
+      lists[dst_type[r]].push_back(&dlist[r]);
+    }
+  std::vector<Tensor> rank(NT);
+  for (size_t t = 0; t < NT; ++t) {
+    Tensor pp = prefix_pos[t], mk = marks[t];
+    set_prefix_pos(empty, pp);
+    for (Tensor* ids : lists[t]) mark_ids(*ids, pp, mk);
+    rank[t] = exclusive_scan_new(mk);
+  }
+  std::vector<Tensor> last;
+  for (size_t t = 0; t < NT; ++t) last.push_back(rank[t].narrow(0, rank[t].numel() - 1, 1));
+  const Tensor n_new = at::cat(last).to(at::kCPU);  // the one size readback
+  std::vector<Tensor> nodes(NT);
+  for (size_t t = 0; t < NT; ++t) {
+    const int64_t nn = n_new.data_ptr<int64_t>()[t];
+    Tensor pp = prefix_pos[t], mk = marks[t];
+    nodes[t] = at::empty({nn}, opt);
+    if (nn) compact_marked(mk, rank[t], nodes[t]);
+    for (Tensor* ids : lists[t]) {
+      Tensor loc = at::empty({ids->numel()}, opt);
+      relabel_ids(*ids, pp, rank[t], 0, loc);
+      *ids = loc;  // the list entry becomes its local ids
+    }
+    clear_prefix_pos(empty, pp);
+    if (nn) mk.index_fill_(0, nodes[t], 0);
+  }
+  return {nodes, ps, pd, ns, nd};
+}
+
 // ---------------------------------------------------------------- host-only queries
 int64_t version() { return gnnrec_version(); }
 void set_concurrency(int64_t reserve_cus, bool dynamic) {
@@ -1363,6 +1440,9 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor? indices_t=None, Tensor? w_mean=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("block_transposes(Tensor[] indptrs, Tensor[] indices, int[] n_src, int[] nnz) "
         "-> (Tensor[], Tensor[], Tensor[])");
+  m.def("edge_batch_pairs(Tensor[] rel_src, Tensor[] rel_dst, int[] src_type, int[] dst_type, "
+        "Tensor[] batch, int[] neg_order, int K, int[] n_nodes, Tensor[] prefix_pos, "
+        "Tensor[] marks) -> (Tensor[], Tensor[], Tensor[], Tensor[], Tensor[])");
   m.def("margin_loss(Tensor pos, Tensor neg, int K, float delta, Tensor? mask, Tensor? recency, "
         "Tensor(a!) g_pos, Tensor(b!) g_neg, Tensor(c!) partial) -> ()");
   m.def("sum_scaled(Tensor x, float scale, Tensor(a!) out) -> ()");
@@ -1436,6 +1516,7 @@ TORCH_LIBRARY(gnnrec, m) {
 TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) {
   GNNREC_IMPLS(m);
   m.impl("sample_layer", &sample_layer);  // data-dependent sizes: device only, no meta form
+  m.impl("edge_batch_pairs", &edge_batch_pairs);
 }
 // Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
 TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }

@@ -14,21 +14,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTile = 128;       // output super-tile per block (M and N)
 constexpr int kKStep = 16;       // input rows per pipeline step (8 MFMA k-pairs)
-constexpr int kLdsStride = kTile + 4;
 constexpr int kTargetBlocks = 512;
 
-// One 16-row step of a [K, ld] operand restricted to columns [c0, c0+128):
-// 512 float4 slots, two per thread (row = slot / 32, cols 4*(slot % 32) .. +3).
+// One 16-row step of a [K, ld] operand restricted to columns [c0, c0+T):
+// 4·T float4 slots, T/64 per thread (row = slot / (T/4), cols 4*(slot % (T/4)) .. +3).
 // VEC: 16-B loads (ld % 4 == 0, 16-B aligned base, full columns checked per slot);
 // otherwise per-element loads.  Rows >= ke and columns >= ncol read as zero.
-template <bool VEC>
+template <bool VEC, int T>
 __device__ inline void load_step(const float* __restrict__ X, int64_t ld, int64_t ncol,
-                                 int64_t c0, int64_t k0, int64_t ke, float4 (&r)[2]) {
+                                 int64_t c0, int64_t k0, int64_t ke, float4 (&r)[T / 64]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < T / 64; ++h) {
     const int slot = threadIdx.x + 256 * h;
-    const int64_t k = k0 + (slot >> 5);
-    const int64_t c = c0 + 4 * (slot & 31);
+    const int64_t k = k0 + slot / (T / 4);
+    const int64_t c = c0 + 4 * (slot % (T / 4));
     const bool k_ok = k < ke;
     const int64_t kc = k_ok ? k : ke - 1;
     const float* row = X + kc * ld;
@@ -50,78 +49,89 @@ __device__ inline void load_step(const float* __restrict__ X, int64_t ld, int64_
   }
 }
 
-__device__ inline void store_step(float* lds, const float4 (&r)[2]) {
+template <int T>
+__device__ inline void store_step(float* lds, const float4 (&r)[T / 64]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < T / 64; ++h) {
     const int slot = threadIdx.x + 256 * h;
-    *reinterpret_cast<float4*>(lds + (slot >> 5) * kLdsStride + 4 * (slot & 31)) = r[h];
+    *reinterpret_cast<float4*>(lds + (slot / (T / 4)) * (T + 4) + 4 * (slot % (T / 4))) = r[h];
   }
 }
 
-// Block: 4 waves as 2x2 wave tiles of 64x64 (2x2 MFMA 32x32 tiles each) over a
-// 128x128 output super-tile; K slice [kb, ke) streamed through double-buffered LDS
+// Block: 4 waves as 2x2 wave tiles of T/2 x T/2 (NT x NT MFMA 32x32 tiles each, NT = T/64)
+// over a T x T output super-tile; K slice [kb, ke) streamed through double-buffered LDS
 // with a register prefetch of the next 16-row step (one barrier per step).
 // MFMA 32x32x2 f32 operands: lane l supplies A^T[i=l&31][k=l>>5] = A[k][i] and
 // B[k=l>>5][j=l&31]; both are consecutive LDS words across the half-wave.
-template <bool VEC>
+// T = 64 serves M, N <= 64 (the d = 64 layers of the minibatch step): the 128 tile spent
+// 3/4 of its MFMAs on zero padding and was MFMA-bound at 4x the useful work.  Every
+// output element sees the same MFMA sequence over the same split either way (bitwise
+// the same partials).
+template <bool VEC, int T>
 __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
     int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part,
     float* __restrict__ part_b) {
-  __shared__ float As[2][kKStep * kLdsStride];
-  __shared__ float Bs[2][kKStep * kLdsStride];
+  constexpr int NT = T / 64, S = T + 4;
+  __shared__ float As[2][kKStep * S];
+  __shared__ float Bs[2][kKStep * S];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 31, lk = lane >> 5;
-  const int wi = (w & 1) * 64, wj = (w >> 1) * 64;
+  const int wi = (w & 1) * (T / 2), wj = (w >> 1) * (T / 2);
   const int64_t split = blockIdx.x;
-  const int64_t i_base = (int64_t)blockIdx.y * kTile, j_base = (int64_t)blockIdx.z * kTile;
+  const int64_t i_base = (int64_t)blockIdx.y * T, j_base = (int64_t)blockIdx.z * T;
   const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
 
   // part_b: column sums of A over this split (the bias gradient Σ_k dY[k, i]); the blocks
   // of the first N tile add up the A tiles they already hold in LDS
-  const bool colsum = part_b != nullptr && blockIdx.z == 0 && threadIdx.x < kTile;
+  const bool colsum = part_b != nullptr && blockIdx.z == 0 && threadIdx.x < T;
   float csum = 0.f;
-  f32x16 acc[2][2];
+  f32x16 acc[NT][NT];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < NT; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int y = 0; y < NT; ++y)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[x][y][v] = 0.f;
 
   if (kb < ke) {  // uniform per block
-    float4 ra[2], rb[2];
-    load_step<VEC>(A, lda, M, i_base, kb, ke, ra);
-    load_step<VEC>(B, ldb, N, j_base, kb, ke, rb);
-    store_step(As[0], ra);
-    store_step(Bs[0], rb);
+    float4 ra[NT], rb[NT];
+    load_step<VEC, T>(A, lda, M, i_base, kb, ke, ra);
+    load_step<VEC, T>(B, ldb, N, j_base, kb, ke, rb);
+    store_step<T>(As[0], ra);
+    store_step<T>(Bs[0], rb);
     __syncthreads();
     int buf = 0;
     for (int64_t k0 = kb; k0 < ke; k0 += kKStep) {
       const bool more = k0 + kKStep < ke;
       if (more) {
-        load_step<VEC>(A, lda, M, i_base, k0 + kKStep, ke, ra);
-        load_step<VEC>(B, ldb, N, j_base, k0 + kKStep, ke, rb);
+        load_step<VEC, T>(A, lda, M, i_base, k0 + kKStep, ke, ra);
+        load_step<VEC, T>(B, ldb, N, j_base, k0 + kKStep, ke, rb);
       }
       const float* as = As[buf];
       const float* bs = Bs[buf];
 #pragma unroll
       for (int s = 0; s < kKStep / 2; ++s) {
-        const int kr = (2 * s + lk) * kLdsStride;
-        const float a0 = as[kr + wi + li], a1 = as[kr + wi + 32 + li];
-        const float b0 = bs[kr + wj + li], b1 = bs[kr + wj + 32 + li];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        const int kr = (2 * s + lk) * S;
+        float a[NT], b[NT];
+#pragma unroll
+        for (int x = 0; x < NT; ++x) {
+          a[x] = as[kr + wi + 32 * x + li];
+          b[x] = bs[kr + wj + 32 * x + li];
+        }
+#pragma unroll
+        for (int x = 0; x < NT; ++x)
+#pragma unroll
+          for (int y = 0; y < NT; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
       }
       if (colsum) {
 #pragma unroll
-        for (int r = 0; r < kKStep; ++r) csum += as[r * kLdsStride + threadIdx.x];
+        for (int r = 0; r < kKStep; ++r) csum += as[r * S + threadIdx.x];
       }
       if (more) {
-        store_step(As[buf ^ 1], ra);
-        store_step(Bs[buf ^ 1], rb);
+        store_step<T>(As[buf ^ 1], ra);
+        store_step<T>(Bs[buf ^ 1], rb);
       }
       __syncthreads();
       buf ^= 1;
@@ -130,9 +140,9 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
   if (colsum && i_base + threadIdx.x < M) part_b[split * M + i_base + threadIdx.x] = csum;
   float* P = part + split * M * N;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < NT; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
+    for (int y = 0; y < NT; ++y) {
       const int64_t j = j_base + wj + 32 * y + li;
       if (j >= N) continue;
 #pragma unroll
@@ -296,12 +306,20 @@ extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float*
   const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 &&
                    M % 4 == 0 && N % 4 == 0;
   float* part_b = colsum ? workspace + splits * M * N : nullptr;
-  if (vec)
-    hipLaunchKernelGGL(gemm_tn_partial_kernel<true>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
-                       N, chunk, workspace, part_b);
-  else
-    hipLaunchKernelGGL(gemm_tn_partial_kernel<false>, grid, dim3(256), 0, s, A, lda, B, ldb, K, M,
-                       N, chunk, workspace, part_b);
+  if (M <= 64 && N <= 64) {  // one 64 x 64 tile (the split count is the 128 tile's)
+    if (vec)
+      hipLaunchKernelGGL((gemm_tn_partial_kernel<true, 64>), grid, dim3(256), 0, s, A, lda, B,
+                         ldb, K, M, N, chunk, workspace, part_b);
+    else
+      hipLaunchKernelGGL((gemm_tn_partial_kernel<false, 64>), grid, dim3(256), 0, s, A, lda, B,
+                         ldb, K, M, N, chunk, workspace, part_b);
+  } else if (vec) {
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<true, kTile>), grid, dim3(256), 0, s, A, lda, B,
+                       ldb, K, M, N, chunk, workspace, part_b);
+  } else {
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<false, kTile>), grid, dim3(256), 0, s, A, lda, B,
+                       ldb, K, M, N, chunk, workspace, part_b);
+  }
   const int64_t nout = M * N + (colsum ? M : 0);
   hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s,
                      workspace, part_b, splits, M, N, C, ldc, colsum, accumulate);

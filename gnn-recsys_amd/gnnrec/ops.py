@@ -1018,6 +1018,19 @@ def sample_layer(indptrs, indices, eids, masks, src_type, dst_type, fanouts, key
                              list(seeds), list(prefix_pos), list(marks))
 
 
+def edge_batch_pairs(rel_src, rel_dst, src_type, dst_type, batch, neg_order, k, n_nodes,
+                     prefix_pos, marks):
+    """EdgeDataLoader's batch head in one call (gnnrec::edge_batch_pairs): positive pairs of
+    the batch's edges, k uniform negatives per positive (negative_sampler.Uniform's draws),
+    and compact_graphs over both, one host size read.
+    -> ([node ids per type], [pos src], [pos dst], [neg src], [neg dst]) in local ids."""
+    for t in list(rel_src) + list(rel_dst) + list(batch) + list(prefix_pos):
+        _dev(t, "edge_batch_pairs operand", torch.int64)
+    return _T().edge_batch_pairs(list(rel_src), list(rel_dst), list(src_type), list(dst_type),
+                                 list(batch), list(neg_order), int(k), list(n_nodes),
+                                 list(prefix_pos), list(marks))
+
+
 class Relabeler:
     """Per-node-type scratch for to_block relabelling (mark array + prefix map).
 

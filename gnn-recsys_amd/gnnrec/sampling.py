@@ -431,6 +431,10 @@ class EdgeDataLoader:
             if k in names:
                 self.reverse_etypes[self.g.to_canonical_etype(k)] = self.g.to_canonical_etype(v)
         self.negative_sampler = negative_sampler
+        # the batch head (pairs, negatives, compaction) as one C++ call on the GPU for the
+        # Uniform sampler; any other sampler is called as given
+        self.fused_head = (g.device.type == "cuda" and
+                           (negative_sampler is None or type(negative_sampler) is _Uniform))
         dev = g.device
         if not isinstance(eids, dict):
             eids = {g.canonical_etypes[0]: eids}
@@ -480,6 +484,26 @@ class EdgeDataLoader:
                 dst_map[ce] = (s, d)
         return node_ids, pos_l, neg_l
 
+    def _head(self, batch):
+        """find_edges + negative_sampler.Uniform + _compact in one C++ call
+        (gnnrec::edge_batch_pairs), bitwise the same pair graphs as the three steps above."""
+        g = self.g
+        ces, nts = list(g.canonical_etypes), list(g.ntypes)
+        tix = {nt: i for i, nt in enumerate(nts)}
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        coo = [g._coo[ce] for ce in ces]
+        rel = [self.sampler._relabeler(g, nt) for nt in nts]
+        k = 0 if self.negative_sampler is None else self.negative_sampler.k
+        nodes, ps, pd, ns, nd = ops.edge_batch_pairs(
+            [c[0] for c in coo], [c[1] for c in coo], [tix[ce[0]] for ce in ces],
+            [tix[ce[2]] for ce in ces], [batch.get(ce, empty) for ce in ces],
+            [ces.index(ce) for ce in batch], k, [g.num_nodes(nt) for nt in nts],
+            [r.prefix_pos for r in rel], [r.mark for r in rel])
+        node_ids = dict(zip(nts, nodes))
+        pos_l = {ce: (ps[i], pd[i]) for i, ce in enumerate(ces)}
+        neg_l = {} if k == 0 else {ce: (ns[i], nd[i]) for i, ce in enumerate(ces)}
+        return node_ids, pos_l, neg_l
+
     def __iter__(self):
         return _maybe_prefetch(self, self._iter_batches)
 
@@ -490,13 +514,16 @@ class EdgeDataLoader:
                             self.drop_last, g.device):
             parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
             batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
-            pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch else (empty, empty)
-                         for ce in g.canonical_etypes}
-            neg_edges = {}
-            if self.negative_sampler is not None:
-                neg = self.negative_sampler(g, batch)
-                neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
-            node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
+            if self.fused_head:
+                node_ids, pos_l, neg_l = self._head(batch)
+            else:  # the readable form: the same kernels, generator draws and order
+                pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch
+                             else (empty, empty) for ce in g.canonical_etypes}
+                neg_edges = {}
+                if self.negative_sampler is not None:
+                    neg = self.negative_sampler(g, batch)
+                    neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
+                node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
             pos_g = PairGraph(pos_l, node_ids)
             for ce, e in batch.items():
                 for k, v in g._edata[ce].items():

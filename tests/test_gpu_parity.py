@@ -423,7 +423,8 @@ def test_spmm_backward_matches_reference(reduce, weighted):
 
 # ------------------------------------------------------- f2 backward kernels ---
 @pytest.mark.parametrize("K,M,N", [(1, 1, 1), (37, 5, 7), (1000, 128, 128), (4099, 200, 96),
-                                   (70001, 128, 256), (0, 4, 3)])
+                                   (70001, 128, 256), (0, 4, 3),
+                                   (200003, 64, 64), (5001, 64, 33)])  # the 64 x 64 tile
 def test_gemm_tn_matches_fp64(K, M, N):
     from gnnrec import ops
     gen = torch.Generator(device="cuda")

@@ -177,6 +177,50 @@ def test_edge_loader_exclusion_negatives_and_training_step():
     assert n_batches == len(loader) == (400 + 500 + 63) // 64
 
 
+@pytest.mark.parametrize("K", [0, 4])
+def test_fused_batch_head_matches_readable_form(K):
+    """EdgeDataLoader's batch head as one C++ call (gnnrec::edge_batch_pairs) yields the same
+    pair graphs, node ids and blocks bit for bit as find_edges + negative_sampler.Uniform +
+    _compact, batch after batch (the same generator draws in the same order)."""
+    from gnnrec.graph import NID
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    g, _ = _graph()
+
+    def epoch(fused):
+        torch.manual_seed(11)
+        loader = EdgeDataLoader(g, {CLICKS: torch.arange(500), BUYS: torch.arange(400)},
+                                MultiLayerNeighborSampler([3, 3], seed=5), exclude='self',
+                                negative_sampler=negative_sampler.Uniform(K) if K else None,
+                                batch_size=96, shuffle=True)
+        assert loader.fused_head
+        loader.fused_head = fused
+        out = []
+        for item in loader:
+            pos_g, blocks = item[1], item[-1]
+            neg_g = item[2] if K else None
+            rec = {nt: pos_g.ndata[NID][nt].cpu() for nt in ("user", "item")}
+            for ce in g.canonical_etypes:
+                rec[("pos",) + ce] = [t.cpu() for t in pos_g.all_edges(etype=ce)]
+                if K:
+                    rec[("neg",) + ce] = [t.cpu() for t in neg_g.all_edges(etype=ce)]
+            rec["b0"] = {nt: blocks[0].srcdata[NID][nt].cpu() for nt in blocks[0].ntypes}
+            out.append(rec)
+        return out
+
+    a, b = epoch(True), epoch(False)
+    assert len(a) == len(b) == -(-900 // 96)
+    for ra, rb in zip(a, b):
+        assert ra.keys() == rb.keys()
+        for key in ra:
+            va, vb = ra[key], rb[key]
+            if isinstance(va, dict):
+                assert all(torch.equal(va[n], vb[n]) for n in va), key
+            elif isinstance(va, list):
+                assert all(torch.equal(x, y) for x, y in zip(va, vb)), key
+            else:
+                assert torch.equal(va, vb), key
+
+
 def test_autograd_matches_torch_reference():
     """Gradients of a ConvModel pass through the HIP-forward autograd Functions equal
     those of a plain torch fp32 restatement of the same math (autograd on torch ops)."""

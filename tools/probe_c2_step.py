@@ -8,6 +8,8 @@ rocprofv3 --kernel-trace of this script gives the per-kernel split).
 
 GNNREC_SWITCH_INTERVAL=<s>: sys.setswitchinterval for the run (the GIL hand-over period
 between the training thread and a prefetching sampler thread).
+GNNREC_FUSED_HEAD=0: the loader's batch head in its Python form (find_edges + Uniform +
+_compact) instead of the one gnnrec::edge_batch_pairs call.
 """
 import os
 import sys
@@ -37,6 +39,7 @@ def main():
                                                                   "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
                         shuffle=True, num_workers=nw)
+    el.fused_head = el.fused_head and os.environ.get("GNNREC_FUSED_HEAD", "1") != "0"
     it = iter(el)
     phases = {"sample": 0.0, "forward": 0.0, "backward": 0.0, "optim": 0.0}
 
@@ -68,7 +71,7 @@ def main():
     host = (time.perf_counter() - t) * 1e3 / n
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t) * 1e3 / n
-    print({"K": K, "num_workers": nw, "switch_interval": sys.getswitchinterval(),
+    print({"K": K, "num_workers": nw, "fused_head": el.fused_head, "switch_interval": sys.getswitchinterval(),
            "wall_ms_per_step": wall, "host_ms_per_step": host,
            "host_phase_ms": {k: v / n for k, v in phases.items()}}, flush=True)
 
