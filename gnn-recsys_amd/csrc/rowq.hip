@@ -19,14 +19,20 @@ std::atomic<int> g_dynamic{[] {
   const char* e = getenv("GNNREC_ROWQ");
   return e && e[0] == '0' ? 0 : 1;
 }()};
-std::mutex g_mu;
-std::atomic<unsigned*> g_ring[kMaxDevices] = {};
-std::atomic<unsigned> g_next[kMaxDevices];
-// completion event of each slot's last launch: a slot whose previous launch (possibly on
-// another stream) has not finished is not handed out again — that launch gets the static
-// schedule instead of sharing heads with a running grid
-hipEvent_t* g_done[kMaxDevices] = {};
-std::atomic<long long> g_queued{0}, g_busy{0};  // launches given a slot / refused one
+// a per-device ring of device scratch slots, zeroed once and left zeroed by each user's
+// last block (self-cleaning); a slot is handed out only when its previous launch (on any
+// stream) has completed — the event per slot — and never to a launch being captured
+struct SlotRing {
+  size_t slot_bytes;
+  unsigned n_slots;
+  std::mutex mu;
+  std::atomic<char*> ring[kMaxDevices] = {};
+  std::atomic<unsigned> next[kMaxDevices] = {};
+  hipEvent_t* done[kMaxDevices] = {};
+};
+SlotRing g_rowq{(size_t)kRqSlotWords * sizeof(unsigned), kRqSlots};
+SlotRing g_scan{(size_t)kScanSlotWords * sizeof(unsigned long long), kScanSlots};
+std::atomic<long long> g_queued{0}, g_busy{0};  // row-queue launches given a slot / refused one
 int g_cus[kMaxDevices] = {};
 
 int current_device() {
@@ -50,6 +56,52 @@ __global__ void hold_kernel(int64_t ticks, float* sink) {
   if (acc < 0.f) sink[threadIdx.x] = acc;  // never taken: keeps the loop's loads
 }
 
+// nullptr: captured launch, allocation failure or busy slot (*busy set) — the caller then
+// takes its slot-free path
+char* ring_slot(SlotRing& r, hipStream_t stream, int* ticket, bool* busy) {
+  *ticket = -1;
+  *busy = false;
+  // a launch captured into a hipGraph would replay with its slot baked in and no
+  // completion check, so an eager launch could take the same slot while the replay runs
+  // (two grids on one slot skip or repeat work): captured launches get no slot
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
+    return nullptr;
+  const int dev = current_device();
+  char* ring = r.ring[dev].load(std::memory_order_acquire);
+  if (ring == nullptr) {
+    std::lock_guard<std::mutex> lk(r.mu);
+    ring = r.ring[dev].load(std::memory_order_relaxed);
+    if (ring == nullptr) {
+      const size_t bytes = r.slot_bytes * r.n_slots;
+      if (hipMalloc(&ring, bytes) != hipSuccess) return nullptr;
+      hipEvent_t* ev = new hipEvent_t[r.n_slots]();
+      bool ok = hipMemset(ring, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+      for (unsigned i = 0; ok && i < r.n_slots; ++i)
+        ok = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess;
+      if (!ok) {
+        (void)hipFree(ring);
+        return nullptr;
+      }
+      r.done[dev] = ev;
+      r.ring[dev].store(ring, std::memory_order_release);
+    }
+  }
+  const unsigned i = r.next[dev].fetch_add(1, std::memory_order_relaxed) % r.n_slots;
+  // never recorded -> hipSuccess; still running -> hipErrorNotReady: no slot
+  if (hipEventQuery(r.done[dev][i]) != hipSuccess) {
+    *busy = true;
+    return nullptr;
+  }
+  *ticket = (int)i;
+  return ring + (size_t)i * r.slot_bytes;
+}
+
+void ring_launched(SlotRing& r, int ticket, hipStream_t stream) {
+  if (ticket < 0) return;
+  (void)hipEventRecord(r.done[current_device()][ticket], stream);
+}
+
 }  // namespace
 
 int device_cus() {
@@ -67,48 +119,22 @@ int cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
 unsigned* rowq_slot(hipStream_t stream, int* ticket) {
   *ticket = -1;
   if (!g_dynamic.load(std::memory_order_relaxed)) return nullptr;
-  // a launch captured into a hipGraph would replay with its slot baked in and no
-  // completion check, so an eager launch could take the same slot while the replay runs
-  // (two grids on one set of heads skip or repeat rows): captured launches get the static
-  // schedule
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
-    return nullptr;
-  const int dev = current_device();
-  unsigned* ring = g_ring[dev].load(std::memory_order_acquire);
-  if (ring == nullptr) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    ring = g_ring[dev].load(std::memory_order_relaxed);
-    if (ring == nullptr) {
-      const size_t bytes = (size_t)kRqSlots * kRqSlotWords * sizeof(unsigned);
-      if (hipMalloc(&ring, bytes) != hipSuccess) return nullptr;  // static schedule instead
-      hipEvent_t* ev = new hipEvent_t[kRqSlots]();
-      bool ok = hipMemset(ring, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
-      for (unsigned i = 0; ok && i < kRqSlots; ++i)
-        ok = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess;
-      if (!ok) {
-        (void)hipFree(ring);
-        return nullptr;
-      }
-      g_done[dev] = ev;
-      g_ring[dev].store(ring, std::memory_order_release);
-    }
-  }
-  const unsigned i = g_next[dev].fetch_add(1, std::memory_order_relaxed) % kRqSlots;
-  // never recorded -> hipSuccess; still running -> hipErrorNotReady: skip the queue
-  if (hipEventQuery(g_done[dev][i]) != hipSuccess) {
-    g_busy.fetch_add(1, std::memory_order_relaxed);
-    return nullptr;
-  }
-  g_queued.fetch_add(1, std::memory_order_relaxed);
-  *ticket = (int)i;
-  return ring + (size_t)i * kRqSlotWords;
+  bool busy = false;
+  char* q = ring_slot(g_rowq, stream, ticket, &busy);
+  if (q) g_queued.fetch_add(1, std::memory_order_relaxed);
+  else if (busy) g_busy.fetch_add(1, std::memory_order_relaxed);
+  return reinterpret_cast<unsigned*>(q);  // nullptr: the static schedule
 }
 
-void rowq_launched(int ticket, hipStream_t stream) {
-  if (ticket < 0) return;
-  (void)hipEventRecord(g_done[current_device()][ticket], stream);
+void rowq_launched(int ticket, hipStream_t stream) { ring_launched(g_rowq, ticket, stream); }
+
+unsigned long long* scan_slot(hipStream_t stream, int* ticket) {
+  bool busy = false;
+  return reinterpret_cast<unsigned long long*>(ring_slot(g_scan, stream, ticket, &busy));
 }
+
+void scan_launched(int ticket, hipStream_t stream) { ring_launched(g_scan, ticket, stream); }
+
 
 }  // namespace gnnrec
 

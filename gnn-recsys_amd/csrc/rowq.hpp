@@ -34,6 +34,14 @@ constexpr int kRqSlotWords = (kRqHeads + 1) * kRqStride;
 // launch still running); after launching with a slot, rowq_launched(ticket, stream)
 unsigned* rowq_slot(hipStream_t stream, int* ticket);
 void rowq_launched(int ticket, hipStream_t stream);
+// the single-pass scan's slots (sampler.hip): [0] tile counter, [1] done counter, tile
+// flags from word kScanFlags0; zero between users (the last block resets what it used)
+constexpr int kScanMaxTiles = 4096;
+constexpr int kScanFlags0 = 16;
+constexpr int kScanSlotWords = kScanFlags0 + kScanMaxTiles;
+constexpr unsigned kScanSlots = 128;
+unsigned long long* scan_slot(hipStream_t stream, int* ticket);  // nullptr: no slot free
+void scan_launched(int ticket, hipStream_t stream);
 int device_cus();       // CUs of the current device
 int cu_reserve();       // CUs the row kernels leave free for concurrent kernels
 

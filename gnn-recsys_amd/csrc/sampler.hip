@@ -11,6 +11,7 @@
 // Pipeline per relation: count -> exclusive scan -> fill; per node type:
 // mark -> scan -> compact (new src ids) -> relabel (local src ids).
 #include "common.hpp"
+#include "rowq.hpp"
 
 namespace gnnrec {
 namespace {
@@ -271,6 +272,151 @@ __global__ __launch_bounds__(kScan1Block) void scan_one_block_kernel(const T* in
   if (t == kScan1Block - 1) out[n] = run;  // the total
 }
 
+// ---- single pass: chained tiles with decoupled look-back ------------------------------
+// One launch instead of three (tile sums, their scan, apply) and one read of the input:
+// a block takes the next tile in dispatch order (atomic tile counter), publishes its
+// aggregate, and its first wave walks back over the predecessors' flags — 64 at a time —
+// until one that holds an inclusive prefix; then it publishes its own inclusive prefix.
+// A tile waits only on tiles taken before it, by blocks already running, so every wave
+// finishes.  Flags are 64-bit words: status in the top 2 bits (0 none, 1 aggregate,
+// 2 inclusive), a signed 62-bit value below.  The slot (rowq.hpp: scan_slot) is zero
+// between users: the last block out resets the counters and the flags it used.
+// The minibatch step scans its relabel marks (1M users, 100k items) and per-seed counts
+// about 14 times per step: ~290 µs over 40-odd launches in three-kernel form (C2 trace).
+constexpr int kCsThreads = 256;
+constexpr int kCsItems = 16;
+constexpr int64_t kCsTile = (int64_t)kCsThreads * kCsItems;
+constexpr unsigned long long kCsAgg = 1ull << 62, kCsIncl = 2ull << 62;
+
+__device__ __forceinline__ unsigned long long cs_pack(unsigned long long status, int64_t v) {
+  return status | ((unsigned long long)v & ((1ull << 62) - 1));
+}
+__device__ __forceinline__ int64_t cs_value(unsigned long long f) {
+  return (int64_t)(f << 2) >> 2;  // sign-extend the 62-bit value
+}
+
+// exclusive scan of one value per thread over the block (wave shuffles, 2 barriers);
+// *total = the block's sum
+__device__ __forceinline__ int64_t cs_block_scan(int64_t x, int64_t* wsum, int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t v = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(v, off);
+    if (lane >= off) v += y;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  constexpr int NW = kCsThreads / 64;
+  int64_t before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int64_t s = wsum[i];
+    if (i < w) before += s;
+    tot += s;
+  }
+  *total = tot;
+  return before + v - x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kCsThreads) void scan_chained_kernel(const T* in, int64_t n,
+                                                                  int64_t* out,
+                                                                  unsigned long long* slot,
+                                                                  int64_t n_tiles) {
+  __shared__ int64_t wsum[kCsThreads / 64];
+  __shared__ int64_t sh_tile, sh_prefix;
+  __shared__ int sh_last;
+  // slot == nullptr: a one-tile scan (no predecessors, no counters)
+  unsigned long long* flags = slot ? slot + kScanFlags0 : nullptr;
+  if (threadIdx.x == 0)
+    sh_tile = slot ? (int64_t)__hip_atomic_fetch_add(slot, 1ull, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                   : 0;
+  __syncthreads();
+  const int64_t tile = sh_tile;
+  const int64_t base = tile * kCsTile + (int64_t)threadIdx.x * kCsItems;
+  int64_t vals[kCsItems];
+  int64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kCsItems; ++j) {
+    vals[j] = base + j < n ? (int64_t)in[base + j] : 0;
+    s += vals[j];
+  }
+  int64_t agg;
+  const int64_t ex = cs_block_scan(s, wsum, &agg);  // (its barrier: every read of in is done)
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (slot == nullptr) {
+      if (lane == 0) sh_prefix = 0;
+    } else if (tile == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(flags, cs_pack(kCsIncl, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        sh_prefix = 0;
+      }
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(flags + tile, cs_pack(kCsAgg, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t prefix = 0;
+      for (int64_t j = tile - 1;; j -= 64) {  // window [j - 63, j], nearest first
+        const int64_t idx = j - lane;
+        unsigned long long f = kCsIncl;  // before tile 0: an inclusive prefix of 0
+        if (idx >= 0) {
+          f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while ((f >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        const uint64_t incl = __ballot((f >> 62) == 2);
+        const int stop = incl ? __builtin_ctzll(incl) : 64;
+        int64_t v = lane <= stop ? cs_value(f) : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        prefix += v;
+        if (incl) break;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(flags + tile, cs_pack(kCsIncl, prefix + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        sh_prefix = prefix;
+      }
+    }
+  }
+  __syncthreads();
+  int64_t run = sh_prefix + ex;
+#pragma unroll
+  for (int j = 0; j < kCsItems; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += vals[j];
+  }
+  if (tile == n_tiles - 1 && threadIdx.x == kCsThreads - 1) out[n] = run;  // the total
+  if (slot == nullptr) return;
+  // count the block out; the last one resets the slot for its next user
+  if (threadIdx.x == 0)
+    sh_last = __hip_atomic_fetch_add(slot + 1, 1ull, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) == (unsigned long long)n_tiles - 1;
+  __syncthreads();
+  if (sh_last) {
+    for (int64_t t = threadIdx.x; t < n_tiles; t += kCsThreads)
+      __hip_atomic_store(flags + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(slot + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+inline bool chained_scan_enabled() {
+  static const bool v = [] {  // GNNREC_SCAN_CHAINED=0: the three-kernel form (A/B)
+    const char* e = getenv("GNNREC_SCAN_CHAINED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <typename T>
 int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStream_t s) {
   GNNREC_REQUIRE(n >= 0, "scan: negative n");
@@ -281,6 +427,21 @@ int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStr
       return GNNREC_EHIP;
     }
     return GNNREC_OK;
+  }
+  const int64_t cs_tiles = (n + kCsTile - 1) / kCsTile;
+  if (cs_tiles == 1 && chained_scan_enabled()) {
+    hipLaunchKernelGGL(scan_chained_kernel<T>, dim3(1), dim3(kCsThreads), 0, s, in, n, out,
+                       nullptr, (int64_t)1);
+    return check_launch("gnnrec_exclusive_scan");
+  }
+  if (cs_tiles <= kScanMaxTiles && chained_scan_enabled()) {
+    int ticket = -1;
+    if (unsigned long long* slot = scan_slot(s, &ticket)) {
+      hipLaunchKernelGGL(scan_chained_kernel<T>, dim3((unsigned)cs_tiles), dim3(kCsThreads), 0, s,
+                         in, n, out, slot, cs_tiles);
+      scan_launched(ticket, s);
+      return check_launch("gnnrec_exclusive_scan");
+    }
   }
   if (n <= kScan1Tile) {
     hipLaunchKernelGGL(scan_one_block_kernel<T>, dim3(1), dim3(kScan1Block), 0, s, in, n, out);

@@ -16,15 +16,15 @@ constexpr int kTile = 128;       // output super-tile per block (M and N)
 constexpr int kKStep = 16;       // input rows per pipeline step (8 MFMA k-pairs)
 constexpr int kTargetBlocks = 512;
 
-// One 16-row step of a [K, ld] operand restricted to columns [c0, c0+T):
-// 4·T float4 slots, T/64 per thread (row = slot / (T/4), cols 4*(slot % (T/4)) .. +3).
+// One KS-row step of a [K, ld] operand restricted to columns [c0, c0+T):
+// KS·T/4 float4 slots, KS·T/1024 per thread (row = slot / (T/4), cols 4*(slot % (T/4)) .. +3).
 // VEC: 16-B loads (ld % 4 == 0, 16-B aligned base, full columns checked per slot);
 // otherwise per-element loads.  Rows >= ke and columns >= ncol read as zero.
-template <bool VEC, int T>
+template <bool VEC, int T, int KS>
 __device__ inline void load_step(const float* __restrict__ X, int64_t ld, int64_t ncol,
-                                 int64_t c0, int64_t k0, int64_t ke, float4 (&r)[T / 64]) {
+                                 int64_t c0, int64_t k0, int64_t ke, float4 (&r)[KS * T / 1024]) {
 #pragma unroll
-  for (int h = 0; h < T / 64; ++h) {
+  for (int h = 0; h < KS * T / 1024; ++h) {
     const int slot = threadIdx.x + 256 * h;
     const int64_t k = k0 + slot / (T / 4);
     const int64_t c = c0 + 4 * (slot % (T / 4));
@@ -49,10 +49,10 @@ __device__ inline void load_step(const float* __restrict__ X, int64_t ld, int64_
   }
 }
 
-template <int T>
-__device__ inline void store_step(float* lds, const float4 (&r)[T / 64]) {
+template <int T, int KS>
+__device__ inline void store_step(float* lds, const float4 (&r)[KS * T / 1024]) {
 #pragma unroll
-  for (int h = 0; h < T / 64; ++h) {
+  for (int h = 0; h < KS * T / 1024; ++h) {
     const int slot = threadIdx.x + 256 * h;
     *reinterpret_cast<float4*>(lds + (slot / (T / 4)) * (T + 4) + 4 * (slot % (T / 4))) = r[h];
   }
@@ -60,21 +60,23 @@ __device__ inline void store_step(float* lds, const float4 (&r)[T / 64]) {
 
 // Block: 4 waves as 2x2 wave tiles of T/2 x T/2 (NT x NT MFMA 32x32 tiles each, NT = T/64)
 // over a T x T output super-tile; K slice [kb, ke) streamed through double-buffered LDS
-// with a register prefetch of the next 16-row step (one barrier per step).
+// with a register prefetch of the next KS-row step (one barrier per step).
 // MFMA 32x32x2 f32 operands: lane l supplies A^T[i=l&31][k=l>>5] = A[k][i] and
 // B[k=l>>5][j=l&31]; both are consecutive LDS words across the half-wave.
 // T = 64 serves M, N <= 64 (the d = 64 layers of the minibatch step): the 128 tile spent
-// 3/4 of its MFMAs on zero padding and was MFMA-bound at 4x the useful work.  Every
-// output element sees the same MFMA sequence over the same split either way (bitwise
-// the same partials).
-template <bool VEC, int T>
+// 3/4 of its MFMAs on zero padding and was MFMA-bound at 4x the useful work.  Its steps
+// are KS = 64 rows (8 KB of each operand per block in flight, not 2): at 16 rows the
+// 512 blocks kept 4 MB in flight and a 200k-row gradient ran latency-bound at 2 TB/s.
+// Rows past the split read as zero and add exact zeros, so the partials do not depend on
+// KS: every output element sees the same MFMA sequence over the same split.
+template <bool VEC, int T, int KS>
 __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
     int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part,
     float* __restrict__ part_b) {
-  constexpr int NT = T / 64, S = T + 4;
-  __shared__ float As[2][kKStep * S];
-  __shared__ float Bs[2][kKStep * S];
+  constexpr int NT = T / 64, S = T + 4, LI = KS * T / 1024;
+  __shared__ float As[2][KS * S];
+  __shared__ float Bs[2][KS * S];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 31, lk = lane >> 5;
   const int wi = (w & 1) * (T / 2), wj = (w >> 1) * (T / 2);
@@ -95,23 +97,23 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
       for (int v = 0; v < 16; ++v) acc[x][y][v] = 0.f;
 
   if (kb < ke) {  // uniform per block
-    float4 ra[NT], rb[NT];
-    load_step<VEC, T>(A, lda, M, i_base, kb, ke, ra);
-    load_step<VEC, T>(B, ldb, N, j_base, kb, ke, rb);
-    store_step<T>(As[0], ra);
-    store_step<T>(Bs[0], rb);
+    float4 ra[LI], rb[LI];
+    load_step<VEC, T, KS>(A, lda, M, i_base, kb, ke, ra);
+    load_step<VEC, T, KS>(B, ldb, N, j_base, kb, ke, rb);
+    store_step<T, KS>(As[0], ra);
+    store_step<T, KS>(Bs[0], rb);
     __syncthreads();
     int buf = 0;
-    for (int64_t k0 = kb; k0 < ke; k0 += kKStep) {
-      const bool more = k0 + kKStep < ke;
+    for (int64_t k0 = kb; k0 < ke; k0 += KS) {
+      const bool more = k0 + KS < ke;
       if (more) {
-        load_step<VEC, T>(A, lda, M, i_base, k0 + kKStep, ke, ra);
-        load_step<VEC, T>(B, ldb, N, j_base, k0 + kKStep, ke, rb);
+        load_step<VEC, T, KS>(A, lda, M, i_base, k0 + KS, ke, ra);
+        load_step<VEC, T, KS>(B, ldb, N, j_base, k0 + KS, ke, rb);
       }
       const float* as = As[buf];
       const float* bs = Bs[buf];
-#pragma unroll
-      for (int s = 0; s < kKStep / 2; ++s) {
+#pragma unroll 8
+      for (int s = 0; s < KS / 2; ++s) {
         const int kr = (2 * s + lk) * S;
         float a[NT], b[NT];
 #pragma unroll
@@ -126,12 +128,12 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
       }
       if (colsum) {
-#pragma unroll
-        for (int r = 0; r < kKStep; ++r) csum += as[r * S + threadIdx.x];
+#pragma unroll 16
+        for (int r = 0; r < KS; ++r) csum += as[r * S + threadIdx.x];
       }
       if (more) {
-        store_step<T>(As[buf ^ 1], ra);
-        store_step<T>(Bs[buf ^ 1], rb);
+        store_step<T, KS>(As[buf ^ 1], ra);
+        store_step<T, KS>(Bs[buf ^ 1], rb);
       }
       __syncthreads();
       buf ^= 1;
@@ -168,14 +170,15 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
   const int64_t pstride = t < mn ? mn : M;
   float s = 0.f;
   if (t < nout) {
+    // this wave's splits w, w+4, w+8, ... summed in order; 16 loads in flight ahead of the
+    // adds (4 made a 512-split sum a chain of 32 round trips)
     int64_t p = w;
-    for (; p + 12 < splits; p += 16) {
-      const float x0 = src[p * pstride], x1 = src[(p + 4) * pstride];
-      const float x2 = src[(p + 8) * pstride], x3 = src[(p + 12) * pstride];
-      s += x0;
-      s += x1;
-      s += x2;
-      s += x3;
+    for (; p + 60 < splits; p += 64) {
+      float x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x[u] = src[(p + 4 * u) * pstride];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += x[u];
     }
     for (; p < splits; p += 4) s += src[p * pstride];
   }
@@ -197,7 +200,10 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
 inline int64_t tn_splits(int64_t K, int64_t M, int64_t N) {
   const int64_t tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   int64_t s = kTargetBlocks / (tiles > 0 ? tiles : 1);
-  const int64_t by_rows = (K + 255) / 256;  // >= 256 rows per split
+  // >= 256 rows per split (128 on the 64 x 64 tile: a short gradient — a 1k-row block
+  // layer — then spreads over 8 blocks instead of 4 serial 16-step chains)
+  const int64_t min_rows = M <= 64 && N <= 64 ? 128 : 256;
+  const int64_t by_rows = (K + min_rows - 1) / min_rows;
   if (s > by_rows) s = by_rows;
   return s < 1 ? 1 : s;
 }
@@ -306,19 +312,19 @@ extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float*
   const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 &&
                    M % 4 == 0 && N % 4 == 0;
   float* part_b = colsum ? workspace + splits * M * N : nullptr;
-  if (M <= 64 && N <= 64) {  // one 64 x 64 tile (the split count is the 128 tile's)
+  if (M <= 64 && N <= 64) {  // one 64 x 64 tile, 64-row steps
     if (vec)
-      hipLaunchKernelGGL((gemm_tn_partial_kernel<true, 64>), grid, dim3(256), 0, s, A, lda, B,
-                         ldb, K, M, N, chunk, workspace, part_b);
+      hipLaunchKernelGGL((gemm_tn_partial_kernel<true, 64, 64>), grid, dim3(256), 0, s, A, lda,
+                         B, ldb, K, M, N, chunk, workspace, part_b);
     else
-      hipLaunchKernelGGL((gemm_tn_partial_kernel<false, 64>), grid, dim3(256), 0, s, A, lda, B,
-                         ldb, K, M, N, chunk, workspace, part_b);
+      hipLaunchKernelGGL((gemm_tn_partial_kernel<false, 64, 64>), grid, dim3(256), 0, s, A, lda,
+                         B, ldb, K, M, N, chunk, workspace, part_b);
   } else if (vec) {
-    hipLaunchKernelGGL((gemm_tn_partial_kernel<true, kTile>), grid, dim3(256), 0, s, A, lda, B,
-                       ldb, K, M, N, chunk, workspace, part_b);
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<true, kTile, kKStep>), grid, dim3(256), 0, s, A,
+                       lda, B, ldb, K, M, N, chunk, workspace, part_b);
   } else {
-    hipLaunchKernelGGL((gemm_tn_partial_kernel<false, kTile>), grid, dim3(256), 0, s, A, lda, B,
-                       ldb, K, M, N, chunk, workspace, part_b);
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<false, kTile, kKStep>), grid, dim3(256), 0, s, A,
+                       lda, B, ldb, K, M, N, chunk, workspace, part_b);
   }
   const int64_t nout = M * N + (colsum ? M : 0);
   hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s,

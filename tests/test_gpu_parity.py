@@ -330,6 +330,47 @@ def test_sampler_bit_exact_vs_oracle(fanout, exclude):
             assert es.size == min(deg, fanout)
 
 
+def test_single_pass_scan_sizes_signs_slots_and_streams():
+    """The chained-tile scan (one launch, decoupled look-back over 4096-entry tiles) against
+    numpy: tile edges, its largest size (4096 tiles) and the first size past it (the
+    three-kernel form), negative and large int64 values (the 62-bit flag values), 300
+    back-to-back scans (the 128-slot ring wraps while earlier scans may still run), scans
+    on two streams at once, and a scan captured into a graph (no slot: three-kernel form)."""
+    from gnnrec import ops
+    rng = np.random.default_rng(9)
+    for n in (4095, 4096, 4097, 64 * 4096 + 1, 1_000_003, 4096 * 4096, 4096 * 4096 + 1):
+        x = rng.integers(0, 3, n).astype(np.int32)
+        got = ops.exclusive_scan(_t(x)).cpu().numpy()
+        np.testing.assert_array_equal(got, np.concatenate([[0], np.cumsum(x.astype(np.int64))]))
+    x = rng.integers(-(1 << 40), 1 << 40, 300_001).astype(np.int64)
+    got = ops.exclusive_scan(_t(x)).cpu().numpy()
+    np.testing.assert_array_equal(got, np.concatenate([[0], np.cumsum(x)]))
+    xs = [rng.integers(0, 1000, int(rng.integers(1, 200_000))).astype(np.int64) for _ in range(300)]
+    dev = [_t(x) for x in xs]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1.wait_stream(torch.cuda.current_stream())
+    s2.wait_stream(torch.cuda.current_stream())
+    outs = []
+    for k, t in enumerate(dev):
+        with torch.cuda.stream(s1 if k % 2 else s2):
+            outs.append(ops.exclusive_scan(t))
+    torch.cuda.synchronize()
+    for x, o in zip(xs, outs):
+        np.testing.assert_array_equal(o.cpu().numpy(), np.concatenate([[0], np.cumsum(x)]))
+    t = _t(rng.integers(0, 7, 50_000).astype(np.int64))
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.exclusive_scan(t)  # warm-up outside the capture
+        with torch.cuda.graph(g, stream=s):
+            cap = ops.exclusive_scan(t)
+    g.replay()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cap.cpu().numpy(),
+                                  np.concatenate([[0], np.cumsum(t.cpu().numpy())]))
+
+
 def test_relabel_and_scan_bit_exact():
     from gnnrec import ops
     rng = np.random.default_rng(4)
