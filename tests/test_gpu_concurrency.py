@@ -48,11 +48,13 @@ def _both(fn, hold=False):
 @pytest.mark.parametrize("hold", [False, True])
 def test_spmm_queue_bitwise(static_mode, d, reduce, weighted, hold):
     from gnnrec import ops
-    n_dst, n_src = 150_000, 40_000
+    n_dst, n_src = 400_000, 40_000  # >= 32 rows per wave: the row kernel takes the queue
     indptr, indices = _csr(n_dst, n_src, 24, 1)
     X = torch.randn(n_src, d, device="cuda")
     ew = torch.rand(indices.numel(), device="cuda") if weighted else None
+    q0, _ = ops.rowq_stats()
     ref, out = _both(lambda: ops.spmm(indptr, indices, X, reduce, edge_weight=ew), hold)
+    assert ops.rowq_stats()[0] > q0  # the second launch did take the queue
     assert torch.equal(ref, out)
     # accumulate in place (a source-range tile onto the partial of earlier tiles)
     base = torch.randn(n_dst, d, device="cuda")
@@ -100,7 +102,7 @@ def test_queue_ring_wraps(static_mode):
     """More launches than the ring has slots (1024): every slot is reset by the last block
     of its previous launch, so reuse starts from zero."""
     from gnnrec import ops
-    n_dst, n_src, d = 70_000, 5_000, 32
+    n_dst, n_src, d = 300_000, 5_000, 32  # >= 32 rows per wave of the grid: queued
     indptr, indices = _csr(n_dst, n_src, 4, 3)
     X = torch.randn(n_src, d, device="cuda")
     ref = ops.spmm(indptr, indices, X, "sum")
