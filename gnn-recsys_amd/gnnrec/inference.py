@@ -152,6 +152,47 @@ class GraphShard:
         self.shard_rows = {nt: padded_shard(n, world) for nt, n in num_nodes.items()
                            if nt != ptype}
         self.rels: Dict[tuple, RelShard] = {}
+        self._graph = None
+        self._full_rows = {}
+
+    @property
+    def ptype_pad(self) -> int:
+        """Rows per rank of the partitioned table gathered in rank order (the largest range)."""
+        b = self.bounds
+        return max(b[r + 1] - b[r] for r in range(self.world))
+
+    def full_in_rows(self, ce):
+        """(indptr [S+1], indices int32) of a relation into a replicated type over this
+        rank's block of destination rows (own_slice): EVERY in-edge of those rows in edge-id
+        order (the reference's mailbox order).  Sources of the partitioned type are numbered
+        as rows of its table all-gathered with `ptype_pad` rows per rank; sources of a
+        replicated type are its rows.  What a reducer that does not split into per-rank
+        partials (the LSTM) runs over at P > 1.  Built once from the graph the shard came
+        from (GraphShard.from_graph)."""
+        hit = self._full_rows.get(ce)
+        if hit is not None:
+            return hit
+        if self._graph is None:
+            raise NotImplementedError(
+                "a relation whose reducer does not split into per-rank partials (lstm) needs "
+                "the whole in-neighbourhood of the rows a rank owns: build the shard with "
+                "GraphShard.from_graph")
+        s_t, _, d_t = ce
+        if d_t == self.ptype:
+            raise ValueError(f"full_in_rows: {ce} ends in the partitioned type")
+        src, dst = self._graph.all_edges(etype=ce)
+        S = self.shard_rows[d_t]
+        lo = self.rank * S
+        sel = (dst >= lo) & (dst < lo + S)
+        src, dst = src[sel], dst[sel] - lo
+        if s_t == self.ptype:
+            bounds = torch.tensor(self.bounds, dtype=torch.int64, device=src.device)
+            owner = torch.searchsorted(bounds, src, right=True) - 1
+            src = owner * self.ptype_pad + (src - bounds[owner])
+        indptr, indices, _ = build_csr(src, dst, S)
+        hit = (indptr.to(self.device), indices.to(self.device))
+        self._full_rows[ce] = hit
+        return hit
 
     @property
     def n_own(self) -> int:
@@ -230,6 +271,7 @@ class GraphShard:
             raise ValueError(f"balance must be 'degree' or 'count', not {balance!r}")
         sh = cls(rank, world, ptype, {nt: g.num_nodes(nt) for nt in g.ntypes},
                  g.canonical_etypes, dev, segments, weight)
+        sh._graph = g  # full_in_rows: the whole in-neighbourhoods of this rank's rows
         for ce in g.canonical_etypes:
             s, d = g.all_edges(etype=ce)
             E = s.numel()
@@ -599,13 +641,18 @@ class ShardedFullGraphPass:
                         partials[ce] = ('fused', msg, reduce, weighted)
                         continue
                 if reduce == 'lstm':
+                    # the recurrence runs over each destination's whole in-edge sequence and
+                    # does not split into per-rank partials: at P > 1 the owner of a block of
+                    # destination rows runs it over their every in-edge, from the partitioned
+                    # table all-gathered (every row: this reducer is off the reference's
+                    # hyper-parameter space and is not sized for C4)
                     if self.ex.ws > 1:
-                        raise NotImplementedError(
-                            "the LSTM reducer runs over each destination's whole in-edge "
-                            "sequence and does not split into per-rank partials: run the "
-                            "lstm aggregator with one rank")
-                    partials[ce] = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm'), None,
-                                    reduce)
+                        ip, ix = sh.full_in_rows(ce)
+                        src = self._gather_ptype(msg) if ce[0] == sh.ptype else msg
+                        own = self._lstm(mod, ip, ix, src)
+                    else:
+                        own = self._lstm(mod, rs.indptr, rs.indices, msg)
+                    partials[ce] = (own, None, reduce)
                     continue
                 with self._time('spmm'):
                     part = O.spmm(rs.indptr, rs.indices, msg, 'max' if reduce == 'max' else 'sum',
@@ -616,6 +663,25 @@ class ShardedFullGraphPass:
                 partials[ce] = (own, work, reduce)
             partials.update(self._tree_partials(tree_rels))
         return partials
+
+    def _lstm(self, mod, indptr, indices, m):
+        """ConvLayer._lstm_reducer (src/model.py:106-121) over a CSR on this pass's backend."""
+        L = mod.lstm
+        return self.ops.lstm_aggregate(indptr, indices, m, L.weight_ih_l0, L.weight_hh_l0,
+                                       L.bias_ih_l0, L.bias_hh_l0)
+
+    def _gather_ptype(self, rows):
+        """This rank's rows of the partitioned type -> the table of every rank's rows,
+        `ptype_pad` rows per rank in rank order (GraphShard.full_in_rows numbers them)."""
+        sh = self.shard
+        S = sh.ptype_pad
+        pad = torch.zeros((S, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        pad[: rows.shape[0]] = rows
+        out = torch.empty((S * self.ex.ws, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        out, work = self.ex.all_gather_rows(pad, out, async_op=True)
+        if work is not None:  # RCCL / the emulation: the current stream waits for it
+            work.wait()
+        return out
 
     def _tree_partials(self, rels):
         """Σ over each relation's segments in one fixed pairwise tree: the rank folds its
@@ -770,7 +836,7 @@ class ShardedFullGraphPass:
                 ev_prev = self._scratch_ev.pop(('agg', ce), None)
                 if ev_prev is not None:  # the last side-stream GEMM that read this scratch
                     torch.cuda.current_stream(self.shard.device).wait_event(ev_prev)
-                a = (mod.aggregate(rs.indptr, rs.indices, msg, 'lstm') if reduce == 'lstm' else
+                a = (self._lstm(mod, rs.indptr, rs.indices, msg) if reduce == 'lstm' else
                      O.spmm(rs.indptr, rs.indices, msg, reduce,
                             edge_weight=rs.weights if weighted else None,
                             out=self._scratch(('agg', ce), (rs.n_rows, msg.shape[1]),

@@ -26,6 +26,16 @@ def spmm(indptr, indices, X, reduce="mean", edge_weight=None, out=None, empty_ne
     return t
 
 
+def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh, out=None):
+    res = torch.from_numpy(oracle.lstm_reduce(
+        indptr.cpu().numpy(), indices.cpu().numpy(), X.detach().cpu().numpy(),
+        *(w.detach().cpu().numpy() for w in (W_ih, W_hh, b_ih, b_hh))))
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
 def _attn_update(out, t, accum, attn_vec, attn_state):
     """online softmax over relations (the product's ACC_ATTN_* semantics) in numpy."""
     z = t.numpy().astype(np.float64)

@@ -122,6 +122,11 @@ def _run(case, world):
     ("model_het_meannnedge_mean_emb#seg", 1),
     ("model_het_meanedge_max_emb#seg", 2),
     ("model_het_mean_sum_skip#part", 4),
+    # the LSTM reducer at P > 1: the owner of a block of item rows runs it over their every
+    # in-edge from the all-gathered user table (GraphShard.full_in_rows)
+    ("model_bip_lstm_sum_emb", 2),
+    ("model_het_lstm_mean_noemb_nn", 4),
+    ("model_bip_lstm_sum_emb#det", 2),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
     """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a

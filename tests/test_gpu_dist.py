@@ -87,7 +87,8 @@ def _worker(rank, world, port, agg, hetero, d, q, segments=None, det=None, two_r
 
 @pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 32), ("pool_nn_edge", "max", 32),
                                           ("mean", "sum", 128), ("pool_nn", "mean", 128),
-                                          ("mean", "attention", 128), ("mean_edge", "attention", 32)])
+                                          ("mean", "attention", 128), ("mean_edge", "attention", 32),
+                                          ("lstm", "sum", 32)])  # item rows: full_in_rows
 def test_two_ranks_one_gpu_match_single_process(agg, hetero, d):
     import torch.multiprocessing as mp
     from gnnrec.inference import full_graph_embeddings
