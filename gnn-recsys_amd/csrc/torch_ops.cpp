@@ -988,6 +988,109 @@ void lstm_step(const Tensor& P, const Tensor& indptr, const Tensor& indices, con
      "gnnrec_lstm_step_f32");
 }
 
+// training: the step with its state kept (step-major packing), one step of BPTT, and the
+// slots' source rows / previous-step slots (gnnrec_lstm_step_save_f32 & co., lstm.hip)
+void lstm_step_save(const Tensor& P, const Tensor& indptr, const Tensor& indices,
+                    const Tensor& order, int64_t t, int64_t n_act, const Tensor& h_in,
+                    Tensor& h_out, const optional<Tensor>& c_in, Tensor& c_out, Tensor& z_out,
+                    const Tensor& W_hhT, Tensor& out) {
+  const OneDevice one_device_;
+  dev(P, "P", at::kFloat);
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(order, "order", at::kLong);
+  dev(h_in, "h_in", at::kFloat);
+  dev(h_out, "h_out", at::kFloat);
+  dev(c_in, "c_in", at::kFloat);
+  dev(c_out, "c_out", at::kFloat);
+  dev(z_out, "z_out", at::kFloat);
+  dev(W_hhT, "W_hhT", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t d = h_out.size(1);
+  TORCH_CHECK_VALUE(W_hhT.size(0) == d && W_hhT.size(1) == 4 * d && W_hhT.is_contiguous(),
+                    "W_hhT must be a contiguous [d, 4d]");
+  for (const Tensor* x : std::initializer_list<const Tensor*>{&h_in, &h_out, &c_out})
+    TORCH_CHECK_VALUE(x->is_contiguous() && x->dim() == 2 && x->size(0) >= n_act &&
+                          x->size(1) == d,
+                      "h_in / h_out / c_out must be contiguous [>= n_act, d]");
+  TORCH_CHECK_VALUE(!has(c_in) || (c_in->is_contiguous() && c_in->size(0) >= n_act &&
+                                   c_in->size(1) == d),
+                    "c_in must be a contiguous [>= n_act, d]");
+  TORCH_CHECK_VALUE(z_out.is_contiguous() && z_out.size(0) >= n_act && z_out.size(1) == 4 * d,
+                    "z_out must be a contiguous [>= n_act, 4d]");
+  TORCH_CHECK_VALUE(order.numel() >= n_act, "order shorter than n_act");
+  const int64_t ldp = ld(P, "P"), ldo = ld(out, "out");
+  if (meta(P)) return;
+  const c10::DeviceGuard g(P.device());
+  ck(gnnrec_lstm_step_save_f32(p<float>(P), ldp, p<int64_t>(indptr), p<int32_t>(indices),
+                               p<int64_t>(order), t, n_act, p<float>(h_in), p<float>(h_out),
+                               p<float>(c_in), p<float>(c_out), p<float>(z_out), d,
+                               p<float>(W_hhT), p<float>(out), ldo, stream_of(P)),
+     "gnnrec_lstm_step_save_f32");
+}
+
+void lstm_backward_step(const Tensor& z, const Tensor& c_t, const optional<Tensor>& c_prev,
+                        const optional<Tensor>& dh_next, const optional<Tensor>& dc_next,
+                        int64_t n_next, const Tensor& g_out, const Tensor& order, int64_t n_act,
+                        Tensor& dz, Tensor& dc_prev) {
+  const OneDevice one_device_;
+  dev(z, "z", at::kFloat);
+  dev(c_t, "c_t", at::kFloat);
+  dev(c_prev, "c_prev", at::kFloat);
+  dev(dh_next, "dh_next", at::kFloat);
+  dev(dc_next, "dc_next", at::kFloat);
+  dev(g_out, "g_out", at::kFloat);
+  dev(order, "order", at::kLong);
+  dev(dz, "dz", at::kFloat);
+  dev(dc_prev, "dc_prev", at::kFloat);
+  const int64_t d = c_t.size(1);
+  TORCH_CHECK_VALUE(n_next >= 0 && n_next <= n_act && order.numel() >= n_act,
+                    "lstm_backward_step: need 0 <= n_next <= n_act <= order.numel()");
+  auto rows = [&](const Tensor& x, int64_t n, int64_t w, const char* name) {
+    TORCH_CHECK_VALUE(x.is_contiguous() && x.dim() == 2 && x.size(0) >= n && x.size(1) == w,
+                      name, ": expected a contiguous [>= ", n, ", ", w, "] tensor");
+  };
+  rows(z, n_act, 4 * d, "z");
+  rows(c_t, n_act, d, "c_t");
+  if (has(c_prev)) rows(*c_prev, n_act, d, "c_prev");
+  TORCH_CHECK_VALUE(n_next == 0 || (has(dh_next) && has(dc_next)),
+                    "lstm_backward_step: rows carried from step t+1 need dh_next and dc_next");
+  if (n_next > 0) {
+    rows(*dh_next, n_next, d, "dh_next");
+    rows(*dc_next, n_next, d, "dc_next");
+  }
+  rows(dz, n_act, 4 * d, "dz");
+  rows(dc_prev, n_act, d, "dc_prev");
+  TORCH_CHECK_VALUE(g_out.dim() == 2 && g_out.size(1) == d && g_out.stride(1) == 1,
+                    "g_out must be [n_dst, d] with unit column stride");
+  if (meta(z)) return;
+  const c10::DeviceGuard g(z.device());
+  ck(gnnrec_lstm_backward_step_f32(p<float>(z), p<float>(c_t), p<float>(c_prev),
+                                   p<float>(dh_next), p<float>(dc_next), n_next, p<float>(g_out),
+                                   g_out.stride(0), p<int64_t>(order), n_act, d, p<float>(dz),
+                                   p<float>(dc_prev), stream_of(z)),
+     "gnnrec_lstm_backward_step_f32");
+}
+
+void lstm_slots(const Tensor& indptr, const Tensor& indices, const Tensor& order,
+                const Tensor& step_off, int64_t n_slots, Tensor& src, Tensor& prev) {
+  const OneDevice one_device_;
+  dev(indptr, "indptr", at::kLong);
+  dev(indices, "indices", at::kInt);
+  dev(order, "order", at::kLong);
+  dev(step_off, "step_off", at::kLong);
+  dev(src, "src", at::kLong);
+  dev(prev, "prev", at::kLong);
+  TORCH_CHECK_VALUE(src.numel() >= n_slots && prev.numel() >= n_slots && step_off.dim() == 1,
+                    "lstm_slots: src / prev shorter than n_slots");
+  if (meta(indptr)) return;
+  const c10::DeviceGuard g(indptr.device());
+  ck(gnnrec_lstm_slots(p<int64_t>(indptr), p<int32_t>(indices), p<int64_t>(order),
+                       p<int64_t>(step_off), step_off.numel(), n_slots, p<int64_t>(src),
+                       p<int64_t>(prev), stream_of(indptr)),
+     "gnnrec_lstm_slots");
+}
+
 // ---------------------------------------------------------------- a10 row gather
 void gather_rows(const Tensor& src, const Tensor& idx, Tensor& out) {
   const OneDevice one_device_;
@@ -1428,6 +1531,14 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("tree_sum_(Tensor(a!) a, Tensor[] rest) -> ()");
   m.def("lstm_step(Tensor P, Tensor indptr, Tensor indices, Tensor order, int t, int n_act, "
         "Tensor h_in, Tensor(a!) h_out, Tensor(b!) c, Tensor W_hhT, Tensor(c!) out) -> ()");
+  m.def("lstm_step_save(Tensor P, Tensor indptr, Tensor indices, Tensor order, int t, "
+        "int n_act, Tensor h_in, Tensor(a!) h_out, Tensor? c_in, Tensor(b!) c_out, "
+        "Tensor(c!) z_out, Tensor W_hhT, Tensor(d!) out) -> ()");
+  m.def("lstm_backward_step(Tensor z, Tensor c_t, Tensor? c_prev, Tensor? dh_next, "
+        "Tensor? dc_next, int n_next, Tensor g_out, Tensor order, int n_act, Tensor(a!) dz, "
+        "Tensor(b!) dc_prev) -> ()");
+  m.def("lstm_slots(Tensor indptr, Tensor indices, Tensor order, Tensor step_off, int n_slots, "
+        "Tensor(a!) src, Tensor(b!) prev) -> ()");
   m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) out) -> ()");
   m.def("csr_has_edges(Tensor indptr, Tensor sorted_indices, int n_src, Tensor u, Tensor v, "
         "Tensor(a!) out) -> ()");
@@ -1502,6 +1613,9 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("add_", &add_);                                 \
   m.impl("tree_sum_", &tree_sum_);                       \
   m.impl("lstm_step", &lstm_step);                       \
+  m.impl("lstm_step_save", &lstm_step_save);             \
+  m.impl("lstm_backward_step", &lstm_backward_step);     \
+  m.impl("lstm_slots", &lstm_slots);                     \
   m.impl("gather_rows", &gather_rows);                   \
   m.impl("csr_has_edges", &csr_has_edges);               \
   m.impl("sage_rel_forward", &sage_rel_forward);         \

@@ -74,6 +74,11 @@ SIGNATURES = {
                                        _P, _P]),
     "gnnrec_lstm_step_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P,
                                     _I64, _P]),
+    "gnnrec_lstm_step_save_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P,
+                                         _I64, _P, _P, _I64, _P]),
+    "gnnrec_lstm_backward_step_f32": (_INT, [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _I64,
+                                             _P, _P, _P]),
+    "gnnrec_lstm_slots": (_INT, [_P, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     "gnnrec_spmm_project_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,
                                        _INT, _INT, _INT, _F32, _P, _P, _P, _I64, _P]),
     "gnnrec_spmm_project_mfma_f32": (_INT, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _I64,

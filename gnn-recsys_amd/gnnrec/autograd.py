@@ -95,42 +95,27 @@ def _spmm_reversed(indptr, indices, g, ew, reduce: str, n_src: int, nnz=None):
 
 class LstmAggFn(torch.autograd.Function):
     """agg[v] = LSTM over m[src of v's in-edges] (ConvLayer._lstm_reducer); forward =
-    gnnrec_lstm_step_f32 per step.  Backward re-runs the same degree-sorted recurrence
-    with differentiable device tensor ops and back-propagates through time (the LSTM
-    aggregator is off the reference's hyper-parameter space, main.py:487, so its
-    training path is not a hot path)."""
+    gnnrec_lstm_step_save_f32 per step, keeping every step's hidden / cell rows and gates;
+    backward = back-propagation through time on the HIP kernels
+    (ops.lstm_aggregate_backward: the gate Jacobian per step, dz·W_hh and the weight /
+    input-projection gradients as GEMMs, dP summed per source row by an spmm)."""
 
     @staticmethod
     def forward(ctx, m, W_ih, W_hh, b_ih, b_hh, indptr, indices):
-        out = ops.lstm_aggregate(indptr, indices, m, W_ih, W_hh, b_ih, b_hh)
-        ctx.save_for_backward(m, W_ih, W_hh, b_ih, b_hh, indptr, indices)
+        out, state = ops.lstm_aggregate_train(indptr, indices, m, W_ih, W_hh, b_ih, b_hh)
+        ctx.save_for_backward(m, W_ih, indptr, indices)
+        ctx.state = state
         return out
 
     @staticmethod
     def backward(ctx, g):
-        m, W_ih, W_hh, b_ih, b_hh, indptr, indices = ctx.saved_tensors
-        plan = ops.LstmPlan.of(indptr)
-        with torch.enable_grad():
-            ins = [t.detach().requires_grad_(True) for t in (m, W_ih, W_hh, b_ih, b_hh)]
-            x, wi, wh, bi, bh = ins
-            d = wh.shape[1]
-            P = x @ wi.t() + (bi + bh)
-            h = torch.zeros((plan.n_rows, d), dtype=x.dtype, device=x.device)
-            c = torch.zeros_like(h)
-            beg = indptr[plan.order[:plan.n_rows]]
-            for t, n in enumerate(plan.n_active):
-                src = indices[beg[:n] + t].long()
-                gates = P[src] + h[:n] @ wh.t()
-                i, f = torch.sigmoid(gates[:, :d]), torch.sigmoid(gates[:, d:2 * d])
-                gg, o = torch.tanh(gates[:, 2 * d:3 * d]), torch.sigmoid(gates[:, 3 * d:])
-                cn = f * c[:n] + i * gg
-                c = torch.cat([cn, c[n:]])
-                h = torch.cat([o * torch.tanh(cn), h[n:]])
-            out = torch.zeros((indptr.numel() - 1, d), dtype=x.dtype, device=x.device)
-            out = out.index_copy(0, plan.order[:plan.n_rows], h)
-            grads = torch.autograd.grad(out, ins, g, allow_unused=True)
-        return tuple(gr if need else None for gr, need in
-                     zip(grads, ctx.needs_input_grad[:5])) + (None, None)
+        m, W_ih, indptr, indices = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dX, dW_ih, dW_hh, db = ops.lstm_aggregate_backward(indptr, indices, m, W_ih, ctx.state,
+                                                          g, need_x=need[0])
+        ctx.state = None
+        return (dX, dW_ih if need[1] else None, dW_hh if need[2] else None,
+                db if need[3] else None, db if need[4] else None, None, None)
 
 
 class SageProjectFn(torch.autograd.Function):

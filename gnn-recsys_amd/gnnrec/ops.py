@@ -823,6 +823,86 @@ def lstm_aggregate(indptr, indices, X, W_ih, W_hh, b_ih, b_hh,
     return out
 
 
+def lstm_aggregate_train(indptr, indices, X, W_ih, W_hh, b_ih, b_hh):
+    """lstm_aggregate keeping what the backward needs: every step's hidden and cell rows and
+    pre-activation gates in a step-major packing (step t: rows order[0..n_t) at slots
+    [off[t], off[t] + n_t)).  -> (out [n_dst, d], state for lstm_aggregate_backward)."""
+    T = _T()
+    _dev(indptr, "indptr", torch.int64)
+    _dev(indices, "indices", torch.int32)
+    d = W_hh.shape[1]
+    n_dst = indptr.numel() - 1
+    plan = LstmPlan.of(indptr)
+    dev = X.device
+    P = gemm(X.contiguous(), W_ih.detach(), bias=(b_ih + b_hh).detach())  # [N_src, 4d]
+    out = torch.zeros((n_dst, d), dtype=torch.float32, device=dev)
+    steps = plan.n_active
+    off = [0]
+    for n in steps:
+        off.append(off[-1] + n)
+    n_slots = off[-1]
+    H = torch.empty((n_slots, d), dtype=torch.float32, device=dev)
+    C = torch.empty((n_slots, d), dtype=torch.float32, device=dev)
+    Z = torch.empty((n_slots, 4 * d), dtype=torch.float32, device=dev)
+    WT = W_hh.detach().t().contiguous()
+    h0 = torch.zeros((plan.n_rows, d), dtype=torch.float32, device=dev)
+    for t, n in enumerate(steps):
+        o, q = off[t], (off[t - 1] if t else 0)
+        T.lstm_step_save(P, indptr, indices, plan.order, t, n, h0[:n] if t == 0 else H[q:q + n],
+                         H[o:o + n], None if t == 0 else C[q:q + n], C[o:o + n], Z[o:o + n], WT,
+                         out)
+    return out, (plan, off, H, C, Z, WT)
+
+
+def lstm_aggregate_backward(indptr, indices, X, W_ih, state, g, need_x: bool = True):
+    """Backward through time of lstm_aggregate_train on the HIP kernels: per step (t
+    descending) the gate Jacobian (gnnrec_lstm_backward_step_f32) and dh_{t-1} = dz·W_hh (a
+    GEMM); then dW_hh = Σ_t dz_tᵀ h_{t-1} (one split-K GEMM over the slots, h_{t-1} rows
+    gathered to the slots' order), dP = dz summed per source row (the slots' CSR by source,
+    one spmm), dX = dP·W_ih, dW_ih = dPᵀ X and db = Σ dP (the same split-K pass).
+    -> (dX or None, dW_ih, dW_hh, db)."""
+    T = _T()
+    plan, off, H, C, Z, WT = state
+    steps = plan.n_active
+    d = WT.shape[0]
+    dev = Z.device
+    n_slots = off[-1]
+    n_src = X.shape[0]
+    if n_slots == 0:
+        z = torch.zeros
+        return (z(X.shape, device=dev) if need_x else None, z(W_ih.shape, device=dev),
+                z((4 * d, d), device=dev), z(4 * d, device=dev))
+    g = g.contiguous()
+    dZ = torch.empty((n_slots, 4 * d), dtype=torch.float32, device=dev)
+    dc = [torch.empty((plan.n_rows, d), dtype=torch.float32, device=dev) for _ in range(2)]
+    dh_next = dc_next = None
+    n_next = 0
+    for t in reversed(range(len(steps))):
+        n, o = steps[t], off[t]
+        q = off[t - 1] if t else 0
+        dcp = dc[t % 2][:n]
+        T.lstm_backward_step(Z[o:o + n], C[o:o + n], C[q:q + n] if t else None, dh_next,
+                             dc_next, n_next, g, plan.order, n, dZ[o:o + n], dcp)
+        if t:
+            dh_next = gemm(dZ[o:o + n], WT)  # dz · W_hh
+            dc_next, n_next = dcp, n
+    src = torch.empty(n_slots, dtype=torch.int64, device=dev)
+    prev = torch.empty(n_slots, dtype=torch.int64, device=dev)
+    T.lstm_slots(indptr, indices, plan.order,
+                 torch.tensor(off[:-1], dtype=torch.int64, device=dev), n_slots, src, prev)
+    if len(steps) > 1:
+        dW_hh = gemm_tn(dZ[off[1]:], gather_rows(H, prev[off[1]:]))
+    else:
+        dW_hh = torch.zeros((4 * d, d), dtype=torch.float32, device=dev)
+    slots = torch.arange(n_slots, dtype=torch.int64, device=dev)
+    ip, ix, _ = csr_build(slots, src, n_src)
+    dP = spmm(ip, ix, dZ, "sum")
+    db = torch.empty(4 * d, dtype=torch.float32, device=dev)
+    dW_ih = gemm_tn(dP, X.detach().contiguous(), colsum=db)
+    dX = gemm(dP, W_ih.detach().t().contiguous()) if need_x else None
+    return dX, dW_ih, dW_hh, db
+
+
 def gather_rows(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """a10: src[idx] along dim 0 for a device tensor of any dtype whose rows are contiguous
     (node features into blocks[0].srcdata, edge data into blocks)."""

@@ -38,6 +38,8 @@
  *   - gnnrec_gemm_tn_f32,      <- torch autograd of those layers in the
  *     gnnrec_act_backward_f32     training step, src/train/run.py:124-138
  *   - gnnrec_lstm_step_f32     <- ConvLayer._lstm_reducer src/model.py:106-121
+ *   - gnnrec_lstm_step_save_f32, gnnrec_lstm_backward_step_f32, gnnrec_lstm_slots
+ *                              <- autograd of _lstm_reducer (src/train/run.py:124-138)
  *   - gnnrec_gather_rows       <- blocks[0].srcdata / block edata copies
  *                                 (src/train/run.py:112,340)
  *   - gnnrec_synth_edges       <- (no reference counterpart: synthetic graph
@@ -440,6 +442,35 @@ int gnnrec_lstm_step_f32(const float* P, int64_t ldp, const int64_t* indptr,
                          const int32_t* indices, const int64_t* order, int64_t t, int64_t n_act,
                          const float* h_in, float* h_out, float* c, int64_t d,
                          const float* W_hhT, float* out, int64_t ldo, void* stream);
+
+/* ---- f4/f2: the LSTM reducer's backward through time ----------------------
+ * Replaces torch autograd of ConvLayer._lstm_reducer (src/model.py:106-121) under
+ * loss.backward() (src/train/run.py:124-138).  Training keeps every step's state in a
+ * step-major packing: step t holds rows order[0..n_t) at slots [off[t], off[t] + n_t).
+ *
+ * gnnrec_lstm_step_save_f32: gnnrec_lstm_step_f32 with the state split into c_in (NULL:
+ *   zero, step 0) and c_out, and the pre-activation gates written to z_out [n_act, 4d].
+ * gnnrec_lstm_backward_step_f32: one step t of BPTT for its n_act rows: from z, c_t and
+ *   c_prev (NULL at t = 0) and the gradient arriving at h_t / c_t — dh_next / dc_next
+ *   [n_next, d] for the rows still running at t+1 (p < n_next), g_out[order[p]] (row
+ *   stride ldg) and 0 for the rows whose last step is t — writes dz [n_act, 4d] (gate
+ *   order i, f, g, o) and dc_prev [n_act, d]; dh_{t-1} = dz W_hh is a gnnrec_gemm_f32.
+ * gnnrec_lstm_slots: for every slot s < n_slots, src[s] = the source row the slot's step
+ *   read (indices[indptr[order[p]] + t]) and prev[s] = the same row's slot at t - 1 (-1 at
+ *   t = 0); step_off [n_steps] holds off[t] on the device. */
+int gnnrec_lstm_step_save_f32(const float* P, int64_t ldp, const int64_t* indptr,
+                              const int32_t* indices, const int64_t* order, int64_t t,
+                              int64_t n_act, const float* h_in, float* h_out, const float* c_in,
+                              float* c_out, float* z_out, int64_t d, const float* W_hhT,
+                              float* out, int64_t ldo, void* stream);
+int gnnrec_lstm_backward_step_f32(const float* z, const float* c_t, const float* c_prev,
+                                  const float* dh_next, const float* dc_next, int64_t n_next,
+                                  const float* g_out, int64_t ldg, const int64_t* order,
+                                  int64_t n_act, int64_t d, float* dz, float* dc_prev,
+                                  void* stream);
+int gnnrec_lstm_slots(const int64_t* indptr, const int32_t* indices, const int64_t* order,
+                      const int64_t* step_off, int64_t n_steps, int64_t n_slots, int64_t* src,
+                      int64_t* prev, void* stream);
 
 /* ---- a10: row gather (block features / edge data) -------------------------
  * dst row i (dst_ld_bytes apart) = src row idx[i] (src_ld_bytes apart), row_bytes each,

@@ -31,6 +31,8 @@ RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_t
            "gnnrec_edge_mlp_f32": "edge_mlp", "gnnrec_act_backward_f32": "act_backward",
            "gnnrec_act_backward_normed_f32": "act_backward_normed",
            "gnnrec_lstm_step_f32": "lstm_step", "gnnrec_topk_rows_f32": "topk_rows",
+           "gnnrec_lstm_step_save_f32": "lstm_step_save",
+           "gnnrec_lstm_backward_step_f32": "lstm_backward_step",
            "gnnrec_margin_loss_f32": "margin_loss", "gnnrec_sum_scaled_f32": "sum_scaled"}
 
 
