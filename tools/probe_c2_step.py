@@ -4,7 +4,9 @@ Times 20 steps of the C2 shape (2 conv layers 'mean' d=64, fanout [10,10], 1024 
 neg, cosine head, Adam) and counts the kernels one step launches (torch profiler-free: a
 rocprofv3 --kernel-trace of this script gives the per-kernel split).
 
-    python tools/probe_c2_step.py [K] [num_workers]
+    python tools/probe_c2_step.py [K] [num_workers] [d] [aggregator]
+
+d=128 aggregator=mean_nn K=2500 is the C3 step (BASELINE configs[2]).
 
 GNNREC_SWITCH_INTERVAL=<s>: sys.setswitchinterval for the run (the GIL hand-over period
 between the training thread and a prefetching sampler thread).
@@ -28,11 +30,13 @@ def main():
     nw = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     if os.environ.get("GNNREC_SWITCH_INTERVAL"):
         sys.setswitchinterval(float(os.environ["GNNREC_SWITCH_INTERVAL"]))
+    d = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    agg = sys.argv[4] if len(sys.argv) > 4 else "mean"
     dev = torch.device("cuda")
-    g = c2_graph(64, dev)
+    g = c2_graph(d, dev)
     torch.manual_seed(0)
-    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
-                          "mean", "cos", "sum", True).to(dev)
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
+                          agg, "cos", "sum", True).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=0.005)
     el = EdgeDataLoader(g, {BUYS: torch.arange(50_000_000)}, MultiLayerNeighborSampler([10, 10]),
                         exclude="reverse_types", reverse_etypes={"buys": "bought-by",
@@ -71,7 +75,7 @@ def main():
     host = (time.perf_counter() - t) * 1e3 / n
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t) * 1e3 / n
-    print({"K": K, "num_workers": nw, "fused_head": el.fused_head, "switch_interval": sys.getswitchinterval(),
+    print({"K": K, "d": d, "aggregator": agg, "num_workers": nw, "fused_head": el.fused_head, "switch_interval": sys.getswitchinterval(),
            "wall_ms_per_step": wall, "host_ms_per_step": host,
            "host_phase_ms": {k: v / n for k, v in phases.items()}}, flush=True)
 
