@@ -703,12 +703,12 @@ constexpr int64_t kSplit = 2048;  // ops.DEFAULT_SPLIT: heavy rows of the transp
 float* pw(const Tensor& t) { return t.defined() ? p<float>(t) : nullptr; }
 
 Tensor gemm_nt(const Tensor& A, const Tensor& W, const Tensor* A2, const Tensor* W2, int epi,
-               Tensor out, Tensor* row_norm) {
+               Tensor out, Tensor* row_norm, int accum = GNNREC_ACC_STORE) {
   const int64_t M = A.size(0), K1 = A.size(1), N = W.size(0);
   const int64_t K2 = A2 ? A2->size(1) : 0;
   ck(gnnrec_gemm_rownorm_f32(p<float>(A), ld(A, "A"), K1, p<float>(W), A2 ? p<float>(*A2) : nullptr,
                              A2 ? ld(*A2, "A2") : 1, K2, W2 ? p<float>(*W2) : nullptr, nullptr,
-                             GNNREC_A2_NONE, nullptr, nullptr, M, N, epi, GNNREC_ACC_STORE, 0.f,
+                             GNNREC_A2_NONE, nullptr, nullptr, M, N, epi, accum, 0.f,
                              nullptr, nullptr, p<float>(out), ld(out, "out"),
                              row_norm ? p<float>(*row_norm) : nullptr, stream_of(A)),
      "gnnrec_gemm_f32");
@@ -730,13 +730,14 @@ Tensor weight_grad(const Tensor& gu, const Tensor& X) {  // guᵀ X, split-K MFM
 // sum gather of X over a CSR whose edge count is known on the host but whose degrees are
 // not (the transposed block): heavy rows planned on the device, as ops.spmm does
 void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const Tensor& X,
-                    int64_t nnz, Tensor& out) {
+                    int64_t nnz, Tensor& out, bool accumulate = false) {
   const int64_t n = ip.numel() - 1, d = X.size(1);
   const int64_t cap_h = std::min<int64_t>(n, nnz / (kSplit + 1));
   void* s = stream_of(X);
+  const int flags = accumulate ? GNNREC_SPMM_ACCUM : 0;
   if (cap_h <= 0) {
     ck(gnnrec_spmm_csr_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X), ld(X, "X"), n, d,
-                           GNNREC_REDUCE_SUM, 0, p<float>(out), ld(out, "out"), s),
+                           GNNREC_REDUCE_SUM, flags, p<float>(out), ld(out, "out"), s),
        "gnnrec_spmm_csr_f32");
     return;
   }
@@ -746,7 +747,7 @@ void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const T
      "gnnrec_spmm_plan_build");
   Tensor wsp = at::empty({cap_c, d}, X.options());
   ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),
-                                 ld(X, "X"), n, d, GNNREC_REDUCE_SUM, 0, p<float>(out),
+                                 ld(X, "X"), n, d, GNNREC_REDUCE_SUM, flags, p<float>(out),
                                  ld(out, "out"), kSplit, p<int64_t>(plan), cap_h, cap_c,
                                  p<float>(wsp), s),
      "gnnrec_spmm_csr_planned_f32");
@@ -797,7 +798,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     const Tensor& agg, const Tensor& Ws, const Tensor& Wn, const Tensor& indptr,
     const Tensor& indices, const optional<Tensor>& ew, int64_t reduce, int64_t n_src,
     int64_t nnz, bool norm, int64_t need, const optional<Tensor>& indptr_t_in,
-    const optional<Tensor>& indices_t_in, const optional<Tensor>& w_mean_in) {
+    const optional<Tensor>& indices_t_in, const optional<Tensor>& w_mean_in,
+    const optional<Tensor>& g_self_out, bool g_self_acc, const optional<Tensor>& g_m_out,
+    bool g_m_acc) {
   const OneDevice one_device_;
   dev(gz_in, "gz", at::kFloat);
   dev(z, "z", at::kFloat);
@@ -813,11 +816,22 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
                         indptr.numel() == M + 1 && (!norm || row_norm.numel() == M),
                     "sage_rel_backward: shapes");
   const Tensor gz = gz_in.contiguous();
+  // g_self_out / g_m_out: a layer's gradient tables (autograd.HeteroSageFn) written in place
+  // — stored, or accumulated when *_acc — instead of fresh tensors that autograd then adds
+  dev(g_self_out, "g_self_out", at::kFloat);
+  dev(g_m_out, "g_m_out", at::kFloat);
+  TORCH_CHECK_VALUE(!has(g_self_out) || (g_self_out->is_contiguous() &&
+                                         g_self_out->size(0) == h_self.size(0) &&
+                                         g_self_out->size(1) == Ws.size(1)),
+                    "sage_rel_backward: g_self_out must be a contiguous [h_self rows, d_self]");
+  TORCH_CHECK_VALUE(!has(g_m_out) || (g_m_out->is_contiguous() && g_m_out->size(0) == n_src &&
+                                      g_m_out->size(1) == Wn.size(1)),
+                    "sage_rel_backward: g_m_out must be a contiguous [n_src, d_neigh]");
   Tensor none = at::empty({0}, z.options());  // outputs not asked for (`need` bits)
   Tensor g_self = none, g_m = none, g_Ws = none, g_Wn = none;
   if (meta(z)) {
-    if (need & 1) g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
-    if (need & 2) g_m = at::empty({n_src, Wn.size(1)}, z.options());
+    if ((need & 1) && !has(g_self_out)) g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
+    if ((need & 2) && !has(g_m_out)) g_m = at::empty({n_src, Wn.size(1)}, z.options());
     if (need & 4) g_Ws = at::empty_like(Ws);
     if (need & 8) g_Wn = at::empty_like(Wn);
     return {g_self, g_m, g_Ws, g_Wn};
@@ -836,10 +850,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
        "gnnrec_act_backward_f32");
   }
   if (need & 1) {  // gu Ws over the whole source table of the dst type (zero past M)
-    g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
+    const bool acc = has(g_self_out) && g_self_acc;
+    g_self = has(g_self_out) ? *g_self_out : at::empty({h_self.size(0), Ws.size(1)}, z.options());
     Tensor head = g_self.narrow(0, 0, M);
-    gemm_nt(gu, Ws.t().contiguous(), nullptr, nullptr, 0, head, nullptr);
-    if (h_self.size(0) > M) g_self.narrow(0, M, h_self.size(0) - M).zero_();
+    gemm_nt(gu, Ws.t().contiguous(), nullptr, nullptr, 0, head, nullptr,
+            acc ? GNNREC_ACC_ADD : GNNREC_ACC_STORE);
+    if (!acc && h_self.size(0) > M) g_self.narrow(0, M, h_self.size(0) - M).zero_();
   }
   if (need & 2) {  // transposed gather of g_agg = gu Wn (DGL: the backward of a gSpMM)
     Tensor g_agg = at::empty({M, Wn.size(1)}, z.options());
@@ -868,12 +884,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
                               p<int32_t>(ix_t), pw(w_t), s),
          "gnnrec_csr_transpose");
     }
-    g_m = at::empty({n_src, Wn.size(1)}, z.options());
-    gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m);
+    g_m = has(g_m_out) ? *g_m_out : at::empty({n_src, Wn.size(1)}, z.options());
+    gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m, has(g_m_out) && g_m_acc);
   }
   if (need & 4) g_Ws = weight_grad(gu, h_self.narrow(0, 0, M).contiguous());
   if (need & 8) g_Wn = weight_grad(gu, agg.contiguous());
-  return {g_self, g_m, g_Ws, g_Wn};
+  // gradients written in place come back as empty tensors (the caller holds the tables)
+  return {has(g_self_out) ? none : g_self, has(g_m_out) ? none : g_m, g_Ws, g_Wn};
 }
 
 // Every relation's source-major CSR of one sampled block, in one call (the sampler's
@@ -1548,7 +1565,9 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
         "int reduce, int n_src, int nnz, bool norm, int need, Tensor? indptr_t=None, "
-        "Tensor? indices_t=None, Tensor? w_mean=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor? indices_t=None, Tensor? w_mean=None, Tensor(a!)? g_self_out=None, "
+        "bool g_self_acc=False, Tensor(b!)? g_m_out=None, bool g_m_acc=False) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("block_transposes(Tensor[] indptrs, Tensor[] indices, int[] n_src, int[] nnz) "
         "-> (Tensor[], Tensor[], Tensor[])");
   m.def("edge_batch_pairs(Tensor[] rel_src, Tensor[] rel_dst, int[] src_type, int[] dst_type, "

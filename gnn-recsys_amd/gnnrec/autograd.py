@@ -211,6 +211,118 @@ class SageRelFn(torch.autograd.Function):
                 None, None, None, None, None, None, None)
 
 
+class HeteroSageFn(torch.autograd.Function):
+    """A whole HeteroGraphConv layer of a training step over a sampled block — every
+    relation a SageRelFn-style sum / mean relation, the cross-relation sum / mean — as ONE
+    autograd node.  Its backward writes each node type's input gradient ONCE: the first
+    relation that reaches a table stores into it, the later ones accumulate (the transposed
+    gather with GNNREC_SPMM_ACCUM, the self GEMM with ACC_ADD), so the per-relation
+    gradients are never materialised and added by autograd (C3: ten full-table adds per
+    step, 0.49 ms), and the engine runs one node per layer instead of one per relation.
+
+    apply(spec, *tables, *[W_preagg_r or None, W_self_r, W_neigh_r for r]) -> one output
+    per dst group.  spec = (n_tables, rels, groups): rels[r] = (src table, dst table, reduce,
+    norm, n_dst, indptr, indices, edge weight, transposed); groups[k] = (dst table, relation
+    indices, 'sum' | 'mean').  W_preagg_r: the relation's fc_preagg (messages relu(x W_preᵀ),
+    src/model.py:102,151), whose input gradient is accumulated into the table as well."""
+
+    @staticmethod
+    def forward(ctx, spec, *args):
+        n_t, rels, groups = spec
+        tables = args[:n_t]
+        per = args[n_t:]
+        T = ops._T()
+        zs, saved = [], []
+        msgs = []
+        for r, (si, di, reduce, norm, n_dst, ip, ix, ew, _tr) in enumerate(rels):
+            Wp = per[3 * r]
+            m = tables[si] if Wp is None else ops.gemm(tables[si].contiguous(), Wp.detach(),
+                                                       relu=True)
+            msgs.append(m if Wp is not None else torch.empty(0))
+            Ws, Wn = per[3 * r + 1], per[3 * r + 2]
+            z, agg, nrm = T.sage_rel_forward(m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip,
+                                             ix, ew, ops.REDUCE[reduce], bool(norm))
+            zs.append(z)
+            saved += [agg, z, nrm]
+        outs = []
+        for _di, idx, mode in groups:
+            o = zs[idx[0]]
+            for r in idx[1:]:
+                o = o + zs[r]
+            if mode == 'mean' and len(idx) > 1:
+                o = o / len(idx)
+            outs.append(o)
+        ctx.save_for_backward(*tables, *[t if t is not None else torch.empty(0) for t in per],
+                              *saved, *msgs)
+        ctx.spec = spec
+        ctx.m_given = [per[3 * r] is not None for r in range(len(rels))]
+        ctx.n_src = [tables[rels[r][0]].shape[0] for r in range(len(rels))]
+        ctx.nnz = [ops._nnz(rel[5]) for rel in rels]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *g_outs):
+        n_t, rels, groups = ctx.spec
+        R = len(rels)
+        sv = ctx.saved_tensors
+        tables, per = sv[:n_t], sv[n_t:n_t + 3 * R]
+        saved, msgs = sv[n_t + 3 * R:n_t + 6 * R], sv[n_t + 6 * R:]
+        need = ctx.needs_input_grad[1:]  # (spec)
+        need_t, need_per = need[:n_t], need[n_t:]
+        T = ops._T()
+        g_tab = [None] * n_t
+        g_per = [None] * (3 * R)
+        for gi, (_di, idx, mode) in enumerate(groups):
+            g = g_outs[gi]
+            if g is None:
+                continue
+            g = g.contiguous()
+            if mode == 'mean' and len(idx) > 1:
+                g = g / len(idx)
+            for r in idx:
+                si, di, reduce, norm, _n, ip, ix, ew, tr = rels[r]
+                agg, z, nrm = saved[3 * r:3 * r + 3]
+                Ws, Wn = per[3 * r + 1], per[3 * r + 2]
+                given = ctx.m_given[r]  # messages through fc_preagg
+                want_m = need_t[si] or (given and need_per[3 * r])
+                mask = (1 if need_t[di] else 0) | (2 if want_m else 0) | \
+                    (4 if need_per[3 * r + 1] else 0) | (8 if need_per[3 * r + 2] else 0)
+                kw = {}
+                if need_t[di]:
+                    acc = g_tab[di] is not None
+                    if not acc:
+                        g_tab[di] = torch.empty((tables[di].shape[0], Ws.shape[1]),
+                                                dtype=torch.float32, device=g.device)
+                    kw.update(g_self_out=g_tab[di], g_self_acc=acc)
+                if want_m and not given:
+                    acc = g_tab[si] is not None
+                    if not acc:
+                        g_tab[si] = torch.empty((tables[si].shape[0], Wn.shape[1]),
+                                                dtype=torch.float32, device=g.device)
+                    kw.update(g_m_out=g_tab[si], g_m_acc=acc)
+                t3 = tr if (tr is not None and ew is None) else (None, None, None)
+                _gs, g_m, g_Ws, g_Wn = T.sage_rel_backward(
+                    g, z, nrm, tables[di], agg, Ws.detach(), Wn.detach(), ip, ix, ew,
+                    ops.REDUCE[reduce], ctx.n_src[r], ctx.nnz[r], bool(norm), mask, *t3, **kw)
+                if given and want_m:  # relu(x W_preᵀ): mask, then W_pre's two gradients
+                    gy = ops.act_backward(msgs[r], g_m, relu=True, l2norm=False)
+                    Wp = per[3 * r]
+                    if need_per[3 * r]:
+                        g_per[3 * r] = ops.gemm_tn(gy, tables[si].contiguous())
+                    if need_t[si]:
+                        acc = g_tab[si] is not None
+                        if not acc:
+                            g_tab[si] = torch.empty((tables[si].shape[0], Wp.shape[1]),
+                                                    dtype=torch.float32, device=g.device)
+                        ops.gemm(gy, Wp.detach().t().contiguous(), out=g_tab[si],
+                                 accum='add' if acc else 'store')
+                if need_per[3 * r + 1]:
+                    g_per[3 * r + 1] = g_Ws
+                if need_per[3 * r + 2]:
+                    g_per[3 * r + 2] = g_Wn
+        return (None, *g_tab, *g_per)
+
+
 def sage_rel_fusable(m, h_self, Wn, reduce: str, norm: bool) -> bool:
     """SageRelFn applies: a linear reduce, fp32 row-major tables, the row norm within one
     GEMM block (ops.GEMM_ROW_N)."""
@@ -243,6 +355,37 @@ class CosineFn(torch.autograd.Function):
         ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(),
                                         g.reshape(-1), need[0], need[1])
         return ga, gb, None, None
+
+
+class CosinePairFn(torch.autograd.Function):
+    """CosineFn over the positive and the negative pair graph of one etype at once (they
+    share node ids): one forward launch over both edge lists, and one backward call whose
+    gradients already sum both graphs' parts.  -> (cos_pos, cos_neg)."""
+
+    @staticmethod
+    def forward(ctx, hs, hd, src_p, dst_p, src_n, dst_n):
+        src, dst = torch.cat([src_p, src_n]), torch.cat([dst_p, dst_n])
+        out = ops.sddmm_cos(src, dst, hs.contiguous(), hd.contiguous())
+        ctx.save_for_backward(hs, hd, src, dst)
+        ctx.n_pos = src_p.numel()
+        return out[:ctx.n_pos], out[ctx.n_pos:]
+
+    @staticmethod
+    def backward(ctx, g_pos, g_neg):
+        hs, hd, src, dst = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        if not (need[0] or need[1]):
+            return None, None, None, None, None, None
+        n_pos = ctx.n_pos
+        g = torch.empty(src.numel(), dtype=torch.float32, device=src.device)
+        for part, gp in ((g[:n_pos], g_pos), (g[n_pos:], g_neg)):
+            if gp is None:
+                part.zero_()
+            else:
+                part.copy_(gp.reshape(-1))
+        ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(), g,
+                                        need[0], need[1])
+        return ga, gb, None, None, None, None
 
 
 class MarginLossFn(torch.autograd.Function):

@@ -229,6 +229,35 @@ class HeteroGraphConv(nn.Module):
         div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
         return acc, div
 
+    def _layer_node(self, g, src_inputs, dst_inputs, active):
+        """Training over a block: the whole layer as ONE autograd node (ag.HeteroSageFn,
+        every relation's gradient written into one table per node type), or None."""
+        plan = _layer_plan(self, g, src_inputs, dst_inputs, active)
+        if plan is None:
+            return None
+        types = []
+        for dtype, ce, *_ in plan:
+            for nt in (ce[0], dtype):
+                if nt not in types:
+                    types.append(nt)
+        tix = {nt: i for i, nt in enumerate(types)}
+        rels, per, groups, order = [], [], {}, []
+        for dtype, ce, mod, rg, preagg, weighted, reduce in plan:
+            ew = mod._edge_weight(rg) if weighted else None
+            if dtype not in groups:
+                groups[dtype] = []
+                order.append(dtype)
+            groups[dtype].append(len(rels))
+            rels.append((tix[ce[0]], tix[dtype], reduce, bool(mod.norm),
+                         dst_inputs[dtype].shape[0], rg.indptr, rg.indices, ew,
+                         getattr(rg, 'transposed', None)))
+            per += [mod.fc_preagg.weight if preagg else None, mod.fc_self.weight,
+                    mod.fc_neigh.weight]
+        spec = (len(types), tuple(rels),
+                tuple((tix[dt], tuple(groups[dt]), self.aggregate) for dt in order))
+        outs = ag.HeteroSageFn.apply(spec, *[src_inputs[nt] for nt in types], *per)
+        return dict(zip(order, outs))
+
     def _pair(self, g, ces, src_inputs, h_dst, out) -> bool:
         """Inference, exactly two relations into one type, both pre-projectable
         (ConvLayer._pre_plan): one ops.spmm_project2 launch with the sum / mean / max
@@ -276,6 +305,10 @@ class HeteroGraphConv(nn.Module):
                 continue
             active.setdefault(dtype, []).append(ce)
         grad = _grad_mode(*src_inputs.values(), *dst_inputs.values(), module=self)
+        if grad and active and g.is_block and not isinstance(inputs, tuple):
+            rsts = self._layer_node(g, src_inputs, dst_inputs, active)
+            if rsts is not None:
+                return rsts
         rsts = {}
         for dtype, ces in active.items():
             if grad:
@@ -323,6 +356,30 @@ class HeteroGraphConv(nn.Module):
                                       out, accum, div, attn)
             rsts[dtype] = out
         return rsts
+
+
+def _layer_plan(hconv, g, src_inputs, dst_inputs, active):
+    """The relations of one training layer as ag.HeteroSageFn takes them, or None when a
+    relation needs the per-relation path (max / LSTM reducers, dropout, attention or max
+    across relations, rows wider than one GEMM block, GNNREC_TRAIN_LAYER=0)."""
+    if os.environ.get("GNNREC_TRAIN_LAYER", "1") == "0" or \
+            hconv.aggregate not in ('sum', 'mean'):
+        return None
+    rels = []
+    for dtype, ces in active.items():
+        if dst_inputs[dtype].shape[0] == 0:
+            return None
+        for ce in ces:
+            mod = hconv.mods[ce[1]]
+            if mod._dropout_active():
+                return None
+            rg = g.rel_graph(ce)
+            preagg, weighted, reduce = mod._plan(rg)
+            if not ag.sage_rel_fusable(src_inputs[ce[0]], src_inputs[dtype], mod.fc_neigh.weight,
+                                       reduce, bool(mod.norm)):
+                return None
+            rels.append((dtype, ce, mod, rg, preagg, weighted, reduce))
+    return rels
 
 
 def _pair_combine(aggregate: str):
@@ -417,6 +474,41 @@ class CosinePrediction(nn.Module):
             ratings[etype] = cos.unsqueeze(1)
         return ratings
 
+    def pair(self, pos_g, neg_g, h):
+        """forward(pos_g, h) and forward(neg_g, h) — the same scores — with each etype's
+        positive and negative edges in ONE cosine launch each way (the pair graphs share
+        their node ids): in training one backward call per etype instead of two, and no
+        add of two gradients per endpoint table."""
+        pos, neg = {}, {}
+        for etype in pos_g.canonical_etypes:
+            if etype[0] not in h or etype[2] not in h:
+                continue
+            ps, pd = pos_g.all_edges(etype=etype)
+            if etype not in neg_g.canonical_etypes:
+                pos[etype] = self.forward_one(h, etype, ps, pd)
+                continue
+            ns, nd = neg_g.all_edges(etype=etype)
+            if _grad_mode(h[etype[0]], h[etype[2]]):
+                a, b = ag.CosinePairFn.apply(h[etype[0]], h[etype[2]], ps, pd, ns, nd)
+            else:
+                cos = ops.sddmm_cos(torch.cat([ps, ns]), torch.cat([pd, nd]), h[etype[0]],
+                                    h[etype[2]])
+                a, b = cos[:ps.numel()], cos[ps.numel():]
+            pos[etype], neg[etype] = a.unsqueeze(1), b.unsqueeze(1)
+        for etype in neg_g.canonical_etypes:
+            if etype not in pos and etype[0] in h and etype[2] in h:
+                ns, nd = neg_g.all_edges(etype=etype)
+                neg[etype] = self.forward_one(h, etype, ns, nd)
+        return pos, neg
+
+    @staticmethod
+    def forward_one(h, etype, src, dst):
+        if _grad_mode(h[etype[0]], h[etype[2]]):
+            cos = ag.CosineFn.apply(h[etype[0]], h[etype[2]], src, dst)
+        else:
+            cos = ops.sddmm_cos(src, dst, h[etype[0]], h[etype[2]])
+        return cos.unsqueeze(1)
+
 
 class ConvModel(nn.Module):
     """Embedding layers + ConvLayers + prediction head (src/model.py:330-470)."""
@@ -480,8 +572,12 @@ class ConvModel(nn.Module):
         if embedding_layer:
             h = self.embed(h)
         h = self.get_repr(blocks, h)
-        pos_score = self.pred_fn(pos_g, h)
-        neg_score = self.pred_fn(neg_g, h)
+        if isinstance(self.pred_fn, CosinePrediction) and \
+                os.environ.get("GNNREC_COS_PAIR", "1") != "0":
+            pos_score, neg_score = self.pred_fn.pair(pos_g, neg_g, h)
+        else:
+            pos_score = self.pred_fn(pos_g, h)
+            neg_score = self.pred_fn(neg_g, h)
         return h, pos_score, neg_score
 
 

@@ -489,8 +489,9 @@ def test_fused_training_relation_equals_two_node_form(monkeypatch, agg, hetero, 
                             negative_sampler=negative_sampler.Uniform(3), batch_size=64)
     _, pos_g, neg_g, blocks = next(iter(loader))
 
-    def grads(fused, full_graph):
+    def grads(fused, full_graph, layer=False):
         monkeypatch.setenv("GNNREC_TRAIN_FUSED", "1" if fused else "0")
+        monkeypatch.setenv("GNNREC_TRAIN_LAYER", "1" if layer else "0")
         model.zero_grad()
         if full_graph:
             h = model.embed(g.ndata["features"])
@@ -511,3 +512,52 @@ def test_fused_training_relation_equals_two_node_form(monkeypatch, agg, hetero, 
         assert g1.keys() == g0.keys() and len(g1) > 0
         for n in g1:
             assert torch.equal(g1[n], g0[n]), n
+    # the whole layer as one node (autograd.HeteroSageFn, blocks only): the same forward
+    # bits; a table's gradient sums the relations' parts in the node's own order (four
+    # parts per table here: not bitwise the autograd engine's order)
+    if agg in ("mean", "mean_edge", "mean_nn_edge", "mean_nn") and hetero in ("sum", "mean"):
+        l2, g2 = grads(True, False, layer=True)
+        l0, g0 = grads(False, False)
+        assert torch.equal(l2, l0)
+        assert g2.keys() == g0.keys()
+        for n in g2:
+            torch.testing.assert_close(g2[n], g0[n], rtol=1e-5, atol=1e-6, msg=n)
+
+
+def test_layer_node_two_relations_bitwise(monkeypatch):
+    """C2's shape — one relation into each node type (buys, bought-by) — through the
+    one-node layer (autograd.HeteroSageFn): every table gradient is one relation's gather
+    plus the other's self part, a single add as in autograd's engine, so loss and every
+    parameter gradient equal the per-relation nodes bit for bit."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    rng = np.random.default_rng(21)
+    n_u, n_i, E = 3000, 400, 30000
+    u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+    g = HeteroGraph({BUYS: (torch.from_numpy(u), torch.from_numpy(i)),
+                     BOUGHT: (torch.from_numpy(i), torch.from_numpy(u))},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    g.nodes["user"].data["features"] = torch.randn(n_u, 64, device=DEV)
+    g.nodes["item"].data["features"] = torch.randn(n_i, 64, device=DEV)
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
+                          "mean", "cos", "sum", True).to(DEV)
+    loader = EdgeDataLoader(g, {BUYS: torch.arange(2000)}, MultiLayerNeighborSampler([10, 10]),
+                            exclude="reverse_types",
+                            reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
+                            negative_sampler=negative_sampler.Uniform(10), batch_size=256)
+    _, pos_g, neg_g, blocks = next(iter(loader))
+    res = {}
+    for layer in ("1", "0"):
+        monkeypatch.setenv("GNNREC_TRAIN_LAYER", layer)
+        model.zero_grad()
+        _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+        loss = gnn.max_margin_loss(ps, ns, 0.266, 10)
+        loss.backward()
+        res[layer] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                      if p.grad is not None})
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert res["1"][1].keys() == res["0"][1].keys() and len(res["1"][1]) > 0
+    for n in res["1"][1]:
+        assert torch.equal(res["1"][1][n], res["0"][1][n]), n
