@@ -552,6 +552,7 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
     if comm_ms > 0:
         overlap = max(0.0, min(1.0, (max(compute) + comm_ms - ms_step) / comm_ms))
     return {"backend": str(ex.backend), "collective_path": rec.path, "ranks_seen": world,
+            "all_gather_mode": getattr(ex, "ag_mode", None),
             "rank_compute_ms": [round(c, 2) for c in compute], "rank_edges": edges,
             "comm_ms": comm_ms, "comm_bytes_per_rank": rec.bytes_sent(),
             "collectives_per_pass": len(rec.calls), "overlap_frac": overlap,

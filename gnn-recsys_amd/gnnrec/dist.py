@@ -16,6 +16,7 @@ emulated by all_reduce + slice and all-gather by the list form.
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -79,6 +80,12 @@ class Exchange:
         # a group created without an explicit backend reports e.g. 'cpu:gloo,cuda:nccl'
         self._rccl = self.backend is not None and "nccl" in str(self.backend)
         self.path = None  # 'rccl' | 'emulated' once the first collective has run
+        # all-gather as RCCL's all-gather ('rccl'), or as an all-to-all of the own block
+        # replicated P times ('a2a': every peer reached over its own xGMI link at once
+        # instead of RCCL's ring schedule — SURVEY §5's ring cap); GNNREC_ALLGATHER
+        self.ag_mode = os.environ.get("GNNREC_ALLGATHER", "rccl")
+        if self.ag_mode not in ("rccl", "a2a"):
+            raise ValueError(f"GNNREC_ALLGATHER={self.ag_mode!r}: 'rccl' or 'a2a'")
 
     def _fast(self, t: torch.Tensor) -> bool:
         """RCCL's reduce-scatter / all-gather-into / all-to-all for device tensors on an
@@ -108,6 +115,14 @@ class Exchange:
             if out.data_ptr() != own.data_ptr():
                 out.copy_(own)
             return out, None
+        if self.ag_mode == "a2a":
+            # block j of every rank's input is its own block: all-to-all delivers rank j's
+            # block into slot j everywhere (one local copy of P blocks to stage it)
+            self._fast(own)
+            src = own.unsqueeze(0).expand((self.ws,) + tuple(own.shape)).contiguous()
+            work = dist.all_to_all_single(out, src.view(out.shape), group=self.group,
+                                          async_op=async_op)
+            return out, work
         if self._fast(own):
             work = dist.all_gather_into_tensor(out, own.contiguous(), group=self.group,
                                                async_op=async_op)
@@ -417,18 +432,34 @@ class RecordingExchange:
 
     def replay_by_kind(self, device, reps: int = 3) -> dict:
         """Per collective kind, that kind's calls of one pass replayed alone:
-        {kind: {'ms': per call, 'calls': per pass, 'bytes': sent per call, 'busbw_GBs'}}."""
+        {kind: {'ms': per call, 'calls': per pass, 'bytes': sent per call, 'busbw_GBs'}}.
+        The all-gathers are replayed in both forms ('all_gather' as the pass ran them,
+        'all_gather_<other mode>' the alternative of Exchange.ag_mode), so one multi-GPU
+        run shows whether RCCL's ring schedule or the direct all-to-all moves them faster."""
         if self.ws == 1 or not self.calls:
             return {}
         out = {}
         for kind in sorted({c[0] for c in self.calls}):
             calls = [c for c in self.calls if c[0] == kind]
-            sub = RecordingExchange(self.inner)
-            sub.calls = calls
-            ms = sub.replay_ms(device, reps) / len(calls)
-            sent = sum(c[4] for c in calls) / len(calls)
-            out[kind] = {"ms": ms, "calls": len(calls), "bytes": int(sent),
-                         "busbw_GBs": sent / (ms * 1e-3) / 1e9 if ms > 0 else None}
+            modes = [None]
+            if kind == "all_gather" and hasattr(self.inner, "ag_mode") and \
+                    type(self.inner) is Exchange:
+                modes.append("a2a" if self.inner.ag_mode == "rccl" else "rccl")
+            for mode in modes:
+                sub = RecordingExchange(self.inner)
+                sub.calls = calls
+                keep = getattr(self.inner, "ag_mode", None)
+                if mode is not None:
+                    self.inner.ag_mode = mode
+                try:
+                    ms = sub.replay_ms(device, reps) / len(calls)
+                finally:
+                    if mode is not None:
+                        self.inner.ag_mode = keep
+                sent = sum(c[4] for c in calls) / len(calls)
+                out[kind if mode is None else f"{kind}_{mode}"] = {
+                    "ms": ms, "calls": len(calls), "bytes": int(sent),
+                    "busbw_GBs": sent / (ms * 1e-3) / 1e9 if ms > 0 else None}
         return out
 
     def _timed(self, once, device, reps):

@@ -58,13 +58,16 @@ def _worker(rank, world, port, case, q):
         model.eval()
         # default: every collective async with a real work handle (gloo's own async works),
         # as RCCL issues them; "~sync": the blocking emulation
-        ex = Exchange() if xk == "sync" else AsyncEmulatedExchange()
+        # "~a2a": the synchronous Exchange with the all-gather as an all-to-all
+        ex = Exchange() if xk in ("sync", "a2a") else AsyncEmulatedExchange()
+        if xk == "a2a":
+            ex.ag_mode = "a2a"
         shard = GraphShard.from_graph(g, rank, world, "user", device="cpu",
                                       segments=8 if (det or seg) else None)
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
         p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
         out = p.run(shard.local_features(feats), replicate_output=not part)
-        if xk != "sync" and world > 1:  # the pass asked for every collective async
+        if not xk and world > 1:  # the pass asked for every collective async
             assert ex.works_issued > 0 and ex.sync_calls == 0, (ex.works_issued, ex.sync_calls)
         users = gather_partitioned(shard, out["user"], ex)
         res = {"user": users.numpy()}
@@ -107,6 +110,7 @@ def _run(case, world):
 @pytest.mark.parametrize("case,world", [
     ("model_bip_mean_sum_emb", 2),
     ("model_bip_mean_sum_emb~sync", 2),
+    ("model_het_meanedge_max_emb~a2a", 4),
     ("model_het_meannnedge_mean_emb", 2),
     ("model_het_pooledge_sum_noemb_nn", 2),
     ("model_het_meanedge_max_emb", 4),
@@ -164,3 +168,50 @@ def test_sharded_pass_matches_single_process_oracle(case, world):
         return  # attention is build-defined: no reference output to compare with
     for nt in ref:
         np.testing.assert_allclose(results[0][1][nt], a["h/" + nt], rtol=1e-5, atol=1e-5)
+
+
+def _ag_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gnnrec.dist import Exchange, RecordingExchange
+        ex = Exchange()
+        own = torch.arange(6 * 3, dtype=torch.float32).view(6, 3) + 100 * rank
+        res = {}
+        for mode in ("rccl", "a2a"):
+            ex.ag_mode = mode
+            out = torch.full((6 * world, 3), -1.0)
+            got, work = ex.all_gather_rows(own, out, async_op=True)
+            if work is not None:
+                work.wait()
+            res[mode] = got.clone()
+        ex.ag_mode = "rccl"
+        rec = RecordingExchange(ex)
+        rec.all_gather_rows(own, torch.empty(6 * world, 3))
+        kinds = rec.replay_by_kind(torch.device("cpu"), reps=1)
+        q.put((rank, res, sorted(kinds)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_all_gather_as_all_to_all(world):
+    """Exchange.ag_mode 'a2a' (GNNREC_ALLGATHER): the all-gather as an all-to-all of the own
+    block replicated P times gives the all-gather's table, and the multi-GPU diagnostics
+    replay the all-gathers in both forms."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ag_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = torch.cat([torch.arange(18, dtype=torch.float32).view(6, 3) + 100 * r
+                      for r in range(world)])
+    for _, res, kinds in results:
+        assert torch.equal(res["rccl"], want) and torch.equal(res["a2a"], want)
+        assert kinds == ["all_gather", "all_gather_a2a"]
