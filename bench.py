@@ -62,6 +62,8 @@ def parse(argv=None):
                     help="row-kernel schedule: 'auto' (static at one rank; 16 CUs reserved + "
                          "work queue beside RCCL at several) or 'R,Q' (R reserved CUs, Q=1 queue)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--minibatch", choices=["auto", "off"], default="auto",
+                    help="also time the C2 training step (one GPU; a secondary field)")
     ap.add_argument("--cpu-sample", type=float, default=1 / 32,
                     help="fraction of each relation's destination rows the bounded CPU "
                          "baseline aggregates (over the full-size tables and edge stream)")
@@ -486,6 +488,13 @@ def main():
             cpu = {"value": None, "unit": "edges/s", "cores": None, "kind": "port",
                    "sample": f"failed: {exc!r}"}
 
+    mb = None
+    if world == 1 and args.minibatch == "auto":
+        try:
+            mb = minibatch_step(dev)
+        except Exception as exc:  # a secondary measurement never masks the metric
+            mb = {"error": repr(exc)}
+
     if rank == 0:
         wl = (args.config.upper() if (args.users, args.items, args.edges) ==
               (10_000_000, 1_000_000, 500_000_000) else "custom")
@@ -513,9 +522,63 @@ def main():
             "data": "synthetic (counter-hash graph seed 11, N(0,1) features, xavier weights)",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu,
         }
+        if mb is not None:
+            rec["minibatch"] = mb
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def minibatch_step(dev, steps: int = 20, warmup: int = 3):
+    """A secondary record beside the metric: BASELINE configs[1]'s (C2) training step —
+    1M users x 100k items x 50M edges per direction, 2 SAGE layers 'mean' d=64 + NodeEmbedding,
+    fanout [10,10], 1024 positive edges x K uniform negatives, cosine head, max-margin loss,
+    Adam — timed over `steps` steps (sampling, forward, backward, optimizer) with the loader's
+    sampling thread (num_workers=2) and without, at K = 10 and the reference's K = 2500."""
+    from gnnrec import nn as gnn
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    from gnnrec.synth import minibatch_graph
+
+    buys = ("user", "buys", "item")
+    g = minibatch_graph(64, dev)
+    out = {"workload": "C2: 1M users x 100k items, 50M edges/dir, 2 SAGE 'mean' d=64, fanout "
+                       "[10,10], 1024 pos x K neg, cosine head, Adam (fp32, synthetic)",
+           "steps": steps}
+    for K in (10, 2500):
+        for nw in (2, 0):
+            torch.manual_seed(0)
+            model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True,
+                                  0.0, "mean", "cos", "sum", True).to(dev)
+            opt = torch.optim.Adam(model.parameters(), lr=0.005)
+            el = EdgeDataLoader(g, {buys: torch.arange(g.num_edges(buys))},
+                                MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
+                                reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
+                                negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
+                                shuffle=True, num_workers=nw)
+            it = iter(el)
+
+            def step():
+                _, pos_g, neg_g, blocks = next(it)
+                _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+                loss = gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                return loss
+
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                loss = step()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+            out[f"K{K}_num_workers{nw}"] = {"ms_per_step": round(ms, 3),
+                                            "pos_edges_per_s": round(1024 / ms * 1e3),
+                                            "loss": float(loss)}
+            del it, el
+    return out
 
 
 def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev, ms_step):

@@ -111,3 +111,26 @@ def node_features(n: int, d: int, seed: int, device, rows: Optional[slice] = Non
     if rows is not None:
         x = x[rows].contiguous()
     return x
+
+
+def minibatch_graph(d: int, device, n_users: int = 1_000_000, n_items: int = 100_000,
+                    n_edges: int = 50_000_000):
+    """BASELINE configs[1]/[2]'s graph (C2 / C3): users x items, one buys relation and its
+    reverse from the counter-hash edge stream (seed 11), N(0,1) features of width d, a
+    'recency' edge field in [1, 30), both in-CSRs built."""
+    from . import ops
+    from .graph import HeteroGraph
+    buys, bought = ("user", "buys", "item"), ("item", "bought-by", "user")
+    u, i = ops.synth_edges(11, 0, n_edges, n_users, n_items, device)
+    u, i = u.long(), i.long()
+    g = HeteroGraph({buys: (u, i), bought: (i, u)}, {"user": n_users, "item": n_items},
+                    device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(0)
+    g.nodes["user"].data["features"] = torch.randn(n_users, d, generator=gen, device=device)
+    g.nodes["item"].data["features"] = torch.randn(n_items, d, generator=gen, device=device)
+    g.edges["buys"].data["recency"] = torch.randint(1, 30, (n_edges,), device=device)
+    for ce in (buys, bought):
+        g.in_csr(ce)
+    return g
+

@@ -185,7 +185,8 @@ def _ag_worker(rank, world, port, q):
             got, work = ex.all_gather_rows(own, out, async_op=True)
             if work is not None:
                 work.wait()
-            res[mode] = got.clone()
+            res[mode] = got.numpy().copy()  # numpy: pickled by value (a tensor's shared
+            # memory would be gone once this process exits)
         ex.ag_mode = "rccl"
         rec = RecordingExchange(ex)
         rec.all_gather_rows(own, torch.empty(6 * world, 3))
@@ -211,7 +212,8 @@ def test_all_gather_as_all_to_all(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     want = torch.cat([torch.arange(18, dtype=torch.float32).view(6, 3) + 100 * r
-                      for r in range(world)])
+                      for r in range(world)]).numpy()
     for _, res, kinds in results:
-        assert torch.equal(res["rccl"], want) and torch.equal(res["a2a"], want)
+        np.testing.assert_array_equal(res["rccl"], want)
+        np.testing.assert_array_equal(res["a2a"], want)
         assert kinds == ["all_gather", "all_gather_a2a"]

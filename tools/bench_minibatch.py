@@ -38,17 +38,8 @@ def sync_time(fn):
 
 
 def c2_graph(d, dev, n_u=1_000_000, n_i=100_000, E=50_000_000):
-    u, i = ops.synth_edges(11, 0, E, n_u, n_i, dev)
-    u, i = u.long(), i.long()
-    g = HeteroGraph({BUYS: (u, i), BOUGHT: (i, u)}, {"user": n_u, "item": n_i}, device=dev)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0)
-    g.nodes["user"].data["features"] = torch.randn(n_u, d, generator=gen, device=dev)
-    g.nodes["item"].data["features"] = torch.randn(n_i, d, generator=gen, device=dev)
-    g.edges["buys"].data["recency"] = torch.randint(1, 30, (E,), device=dev)
-    for ce in (BUYS, BOUGHT):
-        g.in_csr(ce)
-    return g
+    from gnnrec.synth import minibatch_graph
+    return minibatch_graph(d, dev, n_u, n_i, E)
 
 
 def main():
