@@ -576,7 +576,7 @@ def minibatch_step(dev, steps: int = 20, warmup: int = 3):
             ms = (time.perf_counter() - t0) / steps * 1e3
             out[f"K{K}_num_workers{nw}"] = {"ms_per_step": round(ms, 3),
                                             "pos_edges_per_s": round(1024 / ms * 1e3),
-                                            "loss": float(loss)}
+                                            "loss": float(loss.detach())}
             del it, el
     return out
 
