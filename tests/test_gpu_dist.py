@@ -112,7 +112,7 @@ def test_two_ranks_one_gpu_match_single_process(agg, hetero, d):
 
 @pytest.mark.parametrize("agg,hetero,d", [("mean", "sum", 128), ("mean_edge", "attention", 32)])
 def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
-    """with segments=8 the outputs are bitwise identical at P = 1, 2 and 4
+    """with segments=8 the outputs are bitwise identical at P = 1, 2, 4 and 8
     (the replicated type's sums are the same per-segment partials folded in the same tree
     whatever the rank count; every kernel choice is made from global sizes)."""
     import torch.multiprocessing as mp
@@ -128,7 +128,7 @@ def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
     np.testing.assert_allclose(base[0], ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(base[1], ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
     ctx = mp.get_context("spawn")
-    for world in (2, 4):
+    for world in (2, 4, 8):  # 8 ranks sharing the one GPU: HIP kernels, emulated RCCL
         q = ctx.Queue()
         port = _port()
         procs = [ctx.Process(target=_worker, args=(r, world, port, agg, hetero, d, q, 8))
@@ -148,7 +148,7 @@ def test_deterministic_mode_bitwise_across_world_sizes(agg, hetero, d):
 def test_deterministic_pair_launch_bitwise_across_world_sizes(hetero):
     """Two item->user relations (the C5 shape, small) run as ONE pre-projected
     spmm_project2 launch on every rank — the choice is made from the global user count —
-    so deterministic mode stays bitwise identical at P = 1, 2 and 4."""
+    so deterministic mode stays bitwise identical at P = 1, 2, 4 and 8."""
     import torch.multiprocessing as mp
     from gnnrec.dist import Exchange
     from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
@@ -163,7 +163,7 @@ def test_deterministic_pair_launch_bitwise_across_world_sizes(hetero):
     np.testing.assert_allclose(base[0], ref["user"].cpu().numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(base[1], ref["item"].cpu().numpy(), rtol=1e-4, atol=1e-5)
     ctx = mp.get_context("spawn")
-    for world in (2, 4):
+    for world in (2, 4, 8):
         q = ctx.Queue()
         port = _port()
         procs = [ctx.Process(target=_worker, args=(r, world, port, "mean", hetero, 128, q, 8, None,
