@@ -999,7 +999,9 @@ __device__ __forceinline__ bool walk_next(PairWalk& w, unsigned* rq, int64_t n_d
   return true;
 }
 
-template <bool WA, bool WB>
+// NT: the source rows of relation a (1) or b (2) loaded non-temporally, so the other
+// relation's pre-projected table keeps the caches (0: both temporal)
+template <bool WA, bool WB, int NT = 0>
 __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
     PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
     const float* __restrict__ WaT, const float* __restrict__ WbT,
@@ -1061,9 +1063,10 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
     }
   };
   // relation r's aggregate of row i (bounds beg, end; its first kP2Win indices in LDS)
-  auto gather_row = [&](const PreRel& r, auto weighted, int64_t beg, int64_t end,
+  auto gather_row = [&](const PreRel& r, auto weighted, auto nt, int64_t beg, int64_t end,
                         int pre_idx, Frag<VEC>& acc) __attribute__((always_inline)) {
     constexpr bool W = decltype(weighted)::value;
+    constexpr bool NTR = decltype(nt)::value;
     int64_t base = beg;
     int wlen = kP2Win;
     while (base < end) {
@@ -1080,7 +1083,12 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
           ok[u] = k < cnt;
           const int src = __shfl(myidx, k & 63);
           if (ok[u]) {
-            load_frag<VEC>(val[u], r.Y + (int64_t)src * r.ldy + col);
+            if constexpr (NTR) {
+              const float4 t = ld_stream4(r.Y + (int64_t)src * r.ldy + col);
+              val[u].v[0] = t.x; val[u].v[1] = t.y; val[u].v[2] = t.z; val[u].v[3] = t.w;
+            } else {
+              load_frag<VEC>(val[u], r.Y + (int64_t)src * r.ldy + col);
+            }
           } else {
 #pragma unroll
             for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
@@ -1155,7 +1163,9 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
       const int64_t deg = i < nv ? rba[i + 1] - rba[i] : 0;
-      if (i < nv) gather_row(ra, std::integral_constant<bool, WA>{}, rba[i], rba[i + 1], pa[i], acc);
+      if (i < nv)
+        gather_row(ra, std::integral_constant<bool, WA>{}, std::integral_constant<bool, NT == 1>{},
+                   rba[i], rba[i + 1], pa[i], acc);
       finish_rel(ra, acc, deg, ga[i]);
       nea[i] = deg > 0;
     }
@@ -1169,7 +1179,9 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
       const int64_t deg = i < nv ? rbb[i + 1] - rbb[i] : 0;
-      if (i < nv) gather_row(rb, std::integral_constant<bool, WB>{}, rbb[i], rbb[i + 1], pb[i], acc);
+      if (i < nv)
+        gather_row(rb, std::integral_constant<bool, WB>{}, std::integral_constant<bool, NT == 2>{},
+                   rbb[i], rbb[i + 1], pb[i], acc);
       finish_rel(rb, acc, deg, gb[i]);
       neb[i] = deg > 0;
     }
@@ -1262,6 +1274,11 @@ extern "C" int gnnrec_spmm_project2_f32(
     void* stream) {
   GNNREC_REQUIRE(d == kPD, "gnnrec_spmm_project2_f32: only d = %d (got %lld)", kPD,
                  (long long)d);
+  // GNNREC_SRC_STREAM on one relation: its source rows non-temporal (NT = 1: a, 2: b)
+  int nt = ((reduce_a & GNNREC_SRC_STREAM) ? 1 : 0) | ((reduce_b & GNNREC_SRC_STREAM) ? 2 : 0);
+  if (nt == 3) nt = 0;  // both: nothing to keep in the caches for
+  reduce_a &= ~GNNREC_SRC_STREAM;
+  reduce_b &= ~GNNREC_SRC_STREAM;
   GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
                      (reduce_b == GNNREC_REDUCE_SUM || reduce_b == GNNREC_REDUCE_MEAN),
                  "gnnrec_spmm_project2_f32: pre-projected relations reduce by sum or mean");
@@ -1316,7 +1333,21 @@ extern "C" int gnnrec_spmm_project2_f32(
                          W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,       \
                          attn_vec, out_div, out, ldo, rq, rq_ch);                              \
   } while (0)
-  if (ew_a) {
+  // GNNREC_SPP2_NT=0: every source row temporal whatever the flags (A/B knob)
+  static const bool nt_ok = [] {
+    const char* e = getenv("GNNREC_SPP2_NT");
+    return !(e && e[0] == '0');
+  }();
+  if (pipe && nt && nt_ok && !ew_a && !ew_b) {
+    if (nt == 1)
+      hipLaunchKernelGGL((spmm_project2_pipe_kernel<false, false, 1>), grid, block, 0, s, a, b,
+                         H, ldh, W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,
+                         attn_vec, out_div, out, ldo, rq, rq_ch);
+    else
+      hipLaunchKernelGGL((spmm_project2_pipe_kernel<false, false, 2>), grid, block, 0, s, a, b,
+                         H, ldh, W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,
+                         attn_vec, out_div, out, ldo, rq, rq_ch);
+  } else if (ew_a) {
     if (ew_b) GNNREC_SPP2(true, true);
     else GNNREC_SPP2(true, false);
   } else {

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("GNNREC_LIB", os.path.join(_HERE, "libgnnrec.so"))
 # status codes / enums (mirror include/gnnrec.h)
 OK = 0
 REDUCE_SUM, REDUCE_MEAN, REDUCE_MAX = 0, 1, 2
+SRC_STREAM = 0x100  # spmm_project2: a relation's source rows read non-temporally
 SPMM_EMPTY_NEGINF = 1
 SPMM_ACCUM = 2
 EPI_RELU, EPI_L2NORM, EPI_SIGMOID = 1, 2, 4

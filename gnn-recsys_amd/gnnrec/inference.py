@@ -862,42 +862,10 @@ class ShardedFullGraphPass:
         if ev is not None:
             self._ready[id(o)] = ev
 
-    def _pair(self, hconv, h, ces, out) -> bool:
-        """Exactly two relations into the partitioned type, both linear (sum / mean) with a
-        source table at most half the destination count (C5: clicked-by and bought-by
-        from the 1M items into the 10M users): both source tables pre-projected, then one
-        spmm_project2 launch reads each user row once and writes it once (C5 user side
-        39.0 ms vs 41.0 ms for the two fused launches).  GNNREC_PAIR_FUSE=0 disables it.
-        In deterministic mode the decision uses the global user count (same on every
-        rank); the HeteroGraphConv combine runs in the kernel (sum, mean as /2, max, the
-        attention softmax over the two relations)."""
-        sh, O = self.shard, self.ops
-        T = sh.ptype
-        if getattr(O, 'spmm_project2', None) is None or \
-                os.environ.get("GNNREC_PAIR_FUSE", "1") == "0" or \
-                hconv.aggregate not in ('sum', 'mean', 'max', 'attention'):
-            return False
-        n_dec = sh.num_nodes[T] if self.deterministic else sh.n_own
-        plan = []
-        for ce in ces:
-            mod = hconv.mods[ce[1]]
-            preagg, weighted, reduce = mod._plan_rel(ce)
-            rs = sh.rels[ce]
-            src = h.get(ce[0])
-            if reduce not in ('sum', 'mean') or src is None or \
-                    not O.preproject_pays(src.shape[0], n_dec, reduce):
-                return False
-            plan.append((mod, ce, rs, preagg, weighted, reduce))
-        if bool(plan[0][0].norm) != bool(plan[1][0].norm):
-            return False
-        # eligibility from the tables' shapes and layouts before anything is launched or
-        # waited for (a message is the source table itself, or fc_preagg's fresh output of
-        # the same shape): a refused pair costs no GEMM and no main-stream wait
-        for mod, ce, rs, _, _, _ in plan:
-            if not O.can_spmm_project(rs.indptr, h[ce[0]], h[T], mod.fc_self.weight,
-                                      mod.fc_neigh.weight):
-                return False
-        self_rows = self._get(h, T)
+    def _pair_stage(self, plan, h):
+        """The pair launch's inputs: both relations' messages pre-projected (the source
+        tables × W_neigh,r, into per-relation scratch), the self weights and biases."""
+        O = self.ops
         msgs = [self._message(mod, ce, h, preagg) for mod, ce, _, preagg, _, _ in plan]
         rels, Wself, biases = [], [], []
         for (mod, ce, rs, _, weighted, reduce), msg in zip(plan, msgs):
@@ -909,6 +877,24 @@ class ShardedFullGraphPass:
                          bias_ne))
             Wself.append(Ws)
             biases.append(bias)
+        return rels, Wself, biases
+
+    def _pair(self, hconv, h, ces, out) -> bool:
+        """Exactly two relations into the partitioned type, both linear (sum / mean) with a
+        source table at most half the destination count (C5: clicked-by and bought-by
+        from the 1M items into the 10M users): both source tables pre-projected, then one
+        spmm_project2 launch reads each user row once and writes it once (C5 user side
+        39.0 ms vs 41.0 ms for the two fused launches).  GNNREC_PAIR_FUSE=0 disables it.
+        In deterministic mode the decision uses the global user count (same on every
+        rank); the HeteroGraphConv combine runs in the kernel (sum, mean as /2, max, the
+        attention softmax over the two relations)."""
+        sh, O = self.shard, self.ops
+        T = sh.ptype
+        plan = self._pair_plan(hconv, h, ces)
+        if plan is None:
+            return False
+        rels, Wself, biases = self._pair_stage(plan, h)
+        self_rows = self._get(h, T)
         mod = plan[0][0]
         o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
                         device=self_rows.device)
@@ -922,6 +908,37 @@ class ShardedFullGraphPass:
         self.pair_fused.add((ces[0], ces[1]))
         out[T] = o
         return True
+
+    def _pair_plan(self, hconv, h, ces):
+        """The two relations of a pair launch, or None (shapes and layouts only: nothing is
+        launched or waited for)."""
+        sh, O = self.shard, self.ops
+        T = sh.ptype
+        if getattr(O, 'spmm_project2', None) is None or \
+                os.environ.get("GNNREC_PAIR_FUSE", "1") == "0" or \
+                hconv.aggregate not in ('sum', 'mean', 'max', 'attention'):
+            return None
+        n_dec = sh.num_nodes[T] if self.deterministic else sh.n_own
+        plan = []
+        for ce in ces:
+            mod = hconv.mods[ce[1]]
+            preagg, weighted, reduce = mod._plan_rel(ce)
+            rs = sh.rels[ce]
+            src = h.get(ce[0])
+            if reduce not in ('sum', 'mean') or src is None or \
+                    not O.preproject_pays(src.shape[0], n_dec, reduce):
+                return None
+            plan.append((mod, ce, rs, preagg, weighted, reduce))
+        if bool(plan[0][0].norm) != bool(plan[1][0].norm):
+            return None
+        # eligibility from the tables' shapes and layouts before anything is launched or
+        # waited for (a message is the source table itself, or fc_preagg's fresh output of
+        # the same shape): a refused pair costs no GEMM and no main-stream wait
+        for mod, ce, rs, _, _, _ in plan:
+            if not O.can_spmm_project(rs.indptr, h[ce[0]], h[T], mod.fc_self.weight,
+                                      mod.fc_neigh.weight):
+                return None
+        return plan
 
     def _fused_tag(self, rs, avg):
         """timer tag of a fused launch: 'spmm_project' (VALU kernel) or 'spmm_project_mfma'."""

@@ -641,6 +641,13 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
     D = FUSED_D
     args = []
     n_dst = rel_a[0].numel() - 1
+    # the relation with at most half the other's edges (host counts only: no readback) reads
+    # its source rows non-temporally, leaving the Infinity Cache to the busier table
+    # (GNNREC_SRC_STREAM; C5: bought-by's 100M edges beside clicked-by's 400M)
+    ea, eb = (getattr(r[0], "_gnnrec_nnz", None) for r in (rel_a, rel_b))
+    stream = None
+    if ea is not None and eb is not None and rel_a[4] is None and rel_b[4] is None:
+        stream = "b" if 2 * eb <= ea else "a" if 2 * ea <= eb else None
     for name, (indptr, indices, Y, reduce, ew, bne) in (("a", rel_a), ("b", rel_b)):
         _dev(indptr, f"indptr_{name}", torch.int64)
         _dev(indices, f"indices_{name}", torch.int32)
@@ -656,7 +663,8 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
         if bne is not None:
             _dev(bne, f"bias_nonempty_{name}", torch.float32)
             bne = bne.detach().contiguous()
-        args += [indptr, indices, ew, Y, REDUCE[reduce], bne]
+        args += [indptr, indices, ew, Y,
+                 REDUCE[reduce] | (_lib.SRC_STREAM if stream == name else 0), bne]
     _dev(H, "H", torch.float32)
     _rowmajor(H, "H")
     if combine not in ("add", "max", "attention"):
