@@ -15,8 +15,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 3 --warmup 1 --cpu-baseline off $*"
-ONE="$R/bench.py --steps 1 --warmup 0 --cpu-baseline off $*"
+BENCH="$R/bench.py --steps 3 --warmup 1 --cpu-baseline off --minibatch off $*"
+ONE="$R/bench.py --steps 1 --warmup 0 --cpu-baseline off --minibatch off $*"
 
 python3 -c "import sys, json; sys.path.insert(0, '$R'); import bench; \
 json.dump({'csrc_sha': bench.csrc_digest(), 'bench_args': sys.argv[1:], \
