@@ -74,3 +74,64 @@ def test_random_configurations_match_oracle(seed):
             got = h[nt][: ref[nt].shape[0]].cpu().numpy()
             np.testing.assert_allclose(got, ref[nt], rtol=1e-4, atol=1e-5 * scale,
                                        err_msg=f"{nt} d={d} agg={agg} het={het} emb={emb}")
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_training_steps_layer_node_matches_relation_nodes(monkeypatch, seed):
+    """Randomised training steps over sampled blocks: the whole layer as one autograd node
+    (gnnrec.autograd.HeteroSageFn, GNNREC_TRAIN_LAYER=1) against one node per relation
+    (=0): the same loss bits, parameter gradients within fp32 reassociation (a table's
+    gradient sums up to four relation parts in the node's own order).  Aggregators with and
+    without fc_preagg / edge weights, the max / LSTM-free hetero modes, one or two
+    relations per node type, with and without the embedding."""
+    from gnnrec import nn as gnn
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    rng = np.random.default_rng(5000 + seed)
+    d = int(rng.choice([16, 64, 128]))
+    n_u, n_i = int(rng.integers(200, 2000)), int(rng.integers(50, 500))
+    two = bool(rng.random() < 0.5)
+    rels = {}
+    for f, r, share in (("buys", "bought-by", 1.0), ("clicks", "clicked-by", 0.5))[:2 if two else 1]:
+        E = int(n_u * rng.integers(3, 20) * share)
+        u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
+        rels[("user", f, "item")] = (u, i)
+        rels[("item", r, "user")] = (i, u)
+    g = HeteroGraph({ce: (torch.from_numpy(s), torch.from_numpy(t)) for ce, (s, t) in rels.items()},
+                    {"user": n_u, "item": n_i}, device="cuda")
+    for ce, (s, _) in rels.items():
+        g.edges[ce].data["occurrence"] = torch.from_numpy(rng.integers(1, 9, s.size)).cuda()
+    g.nodes["user"].data["features"] = torch.randn(n_u, d, device="cuda")
+    g.nodes["item"].data["features"] = torch.randn(n_i, d, device="cuda")
+    agg = ["mean", "mean_nn", "mean_edge", "mean_nn_edge"][seed % 4]
+    het = ["sum", "mean"][(seed // 4) % 2]
+    emb = bool(rng.random() < 0.7)
+    torch.manual_seed(seed)
+    model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0, agg,
+                          "cos", het, emb).cuda()
+    buys = ("user", "buys", "item")
+    K = int(rng.integers(1, 6))
+    loader = EdgeDataLoader(g, {buys: torch.arange(min(600, len(rels[buys][0])))},
+                            MultiLayerNeighborSampler([int(rng.integers(2, 8))] * 2),
+                            exclude="reverse_types",
+                            reverse_etypes={"buys": "bought-by", "bought-by": "buys",
+                                            "clicks": "clicked-by", "clicked-by": "clicks"},
+                            negative_sampler=negative_sampler.Uniform(K), batch_size=128)
+    _, pos_g, neg_g, blocks = next(iter(loader))
+    res = {}
+    for layer in ("1", "0"):
+        monkeypatch.setenv("GNNREC_TRAIN_LAYER", layer)
+        model.zero_grad()
+        _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, emb)
+        loss = gnn.max_margin_loss(ps, ns, 0.266, K)
+        loss.backward()
+        res[layer] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                      if p.grad is not None})
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert res["1"][1].keys() == res["0"][1].keys() and len(res["1"][1]) > 0
+    for n in res["1"][1]:
+        if two:
+            torch.testing.assert_close(res["1"][1][n], res["0"][1][n], rtol=1e-5, atol=1e-6,
+                                       msg=n)
+        else:  # one relation per type: every table gradient is a single add either way
+            assert torch.equal(res["1"][1][n], res["0"][1][n]), n
