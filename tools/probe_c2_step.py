@@ -68,7 +68,7 @@ def main():
     for _ in range(3):
         step(False).item()
     torch.cuda.synchronize()
-    n = 20
+    n = int(os.environ.get("GNNREC_PROBE_STEPS", "20"))
     t = time.perf_counter()
     for _ in range(n):
         step(True)
