@@ -61,12 +61,121 @@ __device__ __forceinline__ int ticket_rows(int64_t avg_deg, int64_t n_dst, int64
   return (int)(c < 1 ? 1 : c > 64 ? 64 : c);
 }
 
+// Low-degree rows, d <= LPR * VEC: one group of LPR lanes per row, NPI = 64 / LPR rows per
+// wave.  A wave-per-row launch over a 1M-row CSR at 2-3 edges per row (a K = 2500
+// minibatch's transposed blocks) is a chain of indptr -> indices -> source-row loads per row
+// with 2-3 of its 4-16 neighbour slots busy; here every group walks its own row, so a wave
+// keeps NPI rows' chains in flight.  The reduction order is the wave kernel's: neighbour k of
+// a row goes to partial (k - beg) % NPI in increasing k, and the partials are combined by
+// the same pairwise tree as combine_groups -- bitwise the same rows (tests/test_gpu_parity).
+// No cross-lane traffic: each lane loads the (group-uniform) index and weight itself.
+template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
+__device__ __forceinline__ void group_rows(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
+    float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg) {
+  constexpr int NPI = kWave / LPR;
+  constexpr int U = NPI >= 8 ? NPI : 8;  // neighbours in flight per group; a multiple of NPI
+  const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
+  const int lane = threadIdx.x & 63;
+  const int col = (lane % LPR) * VEC;
+  const bool colok = col < d;
+  const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 4 * NPI;
+  int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * NPI + lane / LPR;
+  int64_t beg = 0, end = 0;
+  if (row < n_dst) {
+    beg = ld_stream(indptr + row);
+    end = ld_stream(indptr + row + 1);
+  }
+  for (; row < n_dst; row += stride) {
+    // the next row's bounds are requested before this row gathers
+    const int64_t nrow = row + stride;
+    int64_t nbeg = 0, nend = 0;
+    if (nrow < n_dst) {
+      nbeg = ld_stream(indptr + nrow);
+      nend = ld_stream(indptr + nrow + 1);
+    }
+    if (end - beg <= max_deg) {  // heavy rows: reduced by the chunk kernels
+      Frag<VEC> p[NPI];
+#pragma unroll
+      for (int i = 0; i < NPI; ++i)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) p[i].v[v] = init;
+      for (int64_t k = beg; k < end; k += U) {
+        const int cnt = (int)(end - k < U ? end - k : U);
+        int src[U];
+        float w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          src[u] = u < cnt ? ld_stream(indices + k + u) : 0;
+          if constexpr (WEIGHTED) w[u] = u < cnt ? ld_stream(ew + k + u) : 0.f;
+        }
+        Frag<VEC> val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < cnt && colok) {
+            load_frag<VEC>(val[u], X + (int64_t)src[u] * ldx + col);
+          } else {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) val[u].v[v] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < cnt) {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+              const float m = WEIGHTED ? val[u].v[v] * w[u] : val[u].v[v];
+              if constexpr (REDUCE == GNNREC_REDUCE_MAX) p[u % NPI].v[v] = fmaxf(p[u % NPI].v[v], m);
+              else p[u % NPI].v[v] += m;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int s = 1; s < NPI; s <<= 1)
+#pragma unroll
+        for (int i = 0; i < NPI; i += 2 * s)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) p[i].v[v] = combine<REDUCE>(p[i].v[v], p[i + s].v[v]);
+      finalize<VEC, REDUCE>(p[0], end - beg, empty_neginf);
+      if (colok) {
+        if (flags & GNNREC_SPMM_ACCUM) accumulate_into<VEC, REDUCE>(p[0], out + row * ldo + col);
+        store_frag<VEC>(out + row * ldo + col, p[0]);
+      }
+    }
+    beg = nbeg;
+    end = nend;
+  }
+}
+
+// Mean degree up to which the group kernel takes a d <= 64 CSR (GNNREC_SPMM_GROUP: 0 = never).
+inline int64_t group_max_avg_deg() {
+  static const int64_t v = [] {
+    const char* e = getenv("GNNREC_SPMM_GROUP");
+    return (int64_t)(e ? atol(e) : 16);
+  }();
+  return v;
+}
+
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
     float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq,
-    int rq_ch) {
+    int rq_ch, int64_t group_deg) {
+  if constexpr (VEC == 4 && (LPR == 8 || LPR == 16)) {  // d in (16, 64]; at LPR 4 the 16
+                                                        // partials cost occupancy
+    // low mean degree: one lane group per row (the choice needs the CSR's edge count,
+    // which only the device holds)
+    if (group_deg > 0 && indptr[n_dst] - indptr[0] <= group_deg * n_dst) {
+      group_rows<LPR, VEC, REDUCE, WEIGHTED>(indptr, indices, ew, X, ldx, n_dst, d, out, ldo,
+                                             flags, max_deg);
+      if (rq != nullptr) rq_finish(rq);
+      return;
+    }
+  }
   const int empty_neginf = flags & GNNREC_SPMM_EMPTY_NEGINF;
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
@@ -258,7 +367,8 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
                      : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
-                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk());
+                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk(),
+                     group_max_avg_deg());
   rowq_launched(ticket, s);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),

@@ -1501,3 +1501,51 @@ def test_spmm2_equals_two_launches_bitwise(reduce, weighted, n_dst):
         if reduce == "max":
             got[(ip[1:] - ip[:-1]) == 0] = 0.0  # empty rows stay -inf with empty_neginf
         np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("d", [64, 48, 32, 20])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("n_dst", [3000, 300_000])
+def test_spmm_group_rows_equal_wave_rows_bitwise(d, reduce, weighted, n_dst):
+    """Low mean degree and d <= 64: spmm_csr_kernel reduces one row per lane group
+    (group_rows) instead of one per wave.  Appending one row that lifts the CSR's mean degree
+    above the group threshold (16) sends the same rows through the wave-per-row path: the
+    shared rows must come out bitwise equal (stored, accumulated, split or not)."""
+    from gnnrec import ops
+    rng = np.random.default_rng(d + n_dst + len(reduce) + weighted)
+    n_src = 50_000
+    deg = rng.integers(0, 7, n_dst)
+    deg[rng.random(n_dst) < 0.1] = 0
+    deg[::997] = rng.integers(20, 300, deg[::997].size)  # some rows past one unroll step
+    deg[5] = 5000  # one row above the default split
+    big = np.append(deg, 17 * (n_dst + 1))
+    ip_low = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ip_big = np.concatenate([[0], np.cumsum(big)]).astype(np.int64)
+    assert ip_low[-1] <= 16 * n_dst and ip_big[-1] > 16 * (n_dst + 1)
+    idx = rng.integers(0, n_src, int(ip_big[-1])).astype(np.int32)
+    w = rng.standard_normal(idx.size).astype(np.float32) if weighted else None
+    X = _t(rng.standard_normal((n_src, d)).astype(np.float32))
+    ti, tw = _t(idx), None if w is None else _t(w)
+    neg = reduce == "max"
+    for split in (ops.DEFAULT_SPLIT, None):
+        low = ops.spmm(_t(ip_low), ti[:int(ip_low[-1])], X, reduce,
+                       edge_weight=None if tw is None else tw[:int(ip_low[-1])],
+                       empty_neginf=neg, split=split)
+        wave = ops.spmm(_t(ip_big), ti, X, reduce, edge_weight=tw, empty_neginf=neg, split=split)
+        assert torch.equal(low, wave[:n_dst])
+    if n_dst < 10_000:
+        ref = oracle.spmm_csr(ip_low, idx[:int(ip_low[-1])], X.cpu().numpy(), reduce,
+                              None if w is None else w[:int(ip_low[-1])])
+        got = low.cpu().numpy()
+        if neg:
+            got[deg == 0] = 0.0
+        np.testing.assert_allclose(got, ref, rtol=RTOL, atol=ATOL * max(1, np.abs(ref).max()))
+    if reduce != "mean":  # accumulate onto existing partials
+        base = torch.randn(n_dst + 1, d, device=DEV)
+        a = ops.spmm(_t(ip_low), ti[:int(ip_low[-1])], X, reduce,
+                     edge_weight=None if tw is None else tw[:int(ip_low[-1])],
+                     out=base[:n_dst].clone(), empty_neginf=neg, accumulate=True)
+        b = ops.spmm(_t(ip_big), ti, X, reduce, edge_weight=tw, out=base.clone(),
+                     empty_neginf=neg, accumulate=True)
+        assert torch.equal(a, b[:n_dst])
