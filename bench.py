@@ -549,7 +549,9 @@ def minibatch_step(dev, warmup: int = 5):
             torch.manual_seed(0)
             model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True,
                                   0.0, "mean", "cos", "sum", True).to(dev)
-            opt = torch.optim.Adam(model.parameters(), lr=0.005)
+            # GNNREC_BENCH_ADAM_FUSED=1: torch's single-launch Adam (the same update)
+            opt = torch.optim.Adam(model.parameters(), lr=0.005,
+                                   fused=os.environ.get('GNNREC_BENCH_ADAM_FUSED') == '1')
             el = EdgeDataLoader(g, {buys: torch.arange(g.num_edges(buys))},
                                 MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                                 reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
