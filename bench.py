@@ -543,15 +543,17 @@ def minibatch_step(dev, warmup: int = 5):
     buys = ("user", "buys", "item")
     g = minibatch_graph(64, dev)
     out = {"workload": "C2: 1M users x 100k items, 50M edges/dir, 2 SAGE 'mean' d=64, fanout "
-                       "[10,10], 1024 pos x K neg, cosine head, Adam (fp32, synthetic)"}
+                       "[10,10], 1024 pos x K neg, cosine head, Adam (torch fused=True; fp32, synthetic)"}
     for K, steps in ((10, 100), (2500, 40)):
         for nw in (2, 0):
             torch.manual_seed(0)
             model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True,
                                   0.0, "mean", "cos", "sum", True).to(dev)
-            # GNNREC_BENCH_ADAM_FUSED=1: torch's single-launch Adam (the same update)
+            # torch's single-launch Adam (the same update as the reference's default
+            # multi-tensor one; C2 K=10 step -0.1..0.3 ms, tools/gpu_r03_adam.sh);
+            # GNNREC_BENCH_ADAM_FUSED=0 keeps the default implementation
             opt = torch.optim.Adam(model.parameters(), lr=0.005,
-                                   fused=os.environ.get('GNNREC_BENCH_ADAM_FUSED') == '1')
+                                   fused=os.environ.get('GNNREC_BENCH_ADAM_FUSED') != '0')
             el = EdgeDataLoader(g, {buys: torch.arange(g.num_edges(buys))},
                                 MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                                 reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
