@@ -37,7 +37,8 @@ def main():
     torch.manual_seed(0)
     model = gnn.ConvModel(g, 3, {"user": d, "item": d, "hidden": d, "out": d}, True, 0.0,
                           agg, "cos", "sum", True).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=0.005)
+    opt = torch.optim.Adam(model.parameters(), lr=0.005,
+                           fused=os.environ.get('GNNREC_BENCH_ADAM_FUSED') != '0')
     el = EdgeDataLoader(g, {BUYS: torch.arange(50_000_000)}, MultiLayerNeighborSampler([10, 10]),
                         exclude="reverse_types", reverse_etypes={"buys": "bought-by",
                                                                   "bought-by": "buys"},
