@@ -67,7 +67,13 @@ def parse(argv=None):
     ap.add_argument("--cpu-sample", type=float, default=1 / 32,
                     help="fraction of each relation's destination rows the bounded CPU "
                          "baseline aggregates (over the full-size tables and edge stream)")
-    return ap.parse_args(argv)
+    ap.add_argument("--p1-digests", default=os.path.join(ROOT, "profiles", "p1_output_digests.json"),
+                    help="committed one-GPU output digests a P > 1 run compares its bits with")
+    ap.add_argument("--record-digest", default=None, metavar="PATH",
+                    help="(one GPU) add this run's output digest to the digest file PATH")
+    ap.add_argument("--pg-timeout", type=float, default=300.0,
+                    help="process-group timeout (s): a stuck collective ends the run, named")
+    return ap.parse_args(argv) if argv is None else ap.parse_known_args(argv)[0]
 
 
 class EventTimers:
@@ -190,8 +196,13 @@ def pmc_traffic(args, world):
     if world != 1:
         return {}, "not the profiled workload (profiles are single-GPU)"
     mine = workload_key(args)
+    def key_of(m):  # a profile whose recorded flags no longer parse is skipped, not fatal
+        try:
+            return workload_key(parse(json.load(open(m)).get("bench_args", [])))
+        except (Exception, SystemExit):
+            return None
     metas = [m for m in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_meta.json")))
-             if workload_key(parse(json.load(open(m)).get("bench_args", []))) == mine]
+             if key_of(m) == mine]
     if not metas:
         return {}, "no PMC profile of this workload"
     cur = [m for m in metas if json.load(open(m)).get("csrc_sha") == csrc_digest()]
@@ -214,6 +225,113 @@ def pmc_traffic(args, world):
         if n:
             out[t] = tot / n
     return out, f"{tag} (csrc {meta['csrc_sha']})"
+
+
+def bits_digest() -> str:
+    """sha256 (16 hex) of every source the pass's output BITS depend on: the HIP/C++
+    sources and build flags, the C header and the Python package (kernel choices).  Keys
+    the committed one-GPU output digests (--p1-digests) a P > 1 run compares against."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    pats = (os.path.join(CSRC, "*.hip"), os.path.join(CSRC, "*.hpp"), os.path.join(CSRC, "*.cpp"),
+            os.path.join(CSRC, "Makefile"), os.path.join(ROOT, "include", "*.h"),
+            os.path.join(ROOT, "gnn-recsys_amd", "gnnrec", "*.py"))
+    for f in sorted(p for pat in pats for p in glob.glob(pat)):
+        h.update(os.path.relpath(f, ROOT).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _signed64(x: int) -> int:
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def output_digest(args, shard, out, rank, world, dev):
+    """{ntype: 32-hex digest} of the pass's whole output — every rank's owned user range and
+    item block (gnnrec.dist.table_digest: global-index-weighted sums, additive over ranks),
+    summed over the ranks mod 2^64, so the value is P-independent whenever the bits are.
+    GNNREC_BENCH_PERTURB_RANK=r flips one bit of rank r's first user row first (the check
+    that a wrong rank is caught)."""
+    from gnnrec.dist import digest_add, table_digest
+    S = shard.shard_rows["item"]
+    lo, hi = rank * S, min((rank + 1) * S, args.items)
+    u = out["user"]
+    pert = os.environ.get("GNNREC_BENCH_PERTURB_RANK")
+    if pert is not None and int(pert) == rank:
+        u = u.clone()
+        u.view(torch.int32).reshape(-1)[:1].bitwise_xor_(1)
+    du = table_digest(u, shard.p_lo)
+    di = table_digest(out["item"][: hi - lo], lo) if hi > lo else (0, 0)
+    if world > 1:
+        t = torch.tensor([_signed64(x) for x in du + di], dtype=torch.int64, device=dev)
+        allr = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        parts = [[int(x) & ((1 << 64) - 1) for x in a.tolist()] for a in allr]
+        du = digest_add(*[p[:2] for p in parts])
+        di = digest_add(*[p[2:] for p in parts])
+    return {"user": f"{du[0]:016x}{du[1]:016x}", "item": f"{di[0]:016x}{di[1]:016x}"}
+
+
+def p1_digest_lookup(path, args):
+    """The committed one-GPU digest of this workload on these sources, or (None, reason)."""
+    try:
+        entries = json.load(open(path)).get("entries", [])
+    except OSError:
+        return None, f"no digest file {os.path.relpath(path, ROOT)}"
+    src, wl = bits_digest(), list(workload_key(args))
+    same_wl = [e for e in entries if e.get("workload") == wl]
+    if not same_wl:
+        return None, "no one-GPU digest of this workload"
+    for e in same_wl:
+        if e.get("sources") == src:
+            return e, f"one-GPU run of sources {src} ({e.get('recorded', '?')})"
+    return None, (f"stale: one-GPU digests exist for sources "
+                  f"{sorted({e.get('sources') for e in same_wl})}, now {src}")
+
+
+def p1_digest_record(path, args, digest, ms_step):
+    try:
+        data = json.load(open(path))
+    except OSError:
+        data = {"about": "bench.py output digests at one GPU (--record-digest), keyed by "
+                         "bits_digest() and workload_key(); a P > 1 run reports "
+                         "bitwise_vs_p1 against them", "entries": []}
+    src, wl = bits_digest(), list(workload_key(args))
+    data["entries"] = [e for e in data["entries"]
+                       if not (e.get("sources") == src and e.get("workload") == wl)]
+    data["entries"].append({"sources": src, "workload": wl, "digest": digest,
+                            "ms_per_step": ms_step,
+                            "recorded": time.strftime("%Y-%m-%d %H:%M:%S")})
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    json.dump(data, open(path, "w"), indent=1)
+
+
+class Heartbeat:
+    """A stderr line every `period` s naming the phase the rank is in: a multi-GPU run that
+    stalls (graph build, first collective, a kernel) says where, long before any timeout."""
+
+    def __init__(self, rank, period=60.0):
+        import threading
+        self.rank, self.period, self.phase, self.t0 = rank, period, "start", time.time()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._loop, daemon=True, name="bench-heartbeat")
+        self._th.start()
+
+    def _loop(self):
+        while not self._stop.wait(self.period):
+            self.say(f"alive, in {self.phase}")
+
+    def say(self, msg):
+        print(f"[bench r{self.rank} +{time.time() - self.t0:.0f}s] {msg}", file=sys.stderr,
+              flush=True)
+
+    def enter(self, phase):
+        self.phase = phase
+        self.say(phase)
+
+    def stop(self):
+        self._stop.set()
 
 
 def cpu_model() -> str:
@@ -336,7 +454,15 @@ def cpu_baseline(args, d):
         # the sample is the single-relation (C4) form on C5's tables and edge count: the
         # same edges, without C5's 80/20 relation split and second projection per type
         wl = "C5 sizes in the C4 form (one relation per node type)"
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
     return {"value": port, "unit": "edges/s", "cores": cores, "kind": "port",
+            "cores_affinity": aff, "cores_machine": os.cpu_count(),
+            "cores_note": (f"{cores} OpenMP threads = the job's CPU lease (OMP_NUM_THREADS="
+                           f"{os.environ.get('OMP_NUM_THREADS', 'unset')}); the process may run "
+                           f"on {aff} of the machine's {os.cpu_count()} logical CPUs"),
             "cpu_model": cpu_model(), "index_add_value": alt, "config": wl,
             "sample": f"{wl} full-size tables ({U}x{d} + {I}x{d} fp32) and edge stream; dst rows "
                       f"[0,{f:g}N) of both relations = {edges // 2} edges/layer; 2 layers, "
@@ -351,16 +477,22 @@ def main():
     dev_idx = local_rank % max(1, torch.cuda.device_count())  # rehearsals may share one GPU
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    hb = Heartbeat(rank)
     if world > 1:
-        # RCCL over xGMI; GNNREC_DIST_BACKEND=gloo rehearses several ranks on one GPU
+        # RCCL over xGMI; GNNREC_DIST_BACKEND=gloo rehearses several ranks on one GPU.  An
+        # explicit timeout: a collective that never completes ends the run with the
+        # watchdog's report (op type, sequence number) instead of a silent hang
+        import datetime
         backend = os.environ.get("GNNREC_DIST_BACKEND", "nccl")
+        hb.enter(f"init_process_group({backend}, timeout {args.pg_timeout:g} s)")
+        tmo = datetime.timedelta(seconds=args.pg_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
 
     from gnnrec import nn as gnn
-    from gnnrec.dist import AsyncEmulatedExchange, Exchange
+    from gnnrec.dist import AsyncEmulatedExchange, Exchange, ProgressExchange
     from gnnrec.inference import ShardedFullGraphPass
     from gnnrec.synth import GraphMeta, bipartite_shard, node_features
 
@@ -373,6 +505,7 @@ def main():
         det = False  # the fixed tree needs a power-of-two segment count divisible by P
     if segments is not None and segments < world:
         segments = None
+    hb.enter("graph build (edge stream, CSRs, source tiles)")
     shard = bipartite_shard(args.users, args.items, args.edges, rank, world, dev,
                             zipf_s=args.zipf, split=split, segments=segments)
     feats = {"user": node_features(args.users, d, 0, dev, slice(shard.p_lo, shard.p_hi)),
@@ -393,6 +526,10 @@ def main():
         conc = (int(r), bool(int(q)))
     runner = ShardedFullGraphPass(model, shard, ex, overlap=not args.no_overlap,
                                   deterministic=det, concurrency=conc)
+    pex = None
+    if world > 1:  # one stderr line per layer and collective; the first pass checks each
+        pex = ProgressExchange(ex, runner)
+        runner.ex, runner.progress = pex, pex.layer_start
     timers = EventTimers()
     runner.timers = timers
     torch.cuda.synchronize()
@@ -404,20 +541,34 @@ def main():
         print(f"[bench] allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "
               f"{torch.cuda.memory_reserved() / 2**30:.1f} GiB", file=sys.stderr, flush=True)
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
+        hb.enter(f"warm-up pass {w}" + (" (every collective waited on)" if pex and w == 0 else ""))
+        if pex is not None:
+            pex.pass_no, pex.checked = -args.warmup + w, w == 0
+        t0 = time.perf_counter()
         out = runner.run(feats, replicate_output=False)
+        torch.cuda.synchronize()
+        hb.say(f"warm-up pass {w} done in {(time.perf_counter() - t0) * 1e3:.1f} ms")
+    if pex is not None:
+        pex.checked = False
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    hb.enter(f"timed region ({args.steps} passes)")
     timers.enabled = True
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        if pex is not None:
+            pex.pass_no = k
         out = runner.run(feats, replicate_output=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    hb.enter(f"timed region done: {elapsed / args.steps * 1e3:.2f} ms per pass on this rank")
+    if pex is not None:
+        runner.ex, runner.progress = ex, None
     if os.environ.get("GNNREC_BENCH_MEMINFO"):
         print(f"[bench] after the timed passes: allocated "
               f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "
@@ -426,7 +577,19 @@ def main():
               f"{torch.cuda.memory_stats().get('num_alloc_retries', 0)}", file=sys.stderr,
               flush=True)
     elapsed = ex.max_scalar(elapsed, dev)
+    hb.enter("output digest")
+    digest = output_digest(args, shard, out, rank, world, dev)
     del out
+    bitwise, digest_src = None, None
+    if world > 1:
+        if det:
+            ref, digest_src = p1_digest_lookup(args.p1_digests, args)
+            if ref is not None:
+                bitwise = ref["digest"] == digest
+        else:
+            digest_src = "fast mode: item sums depend on P (not bitwise P-independent)"
+    if args.record_digest and world == 1 and rank == 0:
+        p1_digest_record(args.record_digest, args, digest, elapsed / args.steps * 1e3)
 
     edges_per_step = 2 * sum(rs.global_edges for rs in shard.rels.values())  # L=2 layers
     value = edges_per_step * args.steps / elapsed
@@ -477,11 +640,13 @@ def main():
 
     diag = None
     if world > 1:
+        hb.enter("multi-GPU diagnostics (collective replay, per-rank compute)")
         diag = multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
                                      ms_step)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        hb.enter("CPU baseline")
         try:
             cpu = cpu_baseline(args, d)
         except Exception as exc:  # the baseline never masks the GPU result
@@ -490,6 +655,7 @@ def main():
 
     mb = None
     if world == 1 and args.minibatch == "auto":
+        hb.enter("minibatch (C2 training step)")
         try:
             mb = minibatch_step(dev)
         except Exception as exc:  # a secondary measurement never masks the metric
@@ -512,6 +678,11 @@ def main():
                                 not runner.concurrency[1] else "queue")
                                + (f", {runner.concurrency[0]} CUs reserved"
                                   if runner.concurrency and runner.concurrency[0] else "")}
+        cfg["output_digest"] = digest  # P-independent in deterministic mode
+        cfg["bits_sources"] = bits_digest()
+        if world > 1:
+            cfg["bitwise_vs_p1"] = bitwise
+            cfg["bitwise_vs_p1_src"] = digest_src
         if diag is not None:
             cfg.update(diag)
         rec = {
@@ -525,6 +696,7 @@ def main():
         if mb is not None:
             rec["minibatch"] = mb
         print(json.dumps(rec), flush=True)
+    hb.stop()
     if world > 1:
         dist.destroy_process_group()
 
@@ -542,8 +714,17 @@ def minibatch_step(dev, warmup: int = 5):
 
     buys = ("user", "buys", "item")
     g = minibatch_graph(64, dev)
+    try:  # the §8d rooflines of the minibatch kernels (sampler, cosine, edge MLP)
+        roof = minibatch_rooflines(dev, g=g)
+    except Exception as exc:  # a secondary measurement never masks the step times
+        roof = {"error": repr(exc)}
     out = {"workload": "C2: 1M users x 100k items, 50M edges/dir, 2 SAGE 'mean' d=64, fanout "
-                       "[10,10], 1024 pos x K neg, cosine head, Adam (torch fused=True; fp32, synthetic)"}
+                       "[10,10], 1024 pos x K neg, cosine head, Adam (torch fused=True; fp32, synthetic)",
+           "rooflines": roof}
+    # the three flat keys of the §8d d3/d4 rooflines
+    out["sampler_GBs"] = roof.get("sampler", {}).get("GBs")
+    out["cosine_frac"] = roof.get("cosine", {}).get("frac")
+    out["edge_mlp_mfma_frac"] = roof.get("edge_mlp", {}).get("mfma_frac")
     for K, steps in ((10, 100), (2500, 40)):
         for nw in (2, 0):
             torch.manual_seed(0)
@@ -585,6 +766,131 @@ def minibatch_step(dev, warmup: int = 5):
     return out
 
 
+MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def minibatch_rooflines(dev, reps: int = 50, g=None):
+    """SURVEY §8d d3/d4 for the minibatch kernels, at BASELINE configs[1]/[2]'s shapes:
+      sampler  (a9 + a10) C2 graph, fanout [10,10], 1024 user + 1024 item seeds: sampled
+               edges/s and GB/s of the a9 byte model — per sampled edge 4 B index read +
+               4 B write + 8 B relabel mark/scan, per seed 16 B indptr — plus the a10 gathers
+               (the block's edge data and input features: read + write); wall time per call
+               (the sampler reads sizes back to the host once per layer)
+      cosine   (a7) C3 pair graph, 1024 pos x 2500 neg edges, d = 128, the compacted tables
+               (1024 user rows, 100k item rows): 1036 B/edge; HIP-event time of the kernel
+      edge_mlp (a8) same pair graph through PredictingModule's tail kernel (relu(P[u]+Q[v])
+               -> 128x32 MFMA -> relu . w3 -> sigmoid): executed MFMA flops 2*128*32 per edge
+               over the kernel's time against the 157.3 TF fp32 MFMA peak, and its gather
+               bytes (2 x 512 + 16 + 4 B/edge) against 8 TB/s; the per-node P/Q GEMMs beside.
+    Kernel times are HIP events on the stream the ops launch on (torch's current stream)."""
+    from gnnrec import ops
+    from gnnrec.nn import PredictingLayer
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    from gnnrec.synth import minibatch_graph
+
+    out = {}
+    if g is None:
+        g = minibatch_graph(64, dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    sampler = MultiLayerNeighborSampler([10, 10])
+
+    def seeds():
+        return {"user": torch.randint(0, g.num_nodes("user"), (1024,), device=dev, generator=gen),
+                "item": torch.randint(0, g.num_nodes("item"), (1024,), device=dev, generator=gen)}
+
+    for _ in range(3):
+        blocks = sampler.sample_blocks(g, seeds())
+    torch.cuda.synchronize()
+    t_tot, e_tot, b_tot = 0.0, 0, 0
+    for _ in range(reps):
+        sd = seeds()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        blocks = sampler.sample_blocks(g, sd)
+        torch.cuda.synchronize()
+        t_tot += time.perf_counter() - t0
+        for b in blocks:
+            for ce in b.canonical_etypes:
+                ne = b.num_edges(ce)
+                nd = b.number_of_dst_nodes(ce[2])
+                e_tot += ne
+                b_tot += 16 * ne + 16 * nd  # a9 model
+                b_tot += 2 * ne * sum(v.element_size() for k, v in b._edata[ce].items())  # a10
+        b0 = blocks[0]
+        for nt in b0.ntypes:
+            for k, v in b0._src[nt].items():
+                if k != "_ID":
+                    b_tot += 2 * v.numel() * v.element_size()  # a10 feature gather
+    ms = t_tot / reps * 1e3
+    out["sampler"] = {"ms_per_call": round(ms, 4), "sampled_edges_per_call": e_tot // reps,
+                      "sampled_edges_per_s": e_tot / t_tot, "bytes_per_call": b_tot // reps,
+                      "GBs": b_tot / t_tot / 1e9, "frac": b_tot / t_tot / 1e9 / HBM_PEAK_GBS,
+                      "shape": "C2 graph, fanout [10,10], 1024 user + 1024 item seeds, 2 blocks",
+                      "timing": "wall per call incl. one size readback per layer"}
+
+    # ---- heads on the C3 pair graph: 1024 positive + 1024 x 2500 negative edges ----------
+    d, n_u, n_i, K = 128, 1024, 100_000, 2500
+    Hs = torch.randn(n_u, d, device=dev, generator=gen)
+    Hd = torch.randn(n_i, d, device=dev, generator=gen)
+    src = torch.cat([torch.arange(n_u, device=dev),
+                     torch.arange(n_u, device=dev).repeat_interleave(K)])
+    dst = torch.randint(0, n_i, (src.numel(),), device=dev, generator=gen)
+    E = src.numel()
+
+    def ev_time(fn, n=reps):
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) / n
+
+    ms = ev_time(lambda: ops.sddmm_cos(src, dst, Hs, Hd))
+    b_alg = E * (2 * d * 4 + 2 * 8 + 4)
+    b_min = (n_u + n_i) * d * 4 + E * (2 * 8 + 4)  # every table row once + the edge stream
+    out["cosine"] = {"ms": round(ms, 4), "edges": E, "bytes_per_launch": b_alg,
+                     "achieved_GBs": b_alg / ms / 1e6, "frac": b_alg / ms / 1e6 / HBM_PEAK_GBS,
+                     "compulsory_bytes": b_min,
+                     "compulsory_frac": b_min / ms / 1e6 / HBM_PEAK_GBS,
+                     "kernel": "sddmm_cos_kernel",
+                     "note": "1036 B/edge algorithmic (SURVEY d4); the 51 MB item table is "
+                             "cache-resident, so frac can exceed 1 — compulsory_frac counts "
+                             "each table row once"}
+
+    torch.manual_seed(0)
+    pl = PredictingLayer(d).to(dev).eval()
+    W1 = pl.hidden_1.weight.detach()
+    with torch.no_grad():
+        P = ops.gemm(Hs, W1[:, :d], bias=pl.hidden_1.bias)
+        Q = ops.gemm(Hd, W1[:, d:])
+    w2, b2 = pl.hidden_2.weight.detach(), pl.hidden_2.bias.detach()
+    w3, b3 = pl.output.weight.detach().reshape(-1), pl.output.bias.detach()
+    ms = ev_time(lambda: ops.edge_mlp(src, dst, P, Q, w2, b2, w3, b3))
+    ms_pq = ev_time(lambda: (ops.gemm(Hs, W1[:, :d], bias=pl.hidden_1.bias),
+                             ops.gemm(Hd, W1[:, d:])))
+    fl = E * (2 * 128 * 32)
+    b_alg = E * (2 * 128 * 4 + 2 * 8 + 4)
+    ref_fl = 2 * E * (2 * d * 128 + 128 * 32 + 32)
+    out["edge_mlp"] = {"ms": round(ms, 4), "edges": E, "mfma_flops": fl,
+                       "TFs": fl / ms / 1e9, "mfma_frac": fl / ms / 1e9 / MFMA_F32_PEAK_TFS,
+                       "bytes_per_launch": b_alg, "achieved_GBs": b_alg / ms / 1e6,
+                       "hbm_frac": b_alg / ms / 1e6 / HBM_PEAK_GBS,
+                       "pq_gemms_ms": round(ms_pq, 4),
+                       "head_ms": round(ms + ms_pq, 4),
+                       "reference_flops": ref_fl,
+                       "reference_equivalent_TFs": ref_fl / (ms + ms_pq) / 1e9,
+                       "kernel": "edge_mlp_kernel",
+                       "note": "W1[hu||hv] re-associated into per-node P, Q (two GEMMs): the "
+                               "per-edge kernel runs only the 128x32 layer on the MFMA; "
+                               "reference_equivalent_TFs prices the reference's per-edge "
+                               "flops over the whole head"}
+    return out
+
+
 def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev, ms_step):
     """Self-diagnosis of a P > 1 run (every rank takes part; rank 0 reports):
       rank_compute_ms  each rank's share of the pass with the same kernels and concurrency
@@ -614,6 +920,17 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
         null.run(feats, replicate_output=False)
     torch.cuda.synchronize()
     mine = (time.perf_counter() - t0) / reps * 1e3
+    # the same pass with the last layer's item all-gather (every rank ends with the whole
+    # item table, as the reference's single-device `y`): what replicate_output costs
+    runner.run(feats, replicate_output=True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(2):
+        runner.run(feats, replicate_output=True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    rep_ms = ex.max_scalar((time.perf_counter() - t0) / 2 * 1e3, dev)
     t = torch.tensor([mine, float(shard.local_edge_count())], dtype=torch.float64, device=dev)
     allr = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(allr, t)
@@ -625,6 +942,7 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
     return {"backend": str(ex.backend), "collective_path": rec.path, "ranks_seen": world,
             "all_gather_mode": getattr(ex, "ag_mode", None),
             "rank_compute_ms": [round(c, 2) for c in compute], "rank_edges": edges,
+            "ms_per_step_replicated_output": round(rep_ms, 3),
             "comm_ms": comm_ms, "comm_bytes_per_rank": rec.bytes_sent(),
             "collectives_per_pass": len(rec.calls), "overlap_frac": overlap,
             # per collective kind, replayed alone: ms per call, bytes each rank sends per

@@ -363,6 +363,91 @@ class ComputeOnlyExchange:
         return x
 
 
+_M64 = (1 << 64) - 1
+
+
+def table_digest(t: torch.Tensor, row0: int = 0, chunk: int = 1 << 24):
+    """Bit-pattern checksum of rows [row0, row0 + len(t)) of a global fp32/int32 table, on
+    the tensor's device: (Σ v_i·(2i+1), Σ v_i·(2i+1)²) mod 2^64 over the int32 views v_i,
+    i = the GLOBAL element index.  Any single changed bit changes both sums, and the sums
+    are additive over disjoint row ranges, so the digests of every rank's owned rows add
+    up (mod 2^64) to the one-process digest of the whole table — a P > 1 run checks its
+    bits against P = 1 without moving the tables (bench.py `bitwise_vs_p1`)."""
+    t = t.contiguous()
+    per_row = t[0].numel() if t.dim() > 1 and t.shape[0] else 1
+    v = t.view(torch.int32).reshape(-1)
+    acc = torch.zeros(2, dtype=torch.int64, device=t.device)
+    for e0 in range(0, v.numel(), chunk):
+        blk = v[e0:e0 + chunk].to(torch.int64)
+        g0 = row0 * per_row + e0
+        w = torch.arange(g0, g0 + blk.numel(), device=t.device, dtype=torch.int64) * 2 + 1
+        bw = blk * w
+        acc[0] += bw.sum()
+        acc[1] += (bw * w).sum()
+    s1, s2 = (int(x) for x in acc.tolist())
+    return s1 & _M64, s2 & _M64
+
+
+def digest_add(*ds):
+    """Sum of (s1, s2) digests of disjoint row ranges, mod 2^64."""
+    return (sum(d[0] for d in ds) & _M64, sum(d[1] for d in ds) & _M64)
+
+
+class ProgressExchange:
+    """Wraps an Exchange and prints one stderr line per collective issued — rank, pass,
+    layer, kind, shape — so a multi-GPU run that stops inside a collective names it.  With
+    `checked` (the bench's first warm-up pass) every collective is also waited on and the
+    device synchronised before the pass goes on, and its completion is printed with its
+    time: on first contact with RCCL a stuck collective is then the last 'issued' line
+    without its 'done', and the process group's timeout ends the run instead of a silent
+    hang.  Everything else is the inner exchange's."""
+
+    def __init__(self, inner, runner=None, stream=None):
+        self.inner, self.runner = inner, runner
+        self.stream = stream if stream is not None else __import__("sys").stderr
+        self.checked = False
+        self.pass_no = 0
+        self.enabled = True
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+    def _say(self, msg):
+        if self.enabled:
+            layer = getattr(self.runner, "_layer_idx", None)
+            print(f"[gnnrec r{self.inner.rk}] pass {self.pass_no} layer {layer} {msg}",
+                  file=self.stream, flush=True)
+
+    def layer_start(self, i):
+        """ShardedFullGraphPass.progress hook: one line per layer."""
+        self._say("start")
+
+    def _call(self, kind, t, fn):
+        import time
+        self._say(f"{kind} {tuple(t.shape)} issued")
+        t0 = time.perf_counter()
+        res = fn()
+        if self.checked:
+            work = res[1]
+            if work is not None:
+                work.wait()
+            if t.is_cuda:
+                torch.cuda.synchronize(t.device)
+            self._say(f"{kind} done in {(time.perf_counter() - t0) * 1e3:.1f} ms")
+        return res
+
+    def reduce_scatter_rows(self, full, op, async_op=False):
+        return self._call("reduce_scatter", full,
+                          lambda: self.inner.reduce_scatter_rows(full, op, async_op))
+
+    def all_to_all_rows(self, full, async_op=False):
+        return self._call("all_to_all", full, lambda: self.inner.all_to_all_rows(full, async_op))
+
+    def all_gather_rows(self, own, out, async_op=False):
+        return self._call("all_gather", out,
+                          lambda: self.inner.all_gather_rows(own, out, async_op))
+
+
 class RecordingExchange:
     """Wraps an Exchange and records every collective of a pass: (kind, shape, dtype, op)
     plus the bytes this rank sends (all-to-all / reduce-scatter: (P−1)/P of the table;

@@ -384,6 +384,7 @@ class ShardedFullGraphPass:
         self.timers = None  # optional callable(tag) -> context manager (bench)
         self.side_delay_us = 0  # tests: a delay kernel ahead of every side-stream task
         self.capture = None  # optional list: every layer's output tables are appended (tests)
+        self.progress = None  # optional callable(layer index) at every layer's start (bench)
         self.fused = set()  # relations whose aggregation ran with the projection fused
         self.pair_fused = set()  # (ce_a, ce_b) run as one pre-projected two-relation launch
         self.tile_pairs = set()  # (relation a, relation b) whose tiles ran as one launch
@@ -516,6 +517,8 @@ class ShardedFullGraphPass:
         for i, layer in enumerate(m.layers):
             self._layer_idx = i
             self._last = i == len(m.layers) - 1
+            if self.progress is not None:
+                self.progress(i)
             h = self._layer(layer, h)
             self._prune_ready(h)
             if self.capture is not None:

@@ -343,9 +343,10 @@ def _layer_rows_vs_oracle(model, layer_idx, h_in, h_out, lists, rows, hetero, ra
 
 @pytest.fixture(scope="module", params=["c4", "c5", "c4zipf"])
 def full_shard(request):
-    """The full-size shard plus the rows checked against the oracle: per node type a
-    contiguous 1/32 slice (312,500 users, 31,250 items — the slice bench.cpu_baseline
-    times) and 1000 random rows; with --zipf 1.0 items also the 100 heaviest, whose
+    """The full-size shard plus the rows checked against the oracle: a contiguous slice
+    per node type — 1/32 of the users (312,500: the slice bench.cpu_baseline times) and
+    1/16 of the items (62,500: at least 50k rows of each type) — and 1000 random rows;
+    with --zipf 1.0 items also the 100 heaviest, whose
     ~180M in-edges (the top item ~35M) run through the chunked heavy-row tiles
     (inference.TILE_SPLIT) and their 16-partial combine."""
     from gnnrec.synth import bipartite_shard, node_features, zipf_cdf
@@ -361,8 +362,9 @@ def full_shard(request):
     for nt, n in (("user", N_U), ("item", N_I)):
         # (under Zipf the item ids are popularity ranks: the first 1/32 of them hold ~3/4 of
         # the edges, so the item slice is taken from the light end there)
-        lo = n - n // 32 if zipf and nt == "item" else 0
-        pick = [torch.arange(lo, lo + n // 32, device=DEV),
+        m = n // 16 if nt == "item" else n // 32
+        lo = n - m if zipf and nt == "item" else 0
+        pick = [torch.arange(lo, lo + m, device=DEV),
                 torch.randperm(n, device=DEV, generator=gen)[:1000]]
         if zipf and nt == "item":
             deg = shard.rels[("user", "buys", "item")].deg_own[:N_I].long()

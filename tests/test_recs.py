@@ -1,7 +1,13 @@
 """Row f1: recommendation top-k + metrics vs the reference's own src/metrics.py
 (golden vectors from tests/golden/make_golden.py).  Recommendation lists must
-match item for item (ties are broken by column index; the goldens contain no
-exact ties), metrics exactly."""
+match item for item, metrics exactly.
+
+Ties: the generator keeps only seeds whose ranked lists have no two consecutive
+entries within 1e-5 relative (1e-6 for the MLP head at k = 100; the gap reached is
+in MANIFEST.json), and stores the reference's own rating vectors (`scores`).  A list
+may differ from the fixture only by swapping items whose stored ratings are within
+that gap of each other — a near-tie that fp32 rounding on another host or device may
+order either way — which `_assert_same_ranking` checks from the stored scores."""
 import numpy as np
 import pytest
 import torch
@@ -18,6 +24,38 @@ class _G:
 
     def num_nodes(self, nt):
         return self._n
+
+
+def _assert_same_ranking(got, ref, scores, tol, msg):
+    """got == ref item for item, except swaps among items whose reference ratings are
+    within `tol` relative of each other."""
+    got, ref = np.asarray(got), np.asarray(ref)
+    assert got.shape == ref.shape, msg
+    bad = np.nonzero(got != ref)[0]
+    if bad.size == 0:
+        return
+    assert sorted(got[bad].tolist()) == sorted(ref[bad].tolist()), msg
+    for j in bad:
+        a, b = float(scores[got[j]]), float(scores[ref[j]])
+        assert abs(a - b) <= tol * max(abs(a), abs(b)), f"{msg}: rank {j} {got[j]} vs {ref[j]}"
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fixture_scores_rank_to_fixture_recs(name):
+    """The stored reference ratings, ranked (already-bought removed), give the fixture's
+    lists exactly, and no two consecutive ranks are closer than the manifest's gap: the
+    fixtures hold no near-tie whose order depends on rounding."""
+    from gnnrec.recs import create_ground_truth
+    meta = golden_io.manifest()[name]
+    a = golden_io.load(name)
+    already = create_ground_truth(a["bought/u"], a["bought/i"])
+    for u, s, ref in zip(a["user_ids"], a["scores"], a["recs"]):
+        bought = set(already[int(u)])
+        order = [j for j in np.argsort(-s.astype(np.float64), kind="stable") if j not in bought]
+        np.testing.assert_array_equal(order[: meta["k"]], ref[ref >= 0], err_msg=f"user {u}")
+        v = s[order[: meta["k"] + 1]].astype(np.float64)
+        gaps = (v[:-1] - v[1:]) / np.abs(v[:-1])
+        assert gaps.min() >= meta["min_rel_gap_required"], (u, gaps.min())
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -49,9 +87,9 @@ def test_get_recs_matches_reference(name):
         recs = get_recs(_G(a["h/item"].shape[0], a["popularity"], dev), h, model, meta["embed_dim"],
                         meta["k"], a["user_ids"].tolist(), already, True, True, None, meta["pred"],
                         meta["use_popularity"], meta["weight_popularity"], batch_size=7)
-    for u, ref in zip(a["user_ids"], a["recs"]):
+    for u, ref, s in zip(a["user_ids"], a["recs"], a["scores"]):
         ref = ref[ref >= 0]
-        np.testing.assert_array_equal(recs[int(u)], ref, err_msg=f"user {u}")
+        _assert_same_ranking(recs[int(u)], ref, s, meta["min_rel_gap_required"], f"user {u}")
         assert not set(recs[int(u)].tolist()) & set(already[int(u)])
 
 
