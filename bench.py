@@ -112,6 +112,9 @@ KERNELS = {
     "spmm_tile2": ("spmm_csr2_kernel", "gnnrec spmm_csr2_kernel (gather + segmented sums of two "
                    "relations' source-range tiles from one table in one launch)"),
     "spmm": ("spmm_csr_kernel", "gnnrec spmm_csr_kernel (gather + segmented mean)"),
+    "spmm_pair": ("spmm_pair_mfma_kernel", "gnnrec spmm_pair_mfma_kernel (two relations' "
+                  "gathers + means from ONE source table into 32-row LDS tiles, all four SAGE "
+                  "projections on the fp32 MFMA, ReLU, L2 norm, cross-relation combine)"),
     "spmm_project2": ("spmm_project2_pipe_kernel", "gnnrec spmm_project2_pipe_kernel (two "
                       "pre-projected relations' gathers + means into one dst row, both SAGE self "
                       "projections, ReLU, L2 norm, cross-relation sum; next rows' heads "
@@ -127,9 +130,11 @@ def launch_bytes(shard, d, runner, deterministic):
     out = {}
     paired = {c: pair for pair in runner.tile_pairs for c in pair}
     fused2 = {c: pair for pair in getattr(runner, 'pair_fused', ()) for c in pair}
+    raw2 = {c for pair in getattr(runner, 'pair_raw', ()) for c in pair}
     for ce, rs in shard.rels.items():
         if ce in fused2:  # one launch for both: their edges, 2 indptr, the h_self row + output
-            tag, n = "spmm_project2", 1 if ce == fused2[ce][0] else 0
+            tag = "spmm_pair" if ce in raw2 else "spmm_project2"
+            n = 1 if ce == fused2[ce][0] else 0
             b = rs.local_edges * (d * 4 + 4) + rs.n_rows * (8 + (8 * d if n else 0))
         elif ce in paired:  # both relations' tile bytes, one launch per segment for the pair
             tag, b = "spmm_tile2", 0
@@ -158,7 +163,7 @@ CSRC = os.path.join(ROOT, "gnn-recsys_amd", "csrc")
 
 # the sources of the kernels whose HBM traffic the PMC passes measure (the aggregation
 # launches and what they include) plus the build flags
-PMC_SOURCES = ("spmm.hip", "spmm_project.hip", "gemm.hip", "rowq.hip", "gather.hpp", "rowq.hpp",
+PMC_SOURCES = ("spmm.hip", "spmm_project.hip", "spmm_pair_mfma.hip", "gemm.hip", "rowq.hip", "gather.hpp", "rowq.hpp",
                "common.hpp", "Makefile")
 
 
@@ -322,9 +327,9 @@ class Heartbeat:
         while not self._stop.wait(self.period):
             self.say(f"alive, in {self.phase}")
 
-    def say(self, msg):
-        print(f"[bench r{self.rank} +{time.time() - self.t0:.0f}s] {msg}", file=sys.stderr,
-              flush=True)
+    def say(self, msg):  # one write per line: ranks sharing a stderr do not interleave
+        sys.stderr.write(f"[bench r{self.rank} +{time.time() - self.t0:.0f}s] {msg}\n")
+        sys.stderr.flush()
 
     def enter(self, phase):
         self.phase = phase

@@ -366,6 +366,49 @@ void spmm_project2(const Tensor& indptr_a, const Tensor& indices_a, const option
      "gnnrec_spmm_project2_f32");
 }
 
+void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<Tensor>& ew_a,
+               int64_t reduce_a, const optional<Tensor>& bias_a,
+               const optional<Tensor>& bias_nonempty_a, const Tensor& indptr_b,
+               const Tensor& indices_b, const optional<Tensor>& ew_b, int64_t reduce_b,
+               const optional<Tensor>& bias_b, const optional<Tensor>& bias_nonempty_b,
+               const Tensor& X, const Tensor& H, const Tensor& WT4, int64_t epilogue,
+               int64_t combine, const optional<Tensor>& attn_vec, double out_div, Tensor& out) {
+  const OneDevice one_device_;
+  dev(indptr_a, "indptr_a", at::kLong);
+  dev(indices_a, "indices_a", at::kInt);
+  dev(ew_a, "ew_a", at::kFloat);
+  dev(bias_a, "bias_a", at::kFloat);
+  dev(bias_nonempty_a, "bias_nonempty_a", at::kFloat);
+  dev(indptr_b, "indptr_b", at::kLong);
+  dev(indices_b, "indices_b", at::kInt);
+  dev(ew_b, "ew_b", at::kFloat);
+  dev(bias_b, "bias_b", at::kFloat);
+  dev(bias_nonempty_b, "bias_nonempty_b", at::kFloat);
+  dev(X, "X", at::kFloat);
+  dev(H, "H", at::kFloat);
+  dev(WT4, "WT4", at::kFloat);
+  dev(attn_vec, "attn_vec", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t n_dst = indptr_a.numel() - 1, d = X.size(1);
+  TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1, "spmm_pair: the relations' row counts differ");
+  TORCH_CHECK_VALUE(H.size(1) == d && H.size(0) >= n_dst, "spmm_pair: H shape");
+  TORCH_CHECK_VALUE(WT4.is_contiguous() && WT4.numel() == 4 * d * d,
+                    "spmm_pair: WT4 must be a contiguous [4, d, d] weight array");
+  TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d,
+                    "]");
+  const int64_t ldx = ld(X, "X"), ldh = ld(H, "H"), ldo = ld(out, "out");
+  if (meta(X)) return;
+  const c10::DeviceGuard g(X.device());
+  ck(gnnrec_spmm_pair_f32(p<int64_t>(indptr_a), p<int32_t>(indices_a), p<float>(ew_a),
+                          (int)reduce_a, p<float>(bias_a), p<float>(bias_nonempty_a),
+                          p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b),
+                          (int)reduce_b, p<float>(bias_b), p<float>(bias_nonempty_b),
+                          p<float>(X), ldx, p<float>(H), ldh, p<float>(WT4), n_dst, d,
+                          (int)epilogue, (int)combine, p<float>(attn_vec), (float)out_div,
+                          p<float>(out), ldo, stream_of(X)),
+     "gnnrec_spmm_pair_f32");
+}
+
 // ---------------------------------------------------------------- a7 / a8 heads
 void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                Tensor& out) {
@@ -1514,6 +1557,11 @@ TORCH_LIBRARY(gnnrec, m) {
         "int reduce_b, Tensor? bias_nonempty_b, Tensor H, Tensor W_self_aT, Tensor W_self_bT, "
         "Tensor? bias_a, Tensor? bias_b, int epilogue, int combine, Tensor? attn_vec, "
         "float out_div, Tensor(a!) out) -> ()");
+  m.def("spmm_pair(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, int reduce_a, "
+        "Tensor? bias_a, Tensor? bias_nonempty_a, Tensor indptr_b, Tensor indices_b, "
+        "Tensor? ew_b, int reduce_b, Tensor? bias_b, Tensor? bias_nonempty_b, Tensor X, "
+        "Tensor H, Tensor WT4, int epilogue, int combine, Tensor? attn_vec, float out_div, "
+        "Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
         "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");
@@ -1611,6 +1659,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("row_epilogue", &row_epilogue);                 \
   m.impl("spmm_project", &spmm_project);                 \
   m.impl("spmm_project2", &spmm_project2);               \
+  m.impl("spmm_pair", &spmm_pair);                       \
   m.impl("sddmm_cos", &sddmm_cos);                       \
   m.impl("sddmm_cos_backward", &sddmm_cos_backward);     \
   m.impl("edge_mlp", &edge_mlp);                         \

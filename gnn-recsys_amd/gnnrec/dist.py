@@ -415,8 +415,9 @@ class ProgressExchange:
     def _say(self, msg):
         if self.enabled:
             layer = getattr(self.runner, "_layer_idx", None)
-            print(f"[gnnrec r{self.inner.rk}] pass {self.pass_no} layer {layer} {msg}",
-                  file=self.stream, flush=True)
+            self.stream.write(f"[gnnrec r{self.inner.rk}] pass {self.pass_no} layer {layer} "
+                              f"{msg}\n")  # one write per line (ranks share a stderr)
+            self.stream.flush()
 
     def layer_start(self, i):
         """ShardedFullGraphPass.progress hook: one line per layer."""

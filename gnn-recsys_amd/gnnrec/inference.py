@@ -386,7 +386,8 @@ class ShardedFullGraphPass:
         self.capture = None  # optional list: every layer's output tables are appended (tests)
         self.progress = None  # optional callable(layer index) at every layer's start (bench)
         self.fused = set()  # relations whose aggregation ran with the projection fused
-        self.pair_fused = set()  # (ce_a, ce_b) run as one pre-projected two-relation launch
+        self.pair_fused = set()  # (ce_a, ce_b) run as one two-relation launch
+        self.pair_raw = set()  # ... of them, the one-table form (gnnrec_spmm_pair_f32)
         self.tile_pairs = set()  # (relation a, relation b) whose tiles ran as one launch
         self._pool = {}  # scratch tables reused across passes (_scratch)
         self._scratch_ev = {}  # scratch key -> event of the side-stream work reading it
@@ -902,13 +903,36 @@ class ShardedFullGraphPass:
         plan = self._pair_plan(hconv, h, ces)
         if plan is None:
             return False
-        rels, Wself, biases = self._pair_stage(plan, h)
-        self_rows = self._get(h, T)
         mod = plan[0][0]
-        o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
-                        device=self_rows.device)
         from .nn import _pair_combine
         combine, div = _pair_combine(hconv.aggregate)
+        if self._pair_raw(plan):
+            # both relations gather the SAME raw source table: no pre-projection, the four
+            # projections in the launch's MFMA epilogue (gnnrec_spmm_pair_f32) — the gathered
+            # working set is one 512 MB table at C5 instead of two pre-projected ones
+            X = self._get(h, plan[0][1][0])
+            self_rows = self._get(h, T)
+            rels, Wts = [], []
+            for m, ce, rs, _, weighted, reduce in plan:
+                Ws, Wn, bias, bias_ne = self._folded(m, ce)
+                rels.append((rs.indptr, rs.indices, reduce, rs.weights if weighted else None,
+                             bias_ne))
+                Wts.append((Ws, Wn, bias))
+            o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
+                            device=self_rows.device)
+            with self._time('spmm_pair'):
+                O.spmm_pair(rels[0], rels[1], X, self_rows, Wts[0][0], Wts[0][1], Wts[1][0],
+                            Wts[1][1], Wts[0][2], Wts[1][2], relu=True,
+                            l2norm=bool(mod.norm), combine=combine, out_div=div, out=o,
+                            attn_vec=hconv.attn[T] if combine == 'attention' else None)
+            self.pair_fused.add((ces[0], ces[1]))
+            self.pair_raw.add((ces[0], ces[1]))
+            out[T] = o
+            return True
+        rels, Wself, biases = self._pair_stage(plan, h)
+        self_rows = self._get(h, T)
+        o = torch.empty((sh.n_own, mod._out_feats), dtype=torch.float32,
+                        device=self_rows.device)
         with self._time('spmm_project2'):
             O.spmm_project2(rels[0], rels[1], self_rows, Wself[0], Wself[1], biases[0],
                             biases[1], relu=True, l2norm=bool(mod.norm), combine=combine,
@@ -917,6 +941,14 @@ class ShardedFullGraphPass:
         self.pair_fused.add((ces[0], ces[1]))
         out[T] = o
         return True
+
+    def _pair_raw(self, plan) -> bool:
+        """The pair gathers one raw table (gnnrec_spmm_pair_f32) when both relations come
+        from the same source type with no fc_preagg (their messages are that table itself)
+        and the backend has the op; GNNREC_PAIR_RAW=0 keeps the pre-projected form."""
+        return getattr(self.ops, 'spmm_pair', None) is not None and \
+            os.environ.get("GNNREC_PAIR_RAW", "1") != "0" and \
+            plan[0][1][0] == plan[1][1][0] and not plan[0][3] and not plan[1][3]
 
     def _pair_plan(self, hconv, h, ces):
         """The two relations of a pair launch, or None (shapes and layouts only: nothing is

@@ -260,9 +260,10 @@ class HeteroGraphConv(nn.Module):
 
     def _pair(self, g, ces, src_inputs, h_dst, out) -> bool:
         """Inference, exactly two relations into one type, both pre-projectable
-        (ConvLayer._pre_plan): one ops.spmm_project2 launch with the sum / mean / max
-        combine inside (the sharded pass's _pair does the same).  GNNREC_PAIR_FUSE=0
-        disables it."""
+        (ConvLayer._pre_plan): one launch with the sum / mean / max / attention combine
+        inside — ops.spmm_pair when both gather the same raw table, else ops.spmm_project2
+        over the pre-projected tables (the sharded pass's _pair does the same).
+        GNNREC_PAIR_FUSE=0 disables it."""
         if self.aggregate not in ('sum', 'mean', 'max', 'attention') or \
                 os.environ.get("GNNREC_PAIR_FUSE", "1") == "0":
             return False
@@ -275,13 +276,26 @@ class HeteroGraphConv(nn.Module):
             if p is None:
                 return False
             plans.append(p)
+        combine, div = _pair_combine(self.aggregate)
+        dtype = ces[0][2]
+        if plans[0][0] is plans[1][0] and os.environ.get("GNNREC_PAIR_RAW", "1") != "0":
+            # both messages are the one source table itself: ops.spmm_pair gathers it raw and
+            # runs all four projections in its epilogue (the sharded pass's _pair_raw)
+            rels = []
+            for ce, (m, reduce, ew) in zip(ces, plans):
+                rg = g.rel_graph(ce)
+                rels.append((rg.indptr, rg.indices, reduce, ew, None))
+            ops.spmm_pair(rels[0], rels[1], plans[0][0], h_dst, mods[0].fc_self.weight,
+                          mods[0].fc_neigh.weight, mods[1].fc_self.weight,
+                          mods[1].fc_neigh.weight, relu=True, l2norm=bool(mods[0].norm),
+                          combine=combine, out_div=div, out=out,
+                          attn_vec=self.attn[dtype] if combine == 'attention' else None)
+            return True
         rels = []
         for mod, ce, (m, reduce, ew) in zip(mods, ces, plans):
             rg = g.rel_graph(ce)
             rels.append((rg.indptr, rg.indices, ops.preproject(m, mod.fc_neigh.weight), reduce,
                          ew, None))
-        combine, div = _pair_combine(self.aggregate)
-        dtype = ces[0][2]
         ops.spmm_project2(rels[0], rels[1], h_dst, mods[0].fc_self.weight,
                           mods[1].fc_self.weight, relu=True, l2norm=bool(mods[0].norm),
                           combine=combine, out_div=div, out=out,

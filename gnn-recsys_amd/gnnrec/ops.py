@@ -537,27 +537,67 @@ def _nnz(indptr: torch.Tensor) -> int:
     return v
 
 
-def _transposed(W: torch.Tensor) -> torch.Tensor:
-    """Wᵀ (k-major, contiguous) of a fused kernel's weight, kept on the weight tensor and
-    rebuilt only when the weight changes (its version counter, an optimizer step) — not a
-    transpose-copy kernel per launch inside the pass (C4: two per layer before the fused
-    launch, profiles/r02f_c4_timeline.txt)."""
-    if torch.compiler.is_compiling() or not W.is_cuda:
-        return W.detach().t().contiguous()
-    hit = getattr(W, "_gnnrec_wt", None)
-    key = (W._version, W.data_ptr())
+def _wkey(W: torch.Tensor):
+    return (W._version, W.data_ptr(), getattr(W, "_gnnrec_epoch", 0))
+
+
+def invalidate_weight_cache(*modules_or_tensors) -> None:
+    """Drop the transposed / packed weight copies the fused kernels keep on weight tensors.
+    They are rebuilt when a weight's version counter moves (every in-place op through the
+    autograd-visible tensor: optimizer steps, `with torch.no_grad(): W.copy_(...)`); a write
+    through `W.data` (EMA or custom update code) does not move it — call this afterwards
+    with the modules or tensors written."""
+    for m in modules_or_tensors:
+        ts = m.parameters() if isinstance(m, torch.nn.Module) else [m]
+        for W in ts:
+            try:
+                W._gnnrec_epoch = getattr(W, "_gnnrec_epoch", 0) + 1
+            except (AttributeError, RuntimeError):  # pragma: no cover
+                pass
+
+
+def _cached_on(W: torch.Tensor, attr: str, key, make):
+    """A derived copy of weight W kept as W.<attr>, rebuilt when `key` changes.  Handed to
+    another stream than the one that made it, the consumer first waits for its making and
+    the copy is record_stream-ed there (so replacing it never frees memory a side-stream
+    kernel is still reading)."""
+    hit = getattr(W, attr, None)
     cur = torch.cuda.current_stream(W.device)
     if hit is None or hit[0] != key:
         ev = torch.cuda.Event()
-        hit = (key, W.detach().t().contiguous(), ev, cur.cuda_stream)
+        hit = (key, make(), ev, cur.cuda_stream)
         ev.record(cur)
         try:
-            W._gnnrec_wt = hit
+            setattr(W, attr, hit)
         except (AttributeError, RuntimeError):  # pragma: no cover
             pass
     elif hit[3] != cur.cuda_stream:  # made on another stream: ordered after its copy
         cur.wait_event(hit[2])
+        hit[1].record_stream(cur)
     return hit[1]
+
+
+def _transposed(W: torch.Tensor) -> torch.Tensor:
+    """Wᵀ (k-major, contiguous) of a fused kernel's weight, kept on the weight tensor and
+    rebuilt only when the weight changes (its version counter, an optimizer step, or
+    invalidate_weight_cache) — not a transpose-copy kernel per launch inside the pass (C4:
+    two per layer before the fused launch, profiles/r02f_c4_timeline.txt)."""
+    if torch.compiler.is_compiling() or not W.is_cuda:
+        return W.detach().t().contiguous()
+    return _cached_on(W, "_gnnrec_wt", _wkey(W), lambda: W.detach().t().contiguous())
+
+
+def _packed4(Ws_a, Wn_a, Ws_b, Wn_b) -> torch.Tensor:
+    """[W_self,aᵀ | W_neigh,aᵀ | W_self,bᵀ | W_neigh,bᵀ] as one contiguous [4, d, d] k-major
+    array (gnnrec_spmm_pair_f32's WT4), cached on W_self,a like _transposed."""
+    Ws = (Ws_a, Wn_a, Ws_b, Wn_b)
+
+    def make():
+        return torch.stack([W.detach().t() for W in Ws]).contiguous()
+
+    if torch.compiler.is_compiling() or not Ws_a.is_cuda:
+        return make()
+    return _cached_on(Ws_a, "_gnnrec_wt4", tuple(_wkey(W) for W in Ws), make)
 
 
 def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
@@ -692,6 +732,66 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
                        epi,
                        ACCUM["attn_last" if combine == "attention" else combine], attn_vec,
                        float(out_div), out)
+    return out
+
+
+def spmm_pair(rel_a, rel_b, X, H, W_self_a, W_neigh_a, W_self_b, W_neigh_b, bias_a=None,
+              bias_b=None, *, relu: bool = True, l2norm: bool = False, combine: str = "add",
+              out_div: float = 0.0, out: Optional[torch.Tensor] = None,
+              attn_vec: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Two relations gathering from ONE source table X into one destination type, all four
+    projections in the launch (gnnrec_spmm_pair_f32, MFMA epilogue): out = combine(
+    epi(H W_self_aᵀ + agg_a W_neigh_aᵀ + bias_a [+ bias_nonempty_a]), epi(... b ...)) /
+    out_div.  rel_r = (indptr, indices, reduce, edge_weight, bias_nonempty), reduce sum or
+    mean; combine as spmm_project2.  Unlike spmm_project2 nothing is pre-projected: the
+    gathered working set is X alone."""
+    D = FUSED_D
+    n_dst = rel_a[0].numel() - 1
+    args = []
+    for name, (indptr, indices, reduce, ew, bne), b in (("a", rel_a, bias_a), ("b", rel_b, bias_b)):
+        _dev(indptr, f"indptr_{name}", torch.int64)
+        _dev(indices, f"indices_{name}", torch.int32)
+        if reduce not in ("sum", "mean"):
+            raise ValueError("spmm_pair: both relations reduce by sum or mean")
+        if indptr.numel() - 1 != n_dst:
+            raise ValueError("spmm_pair: the relations' row counts differ")
+        if ew is not None:
+            _dev(ew, f"ew_{name}", torch.float32)
+            ew = ew.contiguous()
+        if bne is not None:
+            _dev(bne, f"bias_nonempty_{name}", torch.float32)
+            bne = bne.detach().contiguous()
+        if b is not None:
+            b = b.detach().contiguous()
+        args += [indptr, indices, ew, REDUCE[reduce], b, bne]
+    _dev(X, "X", torch.float32)
+    _rowmajor(X, "X")
+    _dev(H, "H", torch.float32)
+    _rowmajor(H, "H")
+    if X.shape[1] != D or H.shape[1] != D:
+        raise ValueError(f"spmm_pair needs d = {D}")
+    if combine not in ("add", "max", "attention"):
+        raise ValueError(f"spmm_pair: combine must be 'add', 'max' or 'attention', "
+                         f"not {combine!r}")
+    if (combine == "attention") != (attn_vec is not None):
+        raise ValueError("spmm_pair: attn_vec goes with combine='attention'")
+    if attn_vec is not None:
+        _dev(attn_vec, "attn_vec", torch.float32)
+        if attn_vec.numel() != D:
+            raise ValueError(f"attn_vec must have {D} entries")
+        attn_vec = attn_vec.detach().contiguous()
+    for W in (W_self_a, W_neigh_a, W_self_b, W_neigh_b):
+        if tuple(W.shape) != (D, D):
+            raise ValueError(f"spmm_pair needs {D}x{D} weights")
+    if out is None:
+        out = torch.empty((n_dst, D), dtype=torch.float32, device=H.device)
+    else:
+        _dev(out, "out", torch.float32)
+        _rowmajor(out, "out")
+    epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
+    _T().spmm_pair(*args, X, H, _packed4(W_self_a, W_neigh_a, W_self_b, W_neigh_b), epi,
+                   ACCUM["attn_last" if combine == "attention" else combine], attn_vec,
+                   float(out_div), out)
     return out
 
 

@@ -281,6 +281,28 @@ int gnnrec_spmm_project2_f32(const int64_t* indptr_a, const int32_t* indices_a,
                              const float* attn_vec, float out_div, float* out, int64_t ldo,
                              void* stream);
 
+/* Two relations into one destination type that gather from ONE source table (C5's
+ * clicked-by and bought-by, both from the item table), all four projections in the launch:
+ *   out[v] = combine( epi(H[v] W_self_a^T + agg_a(v) W_neigh_a^T + bias_a [+ bias_nonempty_a]),
+ *                     epi(H[v] W_self_b^T + agg_b(v) W_neigh_b^T + bias_b [+ bias_nonempty_b]) )
+ *            / out_div
+ * agg_r = sum / mean over relation r's in-edges of X[indices_r[e]] (* ew_r[e]).  WT4 is the
+ * packed k-major weight array [W_self_a^T | W_neigh_a^T | W_self_b^T | W_neigh_b^T], four
+ * contiguous d x d blocks (block[k][n] = W[n][k]).  The projections run on the fp32 MFMA
+ * in 32-row tiles; the gathered working set is the one table (gnnrec_spmm_project2_f32
+ * gathers two pre-projected ones).  combine / attn_vec / out_div / epilogue / d /
+ * alignment as gnnrec_spmm_project2_f32; bias_r NULL: none.  Each aggregate has the bits
+ * of gnnrec_spmm_csr_f32's; the projection sums k in a fixed order of its own.  Replaces two
+ * ConvLayer.forward calls + the HeteroGraphConv aggregate, src/model.py:143-235,384-406. */
+int gnnrec_spmm_pair_f32(const int64_t* indptr_a, const int32_t* indices_a, const float* ew_a,
+                         int reduce_a, const float* bias_a, const float* bias_nonempty_a,
+                         const int64_t* indptr_b, const int32_t* indices_b, const float* ew_b,
+                         int reduce_b, const float* bias_b, const float* bias_nonempty_b,
+                         const float* X, int64_t ldx, const float* H, int64_t ldh,
+                         const float* WT4, int64_t n_dst, int64_t d, int epilogue, int combine,
+                         const float* attn_vec, float out_div, float* out, int64_t ldo,
+                         void* stream);
+
 /* ---- a7: cosine edge score (K5) ------------------------------------------
  * out[e] = < Hs[src[e]] / max(||Hs[src[e]]||,1e-12) , Hd[dst[e]] / max(||Hd[dst[e]]||,1e-12) >
  * Replaces CosinePrediction.forward, src/model.py:317-327. */

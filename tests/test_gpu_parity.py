@@ -902,6 +902,122 @@ def test_spmm_project2_two_relations_match_oracle(combine, weighted):
                           targs[1][0])
 
 
+def _pair_case(rng, n_dst, n_src, weighted, reduces=("mean", "sum"), degs=((60, [0, 700, 1]),
+                                                                             (12, [0, 2, 0]))):
+    """Two relations from ONE source table X into n_dst rows: CSRs, weights, the oracle's
+    per-relation ConvLayer outputs z_r (reference src/model.py:143-148,226-235)."""
+    d = 128
+    X = rng.standard_normal((n_src, d)).astype(np.float32)
+    H = rng.standard_normal((n_dst, d)).astype(np.float32)
+    rels, zs, W = [], [], []
+    for r, reduce in enumerate(reduces):
+        hi, head = degs[r]
+        deg = rng.integers(0, hi, n_dst)
+        deg[: len(head)] = head
+        dst = np.repeat(np.arange(n_dst), deg)
+        src = rng.integers(0, n_src, dst.size)
+        indptr, indices, eids = oracle.csr_from_coo(src, dst, n_dst)
+        Ws = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+        Wn = (rng.standard_normal((d, d)) * 0.1).astype(np.float32)
+        b = rng.standard_normal(d).astype(np.float32) * 0.1
+        bne = rng.standard_normal(d).astype(np.float32) * 0.1
+        ew = rng.integers(1, 5, dst.size).astype(np.float32)[eids] if weighted else None
+        agg = oracle.spmm_csr(indptr, indices, X, reduce, ew)
+        z = oracle.linear(H, Ws) + oracle.linear(agg, Wn) + b + \
+            (np.diff(indptr) > 0)[:, None] * bne
+        zs.append(oracle.l2_normalize_rows_guarded(oracle.relu(z)))
+        rels.append((_t(indptr), _t(indices.astype(np.int32)), reduce,
+                     None if ew is None else _t(ew), _t(bne)))
+        W.append((_t(Ws), _t(Wn), _t(b)))
+    return X, H, rels, zs, W
+
+
+def _combine_ref(rng, zs, combine):
+    d = zs[0].shape[1]
+    if combine == "attention":  # softmax over the two relations of a . z_r, per row
+        a = rng.standard_normal(d).astype(np.float32)
+        sc = np.stack([z @ a for z in zs])
+        w = np.exp(sc - sc.max(0))
+        w /= w.sum(0)
+        return w[0][:, None] * zs[0] + w[1][:, None] * zs[1], dict(combine="attention",
+                                                                   attn_vec=_t(a))
+    if combine == "max":
+        return np.maximum(zs[0], zs[1]), dict(combine="max")
+    if combine == "mean":
+        return (zs[0] + zs[1]) / 2, dict(combine="add", out_div=2.0)
+    return zs[0] + zs[1], dict(combine="add")
+
+
+@pytest.mark.parametrize("combine,weighted", [("sum", False), ("mean", False), ("max", True),
+                                              ("attention", False), ("sum", True)])
+def test_spmm_pair_one_table_matches_oracle(combine, weighted):
+    """gnnrec_spmm_pair_f32: two relations gathering ONE raw source table, all four
+    projections on the MFMA, against the oracle's two ConvLayers + HeteroGraphConv sum /
+    mean / max / attention (reference src/model.py:143-235,384-406): mean and sum reduces,
+    empty rows, a 700-edge row (the row-by-row gather past 64 edges), biases on non-empty
+    rows only, a row count that is not a multiple of the 32-row tile; run twice, bitwise."""
+    from gnnrec import ops
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(f"pair1{combine}{weighted}".encode()))
+    X, H, rels, zs, W = _pair_case(rng, 2999, 900, weighted)
+    ref, kw = _combine_ref(rng, zs, combine)
+    args = (rels[0], rels[1], _t(X), _t(H), W[0][0], W[0][1], W[1][0], W[1][1], W[0][2], W[1][2])
+    out = ops.spmm_pair(*args, relu=True, l2norm=True, **kw)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
+    assert torch.equal(out, ops.spmm_pair(*args, relu=True, l2norm=True, **kw))
+    with pytest.raises(ValueError):
+        ops.spmm_pair(rels[0], rels[1][:2] + ("max",) + rels[1][3:], *args[2:])
+
+
+def test_spmm_pair_row_queue_and_small_grids():
+    """Row counts that take the static walk with fewer blocks than XCDs (40, 200 rows), the
+    XCD walk (20k) and the row queue (200k rows: at least 4 tickets per block), with
+    degrees around C5's 40 + 10 per row and no norm — every row written once, against the
+    oracle."""
+    from gnnrec import ops
+    rng = np.random.default_rng(5)
+    for n_dst in (40, 200, 20_000, 200_000):
+        X, H, rels, _, W = _pair_case(rng, n_dst, 3000, False, degs=((80, [0]), (20, [])))
+        zs = []
+        for (ip, ix, reduce, _, bne), (Ws, Wn, b) in zip(rels, W):
+            ipn, ixn = ip.cpu().numpy(), ix.cpu().numpy()
+            agg = oracle.spmm_csr(ipn, ixn, X, reduce)
+            z = oracle.linear(H, Ws.cpu().numpy()) + oracle.linear(agg, Wn.cpu().numpy()) + \
+                b.cpu().numpy() + (np.diff(ipn) > 0)[:, None] * bne.cpu().numpy()
+            zs.append(oracle.relu(z))
+        out = ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), W[0][0], W[0][1], W[1][0], W[1][1],
+                            W[0][2], W[1][2], relu=True, l2norm=False)
+        np.testing.assert_allclose(out.cpu().numpy(), zs[0] + zs[1], rtol=RTOL, atol=ATOL,
+                                   err_msg=f"n_dst={n_dst}")
+
+
+def test_spmm_pair_aggregates_have_the_plain_kernels_bits():
+    """With identity projections (W_self = 0, W_neigh = I, no bias, no ReLU/norm) the pair
+    kernel's output is agg_a + agg_b: each aggregate must carry spmm_csr's bits (same
+    per-row summation order), so the sum equals the plain kernel's two outputs added."""
+    from gnnrec import ops
+    rng = np.random.default_rng(8)
+    X, H, rels, _, _ = _pair_case(rng, 777, 500, False)
+    rels = [r[:4] + (None,) for r in rels]  # no non-empty bias
+    I = torch.eye(128, device=DEV)
+    Z = torch.zeros(128, 128, device=DEV)
+    out = ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), Z, I, Z, I, relu=False, l2norm=False)
+    a = ops.spmm(rels[0][0], rels[0][1], _t(X), rels[0][2])
+    b = ops.spmm(rels[1][0], rels[1][1], _t(X), rels[1][2])
+    torch.testing.assert_close(out, a + b, rtol=0, atol=0)
+
+
+def test_spmm_pair_empty_destination():
+    from gnnrec import ops
+    ip = torch.zeros(1, dtype=torch.int64, device=DEV)
+    ix = torch.zeros(0, dtype=torch.int32, device=DEV)
+    W = torch.zeros(128, 128, device=DEV)
+    out = ops.spmm_pair((ip, ix, "mean", None, None), (ip, ix, "sum", None, None),
+                        torch.zeros(4, 128, device=DEV), torch.zeros(0, 128, device=DEV),
+                        W, W, W, W)
+    assert out.shape == (0, 128)
+
+
 @pytest.mark.parametrize("variant", ["valu", "mfma"])
 def test_spmm_project_accumulate_modes_and_strides(variant):
     from gnnrec import ops

@@ -26,7 +26,7 @@ RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_t
            "gnnrec_spmm_csr_planned_f32": "spmm_csr_planned", "gnnrec_spmm_csr2_f32": "spmm_csr2",
            "gnnrec_spmm_backward_f32": "spmm_backward",
            "gnnrec_spmm_project_f32": "spmm_project", "gnnrec_sddmm_cos_f32": "sddmm_cos",
-           "gnnrec_spmm_project2_f32": "spmm_project2",
+           "gnnrec_spmm_project2_f32": "spmm_project2", "gnnrec_spmm_pair_f32": "spmm_pair",
            "gnnrec_sddmm_cos_backward_f32": "sddmm_cos_backward",
            "gnnrec_edge_mlp_f32": "edge_mlp", "gnnrec_act_backward_f32": "act_backward",
            "gnnrec_act_backward_normed_f32": "act_backward_normed",
