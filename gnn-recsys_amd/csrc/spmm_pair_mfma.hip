@@ -33,6 +33,19 @@
 //            non-temporal 512-B store per row.
 // Two blocks per CU (≈50 KiB of LDS each), so one block's MFMA phase runs under the other's
 // gather.  Rows come from the row queue in whole tiles, or an XCD-contiguous static walk.
+//
+// Measured (C5 user side, 10M rows × (40 + 10) edges, 268 GB, tools/gpu/r04c_pairvar.sh and
+// r04e_pairh.sh): the gather phase alone (timing build GNNREC_SPQ_PHASE=1) 34.6 ms = 0.969 of
+// 8 TB/s — one 512 MB table is the cache-friendly working set the pre-projected launch lacks —
+// the MFMA phase alone 14.8 ms, the launch 38.4–38.6 ms (0.87): while one block sits in its
+// MFMA phase only the other block's 8 waves gather.  The pre-projected launch takes 36.6–37.8
+// ms plus its two 1M-row GEMMs, so the C5 passes come out within 0.5 ms of each other
+// (153.3–154.0 vs 154.0–154.4 ms); the sharded pass keeps the pre-projected form by default
+// (GNNREC_PAIR_RAW=1 selects this one).  Not kept: a software-pipelined form (the previous
+// tile's MFMAs interleaved into this tile's gather steps, operands loaded one chunk ahead,
+// aggregates double-buffered, self rows straight from H by buffer loads) — 43.9 ms, its MFMA
+// state and gather share 128 VGPRs and spill 124–152 B/lane; LU = 1 / 3 lockstep unrolls 39.9
+// / 39.1 ms; the self rows requested ahead of the gathers: unchanged.
 #include "common.hpp"
 #include "gather.hpp"
 #include "rowq.hpp"
@@ -51,9 +64,6 @@ constexpr int kQCLd = kQD + 8;           // C tile row stride
 #endif
 #ifndef GNNREC_SPQ_U
 #define GNNREC_SPQ_U 4  // gather_range unroll for rows above 64 edges
-#endif
-#ifndef GNNREC_SPQ_PLU
-#define GNNREC_SPQ_PLU 1  // the pipelined kernel's lockstep unroll (its MFMA state shares the VGPRs)
 #endif
 #ifndef GNNREC_SPQ_WC
 #define GNNREC_SPQ_WC 16  // B operands per chunk
@@ -93,18 +103,11 @@ __device__ __forceinline__ void activate_q(bool relu, bool l2, float& y0, float&
 
 // The 4 rows [rbase, rbase + nv) of one relation, gathered in lockstep into A tile columns
 // [cofs, cofs + 128) of tile rows [r0, r0 + 4); their non-empty flags into ne[].
-struct NoTick {
-  __device__ __forceinline__ void operator()() const {}
-};
-
-// tick(): called once per lockstep step, between the issue of that step's source-row loads
-// and their accumulation (the pipelined kernel runs a chunk of the previous tile's MFMAs
-// there, under the loads' latency)
-template <bool W, int ALD = kQALd, int U = GNNREC_SPQ_LU, typename Tick = NoTick>
+template <bool W>
 __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict__ X,
                                         int64_t ldx, int64_t rbase, int nv, float* As, int r0,
-                                        int cofs, int* ne, int lane, Tick tick = Tick{}) {
-  constexpr int LPR = 32, VEC = 4, NPI = kWave / LPR, kLR = 4;
+                                        int cofs, int* ne, int lane) {
+  constexpr int LPR = 32, VEC = 4, NPI = kWave / LPR, U = GNNREC_SPQ_LU, kLR = 4;
   const int grp = lane / LPR, col = (lane % LPR) * VEC;
   const int64_t ipl = nv > 0 && lane <= nv ? ld_stream(r.indptr + rbase + lane) : 0;
   int64_t b[kLR + 1];
@@ -145,9 +148,6 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
             for (int v = 0; v < VEC; ++v) val[i][u].v[v] = 0.f;
           }
         }
-      __builtin_amdgcn_sched_barrier(0);
-      tick();
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < kLR; ++i)
 #pragma unroll
@@ -170,7 +170,7 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
     combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc[i]);
     if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc[i], dg[i], 0);
     if (grp == 0)
-      *reinterpret_cast<float4*>(&As[(r0 + i) * ALD + cofs + col]) =
+      *reinterpret_cast<float4*>(&As[(r0 + i) * kQALd + cofs + col]) =
           make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]);
     if (lane == 0) ne[r0 + i] = dg[i] > 0;
   }
@@ -213,15 +213,19 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
     const int64_t left = lim - rbase;
     const int nv = (int)(left <= 0 ? 0 : left < kQRows ? left : kQRows);
     const int r0 = wave * kQRows;
+    // self rows, two per instruction, requested before the gathers (their latency hides
+    // under the gathers instead of ahead of the MFMA phase's barrier)
+    float4 hs[kQRows / 2];
+#pragma unroll
+    for (int q = 0; q < kQRows / 2; ++q) {
+      const int rl = 2 * q + bh;
+      hs[q] = rl < nv ? ld_stream4(H + (rbase + rl) * ldh + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     gather4<WA>(ra, X, ldx, rbase, nv, As, r0, kQD, nes[0], lane);
     gather4<WB>(rb, X, ldx, rbase, nv, As, r0, 2 * kQD, nes[1], lane);
 #pragma unroll
-    for (int q = 0; q < kQRows / 2; ++q) {  // self rows, two per instruction
-      const int rl = 2 * q + bh;
-      const float4 hs = rl < nv ? ld_stream4(H + (rbase + rl) * ldh + col)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(&As[(r0 + rl) * kQALd + col]) = hs;
-    }
+    for (int q = 0; q < kQRows / 2; ++q)
+      *reinterpret_cast<float4*>(&As[(r0 + 2 * q + bh) * kQALd + col]) = hs[q];
     __syncthreads();
 
     constexpr int kWC = GNNREC_SPQ_WC;
@@ -353,224 +357,6 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
   if (rq != nullptr) rq_finish(rq);
 }
 
-// ---- the same launch, software-pipelined: tile t's gather overlaps tile t-1's MFMAs ------
-// Measured with timing builds (C5, tools/gpu/r04c_pairvar.sh): the kernel above gathers in
-// 34.6 ms alone (0.969 of 8 TB/s) and runs its MFMA phase in 14.8 ms alone, but 38.5 ms
-// together — while a block sits in its MFMA phase only the other block's 8 waves gather.
-// Here every wave keeps gathering: the A tile holds only the aggregates [agg_a | agg_b]
-// (double-buffered, 2 × 34 KiB per block), the self operands come straight from H in
-// global memory, and a wave runs the previous tile's 128 MFMAs in chunks of 8 between
-// issuing a lockstep step's source-row loads and accumulating them (gather4's tick): the
-// MFMAs execute under the loads' latency.  Each chunk's operands (8 B values, 8 self values)
-// are loaded one chunk ahead, ahead of the next step's source rows, so waiting for them
-// never waits for the gather.  One barrier closes a tile (its aggregates complete, the
-// previous tile's MFMAs done), then C lands over the previous buffer and the epilogue
-// finishes its rows.  Same arithmetic as the kernel above: the same aggregate bits, the
-// same K order per output.
-constexpr int kQGLd = 2 * kQD + 4;  // aggregate tile row stride (floats): conflict-free b128
-constexpr int kQBuf = (kQT * kQGLd > 2 * kQT * kQCLd) ? kQT * kQGLd : 2 * kQT * kQCLd;
-constexpr int kQChunk = 8;          // MFMAs per tick
-
-template <bool WA, bool WB>
-__global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_pipe_kernel(
-    RawRel ra, RawRel rb, const float* __restrict__ X, int64_t ldx, const float* __restrict__ H,
-    int64_t ldh, const float* __restrict__ WT4, int64_t n_dst, int epilogue, int combine,
-    const float* __restrict__ attn_vec, float out_div, float* __restrict__ out, int64_t ldo,
-    unsigned* rq, int rq_ch) {
-  __shared__ float bufs[2][kQBuf];
-  __shared__ int nes[2][2][kQT];
-  __shared__ int64_t blk_r[2];
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int li = lane & 31, bh = lane >> 5;
-  const int j0 = 2 * lane;
-  const int cb = wave & 3, rr = wave >> 2;
-  const bool relu = epilogue & GNNREC_EPI_RELU, l2 = epilogue & GNNREC_EPI_L2NORM;
-  const uint64_t wbase = ((uint64_t)__builtin_amdgcn_readfirstlane(
-                              (unsigned)((uintptr_t)WT4 >> 32)) << 32) |
-                         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)WT4);
-  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wbase), 0,
-                                                       4 * kQD * kQD * 4, 0x00020000);
-  const int wvoff = ((2 * rr + bh) * kQD * kQD + 32 * cb + li) * 4;
-
-  // MFMA state of the previous tile (wave-uniform but mi)
-  int mi = 128;              // next K index of the previous tile's MFMAs (128: none left)
-  f32x16q c;
-  float pb[kQChunk];         // B operands of the chunk at mi (loaded one chunk ahead)
-  float4 ph0, ph1;           // lane half 0: H[row][mi .. mi + 8) of the previous tile
-  const float* hrow = H;     // lane half 0: the previous tile's self row li (clamped)
-  const float* arow = bufs[0];  // lane half 1: that row's aggregate of relation rr in LDS
-
-  auto prefetch = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < kQChunk; ++i)
-      pb[i] = __uint_as_float(
-          __builtin_amdgcn_raw_buffer_load_b32(wrsrc, wvoff, (mi + i) * kQD * 4, 0));
-    if (bh == 0) {
-      ph0 = *reinterpret_cast<const float4*>(hrow + mi);
-      ph1 = *reinterpret_cast<const float4*>(hrow + mi + 4);
-    }
-  };
-  auto tick = [&]() __attribute__((always_inline)) {
-    if (mi >= 128) return;
-    float4 a0 = ph0, a1 = ph1;
-    if (bh) {
-      a0 = *reinterpret_cast<const float4*>(arow + mi);
-      a1 = *reinterpret_cast<const float4*>(arow + mi + 4);
-    }
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, pb[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, pb[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, pb[2], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, pb[3], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, pb[4], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, pb[5], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, pb[6], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, pb[7], c, 0, 0, 0);
-    mi += kQChunk;
-    if (mi < 128) prefetch();
-  };
-
-  // the epilogue of the tile whose C sits in buffer q: rows [pt0 + 4·wave, +4) below plim
-  auto finish = [&](int q, int64_t pt0, int64_t plim) __attribute__((always_inline)) {
-    float* const Ca = bufs[q];
-    float* const Cb = bufs[q] + kQT * kQCLd;
-    const float ba0 = ra.bias ? ra.bias[j0] : 0.f, ba1 = ra.bias ? ra.bias[j0 + 1] : 0.f;
-    const float bb0 = rb.bias ? rb.bias[j0] : 0.f, bb1 = rb.bias ? rb.bias[j0 + 1] : 0.f;
-#pragma unroll
-    for (int r = 0; r < kQRows; ++r) {
-      const int rl = wave * kQRows + r;
-      const float2 za = *reinterpret_cast<const float2*>(&Ca[rl * kQCLd + j0]);
-      const float2 zb = *reinterpret_cast<const float2*>(&Cb[rl * kQCLd + j0]);
-      float ya0 = za.x + ba0, ya1 = za.y + ba1;
-      float yb0 = zb.x + bb0, yb1 = zb.y + bb1;
-      if (ra.bias_ne && nes[q][0][rl]) {
-        ya0 += ra.bias_ne[j0];
-        ya1 += ra.bias_ne[j0 + 1];
-      }
-      if (rb.bias_ne && nes[q][1][rl]) {
-        yb0 += rb.bias_ne[j0];
-        yb1 += rb.bias_ne[j0 + 1];
-      }
-      activate_q(relu, l2, ya0, ya1);
-      activate_q(relu, l2, yb0, yb1);
-      float y0, y1;
-      if (combine == GNNREC_ACC_MAX) {
-        y0 = fmaxf(ya0, yb0);
-        y1 = fmaxf(ya1, yb1);
-      } else if (combine == GNNREC_ACC_ATTN_LAST) {
-        const float at0 = attn_vec[j0], at1 = attn_vec[j0 + 1];
-        float sa = ya0 * at0 + ya1 * at1, sb = yb0 * at0 + yb1 * at1;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          sa += __shfl_xor(sa, off);
-          sb += __shfl_xor(sb, off);
-        }
-        const float mnew = fmaxf(sa, sb);
-        const float keep = expf(sa - mnew), cnew = expf(sb - mnew);
-        const float nrm = 1.f / (1.f * keep + cnew);
-        y0 = (ya0 * keep + yb0 * cnew) * nrm;
-        y1 = (ya1 * keep + yb1 * cnew) * nrm;
-      } else {
-        y0 = ya0 + yb0;
-        y1 = ya1 + yb1;
-      }
-      if (out_div > 0.f) {
-        y0 = y0 / out_div;
-        y1 = y1 / out_div;
-      }
-      if (pt0 + rl < plim) {
-        typedef float f32x2s __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(f32x2s{y0, y1},
-                                    reinterpret_cast<f32x2s*>(out + (pt0 + rl) * ldo + j0));
-      }
-    }
-  };
-
-  // tiles in order: whole tiles of the queue's chunks, or this block's XCD's contiguous
-  // eighth (block-strided below 8 blocks); wave 0 draws a chunk, the block follows
-  RqCursor cur;
-  if (rq != nullptr && wave == 0) rq_begin(cur, rq);
-  const int64_t tiles = (n_dst + kQT - 1) / kQT;
-  const bool by_xcd = gridDim.x >= (unsigned)kRqHeads;
-  const int xcd = by_xcd ? blockIdx.x % kRqHeads : 0;
-  const int64_t per = by_xcd ? (int64_t)(gridDim.x - xcd + kRqHeads - 1) / kRqHeads
-                             : (int64_t)gridDim.x;
-  int64_t st = by_xcd ? tiles * xcd / kRqHeads + blockIdx.x / kRqHeads : (int64_t)blockIdx.x;
-  const int64_t st_hi = by_xcd ? tiles * (xcd + 1) / kRqHeads : tiles;
-  int64_t ch0 = 0, ch1 = 0;  // the block's current chunk [ch0, ch1), ch0 advancing by tiles
-  auto next_tile = [&](int64_t& t0, int64_t& lim) __attribute__((always_inline)) {
-    if (ch0 >= ch1) {
-      __syncthreads();  // every wave has read blk_r before wave 0 overwrites it
-      if (wave == 0) {
-        int64_t r0 = -1, r1 = 0;
-        if (rq != nullptr) {
-          if (!rq_next(cur, rq, n_dst, rq_ch, r0, r1)) r0 = -1;
-        } else if (st < st_hi) {
-          r0 = st * kQT;
-          r1 = r0 + kQT < n_dst ? r0 + kQT : n_dst;
-          st += per;
-        }
-        if (lane == 0) {
-          blk_r[0] = r0;
-          blk_r[1] = r1;
-        }
-      }
-      __syncthreads();
-      ch0 = blk_r[0];
-      ch1 = blk_r[1];
-      if (ch0 < 0) return false;
-    }
-    t0 = ch0;
-    lim = ch1;
-    ch0 += kQT;
-    return true;
-  };
-
-  int p = 0;  // buffer of the previous tile
-  bool have_prev = false;
-  int64_t pt0 = 0, plim = 0;
-  while (true) {
-    int64_t t0 = 0, lim = 0;
-    const bool have = next_tile(t0, lim);
-    if (have_prev) {  // the previous tile's MFMAs, chunk 0's operands ahead of the gather
-#pragma unroll
-      for (int v = 0; v < 16; ++v) c[v] = 0.f;
-      const int64_t hr = pt0 + li < plim ? pt0 + li : plim - 1;
-      hrow = H + hr * ldh;
-      arow = bufs[p] + li * kQGLd + kQD * rr;
-      mi = 0;
-      prefetch();
-    }
-    if (have) {
-      const int q = p ^ 1;
-      const int64_t rbase = t0 + wave * kQRows;
-      const int64_t left = lim - rbase;
-      const int nv = (int)(left <= 0 ? 0 : left < kQRows ? left : kQRows);
-      gather4<WA, kQGLd, GNNREC_SPQ_PLU>(ra, X, ldx, rbase, nv, bufs[q], wave * kQRows, 0,
-                                         nes[q][0], lane, tick);
-      gather4<WB, kQGLd, GNNREC_SPQ_PLU>(rb, X, ldx, rbase, nv, bufs[q], wave * kQRows, kQD,
-                                         nes[q][1], lane, tick);
-    }
-    while (mi < 128) tick();  // what the gather did not cover
-    __syncthreads();  // this tile's aggregates complete; the previous tile's MFMAs read
-    if (have_prev) {
-      // D map of the 32x32 MFMA: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 bh
-      float* cp = bufs[p] + (rr ? kQT * kQCLd : 0) + 32 * cb + li;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) cp[((v & 3) + 8 * (v >> 2) + 4 * bh) * kQCLd] = c[v];
-      __syncthreads();
-      finish(p, pt0, plim);
-      __syncthreads();  // buffer p is free for the next tile's gather
-    }
-    if (!have) break;
-    have_prev = true;
-    p ^= 1;
-    pt0 = t0;
-    plim = lim;
-  }
-  if (rq != nullptr) rq_finish(rq);
-}
-
 }  // namespace
 }  // namespace gnnrec
 
@@ -580,8 +366,8 @@ extern "C" int gnnrec_spmm_pair_f32(
     const int64_t* indptr_a, const int32_t* indices_a, const float* ew_a, int reduce_a,
     const float* bias_a, const float* bias_nonempty_a, const int64_t* indptr_b,
     const int32_t* indices_b, const float* ew_b, int reduce_b, const float* bias_b,
-    const float* bias_nonempty_b, const float* X, int64_t ldx, const float* H, int64_t ldh,
-    const float* WT4, int64_t n_dst, int64_t d, int epilogue, int combine,
+    const float* bias_nonempty_b, const float* X, int64_t n_src, int64_t ldx, const float* H,
+    int64_t ldh, const float* WT4, int64_t n_dst, int64_t d, int epilogue, int combine,
     const float* attn_vec, float out_div, float* out, int64_t ldo, void* stream) {
   GNNREC_REQUIRE(d == kQD, "gnnrec_spmm_pair_f32: only d = %d (got %lld)", kQD, (long long)d);
   GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
@@ -619,21 +405,10 @@ extern "C" int gnnrec_spmm_pair_f32(
   const RawRel b{indptr_b, indices_b, ew_b, bias_b, bias_nonempty_b,
                  reduce_b == GNNREC_REDUCE_MEAN};
   const dim3 grid((unsigned)blocks), block(kQWaves * 64);
-  static const bool pipe = [] {  // GNNREC_SPQ_PIPE=0: the two-phase kernel (A/B)
-    const char* e = getenv("GNNREC_SPQ_PIPE");
-    return !(e && e[0] == '0');
-  }();
+  GNNREC_REQUIRE(n_src >= 0, "gnnrec_spmm_pair_f32: negative n_src");
 #define GNNREC_SPQ(WA_, WB_)                                                                   \
-  do {                                                                                         \
-    if (pipe)                                                                                  \
-      hipLaunchKernelGGL((spmm_pair_pipe_kernel<WA_, WB_>), grid, block, 0, s, a, b, X, ldx,   \
-                         H, ldh, WT4, n_dst, epilogue, combine, attn_vec, out_div, out, ldo,   \
-                         rq, rq_ch);                                                           \
-    else                                                                                       \
-      hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_>), grid, block, 0, s, a, b, X, ldx,   \
-                         H, ldh, WT4, n_dst, epilogue, combine, attn_vec, out_div, out, ldo,   \
-                         rq, rq_ch);                                                           \
-  } while (0)
+  hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_>), grid, block, 0, s, a, b, X, ldx, H, ldh, \
+                     WT4, n_dst, epilogue, combine, attn_vec, out_div, out, ldo, rq, rq_ch)
   if (ew_a) {
     if (ew_b) GNNREC_SPQ(true, true);
     else GNNREC_SPQ(true, false);

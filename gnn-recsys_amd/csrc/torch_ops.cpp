@@ -403,7 +403,7 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
                           (int)reduce_a, p<float>(bias_a), p<float>(bias_nonempty_a),
                           p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b),
                           (int)reduce_b, p<float>(bias_b), p<float>(bias_nonempty_b),
-                          p<float>(X), ldx, p<float>(H), ldh, p<float>(WT4), n_dst, d,
+                          p<float>(X), X.size(0), ldx, p<float>(H), ldh, p<float>(WT4), n_dst, d,
                           (int)epilogue, (int)combine, p<float>(attn_vec), (float)out_div,
                           p<float>(out), ldo, stream_of(X)),
      "gnnrec_spmm_pair_f32");

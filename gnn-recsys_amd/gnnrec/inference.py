@@ -943,11 +943,12 @@ class ShardedFullGraphPass:
         return True
 
     def _pair_raw(self, plan) -> bool:
-        """The pair gathers one raw table (gnnrec_spmm_pair_f32) when both relations come
-        from the same source type with no fc_preagg (their messages are that table itself)
-        and the backend has the op; GNNREC_PAIR_RAW=0 keeps the pre-projected form."""
+        """The pair gathers one raw table (gnnrec_spmm_pair_f32) when GNNREC_PAIR_RAW=1, both
+        relations come from the same source type with no fc_preagg (their messages are that
+        table itself) and the backend has the op.  Off by default: at C5 the pre-projected
+        launch plus its GEMMs is 0.5 ms faster per pass (csrc/spmm_pair_mfma.hip)."""
         return getattr(self.ops, 'spmm_pair', None) is not None and \
-            os.environ.get("GNNREC_PAIR_RAW", "1") != "0" and \
+            os.environ.get("GNNREC_PAIR_RAW", "0") != "0" and \
             plan[0][1][0] == plan[1][1][0] and not plan[0][3] and not plan[1][3]
 
     def _pair_plan(self, hconv, h, ces):

@@ -278,7 +278,7 @@ class HeteroGraphConv(nn.Module):
             plans.append(p)
         combine, div = _pair_combine(self.aggregate)
         dtype = ces[0][2]
-        if plans[0][0] is plans[1][0] and os.environ.get("GNNREC_PAIR_RAW", "1") != "0":
+        if plans[0][0] is plans[1][0] and os.environ.get("GNNREC_PAIR_RAW", "0") != "0":
             # both messages are the one source table itself: ops.spmm_pair gathers it raw and
             # runs all four projections in its epilogue (the sharded pass's _pair_raw)
             rels = []

@@ -286,7 +286,8 @@ int gnnrec_spmm_project2_f32(const int64_t* indptr_a, const int32_t* indices_a,
  *   out[v] = combine( epi(H[v] W_self_a^T + agg_a(v) W_neigh_a^T + bias_a [+ bias_nonempty_a]),
  *                     epi(H[v] W_self_b^T + agg_b(v) W_neigh_b^T + bias_b [+ bias_nonempty_b]) )
  *            / out_div
- * agg_r = sum / mean over relation r's in-edges of X[indices_r[e]] (* ew_r[e]).  WT4 is the
+ * agg_r = sum / mean over relation r's in-edges of X[indices_r[e]] (* ew_r[e]), X [n_src, d]
+ * with row stride ldx (indices_r < n_src).  WT4 is the
  * packed k-major weight array [W_self_a^T | W_neigh_a^T | W_self_b^T | W_neigh_b^T], four
  * contiguous d x d blocks (block[k][n] = W[n][k]).  The projections run on the fp32 MFMA
  * in 32-row tiles; the gathered working set is the one table (gnnrec_spmm_project2_f32
@@ -298,8 +299,9 @@ int gnnrec_spmm_pair_f32(const int64_t* indptr_a, const int32_t* indices_a, cons
                          int reduce_a, const float* bias_a, const float* bias_nonempty_a,
                          const int64_t* indptr_b, const int32_t* indices_b, const float* ew_b,
                          int reduce_b, const float* bias_b, const float* bias_nonempty_b,
-                         const float* X, int64_t ldx, const float* H, int64_t ldh,
-                         const float* WT4, int64_t n_dst, int64_t d, int epilogue, int combine,
+                         const float* X, int64_t n_src, int64_t ldx, const float* H,
+                         int64_t ldh, const float* WT4, int64_t n_dst, int64_t d, int epilogue,
+                         int combine,
                          const float* attn_vec, float out_div, float* out, int64_t ldo,
                          void* stream);
 

@@ -1108,8 +1108,9 @@ def test_fused_sharded_pass_equals_modules_bitwise():
                                    atol=ATOL)
 
 
+@pytest.mark.parametrize("raw", [False, True])
 @pytest.mark.parametrize("hetero", ["sum", "mean", "max", "attention"])
-def test_pair_launch_modules_and_pass_match_oracle(hetero):
+def test_pair_launch_modules_and_pass_match_oracle(hetero, raw, monkeypatch):
     """Two item->user relations from a table of at most half the users (the C5 shape,
     small): HeteroGraphConv and the sharded pass both run them as ONE pre-projected
     spmm_project2 launch — bitwise the same at P=1 — and match the oracle's two
@@ -1117,6 +1118,9 @@ def test_pair_launch_modules_and_pass_match_oracle(hetero):
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     from gnnrec.inference import GraphShard, ShardedFullGraphPass, full_graph_embeddings
+    # raw: both relations gather the one raw item table (gnnrec_spmm_pair_f32) in the module
+    # path and the pass alike
+    monkeypatch.setenv("GNNREC_PAIR_RAW", "1" if raw else "0")
     rng = np.random.default_rng(11)
     n_u, n_i, d = 900, 300, 128
     edges = {}
@@ -1139,6 +1143,7 @@ def test_pair_launch_modules_and_pass_match_oracle(hetero):
     runner = ShardedFullGraphPass(model, shard, fold_embedding=False)
     h2 = runner.run(lf)
     assert runner.pair_fused == {(("item", "clicked-by", "user"), ("item", "bought-by", "user"))}
+    assert bool(runner.pair_raw) == raw
     for nt in h1:
         assert torch.equal(h1[nt], h2[nt][: h1[nt].shape[0]]), nt
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}

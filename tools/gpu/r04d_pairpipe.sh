@@ -8,7 +8,7 @@ O=gpurun_out/r04d
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
   -k "pair or project2" > $O/tests.log 2>&1 || { echo "pair tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
-for v in pipe twophase pre plu2 pipe; do
+for v in pipe twophase pre plu2; do
   E=""
   case $v in twophase) E="GNNREC_SPQ_PIPE=0";; pre) E="GNNREC_PAIR_RAW=0";; plu2) E="GNNREC_LIB=$PWD/tools/_diag/libgnnrec_spq_plu2.so";; esac
   env $E timeout -k 10 400 python -u bench.py --config c5 --steps 5 --warmup 2 --minibatch off --cpu-baseline off \
