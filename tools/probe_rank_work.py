@@ -99,7 +99,9 @@ def main():
             "imbalance": comp / (sum(x["compute_ms"] for x in ranks) / P),
             "comm_bytes_per_rank": comm_b, "comm_ms_floor": round(comm_ms, 3),
             "projected_ms_no_overlap": round(comp + comm_ms, 3),
-            "projected_ms_full_overlap": round(max(comp, comm_ms), 3)}
+            "projected_ms_full_overlap": round(max(comp, comm_ms), 3),
+            # RCCL's all-to-all reaching half the links' rate, nothing overlapped
+            "projected_ms_half_rate_no_overlap": round(comp + 2 * comm_ms, 3)}
         print(json.dumps({"P": P, **{k: v for k, v in res["per_P"][str(P)].items()
                                      if k != "ranks"}}), flush=True)
     if "1" in res["per_P"]:
@@ -107,6 +109,8 @@ def main():
         for P, v in res["per_P"].items():
             v["speedup_no_overlap"] = round(base / v["projected_ms_no_overlap"], 2)
             v["speedup_full_overlap"] = round(base / v["projected_ms_full_overlap"], 2)
+            v["speedup_half_rate_no_overlap"] = round(
+                base / v["projected_ms_half_rate_no_overlap"], 2)
     out = json.dumps(res, indent=1)
     if a.out:
         open(a.out, "w").write(out)
