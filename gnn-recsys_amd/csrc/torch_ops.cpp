@@ -746,28 +746,37 @@ constexpr int64_t kSplit = 2048;  // ops.DEFAULT_SPLIT: heavy rows of the transp
 float* pw(const Tensor& t) { return t.defined() ? p<float>(t) : nullptr; }
 
 Tensor gemm_nt(const Tensor& A, const Tensor& W, const Tensor* A2, const Tensor* W2, int epi,
-               Tensor out, Tensor* row_norm, int accum = GNNREC_ACC_STORE) {
+               Tensor out, Tensor* row_norm, int accum = GNNREC_ACC_STORE,
+               const float* bias = nullptr, const float* bias_ne = nullptr,
+               const int32_t* a2_deg = nullptr) {
   const int64_t M = A.size(0), K1 = A.size(1), N = W.size(0);
   const int64_t K2 = A2 ? A2->size(1) : 0;
   ck(gnnrec_gemm_rownorm_f32(p<float>(A), ld(A, "A"), K1, p<float>(W), A2 ? p<float>(*A2) : nullptr,
-                             A2 ? ld(*A2, "A2") : 1, K2, W2 ? p<float>(*W2) : nullptr, nullptr,
-                             GNNREC_A2_NONE, nullptr, nullptr, M, N, epi, accum, 0.f,
+                             A2 ? ld(*A2, "A2") : 1, K2, W2 ? p<float>(*W2) : nullptr, a2_deg,
+                             GNNREC_A2_NONE, bias, bias_ne, M, N, epi, accum, 0.f,
                              nullptr, nullptr, p<float>(out), ld(out, "out"),
                              row_norm ? p<float>(*row_norm) : nullptr, stream_of(A)),
      "gnnrec_gemm_f32");
   return out;
 }
 
-Tensor weight_grad(const Tensor& gu, const Tensor& X) {  // guᵀ X, split-K MFMA
+// guᵀ X, split-K MFMA; colsum (nullable, [M]) receives Σ_k gu[k] from the same pass
+Tensor weight_grad(const Tensor& gu, const Tensor& X, Tensor* colsum = nullptr) {
   const int64_t K = gu.size(0), M = gu.size(1), N = X.size(1);
   Tensor out = at::empty({M, N}, gu.options());
   const int64_t wsb = gnnrec_gemm_tn_workspace_bytes(K, M, N);
   Tensor ws = at::empty({std::max<int64_t>(wsb / 4, 1)}, gu.options());
   ck(gnnrec_gemm_tn_bias_f32(p<float>(gu), ld(gu, "gu"), p<float>(X), ld(X, "X"), K, M, N,
-                             p<float>(out), ld(out, "out"), nullptr, 0, p<float>(ws),
-                             stream_of(gu)),
+                             p<float>(out), ld(out, "out"), colsum ? p<float>(*colsum) : nullptr,
+                             0, p<float>(ws), stream_of(gu)),
      "gnnrec_gemm_tn_bias_f32");
   return out;
+}
+
+// int32 in-degrees of a CSR's rows (the GEMM epilogue's non-empty test for bias_nonempty)
+Tensor row_degrees(const Tensor& indptr) {
+  const int64_t M = indptr.numel() - 1;
+  return (indptr.narrow(0, 1, M) - indptr.narrow(0, 0, M)).to(at::kInt).contiguous();
 }
 
 // sum gather of X over a CSR whose edge count is known on the host but whose degrees are
@@ -802,7 +811,8 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                                                     const Tensor& Wn, const Tensor& indptr,
                                                     const Tensor& indices,
                                                     const optional<Tensor>& ew, int64_t reduce,
-                                                    bool norm) {
+                                                    bool norm, const optional<Tensor>& bias,
+                                                    const optional<Tensor>& bias_ne) {
   const OneDevice one_device_;
   dev(m, "m", at::kFloat);
   dev(h_self, "h_self", at::kFloat);
@@ -819,7 +829,15 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                     "sage_rel_forward: h_self must hold the ", M, " destination rows first");
   TORCH_CHECK_VALUE(Wn.size(0) == N && Ws.size(1) == h_self.size(1) && Wn.size(1) == m.size(1),
                     "sage_rel_forward: weight shapes");
+  // bias (every row) and bias_ne (rows with an in-edge): a NodeEmbedding folded into the
+  // layer (autograd.HeteroSageFn's first-layer fold): W_self b_e and W_neigh b_e
+  dev(bias, "bias", at::kFloat);
+  dev(bias_ne, "bias_nonempty", at::kFloat);
+  TORCH_CHECK_VALUE((!has(bias) || bias->numel() == N) && (!has(bias_ne) || bias_ne->numel() == N),
+                    "sage_rel_forward: biases must have ", N, " entries");
   const Tensor X = m.contiguous(), H = h_self.narrow(0, 0, M).contiguous();
+  const Tensor bc = has(bias) ? bias->contiguous() : Tensor();
+  const Tensor bnc = has(bias_ne) ? bias_ne->contiguous() : Tensor();
   const optional<Tensor> ewc = has(ew) ? optional<Tensor>(ew->contiguous()) : ew;
   const Tensor Wsc = Ws.contiguous(), Wnc = Wn.contiguous();
   Tensor agg = at::empty({M, m.size(1)}, m.options());
@@ -831,12 +849,14 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                          ld(X, "m"), M, X.size(1), (int)reduce, 0, p<float>(agg), ld(agg, "agg"),
                          stream_of(m)),
      "gnnrec_spmm_csr_f32");
+  const Tensor deg = bnc.defined() ? row_degrees(indptr) : Tensor();
   gemm_nt(H, Wsc, &agg, &Wnc, GNNREC_EPI_RELU | (norm ? GNNREC_EPI_L2NORM : 0), z,
-          norm ? &nrm : nullptr);
+          norm ? &nrm : nullptr, GNNREC_ACC_STORE, bc.defined() ? p<float>(bc) : nullptr,
+          bnc.defined() ? p<float>(bnc) : nullptr, deg.defined() ? p<int32_t>(deg) : nullptr);
   return {z, agg, nrm};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     const Tensor& gz_in, const Tensor& z, const Tensor& row_norm, const Tensor& h_self,
     const Tensor& agg, const Tensor& Ws, const Tensor& Wn, const Tensor& indptr,
     const Tensor& indices, const optional<Tensor>& ew, int64_t reduce, int64_t n_src,
@@ -844,6 +864,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     const optional<Tensor>& indices_t_in, const optional<Tensor>& w_mean_in,
     const optional<Tensor>& g_self_out, bool g_self_acc, const optional<Tensor>& g_m_out,
     bool g_m_acc) {
+  // need bits: 1 g_self, 2 g_m, 4 g_Ws, 8 g_Wn, 16 g_bias (Σ rows of the pre-activation
+  // gradient), 32 g_bias_nonempty (the same over rows with an in-edge)
   const OneDevice one_device_;
   dev(gz_in, "gz", at::kFloat);
   dev(z, "z", at::kFloat);
@@ -871,13 +893,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
                                       g_m_out->size(1) == Wn.size(1)),
                     "sage_rel_backward: g_m_out must be a contiguous [n_src, d_neigh]");
   Tensor none = at::empty({0}, z.options());  // outputs not asked for (`need` bits)
-  Tensor g_self = none, g_m = none, g_Ws = none, g_Wn = none;
+  Tensor g_self = none, g_m = none, g_Ws = none, g_Wn = none, g_b = none, g_bne = none;
   if (meta(z)) {
     if ((need & 1) && !has(g_self_out)) g_self = at::empty({h_self.size(0), Ws.size(1)}, z.options());
     if ((need & 2) && !has(g_m_out)) g_m = at::empty({n_src, Wn.size(1)}, z.options());
     if (need & 4) g_Ws = at::empty_like(Ws);
     if (need & 8) g_Wn = at::empty_like(Wn);
-    return {g_self, g_m, g_Ws, g_Wn};
+    if (need & 16) g_b = at::empty({N}, z.options());
+    if (need & 32) g_bne = at::empty({N}, z.options());
+    return {g_self, g_m, g_Ws, g_Wn, g_b, g_bne};
   }
   const c10::DeviceGuard g(z.device());
   void* s = stream_of(z);
@@ -930,10 +954,19 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     g_m = has(g_m_out) ? *g_m_out : at::empty({n_src, Wn.size(1)}, z.options());
     gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m, has(g_m_out) && g_m_acc);
   }
-  if (need & 4) g_Ws = weight_grad(gu, h_self.narrow(0, 0, M).contiguous());
+  if (need & 16) g_b = at::empty({N}, z.options());
+  if (need & 4) {
+    g_Ws = weight_grad(gu, h_self.narrow(0, 0, M).contiguous(), (need & 16) ? &g_b : nullptr);
+  } else if (need & 16) {
+    g_b = gu.sum(0);
+  }
   if (need & 8) g_Wn = weight_grad(gu, agg.contiguous());
+  if (need & 32) {  // Σ over the rows with an in-edge: the mean of an empty set carries no bias
+    const Tensor ne = (row_degrees(indptr) > 0).to(gu.scalar_type()).unsqueeze(1);
+    g_bne = (gu * ne).sum(0);
+  }
   // gradients written in place come back as empty tensors (the caller holds the tables)
-  return {has(g_self_out) ? none : g_self, has(g_m_out) ? none : g_m, g_Ws, g_Wn};
+  return {has(g_self_out) ? none : g_self, has(g_m_out) ? none : g_m, g_Ws, g_Wn, g_b, g_bne};
 }
 
 // Every relation's source-major CSR of one sampled block, in one call (the sampler's
@@ -1608,14 +1641,14 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("csr_has_edges(Tensor indptr, Tensor sorted_indices, int n_src, Tensor u, Tensor v, "
         "Tensor(a!) out) -> ()");
   m.def("sage_rel_forward(Tensor m, Tensor h_self, int n_self, Tensor W_self, Tensor W_neigh, "
-        "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm) "
-        "-> (Tensor, Tensor, Tensor)");
+        "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm, "
+        "Tensor? bias=None, Tensor? bias_nonempty=None) -> (Tensor, Tensor, Tensor)");
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
         "int reduce, int n_src, int nnz, bool norm, int need, Tensor? indptr_t=None, "
         "Tensor? indices_t=None, Tensor? w_mean=None, Tensor(a!)? g_self_out=None, "
         "bool g_self_acc=False, Tensor(b!)? g_m_out=None, bool g_m_acc=False) "
-        "-> (Tensor, Tensor, Tensor, Tensor)");
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("block_transposes(Tensor[] indptrs, Tensor[] indices, int[] n_src, int[] nnz) "
         "-> (Tensor[], Tensor[], Tensor[])");
   m.def("edge_batch_pairs(Tensor[] rel_src, Tensor[] rel_dst, int[] src_type, int[] dst_type, "

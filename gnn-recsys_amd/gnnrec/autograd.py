@@ -203,12 +203,15 @@ class SageRelFn(torch.autograd.Function):
         mask = (1 if need[1] else 0) | (2 if need[0] else 0) | (4 if need[2] else 0) | \
             (8 if need[3] else 0)
         tr = ctx.transposed or (None, None, None)
-        g_self, g_m, g_Ws, g_Wn = ops._T().sage_rel_backward(
+        g_self, g_m, g_Ws, g_Wn, _gb, _gbne = ops._T().sage_rel_backward(
             gz, z, nrm, h_self, agg, Ws.detach(), Wn.detach(), indptr, indices, ew,
             ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask, *tr)
         return (g_m if need[0] else None, g_self if need[1] else None,
                 g_Ws if need[2] else None, g_Wn if need[3] else None,
                 None, None, None, None, None, None, None)
+
+
+PER = 5  # HeteroSageFn parameters per relation: W_preagg, W_self, W_neigh, bias, bias_nonempty
 
 
 class HeteroSageFn(torch.autograd.Function):
@@ -220,8 +223,12 @@ class HeteroSageFn(torch.autograd.Function):
     gradients are never materialised and added by autograd (C3: ten full-table adds per
     step, 0.49 ms), and the engine runs one node per layer instead of one per relation.
 
-    apply(spec, *tables, *[W_preagg_r or None, W_self_r, W_neigh_r for r]) -> one output
-    per dst group.  spec = (n_tables, rels, groups): rels[r] = (src table, dst table, reduce,
+    apply(spec, *tables, *[W_preagg_r or None, W_self_r, W_neigh_r, bias_r or None,
+    bias_nonempty_r or None for r]) -> one output per dst group.  bias_r / bias_nonempty_r
+    carry a NodeEmbedding folded into the first layer (nn.ConvModel._fold_plan): the tables
+    are then the raw features, W_self_r = W_s W_e,dst, bias_r = W_s b_e,dst, W_neigh_r = W_n
+    W_e,src, bias_nonempty_r = W_n b_e,src (rows with an in-edge: the mean of an empty set
+    is 0).  spec = (n_tables, rels, groups): rels[r] = (src table, dst table, reduce,
     norm, n_dst, indptr, indices, edge weight, transposed); groups[k] = (dst table, relation
     indices, 'sum' | 'mean').  W_preagg_r: the relation's fc_preagg (messages relu(x W_preᵀ),
     src/model.py:102,151), whose input gradient is accumulated into the table as well."""
@@ -235,13 +242,15 @@ class HeteroSageFn(torch.autograd.Function):
         zs, saved = [], []
         msgs = []
         for r, (si, di, reduce, norm, n_dst, ip, ix, ew, _tr) in enumerate(rels):
-            Wp = per[3 * r]
+            Wp = per[PER * r]
             m = tables[si] if Wp is None else ops.gemm(tables[si].contiguous(), Wp.detach(),
                                                        relu=True)
             msgs.append(m if Wp is not None else torch.empty(0))
-            Ws, Wn = per[3 * r + 1], per[3 * r + 2]
-            z, agg, nrm = T.sage_rel_forward(m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip,
-                                             ix, ew, ops.REDUCE[reduce], bool(norm))
+            Ws, Wn, b, bne = per[PER * r + 1:PER * r + PER]
+            z, agg, nrm = T.sage_rel_forward(
+                m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip, ix, ew, ops.REDUCE[reduce],
+                bool(norm), None if b is None else b.detach(),
+                None if bne is None else bne.detach())
             zs.append(z)
             saved += [agg, z, nrm]
         outs = []
@@ -255,7 +264,7 @@ class HeteroSageFn(torch.autograd.Function):
         ctx.save_for_backward(*tables, *[t if t is not None else torch.empty(0) for t in per],
                               *saved, *msgs)
         ctx.spec = spec
-        ctx.m_given = [per[3 * r] is not None for r in range(len(rels))]
+        ctx.m_given = [per[PER * r] is not None for r in range(len(rels))]
         ctx.n_src = [tables[rels[r][0]].shape[0] for r in range(len(rels))]
         ctx.nnz = [ops._nnz(rel[5]) for rel in rels]
         return tuple(outs)
@@ -265,13 +274,13 @@ class HeteroSageFn(torch.autograd.Function):
         n_t, rels, groups = ctx.spec
         R = len(rels)
         sv = ctx.saved_tensors
-        tables, per = sv[:n_t], sv[n_t:n_t + 3 * R]
-        saved, msgs = sv[n_t + 3 * R:n_t + 6 * R], sv[n_t + 6 * R:]
+        tables, per = sv[:n_t], sv[n_t:n_t + PER * R]
+        saved, msgs = sv[n_t + PER * R:n_t + (PER + 3) * R], sv[n_t + (PER + 3) * R:]
         need = ctx.needs_input_grad[1:]  # (spec)
         need_t, need_per = need[:n_t], need[n_t:]
         T = ops._T()
         g_tab = [None] * n_t
-        g_per = [None] * (3 * R)
+        g_per = [None] * (PER * R)
         for gi, (_di, idx, mode) in enumerate(groups):
             g = g_outs[gi]
             if g is None:
@@ -282,11 +291,12 @@ class HeteroSageFn(torch.autograd.Function):
             for r in idx:
                 si, di, reduce, norm, _n, ip, ix, ew, tr = rels[r]
                 agg, z, nrm = saved[3 * r:3 * r + 3]
-                Ws, Wn = per[3 * r + 1], per[3 * r + 2]
+                Ws, Wn = per[PER * r + 1], per[PER * r + 2]
                 given = ctx.m_given[r]  # messages through fc_preagg
-                want_m = need_t[si] or (given and need_per[3 * r])
+                want_m = need_t[si] or (given and need_per[PER * r])
                 mask = (1 if need_t[di] else 0) | (2 if want_m else 0) | \
-                    (4 if need_per[3 * r + 1] else 0) | (8 if need_per[3 * r + 2] else 0)
+                    (4 if need_per[PER * r + 1] else 0) | (8 if need_per[PER * r + 2] else 0) | \
+                    (16 if need_per[PER * r + 3] else 0) | (32 if need_per[PER * r + 4] else 0)
                 kw = {}
                 if need_t[di]:
                     acc = g_tab[di] is not None
@@ -301,14 +311,14 @@ class HeteroSageFn(torch.autograd.Function):
                                                 dtype=torch.float32, device=g.device)
                     kw.update(g_m_out=g_tab[si], g_m_acc=acc)
                 t3 = tr if (tr is not None and ew is None) else (None, None, None)
-                _gs, g_m, g_Ws, g_Wn = T.sage_rel_backward(
+                _gs, g_m, g_Ws, g_Wn, g_b, g_bne = T.sage_rel_backward(
                     g, z, nrm, tables[di], agg, Ws.detach(), Wn.detach(), ip, ix, ew,
                     ops.REDUCE[reduce], ctx.n_src[r], ctx.nnz[r], bool(norm), mask, *t3, **kw)
                 if given and want_m:  # relu(x W_preᵀ): mask, then W_pre's two gradients
                     gy = ops.act_backward(msgs[r], g_m, relu=True, l2norm=False)
-                    Wp = per[3 * r]
-                    if need_per[3 * r]:
-                        g_per[3 * r] = ops.gemm_tn(gy, tables[si].contiguous())
+                    Wp = per[PER * r]
+                    if need_per[PER * r]:
+                        g_per[PER * r] = ops.gemm_tn(gy, tables[si].contiguous())
                     if need_t[si]:
                         acc = g_tab[si] is not None
                         if not acc:
@@ -316,10 +326,14 @@ class HeteroSageFn(torch.autograd.Function):
                                                     dtype=torch.float32, device=g.device)
                         ops.gemm(gy, Wp.detach().t().contiguous(), out=g_tab[si],
                                  accum='add' if acc else 'store')
-                if need_per[3 * r + 1]:
-                    g_per[3 * r + 1] = g_Ws
-                if need_per[3 * r + 2]:
-                    g_per[3 * r + 2] = g_Wn
+                if need_per[PER * r + 1]:
+                    g_per[PER * r + 1] = g_Ws
+                if need_per[PER * r + 2]:
+                    g_per[PER * r + 2] = g_Wn
+                if need_per[PER * r + 3]:
+                    g_per[PER * r + 3] = g_b
+                if need_per[PER * r + 4]:
+                    g_per[PER * r + 4] = g_bne
         return (None, *g_tab, *g_per)
 
 

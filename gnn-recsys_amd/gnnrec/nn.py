@@ -33,6 +33,7 @@ import torch.nn as nn
 
 from . import _lib, ops
 from . import autograd as ag
+from . import sampling
 
 USER_ITEM = ("user", "item")
 _PREAGG = ("pool_nn", "pool_nn_edge", "mean_nn", "mean_nn_edge")
@@ -229,12 +230,24 @@ class HeteroGraphConv(nn.Module):
         div = float(R) if (self.aggregate == 'mean' and j == R - 1 and R > 1) else 0.0
         return acc, div
 
-    def _layer_node(self, g, src_inputs, dst_inputs, active):
+    def _layer_node(self, g, src_inputs, dst_inputs, active, fold=None):
         """Training over a block: the whole layer as ONE autograd node (ag.HeteroSageFn,
-        every relation's gradient written into one table per node type), or None."""
+        every relation's gradient written into one table per node type), or None.
+
+        fold {ntype: (W_e, b_e)}: the inputs are RAW features and the types' NodeEmbeddings
+        are folded into the layer — per relation W_self W_e,dst with the bias W_self b_e,dst
+        on every row, W_neigh W_e,src with W_neigh b_e,src on rows with an in-edge (the
+        mean of x W_eᵀ + b_e over a non-empty set is mean(x) W_eᵀ + b_e).  Only for mean
+        relations without fc_preagg or edge weights; None otherwise (the caller embeds)."""
         plan = _layer_plan(self, g, src_inputs, dst_inputs, active)
         if plan is None:
             return None
+        folded = None
+        if fold is not None:
+            if any(preagg or weighted or reduce != 'mean' or ce[0] not in fold or
+                   dtype not in fold for dtype, ce, _m, _rg, preagg, weighted, reduce in plan):
+                return None
+            folded = _fold_weights(plan, fold)
         types = []
         for dtype, ce, *_ in plan:
             for nt in (ce[0], dtype):
@@ -251,8 +264,11 @@ class HeteroGraphConv(nn.Module):
             rels.append((tix[ce[0]], tix[dtype], reduce, bool(mod.norm),
                          dst_inputs[dtype].shape[0], rg.indptr, rg.indices, ew,
                          getattr(rg, 'transposed', None)))
-            per += [mod.fc_preagg.weight if preagg else None, mod.fc_self.weight,
-                    mod.fc_neigh.weight]
+            if folded is None:
+                per += [mod.fc_preagg.weight if preagg else None, mod.fc_self.weight,
+                        mod.fc_neigh.weight, None, None]
+            else:
+                per += [None, *folded[len(rels) - 1]]
         spec = (len(types), tuple(rels),
                 tuple((tix[dt], tuple(groups[dt]), self.aggregate) for dt in order))
         outs = ag.HeteroSageFn.apply(spec, *[src_inputs[nt] for nt in types], *per)
@@ -394,6 +410,30 @@ def _layer_plan(hconv, g, src_inputs, dst_inputs, active):
                 return None
             rels.append((dtype, ce, mod, rg, preagg, weighted, reduce))
     return rels
+
+
+def _fold_weights(plan, fold):
+    """Per relation of a training layer plan (W_self W_e,dst, W_neigh W_e,src, W_self b_e,dst,
+    W_neigh b_e,src), autograd-tracked: per node type T every weight its embedding
+    multiplies is stacked and multiplied once ([W; ...] W_e,T and [W; ...] b_e,T), so a
+    layer costs two small products per node type (the C2 layer: 4 instead of 8)."""
+    uses = {}  # node type -> [(relation index, 0 self | 1 neigh, W)]
+    for r, (dtype, ce, mod, *_rest) in enumerate(plan):
+        uses.setdefault(dtype, []).append((r, 0, mod.fc_self.weight))
+        uses.setdefault(ce[0], []).append((r, 1, mod.fc_neigh.weight))
+    out = [[None] * 4 for _ in plan]
+    for nt, lst in uses.items():
+        W_e, b_e = fold[nt]
+        A = torch.cat([W for _r, _k, W in lst], 0) if len(lst) > 1 else lst[0][2]
+        WF = torch.matmul(A, W_e)
+        BF = torch.matmul(A, b_e)
+        o = 0
+        for r, k, W in lst:
+            n = W.shape[0]
+            out[r][k] = WF[o:o + n]
+            out[r][2 + k] = BF[o:o + n]
+            o += n
+    return out
 
 
 def _pair_combine(aggregate: str):
@@ -582,10 +622,48 @@ class ConvModel(nn.Module):
             h['sport'] = self.sport_embed(h['sport'])
         return h
 
+    def _folded_first_layer(self, blocks, h):
+        """Training: the first layer over the RAW features with the NodeEmbeddings folded
+        into it (HeteroGraphConv._layer_node(fold=...)), or None.  The embedding tables of
+        every source node are never formed, and the backward writes no gradient into them:
+        the first block's transposed gathers and the embeddings' weight-gradient GEMMs over
+        every source row disappear (the fold's weight products are per-layer 64×64 work).
+        Numerically the reference's NodeEmbedding + mean up to fp32 rounding.
+        GNNREC_TRAIN_FOLD=0 keeps embed-then-aggregate."""
+        if os.environ.get("GNNREC_TRAIN_FOLD", "1") == "0" or not blocks or \
+                not getattr(blocks[0], 'is_block', False) or not isinstance(
+                    self.layers[0], HeteroGraphConv) or not _grad_mode(module=self):
+            return None
+        g = blocks[0]
+        fold = {}
+        for nt in h:
+            emb = getattr(self, nt + '_embed', None)
+            if emb is None:
+                return None
+            fold[nt] = (emb.proj_feats.weight, emb.proj_feats.bias)
+        src = dict(h)
+        dst = {k: v[:g.number_of_dst_nodes(k)] for k, v in src.items()}
+        active: Dict[str, list] = {}
+        for ce in g.canonical_etypes:
+            if g.num_edges(ce) and ce[0] in src and ce[2] in dst:
+                active.setdefault(ce[2], []).append(ce)
+        if not active:
+            return None
+        out = self.layers[0]._layer_node(g, src, dst, active, fold=fold)
+        if out is not None and sampling.FIRST_BLOCK_TRANSPOSES[0]:
+            sampling.FIRST_BLOCK_TRANSPOSES[0] = False  # nothing reads them any more
+        return out
+
     def forward(self, blocks, h, pos_g, neg_g, embedding_layer: bool = True):
+        start = 0
         if embedding_layer:
-            h = self.embed(h)
-        h = self.get_repr(blocks, h)
+            h1 = self._folded_first_layer(blocks, h)
+            if h1 is not None:
+                h, start = h1, 1
+            else:
+                h = self.embed(h)
+        for i in range(start, len(blocks)):
+            h = self.layers[i](blocks[i], h)
         if isinstance(self.pred_fn, CosinePrediction) and \
                 os.environ.get("GNNREC_COS_PAIR", "1") != "0":
             pos_score, neg_score = self.pred_fn.pair(pos_g, neg_g, h)

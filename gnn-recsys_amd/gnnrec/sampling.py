@@ -100,7 +100,7 @@ class BlockSampler:
         try:
             for block_id in reversed(range(self.num_layers)):
                 block = self._one_block(g, seeds, block_id, masks)
-                if transposes:
+                if transposes and (block_id > 0 or FIRST_BLOCK_TRANSPOSES[0]):
                     _add_transposes(block)
                 blocks.insert(0, block)
                 seeds = {nt: block.srcdata[NID][nt] for nt in block.ntypes
@@ -189,6 +189,13 @@ class BlockSampler:
             for ce, loc in zip(ces, locs):
                 rels[ce][1] = loc.to(torch.int32)
         return Block(src_nid, num_dst, {ce: tuple(v) for ce, v in rels.items()})
+
+
+# The first block's transposes feed only the gradients of its source tables; a ConvModel
+# that folds its NodeEmbeddings into the first layer (nn.ConvModel._folded_first_layer) takes
+# none, and turns them off here the first time it does (they would be built on demand if
+# another model in the process asks for them: sage_rel_backward sorts the block itself)
+FIRST_BLOCK_TRANSPOSES = [True]
 
 
 def _add_transposes(block: Block) -> None:

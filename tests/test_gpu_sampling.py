@@ -478,6 +478,7 @@ def test_fused_training_relation_equals_two_node_form(monkeypatch, agg, hetero, 
     on sampled blocks (dst-prefix self tables) and on the full graph."""
     from gnnrec import nn as gnn
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    monkeypatch.setenv("GNNREC_TRAIN_FOLD", "0")  # bitwise comparisons: embed, then aggregate
     g, _ = _graph()
     torch.manual_seed(0)
     model = gnn.ConvModel(g, 3, {"user": 5, "item": 6, "hidden": 16, "out": 8}, norm, 0.0, agg,
@@ -532,6 +533,7 @@ def test_layer_node_two_relations_bitwise(monkeypatch):
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    monkeypatch.setenv("GNNREC_TRAIN_FOLD", "0")  # bitwise comparisons: embed, then aggregate
     rng = np.random.default_rng(21)
     n_u, n_i, E = 3000, 400, 30000
     u, i = rng.integers(0, n_u, E), rng.integers(0, n_i, E)
@@ -561,3 +563,63 @@ def test_layer_node_two_relations_bitwise(monkeypatch):
     assert res["1"][1].keys() == res["0"][1].keys() and len(res["1"][1]) > 0
     for n in res["1"][1]:
         assert torch.equal(res["1"][1][n], res["0"][1][n]), n
+
+
+@pytest.mark.parametrize("agg,d_in", [("mean", 64), ("mean", 7), ("mean_nn", 64)])
+def test_first_layer_embedding_fold_matches_embed_then_aggregate(monkeypatch, agg, d_in):
+    """ConvModel folds the NodeEmbeddings into the first training layer (raw features in,
+    W_self W_e / W_neigh W_e with W_self b_e on every row and W_neigh b_e only on rows with
+    an in-edge): the loss and every parameter gradient — the embeddings' included — equal
+    the reference order (embed every source row, aggregate, project; src/model.py:10-24,
+    143-148, 226-235, 462-466) within fp32 rounding.  Half the items were never bought and
+    come in as negatives, so rows without in-edges (no neighbour bias) are in the blocks; feature widths differing
+    from the hidden width (7) fold as well.  mean_nn (fc_preagg, non-linear) does not fold:
+    bit-identical to the unfolded run.  The first block's transposes are no longer built."""
+    from gnnrec import nn as gnn
+    from gnnrec import sampling
+    from gnnrec.graph import HeteroGraph
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    rng = np.random.default_rng(4)
+    n_u, n_i, E = 4000, 500, 30000
+    u, i = rng.integers(0, n_u, E), rng.integers(0, n_i // 2, E)  # items >= n_i/2: no edges
+    g = HeteroGraph({BUYS: (torch.from_numpy(u), torch.from_numpy(i)),
+                     BOUGHT: (torch.from_numpy(i), torch.from_numpy(u))},
+                    {"user": n_u, "item": n_i}, device=DEV)
+    g.nodes["user"].data["features"] = torch.randn(n_u, d_in, device=DEV)
+    g.nodes["item"].data["features"] = torch.randn(n_i, d_in, device=DEV)
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": d_in, "item": d_in, "hidden": 64, "out": 64}, True,
+                          0.0, agg, "cos", "sum", True).to(DEV)
+    loader = EdgeDataLoader(g, {BUYS: torch.arange(3000)}, MultiLayerNeighborSampler([10, 10]),
+                            exclude="reverse_types",
+                            reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
+                            negative_sampler=negative_sampler.Uniform(10), batch_size=512)
+    _, pos_g, neg_g, blocks = next(iter(loader))
+    # rows without in-edges are in the first block (never-bought items, from the negatives)
+    deg = [torch.diff(blocks[0]._rels[ce][0]) for ce in blocks[0].canonical_etypes]
+    assert any(bool((d == 0).any()) for d in deg)
+    res = {}
+    keep = sampling.FIRST_BLOCK_TRANSPOSES[0]
+    try:
+        for fold in ("1", "0"):
+            monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
+            model.zero_grad()
+            _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+            loss = gnn.max_margin_loss(ps, ns, 0.266, 10)
+            loss.backward()
+            res[fold] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                         if p.grad is not None})
+            if fold == "1":
+                assert sampling.FIRST_BLOCK_TRANSPOSES[0] == (agg != "mean")
+    finally:
+        sampling.FIRST_BLOCK_TRANSPOSES[0] = keep
+    assert res["1"][1].keys() == res["0"][1].keys()
+    assert "user_embed.proj_feats.weight" in res["1"][1]
+    if agg != "mean":
+        assert torch.equal(res["1"][0], res["0"][0])
+        for n in res["1"][1]:
+            assert torch.equal(res["1"][1][n], res["0"][1][n]), n
+        return
+    torch.testing.assert_close(res["1"][0], res["0"][0], rtol=1e-5, atol=1e-7)
+    for n in res["1"][1]:
+        torch.testing.assert_close(res["1"][1][n], res["0"][1][n], rtol=1e-4, atol=1e-6, msg=n)

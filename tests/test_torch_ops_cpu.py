@@ -185,6 +185,13 @@ def test_sage_rel_ops_meta_shapes():
     z, agg, nrm = T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 1, True)
     assert tuple(z.shape) == (M, N) and tuple(agg.shape) == (M, d) and tuple(nrm.shape) == (M,)
     g = T.sage_rel_backward(z, z, nrm, hs, agg, Ws, Wn, ip, ix, None, 1, n_src, E, True, 15)
-    assert [tuple(t.shape) for t in g] == [(7, d), (n_src, d), (N, d), (N, d)]
+    assert [tuple(t.shape) for t in g] == [(7, d), (n_src, d), (N, d), (N, d), (0,), (0,)]
+    # a folded NodeEmbedding's biases: their gradients when asked for (need bits 16, 32)
+    b = _meta(N)
+    z, agg, nrm = T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 1, True, b, b)
+    g = T.sage_rel_backward(z, z, nrm, hs, agg, Ws, Wn, ip, ix, None, 1, n_src, E, True, 12 | 48)
+    assert [tuple(t.shape) for t in g] == [(0,), (0,), (N, d), (N, d), (N,), (N,)]
+    with pytest.raises(ValueError, match="biases"):
+        T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 1, True, _meta(N + 1), None)
     with pytest.raises(ValueError, match="sum or mean"):
         T.sage_rel_forward(m, hs, M, Ws, Wn, ip, ix, None, 2, True)
