@@ -736,7 +736,7 @@ def minibatch_step(dev, warmup: int = 5):
             model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True,
                                   0.0, "mean", "cos", "sum", True).to(dev)
             # torch's single-launch Adam (the same update as the reference's default
-            # multi-tensor one; C2 K=10 step -0.1..0.3 ms, tools/gpu_r03_adam.sh);
+            # multi-tensor one; C2 K=10 step -0.1..0.3 ms, profiles/r03e_adam_ab.txt);
             # GNNREC_BENCH_ADAM_FUSED=0 keeps the default implementation
             opt = torch.optim.Adam(model.parameters(), lr=0.005,
                                    fused=os.environ.get('GNNREC_BENCH_ADAM_FUSED') != '0')
