@@ -111,6 +111,10 @@ class LstmAggFn(torch.autograd.Function):
     def backward(ctx, g):
         m, W_ih, indptr, indices = ctx.saved_tensors
         need = ctx.needs_input_grad
+        if ctx.state is None:
+            raise RuntimeError("LstmAggFn: the forward's per-step LSTM state was released by "
+                               "the first backward through this graph; a second backward "
+                               "(retain_graph=True) needs a fresh forward")
         dX, dW_ih, dW_hh, db = ops.lstm_aggregate_backward(indptr, indices, m, W_ih, ctx.state,
                                                           g, need_x=need[0])
         ctx.state = None

@@ -152,7 +152,7 @@ class GraphShard:
         self.shard_rows = {nt: padded_shard(n, world) for nt, n in num_nodes.items()
                            if nt != ptype}
         self.rels: Dict[tuple, RelShard] = {}
-        self._graph = None
+        self._in_edges = {}  # ce -> (src, dst - block start): this rank's rows' in-edges
         self._full_rows = {}
 
     @property
@@ -172,19 +172,16 @@ class GraphShard:
         hit = self._full_rows.get(ce)
         if hit is not None:
             return hit
-        if self._graph is None:
+        s_t, _, d_t = ce
+        if d_t == self.ptype:
+            raise ValueError(f"full_in_rows: {ce} ends in the partitioned type")
+        if ce not in self._in_edges:
             raise NotImplementedError(
                 "a relation whose reducer does not split into per-rank partials (lstm) needs "
                 "the whole in-neighbourhood of the rows a rank owns: build the shard with "
                 "GraphShard.from_graph")
-        s_t, _, d_t = ce
-        if d_t == self.ptype:
-            raise ValueError(f"full_in_rows: {ce} ends in the partitioned type")
-        src, dst = self._graph.all_edges(etype=ce)
+        src, dst = self._in_edges[ce]
         S = self.shard_rows[d_t]
-        lo = self.rank * S
-        sel = (dst >= lo) & (dst < lo + S)
-        src, dst = src[sel], dst[sel] - lo
         if s_t == self.ptype:
             bounds = torch.tensor(self.bounds, dtype=torch.int64, device=src.device)
             owner = torch.searchsorted(bounds, src, right=True) - 1
@@ -271,9 +268,14 @@ class GraphShard:
             raise ValueError(f"balance must be 'degree' or 'count', not {balance!r}")
         sh = cls(rank, world, ptype, {nt: g.num_nodes(nt) for nt in g.ntypes},
                  g.canonical_etypes, dev, segments, weight)
-        sh._graph = g  # full_in_rows: the whole in-neighbourhoods of this rank's rows
         for ce in g.canonical_etypes:
             s, d = g.all_edges(etype=ce)
+            if ce[2] != ptype:
+                # full_in_rows' input: every in-edge (edge-id order) of this rank's block of
+                # the replicated destination rows — kept instead of the whole graph
+                S = sh.shard_rows[ce[2]]
+                sel = (d >= rank * S) & (d < (rank + 1) * S)
+                sh._in_edges[ce] = (s[sel], d[sel] - rank * S)
             E = s.numel()
             eid = torch.arange(E, device=s.device)
             w = g._edata[ce].get(weight_field) if weight_field else None

@@ -21,7 +21,7 @@ ONE="$R/bench.py --steps 1 --warmup 0 --cpu-baseline off --minibatch off $*"
 python3 -c "import sys, json; sys.path.insert(0, '$R'); import bench; \
 json.dump({'csrc_sha': bench.csrc_digest(), 'bench_args': sys.argv[1:], \
 'kernels': {'spmm_project': 'spmm_project_kernel', 'spmm_tile': 'spmm_csr_kernel', \
-'spmm_project_mfma': 'spmm_project_mfma_kernel', 'spmm_tile2': 'spmm_csr2_kernel', 'spmm_project2': 'spmm_project2', \
+'spmm_project_mfma': 'spmm_project_mfma_kernel', 'spmm_tile2': 'spmm_csr2_kernel', 'spmm_project2': 'spmm_project2', 'spmm_pair': 'spmm_pair_mfma_kernel', \
 'spmm': 'spmm_csr_kernel'}}, open('$OUT/${TAG}_pmc_meta.json', 'w'), indent=1)" $* \
   || { echo "meta failed"; exit 1; }
 
