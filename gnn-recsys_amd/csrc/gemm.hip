@@ -244,6 +244,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   }
 }
 
+#ifndef GNNREC_GEMM_STORE
+#define GNNREC_GEMM_STORE 0  // A/B builds: 1 = non-temporal output stores, 2 = no store (timing)
+#endif
 // The common epilogues with their flags known at compile time — FE = bias | relu << 1 |
 // l2norm << 2 (the SAGE projection: ReLU + row norm; fc_preagg: ReLU; NodeEmbedding: bias),
 // store-only, full 128-column tiles, 16-B aligned output — instead of runtime flags in the
@@ -306,9 +309,17 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmArgs& g, f32x16 (&a
       const int rl = flat / C4;
       const int c = (flat % C4) * 4;
       const int64_t row = m0 + wave * 32 + rl;
-      if (row < g.M)
-        *reinterpret_cast<f32x4*>(g.out + row * g.ldo + round * SC + c) =
-            *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+      if (row < g.M) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
+        f32x4* o = reinterpret_cast<f32x4*>(g.out + row * g.ldo + round * SC + c);
+#if GNNREC_GEMM_STORE == 1
+        __builtin_nontemporal_store(v, o);
+#elif GNNREC_GEMM_STORE == 2
+        if (v[0] == 1.2345e-38f) *o = v;  // timing build: the store almost never issues
+#else
+        *o = v;
+#endif
+      }
     }
   }
 }

@@ -64,13 +64,17 @@ __device__ inline int64_t floyd_pick(const Group<G>& grp, uint64_t key, int64_t 
 template <int G>
 __global__ __launch_bounds__(kBlock) void sample_count_kernel(
     const int64_t* __restrict__ indptr, const int64_t* __restrict__ eids,
-    const uint8_t* __restrict__ excluded, const int64_t* __restrict__ seeds, int64_t n_seeds,
-    int64_t fanout, uint64_t key, int64_t* __restrict__ counts) {
+    const uint8_t* __restrict__ excluded_all, const uint8_t* __restrict__ xrows,
+    const int64_t* __restrict__ seeds, int64_t n_seeds, int64_t fanout, uint64_t key,
+    int64_t* __restrict__ counts) {
   const Group<G> grp;
   const int64_t i = (int64_t)blockIdx.x * (kBlock / G) + (threadIdx.x / G);
   if (i >= n_seeds) return;  // uniform per group; groups never share a ballot result
   const int64_t v = seeds[i];
   const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+  // xrows[v] == 0: none of v's in-edges is excluded (the exclusions are one batch's edges),
+  // so v's count needs neither its picks nor their eids
+  const uint8_t* const excluded = excluded_all && (!xrows || xrows[v]) ? excluded_all : nullptr;
   int64_t c;
   if (fanout < 0 || deg <= fanout) {
     if (!excluded) {
@@ -94,15 +98,16 @@ __global__ __launch_bounds__(kBlock) void sample_count_kernel(
 template <int G>
 __global__ __launch_bounds__(kBlock) void sample_fill_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const int64_t* __restrict__ eids, const uint8_t* __restrict__ excluded,
-    const int64_t* __restrict__ seeds, int64_t n_seeds, int64_t fanout, uint64_t key,
-    const int64_t* __restrict__ out_indptr, int64_t* __restrict__ out_src,
-    int64_t* __restrict__ out_eid) {
+    const int64_t* __restrict__ eids, const uint8_t* __restrict__ excluded_all,
+    const uint8_t* __restrict__ xrows, const int64_t* __restrict__ seeds, int64_t n_seeds,
+    int64_t fanout, uint64_t key, const int64_t* __restrict__ out_indptr,
+    int64_t* __restrict__ out_src, int64_t* __restrict__ out_eid) {
   const Group<G> grp;
   const int64_t i = (int64_t)blockIdx.x * (kBlock / G) + (threadIdx.x / G);
   if (i >= n_seeds) return;
   const int64_t v = seeds[i];
   const int64_t beg = indptr[v], end = indptr[v + 1], deg = end - beg;
+  const uint8_t* const excluded = excluded_all && (!xrows || xrows[v]) ? excluded_all : nullptr;
   int64_t o = out_indptr[i];
   if (fanout < 0 || deg <= fanout) {
     // whole row in edge order; two chunks in flight per iteration
@@ -505,9 +510,9 @@ inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b
 using namespace gnnrec;
 
 extern "C" int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids,
-                                   const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
-                                   int64_t fanout, uint64_t seed_key, int64_t* counts,
-                                   void* stream) {
+                                   const uint8_t* excluded, const uint8_t* excluded_rows,
+                                   const int64_t* seeds, int64_t n_seeds, int64_t fanout,
+                                   uint64_t seed_key, int64_t* counts, void* stream) {
   GNNREC_REQUIRE(n_seeds >= 0, "gnnrec_sample_count: negative n_seeds");
   GNNREC_REQUIRE(fanout < 0 || fanout <= kMaxFanout, "gnnrec_sample_count: fanout > %d",
                  kMaxFanout);
@@ -517,7 +522,7 @@ extern "C" int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids,
   const dim3 grid((unsigned)((n_seeds + kBlock / G - 1) / (kBlock / G)));
 #define GNNREC_COUNT(g)                                                                     \
   hipLaunchKernelGGL(sample_count_kernel<g>, grid, dim3(kBlock), 0, as_stream(stream), indptr, \
-                     eids, excluded, seeds, n_seeds, fanout, seed_key, counts)
+                     eids, excluded, excluded_rows, seeds, n_seeds, fanout, seed_key, counts)
   switch (G) {
     case 8: GNNREC_COUNT(8); break;
     case 16: GNNREC_COUNT(16); break;
@@ -530,6 +535,7 @@ extern "C" int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids,
 
 extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int32_t* indices,
                                   const int64_t* eids, const uint8_t* excluded,
+                                  const uint8_t* excluded_rows,
                                   const int64_t* seeds, int64_t n_seeds, int64_t fanout,
                                   uint64_t seed_key, const int64_t* out_indptr, int64_t* out_src,
                                   int64_t* out_eid, void* stream) {
@@ -541,8 +547,8 @@ extern "C" int gnnrec_sample_fill(const int64_t* indptr, const int32_t* indices,
   const dim3 grid((unsigned)((n_seeds + kBlock / G - 1) / (kBlock / G)));
 #define GNNREC_FILL(g)                                                                      \
   hipLaunchKernelGGL(sample_fill_kernel<g>, grid, dim3(kBlock), 0, as_stream(stream), indptr,  \
-                     indices, eids, excluded, seeds, n_seeds, fanout, seed_key, out_indptr,    \
-                     out_src, out_eid)
+                     indices, eids, excluded, excluded_rows, seeds, n_seeds, fanout, seed_key, \
+                     out_indptr, out_src, out_eid)
   switch (G) {
     case 8: GNNREC_FILL(8); break;
     case 16: GNNREC_FILL(16); break;

@@ -478,30 +478,35 @@ void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tenso
 
 // ---------------------------------------------------------------- a9 sampler / relabel
 void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tensor>& excluded,
-                  const Tensor& seeds, int64_t fanout, int64_t seed_key, Tensor& counts) {
+                  const Tensor& seeds, int64_t fanout, int64_t seed_key, Tensor& counts,
+                  const optional<Tensor>& excluded_rows) {
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(eids, "eids", at::kLong);
   dev(excluded, "excluded", at::kByte);
+  dev(excluded_rows, "excluded_rows", at::kByte);
   dev(seeds, "seeds", at::kLong);
   dev(counts, "counts", at::kLong);
   TORCH_CHECK_VALUE(counts.numel() >= seeds.numel(), "counts shorter than seeds");
   if (meta(seeds)) return;
   const c10::DeviceGuard g(seeds.device());
   ck(gnnrec_sample_count(p<int64_t>(indptr), p<int64_t>(eids), p<uint8_t>(excluded),
-                         p<int64_t>(seeds), seeds.numel(), fanout, (uint64_t)seed_key,
+                         p<uint8_t>(excluded_rows), p<int64_t>(seeds), seeds.numel(), fanout,
+                         (uint64_t)seed_key,
                          p<int64_t>(counts), stream_of(seeds)),
      "gnnrec_sample_count");
 }
 
 void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids,
                  const optional<Tensor>& excluded, const Tensor& seeds, int64_t fanout,
-                 int64_t seed_key, const Tensor& out_indptr, Tensor& out_src, Tensor& out_eid) {
+                 int64_t seed_key, const Tensor& out_indptr, Tensor& out_src, Tensor& out_eid,
+                 const optional<Tensor>& excluded_rows) {
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
   dev(eids, "eids", at::kLong);
   dev(excluded, "excluded", at::kByte);
+  dev(excluded_rows, "excluded_rows", at::kByte);
   dev(seeds, "seeds", at::kLong);
   dev(out_indptr, "out_indptr", at::kLong);
   dev(out_src, "out_src", at::kLong);
@@ -510,7 +515,8 @@ void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids
   if (meta(seeds)) return;
   const c10::DeviceGuard g(seeds.device());
   ck(gnnrec_sample_fill(p<int64_t>(indptr), p<int32_t>(indices), p<int64_t>(eids),
-                        p<uint8_t>(excluded), p<int64_t>(seeds), seeds.numel(), fanout,
+                        p<uint8_t>(excluded), p<uint8_t>(excluded_rows), p<int64_t>(seeds),
+                        seeds.numel(), fanout,
                         (uint64_t)seed_key, p<int64_t>(out_indptr), p<int64_t>(out_src),
                         p<int64_t>(out_eid), stream_of(seeds)),
      "gnnrec_sample_fill");
@@ -1307,12 +1313,14 @@ Tensor exclusive_scan_new(const Tensor& x) {
 std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>,
            std::vector<int64_t>>
 sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids,
-             const c10::List<optional<Tensor>>& masks, at::IntArrayRef src_type,
+             const c10::List<optional<Tensor>>& masks,
+             const c10::List<optional<Tensor>>& mask_rows, at::IntArrayRef src_type,
              at::IntArrayRef dst_type, at::IntArrayRef fanouts, at::IntArrayRef keys,
              at::TensorList seeds, at::TensorList prefix_pos, at::TensorList marks) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = seeds.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && masks.size() == R &&
+                        mask_rows.size() == R &&
                         src_type.size() == R && dst_type.size() == R && fanouts.size() == R &&
                         keys.size() == R,
                     "sample_layer: one entry per relation in every relation list");
@@ -1337,7 +1345,7 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
     const Tensor& sd = seeds[dst_type[r]];
     Tensor counts = at::empty({sd.numel()}, sd.options().dtype(at::kLong));
     const optional<Tensor> m = masks.get(r);
-    sample_count(indptrs[r], eids[r], m, sd, fanouts[r], keys[r], counts);
+    sample_count(indptrs[r], eids[r], m, sd, fanouts[r], keys[r], counts, mask_rows.get(r));
     o_ip[r] = exclusive_scan_new(counts);
   }
   std::vector<int64_t> totals(R, 0);
@@ -1360,7 +1368,7 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
     o_eid[r] = at::empty({cap}, sd.options().dtype(at::kLong));
     const optional<Tensor> m = masks.get(r);
     sample_fill(indptrs[r], indices[r], eids[r], m, sd, fanouts[r], keys[r], o_ip[r], o_src[r],
-                o_eid[r]);
+                o_eid[r], mask_rows.get(r));
   }
   // relabel: per node type, mark the new sources and scan
   std::vector<Tensor> rank(NT);
@@ -1601,9 +1609,10 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("edge_mlp(Tensor src, Tensor dst, Tensor P, Tensor Q, Tensor W2, Tensor b2, Tensor w3, "
         "Tensor b3, Tensor(a!) out) -> ()");
   m.def("sample_count(Tensor indptr, Tensor eids, Tensor? excluded, Tensor seeds, int fanout, "
-        "int seed_key, Tensor(a!) counts) -> ()");
+        "int seed_key, Tensor(a!) counts, Tensor? excluded_rows=None) -> ()");
   m.def("sample_fill(Tensor indptr, Tensor indices, Tensor eids, Tensor? excluded, Tensor seeds, "
-        "int fanout, int seed_key, Tensor out_indptr, Tensor(a!) out_src, Tensor(b!) out_eid) -> ()");
+        "int fanout, int seed_key, Tensor out_indptr, Tensor(a!) out_src, Tensor(b!) out_eid, "
+        "Tensor? excluded_rows=None) -> ()");
   m.def("exclusive_scan(Tensor x, Tensor(a!) out, Tensor(b!) workspace) -> ()");
   m.def("mark_ids(Tensor ids, Tensor prefix_pos, Tensor(a!) mark) -> ()");
   m.def("relabel_ids(Tensor ids, Tensor prefix_pos, Tensor rank, int n_prefix, "
@@ -1661,7 +1670,7 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor(b!) i) -> ()");
   m.def("hold_cus(int blocks, int threads, int lds_bytes, int usec, Tensor(a!) sink) -> ()");
   m.def("sample_layer(Tensor[] indptrs, Tensor[] indices, Tensor[] eids, Tensor?[] masks, "
-        "int[] src_type, int[] dst_type, int[] fanouts, int[] keys, Tensor[] seeds, "
+        "Tensor?[] mask_rows, int[] src_type, int[] dst_type, int[] fanouts, int[] keys, Tensor[] seeds, "
         "Tensor(a!)[] prefix_pos, Tensor(b!)[] marks) -> "
         "(Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, Tensor[] src_nid, int[] n_edges)");
   // host-only entry points (no tensors: one catch-all kernel each)

@@ -66,8 +66,8 @@ SIGNATURES = {
                                               _P]),
     "gnnrec_sddmm_cos_f32": (_INT, [_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P]),
     "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
-    "gnnrec_sample_fill": (_INT, [_P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P, _P, _P]),
+    "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
+    "gnnrec_sample_fill": (_INT, [_P, _P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P, _P, _P]),
     "gnnrec_scan_workspace_bytes": (_I64, [_I64]),
     "gnnrec_gemm_tn_workspace_bytes": (_I64, [_I64, _I64, _I64]),
     "gnnrec_gemm_tn_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _INT, _P, _P]),

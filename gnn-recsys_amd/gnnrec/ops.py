@@ -1152,21 +1152,27 @@ def exclusive_scan(x: torch.Tensor) -> torch.Tensor:
 
 
 def sample_count(indptr, eids, seeds, fanout: int, seed_key: int = 0,
-                 excluded: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a9 phase 1: per-seed sampled in-edge counts -> out_indptr [n_seeds+1] (device)."""
+                 excluded: Optional[torch.Tensor] = None,
+                 excluded_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a9 phase 1: per-seed sampled in-edge counts -> out_indptr [n_seeds+1] (device).
+    excluded_rows (uint8 per dst node, optional): nonzero exactly on the dst nodes of the
+    excluded eids — the other seeds skip the eid checks (same counts)."""
     for t, n in ((indptr, "indptr"), (eids, "eids"), (seeds, "seeds")):
         _dev(t, n, torch.int64)
-    if excluded is not None:
-        _dev(excluded, "excluded", torch.uint8)
+    for t, n in ((excluded, "excluded"), (excluded_rows, "excluded_rows")):
+        if t is not None:
+            _dev(t, n, torch.uint8)
     n = seeds.numel()
     fan = -1 if fanout is None or fanout < 0 else int(fanout)
     counts = torch.empty(n, dtype=torch.int64, device=seeds.device)
-    _T().sample_count(indptr, eids, excluded, seeds, fan, _lib.i64(seed_key), counts)
+    _T().sample_count(indptr, eids, excluded, seeds, fan, _lib.i64(seed_key), counts,
+                      excluded_rows)
     return exclusive_scan(counts)
 
 
 def sample_fill(indptr, indices, eids, seeds, fanout: int, seed_key: int, out_indptr,
-                total: int, excluded: Optional[torch.Tensor] = None):
+                total: int, excluded: Optional[torch.Tensor] = None,
+                excluded_rows: Optional[torch.Tensor] = None):
     """a9 phase 2: copy the sampled edges at out_indptr offsets -> (src ids, eids).
 
     indices: the CSR's int32 source ids (graph.in_csr); outputs are int64."""
@@ -1176,32 +1182,35 @@ def sample_fill(indptr, indices, eids, seeds, fanout: int, seed_key: int, out_in
     out_src = torch.empty(total, dtype=torch.int64, device=seeds.device)
     out_eid = torch.empty(total, dtype=torch.int64, device=seeds.device)
     _T().sample_fill(indptr, indices, eids, excluded, seeds, fan, _lib.i64(seed_key), out_indptr,
-                     out_src, out_eid)
+                     out_src, out_eid, excluded_rows)
     return out_src, out_eid
 
 
 def sample_neighbors(indptr, indices, eids, seeds, fanout: int, seed_key: int = 0,
-                     excluded: Optional[torch.Tensor] = None):
+                     excluded: Optional[torch.Tensor] = None,
+                     excluded_rows: Optional[torch.Tensor] = None):
     """a9: in-edges of `seeds` (all, or `fanout` without replacement), minus excluded eids.
 
     indices is the CSR's int32 source-id array; returns (out_indptr [n_seeds+1],
     src global ids int64 [E'], eids [E'])."""
-    out_indptr = sample_count(indptr, eids, seeds, fanout, seed_key, excluded)
+    out_indptr = sample_count(indptr, eids, seeds, fanout, seed_key, excluded, excluded_rows)
     total = int(out_indptr[-1].item())  # size readback
     out_src, out_eid = sample_fill(indptr, indices, eids, seeds, fanout, seed_key, out_indptr,
-                                   total, excluded)
+                                   total, excluded, excluded_rows)
     return out_indptr, out_src, out_eid
 
 
 def sample_layer(indptrs, indices, eids, masks, src_type, dst_type, fanouts, keys, seeds,
-                 prefix_pos, marks):
+                 prefix_pos, marks, mask_rows=None):
     """a9, one block layer in one call (gnnrec::sample_layer): sampled in-edges of every
     relation's seeds + the to_block relabel of every node type, two host size reads.
+    mask_rows: per relation the excluded_rows flags of sample_count (or None).
     -> ([out_indptr], [local src int32], [eids], [src node ids per type], [edge counts])."""
     for t in list(indptrs) + list(eids) + list(seeds) + list(prefix_pos):
         _dev(t, "sample_layer operand", torch.int64)
     fans = [-1 if f is None or f < 0 else int(f) for f in fanouts]
-    return _T().sample_layer(list(indptrs), list(indices), list(eids), list(masks),
+    rows = list(mask_rows) if mask_rows is not None else [None] * len(masks)
+    return _T().sample_layer(list(indptrs), list(indices), list(eids), list(masks), rows,
                              list(src_type), list(dst_type), fans, [_lib.i64(k) for k in keys],
                              list(seeds), list(prefix_pos), list(marks))
 

@@ -80,6 +80,16 @@ class BlockSampler:
             self._exclude_masks[key] = m
         return m
 
+    def _mask_rows(self, g, ce):
+        """Per dst node of ce: 1 on the dst of an excluded eid (set and cleared with the
+        mask): the sampler kernels check eids only for those seeds."""
+        key = (id(g), ce, 'rows')
+        m = self._exclude_masks.get(key)
+        if m is None:
+            m = torch.zeros(g.num_nodes(ce[2]), dtype=torch.uint8, device=g.device)
+            self._exclude_masks[key] = m
+        return m
+
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
                       exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
                       transposes: bool = False) -> List[Block]:
@@ -95,7 +105,10 @@ class BlockSampler:
                 ce = g.to_canonical_etype(ce)
                 m = self._mask(g, ce)
                 m.index_fill_(0, eids, 1)  # (m[eids] = 1 copies the scalar: a host sync)
-                masks[ce] = (m, eids)
+                rows = self._mask_rows(g, ce)
+                dst = g.find_edges(eids, ce)[1]
+                rows.index_fill_(0, dst, 1)
+                masks[ce] = (m, eids, rows, dst)
         blocks = []
         try:
             for block_id in reversed(range(self.num_layers)):
@@ -106,8 +119,9 @@ class BlockSampler:
                 seeds = {nt: block.srcdata[NID][nt] for nt in block.ntypes
                          if block.number_of_src_nodes(nt) > 0}
         finally:
-            for ce, (m, eids) in masks.items():
+            for ce, (m, eids, rows, dst) in masks.items():
                 m.index_fill_(0, eids, 0)
+                rows.index_fill_(0, dst, 0)
         # copy edge data into every block and node data into the input block (DGL copies
         # features at block creation; the reference reads blocks[0].srcdata['features'])
         for b in blocks:
@@ -140,7 +154,8 @@ class BlockSampler:
             [tix[ce[2]] for ce in ces], fans,
             [_mix(self.seed, self._calls, block_id, r) for r in range(len(ces))],
             [seeds.get(nt, empty) for nt in nts], [r.prefix_pos for r in rel],
-            [r.mark for r in rel])
+            [r.mark for r in rel],
+            mask_rows=[masks.get(ce, (None, None, None))[2] for ce in ces])
         rels = {}
         for r, ce in enumerate(ces):
             ip = o_ip[r]
@@ -159,15 +174,16 @@ class BlockSampler:
             dseeds = seeds.get(ce[2], empty)
             indptr, indices, eids = g.in_csr_global(ce)
             key = _mix(self.seed, self._calls, block_id, r_idx)
-            mask = masks.get(ce, (None,))[0]
+            mask, _e, mrows = masks.get(ce, (None, None, None))[:3]
             fan = self._fanout(block_id, ce)
-            o_ip = ops.sample_count(indptr, eids, dseeds, fan, key, mask)
-            plan.append((ce, indptr, indices, eids, dseeds, fan, key, mask, o_ip))
+            o_ip = ops.sample_count(indptr, eids, dseeds, fan, key, mask, mrows)
+            plan.append((ce, indptr, indices, eids, dseeds, fan, key, (mask, mrows), o_ip))
         totals = torch.stack([p[-1][-1] for p in plan]).tolist() if plan else []
         rels = {}
         src_lists: Dict[str, list] = {}
         for (ce, indptr, indices, eids, dseeds, fan, key, mask, o_ip), tot in zip(plan, totals):
-            o_src, o_eid = ops.sample_fill(indptr, indices, eids, dseeds, fan, key, o_ip, tot, mask)
+            o_src, o_eid = ops.sample_fill(indptr, indices, eids, dseeds, fan, key, o_ip, tot,
+                                           *mask)
             o_ip._gnnrec_nnz = int(tot)  # edge count known on the host: no later readback
             if fan is not None and 0 <= fan <= ops.DEFAULT_SPLIT:
                 o_ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows possible

@@ -326,14 +326,18 @@ int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
  * in-CSR (indptr/indices/eids), skipping edges whose eid is marked in
  * `excluded` (byte per eid, may be NULL), keeping all of them (fanout < 0)
  * or min(fanout, deg) chosen without replacement by a counter-based RNG
- * keyed on (seed_key, v).  Two phases: count, then fill at caller offsets. */
+ * keyed on (seed_key, v).  Two phases: count, then fill at caller offsets.
+ * excluded_rows (byte per dst node, may be NULL): when given, only seeds v with
+ * excluded_rows[v] != 0 have excluded in-edges (the caller marks the dst of every
+ * excluded eid) — the others skip the eid checks; the result is the same. */
 int gnnrec_sample_count(const int64_t* indptr, const int64_t* eids, const uint8_t* excluded,
-                        const int64_t* seeds, int64_t n_seeds, int64_t fanout,
-                        uint64_t seed_key, int64_t* counts, void* stream);
+                        const uint8_t* excluded_rows, const int64_t* seeds, int64_t n_seeds,
+                        int64_t fanout, uint64_t seed_key, int64_t* counts, void* stream);
 int gnnrec_sample_fill(const int64_t* indptr, const int32_t* indices, const int64_t* eids,
-                       const uint8_t* excluded, const int64_t* seeds, int64_t n_seeds,
-                       int64_t fanout, uint64_t seed_key, const int64_t* out_indptr,
-                       int64_t* out_src, int64_t* out_eid, void* stream);
+                       const uint8_t* excluded, const uint8_t* excluded_rows,
+                       const int64_t* seeds, int64_t n_seeds, int64_t fanout,
+                       uint64_t seed_key, const int64_t* out_indptr, int64_t* out_src,
+                       int64_t* out_eid, void* stream);
 /* exclusive prefix sum of n int64 values (in-place allowed); workspace of
  * gnnrec_scan_workspace_bytes(n) bytes; out[n] receives the total. */
 int64_t gnnrec_scan_workspace_bytes(int64_t n);

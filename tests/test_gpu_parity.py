@@ -318,6 +318,13 @@ def test_sampler_bit_exact_vs_oracle(fanout, exclude):
     np.testing.assert_array_equal(g_ip.cpu().numpy(), r_ip)
     np.testing.assert_array_equal(g_src.cpu().numpy(), r_src)
     np.testing.assert_array_equal(g_eid.cpu().numpy(), r_eid)
+    if exclude:  # per-row flags (the dst of every excluded eid): the same blocks
+        rows = np.zeros(n, np.uint8)
+        rows[dst[excl == 1]] = 1
+        f = ops.sample_neighbors(_t(indptr), _t(indices.astype(np.int32)), _t(eids), _t(seeds),
+                                 fanout, key, _t(excl), _t(rows))
+        for a, b in zip(f, (r_ip, r_src, r_eid)):
+            np.testing.assert_array_equal(a.cpu().numpy(), b)
     # structural: every sampled edge is a real in-edge of its seed, none excluded, no dup
     for i in range(0, seeds.size, 37):
         es = g_eid.cpu().numpy()[r_ip[i]:r_ip[i + 1]]

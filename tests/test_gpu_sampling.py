@@ -457,7 +457,10 @@ def test_cpp_sample_layer_equals_python_form(fanouts):
                     for ce, e in excl.items():
                         m = s._mask(g, ce)
                         m[e] = 1
-                        masks[ce] = (m, e)
+                        rows = s._mask_rows(g, ce)
+                        dst = g.find_edges(e, ce)[1]
+                        rows[dst] = 1
+                        masks[ce] = (m, e, rows, dst)
                 blocks.append(getattr(s, impl)(g, seeds, 1, masks))
             a, b = blocks
             assert a.canonical_etypes == b.canonical_etypes and a._num_dst == b._num_dst
