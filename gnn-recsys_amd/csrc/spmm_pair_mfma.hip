@@ -71,10 +71,49 @@ constexpr int kQCLd = kQD + 8;           // C tile row stride
 #ifndef GNNREC_SPQ_PHASE
 #define GNNREC_SPQ_PHASE 0  // timing builds only: 1 = gather phase alone, 2 = MFMA phase alone
 #endif
+constexpr int kQBLd = 3 * kQD + 8;      // bf16x3: A plane row stride (bf16 elements)
+constexpr int kQPlane = kQT * kQBLd;     // bf16x3: elements per A plane
+#ifndef GNNREC_SPQ_BC
+#define GNNREC_SPQ_BC 2  // bf16x3: K-steps of 16 per double-buffered B chunk
+#endif
 static_assert(2 * kQT * kQCLd <= kQT * kQALd, "C tiles must fit over the A tile");
+static_assert(2 * kQT * kQCLd * 4 <= 3 * kQPlane * 2, "C tiles must fit over the A planes");
 
 typedef float f32x16q __attribute__((ext_vector_type(16)));
 typedef float f32x4q __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8q __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4q __attribute__((ext_vector_type(4)));
+
+// A-tile bytes per block: fp32 [32][388], or the three bf16 planes [3][32][392]
+template <bool BF3>
+constexpr int tile_bytes() { return BF3 ? 3 * kQPlane * 2 : kQT * kQALd * 4; }
+
+// Four consecutive A-tile elements of row `row`, columns [c, c + 4).  BF3: x = hi + mid + lo
+// exactly (each piece the round-to-nearest bf16 of what the previous ones left; the
+// differences are exact in fp32), one plane each, so the six bf16 products of the
+// projection carry the fp32 operand's 24 significant bits.
+template <bool BF3>
+__device__ __forceinline__ void put4(unsigned char* tile, int row, int c, float4 v) {
+  if constexpr (!BF3) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(tile) + row * kQALd + c) = v;
+  } else {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    bf16x4q h, m, l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const __bf16 hi = (__bf16)x[i];
+      const float r1 = x[i] - (float)hi;
+      const __bf16 mi = (__bf16)r1;
+      h[i] = hi;
+      m[i] = mi;
+      l[i] = (__bf16)(r1 - (float)mi);
+    }
+    __bf16* t = reinterpret_cast<__bf16*>(tile) + row * kQBLd + c;
+    *reinterpret_cast<bf16x4q*>(t) = h;
+    *reinterpret_cast<bf16x4q*>(t + kQPlane) = m;
+    *reinterpret_cast<bf16x4q*>(t + 2 * kQPlane) = l;
+  }
+}
 
 struct RawRel {
   const int64_t* indptr;
@@ -103,10 +142,10 @@ __device__ __forceinline__ void activate_q(bool relu, bool l2, float& y0, float&
 
 // The 4 rows [rbase, rbase + nv) of one relation, gathered in lockstep into A tile columns
 // [cofs, cofs + 128) of tile rows [r0, r0 + 4); their non-empty flags into ne[].
-template <bool W>
+template <bool W, bool BF3>
 __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict__ X,
-                                        int64_t ldx, int64_t rbase, int nv, float* As, int r0,
-                                        int cofs, int* ne, int lane) {
+                                        int64_t ldx, int64_t rbase, int nv, unsigned char* As,
+                                        int r0, int cofs, int* ne, int lane) {
   constexpr int LPR = 32, VEC = 4, NPI = kWave / LPR, U = GNNREC_SPQ_LU, kLR = 4;
   const int grp = lane / LPR, col = (lane % LPR) * VEC;
   const int64_t ipl = nv > 0 && lane <= nv ? ld_stream(r.indptr + rbase + lane) : 0;
@@ -170,23 +209,23 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
     combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc[i]);
     if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc[i], dg[i], 0);
     if (grp == 0)
-      *reinterpret_cast<float4*>(&As[(r0 + i) * kQALd + cofs + col]) =
-          make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]);
+      put4<BF3>(As, r0 + i, cofs + col,
+                make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]));
     if (lane == 0) ne[r0 + i] = dg[i] > 0;
   }
 }
 
-template <bool WA, bool WB>
+template <bool WA, bool WB, bool BF3>
 __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
     RawRel ra, RawRel rb, const float* __restrict__ X, int64_t ldx, const float* __restrict__ H,
-    int64_t ldh, const float* __restrict__ WT4, int64_t n_dst, int epilogue, int combine,
-    const float* __restrict__ attn_vec, float out_div, float* __restrict__ out, int64_t ldo,
-    unsigned* rq, int rq_ch) {
-  __shared__ float As[kQT * kQALd];
+    int64_t ldh, const float* __restrict__ WT4, const __bf16* __restrict__ W3, int64_t n_dst,
+    int epilogue, int combine, const float* __restrict__ attn_vec, float out_div,
+    float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
+  __shared__ __attribute__((aligned(16))) unsigned char As[tile_bytes<BF3>()];
   __shared__ int nes[2][kQT];
   __shared__ int64_t blk_r[2];
-  float* const Ca = As;               // over the A tile once the MFMAs have read it
-  float* const Cb = As + kQT * kQCLd;
+  float* const Ca = reinterpret_cast<float*>(As);  // over the A tile once the MFMAs read it
+  float* const Cb = Ca + kQT * kQCLd;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 31, bh = lane >> 5;
@@ -198,15 +237,22 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
   // B operands: lane half bh of a relation-rr wave reads matrix 2·rr + bh of the packed
   // [W_self,aᵀ, W_neigh,aᵀ, W_self,bᵀ, W_neigh,bᵀ] (each k-major 128×128): element
   // [i][32·cb + li]; one 32-bit per-lane offset + an immediate row offset per load
+  // BF3: lane half bh reads matrix 2·rr + bh of W3 [4][3 planes][128 n][128 k] (W itself,
+  // n-major, split as put4 splits A): row 32·cb + li, 8 consecutive k per plane and K-step
+  const void* const wsrc = BF3 ? static_cast<const void*>(W3) : static_cast<const void*>(WT4);
   const uint64_t wbase = ((uint64_t)__builtin_amdgcn_readfirstlane(
-                              (unsigned)((uintptr_t)WT4 >> 32)) << 32) |
-                         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)WT4);
-  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wbase), 0,
-                                                       4 * kQD * kQD * 4, 0x00020000);
-  const int wvoff = ((2 * rr + bh) * kQD * kQD + 32 * cb + li) * 4;
+                              (unsigned)((uintptr_t)wsrc >> 32)) << 32) |
+                         (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)wsrc);
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(wbase), 0, BF3 ? 4 * 3 * kQD * kQD * 2 : 4 * kQD * kQD * 4,
+      0x00020000);
+  const int wvoff = BF3 ? (((2 * rr + bh) * 3 * kQD + 32 * cb + li) * kQD) * 2
+                        : ((2 * rr + bh) * kQD * kQD + 32 * cb + li) * 4;
   // A operands: row li of the tile, K columns [0, 128) (self) for lane half 0 and the
   // relation's aggregate [128 + 128·rr, +128) for lane half 1
-  const float* const ap = As + li * kQALd + (bh ? kQD + kQD * rr : 0);
+  const int acol = bh ? kQD + kQD * rr : 0;
+  const float* const ap = reinterpret_cast<const float*>(As) + li * kQALd + acol;
+  const __bf16* const ab = reinterpret_cast<const __bf16*>(As) + li * kQBLd + acol;
 
   auto tile = [&](int64_t t0, int64_t lim) __attribute__((always_inline)) {
     const int64_t rbase = t0 + wave * kQRows;
@@ -221,11 +267,10 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
       const int rl = 2 * q + bh;
       hs[q] = rl < nv ? ld_stream4(H + (rbase + rl) * ldh + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    gather4<WA>(ra, X, ldx, rbase, nv, As, r0, kQD, nes[0], lane);
-    gather4<WB>(rb, X, ldx, rbase, nv, As, r0, 2 * kQD, nes[1], lane);
+    gather4<WA, BF3>(ra, X, ldx, rbase, nv, As, r0, kQD, nes[0], lane);
+    gather4<WB, BF3>(rb, X, ldx, rbase, nv, As, r0, 2 * kQD, nes[1], lane);
 #pragma unroll
-    for (int q = 0; q < kQRows / 2; ++q)
-      *reinterpret_cast<float4*>(&As[(r0 + 2 * q + bh) * kQALd + col]) = hs[q];
+    for (int q = 0; q < kQRows / 2; ++q) put4<BF3>(As, r0 + 2 * q + bh, col, hs[q]);
     __syncthreads();
 
     constexpr int kWC = GNNREC_SPQ_WC;
@@ -240,9 +285,46 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
 #pragma unroll
     for (int v = 0; v < 16; ++v) c[v] = 0.f;
 #if GNNREC_SPQ_PHASE == 1
-    if (nv < 0)
+    if (nv >= 0) {
+    } else
 #endif
-    {
+    if constexpr (BF3) {
+      // K = 256 as 16 steps of v_mfma_f32_32x32x16_bf16 (self k in lane half 0, aggregate k
+      // in half 1, as the fp32 form), six per step: hi·hi, hi·mid, mid·hi, hi·lo, mid·mid,
+      // lo·hi — the dropped products are below 2^-24 of |a·b| — smallest first
+      constexpr int BC = GNNREC_SPQ_BC, kSteps = kQD / 8;
+      bf16x8q bq[2][BC][3];
+      auto load_b = [&](bf16x8q (*dst)[3], int s0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int st = 0; st < BC; ++st)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            dst[st][p] = __builtin_bit_cast(
+                bf16x8q, __builtin_amdgcn_raw_buffer_load_b128(
+                             wrsrc, wvoff + (s0 + st) * 16, p * kQD * kQD * 2, 0));
+      };
+      load_b(bq[0], 0);
+#pragma unroll
+      for (int ch = 0; ch < kSteps / BC; ++ch) {
+        if (ch + 1 < kSteps / BC) load_b(bq[(ch + 1) & 1], (ch + 1) * BC);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < BC; ++st) {
+          const int s8 = 8 * (ch * BC + st);
+          const bf16x8q a0 = *reinterpret_cast<const bf16x8q*>(ab + s8);
+          const bf16x8q a1 = *reinterpret_cast<const bf16x8q*>(ab + kQPlane + s8);
+          const bf16x8q a2 = *reinterpret_cast<const bf16x8q*>(ab + 2 * kQPlane + s8);
+          const bf16x8q* b = bq[ch & 1][st];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0], c, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
     load_w(bw[0], 0);
 #pragma unroll
     for (int ch = 0; ch < kQD / kWC; ++ch) {
@@ -367,8 +449,8 @@ extern "C" int gnnrec_spmm_pair_f32(
     const float* bias_a, const float* bias_nonempty_a, const int64_t* indptr_b,
     const int32_t* indices_b, const float* ew_b, int reduce_b, const float* bias_b,
     const float* bias_nonempty_b, const float* X, int64_t n_src, int64_t ldx, const float* H,
-    int64_t ldh, const float* WT4, int64_t n_dst, int64_t d, int epilogue, int combine,
-    const float* attn_vec, float out_div, float* out, int64_t ldo, void* stream) {
+    int64_t ldh, const float* WT4, const uint16_t* W3, int64_t n_dst, int64_t d, int epilogue,
+    int combine, const float* attn_vec, float out_div, float* out, int64_t ldo, void* stream) {
   GNNREC_REQUIRE(d == kQD, "gnnrec_spmm_pair_f32: only d = %d (got %lld)", kQD, (long long)d);
   GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
                      (reduce_b == GNNREC_REDUCE_SUM || reduce_b == GNNREC_REDUCE_MEAN),
@@ -382,9 +464,10 @@ extern "C" int gnnrec_spmm_pair_f32(
                  "gnnrec_spmm_pair_f32: attn_vec goes with combine GNNREC_ACC_ATTN_LAST");
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_pair_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(indptr_a && indptr_b && X && H && WT4 && out,
-                 "gnnrec_spmm_pair_f32: null pointer");
-  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(WT4) && ldx % 4 == 0 &&
+  GNNREC_REQUIRE(indptr_a && indptr_b && X && H && out, "gnnrec_spmm_pair_f32: null pointer");
+  GNNREC_REQUIRE((WT4 != nullptr) != (W3 != nullptr),
+                 "gnnrec_spmm_pair_f32: pass exactly one of WT4 (fp32) and W3 (bf16x3)");
+  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(WT4) && aligned16(W3) && ldx % 4 == 0 &&
                      ldh % 4 == 0 && ldo % 2 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                  "gnnrec_spmm_pair_f32: X/H/W need 16-B aligned rows, out 8-B");
@@ -406,16 +489,25 @@ extern "C" int gnnrec_spmm_pair_f32(
                  reduce_b == GNNREC_REDUCE_MEAN};
   const dim3 grid((unsigned)blocks), block(kQWaves * 64);
   GNNREC_REQUIRE(n_src >= 0, "gnnrec_spmm_pair_f32: negative n_src");
-#define GNNREC_SPQ(WA_, WB_)                                                                   \
-  hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_>), grid, block, 0, s, a, b, X, ldx, H, ldh, \
-                     WT4, n_dst, epilogue, combine, attn_vec, out_div, out, ldo, rq, rq_ch)
-  if (ew_a) {
-    if (ew_b) GNNREC_SPQ(true, true);
-    else GNNREC_SPQ(true, false);
-  } else {
-    if (ew_b) GNNREC_SPQ(false, true);
-    else GNNREC_SPQ(false, false);
+  const __bf16* w3 = reinterpret_cast<const __bf16*>(W3);
+#define GNNREC_SPQ(WA_, WB_, BF3_)                                                              \
+  hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_, BF3_>), grid, block, 0, s, a, b, X, ldx, \
+                     H, ldh, WT4, w3, n_dst, epilogue, combine, attn_vec, out_div, out, ldo, rq, \
+                     rq_ch)
+#define GNNREC_SPQ_W(BF3_)                  \
+  if (ew_a) {                               \
+    if (ew_b) GNNREC_SPQ(true, true, BF3_); \
+    else GNNREC_SPQ(true, false, BF3_);     \
+  } else {                                  \
+    if (ew_b) GNNREC_SPQ(false, true, BF3_); \
+    else GNNREC_SPQ(false, false, BF3_);    \
   }
+  if (W3 != nullptr) {
+    GNNREC_SPQ_W(true)
+  } else {
+    GNNREC_SPQ_W(false)
+  }
+#undef GNNREC_SPQ_W
 #undef GNNREC_SPQ
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_pair_f32");

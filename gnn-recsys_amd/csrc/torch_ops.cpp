@@ -371,8 +371,9 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
                const optional<Tensor>& bias_nonempty_a, const Tensor& indptr_b,
                const Tensor& indices_b, const optional<Tensor>& ew_b, int64_t reduce_b,
                const optional<Tensor>& bias_b, const optional<Tensor>& bias_nonempty_b,
-               const Tensor& X, const Tensor& H, const Tensor& WT4, int64_t epilogue,
-               int64_t combine, const optional<Tensor>& attn_vec, double out_div, Tensor& out) {
+               const Tensor& X, const Tensor& H, const optional<Tensor>& WT4,
+               const optional<Tensor>& W3, int64_t epilogue, int64_t combine,
+               const optional<Tensor>& attn_vec, double out_div, Tensor& out) {
   const OneDevice one_device_;
   dev(indptr_a, "indptr_a", at::kLong);
   dev(indices_a, "indices_a", at::kInt);
@@ -387,13 +388,18 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
   dev(X, "X", at::kFloat);
   dev(H, "H", at::kFloat);
   dev(WT4, "WT4", at::kFloat);
+  dev(W3, "W3", at::kBFloat16);
   dev(attn_vec, "attn_vec", at::kFloat);
   dev(out, "out", at::kFloat);
   const int64_t n_dst = indptr_a.numel() - 1, d = X.size(1);
   TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1, "spmm_pair: the relations' row counts differ");
   TORCH_CHECK_VALUE(H.size(1) == d && H.size(0) >= n_dst, "spmm_pair: H shape");
-  TORCH_CHECK_VALUE(WT4.is_contiguous() && WT4.numel() == 4 * d * d,
+  TORCH_CHECK_VALUE(has(WT4) != has(W3),
+                    "spmm_pair: pass exactly one of WT4 (fp32) and W3 (bf16x3 planes)");
+  TORCH_CHECK_VALUE(!has(WT4) || (WT4->is_contiguous() && WT4->numel() == 4 * d * d),
                     "spmm_pair: WT4 must be a contiguous [4, d, d] weight array");
+  TORCH_CHECK_VALUE(!has(W3) || (W3->is_contiguous() && W3->numel() == 12 * d * d),
+                    "spmm_pair: W3 must be a contiguous [4, 3, d, d] bf16 array");
   TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d,
                     "]");
   const int64_t ldx = ld(X, "X"), ldh = ld(H, "H"), ldo = ld(out, "out");
@@ -403,7 +409,7 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
                           (int)reduce_a, p<float>(bias_a), p<float>(bias_nonempty_a),
                           p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b),
                           (int)reduce_b, p<float>(bias_b), p<float>(bias_nonempty_b),
-                          p<float>(X), X.size(0), ldx, p<float>(H), ldh, p<float>(WT4), n_dst, d,
+                          p<float>(X), X.size(0), ldx, p<float>(H), ldh, p<float>(WT4), p<uint16_t>(W3), n_dst, d,
                           (int)epilogue, (int)combine, p<float>(attn_vec), (float)out_div,
                           p<float>(out), ldo, stream_of(X)),
      "gnnrec_spmm_pair_f32");
@@ -1601,7 +1607,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("spmm_pair(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, int reduce_a, "
         "Tensor? bias_a, Tensor? bias_nonempty_a, Tensor indptr_b, Tensor indices_b, "
         "Tensor? ew_b, int reduce_b, Tensor? bias_b, Tensor? bias_nonempty_b, Tensor X, "
-        "Tensor H, Tensor WT4, int epilogue, int combine, Tensor? attn_vec, float out_div, "
+        "Tensor H, Tensor? WT4, Tensor? W3, int epilogue, int combine, Tensor? attn_vec, "
+        "float out_div, "
         "Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
