@@ -46,6 +46,15 @@
 // aggregates double-buffered, self rows straight from H by buffer loads) — 43.9 ms, its MFMA
 // state and gather share 128 VGPRs and spill 124–152 B/lane; LU = 1 / 3 lockstep unrolls 39.9
 // / 39.1 ms; the self rows requested ahead of the gathers: unchanged.
+//
+// bf16x3 (W3 instead of WT4): the projections as six v_mfma_f32_32x32x16_bf16 products per
+// K-step of operands split three ways (A split as the tile is written to LDS, three bf16
+// planes; B pre-split by the caller) — fp32-accurate, 2.7x fewer MFMA issue cycles (3.1 vs
+// 8.3 ms at C5), but 1.5x the weight bytes per tile (768 vs 512 B per lane).  Measured
+// (tools/gpu/r04j_*.sh, profiles/r04j_pair_bf16x3_ab.md): MFMA phase alone 19.8 ms vs 14.2 ms
+// for fp32, the launch 47.3 vs 38.7 ms — the projection phase is bound by streaming the four
+// weight matrices from L2 once per 32-row tile, not by the MFMA.  Kept selectable, not the
+// default.
 #include "common.hpp"
 #include "gather.hpp"
 #include "rowq.hpp"

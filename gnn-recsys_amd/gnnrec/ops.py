@@ -621,8 +621,11 @@ def _packed_bf16x3(Ws_a, Wn_a, Ws_b, Wn_b) -> torch.Tensor:
     return _cached_on(Ws_a, "_gnnrec_w3", tuple(_wkey(W) for W in Ws), make)
 
 
-# Projection arithmetic of the one-table pair launch (GNNREC_PAIR_MFMA: bf16x3 | f32)
-PAIR_MFMA = os.environ.get("GNNREC_PAIR_MFMA", "bf16x3")
+# Projection arithmetic of the one-table pair launch (GNNREC_PAIR_MFMA: f32 | bf16x3).  bf16x3
+# issues 2.7x fewer MFMA cycles but streams 1.5x the weight bytes per tile, and that stream,
+# not the MFMA, bounds the projection phase: C5's pair launch 38.7 ms (f32) vs 47.3 ms
+# (profiles/r04j_pair_bf16x3_ab.md)
+PAIR_MFMA = os.environ.get("GNNREC_PAIR_MFMA", "f32")
 
 
 def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
@@ -772,7 +775,7 @@ def spmm_pair(rel_a, rel_b, X, H, W_self_a, W_neigh_a, W_self_b, W_neigh_b, bias
     mean; combine as spmm_project2.  Unlike spmm_project2 nothing is pre-projected: the
     gathered working set is X alone.  mfma (default PAIR_MFMA): 'f32' runs the projections
     on the fp32 MFMA, 'bf16x3' as six bf16 MFMA products of three-way split operands
-    (fp32-accurate, 2.7x fewer MFMA cycles; _packed_bf16x3)."""
+    (fp32-accurate, 2.7x fewer MFMA cycles, 1.5x the weight bytes; _packed_bf16x3)."""
     D = FUSED_D
     n_dst = rel_a[0].numel() - 1
     args = []
