@@ -83,7 +83,8 @@ def test_random_training_steps_layer_node_matches_relation_nodes(monkeypatch, se
     (=0): the same loss bits, parameter gradients within fp32 reassociation (a table's
     gradient sums up to four relation parts in the node's own order).  Aggregators with and
     without fc_preagg / edge weights, the max / LSTM-free hetero modes, one or two
-    relations per node type, with and without the embedding."""
+    relations per node type, with and without the embedding; and the first layer with the
+    NodeEmbedding folded into it (GNNREC_TRAIN_FOLD=1) within fp32 reassociation."""
     from gnnrec import nn as gnn
     from gnnrec.graph import HeteroGraph
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
@@ -119,8 +120,11 @@ def test_random_training_steps_layer_node_matches_relation_nodes(monkeypatch, se
                             negative_sampler=negative_sampler.Uniform(K), batch_size=128)
     _, pos_g, neg_g, blocks = next(iter(loader))
     res = {}
-    for layer in ("1", "0"):
-        monkeypatch.setenv("GNNREC_TRAIN_LAYER", layer)
+    # layer node vs relation nodes, both embedding then aggregating (GNNREC_TRAIN_FOLD=0: the
+    # bitwise comparison below); then the first layer with the NodeEmbedding folded in
+    for layer, fold in (("1", "0"), ("0", "0"), ("fold", "1")):
+        monkeypatch.setenv("GNNREC_TRAIN_LAYER", "0" if layer == "0" else "1")
+        monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
         model.zero_grad()
         _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, emb)
         loss = gnn.max_margin_loss(ps, ns, 0.266, K)
@@ -135,3 +139,9 @@ def test_random_training_steps_layer_node_matches_relation_nodes(monkeypatch, se
                                        msg=n)
         else:  # one relation per type: every table gradient is a single add either way
             assert torch.equal(res["1"][1][n], res["0"][1][n]), n
+    # the fold: the same layer up to fp32 reassociation (W_s (W_e x) = (W_s W_e) x)
+    torch.testing.assert_close(res["fold"][0], res["1"][0], rtol=1e-5, atol=1e-6)
+    assert res["fold"][1].keys() == res["1"][1].keys()
+    for n in res["1"][1]:
+        torch.testing.assert_close(res["fold"][1][n], res["1"][1][n], rtol=1e-4, atol=2e-6,
+                                   msg=n)
