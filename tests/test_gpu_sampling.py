@@ -603,6 +603,7 @@ def test_first_layer_embedding_fold_matches_embed_then_aggregate(monkeypatch, ag
     assert any(bool((d == 0).any()) for d in deg)
     res = {}
     keep = sampling.FIRST_BLOCK_TRANSPOSES[0]
+    sampling.FIRST_BLOCK_TRANSPOSES[0] = True  # as in a fresh process (other tests fold too)
     try:
         for fold in ("1", "0"):
             monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
