@@ -436,6 +436,12 @@ def _fold_weights(plan, fold):
     return out
 
 
+# First-block source rows from which ConvModel folds its NodeEmbeddings into the first
+# training layer by default (GNNREC_TRAIN_FOLD=auto; C2: ≈0.25M rows at K = 10, ≈1.1M at
+# the reference's K = 2500)
+FOLD_MIN_SRC_ROWS = int(os.environ.get("GNNREC_TRAIN_FOLD_MIN_ROWS", 1 << 19))
+
+
 def _pair_combine(aggregate: str):
     """(spmm_project2 combine, out_div) of a HeteroGraphConv aggregate over two relations."""
     if aggregate in ('max', 'attention'):
@@ -629,12 +635,21 @@ class ConvModel(nn.Module):
         the first block's transposed gathers and the embeddings' weight-gradient GEMMs over
         every source row disappear (the fold's weight products are per-layer 64×64 work).
         Numerically the reference's NodeEmbedding + mean up to fp32 rounding.
-        GNNREC_TRAIN_FOLD=0 keeps embed-then-aggregate."""
-        if os.environ.get("GNNREC_TRAIN_FOLD", "1") == "0" or not blocks or \
+        GNNREC_TRAIN_FOLD: 'auto' (default) folds when the first block has at least
+        FOLD_MIN_SRC_ROWS source rows — the fold's weight products cost ≈0.3 ms of host time
+        per step, which a host-bound small step pays (C2 at K = 10: 2.62 → 2.92 ms without the
+        sampling thread) and a GPU-bound large one recovers several times over (K = 2500:
+        4.3 → 3.46 ms; profiles/r04h_train_fold_ab.md, r04l_k10_fold_ab.md); '1' always, '0'
+        never (embed, then aggregate)."""
+        mode = os.environ.get("GNNREC_TRAIN_FOLD", "auto")
+        if mode == "0" or not blocks or \
                 not getattr(blocks[0], 'is_block', False) or not isinstance(
                     self.layers[0], HeteroGraphConv) or not _grad_mode(module=self):
             return None
         g = blocks[0]
+        if mode != "1" and sum(g.number_of_src_nodes(nt) for nt in g.ntypes) < \
+                FOLD_MIN_SRC_ROWS:
+            return None
         fold = {}
         for nt in h:
             emb = getattr(self, nt + '_embed', None)
