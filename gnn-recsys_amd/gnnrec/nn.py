@@ -437,7 +437,7 @@ def _fold_weights(plan, fold):
 
 
 # First-block source rows from which ConvModel folds its NodeEmbeddings into the first
-# training layer by default (GNNREC_TRAIN_FOLD=auto; C2: ≈0.25M rows at K = 10, ≈1.1M at
+# training layer by default (GNNREC_TRAIN_FOLD=auto; C2: ≈0.36M rows at K = 10, ≈0.96M at
 # the reference's K = 2500)
 FOLD_MIN_SRC_ROWS = int(os.environ.get("GNNREC_TRAIN_FOLD_MIN_ROWS", 1 << 19))
 

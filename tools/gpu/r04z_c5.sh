@@ -1,21 +1,10 @@
 #!/bin/bash
-# round 4 final tree (z3): the C5 bench line + its rocprof record, the 2-rank gloo rehearsal
-# of the multi-GPU bench path against the one-GPU digests (and one rank perturbed), the
-# minibatch kernels' rooflines under rocprofv3
+# round 4 final tree (z3): the C5 bench line + its one-GPU digest, and its rocprof record
 set -o pipefail
 mkdir -p gpurun_out/r04z
 O=gpurun_out/r04z
-SMALL="--users 1000000 --items 100000 --edges 50000000"
-timeout -k 10 400 python -u bench.py --config c5 --minibatch off --cpu-baseline off --record-digest $O/p1_digests.json \
+cp profiles/p1_output_digests.json $O/p1_digests_c5.json || exit 1
+timeout -k 10 400 python -u bench.py --config c5 --minibatch off --cpu-baseline off --record-digest $O/p1_digests_c5.json \
   > $O/c5_bench_n1.json 2> $O/c5_bench_n1.err || { echo "c5 bench failed"; tail -20 $O/c5_bench_n1.err; exit 1; }
-head -c 400 $O/c5_bench_n1.json; echo
-timeout -k 10 1200 bash tools/profile_round.sh r04z_c5 --config c5 || exit 1
-GNNREC_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 $SMALL --steps 3 --warmup 1 \
-  --p1-digests $O/p1_digests.json > $O/gloo2.json 2> $O/gloo2.err || { echo "gloo2 failed"; tail -30 $O/gloo2.err; exit 1; }
-GNNREC_BENCH_PERTURB_RANK=1 GNNREC_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 $SMALL --steps 3 --warmup 1 \
-  --p1-digests $O/p1_digests.json > $O/gloo2_perturbed.json 2> $O/gloo2_perturbed.err || { echo "perturbed failed"; exit 1; }
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_mb -o mb -- python3 $GRAFT_REPO_ROOT/tools/minibatch_roofline.py \
-  > $GRAFT_REPO_ROOT/$O/mb_roof_prof.json 2> $GRAFT_REPO_ROOT/$O/mb_roof_prof.err || { echo "mb rocprof failed"; exit 1; }
+head -c 600 $O/c5_bench_n1.json; echo
+timeout -k 10 900 bash tools/profile_round.sh r04z_c5 --config c5 || exit 1
