@@ -332,6 +332,10 @@ __global__ __launch_bounds__(kCsThreads) void scan_chained_kernel(const T* in, i
   __shared__ int64_t wsum[kCsThreads / 64];
   __shared__ int64_t sh_tile, sh_prefix;
   __shared__ int sh_last;
+  // the tile staged through LDS: loaded and stored coalesced (lane i of a wave on element
+  // i), scanned blocked (16 consecutive elements per thread); one pad word per 16 keeps the
+  // blocked reads off a single bank group
+  __shared__ int64_t stage[kCsTile + kCsTile / kCsItems];
   // slot == nullptr: a one-tile scan (no predecessors, no counters)
   unsigned long long* flags = slot ? slot + kScanFlags0 : nullptr;
   if (threadIdx.x == 0)
@@ -340,12 +344,19 @@ __global__ __launch_bounds__(kCsThreads) void scan_chained_kernel(const T* in, i
                    : 0;
   __syncthreads();
   const int64_t tile = sh_tile;
-  const int64_t base = tile * kCsTile + (int64_t)threadIdx.x * kCsItems;
+  const int64_t t0 = tile * kCsTile;
+  auto pad = [](int i) { return i + i / kCsItems; };
+#pragma unroll
+  for (int j = 0; j < kCsItems; ++j) {
+    const int i = j * kCsThreads + threadIdx.x;
+    stage[pad(i)] = t0 + i < n ? (int64_t)in[t0 + i] : 0;
+  }
+  __syncthreads();
   int64_t vals[kCsItems];
   int64_t s = 0;
 #pragma unroll
   for (int j = 0; j < kCsItems; ++j) {
-    vals[j] = base + j < n ? (int64_t)in[base + j] : 0;
+    vals[j] = stage[pad(threadIdx.x * kCsItems + j)];
     s += vals[j];
   }
   int64_t agg;
@@ -394,10 +405,16 @@ __global__ __launch_bounds__(kCsThreads) void scan_chained_kernel(const T* in, i
   int64_t run = sh_prefix + ex;
 #pragma unroll
   for (int j = 0; j < kCsItems; ++j) {
-    if (base + j < n) out[base + j] = run;
+    stage[pad(threadIdx.x * kCsItems + j)] = run;
     run += vals[j];
   }
   if (tile == n_tiles - 1 && threadIdx.x == kCsThreads - 1) out[n] = run;  // the total
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kCsItems; ++j) {
+    const int i = j * kCsThreads + threadIdx.x;
+    if (t0 + i < n) out[t0 + i] = stage[pad(i)];
+  }
   if (slot == nullptr) return;
   // count the block out; the last one resets the slot for its next user
   if (threadIdx.x == 0)
