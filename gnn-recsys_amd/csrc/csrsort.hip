@@ -129,150 +129,6 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
   }
 }
 
-// ---- one-sweep passes (sorts of 4..kOsMaxTiles tiles: the minibatch blocks' transposes) ----
-// The three launches of a pass (hist, scan of the digit table, scatter) become one: a global
-// histogram of every pass's digits up front (one read of the keys), then per pass one
-// kernel whose block takes the next tile in dispatch order (atomic counter), ranks it as
-// radix_scatter_kernel does, publishes its per-digit counts and walks back over the
-// predecessors' per-digit flags (decoupled look-back, one thread per digit) until one holds
-// an inclusive prefix.  A tile waits only on tiles taken before it, by running blocks, so
-// every wave finishes.  Flags: status in the top 2 bits (0 none, 1 aggregate, 2 inclusive),
-// the count below; zeroed with the counters by one memset per sort.  Same positions as the
-// three-launch form: digit base (exclusive over digits of the global counts) + the earlier
-// tiles' counts of the digit + the earlier waves' + the rank — bitwise the same output.
-constexpr int64_t kOsMaxTiles = 4096;
-constexpr int kOsMaxPasses = 4;
-constexpr unsigned long long kOsAgg = 1ull << 62, kOsIncl = 2ull << 62;
-
-template <class K>
-__global__ __launch_bounds__(kRT) void radix_global_hist_kernel(const K* __restrict__ keys,
-                                                                int64_t E, int passes,
-                                                                unsigned* __restrict__ gcount) {
-  __shared__ unsigned cnt[kOsMaxPasses][kDigits];
-  for (int i = threadIdx.x; i < kOsMaxPasses * kDigits; i += kRT) cnt[i / kDigits][i % kDigits] = 0;
-  __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * kRT;
-  for (int64_t i = (int64_t)blockIdx.x * kRT + threadIdx.x; i < E; i += stride) {
-    const uint32_t k = (uint32_t)keys[i];
-    for (int ps = 0; ps < passes; ++ps) atomicAdd(&cnt[ps][(k >> (8 * ps)) & (kDigits - 1)], 1u);
-  }
-  __syncthreads();
-  for (int ps = 0; ps < passes; ++ps) {
-    const unsigned c = cnt[ps][threadIdx.x];
-    if (c) atomicAdd(&gcount[ps * kDigits + threadIdx.x], c);
-  }
-}
-
-template <class K, bool VIN, int MODE>
-__global__ __launch_bounds__(kRT) void radix_onesweep_kernel(
-    const K* __restrict__ keys, const int32_t* __restrict__ vals, int64_t E, int shift,
-    int64_t n_tiles, const unsigned* __restrict__ gcount, unsigned long long* __restrict__ flags,
-    unsigned long long* __restrict__ tile_ctr, uint32_t* __restrict__ keys_out,
-    int32_t* __restrict__ vals_out, const int64_t* __restrict__ src,
-    int32_t* __restrict__ idx_out, int64_t* __restrict__ eid_out) {
-  __shared__ int cnt[kRT / kWave][kDigits];
-  __shared__ int64_t pos[kRT / kWave][kDigits];
-  __shared__ int64_t dbase[kDigits];
-  __shared__ int64_t sh_tile;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
-  if (tid == 0)
-    sh_tile = (int64_t)__hip_atomic_fetch_add(tile_ctr, 1ull, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-  for (int i = tid; i < (kRT / kWave) * kDigits; i += kRT) cnt[i / kDigits][i % kDigits] = 0;
-  dbase[tid] = (int64_t)gcount[tid];
-  __syncthreads();
-  const int64_t t = sh_tile;
-  // digit bases: exclusive scan of the global counts over the digits (every block)
-  for (int off = 1; off < kDigits; off <<= 1) {
-    const int64_t y = tid >= off ? dbase[tid - off] : 0;
-    __syncthreads();
-    dbase[tid] += y;
-    __syncthreads();
-  }
-  const int64_t base = t * kRTile + (int64_t)w * (kRRounds * kWave);
-  uint32_t kk[kRRounds];
-  int32_t vv[kRRounds];
-  uint32_t dr[kRRounds];
-#pragma unroll
-  for (int j = 0; j < kRRounds; ++j) {
-    const int64_t i = base + j * kWave + lane;
-    const bool act = i < E;
-    const uint32_t k = act ? (uint32_t)keys[i] : 0u;
-    kk[j] = k;
-    vv[j] = act ? (VIN ? vals[i] : (int32_t)i) : 0;
-    const uint32_t d = (k >> shift) & (kDigits - 1);
-    uint64_t peers = __ballot(act);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const uint64_t bb = __ballot((d >> b) & 1u);
-      peers &= ((d >> b) & 1u) ? bb : ~bb;
-    }
-    const unsigned r = __builtin_amdgcn_mbcnt_hi(
-        (unsigned)(peers >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)peers, 0u));
-    const int old = act ? cnt[w][d] : 0;
-    if (act && r == 0) cnt[w][d] = old + __popcll(peers);
-    dr[j] = (d << 16) | (uint32_t)(old + (int)r);
-  }
-  __syncthreads();
-  {  // thread d: the tile's count of digit d, published; then the earlier tiles' counts
-    const int d = tid;
-    int64_t tc = 0;
-#pragma unroll
-    for (int ww = 0; ww < kRT / kWave; ++ww) tc += cnt[ww][d];
-    unsigned long long* f = flags + (int64_t)d * n_tiles;
-    int64_t prefix = 0;
-    if (t == 0) {
-      __hip_atomic_store(f, kOsIncl | (unsigned long long)tc, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(f + t, kOsAgg | (unsigned long long)tc, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      for (int64_t j = t - 1; j >= 0; --j) {
-        unsigned long long v =
-            __hip_atomic_load(f + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((v >> 62) == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          v = __hip_atomic_load(f + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        prefix += (int64_t)(v & ((1ull << 62) - 1));
-        if ((v >> 62) == 2) break;
-      }
-      __hip_atomic_store(f + t, kOsIncl | (unsigned long long)(prefix + tc), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    int64_t run = (d > 0 ? dbase[d - 1] : 0) + prefix;
-#pragma unroll
-    for (int ww = 0; ww < kRT / kWave; ++ww) {
-      pos[ww][d] = run;
-      run += cnt[ww][d];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kRRounds; ++j) {
-    const int64_t i = base + j * kWave + lane;
-    if (i >= E) continue;
-    const int64_t p = pos[w][dr[j] >> 16] + (dr[j] & 0xffff);
-    if (keys_out) keys_out[p] = kk[j];
-    if (MODE == 0) {
-      vals_out[p] = vv[j];
-    } else {
-      idx_out[p] = (int32_t)src[vv[j]];
-      eid_out[p] = vv[j];
-    }
-  }
-}
-
-inline bool onesweep_enabled() {
-  static const bool v = [] {  // GNNREC_RADIX_ONESWEEP=0: the three-launch passes (A/B)
-    const char* e = getenv("GNNREC_RADIX_ONESWEEP");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-inline bool onesweep_fits(int64_t n_tiles) { return n_tiles >= 1 && n_tiles <= kOsMaxTiles; }
-
 // row_ptr[r] = first sorted position with key >= r (run boundaries, one write per row)
 __global__ __launch_bounds__(256) void row_bounds_kernel(const uint32_t* __restrict__ keys,
                                                          int64_t E, int64_t n_rows,
@@ -323,13 +179,6 @@ void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64
 
 }  // namespace
 
-// one-sweep state: the global digit counts and tile counters of every pass, then every
-// pass's [256][tiles] flags
-inline size_t onesweep_bytes(int64_t n_tiles) {
-  return align_up(kOsMaxPasses * (kDigits * 4 + 8)) +
-         align_up((size_t)kOsMaxPasses * kDigits * n_tiles * 8);
-}
-
 size_t radix_ws_bytes(int64_t E, int64_t n_rows) {
   (void)n_rows;
   if (E <= 0) return 0;
@@ -338,35 +187,8 @@ size_t radix_ws_bytes(int64_t E, int64_t n_rows) {
   return 4 * align_up((size_t)E * 4)                            // two (key, value) buffers
          + align_up((size_t)n_hist * 4)                         // per-tile digit counts
          + align_up((size_t)(n_hist + 1) * 8)                   // their scan
-         + align_up((size_t)gnnrec_scan_workspace_bytes(n_hist))
-         + (onesweep_fits(n_tiles) ? onesweep_bytes(n_tiles) : 0);
+         + align_up((size_t)gnnrec_scan_workspace_bytes(n_hist));
 }
-
-namespace {
-
-template <class K>
-void launch_onesweep(const K* keys, const int32_t* vals, int64_t E, int shift, int64_t n_tiles,
-                     const unsigned* gcount, unsigned long long* flags,
-                     unsigned long long* tile_ctr, uint32_t* k_out, int32_t* v_out,
-                     const CsrGather* g, hipStream_t s) {
-  const int64_t* src = g ? g->src : nullptr;
-  int32_t* idx = g ? g->idx_out : nullptr;
-  int64_t* eid = g ? g->eid_out : nullptr;
-#define GNNREC_ONESWEEP(VIN, MODE)                                                          \
-  hipLaunchKernelGGL((radix_onesweep_kernel<K, VIN, MODE>), dim3((unsigned)n_tiles), dim3(kRT), \
-                     0, s, keys, vals, E, shift, n_tiles, gcount, flags, tile_ctr, k_out, v_out, \
-                     src, idx, eid)
-  if (g) {
-    if (vals) GNNREC_ONESWEEP(true, 1);
-    else GNNREC_ONESWEEP(false, 1);
-  } else {
-    if (vals) GNNREC_ONESWEEP(true, 0);
-    else GNNREC_ONESWEEP(false, 0);
-  }
-#undef GNNREC_ONESWEEP
-}
-
-}  // namespace
 
 int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, int64_t E,
                     int64_t n_rows, uint32_t* keys_out, int32_t* vals_out, const CsrGather* g,
@@ -395,45 +217,6 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
   int64_t* offs = reinterpret_cast<int64_t*>(p + 4 * slot + align_up((size_t)n_hist * 4));
   void* scan_ws = p + 4 * slot + align_up((size_t)n_hist * 4) + align_up((size_t)(n_hist + 1) * 8);
   const int passes = key_passes(n_rows);
-  if (onesweep_fits(n_tiles) && passes <= kOsMaxPasses && onesweep_enabled()) {
-    char* q = static_cast<char*>(scan_ws) + align_up((size_t)gnnrec_scan_workspace_bytes(n_hist));
-    unsigned* gcount = reinterpret_cast<unsigned*>(q);  // [passes][256]
-    unsigned long long* ctr = reinterpret_cast<unsigned long long*>(q + kOsMaxPasses * kDigits * 4);
-    unsigned long long* flags =
-        reinterpret_cast<unsigned long long*>(q + align_up(kOsMaxPasses * (kDigits * 4 + 8)));
-    const size_t zero = align_up(kOsMaxPasses * (kDigits * 4 + 8)) +
-                        (size_t)passes * kDigits * n_tiles * 8;
-    if (hipMemsetAsync(q, 0, zero, s) != hipSuccess) return check_launch("radix sort");
-    const unsigned hgrid = (unsigned)std::min<int64_t>((E + kRT * 16 - 1) / (kRT * 16), 1024);
-    if (keys64)
-      hipLaunchKernelGGL(radix_global_hist_kernel<int64_t>, dim3(hgrid), dim3(kRT), 0, s,
-                         static_cast<const int64_t*>(keys_in), E, passes, gcount);
-    else
-      hipLaunchKernelGGL(radix_global_hist_kernel<int32_t>, dim3(hgrid), dim3(kRT), 0, s,
-                         static_cast<const int32_t*>(keys_in), E, passes, gcount);
-    for (int ps = 0; ps < passes; ++ps) {
-      const bool last = ps == passes - 1;
-      uint32_t* k_out = last ? keys_out : kb[ps & 1];
-      int32_t* v_out = last ? vals_out : vb[ps & 1];
-      const CsrGather* gg = last ? g : nullptr;
-      unsigned long long* f = flags + (size_t)ps * kDigits * n_tiles;
-      if (ps == 0) {
-        if (keys64)
-          launch_onesweep(static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles,
-                          gcount, f, ctr, k_out, v_out, gg, s);
-        else
-          launch_onesweep(static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles,
-                          gcount, f, ctr, k_out, v_out, gg, s);
-      } else {
-        launch_onesweep(kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, 8 * ps, n_tiles,
-                        gcount + ps * kDigits, f, ctr + ps, k_out, v_out, gg, s);
-      }
-    }
-    if (row_ptr)
-      hipLaunchKernelGGL(row_bounds_kernel, dim3(flat_grid(E + 1)), dim3(256), 0, s, keys_out, E,
-                         n_rows, row_ptr);
-    return check_launch("radix sort");
-  }
   for (int ps = 0; ps < passes; ++ps) {
     const bool last = ps == passes - 1;
     uint32_t* k_out = last ? keys_out : kb[ps & 1];

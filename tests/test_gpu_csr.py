@@ -25,12 +25,10 @@ def _check(src, dst, n_dst, ref=None):
 
 @pytest.mark.parametrize("E,n_dst", [(0, 1), (0, 9), (1, 1), (5, 1), (5000, 7), (5000, 300),
                                      (2049, 70_000), (100_000, 255), (100_000, 256),
-                                     (100_000, 257), (300_000, 65_536), (300_000, 20_000_000),
-                                     (8_388_608, 1_000_000), (8_388_609, 1_000_000)])
+                                     (100_000, 257), (300_000, 65_536), (300_000, 20_000_000)])
 def test_csr_build_matches_oracle(E, n_dst):
     """every pass count (1-4 passes of 8 bits), tile tails (E not a multiple of 2048),
-    empty rows, one row, empty relations; the one-sweep passes' upper bound (4096 tiles of
-    2048 keys) and one key past it (the three-launch passes)"""
+    empty rows, one row, empty relations"""
     g = torch.Generator(device=DEV)
     g.manual_seed(E + n_dst)
     src = torch.randint(0, 1 << 31, (E,), device=DEV, generator=g)
