@@ -125,7 +125,9 @@ def test_compile_convlayer_forward_fullgraph(d, agg, n_src, deg):
     launch is a torch.ops.gnnrec op with a meta kernel, nothing breaks the graph (the last
     case: a small source table at 10 edges/row, projected before the reduction)."""
     import torch._dynamo
+    from gnnrec import _lib
     from gnnrec import nn as gnn
+    _lib.torch_ops()  # the registration loads on first use: not inside the traced region
     torch._dynamo.reset()
     layer = gnn.ConvLayer((d, d), d, 0.0, agg, True).eval().to("meta")
     g = _meta_rel(n_src, 40, 40 * deg)
