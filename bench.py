@@ -39,7 +39,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICRO
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks).  Without a launcher (WORLD_SIZE unset) N > 1 starts N "
+                         "rank processes itself (torch.distributed.run as a child); under a "
+                         "launcher WORLD_SIZE must equal N (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--users", type=int, default=10_000_000)
@@ -474,9 +477,63 @@ def cpu_baseline(args, d):
                       f"{reps} passes, {tot:.1f} s (setup {t_setup:.0f} s)"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_world(args, env=None):
+    """(world size, None) for this process, or (None, N) when this process must start N
+    ranks itself.  Decided before anything touches the GPU:
+      WORLD_SIZE unset, --gpus N > 1  -> spawn N ranks (the driver or a user ran
+                                         `python bench.py --gpus N` without torchrun);
+      WORLD_SIZE set                  -> it must equal --gpus when --gpus is given: a
+                                         mismatch would print a line whose n_gpus is not
+                                         the GPU count asked for, so it is an error."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            raise SystemExit(f"bench.py: --gpus {n}: need at least one GPU")
+        return (1, None) if n == 1 else (None, n)
+    ws = int(ws)
+    if args.gpus is not None and args.gpus != ws:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}: the launcher "
+                         f"started {ws} rank(s); refusing to report a {ws}-GPU line as "
+                         f"{args.gpus} GPUs")
+    return ws, None
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script with torch.distributed.run (one per GPU, RCCL
+    rendezvous on 127.0.0.1) as a CHILD process and return its exit status (non-zero if any
+    rank failed).  The ranks inherit stdout, so rank 0's JSON line is this run's output.
+    Nothing here initialises the GPU (device_count does not, on this image), so the parent
+    never holds a device while its children run."""
+    import subprocess
+    backend = os.environ.get("GNNREC_DIST_BACKEND", "nccl")
+    have = torch.cuda.device_count()
+    if backend == "nccl" and have < n:
+        sys.stderr.write(f"bench.py: --gpus {n} needs {n} visible GPUs for RCCL, found {have}\n")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    sys.stderr.write(f"[bench] starting {n} ranks: {' '.join(cmd)}\n")
+    sys.stderr.flush()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, spawn = resolve_world(args)
+    if spawn is not None:
+        sys.exit(spawn_ranks(spawn, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev_idx = local_rank % max(1, torch.cuda.device_count())  # rehearsals may share one GPU
@@ -555,7 +612,10 @@ def main():
         torch.cuda.synchronize()
         hb.say(f"warm-up pass {w} done in {(time.perf_counter() - t0) * 1e3:.1f} ms")
     if pex is not None:
-        pex.checked = False
+        # the warm-up passes named every collective; the timed passes run the bare exchange
+        # (no per-collective stderr writes inside the measurement) and only the heartbeat
+        # says where a stalled rank is
+        runner.ex, runner.progress = ex, None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -564,16 +624,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if pex is not None:
-            pex.pass_no = k
         out = runner.run(feats, replicate_output=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     hb.enter(f"timed region done: {elapsed / args.steps * 1e3:.2f} ms per pass on this rank")
-    if pex is not None:
-        runner.ex, runner.progress = ex, None
     if os.environ.get("GNNREC_BENCH_MEMINFO"):
         print(f"[bench] after the timed passes: allocated "
               f"{torch.cuda.memory_allocated() / 2**30:.1f} GiB, reserved "

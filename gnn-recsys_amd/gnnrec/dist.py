@@ -35,6 +35,12 @@ def rank() -> int:
     return dist.get_rank() if is_initialized() else 0
 
 
+def multi_rank(ex) -> bool:
+    """Does the sharded pass run its multi-rank schedule with exchange `ex` (world size > 1,
+    or an Exchange forcing its collectives at world size 1)?"""
+    return bool(getattr(ex, "multi", ex.ws > 1))
+
+
 def even_ranges(n: int, parts: int) -> List[int]:
     """Boundaries b[0..parts] of a contiguous, count-balanced split of [0, n)."""
     return [(n * p) // parts for p in range(parts + 1)]
@@ -72,10 +78,14 @@ def padded_shard(n: int, parts: int) -> int:
 class Exchange:
     """reduce-scatter / all-gather of equal row blocks of a [P·S, d] table."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_collectives: bool = False):
         self.group = group
         self.ws = world()
         self.rk = rank()
+        # force_collectives: issue every collective even at world size 1 (no shortcut), and
+        # make the sharded pass take its multi-rank schedule (`multi`) — the RCCL forms
+        # then run on a one-GPU box (tests/test_gpu_rccl.py), bitwise the one-rank pass
+        self.multi = self.ws > 1 or bool(force_collectives)
         self.backend = dist.get_backend(group) if is_initialized() else None
         # a group created without an explicit backend reports e.g. 'cpu:gloo,cuda:nccl'
         self._rccl = self.backend is not None and "nccl" in str(self.backend)
@@ -97,7 +107,7 @@ class Exchange:
 
     def reduce_scatter_rows(self, full: torch.Tensor, op: str, async_op: bool = False):
         """full [P·S, d] partial on every rank -> (own [S, d], work|None)."""
-        if self.ws == 1:
+        if not self.multi:
             return full, None
         S = full.shape[0] // self.ws
         rop = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
@@ -111,7 +121,7 @@ class Exchange:
 
     def all_gather_rows(self, own: torch.Tensor, out: torch.Tensor, async_op: bool = False):
         """own [S, d] -> out [P·S, d] in rank order, returns (out, work|None)."""
-        if self.ws == 1:
+        if not self.multi:
             if out.data_ptr() != own.data_ptr():
                 out.copy_(own)
             return out, None
@@ -139,7 +149,7 @@ class Exchange:
         table, in source-rank order (the deterministic pass folds them in a fixed tree)."""
         S = full.shape[0] // self.ws
         shape = (self.ws, S) + tuple(full.shape[1:])
-        if self.ws == 1:
+        if not self.multi:
             return full.view(shape), None
         out = torch.empty_like(full)
         if self._fast(full):
@@ -154,7 +164,7 @@ class Exchange:
         return out.view(shape), None
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum"):
-        if self.ws > 1:
+        if self.multi:
             dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX,
                             group=self.group)
         return t
@@ -342,6 +352,7 @@ class ComputeOnlyExchange:
 
     def __init__(self, ws: int, rk: int = 0):
         self.ws, self.rk, self.backend, self.group, self.path = ws, rk, None, None, "none"
+        self.multi = ws > 1
 
     def reduce_scatter_rows(self, full, op, async_op=False):
         S = full.shape[0] // self.ws
@@ -458,6 +469,7 @@ class RecordingExchange:
     def __init__(self, inner: Exchange):
         self.inner = inner
         self.ws, self.rk, self.group = inner.ws, inner.rk, inner.group
+        self.multi = multi_rank(inner)
         self.backend = inner.backend
         self.calls = []
 

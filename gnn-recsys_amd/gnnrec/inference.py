@@ -31,7 +31,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import _lib, ops
-from .dist import Exchange, degree_ranges, even_ranges, padded_shard
+from .dist import Exchange, degree_ranges, even_ranges, multi_rank, padded_shard
 from .graph import HeteroGraph, build_csr
 
 
@@ -380,7 +380,7 @@ class ShardedFullGraphPass:
         # (tools/probe_comm_overlap.py).  Default on HIP devices: (0, True) at one rank,
         # (RESERVE_CUS, True) at several with overlap on.
         if concurrency is None and shard.device.type == 'cuda':
-            concurrency = (RESERVE_CUS if self.ex.ws > 1 and self.side is not None else 0,
+            concurrency = (RESERVE_CUS if multi_rank(self.ex) and self.side is not None else 0,
                            True)
         self.concurrency = concurrency
         self.timers = None  # optional callable(tag) -> context manager (bench)
@@ -515,7 +515,7 @@ class ShardedFullGraphPass:
         # one rank with a side stream: the replicated type's tree + projection GEMMs run on
         # the side stream under the partitioned type's (HBM-bound) aggregation of the same
         # layer; the tile partials then alternate between two scratch sets by layer parity
-        self._owned_side = self.ex.ws == 1 and self.side is not None and \
+        self._owned_side = not multi_rank(self.ex) and self.side is not None and \
             os.environ.get("GNNREC_OWNED_SIDE", "1") != "0"
         for i, layer in enumerate(m.layers):
             self._layer_idx = i
@@ -638,7 +638,7 @@ class ShardedFullGraphPass:
                     own, work = self.ex.reduce_scatter_rows(part, op, async_op=self.overlap)
                     partials[ce] = (own, work, reduce)
                     continue
-                if self.ex.ws == 1 and reduce != 'lstm' and can_fuse is not None and \
+                if not multi_rank(self.ex) and reduce != 'lstm' and can_fuse is not None and \
                         not self.deterministic:
                     self_rows = self._get(h, T)
                     if can_fuse(rs.indptr, msg, self_rows, mod.fc_self.weight,
@@ -652,7 +652,7 @@ class ShardedFullGraphPass:
                     # destination rows runs it over their every in-edge, from the partitioned
                     # table all-gathered (every row: this reducer is off the reference's
                     # hyper-parameter space and is not sized for C4)
-                    if self.ex.ws > 1:
+                    if multi_rank(self.ex):
                         ip, ix = sh.full_in_rows(ce)
                         src = self._gather_ptype(msg) if ce[0] == sh.ptype else msg
                         own = self._lstm(mod, ip, ix, src)
@@ -744,7 +744,7 @@ class ShardedFullGraphPass:
                                       accumulate=True, split=TILE_SPLIT)
         out = {}
         for ce, rs, msg, weighted, reduce in rels:
-            if self.ex.ws == 1 and self._owned_side and \
+            if not multi_rank(self.ex) and self._owned_side and \
                     os.environ.get("GNNREC_TREE_SIDE", "1") != "0":
                 # one rank, owner work on the side stream: the whole tree is folded there
                 # (_owned), off the main stream that runs the pair launch's inputs next
@@ -1042,7 +1042,7 @@ class ShardedFullGraphPass:
                        a2_mode=(_lib.A2_NONE if reduce == 'lstm' else
                                 _lib.A2_ZERO_DEG if reduce == 'max' else _lib.A2_DIV_DEG),
                        **akw, **fkw)
-            if self.ex.ws == 1 or (self._last and not self._replicate_last):
+            if not multi_rank(self.ex) or (self._last and not self._replicate_last):
                 out[T] = o  # the owned rows ARE the table (one rank), or stay partitioned
                 continue
             table = torch.empty((sh.padded_rows(T), o.shape[1]), dtype=torch.float32,
@@ -1081,7 +1081,7 @@ class ShardedFullGraphPass:
             self._local(hconv, h, active, out)
             self._fold.clear()
             return out
-        if self.ex.ws > 1:
+        if multi_rank(self.ex):
             partials = self._partials(hconv, h, active)
             self._local(hconv, h, active, out)
         else:

@@ -59,7 +59,10 @@ def _worker(rank, world, port, case, q):
         # default: every collective async with a real work handle (gloo's own async works),
         # as RCCL issues them; "~sync": the blocking emulation
         # "~a2a": the synchronous Exchange with the all-gather as an all-to-all
-        ex = Exchange() if xk in ("sync", "a2a") else AsyncEmulatedExchange()
+        # "~force": the Exchange issuing every collective at world size 1 too (the
+        # multi-rank schedule of the pass on one rank; its RCCL form: test_gpu_rccl.py)
+        ex = (Exchange(force_collectives=True) if xk == "force" else
+              Exchange() if xk in ("sync", "a2a") else AsyncEmulatedExchange())
         if xk == "a2a":
             ex.ag_mode = "a2a"
         shard = GraphShard.from_graph(g, rank, world, "user", device="cpu",
@@ -67,6 +70,8 @@ def _worker(rank, world, port, case, q):
         feats = {k[5:]: torch.from_numpy(v) for k, v in a.items() if k.startswith("feat/")}
         p = ShardedFullGraphPass(model, shard, ex, ops_backend=oracle_ops, deterministic=bool(det))
         out = p.run(shard.local_features(feats), replicate_output=not part)
+        if xk == "force":
+            assert ex.multi and ex.path == "emulated", ex.path
         if not xk and world > 1:  # the pass asked for every collective async
             assert ex.works_issued > 0 and ex.sync_calls == 0, (ex.works_issued, ex.sync_calls)
         users = gather_partitioned(shard, out["user"], ex)
@@ -131,6 +136,10 @@ def _run(case, world):
     ("model_bip_lstm_sum_emb", 2),
     ("model_het_lstm_mean_noemb_nn", 4),
     ("model_bip_lstm_sum_emb#det", 2),
+    # one rank through the multi-rank schedule (every collective issued, none shortcut)
+    ("model_bip_mean_sum_emb#det~force", 1),
+    ("model_het_meanedge_max_emb~force", 1),
+    ("model_het_mean_sum_skip#part~force", 1),
 ])
 def test_sharded_pass_matches_single_process_oracle(case, world):
     """(#det: the deterministic segment mode, segments=8: per-segment partials folded in a
