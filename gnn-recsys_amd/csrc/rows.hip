@@ -61,6 +61,86 @@ extern "C" int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const i
   return launch<uint8_t>(src, src_ld_bytes, idx, n, row_bytes, dst, dst_ld_bytes, s);
 }
 
+// ---- many gathers in one launch (a sampled batch's edge data + input features) ----
+namespace gnnrec {
+namespace {
+
+struct GatherJobs {
+  const char* src[GNNREC_GATHER_MAX_JOBS];
+  char* dst[GNNREC_GATHER_MAX_JOBS];
+  const int64_t* idx[GNNREC_GATHER_MAX_JOBS];
+  int64_t src_ld[GNNREC_GATHER_MAX_JOBS], dst_ld[GNNREC_GATHER_MAX_JOBS];
+  int64_t n[GNNREC_GATHER_MAX_JOBS], upr[GNNREC_GATHER_MAX_JOBS];
+  int unit[GNNREC_GATHER_MAX_JOBS];  // log2 of the unit bytes: 4, 3, 2 or 0
+  int block0[GNNREC_GATHER_MAX_JOBS + 1];
+  int n_jobs;
+};
+
+template <typename U>
+__device__ __forceinline__ void gather_job(const GatherJobs& J, int j, int64_t t0, int64_t step) {
+  const int64_t upr = J.upr[j], total = J.n[j] * upr;
+  for (int64_t t = t0; t < total; t += step) {
+    const int64_t row = t / upr, u = t - row * upr;
+    const U* s = reinterpret_cast<const U*>(J.src[j] + J.idx[j][row] * J.src_ld[j]) + u;
+    U* d = reinterpret_cast<U*>(J.dst[j] + row * J.dst_ld[j]) + u;
+    *d = *s;
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_rows_batch_kernel(GatherJobs J) {
+  int j = 0;
+  while (j + 1 < J.n_jobs && (int)blockIdx.x >= J.block0[j + 1]) ++j;  // block-uniform
+  const int nb = J.block0[j + 1] - J.block0[j];
+  const int64_t t0 = (int64_t)((int)blockIdx.x - J.block0[j]) * 256 + threadIdx.x;
+  const int64_t step = (int64_t)nb * 256;
+  switch (J.unit[j]) {
+    case 4: gather_job<uint4>(J, j, t0, step); break;
+    case 3: gather_job<uint64_t>(J, j, t0, step); break;
+    case 2: gather_job<uint32_t>(J, j, t0, step); break;
+    default: gather_job<uint8_t>(J, j, t0, step); break;
+  }
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_jobs, void* stream) {
+  GNNREC_REQUIRE(n_jobs >= 0 && n_jobs <= GNNREC_GATHER_MAX_JOBS,
+                 "gnnrec_gather_rows_batch: n_jobs=%d (0..%d)", n_jobs, GNNREC_GATHER_MAX_JOBS);
+  GNNREC_REQUIRE(n_jobs == 0 || jobs, "gnnrec_gather_rows_batch: null jobs");
+  gnnrec::GatherJobs J{};
+  int blocks = 0;
+  for (int i = 0; i < n_jobs; ++i) {
+    const gnnrec_gather_job& g = jobs[i];
+    GNNREC_REQUIRE(g.n >= 0 && g.row_bytes >= 0, "gnnrec_gather_rows_batch: job %d: negative size", i);
+    if (g.n == 0 || g.row_bytes == 0) continue;
+    GNNREC_REQUIRE(g.src && g.idx && g.dst, "gnnrec_gather_rows_batch: job %d: null pointer", i);
+    GNNREC_REQUIRE(g.src_ld_bytes >= g.row_bytes && g.dst_ld_bytes >= g.row_bytes,
+                   "gnnrec_gather_rows_batch: job %d: row stride below the row width", i);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(g.src) | reinterpret_cast<uintptr_t>(g.dst) |
+                         (uintptr_t)g.src_ld_bytes | (uintptr_t)g.dst_ld_bytes | (uintptr_t)g.row_bytes;
+    const int unit = (al & 15u) == 0 ? 4 : (al & 7u) == 0 ? 3 : (al & 3u) == 0 ? 2 : 0;
+    const int k = J.n_jobs++;
+    J.src[k] = static_cast<const char*>(g.src);
+    J.dst[k] = static_cast<char*>(g.dst);
+    J.idx[k] = g.idx;
+    J.src_ld[k] = g.src_ld_bytes;
+    J.dst_ld[k] = g.dst_ld_bytes;
+    J.n[k] = g.n;
+    J.unit[k] = unit;
+    J.upr[k] = g.row_bytes >> unit;
+    int64_t nb = (g.n * J.upr[k] + 255) / 256;
+    if (nb > 8192) nb = 8192;  // grid-stride beyond: 2M units in flight per job
+    J.block0[k] = blocks;
+    blocks += (int)nb;
+  }
+  if (J.n_jobs == 0) return GNNREC_OK;
+  J.block0[J.n_jobs] = blocks;
+  hipLaunchKernelGGL(gnnrec::gather_rows_batch_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     gnnrec::as_stream(stream), J);
+  return gnnrec::check_launch("gnnrec_gather_rows_batch");
+}
+
 // ---- partial-table add (the deterministic pass's fixed tree over source-range tiles) ----
 namespace gnnrec {
 namespace {

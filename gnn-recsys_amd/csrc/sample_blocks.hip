@@ -1,0 +1,568 @@
+// a9 — every block of one bounded-fanout BlockSampler.sample_blocks call in 1 + 3L launches
+// (reference src/sampling.py:153-161: MultiLayerNeighborSampler + to_block + exclude_eids,
+// DGL 0.5.2's _CAPI_DGLSampleNeighbors / _CAPI_DGLToBlock per layer).  The blocks are
+// bitwise those of the per-layer path (sampler.hip: count -> scan -> fill, mark -> scan ->
+// compact -> relabel): the same Floyd picks in the same slots, the same local ids (a seed
+// keeps its position, a new source follows the seeds in ascending global id).
+//
+// What changes is where the relabel state lives and how many launches it takes:
+//   * seed positions: `pos[id]` = (stamp << 32) | position, int64 per node.  A step's seeds
+//     are the entries holding its stamp, so nothing is ever cleared: the next step writes
+//     stamp + 1, and a call starts at a stamp no earlier call used.  The finalize of step s
+//     writes step s+1's entries (its source nodes) while its own relabel reads step s's:
+//     a reader that finds stamp + 1 reads the same position (seeds keep their positions,
+//     new sources get theirs), so the race is benign by construction.
+//   * new sources: one BIT per node (a 1M-node type: 128 KB, not a 4 MB mark array and an
+//     8 MB scan), ranked by a scan of the words' popcounts; two bitmaps per type, the pick
+//     kernel of step s zeroing the one step s+1 uses (the other was read by step s-1).
+//   * sizes stay on the device (`sizes`): step s+1's grids are sized by capacities
+//     (seeds x fanout) and read the actual counts there, so one host read after the call
+//     sizes every block (the per-layer path read back twice per layer).
+#include "common.hpp"
+#include "sampler.hpp"
+
+namespace gnnrec {
+namespace {
+
+constexpr int kSbBlock = 256;
+constexpr int kScanThreads = 1024;
+constexpr int kMaxSec = 4 * GNNREC_SB_MAX_TYPES + 2 * GNNREC_SB_MAX_RELS;
+
+struct RelArgs {
+  const int64_t* indptr;
+  const int32_t* indices;
+  const int64_t* eids;
+  const uint8_t* excl_mask;  // NULL: nothing excluded in this call
+  const uint8_t* excl_rows;
+  int src_t, dst_t;
+  int64_t fanout;
+  uint64_t key;
+  int64_t* counts;
+  int32_t* pick_src;
+  int64_t* pick_eid;
+  int64_t* out_indptr;
+  int32_t* out_src;
+  int64_t* out_eid;
+  int64_t* edge_total;  // sizes entry
+  // exclusion flags set by begin, cleared by the last finalize
+  const int64_t* excl_eids;
+  int64_t n_excl;
+  const int64_t* coo_dst;
+  uint8_t* mask_w;
+  uint8_t* rows_w;
+};
+
+struct TypeArgs {
+  const int64_t* seeds;    // this step's destination nodes
+  const int64_t* n_seeds;  // device count (sizes row s - 1)
+  int64_t seed_cap;
+  unsigned long long* pos;
+  unsigned long long* bits_cur;
+  unsigned long long* bits_next;
+  int64_t* word_rank;
+  int64_t words;
+  int64_t* nodes;          // this step's source node list (the next step's seeds)
+  int64_t* n_nodes_out;    // sizes entry
+  int64_t n_seeds_host;    // begin only: the batch's seed count
+};
+
+// sections of one launch: block ranges [begin[k], begin[k+1]) run job kind[k] on index idx[k]
+struct Sections {
+  int n;
+  int kind[kMaxSec];
+  int idx[kMaxSec];
+  int begin[kMaxSec + 1];
+  __device__ int find(int b) const {
+    int k = 0;
+    while (k + 1 < n && b >= begin[k + 1]) ++k;
+    return k;
+  }
+};
+
+struct StepArgs {
+  int n_rels, n_types, last;
+  uint32_t stamp;
+  RelArgs rel[GNNREC_SB_MAX_RELS];
+  TypeArgs type[GNNREC_SB_MAX_TYPES];
+  Sections sec;
+  int64_t* sizes_seed_row;  // begin: sizes row -1
+};
+
+enum { kSecSeedPos, kSecZeroBits, kSecExclSet, kSecPick, kSecZeroNext, kSecCompact,
+       kSecNewNodes, kSecPrefix, kSecExclClear };
+
+__device__ __forceinline__ unsigned long long pack_pos(uint32_t stamp, int64_t p) {
+  return ((unsigned long long)stamp << 32) | (unsigned long long)(uint32_t)p;
+}
+
+// ---------------------------------------------------------------- begin
+__global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
+  const int k = A.sec.find((int)blockIdx.x);
+  const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
+  const int i = A.sec.idx[k];
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)A.n_types)
+    A.sizes_seed_row[threadIdx.x] = A.type[threadIdx.x].n_seeds_host;
+  switch (A.sec.kind[k]) {
+    case kSecSeedPos: {
+      const TypeArgs& T = A.type[i];
+      if (t < T.n_seeds_host) T.pos[T.seeds[t]] = pack_pos(A.stamp, t);
+      break;
+    }
+    case kSecZeroBits: {
+      const TypeArgs& T = A.type[i];
+      if (t < T.words) T.bits_cur[t] = 0ull;
+      break;
+    }
+    case kSecExclSet: {
+      const RelArgs& R = A.rel[i];
+      if (t < R.n_excl) {
+        const int64_t e = R.excl_eids[t];
+        R.mask_w[e] = 1;
+        R.rows_w[R.coo_dst[e]] = 1;
+      }
+      break;
+    }
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------- pick (step s)
+template <int G>
+__global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
+  const int k = A.sec.find((int)blockIdx.x);
+  const int b = (int)blockIdx.x - A.sec.begin[k];
+  if (A.sec.kind[k] == kSecZeroNext) {
+    const TypeArgs& T = A.type[A.sec.idx[k]];
+    const int64_t w = (int64_t)b * kSbBlock + threadIdx.x;
+    if (w < T.words) T.bits_next[w] = 0ull;
+    return;
+  }
+  const RelArgs& R = A.rel[A.sec.idx[k]];
+  const TypeArgs& D = A.type[R.dst_t];
+  const TypeArgs& S = A.type[R.src_t];
+  const Group<G> grp;
+  const int64_t i = (int64_t)b * (kSbBlock / G) + (threadIdx.x / G);
+  if (i >= *D.n_seeds) return;  // group-uniform
+  const int64_t v = D.seeds[i];
+  const int64_t beg = R.indptr[v], end = R.indptr[v + 1], deg = end - beg;
+  const uint8_t* const excluded =
+      R.excl_mask && (!R.excl_rows || R.excl_rows[v]) ? R.excl_mask : nullptr;
+  const int64_t f = R.fanout;
+  bool keep;
+  int slot, c;
+  int32_t src = 0;
+  int64_t id = 0;
+  if (deg <= f) {  // the whole row (deg <= fanout <= G: one chunk), in edge order
+    const int64_t e = beg + grp.lane;
+    const bool valid = e < end;
+    id = valid ? R.eids[e] : 0;
+    src = valid ? R.indices[e] : 0;
+    keep = valid && !(excluded && excluded[id]);
+    const uint64_t m = grp.ballot(keep);
+    slot = grp.below(m);
+    c = __popcll(m);
+  } else {  // fanout of deg by Floyd's algorithm, kept picks in position order
+    const int kf = (int)f;
+    const int64_t p = floyd_pick(grp, R.key, v, deg, kf);
+    const bool valid = p >= 0;
+    const int64_t e = beg + (valid ? p : 0);
+    id = valid ? R.eids[e] : 0;
+    src = valid ? R.indices[e] : 0;
+    keep = valid && !(excluded && excluded[id]);
+    slot = 0;
+    for (int r = 0; r < kf; ++r) {
+      const int64_t pr = __shfl(p, grp.base + r);
+      const int kr = __shfl((int)keep, grp.base + r);
+      slot += (kr && pr < p) ? 1 : 0;
+    }
+    c = __popcll(grp.ballot(keep));
+  }
+  if (keep) {
+    const int64_t q = i * f + slot;
+    R.pick_src[q] = src;
+    R.pick_eid[q] = id;
+    // a source that is not one of its type's seeds at this step is a new node
+    if ((uint32_t)(S.pos[src] >> 32) != A.stamp) {
+      unsigned long long* w = S.bits_cur + (src >> 6);
+      const unsigned long long bit = 1ull << (src & 63);
+      if ((*w & bit) == 0ull)
+        __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (grp.lane == 0) R.counts[i] = c;
+}
+
+// ---------------------------------------------------------------- scan (step s)
+// one block per relation (counts -> out_indptr, total) and per type (popcounts of the
+// new-source bitmap -> word ranks, total new nodes)
+__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t* wsum, int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t v = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(v, off);
+    if (lane >= off) v += y;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  constexpr int NW = kScanThreads / 64;
+  int64_t before = 0, tot = 0;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int64_t s = wsum[j];
+    if (j < w) before += s;
+    tot += s;
+  }
+  __syncthreads();  // wsum is reused by the next chunk
+  *total = tot;
+  return before + v - x;
+}
+
+__global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
+  __shared__ int64_t wsum[kScanThreads / 64];
+  constexpr int kItems = 4;
+  const int seg = (int)blockIdx.x;
+  const bool is_rel = seg < A.n_rels;
+  int64_t n;
+  const int64_t* cnt = nullptr;
+  const unsigned long long* bits = nullptr;
+  int64_t* out;
+  if (is_rel) {
+    const RelArgs& R = A.rel[seg];
+    n = *A.type[R.dst_t].n_seeds;
+    cnt = R.counts;
+    out = R.out_indptr;
+  } else {
+    const TypeArgs& T = A.type[seg - A.n_rels];
+    n = T.words;
+    bits = T.bits_cur;
+    out = T.word_rank;
+  }
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kItems) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kItems;
+    int64_t v[kItems], s = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      const int64_t i = i0 + j;
+      v[j] = i < n ? (is_rel ? cnt[i] : (int64_t)__popcll(bits[i])) : 0;
+      s += v[j];
+    }
+    int64_t tot;
+    int64_t run = carry + block_excl_scan(s, wsum, &tot);
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      if (i0 + j < n) out[i0 + j] = run;
+      run += v[j];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    out[n] = carry;
+    if (is_rel) {
+      *A.rel[seg].edge_total = carry;
+    } else {
+      const TypeArgs& T = A.type[seg - A.n_rels];
+      *T.n_nodes_out = *T.n_seeds + carry;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- finalize (step s)
+__device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint32_t stamp,
+                                            int32_t s) {
+  const unsigned long long v =
+      __hip_atomic_load(T.pos + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t hi = (uint32_t)(v >> 32);
+  if (hi == stamp || hi == stamp + 1u) return (int64_t)(uint32_t)v;  // a seed, or written
+  const int64_t w = s >> 6;                                          // by this finalize
+  return n_p + T.word_rank[w] + __popcll(T.bits_cur[w] & ((1ull << (s & 63)) - 1ull));
+}
+
+__global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
+  const int k = A.sec.find((int)blockIdx.x);
+  const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
+  const int x = A.sec.idx[k];
+  switch (A.sec.kind[k]) {
+    case kSecCompact: {  // capacity slot t = (seed i, pick j) -> the block CSR
+      const RelArgs& R = A.rel[x];
+      const TypeArgs& D = A.type[R.dst_t];
+      const TypeArgs& S = A.type[R.src_t];
+      const int64_t i = t / R.fanout, j = t - i * R.fanout;
+      if (i >= *D.n_seeds || j >= R.counts[i]) return;
+      const int64_t o = R.out_indptr[i] + j;
+      R.out_src[o] = (int32_t)local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
+      R.out_eid[o] = R.pick_eid[t];
+      break;
+    }
+    case kSecNewNodes: {  // bitmap word t -> its new nodes, ascending, after the seeds
+      const TypeArgs& T = A.type[x];
+      if (t >= T.words) return;
+      unsigned long long word = T.bits_cur[t];
+      if (!word) return;
+      int64_t p = *T.n_seeds + T.word_rank[t];
+      while (word) {
+        const int64_t id = t * 64 + __builtin_ctzll(word);
+        T.nodes[p] = id;
+        __hip_atomic_store(T.pos + id, pack_pos(A.stamp + 1u, p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        word &= word - 1ull;
+        ++p;
+      }
+      break;
+    }
+    case kSecPrefix: {  // the seeds open the source node list, at their positions
+      const TypeArgs& T = A.type[x];
+      if (t >= *T.n_seeds) return;
+      const int64_t id = T.seeds[t];
+      T.nodes[t] = id;
+      __hip_atomic_store(T.pos + id, pack_pos(A.stamp + 1u, t), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    case kSecExclClear: {
+      const RelArgs& R = A.rel[x];
+      if (t < R.n_excl) {
+        const int64_t e = R.excl_eids[t];
+        R.mask_w[e] = 0;
+        R.rows_w[R.coo_dst[e]] = 0;
+      }
+      break;
+    }
+    default: break;
+  }
+}
+
+inline int64_t words_of(int64_t n) { return (n + 63) / 64; }
+inline int64_t up256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+inline int nblocks(int64_t threads) { return (int)((threads + kSbBlock - 1) / kSbBlock); }
+
+struct Caps {
+  int64_t seed[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
+  int64_t edge[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int64_t node[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
+  int64_t ws_bytes;
+};
+
+int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
+  GNNREC_REQUIRE(P, "gnnrec_sample_blocks: null plan");
+  GNNREC_REQUIRE(P->n_rels >= 0 && P->n_rels <= GNNREC_SB_MAX_RELS && P->n_types >= 1 &&
+                     P->n_types <= GNNREC_SB_MAX_TYPES && P->n_steps >= 1 &&
+                     P->n_steps <= GNNREC_SB_MAX_STEPS,
+                 "gnnrec_sample_blocks: %d relations (<= %d), %d types (1..%d), %d steps (1..%d)",
+                 P->n_rels, GNNREC_SB_MAX_RELS, P->n_types, GNNREC_SB_MAX_TYPES, P->n_steps,
+                 GNNREC_SB_MAX_STEPS);
+  for (int r = 0; r < P->n_rels; ++r) {
+    const gnnrec_sample_rel& R = P->rel[r];
+    GNNREC_REQUIRE(R.src_type >= 0 && R.src_type < P->n_types && R.dst_type >= 0 &&
+                       R.dst_type < P->n_types,
+                   "gnnrec_sample_blocks: relation %d: node-type index out of range", r);
+    for (int s = 0; s < P->n_steps; ++s)
+      GNNREC_REQUIRE(P->fanout[s][r] >= 0 && P->fanout[s][r] <= kMaxFanout,
+                     "gnnrec_sample_blocks: fanout %lld at step %d (bounded: 0..%d)",
+                     (long long)P->fanout[s][r], s, kMaxFanout);
+    GNNREC_REQUIRE(R.n_excl >= 0, "gnnrec_sample_blocks: negative exclusion count");
+  }
+  for (int t = 0; t < P->n_types; ++t) {
+    GNNREC_REQUIRE(P->type[t].n_seeds >= 0 && P->type[t].n_nodes >= 0 &&
+                       P->type[t].n_nodes < (int64_t(1) << 31),
+                   "gnnrec_sample_blocks: type %d: sizes", t);
+    C->seed[0][t] = P->type[t].n_seeds;
+  }
+  int64_t ws = 0;
+  for (int s = 0; s < P->n_steps; ++s) {
+    for (int r = 0; r < P->n_rels; ++r) {
+      C->edge[s][r] = C->seed[s][P->rel[r].dst_type] * P->fanout[s][r];
+      ws += up256(8 * C->seed[s][P->rel[r].dst_type]) + up256(4 * C->edge[s][r]) +
+            up256(8 * C->edge[s][r]);
+    }
+    for (int t = 0; t < P->n_types; ++t) {
+      int64_t e = 0;
+      for (int r = 0; r < P->n_rels; ++r)
+        if (P->rel[r].src_type == t) e += C->edge[s][r];
+      C->node[s][t] = C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
+      if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
+    }
+  }
+  C->ws_bytes = ws;
+  return GNNREC_OK;
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+extern "C" int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
+                                         int64_t* edge_cap, int64_t* node_cap,
+                                         int64_t* workspace_bytes) {
+  Caps C{};
+  if (int st = plan_caps(plan, &C)) return st;
+  for (int s = 0; s < GNNREC_SB_MAX_STEPS; ++s) {
+    for (int t = 0; t < GNNREC_SB_MAX_TYPES; ++t) {
+      if (seed_cap) seed_cap[s * GNNREC_SB_MAX_TYPES + t] = C.seed[s][t];
+      if (node_cap) node_cap[s * GNNREC_SB_MAX_TYPES + t] = C.node[s][t];
+    }
+    for (int r = 0; r < GNNREC_SB_MAX_RELS; ++r)
+      if (edge_cap) edge_cap[s * GNNREC_SB_MAX_RELS + r] = C.edge[s][r];
+  }
+  if (workspace_bytes) *workspace_bytes = C.ws_bytes;
+  return GNNREC_OK;
+}
+
+extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
+  Caps C{};
+  if (int st = plan_caps(P, &C)) return st;
+  GNNREC_REQUIRE(P->stamp >= 1u && P->stamp <= 0xFFFFFFFFu - (uint32_t)P->n_steps - 2u,
+                 "gnnrec_sample_blocks: stamp %u out of range (restart at 1 with zeroed pos)",
+                 P->stamp);
+  GNNREC_REQUIRE(P->sizes && (C.ws_bytes == 0 || P->workspace),
+                 "gnnrec_sample_blocks: null sizes / workspace");
+  const int R = P->n_rels, T = P->n_types, L = P->n_steps;
+  for (int t = 0; t < T; ++t) {
+    const gnnrec_sample_type& ty = P->type[t];
+    GNNREC_REQUIRE(ty.pos && ty.bits && ty.word_rank && (ty.n_seeds == 0 || ty.seeds),
+                   "gnnrec_sample_blocks: type %d: null scratch or seeds", t);
+    for (int s = 0; s < L; ++s)
+      GNNREC_REQUIRE(P->nodes[s][t] || C.node[s][t] == 0,
+                     "gnnrec_sample_blocks: null nodes output (step %d, type %d)", s, t);
+  }
+  for (int r = 0; r < R; ++r) {
+    const gnnrec_sample_rel& re = P->rel[r];
+    GNNREC_REQUIRE(re.indptr && re.indices && re.eids, "gnnrec_sample_blocks: relation %d: null CSR", r);
+    GNNREC_REQUIRE(re.n_excl == 0 || (re.excl_eids && re.coo_dst && re.excl_mask && re.excl_rows),
+                   "gnnrec_sample_blocks: relation %d: exclusion needs eids, coo_dst and flags", r);
+    for (int s = 0; s < L; ++s)
+      GNNREC_REQUIRE(P->out_indptr[s][r] && (C.edge[s][r] == 0 ||
+                                             (P->out_src[s][r] && P->out_eid[s][r])),
+                     "gnnrec_sample_blocks: null output (step %d, relation %d)", s, r);
+  }
+  hipStream_t hs = as_stream(stream);
+  // workspace: per (step, relation) counts, pick sources, pick eids
+  char* ws = static_cast<char*>(P->workspace);
+  int64_t* cnt[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int32_t* psrc[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int64_t* peid[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  for (int s = 0; s < L; ++s)
+    for (int r = 0; r < R; ++r) {
+      cnt[s][r] = reinterpret_cast<int64_t*>(ws);
+      ws += up256(8 * C.seed[s][P->rel[r].dst_type]);
+      psrc[s][r] = reinterpret_cast<int32_t*>(ws);
+      ws += up256(4 * C.edge[s][r]);
+      peid[s][r] = reinterpret_cast<int64_t*>(ws);
+      ws += up256(8 * C.edge[s][r]);
+    }
+  int64_t* node_count = P->sizes;                   // [(L + 1) x T], row -1 first
+  int64_t* edge_count = P->sizes + (int64_t)(L + 1) * T;  // [L x R]
+
+  auto step_args = [&](int s, StepArgs& A) {
+    A = StepArgs{};
+    A.n_rels = R;
+    A.n_types = T;
+    A.last = s == L - 1;
+    A.stamp = P->stamp + (uint32_t)s;
+    A.sizes_seed_row = node_count;
+    for (int t = 0; t < T; ++t) {
+      const gnnrec_sample_type& ty = P->type[t];
+      TypeArgs& a = A.type[t];
+      const int64_t W = words_of(ty.n_nodes);
+      a.seeds = s == 0 ? ty.seeds : P->nodes[s - 1][t];
+      a.n_seeds = node_count + (int64_t)s * T + t;
+      a.seed_cap = C.seed[s][t];
+      a.n_seeds_host = ty.n_seeds;
+      a.pos = reinterpret_cast<unsigned long long*>(ty.pos);
+      a.bits_cur = reinterpret_cast<unsigned long long*>(ty.bits) + (A.stamp & 1u) * W;
+      a.bits_next = reinterpret_cast<unsigned long long*>(ty.bits) + ((A.stamp + 1u) & 1u) * W;
+      a.word_rank = ty.word_rank;
+      a.words = W;
+      a.nodes = P->nodes[s][t];
+      a.n_nodes_out = node_count + (int64_t)(s + 1) * T + t;
+    }
+    for (int r = 0; r < R; ++r) {
+      const gnnrec_sample_rel& re = P->rel[r];
+      RelArgs& a = A.rel[r];
+      a.indptr = re.indptr;
+      a.indices = re.indices;
+      a.eids = re.eids;
+      a.excl_mask = re.n_excl ? re.excl_mask : nullptr;
+      a.excl_rows = re.n_excl ? re.excl_rows : nullptr;
+      a.src_t = re.src_type;
+      a.dst_t = re.dst_type;
+      a.fanout = P->fanout[s][r];
+      a.key = P->key[s][r];
+      a.counts = cnt[s][r];
+      a.pick_src = psrc[s][r];
+      a.pick_eid = peid[s][r];
+      a.out_indptr = P->out_indptr[s][r];
+      a.out_src = P->out_src[s][r];
+      a.out_eid = P->out_eid[s][r];
+      a.edge_total = edge_count + (int64_t)s * R + r;
+      a.excl_eids = re.excl_eids;
+      a.n_excl = re.n_excl;
+      a.coo_dst = re.coo_dst;
+      a.mask_w = re.excl_mask;
+      a.rows_w = re.excl_rows;
+    }
+  };
+  auto add_sec = [](Sections& S, int kind, int idx, int blocks) {
+    if (blocks <= 0) return;
+    S.kind[S.n] = kind;
+    S.idx[S.n] = idx;
+    S.begin[S.n + 1] = S.begin[S.n] + blocks;
+    ++S.n;
+  };
+
+  StepArgs A;
+  // begin: seed positions, the first step's bitmaps, the exclusion flags
+  step_args(0, A);
+  A.sec.n = 0;
+  A.sec.begin[0] = 0;
+  for (int t = 0; t < T; ++t) add_sec(A.sec, kSecSeedPos, t, nblocks(P->type[t].n_seeds));
+  for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroBits, t, nblocks(A.type[t].words));
+  for (int r = 0; r < R; ++r) add_sec(A.sec, kSecExclSet, r, nblocks(P->rel[r].n_excl));
+  if (A.sec.n == 0) add_sec(A.sec, kSecSeedPos, 0, 1);  // the seed-count row still lands
+  hipLaunchKernelGGL(sb_begin_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0, hs,
+                     A);
+  if (int st = check_launch("gnnrec_sample_blocks(begin)")) return st;
+
+  for (int s = 0; s < L; ++s) {
+    step_args(s, A);
+    int64_t fmax = 1;
+    for (int r = 0; r < R; ++r) fmax = std::max<int64_t>(fmax, P->fanout[s][r]);
+    const int G = group_size(fmax);
+    // pick
+    A.sec.n = 0;
+    A.sec.begin[0] = 0;
+    for (int r = 0; r < R; ++r)
+      add_sec(A.sec, kSecPick, r,
+              (int)((C.seed[s][P->rel[r].dst_type] + kSbBlock / G - 1) / (kSbBlock / G)));
+    for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroNext, t, nblocks(A.type[t].words));
+    if (A.sec.n) {
+      const dim3 grid((unsigned)A.sec.begin[A.sec.n]);
+      switch (G) {
+        case 8: hipLaunchKernelGGL(sb_pick_kernel<8>, grid, dim3(kSbBlock), 0, hs, A); break;
+        case 16: hipLaunchKernelGGL(sb_pick_kernel<16>, grid, dim3(kSbBlock), 0, hs, A); break;
+        case 32: hipLaunchKernelGGL(sb_pick_kernel<32>, grid, dim3(kSbBlock), 0, hs, A); break;
+        default: hipLaunchKernelGGL(sb_pick_kernel<64>, grid, dim3(kSbBlock), 0, hs, A); break;
+      }
+      if (int st = check_launch("gnnrec_sample_blocks(pick)")) return st;
+    }
+    // scan: one block per relation and per type
+    hipLaunchKernelGGL(sb_scan_kernel, dim3((unsigned)(R + T)), dim3(kScanThreads), 0, hs, A);
+    if (int st = check_launch("gnnrec_sample_blocks(scan)")) return st;
+    // finalize
+    A.sec.n = 0;
+    A.sec.begin[0] = 0;
+    for (int r = 0; r < R; ++r) add_sec(A.sec, kSecCompact, r, nblocks(C.edge[s][r]));
+    for (int t = 0; t < T; ++t) add_sec(A.sec, kSecNewNodes, t, nblocks(A.type[t].words));
+    for (int t = 0; t < T; ++t) add_sec(A.sec, kSecPrefix, t, nblocks(C.seed[s][t]));
+    if (s == L - 1)
+      for (int r = 0; r < R; ++r) add_sec(A.sec, kSecExclClear, r, nblocks(P->rel[r].n_excl));
+    if (A.sec.n) {
+      hipLaunchKernelGGL(sb_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock),
+                         0, hs, A);
+      if (int st = check_launch("gnnrec_sample_blocks(finalize)")) return st;
+    }
+  }
+  return GNNREC_OK;
+}

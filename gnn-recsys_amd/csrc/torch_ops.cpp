@@ -1453,6 +1453,190 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
   return {o_ip, src_loc, o_eid, src_nid, totals};
 }
 
+// ---------------------------------------------------------------- a9 fused sample_blocks
+// Every block of one bounded-fanout BlockSampler.sample_blocks call (gnnrec_sample_blocks:
+// 1 + 3L launches, include/gnnrec.h) with ONE host read of the sizes at the end: outputs are
+// allocated at their capacities and returned narrowed to the actual sizes.
+//   relations r: global in-CSR, src / dst type index, exclusion (eids, COO dst, flag arrays:
+//   all four or none); types t: node count, step-0 seeds, scratch (pos int64 [n], bits int64
+//   [2 ceil(n/64)], word_rank int64 [ceil(n/64) + 1]); fanouts / keys flattened [step][r].
+//   -> per step s and relation r (flattened [s][r]): out_indptr [n_dst + 1], local src int32,
+//   eids; per step and type ([s][t]): the source node ids (seeds first); the sizes (node
+//   counts rows -1..L-1 x T, then edge counts L x R).
+std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>,
+           std::vector<int64_t>>
+sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eids,
+              at::IntArrayRef src_type, at::IntArrayRef dst_type,
+              const c10::List<optional<Tensor>>& excl_eids,
+              const c10::List<optional<Tensor>>& coo_dst,
+              const c10::List<optional<Tensor>>& excl_masks,
+              const c10::List<optional<Tensor>>& excl_rows, at::IntArrayRef n_nodes,
+              at::TensorList seeds, at::TensorList pos, at::TensorList bits,
+              at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
+              int64_t steps, int64_t stamp) {
+  const OneDevice one_device_;
+  const size_t R = indptrs.size(), NT = n_nodes.size();
+  TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
+                        dst_type.size() == R && excl_eids.size() == R && coo_dst.size() == R &&
+                        excl_masks.size() == R && excl_rows.size() == R,
+                    "sample_blocks: one entry per relation in every relation list");
+  TORCH_CHECK_VALUE(seeds.size() == NT && pos.size() == NT && bits.size() == NT &&
+                        word_rank.size() == NT,
+                    "sample_blocks: one seed list and one scratch triple per node type");
+  TORCH_CHECK_VALUE(steps >= 1 && steps <= GNNREC_SB_MAX_STEPS && R <= GNNREC_SB_MAX_RELS &&
+                        NT >= 1 && NT <= GNNREC_SB_MAX_TYPES,
+                    "sample_blocks: ", steps, " steps, ", R, " relations, ", NT,
+                    " types exceed the fused sampler's limits");
+  TORCH_CHECK_VALUE((int64_t)fanouts.size() == steps * (int64_t)R &&
+                        (int64_t)keys.size() == steps * (int64_t)R,
+                    "sample_blocks: fanouts / keys must hold steps x relations entries");
+  gnnrec_sample_plan P{};
+  P.n_rels = (int)R;
+  P.n_types = (int)NT;
+  P.n_steps = (int)steps;
+  P.stamp = (uint32_t)stamp;
+  for (size_t r = 0; r < R; ++r) {
+    dev(indptrs[r], "indptr", at::kLong);
+    dev(indices[r], "indices", at::kInt);
+    dev(eids[r], "eids", at::kLong);
+    TORCH_CHECK_VALUE(src_type[r] >= 0 && (size_t)src_type[r] < NT && dst_type[r] >= 0 &&
+                          (size_t)dst_type[r] < NT,
+                      "sample_blocks: node-type index out of range");
+    TORCH_CHECK_VALUE(indptrs[r].numel() == n_nodes[dst_type[r]] + 1 &&
+                          eids[r].numel() == indices[r].numel(),
+                      "sample_blocks: relation ", r, ": indptr must hold n_dst + 1 entries and "
+                      "eids one per index");
+    gnnrec_sample_rel& re = P.rel[r];
+    re.indptr = p<int64_t>(indptrs[r]);
+    re.indices = p<int32_t>(indices[r]);
+    re.eids = p<int64_t>(eids[r]);
+    re.src_type = (int32_t)src_type[r];
+    re.dst_type = (int32_t)dst_type[r];
+    const optional<Tensor> xe = excl_eids.get(r), cd = coo_dst.get(r), xm = excl_masks.get(r),
+                           xr = excl_rows.get(r);
+    TORCH_CHECK_VALUE(has(xe) == has(cd) && has(xe) == has(xm) && has(xe) == has(xr),
+                      "sample_blocks: relation ", r,
+                      ": exclusion needs the eids, the COO dst and both flag arrays");
+    if (has(xe)) {
+      dev(xe, "excl_eids", at::kLong);
+      dev(cd, "coo_dst", at::kLong);
+      dev(xm, "excl_mask", at::kByte);
+      dev(xr, "excl_rows", at::kByte);
+      TORCH_CHECK_VALUE(xe->is_contiguous() && cd->numel() == eids[r].numel() &&
+                            xm->numel() == eids[r].numel() &&
+                            xr->numel() == n_nodes[dst_type[r]],
+                        "sample_blocks: relation ", r, ": exclusion arrays sized E, E, n_dst");
+      re.excl_eids = p<int64_t>(xe);
+      re.n_excl = xe->numel();
+      re.coo_dst = p<int64_t>(cd);
+      re.excl_mask = p<uint8_t>(xm);
+      re.excl_rows = p<uint8_t>(xr);
+    }
+    for (int64_t s = 0; s < steps; ++s) {
+      P.fanout[s][r] = fanouts[s * R + r];
+      P.key[s][r] = (uint64_t)keys[s * R + r];
+    }
+  }
+  for (size_t t = 0; t < NT; ++t) {
+    dev(seeds[t], "seeds", at::kLong);
+    dev(pos[t], "pos", at::kLong);
+    dev(bits[t], "bits", at::kLong);
+    dev(word_rank[t], "word_rank", at::kLong);
+    const int64_t W = (n_nodes[t] + 63) / 64;
+    TORCH_CHECK_VALUE(seeds[t].is_contiguous() && pos[t].numel() == n_nodes[t] &&
+                          bits[t].numel() == 2 * W && word_rank[t].numel() == W + 1,
+                      "sample_blocks: type ", t, ": scratch sized n, 2 ceil(n/64), ceil(n/64)+1");
+    gnnrec_sample_type& ty = P.type[t];
+    ty.n_nodes = n_nodes[t];
+    ty.seeds = p<int64_t>(seeds[t]);
+    ty.n_seeds = seeds[t].numel();
+    ty.pos = p<int64_t>(pos[t]);
+    ty.bits = p<uint64_t>(bits[t]);
+    ty.word_rank = p<int64_t>(word_rank[t]);
+  }
+  int64_t seed_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
+  int64_t edge_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_RELS];
+  int64_t node_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
+  int64_t ws_bytes = 0;
+  ck(gnnrec_sample_blocks_caps(&P, seed_cap, edge_cap, node_cap, &ws_bytes),
+     "gnnrec_sample_blocks_caps");
+  const c10::DeviceGuard g(pos[0].device());
+  const auto i64 = pos[0].options();
+  std::vector<Tensor> o_ip(steps * R), o_src(steps * R), o_eid(steps * R), nodes(steps * NT);
+  for (int64_t s = 0; s < steps; ++s) {
+    for (size_t r = 0; r < R; ++r) {
+      const int64_t sc = seed_cap[s * GNNREC_SB_MAX_TYPES + dst_type[r]];
+      const int64_t ec = edge_cap[s * GNNREC_SB_MAX_RELS + r];
+      o_ip[s * R + r] = at::empty({sc + 1}, i64);
+      o_src[s * R + r] = at::empty({ec}, i64.dtype(at::kInt));
+      o_eid[s * R + r] = at::empty({ec}, i64);
+      P.out_indptr[s][r] = p<int64_t>(o_ip[s * R + r]);
+      P.out_src[s][r] = p<int32_t>(o_src[s * R + r]);
+      P.out_eid[s][r] = p<int64_t>(o_eid[s * R + r]);
+    }
+    for (size_t t = 0; t < NT; ++t) {
+      nodes[s * NT + t] = at::empty({node_cap[s * GNNREC_SB_MAX_TYPES + t]}, i64);
+      P.nodes[s][t] = p<int64_t>(nodes[s * NT + t]);
+    }
+  }
+  const int64_t n_sizes = (steps + 1) * (int64_t)NT + steps * (int64_t)R;
+  Tensor sizes = at::empty({n_sizes}, i64);
+  Tensor ws = at::empty({std::max<int64_t>(ws_bytes, 1)}, i64.dtype(at::kByte));
+  P.sizes = p<int64_t>(sizes);
+  P.workspace = ws.data_ptr();
+  ck(gnnrec_sample_blocks(&P, stream_of(pos[0])), "gnnrec_sample_blocks");
+  const Tensor hs = sizes.to(at::kCPU);  // the call's one size readback
+  const int64_t* h = hs.data_ptr<int64_t>();
+  std::vector<int64_t> out_sizes(h, h + n_sizes);
+  for (int64_t s = 0; s < steps; ++s) {
+    for (size_t r = 0; r < R; ++r) {
+      const int64_t n_dst = h[s * NT + dst_type[r]];
+      const int64_t ne = h[(steps + 1) * NT + s * R + r];
+      o_ip[s * R + r] = o_ip[s * R + r].narrow(0, 0, n_dst + 1);
+      o_src[s * R + r] = o_src[s * R + r].narrow(0, 0, ne);
+      o_eid[s * R + r] = o_eid[s * R + r].narrow(0, 0, ne);
+    }
+    for (size_t t = 0; t < NT; ++t)
+      nodes[s * NT + t] = nodes[s * NT + t].narrow(0, 0, h[(s + 1) * NT + t]);
+  }
+  return {o_ip, o_src, o_eid, nodes, out_sizes};
+}
+
+// a10: several row gathers in one launch (gnnrec_gather_rows_batch): out[j] = src[j][idx[j]]
+void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList out) {
+  const OneDevice one_device_;
+  const size_t n = src.size();
+  TORCH_CHECK_VALUE(idx.size() == n && out.size() == n && n <= GNNREC_GATHER_MAX_JOBS,
+                    "gather_rows_batch: one idx and out per src, at most ",
+                    GNNREC_GATHER_MAX_JOBS, " jobs");
+  std::vector<gnnrec_gather_job> jobs(n);
+  for (size_t j = 0; j < n; ++j) {
+    dev(idx[j], "idx", at::kLong);
+    TORCH_CHECK_VALUE(src[j].is_cuda() || src[j].is_meta(),
+                      "src: expected a device tensor (there is no CPU path)");
+    same_dev(src[j], "src");
+    same_dev(out[j], "out");
+    TORCH_CHECK_VALUE(src[j].dim() >= 1 && out[j].dim() == src[j].dim() &&
+                          out[j].scalar_type() == src[j].scalar_type() && idx[j].is_contiguous() &&
+                          out[j].size(0) == idx[j].numel() && out[j].is_contiguous(),
+                      "gather_rows_batch: job ", j, ": out [n, ...] of src's dtype and rank, "
+                      "contiguous idx [n]");
+    int64_t inner = 1;
+    for (int64_t k = src[j].dim() - 1; k >= 1; --k) {
+      TORCH_CHECK_VALUE(out[j].size(k) == src[j].size(k), "gather_rows_batch: row shapes differ");
+      TORCH_CHECK_VALUE(src[j].size(k) <= 1 || src[j].stride(k) == inner,
+                        "gather_rows_batch: src rows must be contiguous");
+      inner *= src[j].size(k);
+    }
+    const int64_t es = src[j].element_size();
+    jobs[j] = gnnrec_gather_job{src[j].data_ptr(), src[j].stride(0) * es, p<int64_t>(idx[j]),
+                                idx[j].numel(), inner * es, out[j].data_ptr(), inner * es};
+  }
+  if (n == 0 || meta(src[0])) return;
+  const c10::DeviceGuard g(src[0].device());
+  ck(gnnrec_gather_rows_batch(jobs.data(), (int)n, stream_of(src[0])), "gnnrec_gather_rows_batch");
+}
+
 // EdgeDataLoader's batch head in one call (gnnrec/sampling.py _iter_batches): the batch's
 // positive pairs (find_edges), the uniform negatives (src repeated K times, dst =
 // randint(N_dst) from the default generator — the same draws as negative_sampler.Uniform),
@@ -1680,6 +1864,13 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor?[] mask_rows, int[] src_type, int[] dst_type, int[] fanouts, int[] keys, Tensor[] seeds, "
         "Tensor(a!)[] prefix_pos, Tensor(b!)[] marks) -> "
         "(Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, Tensor[] src_nid, int[] n_edges)");
+  m.def("sample_blocks(Tensor[] indptrs, Tensor[] indices, Tensor[] eids, int[] src_type, "
+        "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
+        "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
+        "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
+        "int stamp) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
+        "Tensor[] src_nid, int[] sizes)");
+  m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out) -> ()");
   // host-only entry points (no tensors: one catch-all kernel each)
   m.def("version() -> int", &version);
   m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);
@@ -1734,6 +1925,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("lstm_backward_step", &lstm_backward_step);     \
   m.impl("lstm_slots", &lstm_slots);                     \
   m.impl("gather_rows", &gather_rows);                   \
+  m.impl("gather_rows_batch", &gather_rows_batch);       \
   m.impl("csr_has_edges", &csr_has_edges);               \
   m.impl("sage_rel_forward", &sage_rel_forward);         \
   m.impl("sage_rel_backward", &sage_rel_backward);       \
@@ -1748,6 +1940,7 @@ TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) {
   GNNREC_IMPLS(m);
   m.impl("sample_layer", &sample_layer);  // data-dependent sizes: device only, no meta form
   m.impl("edge_batch_pairs", &edge_batch_pairs);
+  m.impl("sample_blocks", &sample_blocks);
 }
 // Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
 TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }

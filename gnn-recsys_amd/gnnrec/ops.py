@@ -1251,6 +1251,70 @@ def sample_layer(indptrs, indices, eids, masks, src_type, dst_type, fanouts, key
                              list(seeds), list(prefix_pos), list(marks))
 
 
+SB_MAX_RELS, SB_MAX_TYPES, SB_MAX_STEPS, SB_MAX_FANOUT = 8, 4, 4, 64
+GATHER_MAX_JOBS = 16
+
+
+class SampleScratch:
+    """Per-node-type state of the fused sampler (gnnrec_sample_blocks, include/gnnrec.h):
+    `pos` (stamped seed positions, never cleared), two new-source bitmaps and their word
+    ranks.  `stamp` advances by steps + 1 per call; before it would wrap, `pos` is zeroed
+    and the count restarts (one memset per ~4e9 sampled layers)."""
+
+    def __init__(self, n_nodes: int, device):
+        w = (n_nodes + 63) // 64
+        self.n_nodes = n_nodes
+        self.pos = torch.zeros(n_nodes, dtype=torch.int64, device=device)
+        self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
+        self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
+
+
+def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
+                  fanouts, keys, stamp):
+    """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
+    1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
+    output block); excl: per relation None or (eids, coo_dst, mask, rows).
+    -> per step: ([out_indptr], [local src int32], [eids]) per relation, [src node ids] per
+    type, and the sizes (node counts rows -1..L-1 x types, then edge counts)."""
+    steps, R = len(fanouts), len(indptrs)
+    ex = [e if e is not None else (None,) * 4 for e in excl]
+    o_ip, o_src, o_eid, nodes, sizes = _T().sample_blocks(
+        list(indptrs), list(indices), list(eids), list(src_type), list(dst_type),
+        [e[0] for e in ex], [e[1] for e in ex], [e[2] for e in ex], [e[3] for e in ex],
+        list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
+        [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
+        [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp))
+    NT = len(n_nodes)
+    out = []
+    for s in range(steps):
+        out.append(([o_ip[s * R + r] for r in range(R)], [o_src[s * R + r] for r in range(R)],
+                    [o_eid[s * R + r] for r in range(R)], [nodes[s * NT + t] for t in range(NT)]))
+    return out, sizes
+
+
+def gather_rows_batch(jobs):
+    """a10, several gathers in one launch: jobs = [(src, idx)] -> [src[idx]] (any dtype,
+    contiguous rows; at most GATHER_MAX_JOBS per launch)."""
+    outs = []
+    for i in range(0, len(jobs), GATHER_MAX_JOBS):
+        part = jobs[i:i + GATHER_MAX_JOBS]
+        srcs, idxs, res = [], [], []
+        for src, idx in part:
+            _dev(idx, "idx", torch.int64)
+            if src.dim() == 0:
+                raise ValueError("src: expected at least one dimension")
+            row = src[0] if src.shape[0] else src.new_empty(src.shape[1:])
+            if not (row.is_contiguous() and (src.dim() == 1 or src.stride(0) >= row.numel())):
+                src = src.contiguous()
+            srcs.append(src)
+            idxs.append(idx.contiguous())
+            res.append(torch.empty((idx.numel(),) + tuple(src.shape[1:]), dtype=src.dtype,
+                                   device=src.device))
+        _T().gather_rows_batch(srcs, idxs, res)
+        outs.extend(res)
+    return outs
+
+
 def edge_batch_pairs(rel_src, rel_dst, src_type, dst_type, batch, neg_order, k, n_nodes,
                      prefix_pos, marks):
     """EdgeDataLoader's batch head in one call (gnnrec::edge_batch_pairs): positive pairs of

@@ -55,6 +55,11 @@ class BlockSampler:
         self._calls = 0
         self._relabelers = {}
         self._exclude_masks = {}
+        # bounded fanouts: every block of a call in one fused op (ops.sample_blocks); False
+        # keeps the per-layer ops (the blocks are bitwise the same; tests compare the two)
+        self.fused = True
+        self._sb_scratch = {}
+        self._stamp = 1
 
     def _fanout(self, block_id: int, ce) -> int:
         if self.fanouts is None:
@@ -90,6 +95,73 @@ class BlockSampler:
             self._exclude_masks[key] = m
         return m
 
+    def _fused_ok(self, g) -> bool:
+        """Every block of a call in one ops.sample_blocks: bounded fanouts (0..64) for every
+        block and relation, on a HIP device, within the fused op's limits."""
+        if not self.fused or g.device.type != "cuda" or self.fanouts is None:
+            return False
+        ces = g.canonical_etypes
+        if not (1 <= self.num_layers <= ops.SB_MAX_STEPS and len(ces) <= ops.SB_MAX_RELS
+                and 1 <= len(g.ntypes) <= ops.SB_MAX_TYPES):
+            return False
+        return all(0 <= self._fanout(b, ce) <= ops.SB_MAX_FANOUT
+                   for b in range(self.num_layers) for ce in ces)
+
+    def _sample_fused(self, g, seeds, exclude_eids, transposes):
+        """sample_blocks through gnnrec_sample_blocks: 1 + 3L launches and one host read for
+        all L blocks (bitwise the blocks of the per-layer path, _one_block)."""
+        ces, nts = list(g.canonical_etypes), list(g.ntypes)
+        tix = {nt: i for i, nt in enumerate(nts)}
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        L = self.num_layers
+        scratch = []
+        for nt in nts:
+            key = (id(g), nt)
+            sc = self._sb_scratch.get(key)
+            if sc is None:
+                sc = self._sb_scratch[key] = ops.SampleScratch(g.num_nodes(nt), g.device)
+            scratch.append(sc)
+        if self._stamp + L + 3 >= (1 << 32):  # never in practice: restart the stamps
+            for sc in self._sb_scratch.values():
+                sc.pos.zero_()
+            self._stamp = 1
+        stamp = self._stamp
+        self._stamp += L + 1
+        excl = [None] * len(ces)
+        for ce, e in (exclude_eids or {}).items():
+            ce = g.to_canonical_etype(ce)
+            e = torch.as_tensor(e, dtype=torch.int64, device=g.device).reshape(-1)
+            if e.numel():
+                excl[ces.index(ce)] = (e, g._coo[ce][1], self._mask(g, ce),
+                                       self._mask_rows(g, ce))
+        csrs = [g.in_csr_global(ce) for ce in ces]
+        # step s samples block L-1-s (the output block first), with that block's keys
+        fans = [[self._fanout(L - 1 - s, ce) for ce in ces] for s in range(L)]
+        keys = [[_mix(self.seed, self._calls, L - 1 - s, r) for r in range(len(ces))]
+                for s in range(L)]
+        steps, sizes = ops.sample_blocks(
+            [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
+            [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
+            [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
+            fans, keys, stamp)
+        NT, R = len(nts), len(ces)
+        blocks = []
+        for s, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
+            rels = {}
+            for r, ce in enumerate(ces):
+                ip = o_ip[r]
+                ip._gnnrec_nnz = int(sizes[(L + 1) * NT + s * R + r])
+                if 0 <= fans[s][r] <= ops.DEFAULT_SPLIT:
+                    ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
+                rels[ce] = (ip, src_loc[r], o_eid[r])
+            num_dst = {nt: int(sizes[s * NT + t]) for t, nt in enumerate(nts)}
+            blocks.insert(0, Block(dict(zip(nts, nodes)), num_dst, rels))
+        if transposes:
+            for block_id, b in enumerate(blocks):
+                if block_id > 0 or FIRST_BLOCK_TRANSPOSES[0]:
+                    _add_transposes(b)
+        return blocks
+
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
                       exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
                       transposes: bool = False) -> List[Block]:
@@ -99,6 +171,10 @@ class BlockSampler:
         self._calls += 1
         seeds = {nt: torch.as_tensor(v, dtype=torch.int64, device=g.device)
                  for nt, v in seed_nodes.items()}
+        if self._fused_ok(g):
+            blocks = self._sample_fused(g, seeds, exclude_eids, transposes)
+            _copy_block_data(g, blocks)
+            return blocks
         masks = {}
         if exclude_eids:
             for ce, eids in exclude_eids.items():
@@ -122,18 +198,7 @@ class BlockSampler:
             for ce, (m, eids, rows, dst) in masks.items():
                 m.index_fill_(0, eids, 0)
                 rows.index_fill_(0, dst, 0)
-        # copy edge data into every block and node data into the input block (DGL copies
-        # features at block creation; the reference reads blocks[0].srcdata['features'])
-        for b in blocks:
-            for ce in b.canonical_etypes:
-                eid = b._edata[ce][EID]
-                for k, v in g._edata[ce].items():
-                    b._edata[ce][k] = ops.gather_rows(v, eid)
-        b0 = blocks[0]
-        for nt in b0.ntypes:
-            ids = b0._src[nt][NID]
-            for k, v in g._ndata[nt].items():
-                b0._src[nt][k] = ops.gather_rows(v, ids)
+        _copy_block_data(g, blocks)
         return blocks
 
     def _one_block(self, g, seeds, block_id, masks) -> Block:
@@ -205,6 +270,29 @@ class BlockSampler:
             for ce, loc in zip(ces, locs):
                 rels[ce][1] = loc.to(torch.int32)
         return Block(src_nid, num_dst, {ce: tuple(v) for ce, v in rels.items()})
+
+
+def _copy_block_data(g, blocks) -> None:
+    """Edge data into every block, node data into the input block (DGL copies features at
+    block creation; the reference reads blocks[0].srcdata['features']): every table in ONE
+    launch (ops.gather_rows_batch)."""
+    jobs, dests = [], []
+    for b in blocks:
+        for ce in b.canonical_etypes:
+            eid = b._edata[ce][EID]
+            for k, v in g._edata[ce].items():
+                jobs.append((v, eid))
+                dests.append((b._edata[ce], k))
+    b0 = blocks[0]
+    for nt in b0.ntypes:
+        ids = b0._src[nt][NID]
+        for k, v in g._ndata[nt].items():
+            jobs.append((v, ids))
+            dests.append((b0._src[nt], k))
+    if not jobs:
+        return
+    for (frame, k), t in zip(dests, ops.gather_rows_batch(jobs)):
+        frame[k] = t
 
 
 # The first block's transposes feed only the gradients of its source tables; a ConvModel

@@ -363,6 +363,84 @@ int gnnrec_compact_marked(const int32_t* mark, const int64_t* rank, int64_t n_no
 int gnnrec_set_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
 int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_pos, void* stream);
 
+/* ---- a9: every block of one bounded-fanout sample_blocks call, fused ------
+ * BlockSampler.sample_blocks (src/sampling.py:153-161: MultiLayerNeighborSampler, the
+ * per-layer to_block, exclude_eids) for L steps — step 0 is the OUTPUT block, sampled from
+ * the batch seeds; step s+1 samples from step s's source nodes — in 1 + 3L launches with no
+ * host synchronisation (DGL: _CAPI_DGLSampleNeighbors + _CAPI_DGLToBlock per layer):
+ *   begin       every type's seed positions, the first step's new-source bitmaps zeroed,
+ *               the exclusion flags set (excl_mask[eid], excl_rows[dst(eid)]);
+ *   pick(s)     per (relation, seed) the in-edges (all when deg <= fanout, else `fanout`
+ *               by Floyd's algorithm on the counter hash — the picks of gnnrec_sample_fill),
+ *               excluded eids dropped, written at seed x fanout capacity slots with the
+ *               per-seed count; every picked source that is not a seed of its type sets its
+ *               bit in the type's bitmap; the next step's bitmaps are zeroed;
+ *   scan(s)     per relation the counts -> out_indptr, per type the bitmap popcounts ->
+ *               word ranks (one block per relation / type);
+ *   finalize(s) the picks compacted into the block CSR with LOCAL source ids (a seed keeps
+ *               its position, a new source = n_seeds + its rank among the new ids, i.e.
+ *               ascending global id: the relabel of gnnrec_mark_ids/relabel_ids), the
+ *               source node list (seeds, then new ids ascending) = the next step's seeds,
+ *               and the last step clears the exclusion flags.
+ * The blocks are bitwise those of gnnrec_sample_count/fill + the mark/scan/relabel path
+ * with the same keys.  Capacities bound every output (gnnrec_sample_blocks_caps), and the
+ * actual sizes land in `sizes` on the device: [-1..L-1][types] source node counts
+ * (row -1: the seed counts) at sizes[0 .. (L+1)*T), then [0..L-1][rels] edge counts.
+ * Per type the caller keeps `pos` (int64 [n_nodes], all zero before the first call) and
+ * `bits` (uint64 [2 * ceil(n_nodes/64)]) / `word_rank` (int64 [ceil(n_nodes/64) + 1])
+ * scratch across calls; `stamp` >= 1 grows by L + 1 per call on the same `pos` arrays (the
+ * caller zeroes `pos` and restarts at 1 before it would pass 2^32 - 2). */
+#define GNNREC_SB_MAX_RELS 8
+#define GNNREC_SB_MAX_TYPES 4
+#define GNNREC_SB_MAX_STEPS 4
+
+typedef struct gnnrec_sample_rel {
+  const int64_t* indptr;  /* in-CSR over global ids: [n_dst + 1] */
+  const int32_t* indices; /* global source ids [E] */
+  const int64_t* eids;    /* [E] */
+  int32_t src_type, dst_type;
+  const int64_t* excl_eids; /* excluded eids of this relation (NULL / 0: none) */
+  int64_t n_excl;
+  const int64_t* coo_dst; /* [E] dst of every eid (for the excluded eids' dst rows) */
+  uint8_t* excl_mask;     /* [E] flags, zero between calls */
+  uint8_t* excl_rows;     /* [n_dst] flags, zero between calls */
+} gnnrec_sample_rel;
+
+typedef struct gnnrec_sample_type {
+  int64_t n_nodes;
+  const int64_t* seeds; /* step 0's destination nodes (the batch) */
+  int64_t n_seeds;
+  int64_t* pos;         /* scratch, see above */
+  uint64_t* bits;
+  int64_t* word_rank;
+} gnnrec_sample_type;
+
+typedef struct gnnrec_sample_plan {
+  int n_rels, n_types, n_steps;
+  gnnrec_sample_rel rel[GNNREC_SB_MAX_RELS];
+  gnnrec_sample_type type[GNNREC_SB_MAX_TYPES];
+  int64_t fanout[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS]; /* 0..64 */
+  uint64_t key[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  uint32_t stamp;
+  /* outputs, sized by gnnrec_sample_blocks_caps: per step s and relation r the block CSR
+   * (out_indptr [seed_cap + 1], out_src int32 local ids [edge_cap], out_eid [edge_cap]),
+   * per step and type the source node ids [node_cap] (seeds first) */
+  int64_t* out_indptr[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int32_t* out_src[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int64_t* out_eid[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
+  int64_t* nodes[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
+  int64_t* sizes;       /* device, (L + 1) * T + L * R int64 */
+  void* workspace;      /* device, gnnrec_sample_blocks_caps' workspace_bytes */
+} gnnrec_sample_plan;
+
+/* Host only: per step the capacities of the outputs (seed_cap [s][t]: destination nodes,
+ * edge_cap [s][r] = seed_cap[s][dst] x fanout, node_cap [s][t] = seed_cap[s][t] +
+ * min(n_nodes_t, sum of edge_cap[s][r] over relations sourced from t); seed_cap[s+1] =
+ * node_cap[s]), each flattened [step][GNNREC_SB_MAX_*], and the workspace bytes. */
+int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
+                              int64_t* edge_cap, int64_t* node_cap, int64_t* workspace_bytes);
+int gnnrec_sample_blocks(const gnnrec_sample_plan* plan, void* stream);
+
 /* ---- f1: recommendation top-k --------------------------------------------
  * For each row r of scores[n_rows, n_cols] (leading dimension ld): the k
  * (1..2^20) best columns ordered by (score desc, column asc), skipping the
@@ -515,6 +593,20 @@ int gnnrec_lstm_slots(const int64_t* indptr, const int32_t* indices, const int64
  * dst row i (dst_ld_bytes apart) = src row idx[i] (src_ld_bytes apart), row_bytes each,
  * any dtype.  Replaces DGL's copy of node features into blocks[0].srcdata and of edge
  * data into the blocks (read at src/train/run.py:112,340). */
+/* Up to GNNREC_GATHER_MAX_JOBS independent row gathers of gnnrec_gather_rows in ONE launch
+ * (a sampled batch's edge data for every block and relation plus the input block's node
+ * features: one launch instead of one per table). */
+#define GNNREC_GATHER_MAX_JOBS 16
+typedef struct gnnrec_gather_job {
+  const void* src;
+  int64_t src_ld_bytes;
+  const int64_t* idx;
+  int64_t n;
+  int64_t row_bytes;
+  void* dst;
+  int64_t dst_ld_bytes;
+} gnnrec_gather_job;
+int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_jobs, void* stream);
 int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx, int64_t n,
                        int64_t row_bytes, void* dst, int64_t dst_ld_bytes, void* stream);
 

@@ -627,3 +627,93 @@ def test_first_layer_embedding_fold_matches_embed_then_aggregate(monkeypatch, ag
     torch.testing.assert_close(res["1"][0], res["0"][0], rtol=1e-5, atol=1e-7)
     for n in res["1"][1]:
         torch.testing.assert_close(res["1"][1][n], res["0"][1][n], rtol=1e-4, atol=1e-6, msg=n)
+
+
+def _same_blocks(A, B):
+    assert len(A) == len(B)
+    for a, b in zip(A, B):
+        assert a.canonical_etypes == b.canonical_etypes and a._num_dst == b._num_dst
+        assert a.ntypes == b.ntypes
+        for nt in a.ntypes:
+            assert set(a._src[nt]) == set(b._src[nt])
+            for k in a._src[nt]:
+                assert torch.equal(a._src[nt][k], b._src[nt][k]), (nt, k)
+        for ce in a.canonical_etypes:
+            for x, y in zip(a._rels[ce], b._rels[ce]):
+                assert x.dtype == y.dtype and torch.equal(x, y), ce
+            assert a._rels[ce][0]._gnnrec_nnz == b._rels[ce][0]._gnnrec_nnz
+            assert set(a._edata[ce]) == set(b._edata[ce])
+            for k in a._edata[ce]:
+                assert torch.equal(a._edata[ce][k], b._edata[ce][k]), (ce, k)
+            assert set(a._t) == set(b._t)
+            if ce in a._t:
+                for x, y in zip(a._t[ce], b._t[ce]):
+                    assert torch.equal(x, y), ce
+
+
+@pytest.mark.parametrize("fanouts", [[3, 2], [{"buys": 2, "bought-by": 4, "clicks": 0,
+                                               "clicked-by": 64}, 1], [10, 10, 5], [1]])
+def test_fused_sample_blocks_equal_per_layer_path(fanouts):
+    """gnnrec_sample_blocks (every block of a call: 1 + 3L launches, one host read) builds the
+    blocks of the per-layer path bit for bit — local ids, eids, node lists, edge data, input
+    features and the training transposes — over consecutive calls (the stamped seed positions
+    and the alternating bitmaps carried from call to call), seeds of one or both types,
+    fanouts 0 / above the degree / per relation, and reverse-type exclusion, whose flags are
+    cleared again."""
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    g, edges = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    fused = MultiLayerNeighborSampler(fanouts, seed=9)
+    layer = MultiLayerNeighborSampler(fanouts, seed=9)
+    layer.fused = False
+    assert fused._fused_ok(g) and not layer._fused_ok(g)
+    rng = np.random.default_rng(3)
+    cases = [({"user": torch.arange(0, 300, 5, device=DEV),
+               "item": torch.tensor([3, 1, 77, 5], device=DEV)}, None),
+             ({"item": torch.arange(0, 120, 3, device=DEV)},
+              {BUYS: torch.arange(0, 4000, 3, device=DEV),
+               BOUGHT: torch.arange(0, 4000, 3, device=DEV)}),
+             ({"user": torch.from_numpy(rng.permutation(300)[:50]).to(DEV)},
+              {CLICKS: torch.from_numpy(rng.integers(0, 3000, 700)).to(DEV)}),
+             ({"user": torch.tensor([299], device=DEV), "item": torch.tensor([0], device=DEV)},
+              None)]
+    for rep in range(2):
+        for seeds, excl in cases:
+            a = fused.sample_blocks(g, seeds, excl, transposes=rep == 1)
+            b = layer.sample_blocks(g, seeds, excl, transposes=rep == 1)
+            _same_blocks(a, b)
+    for key, m in fused._exclude_masks.items():
+        assert int(m.sum()) == 0, key  # the last finalize cleared every exclusion flag
+
+
+def test_fused_sampler_stamp_restart():
+    """Near the end of the 32-bit stamp range the positions are zeroed and the stamps restart:
+    the blocks stay those of the per-layer path."""
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    g, _ = _graph(n_u=200, n_i=100, e_b=3000, e_c=2000, min_deg=False)
+    fused = MultiLayerNeighborSampler([4, 3], seed=2)
+    layer = MultiLayerNeighborSampler([4, 3], seed=2)
+    layer.fused = False
+    seeds = {"user": torch.arange(0, 200, 3, device=DEV)}
+    _same_blocks(fused.sample_blocks(g, seeds), layer.sample_blocks(g, seeds))
+    fused._stamp = (1 << 32) - 6
+    for _ in range(3):
+        _same_blocks(fused.sample_blocks(g, seeds), layer.sample_blocks(g, seeds))
+    assert fused._stamp < 100
+
+
+def test_gather_rows_batch_equals_single_gathers():
+    from gnnrec import ops
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(0)
+    srcs = [torch.randint(0, 1 << 40, (1000,), device=DEV, generator=gen),          # 8-B rows
+            torch.randn(500, 64, device=DEV, generator=gen),                         # 256-B rows
+            torch.randint(0, 255, (300, 7), device=DEV, generator=gen).to(torch.uint8),  # 7 B
+            torch.randn(400, 12, device=DEV, generator=gen)[:, :6],                  # strided rows
+            torch.randn(10, 3, device=DEV, generator=gen).to(torch.float64),
+            torch.zeros(0, 4, device=DEV)]
+    idxs = [torch.randint(0, max(s.shape[0], 1), (n,), device=DEV, generator=gen)
+            for s, n in zip(srcs, (777, 4096, 33, 1000, 5, 0))]
+    jobs = list(zip(srcs, idxs)) * 3  # 18 jobs: more than one launch's worth
+    got = ops.gather_rows_batch(jobs)
+    for (s, i), o in zip(jobs, got):
+        assert torch.equal(o, s[i]), (s.shape, s.dtype)
