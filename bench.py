@@ -828,6 +828,10 @@ def minibatch_step(dev, warmup: int = 5):
 
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
+# random-row gathers served by the 256 MB Infinity Cache: 8.6 TB/s chip-wide from a 38 MB table
+# (MI355X_MICROARCH.md §Indexed rows: gather into LDS; register gathers read at the same rate)
+IC_GATHER_GBS = 8600.0
+IC_BYTES = 256 * 2**20
 
 
 def minibatch_rooflines(dev, reps: int = 50, g=None):
@@ -863,14 +867,18 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
     for _ in range(3):
         blocks = sampler.sample_blocks(g, seeds())
     torch.cuda.synchronize()
-    t_tot, e_tot, b_tot = 0.0, 0, 0
+    t_tot, e_tot, b_tot, span = 0.0, 0, 0, 0.0
     for _ in range(reps):
         sd = seeds()
         torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        ev0.record()
         blocks = sampler.sample_blocks(g, sd)
+        ev1.record()
         torch.cuda.synchronize()
         t_tot += time.perf_counter() - t0
+        span += ev0.elapsed_time(ev1)
         for b in blocks:
             for ce in b.canonical_etypes:
                 ne = b.num_edges(ce)
@@ -884,11 +892,18 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
                 if k != "_ID":
                     b_tot += 2 * v.numel() * v.element_size()  # a10 feature gather
     ms = t_tot / reps * 1e3
+    fused = sampler._fused_ok(g)
     out["sampler"] = {"ms_per_call": round(ms, 4), "sampled_edges_per_call": e_tot // reps,
+                      "gpu_span_ms_per_call": round(span / reps, 4),
                       "sampled_edges_per_s": e_tot / t_tot, "bytes_per_call": b_tot // reps,
                       "GBs": b_tot / t_tot / 1e9, "frac": b_tot / t_tot / 1e9 / HBM_PEAK_GBS,
                       "shape": "C2 graph, fanout [10,10], 1024 user + 1024 item seeds, 2 blocks",
-                      "timing": "wall per call incl. one size readback per layer"}
+                      "path": ("fused: gnnrec_sample_blocks (begin + pick/scan/finalize per "
+                               "block) + one gnnrec_gather_rows_batch, one host size read per "
+                               "call") if fused else "per-layer sample_layer",
+                      "launches_per_call": (1 + 3 * 2 + 1) if fused else None,
+                      "timing": "ms_per_call: wall per sample_blocks call, host included; "
+                                "gpu_span: HIP events around the call on its stream"}
 
     # ---- heads on the C3 pair graph: 1024 positive + 1024 x 2500 negative edges ----------
     d, n_u, n_i, K = 128, 1024, 100_000, 2500
@@ -910,17 +925,29 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
         e.synchronize()
         return s.elapsed_time(e) / n
 
-    ms = ev_time(lambda: ops.sddmm_cos(src, dst, Hs, Hd))
-    b_alg = E * (2 * d * 4 + 2 * 8 + 4)
-    b_min = (n_u + n_i) * d * 4 + E * (2 * 8 + 4)  # every table row once + the edge stream
+    # the head as CosinePrediction.pair runs it on the loader's pair graphs: group g = one
+    # positive edge (g, pd[g]) and its K negatives (g, nd[g K + j]) — the grouped launch
+    ps, pd, nd = src[:n_u], dst[:n_u], dst[n_u:]
+    ms = ev_time(lambda: ops.sddmm_cos_grouped(ps, pd, K, nd, Hs, Hd))
+    ms_edge = ev_time(lambda: ops.sddmm_cos(src, dst, Hs, Hd))
+    # bytes the grouped launch must move: per edge one gathered row + its dst id + the score,
+    # per group the source row and its two ids; the gathered table (100k x 128 fp32 = 51 MB)
+    # sits in the 256 MB Infinity Cache, so the roof is the cache's random-row gather rate
+    b_alg = E * (d * 4 + 8 + 4) + n_u * (d * 4 + 8)
+    tbl = n_i * d * 4
+    roof = IC_GATHER_GBS if tbl <= IC_BYTES else HBM_PEAK_GBS
     out["cosine"] = {"ms": round(ms, 4), "edges": E, "bytes_per_launch": b_alg,
-                     "achieved_GBs": b_alg / ms / 1e6, "frac": b_alg / ms / 1e6 / HBM_PEAK_GBS,
-                     "compulsory_bytes": b_min,
-                     "compulsory_frac": b_min / ms / 1e6 / HBM_PEAK_GBS,
-                     "kernel": "sddmm_cos_kernel",
-                     "note": "1036 B/edge algorithmic (SURVEY d4); the 51 MB item table is "
-                             "cache-resident, so frac can exceed 1 — compulsory_frac counts "
-                             "each table row once"}
+                     "achieved_GBs": b_alg / ms / 1e6, "peak_GBs": roof,
+                     "frac": b_alg / ms / 1e6 / roof,
+                     "bound": "infinity-cache gather" if tbl <= IC_BYTES else "hbm",
+                     "table_bytes": tbl, "kernel": "sddmm_cos_grouped_kernel",
+                     "per_edge_kernel_ms": round(ms_edge, 4),
+                     "note": "negatives grouped by their source (negative_sampler.Uniform "
+                             "repeats each positive's source K times): one 512-B row + 12 B "
+                             "per edge; roof = the Infinity Cache's random-row gather rate "
+                             "(MI355X_MICROARCH.md §Indexed rows, 38 MB table) for a "
+                             "cache-resident table, else 8 TB/s; per_edge_kernel_ms = "
+                             "sddmm_cos_kernel on the expanded lists (two rows per edge)"}
 
     torch.manual_seed(0)
     pl = PredictingLayer(d).to(dev).eval()

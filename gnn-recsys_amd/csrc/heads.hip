@@ -24,6 +24,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------- cosine ----
+// one lane's 4-column partial of <a, b>, the fma chain written out: the per-edge and the
+// grouped kernel must round every score the same way (left to the compiler's contraction,
+// the same source expression fused differently in the two kernels: 1-ulp differences)
+__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
+  return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+
 template <int LPR, int VEC>
 __global__ __launch_bounds__(256) void sddmm_cos_kernel(const int64_t* __restrict__ src,
                                                         const int64_t* __restrict__ dst,
@@ -48,9 +55,9 @@ __global__ __launch_bounds__(256) void sddmm_cos_kernel(const int64_t* __restric
         if constexpr (VEC == 4) {
           const float4 a = *reinterpret_cast<const float4*>(pu + c);
           const float4 b = *reinterpret_cast<const float4*>(pv + c);
-          dot += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
-          su += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
-          sv += b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+          dot += dot4(a, b);
+          su += dot4(a, a);
+          sv += dot4(b, b);
         } else {
           const float a = pu[c], b = pv[c];
           dot += a * b;
@@ -83,6 +90,97 @@ int launch_cos(const int64_t* src, const int64_t* dst, int64_t n, const float* H
   hipLaunchKernelGGL((sddmm_cos_kernel<LPR, VEC>), dim3((unsigned)blocks), dim3(256), 0, s, src,
                      dst, n, Hs, lds, Hd, ldd, d, out);
   return check_launch("gnnrec_sddmm_cos_f32");
+}
+
+// ------------------------------------------------------- grouped cosine ----
+// The training pair graphs of EdgeDataLoader + negative_sampler.Uniform(K) (reference
+// src/sampling.py:163-165: neg src = pos src repeated K times, dst uniform): group g is one
+// positive edge (u_g, first[g]) and its K negatives (u_g, dst[g K + j]).  A wave takes a
+// chunk of one group's negatives and keeps h_u — its fragment in registers, its norm
+// reduced once — so every edge reads one gathered row (4d B) and its dst id, not two rows and
+// two ids, and the u norm is not recomputed K times.  Each value is formed exactly as
+// sddmm_cos_kernel forms it (same lane fragments, same xor tree, same final expression):
+// the scores are bitwise those of the per-edge kernel.
+constexpr int kCosU = 8;       // edges in flight per lane group
+constexpr int kCosChunk = 256; // negatives per wave
+
+template <int LPR>
+__global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
+    const int64_t* __restrict__ src_g, int64_t n_groups, const int64_t* __restrict__ first,
+    float* __restrict__ out_first, int64_t K, int64_t chunks, const int64_t* __restrict__ dst,
+    float* __restrict__ out, const float* __restrict__ Hs, int64_t lds,
+    const float* __restrict__ Hd, int64_t ldd, int d) {
+  constexpr int NPW = kWave / LPR;   // edges per wave-instruction
+  constexpr int STEP = NPW * kCosU;  // edges per step (<= 64: one id per lane)
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / LPR;
+  const int gl = lane % LPR;
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= n_groups * chunks) return;  // wave-uniform
+  const int64_t g = task / chunks, c = task - g * chunks;
+  const int col = gl * 4;
+  const bool cok = col < d;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  float su = 0.f;
+  if (cok) {
+    a = *reinterpret_cast<const float4*>(Hs + src_g[g] * lds + col);
+    su += dot4(a, a);
+  }
+#pragma unroll
+  for (int off = 1; off < LPR; off <<= 1) su += __shfl_xor(su, off);
+  const float nu = fmaxf(sqrtf(su), 1e-12f);
+  auto score = [&](const float4& b, bool ok) {  // -> the cosine on lane gl == 0 of the group
+    float dot = 0.f, sv = 0.f;
+    if (ok) {
+      dot += dot4(a, b);
+      sv += dot4(b, b);
+    }
+#pragma unroll
+    for (int off = 1; off < LPR; off <<= 1) {
+      dot += __shfl_xor(dot, off);
+      sv += __shfl_xor(sv, off);
+    }
+    const float nv = fmaxf(sqrtf(sv), 1e-12f);
+    return dot / (nu * nv);
+  };
+  if (c == 0 && first != nullptr) {  // the group's positive edge
+    const int64_t v = first[g];
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cok) b = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
+    const float r = score(b, cok);
+    if (lane == 0) out_first[g] = r;
+  }
+  const int64_t e_beg = g * K + c * kCosChunk;
+  const int64_t e_end = g * K + min<int64_t>(K, (c + 1) * kCosChunk);
+  for (int64_t e0 = e_beg; e0 < e_end; e0 += STEP) {
+    const int64_t my = e0 + lane;  // lane l fetches the id of the step's l-th edge
+    const int64_t id = (lane < STEP && my < e_end) ? dst[my] : 0;
+    float4 b[kCosU];
+#pragma unroll
+    for (int k = 0; k < kCosU; ++k) {
+      const int slot = k * NPW + grp;
+      const int64_t v = __shfl(id, slot);
+      b[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (cok && e0 + slot < e_end) b[k] = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
+    }
+#pragma unroll
+    for (int k = 0; k < kCosU; ++k) {
+      const int64_t e = e0 + k * NPW + grp;
+      const float r = score(b[k], cok && e < e_end);
+      if (gl == 0 && e < e_end) out[e] = r;
+    }
+  }
+}
+
+template <int LPR>
+int launch_cos_grouped(const int64_t* src_g, int64_t G, const int64_t* first, float* out_first,
+                       int64_t K, const int64_t* dst, float* out, const float* Hs, int64_t lds,
+                       const float* Hd, int64_t ldd, int d, hipStream_t s) {
+  const int64_t chunks = K > 0 ? (K + kCosChunk - 1) / kCosChunk : 1;
+  const int64_t waves = G * chunks;
+  hipLaunchKernelGGL(sddmm_cos_grouped_kernel<LPR>, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                     0, s, src_g, G, first, out_first, K, chunks, dst, out, Hs, lds, Hd, ldd, d);
+  return check_launch("gnnrec_sddmm_cos_grouped_f32");
 }
 
 // ------------------------------------------------------------- edge MLP ----
@@ -158,6 +256,34 @@ extern "C" int gnnrec_sddmm_cos_f32(const int64_t* src, const int64_t* dst, int6
   if (d <= 64) return launch_cos<16, 4>(src, dst, n_edges, Hs, lds, Hd, ldd, (int)d, out, s);
   if (d <= 128) return launch_cos<32, 4>(src, dst, n_edges, Hs, lds, Hd, ldd, (int)d, out, s);
   return launch_cos<64, 4>(src, dst, n_edges, Hs, lds, Hd, ldd, (int)d, out, s);
+}
+
+extern "C" int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_groups,
+                                            const int64_t* first, float* out_first, int64_t K,
+                                            const int64_t* dst, float* out, const float* Hs,
+                                            int64_t lds, const float* Hd, int64_t ldd, int64_t d,
+                                            void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_groups >= 0 && K >= 0 && d >= 0, "gnnrec_sddmm_cos_grouped_f32: negative size");
+  if (n_groups == 0 || (K == 0 && first == nullptr)) return GNNREC_OK;
+  GNNREC_REQUIRE(src_g && Hs && Hd && (K == 0 || (dst && out)) && (!first || out_first),
+                 "gnnrec_sddmm_cos_grouped_f32: null pointer");
+  GNNREC_REQUIRE(lds >= d && ldd >= d, "gnnrec_sddmm_cos_grouped_f32: leading dimension < d");
+  GNNREC_REQUIRE(d % 4 == 0 && d <= 256 && lds % 4 == 0 && ldd % 4 == 0 && aligned16(Hs) &&
+                     aligned16(Hd),
+                 "gnnrec_sddmm_cos_grouped_f32: needs d %% 4 == 0, d <= 256 and 16-B aligned "
+                 "rows (gnnrec_sddmm_cos_f32 takes the rest)");
+  GNNREC_REQUIRE(n_groups * ((K + 255) / 256 + 1) < (int64_t(1) << 32),
+                 "gnnrec_sddmm_cos_grouped_f32: too many groups");
+  hipStream_t s = as_stream(stream);
+  if (d <= 64)
+    return launch_cos_grouped<16>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd, ldd,
+                                  (int)d, s);
+  if (d <= 128)
+    return launch_cos_grouped<32>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd, ldd,
+                                  (int)d, s);
+  return launch_cos_grouped<64>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd, ldd,
+                                (int)d, s);
 }
 
 extern "C" int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,

@@ -436,6 +436,36 @@ void sddmm_cos(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Ten
      "gnnrec_sddmm_cos_f32");
 }
 
+void sddmm_cos_grouped(const Tensor& src_g, const optional<Tensor>& first, int64_t K,
+                       const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
+                       Tensor& out_first, Tensor& out) {
+  const OneDevice one_device_;
+  dev(src_g, "src_g", at::kLong);
+  dev(first, "first", at::kLong);
+  dev(dst, "dst", at::kLong);
+  dev(Hs, "Hs", at::kFloat);
+  dev(Hd, "Hd", at::kFloat);
+  dev(out_first, "out_first", at::kFloat);
+  dev(out, "out", at::kFloat);
+  const int64_t G = src_g.numel();
+  TORCH_CHECK_VALUE(K >= 0 && dst.numel() == G * K && out.numel() == G * K,
+                    "sddmm_cos_grouped: dst and out must hold n_groups x K entries");
+  TORCH_CHECK_VALUE(!has(first) || (first->numel() == G && out_first.numel() == G),
+                    "sddmm_cos_grouped: first and out_first must hold n_groups entries");
+  TORCH_CHECK_VALUE(Hs.size(1) == Hd.size(1), "endpoint feature sizes differ");
+  TORCH_CHECK_VALUE(src_g.is_contiguous() && dst.is_contiguous() &&
+                        (!has(first) || first->is_contiguous()) && out.is_contiguous() &&
+                        out_first.is_contiguous(),
+                    "sddmm_cos_grouped: contiguous ids and outputs");
+  const int64_t lds = ld(Hs, "Hs"), ldd = ld(Hd, "Hd");
+  if (meta(Hs)) return;
+  const c10::DeviceGuard g(Hs.device());
+  ck(gnnrec_sddmm_cos_grouped_f32(p<int64_t>(src_g), G, p<int64_t>(first), p<float>(out_first),
+                                  K, p<int64_t>(dst), p<float>(out), p<float>(Hs), lds,
+                                  p<float>(Hd), ldd, Hs.size(1), stream_of(Hs)),
+     "gnnrec_sddmm_cos_grouped_f32");
+}
+
 void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                         const Tensor& grad, const optional<Tensor>& gHs,
                         const optional<Tensor>& gHd, Tensor& ws) {
@@ -1795,6 +1825,8 @@ TORCH_LIBRARY(gnnrec, m) {
         "float out_div, "
         "Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");
+  m.def("sddmm_cos_grouped(Tensor src_g, Tensor? first, int K, Tensor dst, Tensor Hs, Tensor Hd, "
+        "Tensor(a!) out_first, Tensor(b!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
         "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");
   m.def("edge_mlp(Tensor src, Tensor dst, Tensor P, Tensor Q, Tensor W2, Tensor b2, Tensor w3, "
@@ -1901,6 +1933,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("spmm_project2", &spmm_project2);               \
   m.impl("spmm_pair", &spmm_pair);                       \
   m.impl("sddmm_cos", &sddmm_cos);                       \
+  m.impl("sddmm_cos_grouped", &sddmm_cos_grouped);       \
   m.impl("sddmm_cos_backward", &sddmm_cos_backward);     \
   m.impl("edge_mlp", &edge_mlp);                         \
   m.impl("sample_count", &sample_count);                 \

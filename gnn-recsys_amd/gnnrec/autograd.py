@@ -378,22 +378,30 @@ class CosineFn(torch.autograd.Function):
 class CosinePairFn(torch.autograd.Function):
     """CosineFn over the positive and the negative pair graph of one etype at once (they
     share node ids): one forward launch over both edge lists, and one backward call whose
-    gradients already sum both graphs' parts.  -> (cos_pos, cos_neg)."""
+    gradients already sum both graphs' parts.  -> (cos_pos, cos_neg).
+    K (optional): the negatives' sources are the positives' repeated K times
+    (negative_sampler.Uniform) — the forward is then the grouped launch
+    (ops.sddmm_cos_grouped: one gathered row per edge, the same bits)."""
 
     @staticmethod
-    def forward(ctx, hs, hd, src_p, dst_p, src_n, dst_n):
-        src, dst = torch.cat([src_p, src_n]), torch.cat([dst_p, dst_n])
-        out = ops.sddmm_cos(src, dst, hs.contiguous(), hd.contiguous())
-        ctx.save_for_backward(hs, hd, src, dst)
+    def forward(ctx, hs, hd, src_p, dst_p, src_n, dst_n, K=None):
+        hs, hd = hs.contiguous(), hd.contiguous()
+        if K is not None:
+            a, b = ops.sddmm_cos_grouped(src_p, dst_p, K, dst_n, hs, hd)
+        else:
+            out = ops.sddmm_cos(torch.cat([src_p, src_n]), torch.cat([dst_p, dst_n]), hs, hd)
+            a, b = out[:src_p.numel()], out[src_p.numel():]
+        ctx.save_for_backward(hs, hd, src_p, dst_p, src_n, dst_n)
         ctx.n_pos = src_p.numel()
-        return out[:ctx.n_pos], out[ctx.n_pos:]
+        return a, b
 
     @staticmethod
     def backward(ctx, g_pos, g_neg):
-        hs, hd, src, dst = ctx.saved_tensors
+        hs, hd, src_p, dst_p, src_n, dst_n = ctx.saved_tensors
         need = ctx.needs_input_grad
         if not (need[0] or need[1]):
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
+        src, dst = torch.cat([src_p, src_n]), torch.cat([dst_p, dst_n])
         n_pos = ctx.n_pos
         g = torch.empty(src.numel(), dtype=torch.float32, device=src.device)
         for part, gp in ((g[:n_pos], g_pos), (g[n_pos:], g_neg)):
@@ -403,7 +411,7 @@ class CosinePairFn(torch.autograd.Function):
                 part.copy_(gp.reshape(-1))
         ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(), g,
                                         need[0], need[1])
-        return ga, gb, None, None, None, None
+        return ga, gb, None, None, None, None, None
 
 
 class MarginLossFn(torch.autograd.Function):

@@ -404,6 +404,9 @@ class PairGraph:
         self._ndata = {nt: _FrameDict({NID: node_ids[nt]}) for nt in self.ntypes}
         self._edata = {ce: _FrameDict() for ce in self.canonical_etypes}
         self.nodes = _TypeAccessor(self._ndata, lambda k: k)
+        # K when this is the negative graph of negative_sampler.Uniform(K): every etype's
+        # sources are the positive graph's repeated K times (EdgeDataLoader sets it)
+        self.src_repeats_pos = None
 
     @property
     def ndata(self):
@@ -437,6 +440,7 @@ class PairGraph:
         for ce, f in self._edata.items():
             for k, v in f.items():
                 p._edata[ce][k] = v.to(device)
+        p.src_repeats_pos = self.src_repeats_pos
         return p
 
 

@@ -33,7 +33,6 @@ import torch.nn as nn
 
 from . import _lib, ops
 from . import autograd as ag
-from . import sampling
 
 USER_ITEM = ("user", "item")
 _PREAGG = ("pool_nn", "pool_nn_edge", "mean_nn", "mean_nn_edge")
@@ -548,8 +547,16 @@ class CosinePrediction(nn.Module):
                 pos[etype] = self.forward_one(h, etype, ps, pd)
                 continue
             ns, nd = neg_g.all_edges(etype=etype)
+            # negative_sampler.Uniform's pairs (the loader marks them): every positive's
+            # source repeated K times -> the grouped launch, one gathered row per edge
+            K = getattr(neg_g, 'src_repeats_pos', None)
+            if K is not None and (ns.numel() != ps.numel() * K or
+                                  not ops.cos_grouped_ok(h[etype[0]], h[etype[2]])):
+                K = None
             if _grad_mode(h[etype[0]], h[etype[2]]):
-                a, b = ag.CosinePairFn.apply(h[etype[0]], h[etype[2]], ps, pd, ns, nd)
+                a, b = ag.CosinePairFn.apply(h[etype[0]], h[etype[2]], ps, pd, ns, nd, K)
+            elif K is not None:
+                a, b = ops.sddmm_cos_grouped(ps, pd, K, nd, h[etype[0]], h[etype[2]])
             else:
                 cos = ops.sddmm_cos(torch.cat([ps, ns]), torch.cat([pd, nd]), h[etype[0]],
                                     h[etype[2]])
@@ -665,8 +672,14 @@ class ConvModel(nn.Module):
         if not active:
             return None
         out = self.layers[0]._layer_node(g, src, dst, active, fold=fold)
-        if out is not None and sampling.FIRST_BLOCK_TRANSPOSES[0]:
-            sampling.FIRST_BLOCK_TRANSPOSES[0] = False  # nothing reads them any more
+        ref = getattr(g, '_sampler', None)
+        sampler = ref() if ref is not None else None
+        if out is not None and sampler is not None:
+            # the sampler that built these blocks stops building the first block's transposes
+            # for the blocks this model folds (nothing reads them): every one under '1', those
+            # of at least FOLD_MIN_SRC_ROWS source rows under 'auto' — smaller ones, which
+            # the model does not fold, keep theirs for the backward
+            sampler.first_transposes_below = 0 if mode == "1" else FOLD_MIN_SRC_ROWS
         return out
 
     def forward(self, blocks, h, pos_g, neg_g, embedding_layer: bool = True):

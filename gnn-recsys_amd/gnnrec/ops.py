@@ -1082,6 +1082,33 @@ def sddmm_cos(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor,
     return out
 
 
+def cos_grouped_ok(Hs: torch.Tensor, Hd: torch.Tensor) -> bool:
+    """Can gnnrec_sddmm_cos_grouped_f32 score these tables (d % 4 == 0, d <= 256, 16-B rows)?"""
+    d = Hs.shape[1]
+    return (Hs.is_cuda and d % 4 == 0 and d <= 256 and Hs.dim() == 2 and Hd.dim() == 2 and
+            Hs.stride(1) == 1 and Hd.stride(1) == 1 and Hs.stride(0) % 4 == 0 and
+            Hd.stride(0) % 4 == 0 and Hs.data_ptr() % 16 == 0 and Hd.data_ptr() % 16 == 0)
+
+
+def sddmm_cos_grouped(src_g: torch.Tensor, first: Optional[torch.Tensor], K: int,
+                      dst: torch.Tensor, Hs: torch.Tensor, Hd: torch.Tensor):
+    """a7 for the pair graphs of negative_sampler.Uniform(K): group g's positive edge
+    (src_g[g], first[g]) and its K negatives (src_g[g], dst[g K + j]) -> (positive scores [G]
+    (None without `first`), negative scores [G K]); bitwise sddmm_cos of the expanded lists."""
+    for t, n in ((src_g, "src_g"), (dst, "dst")):
+        _dev(t, n, torch.int64)
+    if first is not None:
+        _dev(first, "first", torch.int64)
+    _dev(Hs, "Hs", torch.float32)
+    _dev(Hd, "Hd", torch.float32)
+    G = src_g.numel()
+    out_first = torch.empty(G if first is not None else 0, dtype=torch.float32, device=Hs.device)
+    out = torch.empty(G * int(K), dtype=torch.float32, device=Hs.device)
+    _T().sddmm_cos_grouped(src_g.contiguous(), None if first is None else first.contiguous(),
+                           int(K), dst.contiguous(), Hs, Hd, out_first, out)
+    return (out_first if first is not None else None), out
+
+
 def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, Hd: torch.Tensor,
                        grad: torch.Tensor, need_src: bool = True, need_dst: bool = True):
     """f2: gradients of sddmm_cos w.r.t. Hs and Hd given dL/dcos [E] -> (gHs|None, gHd|None),

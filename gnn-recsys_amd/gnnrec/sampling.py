@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import queue
 import threading
+import weakref
 from typing import Dict, List, Optional
 
 import torch
@@ -60,6 +61,11 @@ class BlockSampler:
         self.fused = True
         self._sb_scratch = {}
         self._stamp = 1
+        # the first block's source-major CSRs (sample_blocks(transposes=True)) are skipped
+        # for first blocks of at least this many source rows: a model that folds its
+        # NodeEmbeddings into the first layer (nn.ConvModel._folded_first_layer) never reads
+        # them there and sets the bound it folds from (None: always build them)
+        self.first_transposes_below = None
 
     def _fanout(self, block_id: int, ce) -> int:
         if self.fanouts is None:
@@ -158,9 +164,13 @@ class BlockSampler:
             blocks.insert(0, Block(dict(zip(nts, nodes)), num_dst, rels))
         if transposes:
             for block_id, b in enumerate(blocks):
-                if block_id > 0 or FIRST_BLOCK_TRANSPOSES[0]:
+                if block_id > 0 or self._first_transposes(b):
                     _add_transposes(b)
         return blocks
+
+    def _first_transposes(self, block) -> bool:
+        lim = self.first_transposes_below
+        return lim is None or sum(block.number_of_src_nodes(nt) for nt in block.ntypes) < lim
 
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
                       exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
@@ -174,6 +184,8 @@ class BlockSampler:
         if self._fused_ok(g):
             blocks = self._sample_fused(g, seeds, exclude_eids, transposes)
             _copy_block_data(g, blocks)
+            for b in blocks:
+                b._sampler = weakref.ref(self)
             return blocks
         masks = {}
         if exclude_eids:
@@ -189,7 +201,7 @@ class BlockSampler:
         try:
             for block_id in reversed(range(self.num_layers)):
                 block = self._one_block(g, seeds, block_id, masks)
-                if transposes and (block_id > 0 or FIRST_BLOCK_TRANSPOSES[0]):
+                if transposes and (block_id > 0 or self._first_transposes(block)):
                     _add_transposes(block)
                 blocks.insert(0, block)
                 seeds = {nt: block.srcdata[NID][nt] for nt in block.ntypes
@@ -199,6 +211,8 @@ class BlockSampler:
                 m.index_fill_(0, eids, 0)
                 rows.index_fill_(0, dst, 0)
         _copy_block_data(g, blocks)
+        for b in blocks:  # (the model's fold sets first_transposes_below through it)
+            b._sampler = weakref.ref(self)
         return blocks
 
     def _one_block(self, g, seeds, block_id, masks) -> Block:
@@ -293,13 +307,6 @@ def _copy_block_data(g, blocks) -> None:
         return
     for (frame, k), t in zip(dests, ops.gather_rows_batch(jobs)):
         frame[k] = t
-
-
-# The first block's transposes feed only the gradients of its source tables; a ConvModel
-# that folds its NodeEmbeddings into the first layer (nn.ConvModel._folded_first_layer) takes
-# none, and turns them off here the first time it does (they would be built on demand if
-# another model in the process asks for them: sage_rel_backward sorts the block itself)
-FIRST_BLOCK_TRANSPOSES = [True]
 
 
 def _add_transposes(block: Block) -> None:
@@ -656,4 +663,10 @@ class EdgeDataLoader:
             if self.negative_sampler is None:
                 yield input_nodes, pos_g, blocks
             else:
-                yield input_nodes, pos_g, PairGraph(neg_l, node_ids), blocks
+                neg_g = PairGraph(neg_l, node_ids)
+                if type(self.negative_sampler) is _Uniform:
+                    # every etype's negative sources are its positive sources repeated K times
+                    # (in local ids too: one relabel maps both): CosinePrediction.pair scores
+                    # them with the grouped launch
+                    neg_g.src_repeats_pos = self.negative_sampler.k
+                yield input_nodes, pos_g, neg_g, blocks

@@ -248,6 +248,45 @@ def test_c2_training_steps_match_oracle(c2_graph):
         opt.step()
 
 
+def test_c2_k2500_default_fold_gradients_match_unfolded(c2_graph, monkeypatch):
+    """C2 at the reference's K = 2500: the first block has ~960k source rows, above
+    FOLD_MIN_SRC_ROWS, so the DEFAULT mode (GNNREC_TRAIN_FOLD unset = 'auto') folds the
+    NodeEmbeddings into the first layer — (W_s W_e) x instead of W_s (W_e x).  Its loss and
+    every parameter gradient against the unfolded order (embed every source row, aggregate,
+    project; src/model.py:10-24, 143-148, 226-235) on the same blocks: fp32-reassociation
+    close (rtol 1e-4, the north star's tolerance), not bitwise."""
+    from gnnrec import nn as gnn
+    g, feats = c2_graph
+    _set_feats(g, feats[64])
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
+                          "mean", "cos", "sum", True).to(DEV).train()
+    K = 2500
+    _, pos_g, neg_g, blocks = next(iter(_edge_loader(g, [10, 10], K)))
+    n_src = sum(blocks[0].number_of_src_nodes(nt) for nt in blocks[0].ntypes)
+    assert n_src >= gnn.FOLD_MIN_SRC_ROWS, n_src
+    res = {}
+    for mode in ("auto", "0"):
+        if mode == "auto":
+            monkeypatch.delenv("GNNREC_TRAIN_FOLD", raising=False)
+        else:
+            monkeypatch.setenv("GNNREC_TRAIN_FOLD", "0")
+        model.zero_grad()
+        folded = model._folded_first_layer(blocks, blocks[0].srcdata["features"]) is not None
+        assert folded == (mode == "auto")
+        model.zero_grad()
+        _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+        loss = gnn.max_margin_loss(ps, ns, 0.266, K, True, {BUYS: pos_g.edata["recency"][BUYS]})
+        loss.backward()
+        res[mode] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                     if p.grad is not None})
+    assert res["auto"][1].keys() == res["0"][1].keys()
+    torch.testing.assert_close(res["auto"][0], res["0"][0], rtol=1e-4, atol=1e-7)
+    for n in res["auto"][1]:
+        torch.testing.assert_close(res["auto"][1][n], res["0"][1][n], rtol=1e-4, atol=1e-6,
+                                   msg=n)
+
+
 @pytest.mark.parametrize("n_layers", [3, 4])
 def test_c3_mean_nn_cosine_1024x2500_matches_oracle(c2_graph, n_layers):
     from gnnrec import nn as gnn

@@ -119,8 +119,6 @@ def test_random_training_steps_layer_node_matches_relation_nodes(monkeypatch, se
                                             "clicks": "clicked-by", "clicked-by": "clicks"},
                             negative_sampler=negative_sampler.Uniform(K), batch_size=128)
     _, pos_g, neg_g, blocks = next(iter(loader))
-    from gnnrec import sampling
-    monkeypatch.setattr(sampling, "FIRST_BLOCK_TRANSPOSES", [True])  # the fold below clears it
     res = {}
     # layer node vs relation nodes, both embedding then aggregating (GNNREC_TRAIN_FOLD=0: the
     # bitwise comparison below); then the first layer with the NodeEmbedding folded in

@@ -1712,3 +1712,66 @@ def test_spmm_group_rows_equal_wave_rows_bitwise(d, reduce, weighted, n_dst):
         b = ops.spmm(_t(ip_big), ti, X, reduce, edge_weight=tw, out=base.clone(),
                      empty_neginf=neg, accumulate=True)
         assert torch.equal(a, b[:n_dst])
+
+
+@pytest.mark.parametrize("d", [32, 64, 100, 128, 200, 256])
+def test_sddmm_cos_grouped_bitwise_equals_per_edge_and_oracle(d):
+    """a7 for negative_sampler.Uniform's pair graphs (src/sampling.py:163-165): the grouped
+    launch (each positive's source held in registers across its K negatives) scores bitwise
+    what the per-edge kernel scores on the expanded lists, and matches the oracle's
+    CosinePrediction (src/model.py:317-327) — zero rows (eps guard), K = 0 / 1 / chunk
+    boundaries / the reference's 2500, with and without the positive edges."""
+    from gnnrec import ops
+    rng = np.random.default_rng(d)
+    hs = rng.standard_normal((70, d)).astype(np.float32)
+    hd = rng.standard_normal((900, d)).astype(np.float32)
+    hs[5] = 0
+    hd[7] = 0
+    for G, K in ((13, 0), (13, 1), (9, 255), (9, 256), (9, 257), (4, 2500)):
+        src_g = rng.integers(0, 70, G)
+        src_g[0] = 5
+        first = rng.integers(0, 900, G)
+        dst = rng.integers(0, 900, G * K)
+        if G * K:
+            dst[0] = 7
+        pos, neg = ops.sddmm_cos_grouped(_t(src_g), _t(first), K, _t(dst), _t(hs), _t(hd))
+        _, neg2 = ops.sddmm_cos_grouped(_t(src_g), None, K, _t(dst), _t(hs), _t(hd))
+        src = np.concatenate([src_g, np.repeat(src_g, K)])
+        dd = np.concatenate([first, dst])
+        ref = ops.sddmm_cos(_t(src), _t(dd), _t(hs), _t(hd))
+        assert torch.equal(pos, ref[:G]) and torch.equal(neg, ref[G:]), (G, K)
+        assert torch.equal(neg2, neg)
+        ora = oracle.cosine_prediction({("user", "buys", "item"): (src, dd)},
+                                       {"user": hs, "item": hd})[("user", "buys", "item")][:, 0]
+        np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
+
+
+def test_cosine_pair_head_grouped_path_forward_and_gradients():
+    """CosinePrediction.pair on a negative graph marked by the loader (src_repeats_pos = K)
+    takes the grouped launch: the same scores and the same gradients as the unmarked graph."""
+    from gnnrec.graph import PairGraph
+    from gnnrec.nn import CosinePrediction
+    rng = np.random.default_rng(1)
+    ce = ("user", "buys", "item")
+    K, P = 50, 40
+    ps, pd = rng.integers(0, 30, P), rng.integers(0, 60, P)
+    nd = rng.integers(0, 60, P * K)
+    nodes = {"user": _t(np.arange(30)), "item": _t(np.arange(60))}
+    pos_g = PairGraph({ce: (_t(ps), _t(pd))}, nodes)
+    neg_plain = PairGraph({ce: (_t(np.repeat(ps, K)), _t(nd))}, nodes)
+    neg_marked = PairGraph({ce: (_t(np.repeat(ps, K)), _t(nd))}, nodes)
+    neg_marked.src_repeats_pos = K
+    head = CosinePrediction()
+    res = []
+    for neg_g in (neg_plain, neg_marked):
+        h = {"user": _t(np.random.default_rng(2).standard_normal((30, 64)).astype(np.float32)),
+             "item": _t(np.random.default_rng(3).standard_normal((60, 64)).astype(np.float32))}
+        for t in h.values():
+            t.requires_grad_(True)
+        a, b = head.pair(pos_g, neg_g, h)
+        (a[ce].sum() * 0.3 + (b[ce] ** 2).sum()).backward()
+        with torch.no_grad():
+            c, e = head.pair(pos_g, neg_g, {k: v.detach() for k, v in h.items()})
+        res.append((a[ce].detach(), b[ce].detach(), c[ce], e[ce], h["user"].grad, h["item"].grad))
+    for x, y in zip(*res):
+        assert torch.equal(x, y)

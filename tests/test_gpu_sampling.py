@@ -579,7 +579,6 @@ def test_first_layer_embedding_fold_matches_embed_then_aggregate(monkeypatch, ag
     from the hidden width (7) fold as well.  mean_nn (fc_preagg, non-linear) does not fold:
     bit-identical to the unfolded run.  The first block's transposes are no longer built."""
     from gnnrec import nn as gnn
-    from gnnrec import sampling
     from gnnrec.graph import HeteroGraph
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
     rng = np.random.default_rng(4)
@@ -602,21 +601,18 @@ def test_first_layer_embedding_fold_matches_embed_then_aggregate(monkeypatch, ag
     deg = [torch.diff(blocks[0]._rels[ce][0]) for ce in blocks[0].canonical_etypes]
     assert any(bool((d == 0).any()) for d in deg)
     res = {}
-    keep = sampling.FIRST_BLOCK_TRANSPOSES[0]
-    sampling.FIRST_BLOCK_TRANSPOSES[0] = True  # as in a fresh process (other tests fold too)
-    try:
-        for fold in ("1", "0"):
-            monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
-            model.zero_grad()
-            _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
-            loss = gnn.max_margin_loss(ps, ns, 0.266, 10)
-            loss.backward()
-            res[fold] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
-                                         if p.grad is not None})
-            if fold == "1":
-                assert sampling.FIRST_BLOCK_TRANSPOSES[0] == (agg != "mean")
-    finally:
-        sampling.FIRST_BLOCK_TRANSPOSES[0] = keep
+    sampler = blocks[0]._sampler()
+    assert sampler is loader.sampler and sampler.first_transposes_below is None
+    for fold in ("1", "0"):
+        monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
+        model.zero_grad()
+        _, ps, ns = model(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+        loss = gnn.max_margin_loss(ps, ns, 0.266, 10)
+        loss.backward()
+        res[fold] = (loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                     if p.grad is not None})
+        if fold == "1":  # the fold tells the loader's own sampler, nothing process-wide
+            assert (sampler.first_transposes_below is None) == (agg != "mean")
     assert res["1"][1].keys() == res["0"][1].keys()
     assert "user_embed.proj_feats.weight" in res["1"][1]
     if agg != "mean":
