@@ -1,0 +1,144 @@
+// asan_capi.cpp — the library's HOST code under AddressSanitizer + UBSan,
+// no GPU needed: `make -C gnn-recsys_amd/csrc asan` compiles every source with the host
+// side instrumented (-Xarch_host -fsanitize=...; device code is not, there is no GPU ASan on
+// this pool) into build_asan/, links this driver and runs it.  It drives what runs on the
+// host before any launch: every entry point's argument validation (null pointers, negative
+// or inconsistent sizes, unsupported modes), the empty-problem no-ops, the error string,
+// and the fused sampler's capacity / workspace planner over many plans.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "gnnrec.h"
+
+static int g_fail = 0;
+#define CHECK(c, what)                                                              \
+  do {                                                                              \
+    if (!(c)) {                                                                     \
+      std::fprintf(stderr, "FAIL %s:%d %s (last error: %s)\n", __FILE__, __LINE__, what, \
+                   gnnrec_last_error());                                            \
+      g_fail = 1;                                                                   \
+    }                                                                               \
+  } while (0)
+
+static bool err_has(const char* s) { return std::strstr(gnnrec_last_error(), s) != nullptr; }
+
+static void validation() {
+  CHECK(gnnrec_version() >= 1, "version");
+  void* p16 = reinterpret_cast<void*>(16);
+  CHECK(gnnrec_spmm_csr_f32(nullptr, nullptr, nullptr, nullptr, 4, 3, 4, 7, 0, nullptr, 4,
+                            nullptr) == GNNREC_EINVAL && err_has("unknown reduce"),
+        "spmm reduce");
+  CHECK(gnnrec_spmm_csr_f32(nullptr, nullptr, nullptr, nullptr, 4, 0, 4, 1, 0, nullptr, 4,
+                            nullptr) == GNNREC_OK,
+        "spmm empty");
+  CHECK(gnnrec_gemm_f32(nullptr, 4, 4, nullptr, nullptr, 1, 0, nullptr, nullptr, 0, nullptr,
+                        nullptr, 10, 300, GNNREC_EPI_L2NORM, 0, 0.f, nullptr, nullptr,
+                        static_cast<float*>(p16), 300, nullptr) != GNNREC_OK && err_has("A1"),
+        "gemm A1");
+  const float* parts3[3] = {static_cast<float*>(p16), static_cast<float*>(p16),
+                            static_cast<float*>(p16)};
+  CHECK(gnnrec_tree_sum_f32(parts3, 3, 8, static_cast<float*>(p16), nullptr) != GNNREC_OK &&
+            err_has("n_parts=3"),
+        "tree parts");
+  CHECK(gnnrec_sddmm_cos_f32(nullptr, nullptr, -1, nullptr, 0, nullptr, 0, 4, nullptr,
+                             nullptr) == GNNREC_EINVAL,
+        "cos negative");
+  CHECK(gnnrec_sddmm_cos_grouped_f32(nullptr, 4, nullptr, nullptr, 3, nullptr, nullptr, nullptr,
+                                     8, nullptr, 8, 8, nullptr) == GNNREC_EINVAL &&
+            err_has("null pointer"),
+        "cos grouped null");
+  CHECK(gnnrec_sddmm_cos_grouped_f32(nullptr, 0, nullptr, nullptr, 3, nullptr, nullptr, nullptr,
+                                     8, nullptr, 8, 8, nullptr) == GNNREC_OK,
+        "cos grouped empty");
+  CHECK(gnnrec_sample_count(nullptr, nullptr, nullptr, nullptr, nullptr, 4, 65, 0, nullptr,
+                            nullptr) == GNNREC_EINVAL && err_has("fanout"),
+        "sample_count fanout");
+  CHECK(gnnrec_gather_rows(nullptr, 4, nullptr, -1, 4, nullptr, 4, nullptr) == GNNREC_EINVAL,
+        "gather negative");
+  gnnrec_gather_job jobs[GNNREC_GATHER_MAX_JOBS + 1];
+  std::memset(jobs, 0, sizeof(jobs));
+  CHECK(gnnrec_gather_rows_batch(jobs, GNNREC_GATHER_MAX_JOBS + 1, nullptr) == GNNREC_EINVAL,
+        "gather batch n_jobs");
+  jobs[0].n = 5;
+  jobs[0].row_bytes = 8;
+  CHECK(gnnrec_gather_rows_batch(jobs, 1, nullptr) == GNNREC_EINVAL && err_has("null pointer"),
+        "gather batch null");
+  jobs[0].n = 0;
+  CHECK(gnnrec_gather_rows_batch(jobs, 3, nullptr) == GNNREC_OK, "gather batch empty");
+  CHECK(gnnrec_lstm_step_f32(nullptr, 4, nullptr, nullptr, nullptr, 0, 1, nullptr, nullptr,
+                             nullptr, 1000, nullptr, nullptr, 1000, nullptr) != GNNREC_OK &&
+            err_has("hidden size"),
+        "lstm hidden");
+}
+
+// the fused sampler's planner: capacities grow as the docs say, and bad plans are refused
+static void sampler_plans() {
+  gnnrec_sample_plan P;
+  std::memset(&P, 0, sizeof(P));
+  int64_t seed[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
+  int64_t edge[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_RELS];
+  int64_t node[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
+  int64_t ws = -1;
+  CHECK(gnnrec_sample_blocks_caps(nullptr, seed, edge, node, &ws) == GNNREC_EINVAL, "null plan");
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL, "zero types");
+  std::srand(5);
+  for (int it = 0; it < 2000; ++it) {
+    std::memset(&P, 0, sizeof(P));
+    P.n_types = 1 + std::rand() % GNNREC_SB_MAX_TYPES;
+    P.n_rels = std::rand() % (GNNREC_SB_MAX_RELS + 1);
+    P.n_steps = 1 + std::rand() % GNNREC_SB_MAX_STEPS;
+    for (int t = 0; t < P.n_types; ++t) {
+      P.type[t].n_nodes = std::rand() % 100000;
+      P.type[t].n_seeds = std::rand() % 2000;
+    }
+    for (int r = 0; r < P.n_rels; ++r) {
+      P.rel[r].src_type = std::rand() % P.n_types;
+      P.rel[r].dst_type = std::rand() % P.n_types;
+      for (int s = 0; s < P.n_steps; ++s) P.fanout[s][r] = std::rand() % 65;
+    }
+    CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_OK, "plan");
+    for (int s = 0; s < P.n_steps; ++s) {
+      for (int r = 0; r < P.n_rels; ++r)
+        CHECK(edge[s * GNNREC_SB_MAX_RELS + r] ==
+                  seed[s * GNNREC_SB_MAX_TYPES + P.rel[r].dst_type] * P.fanout[s][r],
+              "edge cap");
+      for (int t = 0; t < P.n_types; ++t) {
+        CHECK(node[s * GNNREC_SB_MAX_TYPES + t] >= seed[s * GNNREC_SB_MAX_TYPES + t] &&
+                  node[s * GNNREC_SB_MAX_TYPES + t] <=
+                      seed[s * GNNREC_SB_MAX_TYPES + t] + P.type[t].n_nodes,
+              "node cap");
+        if (s + 1 < P.n_steps)
+          CHECK(seed[(s + 1) * GNNREC_SB_MAX_TYPES + t] == node[s * GNNREC_SB_MAX_TYPES + t],
+                "next seeds");
+      }
+    }
+    CHECK(ws >= 0, "workspace");
+    // the launcher refuses the same plan without its buffers, before any launch
+    P.stamp = 1;
+    CHECK(gnnrec_sample_blocks(&P, nullptr) == GNNREC_EINVAL, "no buffers");
+  }
+  std::memset(&P, 0, sizeof(P));
+  P.n_types = 1;
+  P.n_rels = 1;
+  P.n_steps = 1;
+  P.fanout[0][0] = 65;
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL && err_has("fanout"),
+        "fanout bound");
+  P.fanout[0][0] = 3;
+  P.rel[0].dst_type = 2;
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL, "type range");
+  P.rel[0].dst_type = 0;
+  P.stamp = 0;
+  CHECK(gnnrec_sample_blocks(&P, nullptr) == GNNREC_EINVAL && err_has("stamp"), "stamp 0");
+  P.stamp = 0xFFFFFFFFu;
+  CHECK(gnnrec_sample_blocks(&P, nullptr) == GNNREC_EINVAL && err_has("stamp"), "stamp wrap");
+}
+
+int main() {
+  validation();
+  sampler_plans();
+  std::fprintf(stderr, g_fail ? "asan_capi: FAILED\n" : "asan_capi: ok\n");
+  return g_fail;
+}

@@ -6,12 +6,14 @@
 // keeps its position, a new source follows the seeds in ascending global id).
 //
 // What changes is where the relabel state lives and how many launches it takes:
-//   * seed positions: `pos[id]` = (stamp << 32) | position, int64 per node.  A step's seeds
-//     are the entries holding its stamp, so nothing is ever cleared: the next step writes
-//     stamp + 1, and a call starts at a stamp no earlier call used.  The finalize of step s
-//     writes step s+1's entries (its source nodes) while its own relabel reads step s's:
-//     a reader that finds stamp + 1 reads the same position (seeds keep their positions,
-//     new sources get theirs), so the race is benign by construction.
+//   * seed positions: `pos[id]` = (stamp << 32) | ~position, int64 per node, two arrays per
+//     type used alternately: step s reads the one its seeds were written to (by begin or by
+//     step s-1's finalize) and its finalize writes step s+1's seeds (its source nodes) into
+//     the other, so no kernel reads an array it writes.  A step's seeds are the entries
+//     holding its stamp: nothing is ever cleared, and a call starts at a stamp no earlier
+//     call used.  The position is stored complemented and written by atomicMax, so a seed
+//     listed twice keeps its FIRST position, whatever the order the writes land in (DGL's
+//     to_block hash map keeps the first insertion too).
 //   * new sources: one BIT per node (a 1M-node type: 128 KB, not a 4 MB mark array and an
 //     8 MB scan), ranked by a scan of the words' popcounts; two bitmaps per type, the pick
 //     kernel of step s zeroing the one step s+1 uses (the other was read by step s-1).
@@ -56,7 +58,8 @@ struct TypeArgs {
   const int64_t* seeds;    // this step's destination nodes
   const int64_t* n_seeds;  // device count (sizes row s - 1)
   int64_t seed_cap;
-  unsigned long long* pos;
+  unsigned long long* pos_cur;   // this step's seed positions (read)
+  unsigned long long* pos_next;  // the next step's (written by finalize)
   unsigned long long* bits_cur;
   unsigned long long* bits_next;
   int64_t* word_rank;
@@ -91,8 +94,18 @@ struct StepArgs {
 enum { kSecSeedPos, kSecZeroBits, kSecExclSet, kSecPick, kSecZeroNext, kSecCompact,
        kSecNewNodes, kSecPrefix, kSecExclClear };
 
+// (stamp << 32) | ~position: the atomicMax of two writes of one stamp keeps the smaller
+// position, and any write of a newer stamp beats every older entry
 __device__ __forceinline__ unsigned long long pack_pos(uint32_t stamp, int64_t p) {
-  return ((unsigned long long)stamp << 32) | (unsigned long long)(uint32_t)p;
+  return ((unsigned long long)stamp << 32) | (unsigned long long)(~(uint32_t)p);
+}
+__device__ __forceinline__ int64_t pos_of(unsigned long long v) {
+  return (int64_t)(~(uint32_t)v);
+}
+__device__ __forceinline__ void set_pos(unsigned long long* pos, int64_t id, uint32_t stamp,
+                                        int64_t p) {
+  __hip_atomic_fetch_max(pos + id, pack_pos(stamp, p), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------- begin
@@ -105,7 +118,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
   switch (A.sec.kind[k]) {
     case kSecSeedPos: {
       const TypeArgs& T = A.type[i];
-      if (t < T.n_seeds_host) T.pos[T.seeds[t]] = pack_pos(A.stamp, t);
+      if (t < T.n_seeds_host) set_pos(T.pos_cur, T.seeds[t], A.stamp, t);
       break;
     }
     case kSecZeroBits: {
@@ -182,7 +195,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
     R.pick_src[q] = src;
     R.pick_eid[q] = id;
     // a source that is not one of its type's seeds at this step is a new node
-    if ((uint32_t)(S.pos[src] >> 32) != A.stamp) {
+    if ((uint32_t)(S.pos_cur[src] >> 32) != A.stamp) {
       unsigned long long* w = S.bits_cur + (src >> 6);
       const unsigned long long bit = 1ull << (src & 63);
       if ((*w & bit) == 0ull)
@@ -271,11 +284,9 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
 // ---------------------------------------------------------------- finalize (step s)
 __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint32_t stamp,
                                             int32_t s) {
-  const unsigned long long v =
-      __hip_atomic_load(T.pos + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t hi = (uint32_t)(v >> 32);
-  if (hi == stamp || hi == stamp + 1u) return (int64_t)(uint32_t)v;  // a seed, or written
-  const int64_t w = s >> 6;                                          // by this finalize
+  const unsigned long long v = T.pos_cur[s];
+  if ((uint32_t)(v >> 32) == stamp) return pos_of(v);  // one of this step's seeds
+  const int64_t w = s >> 6;                           // a new source: its rank among them
   return n_p + T.word_rank[w] + __popcll(T.bits_cur[w] & ((1ull << (s & 63)) - 1ull));
 }
 
@@ -304,8 +315,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       while (word) {
         const int64_t id = t * 64 + __builtin_ctzll(word);
         T.nodes[p] = id;
-        __hip_atomic_store(T.pos + id, pack_pos(A.stamp + 1u, p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        T.pos_next[id] = pack_pos(A.stamp + 1u, p);  // (new ids are distinct)
         word &= word - 1ull;
         ++p;
       }
@@ -316,8 +326,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (t >= *T.n_seeds) return;
       const int64_t id = T.seeds[t];
       T.nodes[t] = id;
-      __hip_atomic_store(T.pos + id, pack_pos(A.stamp + 1u, t), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      set_pos(T.pos_next, id, A.stamp + 1u, t);
       break;
     }
     case kSecExclClear: {
@@ -470,7 +479,9 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.n_seeds = node_count + (int64_t)s * T + t;
       a.seed_cap = C.seed[s][t];
       a.n_seeds_host = ty.n_seeds;
-      a.pos = reinterpret_cast<unsigned long long*>(ty.pos);
+      a.pos_cur = reinterpret_cast<unsigned long long*>(ty.pos) + (A.stamp & 1u) * ty.n_nodes;
+      a.pos_next =
+          reinterpret_cast<unsigned long long*>(ty.pos) + ((A.stamp + 1u) & 1u) * ty.n_nodes;
       a.bits_cur = reinterpret_cast<unsigned long long*>(ty.bits) + (A.stamp & 1u) * W;
       a.bits_next = reinterpret_cast<unsigned long long*>(ty.bits) + ((A.stamp + 1u) & 1u) * W;
       a.word_rank = ty.word_rank;

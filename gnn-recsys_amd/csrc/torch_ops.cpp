@@ -1488,7 +1488,7 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
 // 1 + 3L launches, include/gnnrec.h) with ONE host read of the sizes at the end: outputs are
 // allocated at their capacities and returned narrowed to the actual sizes.
 //   relations r: global in-CSR, src / dst type index, exclusion (eids, COO dst, flag arrays:
-//   all four or none); types t: node count, step-0 seeds, scratch (pos int64 [n], bits int64
+//   all four or none); types t: node count, step-0 seeds, scratch (pos int64 [2n], bits int64
 //   [2 ceil(n/64)], word_rank int64 [ceil(n/64) + 1]); fanouts / keys flattened [step][r].
 //   -> per step s and relation r (flattened [s][r]): out_indptr [n_dst + 1], local src int32,
 //   eids; per step and type ([s][t]): the source node ids (seeds first); the sizes (node
@@ -1573,9 +1573,10 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     dev(bits[t], "bits", at::kLong);
     dev(word_rank[t], "word_rank", at::kLong);
     const int64_t W = (n_nodes[t] + 63) / 64;
-    TORCH_CHECK_VALUE(seeds[t].is_contiguous() && pos[t].numel() == n_nodes[t] &&
+    TORCH_CHECK_VALUE(seeds[t].is_contiguous() && pos[t].numel() == 2 * n_nodes[t] &&
                           bits[t].numel() == 2 * W && word_rank[t].numel() == W + 1,
-                      "sample_blocks: type ", t, ": scratch sized n, 2 ceil(n/64), ceil(n/64)+1");
+                      "sample_blocks: type ", t,
+                      ": scratch sized 2n, 2 ceil(n/64), ceil(n/64)+1");
     gnnrec_sample_type& ty = P.type[t];
     ty.n_nodes = n_nodes[t];
     ty.seeds = p<int64_t>(seeds[t]);

@@ -1284,14 +1284,14 @@ GATHER_MAX_JOBS = 16
 
 class SampleScratch:
     """Per-node-type state of the fused sampler (gnnrec_sample_blocks, include/gnnrec.h):
-    `pos` (stamped seed positions, never cleared), two new-source bitmaps and their word
-    ranks.  `stamp` advances by steps + 1 per call; before it would wrap, `pos` is zeroed
+    `pos` (two arrays of stamped seed positions, used alternately, never cleared), two
+    new-source bitmaps and their word ranks.  `stamp` advances by steps + 1 per call; before it would wrap, `pos` is zeroed
     and the count restarts (one memset per ~4e9 sampled layers)."""
 
     def __init__(self, n_nodes: int, device):
         w = (n_nodes + 63) // 64
         self.n_nodes = n_nodes
-        self.pos = torch.zeros(n_nodes, dtype=torch.int64, device=device)
+        self.pos = torch.zeros(2 * n_nodes, dtype=torch.int64, device=device)
         self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
         self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
 

@@ -395,10 +395,11 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * with the same keys.  Capacities bound every output (gnnrec_sample_blocks_caps), and the
  * actual sizes land in `sizes` on the device: [-1..L-1][types] source node counts
  * (row -1: the seed counts) at sizes[0 .. (L+1)*T), then [0..L-1][rels] edge counts.
- * Per type the caller keeps `pos` (int64 [n_nodes], all zero before the first call) and
+ * Per type the caller keeps `pos` (int64 [2 * n_nodes], all zero before the first call) and
  * `bits` (uint64 [2 * ceil(n_nodes/64)]) / `word_rank` (int64 [ceil(n_nodes/64) + 1])
  * scratch across calls; `stamp` >= 1 grows by L + 1 per call on the same `pos` arrays (the
- * caller zeroes `pos` and restarts at 1 before it would pass 2^32 - 2). */
+ * caller zeroes `pos` and restarts at 1 before it would pass 2^32 - 2).  A seed listed twice
+ * keeps its first position (its later copies get local ids but no edges point at them). */
 #define GNNREC_SB_MAX_RELS 8
 #define GNNREC_SB_MAX_TYPES 4
 #define GNNREC_SB_MAX_STEPS 4
@@ -419,7 +420,7 @@ typedef struct gnnrec_sample_type {
   int64_t n_nodes;
   const int64_t* seeds; /* step 0's destination nodes (the batch) */
   int64_t n_seeds;
-  int64_t* pos;         /* scratch, see above */
+  int64_t* pos;         /* scratch, see above: [2 * n_nodes] */
   uint64_t* bits;
   int64_t* word_rank;
 } gnnrec_sample_type;

@@ -713,3 +713,31 @@ def test_gather_rows_batch_equals_single_gathers():
     got = ops.gather_rows_batch(jobs)
     for (s, i), o in zip(jobs, got):
         assert torch.equal(o, s[i]), (s.shape, s.dtype)
+
+
+def test_fused_sampler_repeated_seeds_keep_their_first_position():
+    """A seed listed twice (DGL's to_block hash map keeps its first insertion): the fused
+    sampler's stamped positions are written by atomicMax of ~position, so every edge whose
+    source is that id points at its FIRST position, deterministically, at every step."""
+    from gnnrec.graph import NID
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    g, edges = _graph(n_u=200, n_i=100, e_b=4000, e_c=3000, min_deg=False)
+    s = MultiLayerNeighborSampler([4, 3], seed=3)
+    seeds = {"user": torch.tensor([5, 9, 5, 17, 9, 5], device=DEV),
+             "item": torch.tensor([2, 2, 40], device=DEV)}
+    runs = [s.sample_blocks(g, seeds) for _ in range(3)]
+    for blocks in runs:
+        for b in blocks:
+            for ce in b.canonical_etypes:
+                ip, loc, eid = (t.cpu().numpy() for t in b._rels[ce])
+                src_nodes = b.srcdata[NID][ce[0]].cpu().numpy()
+                n_p = b.number_of_dst_nodes(ce[0])
+                first = {}
+                for k, v in enumerate(src_nodes[:n_p].tolist()):
+                    first.setdefault(v, k)
+                s_all = edges[ce][0]
+                for q in range(loc.size):
+                    gid = int(s_all[eid[q]])
+                    assert src_nodes[loc[q]] == gid
+                    if gid in first:
+                        assert loc[q] == first[gid], (ce, gid, loc[q], first[gid])

@@ -24,8 +24,10 @@ def main():
     g = minibatch_graph(64, dev)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
-    seeds = [{"user": torch.randint(0, g.num_nodes("user"), (1024,), device=dev, generator=gen),
-              "item": torch.randint(0, g.num_nodes("item"), (1024,), device=dev, generator=gen)}
+    # distinct seeds (the per-layer path's prefix map is racy for repeated seeds; the fused
+    # one keeps the first position)
+    seeds = [{"user": torch.randperm(g.num_nodes("user"), device=dev, generator=gen)[:1024],
+              "item": torch.randperm(g.num_nodes("item"), device=dev, generator=gen)[:1024]}
              for _ in range(reps)]
     fused = MultiLayerNeighborSampler([10, 10], seed=4)
     layer = MultiLayerNeighborSampler([10, 10], seed=4)
