@@ -14,33 +14,21 @@ struct Frag {
 };
 
 // Streams read or written once per launch (CSR indices / indptr, self rows, outputs and
-// partials) vs the gathered source table, which should keep the caches: with
-// GNNREC_NT_STREAM=1 (default) the streams use non-temporal loads / stores: C4 pass 143.0 -> 142.3
-// ms in an alternating A/B (tools/micro/bench_ab.sh; tiles 4.45 -> 4.42 ms, fused 34.58 -> 34.45).
-#ifndef GNNREC_NT_STREAM
-#define GNNREC_NT_STREAM 1
-#endif
+// partials) vs the gathered source table, which should keep the caches: the streams use
+// non-temporal loads / stores (C4 pass 143.0 -> 142.3 ms against plain ones in an alternating
+// A/B, tools/micro/bench_ab.sh; tiles 4.45 -> 4.42 ms, fused 34.58 -> 34.45).
 typedef float f32x4s __attribute__((ext_vector_type(4)));
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (GNNREC_NT_STREAM) return __builtin_nontemporal_load(p);
-  else return *p;
+  return __builtin_nontemporal_load(p);
 }
 __device__ __forceinline__ float4 ld_stream4(const float* p) {
-  if constexpr (GNNREC_NT_STREAM) {
-    const f32x4s t = __builtin_nontemporal_load(reinterpret_cast<const f32x4s*>(p));
-    return make_float4(t[0], t[1], t[2], t[3]);
-  } else {
-    return *reinterpret_cast<const float4*>(p);
-  }
+  const f32x4s t = __builtin_nontemporal_load(reinterpret_cast<const f32x4s*>(p));
+  return make_float4(t[0], t[1], t[2], t[3]);
 }
 __device__ __forceinline__ void st_stream4(float* p, float a, float b, float c, float d) {
-  if constexpr (GNNREC_NT_STREAM) {
-    const f32x4s t = {a, b, c, d};
-    __builtin_nontemporal_store(t, reinterpret_cast<f32x4s*>(p));
-  } else {
-    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
-  }
+  const f32x4s t = {a, b, c, d};
+  __builtin_nontemporal_store(t, reinterpret_cast<f32x4s*>(p));
 }
 
 template <int VEC>

@@ -34,9 +34,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int LDSK = 36;  // padded k stride (floats)
-#ifndef GEMM_WAVES_PER_SIMD
-#define GEMM_WAVES_PER_SIMD 2
-#endif
+constexpr int GEMM_WAVES_PER_SIMD = 2;
 
 struct GemmArgs {
   const float* A1; int64_t lda1; int64_t K1; const float* W1;
@@ -67,10 +65,6 @@ __device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t l
   return v;
 }
 
-// FAST: every operand 16-B aligned with K1, K2 multiples of BK.  The loads are
-// then unconditional (out-of-range rows are clamped and zeroed by a select at
-// LDS-store time), so the next tile's loads stay in flight across the MFMAs —
-// a bounds check per load makes hipcc branch around it and wait vmcnt(0).
 // the epilogue stages the output tile in LDS in column halves, so the block's LDS
 // is just the K-loop tiles (36.9 KB at BN=128) and LDS never limits occupancy
 template <int BN>
@@ -244,9 +238,6 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
   }
 }
 
-#ifndef GNNREC_GEMM_STORE
-#define GNNREC_GEMM_STORE 0  // A/B builds: 1 = non-temporal output stores, 2 = no store (timing)
-#endif
 // The common epilogues with their flags known at compile time — FE = bias | relu << 1 |
 // l2norm << 2 (the SAGE projection: ReLU + row norm; fc_preagg: ReLU; NodeEmbedding: bias),
 // store-only, full 128-column tiles, 16-B aligned output — instead of runtime flags in the
@@ -312,19 +303,16 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmArgs& g, f32x16 (&a
       if (row < g.M) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(Ot + rl * OSTR + c);
         f32x4* o = reinterpret_cast<f32x4*>(g.out + row * g.ldo + round * SC + c);
-#if GNNREC_GEMM_STORE == 1
-        __builtin_nontemporal_store(v, o);
-#elif GNNREC_GEMM_STORE == 2
-        if (v[0] == 1.2345e-38f) *o = v;  // timing build: the store almost never issues
-#else
-        *o = v;
-#endif
+        *o = v;  // (non-temporal stores: +1 %, no store at all: the K loop still holds it —
+                 // profiles/r04i_gemm_store_ab.md)
       }
     }
   }
 }
 
-template <int BN, bool FAST>
+// the general form (any alignment, any K): bounds-checked loads staged through registers;
+// aligned operands with K a multiple of BK take gemm_f32_glds_kernel / gemm_f32_glds16_kernel
+template <int BN>
 __global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float smem[smem_floats<BN>()];
   float* As = smem;
@@ -391,19 +379,10 @@ __global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(Gemm
     }
     f32x4 ra[4], rw[NT];
     auto load_tile = [&](int64_t k0) {
-      if constexpr (FAST) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ra[i] = *reinterpret_cast<const f32x4*>(A + arow[i] * lda + k0 + kc);
+      for (int i = 0; i < 4; ++i) ra[i] = load4(A, arow[i], lda, k0 + kc, K, true, vecA);
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-          rw[i] = *reinterpret_cast<const f32x4*>(W + wrow[i] * K + k0 + kc);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ra[i] = load4(A, arow[i], lda, k0 + kc, K, true, vecA);
-#pragma unroll
-        for (int i = 0; i < NT; ++i) rw[i] = load4(W, wrow[i], K, k0 + kc, K, true, vecW);
-      }
+      for (int i = 0; i < NT; ++i) rw[i] = load4(W, wrow[i], K, k0 + kc, K, true, vecW);
     };
     load_tile(0);
 #pragma unroll 1
@@ -737,43 +716,19 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   dim3 grid((unsigned)((g.M + BM - 1) / BM), (unsigned)((g.N + BN - 1) / BN));
   const bool fast = g.vecA1 && g.vecW1 && g.K1 % BK == 0 &&
                     (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK == 0));
-  static const bool use_dma = [] {
-    const char* e = getenv("GNNREC_GEMM_DMA");
-    return !(e && e[0] == '0');
-  }();
-  // 16-deep K tiles (three blocks per CU) for 128-column outputs: +5-10 % at K = 128..256
-  // (tools/bench_gemm_k.py); GNNREC_GEMM_BK16=0 keeps the 32-deep kernel
-  static const bool use_bk16 = [] {
-    const char* e = getenv("GNNREC_GEMM_BK16");
-    return !(e && e[0] == '0');
-  }();
-  // 64-column outputs (the d = 64 minibatch layers, K = 64..128): the same 3-stage kernel
-  // overlaps one block's DMA prologue and epilogue with the other blocks' MFMAs;
-  // GNNREC_GEMM_BK16_N64=0 keeps the 32-deep kernel there
-  static const bool use_bk16_64 = [] {
-    const char* e = getenv("GNNREC_GEMM_BK16_N64");
-    return !(e && e[0] == '0');
-  }();
+  // 16-deep K tiles, three stages (three blocks per CU) for 128- and 64-column outputs:
+  // +5-10 % at K = 128..256 (tools/bench_gemm_k.py; the d = 64 minibatch layers overlap one
+  // block's DMA prologue and epilogue with the other blocks' MFMAs), and the compile-time
+  // epilogue (gemm_epilogue_fast) for the common flag sets (profiles/r03_gemm_experiments.md)
   if constexpr (BN == 128 || BN == 64) {
     const bool fast16 = g.vecA1 && g.vecW1 && g.K1 % BK16 == 0 &&
                         (g.K2 == 0 || (g.vecA2 && g.vecW2 && g.K2 % BK16 == 0));
-    if (fast16 && use_dma && use_bk16 && (BN == 128 || use_bk16_64)) {
-      static const int stages = [] {  // GNNREC_GEMM_STAGES: tuning knob
-        const char* e = getenv("GNNREC_GEMM_STAGES");
-        const int x = e ? atoi(e) : 3;
-        return x >= 2 && x <= 4 ? x : 3;
-      }();
-      // the compile-time epilogue (gemm_epilogue_fast) for the common flag sets:
-      // GNNREC_GEMM_FAST_EPI=0 keeps the runtime-flag epilogue (A/B)
-      static const bool fast_epi = [] {
-        const char* e = getenv("GNNREC_GEMM_FAST_EPI");
-        return !(e && e[0] == '0');
-      }();
+    if (fast16) {
       const bool sig = g.epilogue & GNNREC_EPI_SIGMOID;
       const int fe = (g.bias ? 1 : 0) | ((g.epilogue & GNNREC_EPI_RELU) ? 2 : 0) |
                      ((g.epilogue & GNNREC_EPI_L2NORM) ? 4 : 0);
-      if (fast_epi && stages == 3 && !sig && g.accum == GNNREC_ACC_STORE && !g.bias_ne &&
-          g.N == BN && g.vecO && (g.row_norm == nullptr || (fe & 4))) {
+      if (!sig && g.accum == GNNREC_ACC_STORE && !g.bias_ne && g.N == BN && g.vecO &&
+          (g.row_norm == nullptr || (fe & 4))) {
         switch (fe) {
           case 0: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 0>), grid, dim3(256), 0, s, g); break;
           case 1: hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3, 1>), grid, dim3(256), 0, s, g); break;
@@ -785,15 +740,12 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
         }
         return check_launch("gnnrec_gemm_f32");
       }
-      if (stages == 2) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 2>), grid, dim3(256), 0, s, g);
-      else if (stages == 4) hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 4>), grid, dim3(256), 0, s, g);
-      else hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3>), grid, dim3(256), 0, s, g);
+      hipLaunchKernelGGL((gemm_f32_glds16_kernel<BN, 3>), grid, dim3(256), 0, s, g);
       return check_launch("gnnrec_gemm_f32");
     }
   }
-  if (fast && use_dma) hipLaunchKernelGGL((gemm_f32_glds_kernel<BN>), grid, dim3(256), 0, s, g);
-  else if (fast) hipLaunchKernelGGL((gemm_f32_kernel<BN, true>), grid, dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((gemm_f32_kernel<BN, false>), grid, dim3(256), 0, s, g);
+  if (fast) hipLaunchKernelGGL((gemm_f32_glds_kernel<BN>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BN>), grid, dim3(256), 0, s, g);
   return check_launch("gnnrec_gemm_f32");
 }
 
@@ -858,7 +810,6 @@ extern "C" int gnnrec_gemm_rownorm_f32(const float* A1, int64_t lda1, int64_t K1
   if (N <= 128) return launch_gemm<128>(g, s);
   // wider outputs: 128-column blocks (two waves per SIMD) unless the row norm needs the
   // whole row in one block (the 256-column tile runs at one wave per SIMD)
-  if (!(epilogue & GNNREC_EPI_L2NORM) && !attn && getenv("GNNREC_GEMM_BN256") == nullptr)
-    return launch_gemm<128>(g, s);
+  if (!(epilogue & GNNREC_EPI_L2NORM) && !attn) return launch_gemm<128>(g, s);
   return launch_gemm<256>(g, s);
 }

@@ -101,8 +101,9 @@ int launch_cos(const int64_t* src, const int64_t* dst, int64_t n, const float* H
 // two ids, and the u norm is not recomputed K times.  Each value is formed exactly as
 // sddmm_cos_kernel forms it (same lane fragments, same xor tree, same final expression):
 // the scores are bitwise those of the per-edge kernel.
-constexpr int kCosU = 8;       // edges in flight per lane group
-constexpr int kCosChunk = 256; // negatives per wave
+constexpr int kCosU = 16;      // edges in flight per lane group
+constexpr int kCosChunk = 64;  // negatives per wave (40 waves per group at K = 2500: the
+                               // grid ends in a short tail; 256 per wave left a 25 % round)
 
 template <int LPR>
 __global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
     const float* __restrict__ Hd, int64_t ldd, int d) {
   constexpr int NPW = kWave / LPR;   // edges per wave-instruction
   constexpr int STEP = NPW * kCosU;  // edges per step (<= 64: one id per lane)
+  static_assert(kCosChunk <= 64 && kCosChunk % STEP == 0, "a chunk's ids fit one wave load");
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR;
   const int gl = lane % LPR;
@@ -152,9 +154,10 @@ __global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
   }
   const int64_t e_beg = g * K + c * kCosChunk;
   const int64_t e_end = g * K + min<int64_t>(K, (c + 1) * kCosChunk);
+  // the chunk's ids in one coalesced load (lane l: the chunk's l-th edge)
+  const int64_t all_ids = e_beg + lane < e_end ? dst[e_beg + lane] : 0;
   for (int64_t e0 = e_beg; e0 < e_end; e0 += STEP) {
-    const int64_t my = e0 + lane;  // lane l fetches the id of the step's l-th edge
-    const int64_t id = (lane < STEP && my < e_end) ? dst[my] : 0;
+    const int64_t id = STEP == kCosChunk ? all_ids : __shfl(all_ids, (int)(e0 - e_beg) + lane);
     float4 b[kCosU];
 #pragma unroll
     for (int k = 0; k < kCosU; ++k) {

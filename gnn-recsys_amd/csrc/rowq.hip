@@ -14,11 +14,9 @@ constexpr int kMaxDevices = 64;
 constexpr unsigned kRqSlots = 1024;  // launches that may be in flight on one device at once
 
 std::atomic<int> g_reserve{0};
-// the queue is the default schedule; GNNREC_ROWQ=0 makes the static grid-stride the default
-std::atomic<int> g_dynamic{[] {
-  const char* e = getenv("GNNREC_ROWQ");
-  return e && e[0] == '0' ? 0 : 1;
-}()};
+// the queue is the default schedule (gnnrec_set_concurrency(…, 0) selects the static
+// grid-stride)
+std::atomic<int> g_dynamic{1};
 // a per-device ring of device scratch slots, zeroed once and left zeroed by each user's
 // last block (self-cleaning); a slot is handed out only when its previous launch (on any
 // stream) has completed — the event per slot — and never to a launch being captured

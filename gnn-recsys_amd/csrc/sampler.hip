@@ -381,14 +381,6 @@ __global__ __launch_bounds__(kCsThreads) void scan_chained_kernel(const T* in, i
   }
 }
 
-inline bool chained_scan_enabled() {
-  static const bool v = [] {  // GNNREC_SCAN_CHAINED=0: the three-kernel form (A/B)
-    const char* e = getenv("GNNREC_SCAN_CHAINED");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 template <typename T>
 int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStream_t s) {
   GNNREC_REQUIRE(n >= 0, "scan: negative n");
@@ -401,12 +393,12 @@ int exclusive_scan(const T* in, int64_t n, int64_t* out, void* workspace, hipStr
     return GNNREC_OK;
   }
   const int64_t cs_tiles = (n + kCsTile - 1) / kCsTile;
-  if (cs_tiles == 1 && chained_scan_enabled()) {
+  if (cs_tiles == 1) {
     hipLaunchKernelGGL(scan_chained_kernel<T>, dim3(1), dim3(kCsThreads), 0, s, in, n, out,
                        nullptr, (int64_t)1);
     return check_launch("gnnrec_exclusive_scan");
   }
-  if (cs_tiles <= kScanMaxTiles && chained_scan_enabled()) {
+  if (cs_tiles <= kScanMaxTiles) {
     int ticket = -1;
     if (unsigned long long* slot = scan_slot(s, &ticket)) {
       hipLaunchKernelGGL(scan_chained_kernel<T>, dim3((unsigned)cs_tiles), dim3(kCsThreads), 0, s,

@@ -29,11 +29,10 @@
 namespace gnnrec {
 namespace {
 
-// rows per queue ticket of the row kernel (rowq.hpp): 0 = about kRqTicketEdges edges per
-// ticket from the CSR's mean degree (C4 tiles: 8 rows ≈ 280 µs of one wave, 0.5 % faster
-// than 4; minibatch blocks at 7-10 edges/row: 51-64 rows, so the ticket round trip stays
-// amortised);
-// GNNREC_RQ_CHUNK > 0 fixes it (tuning)
+// rows per queue ticket of the row kernel (rowq.hpp): about kRqTicketEdges edges per ticket
+// from the CSR's mean degree (C4 tiles: 8 rows ≈ 280 µs of one wave, 0.5 % faster than 4;
+// minibatch blocks at 7-10 edges/row: 51-64 rows, so the ticket round trip stays amortised);
+// the kernels' `chunk` argument > 0 would fix it (0: this rule)
 constexpr int64_t kRqTicketEdges = 512;
 // Below 32 rows per wave the static grid-stride wins: the queue's dequeues are bound by
 // the heads' atomic rate (≈88 per µs each), so a short launch either takes few long tickets
@@ -41,14 +40,7 @@ constexpr int64_t kRqTicketEdges = 512;
 // block relation (100k rows x 10 edges, d = 64): 52 µs static vs 127-165 µs queued; 1M rows:
 // 444 µs queued vs 472 static (tools/micro/spmm_one.py, profiles/r03_spmm_rowq.txt).
 constexpr int64_t kRqMinRowsPerWave = 32;
-inline int row_chunk() {
-  static const int v = [] {
-    const char* e = getenv("GNNREC_RQ_CHUNK");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? x : 0;
-  }();
-  return v;
-}
+constexpr int kRowChunk = 0;
 
 // rows per ticket: about kRqTicketEdges edges, but at least 4 tickets per wave of the grid.
 // A minibatch block (100k rows at 10 edges) at 51 rows per ticket fed 1960 of the grid's
@@ -150,14 +142,8 @@ __device__ __forceinline__ void group_rows(
   }
 }
 
-// Mean degree up to which the group kernel takes a d <= 64 CSR (GNNREC_SPMM_GROUP: 0 = never).
-inline int64_t group_max_avg_deg() {
-  static const int64_t v = [] {
-    const char* e = getenv("GNNREC_SPMM_GROUP");
-    return (int64_t)(e ? atol(e) : 16);
-  }();
-  return v;
-}
+// Mean degree up to which the group kernel takes a d <= 64 CSR.
+constexpr int64_t kGroupMaxAvgDeg = 16;
 
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED, int UNROLL>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
@@ -328,33 +314,23 @@ struct SpmmArgs {
                           // are then the plan's capacities (grid sizes)
 };
 
-// Resident 256-thread blocks per CU the row kernels may occupy (grid-stride beyond).
-// 8 = every wave slot of a CU; fewer leaves room for a concurrent kernel (the
-// projection GEMM on the side stream).  GNNREC_SPMM_BLOCKS_PER_CU overrides.
-inline int64_t blocks_per_cu() {
-  static int64_t v = [] {
-    const char* e = getenv("GNNREC_SPMM_BLOCKS_PER_CU");
-    const long x = e ? atol(e) : 0;
-    return (int64_t)(x > 0 && x <= 64 ? x : 8);
-  }();
-  return v;
-}
+// Resident 256-thread blocks per CU the row kernels occupy (grid-stride beyond): every wave
+// slot of a CU (CUs kept for concurrent kernels come off through gnnrec_set_concurrency).
+constexpr int64_t kBlocksPerCu = 8;
 
 inline unsigned grid_waves(int64_t units) {
   int64_t blocks = (units + 3) / 4;
   // CUs reserved for concurrent kernels (gnnrec_set_concurrency) come off the grid
   const int cus = device_cus() - cu_reserve();
-  const int64_t max_blocks = (int64_t)(cus > 8 ? cus : 8) * blocks_per_cu();
+  const int64_t max_blocks = (int64_t)(cus > 8 ? cus : 8) * kBlocksPerCu;
   if (blocks > max_blocks) blocks = max_blocks;
   return (unsigned)(blocks < 1 ? 1 : blocks);
 }
 
-#ifndef GNNREC_SPMM_UNROLL
-#define GNNREC_SPMM_UNROLL 4
-#endif
+constexpr int kSpmmUnroll = 4;  // wave-instructions in flight per lane (6, 8: the same)
 template <int LPR, int VEC, int REDUCE, bool WEIGHTED>
 int launch_all(const SpmmArgs& a, hipStream_t s) {
-  constexpr int UNROLL = (VEC == 4) ? GNNREC_SPMM_UNROLL : 2;
+  constexpr int UNROLL = (VEC == 4) ? kSpmmUnroll : 2;
   const int cols_per_slice = LPR * VEC;
   const unsigned slices = (unsigned)((a.d + cols_per_slice - 1) / cols_per_slice);
   const int eni = a.flags & (GNNREC_SPMM_EMPTY_NEGINF | GNNREC_SPMM_ACCUM);
@@ -367,8 +343,8 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
                      : nullptr;
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
-                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, row_chunk(),
-                     group_max_avg_deg());
+                     a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, kRowChunk,
+                     kGroupMaxAvgDeg);
   rowq_launched(ticket, s);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
@@ -463,9 +439,9 @@ int launch_csr2(const Csr2& c, const float* X, int64_t ldx, int64_t n_dst, int d
   const unsigned grid = grid_waves(n_dst);
   int ticket = -1;
   unsigned* rq = n_dst >= (int64_t)grid * 4 * 8 ? rowq_slot(s, &ticket) : nullptr;
-  hipLaunchKernelGGL((spmm_csr2_kernel<LPR, 4, REDUCE, WEIGHTED, GNNREC_SPMM_UNROLL>),
+  hipLaunchKernelGGL((spmm_csr2_kernel<LPR, 4, REDUCE, WEIGHTED, kSpmmUnroll>),
                      dim3(grid), dim3(256), 0, s, c, X, ldx, n_dst, d, ldo, flags, rq,
-                     row_chunk());
+                     kRowChunk);
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_csr2_f32");
 }

@@ -35,7 +35,7 @@
 // gather.  Rows come from the row queue in whole tiles, or an XCD-contiguous static walk.
 //
 // Measured (C5 user side, 10M rows × (40 + 10) edges, 268 GB, tools/gpu/r04c_pairvar.sh and
-// r04e_pairh.sh): the gather phase alone (timing build GNNREC_SPQ_PHASE=1) 34.6 ms = 0.969 of
+// r04e_pairh.sh): the gather phase alone (a round-4 timing build) 34.6 ms = 0.969 of
 // 8 TB/s — one 512 MB table is the cache-friendly working set the pre-projected launch lacks —
 // the MFMA phase alone 14.8 ms, the launch 38.4–38.6 ms (0.87): while one block sits in its
 // MFMA phase only the other block's 8 waves gather.  The pre-projected launch takes 36.6–37.8
@@ -47,14 +47,12 @@
 // state and gather share 128 VGPRs and spill 124–152 B/lane; LU = 1 / 3 lockstep unrolls 39.9
 // / 39.1 ms; the self rows requested ahead of the gathers: unchanged.
 //
-// bf16x3 (W3 instead of WT4): the projections as six v_mfma_f32_32x32x16_bf16 products per
-// K-step of operands split three ways (A split as the tile is written to LDS, three bf16
-// planes; B pre-split by the caller) — fp32-accurate, 2.7x fewer MFMA issue cycles (3.1 vs
-// 8.3 ms at C5), but 1.5x the weight bytes per tile (768 vs 512 B per lane).  Measured
-// (tools/gpu/r04j_*.sh, profiles/r04j_pair_bf16x3_ab.md): MFMA phase alone 19.8 ms vs 14.2 ms
-// for fp32, the launch 47.3 vs 38.7 ms — the projection phase is bound by streaming the four
-// weight matrices from L2 once per 32-row tile, not by the MFMA.  Kept selectable, not the
-// default.
+// Not kept either (tools/EXPERIMENTS.md): the projections as six bf16 MFMA products of
+// three-way split operands (fp32-accurate, 2.7x fewer MFMA issue cycles but 1.5x the weight
+// bytes per tile: launch 47.3 vs 38.7 ms, profiles/r04j_pair_bf16x3_ab.md — the projection
+// phase is bound by streaming the four weight matrices from L2 once per 32-row tile, not by
+// the MFMA); 48-row tiles / a third block per CU (round 5 verdict) were not attempted: the
+// pre-projected launch stays the default.
 #include "common.hpp"
 #include "gather.hpp"
 #include "rowq.hpp"
@@ -68,60 +66,17 @@ constexpr int kQWaves = 8;               // waves per block
 constexpr int kQRows = kQT / kQWaves;    // rows gathered per wave per tile
 constexpr int kQALd = 3 * kQD + 4;       // A tile row stride (floats)
 constexpr int kQCLd = kQD + 8;           // C tile row stride
-#ifndef GNNREC_SPQ_LU
-#define GNNREC_SPQ_LU 2  // lockstep gather: steps of 2·LU neighbours of 4 rows at once
-#endif
-#ifndef GNNREC_SPQ_U
-#define GNNREC_SPQ_U 4  // gather_range unroll for rows above 64 edges
-#endif
-#ifndef GNNREC_SPQ_WC
-#define GNNREC_SPQ_WC 16  // B operands per chunk
-#endif
-#ifndef GNNREC_SPQ_PHASE
-#define GNNREC_SPQ_PHASE 0  // timing builds only: 1 = gather phase alone, 2 = MFMA phase alone
-#endif
-constexpr int kQBLd = 3 * kQD + 8;      // bf16x3: A plane row stride (bf16 elements)
-constexpr int kQPlane = kQT * kQBLd;     // bf16x3: elements per A plane
-#ifndef GNNREC_SPQ_BC
-#define GNNREC_SPQ_BC 2  // bf16x3: K-steps of 16 per double-buffered B chunk
-#endif
+constexpr int kQLU = 2;   // lockstep gather: steps of 2·LU neighbours of 4 rows at once
+constexpr int kQU = 4;    // gather_range unroll for rows above 64 edges
+constexpr int kQWC = 16;  // B operands per chunk
 static_assert(2 * kQT * kQCLd <= kQT * kQALd, "C tiles must fit over the A tile");
-static_assert(2 * kQT * kQCLd * 4 <= 3 * kQPlane * 2, "C tiles must fit over the A planes");
 
 typedef float f32x16q __attribute__((ext_vector_type(16)));
 typedef float f32x4q __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8q __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4q __attribute__((ext_vector_type(4)));
 
-// A-tile bytes per block: fp32 [32][388], or the three bf16 planes [3][32][392]
-template <bool BF3>
-constexpr int tile_bytes() { return BF3 ? 3 * kQPlane * 2 : kQT * kQALd * 4; }
-
-// Four consecutive A-tile elements of row `row`, columns [c, c + 4).  BF3: x = hi + mid + lo
-// exactly (each piece the round-to-nearest bf16 of what the previous ones left; the
-// differences are exact in fp32), one plane each, so the six bf16 products of the
-// projection carry the fp32 operand's 24 significant bits.
-template <bool BF3>
-__device__ __forceinline__ void put4(unsigned char* tile, int row, int c, float4 v) {
-  if constexpr (!BF3) {
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(tile) + row * kQALd + c) = v;
-  } else {
-    const float x[4] = {v.x, v.y, v.z, v.w};
-    bf16x4q h, m, l;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const __bf16 hi = (__bf16)x[i];
-      const float r1 = x[i] - (float)hi;
-      const __bf16 mi = (__bf16)r1;
-      h[i] = hi;
-      m[i] = mi;
-      l[i] = (__bf16)(r1 - (float)mi);
-    }
-    __bf16* t = reinterpret_cast<__bf16*>(tile) + row * kQBLd + c;
-    *reinterpret_cast<bf16x4q*>(t) = h;
-    *reinterpret_cast<bf16x4q*>(t + kQPlane) = m;
-    *reinterpret_cast<bf16x4q*>(t + 2 * kQPlane) = l;
-  }
+// Four consecutive A-tile elements of row `row`, columns [c, c + 4)
+__device__ __forceinline__ void put4(float* tile, int row, int c, float4 v) {
+  *reinterpret_cast<float4*>(tile + row * kQALd + c) = v;
 }
 
 struct RawRel {
@@ -151,11 +106,11 @@ __device__ __forceinline__ void activate_q(bool relu, bool l2, float& y0, float&
 
 // The 4 rows [rbase, rbase + nv) of one relation, gathered in lockstep into A tile columns
 // [cofs, cofs + 128) of tile rows [r0, r0 + 4); their non-empty flags into ne[].
-template <bool W, bool BF3>
+template <bool W>
 __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict__ X,
-                                        int64_t ldx, int64_t rbase, int nv, unsigned char* As,
+                                        int64_t ldx, int64_t rbase, int nv, float* As,
                                         int r0, int cofs, int* ne, int lane) {
-  constexpr int LPR = 32, VEC = 4, NPI = kWave / LPR, U = GNNREC_SPQ_LU, kLR = 4;
+  constexpr int LPR = 32, VEC = 4, NPI = kWave / LPR, U = kQLU, kLR = 4;
   const int grp = lane / LPR, col = (lane % LPR) * VEC;
   const int64_t ipl = nv > 0 && lane <= nv ? ld_stream(r.indptr + rbase + lane) : 0;
   int64_t b[kLR + 1];
@@ -167,9 +122,6 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
 #pragma unroll
   for (int i = 0; i < kLR; ++i) {
     dg[i] = i < nv ? (int)(b[i + 1] - b[i]) : 0;
-#if GNNREC_SPQ_PHASE == 2
-    dg[i] = 0;
-#endif
     ridx[i] = lane < dg[i] ? ld_stream(r.indices + b[i] + lane) : 0;
     rwt[i] = 0.f;
     if constexpr (W) rwt[i] = lane < dg[i] ? ld_stream(r.ew + b[i] + lane) : 0.f;
@@ -210,7 +162,7 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
 #pragma unroll
     for (int i = 0; i < kLR; ++i)
       if (i < nv)
-        gather_range<LPR, VEC, GNNREC_REDUCE_SUM, W, GNNREC_SPQ_U, true>(
+        gather_range<LPR, VEC, GNNREC_REDUCE_SUM, W, kQU, true>(
             b[i], b[i + 1], r.indices, r.ew, X, ldx, col, true, lane, grp, acc[i], ridx[i]);
   }
 #pragma unroll
@@ -218,19 +170,19 @@ __device__ __forceinline__ void gather4(const RawRel& r, const float* __restrict
     combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc[i]);
     if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc[i], dg[i], 0);
     if (grp == 0)
-      put4<BF3>(As, r0 + i, cofs + col,
+      put4(As, r0 + i, cofs + col,
                 make_float4(acc[i].v[0], acc[i].v[1], acc[i].v[2], acc[i].v[3]));
     if (lane == 0) ne[r0 + i] = dg[i] > 0;
   }
 }
 
-template <bool WA, bool WB, bool BF3>
+template <bool WA, bool WB>
 __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
     RawRel ra, RawRel rb, const float* __restrict__ X, int64_t ldx, const float* __restrict__ H,
-    int64_t ldh, const float* __restrict__ WT4, const __bf16* __restrict__ W3, int64_t n_dst,
-    int epilogue, int combine, const float* __restrict__ attn_vec, float out_div,
-    float* __restrict__ out, int64_t ldo, unsigned* rq, int rq_ch) {
-  __shared__ __attribute__((aligned(16))) unsigned char As[tile_bytes<BF3>()];
+    int64_t ldh, const float* __restrict__ WT4, int64_t n_dst, int epilogue, int combine,
+    const float* __restrict__ attn_vec, float out_div, float* __restrict__ out, int64_t ldo,
+    unsigned* rq, int rq_ch) {
+  __shared__ __attribute__((aligned(16))) float As[kQT * kQALd];
   __shared__ int nes[2][kQT];
   __shared__ int64_t blk_r[2];
   float* const Ca = reinterpret_cast<float*>(As);  // over the A tile once the MFMAs read it
@@ -246,22 +198,17 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
   // B operands: lane half bh of a relation-rr wave reads matrix 2·rr + bh of the packed
   // [W_self,aᵀ, W_neigh,aᵀ, W_self,bᵀ, W_neigh,bᵀ] (each k-major 128×128): element
   // [i][32·cb + li]; one 32-bit per-lane offset + an immediate row offset per load
-  // BF3: lane half bh reads matrix 2·rr + bh of W3 [4][3 planes][128 n][128 k] (W itself,
-  // n-major, split as put4 splits A): row 32·cb + li, 8 consecutive k per plane and K-step
-  const void* const wsrc = BF3 ? static_cast<const void*>(W3) : static_cast<const void*>(WT4);
+  const void* const wsrc = WT4;
   const uint64_t wbase = ((uint64_t)__builtin_amdgcn_readfirstlane(
                               (unsigned)((uintptr_t)wsrc >> 32)) << 32) |
                          (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)wsrc);
   const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(wbase), 0, BF3 ? 4 * 3 * kQD * kQD * 2 : 4 * kQD * kQD * 4,
-      0x00020000);
-  const int wvoff = BF3 ? (((2 * rr + bh) * 3 * kQD + 32 * cb + li) * kQD) * 2
-                        : ((2 * rr + bh) * kQD * kQD + 32 * cb + li) * 4;
+      reinterpret_cast<void*>(wbase), 0, 4 * kQD * kQD * 4, 0x00020000);
+  const int wvoff = ((2 * rr + bh) * kQD * kQD + 32 * cb + li) * 4;
   // A operands: row li of the tile, K columns [0, 128) (self) for lane half 0 and the
   // relation's aggregate [128 + 128·rr, +128) for lane half 1
   const int acol = bh ? kQD + kQD * rr : 0;
-  const float* const ap = reinterpret_cast<const float*>(As) + li * kQALd + acol;
-  const __bf16* const ab = reinterpret_cast<const __bf16*>(As) + li * kQBLd + acol;
+  const float* const ap = As + li * kQALd + acol;
 
   auto tile = [&](int64_t t0, int64_t lim) __attribute__((always_inline)) {
     const int64_t rbase = t0 + wave * kQRows;
@@ -276,13 +223,13 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
       const int rl = 2 * q + bh;
       hs[q] = rl < nv ? ld_stream4(H + (rbase + rl) * ldh + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    gather4<WA, BF3>(ra, X, ldx, rbase, nv, As, r0, kQD, nes[0], lane);
-    gather4<WB, BF3>(rb, X, ldx, rbase, nv, As, r0, 2 * kQD, nes[1], lane);
+    gather4<WA>(ra, X, ldx, rbase, nv, As, r0, kQD, nes[0], lane);
+    gather4<WB>(rb, X, ldx, rbase, nv, As, r0, 2 * kQD, nes[1], lane);
 #pragma unroll
-    for (int q = 0; q < kQRows / 2; ++q) put4<BF3>(As, r0 + 2 * q + bh, col, hs[q]);
+    for (int q = 0; q < kQRows / 2; ++q) put4(As, r0 + 2 * q + bh, col, hs[q]);
     __syncthreads();
 
-    constexpr int kWC = GNNREC_SPQ_WC;
+    constexpr int kWC = kQWC;
     float bw[2][kWC];
     auto load_w = [&](float* dst, int i0) __attribute__((always_inline)) {
 #pragma unroll
@@ -293,47 +240,6 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
     f32x16q c;
 #pragma unroll
     for (int v = 0; v < 16; ++v) c[v] = 0.f;
-#if GNNREC_SPQ_PHASE == 1
-    if (nv >= 0) {
-    } else
-#endif
-    if constexpr (BF3) {
-      // K = 256 as 16 steps of v_mfma_f32_32x32x16_bf16 (self k in lane half 0, aggregate k
-      // in half 1, as the fp32 form), six per step: hi·hi, hi·mid, mid·hi, hi·lo, mid·mid,
-      // lo·hi — the dropped products are below 2^-24 of |a·b| — smallest first
-      constexpr int BC = GNNREC_SPQ_BC, kSteps = kQD / 8;
-      bf16x8q bq[2][BC][3];
-      auto load_b = [&](bf16x8q (*dst)[3], int s0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int st = 0; st < BC; ++st)
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            dst[st][p] = __builtin_bit_cast(
-                bf16x8q, __builtin_amdgcn_raw_buffer_load_b128(
-                             wrsrc, wvoff + (s0 + st) * 16, p * kQD * kQD * 2, 0));
-      };
-      load_b(bq[0], 0);
-#pragma unroll
-      for (int ch = 0; ch < kSteps / BC; ++ch) {
-        if (ch + 1 < kSteps / BC) load_b(bq[(ch + 1) & 1], (ch + 1) * BC);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int st = 0; st < BC; ++st) {
-          const int s8 = 8 * (ch * BC + st);
-          const bf16x8q a0 = *reinterpret_cast<const bf16x8q*>(ab + s8);
-          const bf16x8q a1 = *reinterpret_cast<const bf16x8q*>(ab + kQPlane + s8);
-          const bf16x8q a2 = *reinterpret_cast<const bf16x8q*>(ab + 2 * kQPlane + s8);
-          const bf16x8q* b = bq[ch & 1][st];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0], c, 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
     load_w(bw[0], 0);
 #pragma unroll
     for (int ch = 0; ch < kQD / kWC; ++ch) {
@@ -349,7 +255,6 @@ __global__ __launch_bounds__(kQWaves * 64, 4) void spmm_pair_mfma_kernel(
         c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], w[i + 3], c, 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-    }
     }
     __syncthreads();  // every wave's MFMAs have read the A tile: C goes over it
     // D map of the 32x32 MFMA: col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 bh
@@ -458,7 +363,7 @@ extern "C" int gnnrec_spmm_pair_f32(
     const float* bias_a, const float* bias_nonempty_a, const int64_t* indptr_b,
     const int32_t* indices_b, const float* ew_b, int reduce_b, const float* bias_b,
     const float* bias_nonempty_b, const float* X, int64_t n_src, int64_t ldx, const float* H,
-    int64_t ldh, const float* WT4, const uint16_t* W3, int64_t n_dst, int64_t d, int epilogue,
+    int64_t ldh, const float* WT4, int64_t n_dst, int64_t d, int epilogue,
     int combine, const float* attn_vec, float out_div, float* out, int64_t ldo, void* stream) {
   GNNREC_REQUIRE(d == kQD, "gnnrec_spmm_pair_f32: only d = %d (got %lld)", kQD, (long long)d);
   GNNREC_REQUIRE((reduce_a == GNNREC_REDUCE_SUM || reduce_a == GNNREC_REDUCE_MEAN) &&
@@ -474,9 +379,8 @@ extern "C" int gnnrec_spmm_pair_f32(
   GNNREC_REQUIRE(n_dst >= 0, "gnnrec_spmm_pair_f32: negative n_dst");
   if (n_dst == 0) return GNNREC_OK;
   GNNREC_REQUIRE(indptr_a && indptr_b && X && H && out, "gnnrec_spmm_pair_f32: null pointer");
-  GNNREC_REQUIRE((WT4 != nullptr) != (W3 != nullptr),
-                 "gnnrec_spmm_pair_f32: pass exactly one of WT4 (fp32) and W3 (bf16x3)");
-  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(WT4) && aligned16(W3) && ldx % 4 == 0 &&
+  GNNREC_REQUIRE(WT4 != nullptr, "gnnrec_spmm_pair_f32: null WT4");
+  GNNREC_REQUIRE(aligned16(X) && aligned16(H) && aligned16(WT4) && ldx % 4 == 0 &&
                      ldh % 4 == 0 && ldo % 2 == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                  "gnnrec_spmm_pair_f32: X/H/W need 16-B aligned rows, out 8-B");
@@ -484,11 +388,7 @@ extern "C" int gnnrec_spmm_pair_f32(
   const int64_t cus = device_cus() - cu_reserve();
   int64_t blocks = 2 * (cus > 8 ? cus : 8);
   if (blocks > tiles) blocks = tiles;
-  static const int rq_ch = [] {  // rows per queue ticket (whole tiles)
-    const char* e = getenv("GNNREC_RQ_CHUNK_PAIR");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 16 ? x * kQT : 2 * kQT;
-  }();
+  constexpr int rq_ch = 2 * kQT;  // rows per queue ticket (whole tiles)
   hipStream_t s = as_stream(stream);
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
@@ -498,25 +398,16 @@ extern "C" int gnnrec_spmm_pair_f32(
                  reduce_b == GNNREC_REDUCE_MEAN};
   const dim3 grid((unsigned)blocks), block(kQWaves * 64);
   GNNREC_REQUIRE(n_src >= 0, "gnnrec_spmm_pair_f32: negative n_src");
-  const __bf16* w3 = reinterpret_cast<const __bf16*>(W3);
-#define GNNREC_SPQ(WA_, WB_, BF3_)                                                              \
-  hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_, BF3_>), grid, block, 0, s, a, b, X, ldx, \
-                     H, ldh, WT4, w3, n_dst, epilogue, combine, attn_vec, out_div, out, ldo, rq, \
-                     rq_ch)
-#define GNNREC_SPQ_W(BF3_)                  \
-  if (ew_a) {                               \
-    if (ew_b) GNNREC_SPQ(true, true, BF3_); \
-    else GNNREC_SPQ(true, false, BF3_);     \
-  } else {                                  \
-    if (ew_b) GNNREC_SPQ(false, true, BF3_); \
-    else GNNREC_SPQ(false, false, BF3_);    \
-  }
-  if (W3 != nullptr) {
-    GNNREC_SPQ_W(true)
+#define GNNREC_SPQ(WA_, WB_)                                                                 \
+  hipLaunchKernelGGL((spmm_pair_mfma_kernel<WA_, WB_>), grid, block, 0, s, a, b, X, ldx, H, ldh, \
+                     WT4, n_dst, epilogue, combine, attn_vec, out_div, out, ldo, rq, rq_ch)
+  if (ew_a) {
+    if (ew_b) GNNREC_SPQ(true, true);
+    else GNNREC_SPQ(true, false);
   } else {
-    GNNREC_SPQ_W(false)
+    if (ew_b) GNNREC_SPQ(false, true);
+    else GNNREC_SPQ(false, false);
   }
-#undef GNNREC_SPQ_W
 #undef GNNREC_SPQ
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_pair_f32");

@@ -30,16 +30,8 @@ namespace {
 constexpr int kPD = 128;       // d_neigh = d_self = N
 constexpr int kPWaves = 16;    // waves per block (one persistent block per CU)
 constexpr int kPRows = 2;      // rows per wave per iteration (halves the LDS weight reads)
-// rows per queue ticket (rowq.hpp): four iterations, ≈120 µs at C4; GNNREC_RQ_CHUNK_FUSED
-// overrides (tuning; rounded up to a multiple of kPRows)
-inline int fused_chunk() {
-  static const int v = [] {
-    const char* e = getenv("GNNREC_RQ_CHUNK_FUSED");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 8;
-  }();
-  return v;
-}
+// rows per queue ticket (rowq.hpp): four iterations, ≈120 µs at C4 (a multiple of kPRows)
+constexpr int kFusedChunk = 8;
 
 // The per-row epilogue both fused kernels share: lane = output columns j0, j0+1 of `row`
 // (y = the projected pre-activation incl. bias): ReLU, zero-guarded L2 norm over the 64
@@ -119,12 +111,8 @@ __device__ __forceinline__ void epilogue_row(const EpiArgs& e, int64_t row, bool
     y0 = y0 / e.out_div;
     y1 = y1 / e.out_div;
   }
-  if constexpr (GNNREC_NT_STREAM) {
-    typedef float f32x2s __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(f32x2s{y0, y1}, reinterpret_cast<f32x2s*>(p));
-  } else {
-    *p = make_float2(y0, y1);
-  }
+  typedef float f32x2s __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(f32x2s{y0, y1}, reinterpret_cast<f32x2s*>(p));  // (gather.hpp)
 }
 
 template <int REDUCE, bool WEIGHTED, int UNROLL>
@@ -287,7 +275,7 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 // Measured (C5 bought-by, 10M rows × 10 edges, tools/probe_c5.py, one box): 12.8–13.1 ms
 // (13.1 with the rows gathered one after another), PRE 10.6 ms + 0.38 ms for the 1M-row
 // source projection; 18.0 ms for the VALU kernel; 7.6 + 7.1 ms for gather + GEMM launched
-// back to back.  Timing builds (GNNREC_SPM_PHASE): the GEMM phase alone (no neighbour
+// back to back.  Timing builds (round 2, tools/EXPERIMENTS.md): the GEMM phase alone (no neighbour
 // loads) takes 7.3–7.8 ms — the fp32 MFMA at ≈0.6 of its peak, as in the plain GEMM
 // (profiles/r02_gemm_experiments.md) — so the two phases overlap by ≈2 ms only.  Not kept
 // (same session A/B): 64-row tiles (C in the A tile's LDS, 12.6–12.7 ms, within noise of
@@ -297,24 +285,11 @@ __global__ __launch_bounds__(kPWaves * 64) void spmm_project_kernel(
 // the MFMA waves' registers, one barrier per pipelined step) took 17–22 ms: 8 gathering
 // waves per CU cannot keep HBM busy at 10 edges per row.  The sharded pass fuses such a
 // relation only in the PRE form (else gather + GEMM on the side stream).
-#ifndef GNNREC_SPP_UDEF
-#define GNNREC_SPP_UDEF 4  // the VALU kernel's default gather unroll (GNNREC_SPP_UNROLL=2|8 env)
-#endif
-#ifndef GNNREC_SPM_U
-#define GNNREC_SPM_U 4  // gather wave-instructions in flight per lane (rows > 64 edges)
-#endif
-#ifndef GNNREC_SPM_PHASE
-#define GNNREC_SPM_PHASE 0  // timing builds only: 1 = gather phase alone, 2 = GEMM phase alone
-#endif
-#ifndef GNNREC_SPM_LU
-#define GNNREC_SPM_LU 2  // lockstep gather: steps of 2·LU neighbours of 4 rows at once
-#endif
-#ifndef GNNREC_SPM_WC
-#define GNNREC_SPM_WC 16  // W operands per chunk (64: all loaded up front)
-#endif
-#ifndef GNNREC_SPM_EU
-#define GNNREC_SPM_EU 4  // epilogue rows unrolled
-#endif
+constexpr int kSppU = 4;   // the VALU kernel's gather wave-instructions in flight per lane
+constexpr int kSpmU = 4;   // the MFMA kernel's, rows > 64 edges
+constexpr int kSpmLU = 2;  // lockstep gather: steps of 2·LU neighbours of 4 rows at once
+constexpr int kSpmWC = 16; // W operands per chunk (64 — all loaded up front — measured slower)
+constexpr int kSpmEU = 4;  // epilogue rows unrolled
 constexpr int kMT = 32;                  // rows per tile
 constexpr int kMB = kMT / 32;            // 32-row MFMA blocks per tile
 constexpr int kMWaves = 8;               // waves per block
@@ -389,7 +364,7 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
     // row's neighbours are still summed by group in gather_range's order
     // (k = j + u·NPI + grp, ascending — the same sequence for any LU): the same aggregate
     // bits.  Rows with more than 64 edges take gather_range row by row.
-    constexpr int NPI = kWave / LPR, U = GNNREC_SPM_LU, kLR = 4;
+    constexpr int NPI = kWave / LPR, U = kSpmLU, kLR = 4;
 #pragma unroll
     for (int g = 0; g < kMRows; g += kLR) {
       int ridx[kLR];
@@ -400,9 +375,6 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
       for (int r = 0; r < kLR; ++r) {
         const int64_t b = bound(g + r);
         dg[r] = g + r < nv ? (int)(bound(g + r + 1) - b) : 0;
-#if GNNREC_SPM_PHASE == 2
-        dg[r] = 0;
-#endif
         ridx[r] = lane < dg[r] ? ld_stream(indices + b + lane) : 0;
         rwt[r] = 0.f;
         if constexpr (WEIGHTED) rwt[r] = lane < dg[r] ? ld_stream(ew + b + lane) : 0.f;
@@ -476,7 +448,7 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
     // W operands loaded once for the tile's kMB row blocks
     // W operands stream in 4 chunks of 16 (double-buffered, the next chunk's loads in
     // flight under this chunk's MFMAs) instead of 64 live registers
-    constexpr int kWC = GNNREC_SPM_WC;
+    constexpr int kWC = kSpmWC;
     float bw[2][kWC];
     auto load_w = [&](float* dst, int i0) __attribute__((always_inline)) {
 #pragma unroll
@@ -490,9 +462,6 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
 #pragma unroll
       for (int v = 0; v < 16; ++v) c[b][v] = 0.f;
     const float* ap = As + li * kALd + (PRE ? 64 * kh + 32 * bh : kh * kPD + 64 * bh);
-#if GNNREC_SPM_PHASE == 1
-    if (nv < 0)
-#endif
     {
       load_w(bw[0], 0);
 #pragma unroll
@@ -523,7 +492,7 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
         cp[(32 * b + (v & 3) + 8 * (v >> 2) + 4 * bh) * kCLd] = c[b][v];
     __syncthreads();
 
-#pragma unroll GNNREC_SPM_EU
+#pragma unroll kSpmEU
     for (int r = 0; r < kMRows; ++r) {
       const int rl = wave * kMRows + r;
       const float2 s2 = *reinterpret_cast<const float2*>(&Cs0[rl * kCLd + j0]);
@@ -625,25 +594,15 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
   const int64_t cus = device_cus() - cu_reserve();
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
   // queued rows when every wave has several tickets of work
-  const int rq_ch = fused_chunk();
+  const int rq_ch = kFusedChunk;
   hipStream_t s = as_stream(stream);
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * kPWaves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
   const dim3 grid((unsigned)blocks), block(kPWaves * 64);
-  static const int unroll = [] {  // gather wave-instructions in flight per lane (tuning knob)
-    const char* e = getenv("GNNREC_SPP_UNROLL");
-    return e ? atoi(e) : 4;
-  }();
-#define GNNREC_SPP_ONE(R, W, U)                                                              \
-  hipLaunchKernelGGL((spmm_project_kernel<R, W, U>), grid, block, 0, s, indptr, indices, ew, X, \
-                     ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue, accum, \
-                     out_div, attn_vec, attn_state, out, ldo, rq, rq_ch)
-#define GNNREC_SPP(R, W)                                  \
-  do {                                                    \
-    if (unroll == 8) GNNREC_SPP_ONE(R, W, 8);             \
-    else if (unroll == 2) GNNREC_SPP_ONE(R, W, 2);        \
-    else GNNREC_SPP_ONE(R, W, GNNREC_SPP_UDEF);           \
-  } while (0)
+#define GNNREC_SPP(R, W)                                                                      \
+  hipLaunchKernelGGL((spmm_project_kernel<R, W, kSppU>), grid, block, 0, s, indptr, indices, ew, \
+                     X, ldx, H, ldh, W_selfT, W_neighT, bias, bias_nonempty, n_dst, epilogue,    \
+                     accum, out_div, attn_vec, attn_state, out, ldo, rq, rq_ch)
   if (ew) {
     if (reduce == GNNREC_REDUCE_SUM) GNNREC_SPP(GNNREC_REDUCE_SUM, true);
     else if (reduce == GNNREC_REDUCE_MEAN) GNNREC_SPP(GNNREC_REDUCE_MEAN, true);
@@ -654,7 +613,6 @@ extern "C" int gnnrec_spmm_project_f32(const int64_t* indptr, const int32_t* ind
     else GNNREC_SPP(GNNREC_REDUCE_MAX, false);
   }
 #undef GNNREC_SPP
-#undef GNNREC_SPP_ONE
   rowq_launched(ticket, s);
   return check_launch("gnnrec_spmm_project_f32");
 }
@@ -699,17 +657,13 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
   const int64_t cus = device_cus() - cu_reserve();
   int64_t blocks = 2 * (cus > 8 ? cus : 8);
   if (blocks > tiles) blocks = tiles;
-  static const int rq_ch = [] {  // rows per queue ticket (whole tiles)
-    const char* e = getenv("GNNREC_RQ_CHUNK_MFMA");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 16 ? x * kMT : 2 * kMT;
-  }();
+  constexpr int rq_ch = 2 * kMT;  // rows per queue ticket (whole tiles)
   hipStream_t s = as_stream(stream);
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
   const dim3 grid((unsigned)blocks), block(kMWaves * 64);
 #define GNNREC_SPM(R, W, P)                                                                     \
-  hipLaunchKernelGGL((spmm_project_mfma_kernel<R, W, GNNREC_SPM_U, P>), grid, block, 0, s,      \
+  hipLaunchKernelGGL((spmm_project_mfma_kernel<R, W, kSpmU, P>), grid, block, 0, s,      \
                      indptr, indices, ew, X, ldx, H, ldh, W_selfT, W_neighT, bias,              \
                      bias_nonempty, n_dst, epilogue, accum, out_div, attn_vec, attn_state, out, \
                      ldo, rq, rq_ch)
@@ -753,14 +707,11 @@ extern "C" int gnnrec_spmm_project_mfma_f32(const int64_t* indptr, const int32_t
 namespace gnnrec {
 namespace {
 
-#ifndef GNNREC_SPP2_WAVES
-#define GNNREC_SPP2_WAVES 16  // waves per (one-per-CU) block: 12 waves at U = 8-10 took 59.5 ms,
-#endif                        // 8 waves at U = 12-16 75 ms (vs 38.2): the wave count, not the
-                              // loads in flight per wave, sets this kernel's rate
-constexpr int kP2Waves = GNNREC_SPP2_WAVES;
-#ifndef GNNREC_SPP2_U
-#define GNNREC_SPP2_U 5  // gather wave-instructions in flight per lane (C5: 5 beats 4 by ≈0.6 ms; 6 and 8 slow down)
-#endif
+// waves per (one-per-CU) block: 12 waves at U = 8-10 took 59.5 ms, 8 waves at U = 12-16
+// 75 ms (vs 38.2): the wave count, not the loads in flight per wave, sets this kernel's rate
+constexpr int kP2Waves = 16;
+// gather wave-instructions in flight per lane (C5: 5 beats 4 by ≈0.6 ms; 6 and 8 slow down)
+constexpr int kP2U = 5;
 
 struct PreRel {
   const int64_t* indptr;
@@ -772,183 +723,9 @@ struct PreRel {
   int mean;
 };
 
-template <bool WA, bool WB>
-__global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_kernel(
-    PreRel ra, PreRel rb, const float* __restrict__ H, int64_t ldh,
-    const float* __restrict__ WaT, const float* __restrict__ WbT,
-    const float* __restrict__ bias_a, const float* __restrict__ bias_b, int64_t n_dst,
-    int epilogue, int combine, const float* __restrict__ attn_vec, float out_div,
-    float* __restrict__ out, int64_t ldo,
-    unsigned* rq, int rq_ch) {
-  __shared__ float Wa[kPD * kPD];
-  __shared__ float Wb[kPD * kPD];
-  __shared__ float slots[kP2Waves][kPRows][kPD];
-  for (int i = threadIdx.x; i < kPD * kPD / 4; i += kP2Waves * 64) {
-    reinterpret_cast<float4*>(Wa)[i] = reinterpret_cast<const float4*>(WaT)[i];
-    reinterpret_cast<float4*>(Wb)[i] = reinterpret_cast<const float4*>(WbT)[i];
-  }
-  __syncthreads();
-
-  constexpr int LPR = 32, VEC = 4, U = GNNREC_SPP2_U;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int grp = lane / LPR;
-  const int col = (lane % LPR) * VEC;
-  const int j0 = 2 * lane;
-  const bool relu = epilogue & GNNREC_EPI_RELU;
-  const bool l2 = epilogue & GNNREC_EPI_L2NORM;
-  const int64_t stride = (int64_t)gridDim.x * kP2Waves * kPRows;
-  const float ba0 = bias_a ? bias_a[j0] : 0.f, ba1 = bias_a ? bias_a[j0 + 1] : 0.f;
-  const float bb0 = bias_b ? bias_b[j0] : 0.f, bb1 = bias_b ? bias_b[j0 + 1] : 0.f;
-  const float ca0 = ra.bias_ne ? ra.bias_ne[j0] : 0.f, ca1 = ra.bias_ne ? ra.bias_ne[j0 + 1] : 0.f;
-  const float cb0 = rb.bias_ne ? rb.bias_ne[j0] : 0.f, cb1 = rb.bias_ne ? rb.bias_ne[j0 + 1] : 0.f;
-  const float at0 = attn_vec ? attn_vec[j0] : 0.f, at1 = attn_vec ? attn_vec[j0 + 1] : 0.f;
-
-  // a relation's bounds and first 64 indices of rows [row0, row0 + nv) (both relations'
-  // are requested before either gathers: B's indptr -> indices chain hides under A's rows)
-  struct Heads {
-    int64_t rbd[kPRows + 1];
-    int pidx[kPRows];
-  };
-  auto heads = [&](const PreRel& r, int64_t row0, int nv, Heads& h) __attribute__((always_inline)) {
-    const int64_t ipl = lane <= nv ? ld_stream(r.indptr + row0 + lane) : 0;
-#pragma unroll
-    for (int i = 0; i <= kPRows; ++i) h.rbd[i] = __shfl(ipl, i <= nv ? i : nv);
-#pragma unroll
-    for (int i = 0; i < kPRows; ++i)
-      h.pidx[i] = i < nv && lane < h.rbd[i + 1] - h.rbd[i] ? ld_stream(r.indices + h.rbd[i] + lane)
-                                                            : 0;
-  };
-  // the aggregate of relation `r` for rows [row0, row0 + nv) into this lane's columns
-  // j0, j0 + 1 (g), and whether each row has an in-edge
-  auto gather_rel = [&](const PreRel& r, auto weighted, const Heads& h, int nv,
-                        float (&g)[kPRows][2], bool (&ne)[kPRows]) __attribute__((always_inline)) {
-    constexpr bool W = decltype(weighted)::value;
-#pragma unroll
-    for (int i = 0; i < kPRows; ++i) {
-      Frag<VEC> acc;
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) acc.v[v] = 0.f;
-      int64_t deg = 0;
-      if (i < nv) {
-        deg = h.rbd[i + 1] - h.rbd[i];
-        gather_range<LPR, VEC, GNNREC_REDUCE_SUM, W, U, true>(h.rbd[i], h.rbd[i + 1], r.indices,
-                                                              r.ew, r.Y, r.ldy, col, true, lane,
-                                                              grp, acc, h.pidx[i]);
-      }
-      combine_groups<LPR, VEC, GNNREC_REDUCE_SUM>(acc);
-      if (r.mean) finalize<VEC, GNNREC_REDUCE_MEAN>(acc, deg, 0);
-      ne[i] = deg > 0;
-      // lane L takes columns 2L, 2L+1 = components 2(L&1), 2(L&1)+1 of lane L/2's fragment
-      const int sl = lane >> 1;
-      const float x0 = __shfl(acc.v[0], sl), x1 = __shfl(acc.v[1], sl);
-      const float x2 = __shfl(acc.v[2], sl), x3 = __shfl(acc.v[3], sl);
-      g[i][0] = (lane & 1) ? x2 : x0;
-      g[i][1] = (lane & 1) ? x3 : x1;
-    }
-  };
-
-  auto step = [&](int64_t row0, int64_t lim) {
-    const int nv = (int)(lim - row0 < kPRows ? lim - row0 : kPRows);  // valid rows, >= 1
-#pragma unroll
-    for (int i = 0; i < kPRows; ++i) {  // self rows into this wave's slots first
-      const float4 hs = i < nv && grp == 0 ? ld_stream4(H + (row0 + i) * ldh + col)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (grp == 0) *reinterpret_cast<float4*>(&slots[wave][i][col]) = hs;
-    }
-    float ga[kPRows][2], gb[kPRows][2];
-    bool nea[kPRows], neb[kPRows];
-    Heads ha, hb;
-    heads(ra, row0, nv, ha);
-    heads(rb, row0, nv, hb);
-    gather_rel(ra, std::integral_constant<bool, WA>{}, ha, nv, ga, nea);
-    gather_rel(rb, std::integral_constant<bool, WB>{}, hb, nv, gb, neb);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-    float za[kPRows][2], zb[kPRows][2];
-#pragma unroll
-    for (int i = 0; i < kPRows; ++i) {
-      za[i][0] = ba0 + (nea[i] ? ca0 : 0.f);
-      za[i][1] = ba1 + (nea[i] ? ca1 : 0.f);
-      zb[i][0] = bb0 + (neb[i] ? cb0 : 0.f);
-      zb[i][1] = bb1 + (neb[i] ? cb1 : 0.f);
-    }
-#pragma unroll 2
-    for (int k = 0; k < kPD; k += 4) {
-      float4 s4[kPRows];
-#pragma unroll
-      for (int i = 0; i < kPRows; ++i) s4[i] = *reinterpret_cast<const float4*>(&slots[wave][i][k]);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const float2 wa = *reinterpret_cast<const float2*>(&Wa[(k + kk) * kPD + j0]);
-        const float2 wb = *reinterpret_cast<const float2*>(&Wb[(k + kk) * kPD + j0]);
-#pragma unroll
-        for (int i = 0; i < kPRows; ++i) {
-          const float s = kk == 0 ? s4[i].x : kk == 1 ? s4[i].y : kk == 2 ? s4[i].z : s4[i].w;
-          za[i][0] = fmaf(s, wa.x, za[i][0]);
-          za[i][1] = fmaf(s, wa.y, za[i][1]);
-          zb[i][0] = fmaf(s, wb.x, zb[i][0]);
-          zb[i][1] = fmaf(s, wb.y, zb[i][1]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots free for the next rows
-
-#pragma unroll
-    for (int i = 0; i < kPRows; ++i) {
-      float ya0 = za[i][0] + ga[i][0], ya1 = za[i][1] + ga[i][1];
-      float yb0 = zb[i][0] + gb[i][0], yb1 = zb[i][1] + gb[i][1];
-      activate(relu, l2, ya0, ya1);
-      activate(relu, l2, yb0, yb1);
-      float y0, y1;
-      if (combine == GNNREC_ACC_MAX) {
-        y0 = fmaxf(ya0, yb0);
-        y1 = fmaxf(ya1, yb1);
-      } else if (combine == GNNREC_ACC_ATTN_LAST) {
-        // softmax over the two relations of s_r = a·y_r, in the order of the single-relation
-        // launches' online form: a first (max s_a, sum 1), then b rescales and normalises
-        float sa = ya0 * at0 + ya1 * at1, sb = yb0 * at0 + yb1 * at1;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          sa += __shfl_xor(sa, off);
-          sb += __shfl_xor(sb, off);
-        }
-        const float mnew = fmaxf(sa, sb);
-        const float keep = expf(sa - mnew), cnew = expf(sb - mnew);
-        const float nrm = 1.f / (1.f * keep + cnew);
-        y0 = ya0 * keep + yb0 * cnew;
-        y1 = ya1 * keep + yb1 * cnew;
-        y0 *= nrm;
-        y1 *= nrm;
-      } else {
-        y0 = ya0 + yb0;
-        y1 = ya1 + yb1;
-      }
-      if (out_div > 0.f) {
-        y0 = y0 / out_div;
-        y1 = y1 / out_div;
-      }
-      if (i < nv) {
-        typedef float f32x2s __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store(f32x2s{y0, y1},
-                                    reinterpret_cast<f32x2s*>(out + (row0 + i) * ldo + j0));
-      }
-    }
-  };
-
-  if (rq != nullptr) {
-    rq_for_each(rq, n_dst, rq_ch, [&](int64_t r0, int64_t r1) {
-      for (int64_t row0 = r0; row0 < r1; row0 += kPRows) step(row0, r1);
-    });
-    rq_finish(rq);
-    return;
-  }
-  for (int64_t row0 = ((int64_t)blockIdx.x * kP2Waves + wave) * kPRows; row0 < n_dst;
-       row0 += stride)
-    step(row0, n_dst);
-}
-
-// ---- the same launch with each step's row heads prefetched one step ahead ------------
-// The kernel above spends 64 % of its wave cycles parked on s_waitcnt (DESIGN.md §9 item
+// ---- each step's row heads prefetched one step ahead ------------------------------------
+// A wave that takes 2 rows at a time and gathers both relations of each (the round-2 form,
+// tools/EXPERIMENTS.md) spent 64 % of its wave cycles parked on s_waitcnt (DESIGN.md §9 item
 // 8): every step of 2 rows opens with two dependent round trips — indptr, then the first
 // indices of both relations — before the first source row can be requested.  Here a wave
 // knows its NEXT row pair while it works on the current one (the static walk, or the row
@@ -959,8 +736,8 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_kernel(
 //     global_load_lds (no registers live across the matvec: the earlier register-carried
 //     form spilled to scratch and ran at 73 ms),
 // so step i+1 starts gathering immediately from LDS-resident heads.  A row's later index
-// windows (past 48 edges) load as before.  Summation order per row is unchanged: the
-// aggregate bits equal the kernel above (and spmm_csr_kernel's).
+// windows (past 48 edges) load as before.  Summation order per row is gather_range's: the
+// aggregate bits equal spmm_csr_kernel's.
 // LDS: 2 x 64 KiB weights + 16 KiB self-row slots + 16 waves x (4 x 192 B index windows +
 // 48 B bounds) = 156.75 KiB of the CU's 160.
 constexpr int kP2Win = 48;  // prefetched indices per (row, relation)
@@ -1019,7 +796,7 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
   }
   __syncthreads();
 
-  constexpr int LPR = 32, VEC = 4, U = GNNREC_SPP2_U, NPI = kWave / LPR;
+  constexpr int LPR = 32, VEC = 4, U = kP2U, NPI = kWave / LPR;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane / LPR;
   const int col = (lane % LPR) * VEC;
@@ -1302,13 +1079,8 @@ extern "C" int gnnrec_spmm_project2_f32(
   const int64_t cus = device_cus() - cu_reserve();
   if (blocks > (cus > 8 ? cus : 8)) blocks = cus > 8 ? cus : 8;
   // rows per queue ticket: 16 (C5 user side, one session: 38.4–38.8 ms at 8, 37.4 at 16,
-  // 37.5 at 32 — within the kernel's ±1 ms run-to-run spread); GNNREC_RQ_CHUNK_FUSED2
-  // overrides
-  static const int rq_ch = [] {
-    const char* e = getenv("GNNREC_RQ_CHUNK_FUSED2");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? (x + kPRows - 1) / kPRows * kPRows : 16;
-  }();
+  // 37.5 at 32 — within the kernel's ±1 ms run-to-run spread)
+  constexpr int rq_ch = 16;
   hipStream_t s = as_stream(stream);
   int ticket = -1;
   unsigned* rq = n_dst >= blocks * kP2Waves * rq_ch * 4 ? rowq_slot(s, &ticket) : nullptr;
@@ -1317,28 +1089,11 @@ extern "C" int gnnrec_spmm_project2_f32(
                  reduce_a == GNNREC_REDUCE_MEAN};
   const PreRel b{indptr_b, indices_b, ew_b, Yb, ldyb, bias_nonempty_b,
                  reduce_b == GNNREC_REDUCE_MEAN};
-  // GNNREC_SPP2_PIPE=0: the kernel without the one-step-ahead heads (A/B)
-  static const bool pipe = [] {
-    const char* e = getenv("GNNREC_SPP2_PIPE");
-    return !(e && e[0] == '0');
-  }();
-#define GNNREC_SPP2(WA_, WB_)                                                                  \
-  do {                                                                                         \
-    if (pipe)                                                                                  \
-      hipLaunchKernelGGL((spmm_project2_pipe_kernel<WA_, WB_>), grid, block, 0, s, a, b, H,    \
-                         ldh, W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,  \
-                         attn_vec, out_div, out, ldo, rq, rq_ch);                              \
-    else                                                                                       \
-      hipLaunchKernelGGL((spmm_project2_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,   \
-                         W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,       \
-                         attn_vec, out_div, out, ldo, rq, rq_ch);                              \
-  } while (0)
-  // GNNREC_SPP2_NT=0: every source row temporal whatever the flags (A/B knob)
-  static const bool nt_ok = [] {
-    const char* e = getenv("GNNREC_SPP2_NT");
-    return !(e && e[0] == '0');
-  }();
-  if (pipe && nt && nt_ok && !ew_a && !ew_b) {
+#define GNNREC_SPP2(WA_, WB_)                                                                \
+  hipLaunchKernelGGL((spmm_project2_pipe_kernel<WA_, WB_>), grid, block, 0, s, a, b, H, ldh,    \
+                     W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine, attn_vec, \
+                     out_div, out, ldo, rq, rq_ch)
+  if (nt && !ew_a && !ew_b) {
     if (nt == 1)
       hipLaunchKernelGGL((spmm_project2_pipe_kernel<false, false, 1>), grid, block, 0, s, a, b,
                          H, ldh, W_self_aT, W_self_bT, bias_a, bias_b, n_dst, epilogue, combine,

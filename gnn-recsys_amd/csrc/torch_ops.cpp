@@ -20,6 +20,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <utility>
 #include <vector>
 
 #include "gnnrec.h"
@@ -371,8 +372,8 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
                const optional<Tensor>& bias_nonempty_a, const Tensor& indptr_b,
                const Tensor& indices_b, const optional<Tensor>& ew_b, int64_t reduce_b,
                const optional<Tensor>& bias_b, const optional<Tensor>& bias_nonempty_b,
-               const Tensor& X, const Tensor& H, const optional<Tensor>& WT4,
-               const optional<Tensor>& W3, int64_t epilogue, int64_t combine,
+               const Tensor& X, const Tensor& H, const Tensor& WT4, int64_t epilogue,
+               int64_t combine,
                const optional<Tensor>& attn_vec, double out_div, Tensor& out) {
   const OneDevice one_device_;
   dev(indptr_a, "indptr_a", at::kLong);
@@ -388,20 +389,22 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
   dev(X, "X", at::kFloat);
   dev(H, "H", at::kFloat);
   dev(WT4, "WT4", at::kFloat);
-  dev(W3, "W3", at::kBFloat16);
   dev(attn_vec, "attn_vec", at::kFloat);
   dev(out, "out", at::kFloat);
   const int64_t n_dst = indptr_a.numel() - 1, d = X.size(1);
   TORCH_CHECK_VALUE(indptr_b.numel() == n_dst + 1, "spmm_pair: the relations' row counts differ");
   TORCH_CHECK_VALUE(H.size(1) == d && H.size(0) >= n_dst, "spmm_pair: H shape");
-  TORCH_CHECK_VALUE(has(WT4) != has(W3),
-                    "spmm_pair: pass exactly one of WT4 (fp32) and W3 (bf16x3 planes)");
-  TORCH_CHECK_VALUE(!has(WT4) || (WT4->is_contiguous() && WT4->numel() == 4 * d * d),
+  TORCH_CHECK_VALUE(WT4.is_contiguous() && WT4.numel() == 4 * d * d,
                     "spmm_pair: WT4 must be a contiguous [4, d, d] weight array");
-  TORCH_CHECK_VALUE(!has(W3) || (W3->is_contiguous() && W3->numel() == 12 * d * d),
-                    "spmm_pair: W3 must be a contiguous [4, 3, d, d] bf16 array");
   TORCH_CHECK_VALUE(out.size(0) == n_dst && out.size(1) == d, "out must be [", n_dst, ", ", d,
                     "]");
+  // the kernel reads d entries of every bias and of the attention vector
+  for (const auto& v : {std::make_pair(&bias_a, "bias_a"), std::make_pair(&bias_b, "bias_b"),
+                        std::make_pair(&bias_nonempty_a, "bias_nonempty_a"),
+                        std::make_pair(&bias_nonempty_b, "bias_nonempty_b"),
+                        std::make_pair(&attn_vec, "attn_vec")})
+    TORCH_CHECK_VALUE(!has(*v.first) || ((*v.first)->numel() == d && (*v.first)->is_contiguous()),
+                      "spmm_pair: ", v.second, " must be a contiguous vector of ", d, " floats");
   const int64_t ldx = ld(X, "X"), ldh = ld(H, "H"), ldo = ld(out, "out");
   if (meta(X)) return;
   const c10::DeviceGuard g(X.device());
@@ -409,7 +412,7 @@ void spmm_pair(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
                           (int)reduce_a, p<float>(bias_a), p<float>(bias_nonempty_a),
                           p<int64_t>(indptr_b), p<int32_t>(indices_b), p<float>(ew_b),
                           (int)reduce_b, p<float>(bias_b), p<float>(bias_nonempty_b),
-                          p<float>(X), X.size(0), ldx, p<float>(H), ldh, p<float>(WT4), p<uint16_t>(W3), n_dst, d,
+                          p<float>(X), X.size(0), ldx, p<float>(H), ldh, p<float>(WT4), n_dst, d,
                           (int)epilogue, (int)combine, p<float>(attn_vec), (float)out_div,
                           p<float>(out), ldo, stream_of(X)),
      "gnnrec_spmm_pair_f32");
@@ -513,6 +516,17 @@ void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tenso
 }
 
 // ---------------------------------------------------------------- a9 sampler / relabel
+// excluded_rows flags one byte per destination row (the kernels index it by the seed's global
+// id) and only narrows the exclusion: it means nothing without the eid mask
+void check_excluded_rows(const Tensor& indptr, const optional<Tensor>& excluded,
+                         const optional<Tensor>& excluded_rows) {
+  if (!has(excluded_rows)) return;
+  TORCH_CHECK_VALUE(has(excluded), "excluded_rows given without the excluded eid mask");
+  TORCH_CHECK_VALUE(excluded_rows->numel() >= indptr.numel() - 1,
+                    "excluded_rows must hold one flag per destination row (",
+                    indptr.numel() - 1, "), got ", excluded_rows->numel());
+}
+
 void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tensor>& excluded,
                   const Tensor& seeds, int64_t fanout, int64_t seed_key, Tensor& counts,
                   const optional<Tensor>& excluded_rows) {
@@ -524,6 +538,7 @@ void sample_count(const Tensor& indptr, const Tensor& eids, const optional<Tenso
   dev(seeds, "seeds", at::kLong);
   dev(counts, "counts", at::kLong);
   TORCH_CHECK_VALUE(counts.numel() >= seeds.numel(), "counts shorter than seeds");
+  check_excluded_rows(indptr, excluded, excluded_rows);
   if (meta(seeds)) return;
   const c10::DeviceGuard g(seeds.device());
   ck(gnnrec_sample_count(p<int64_t>(indptr), p<int64_t>(eids), p<uint8_t>(excluded),
@@ -548,6 +563,7 @@ void sample_fill(const Tensor& indptr, const Tensor& indices, const Tensor& eids
   dev(out_src, "out_src", at::kLong);
   dev(out_eid, "out_eid", at::kLong);
   TORCH_CHECK_VALUE(out_indptr.numel() >= seeds.numel() + 1, "out_indptr shorter than seeds + 1");
+  check_excluded_rows(indptr, excluded, excluded_rows);
   if (meta(seeds)) return;
   const c10::DeviceGuard g(seeds.device());
   ck(gnnrec_sample_fill(p<int64_t>(indptr), p<int32_t>(indices), p<int64_t>(eids),
@@ -1822,7 +1838,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("spmm_pair(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, int reduce_a, "
         "Tensor? bias_a, Tensor? bias_nonempty_a, Tensor indptr_b, Tensor indices_b, "
         "Tensor? ew_b, int reduce_b, Tensor? bias_b, Tensor? bias_nonempty_b, Tensor X, "
-        "Tensor H, Tensor? WT4, Tensor? W3, int epilogue, int combine, Tensor? attn_vec, "
+        "Tensor H, Tensor WT4, int epilogue, int combine, Tensor? attn_vec, "
         "float out_div, "
         "Tensor(a!) out) -> ()");
   m.def("sddmm_cos(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor(a!) out) -> ()");

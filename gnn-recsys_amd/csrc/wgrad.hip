@@ -198,19 +198,12 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
   }
 }
 
-// blocks the split-K grid aims for (GNNREC_TN_BLOCKS: tuning knob)
-inline int64_t tn_target_blocks() {
-  static const int64_t b = [] {
-    const char* e = getenv("GNNREC_TN_BLOCKS");
-    const int64_t x = e ? (int64_t)atoll(e) : 0;
-    return x >= 64 && x <= 8192 ? x : (int64_t)kTargetBlocks;
-  }();
-  return b;
-}
+// blocks the split-K grid aims for: kTargetBlocks (1024 / 2048: slower at 200k rows, equal
+// at 1M, profiles/r03e_tn_blocks_ab.txt)
 
 inline int64_t tn_splits(int64_t K, int64_t M, int64_t N) {
   const int64_t tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
-  int64_t s = tn_target_blocks() / (tiles > 0 ? tiles : 1);
+  int64_t s = (int64_t)kTargetBlocks / (tiles > 0 ? tiles : 1);
   // >= 256 rows per split (128 on the 64 x 64 tile: a short gradient — a 1k-row block
   // layer — then spreads over 8 blocks instead of 4 serial 16-step chains)
   const int64_t min_rows = M <= 64 && N <= 64 ? 128 : 256;

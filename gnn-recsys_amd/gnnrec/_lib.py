@@ -90,7 +90,7 @@ SIGNATURES = {
                                         _P, _P, _I64, _P, _P, _P, _P, _I64, _I64, _INT, _INT,
                                         _P, _F32, _P, _I64, _P]),
     "gnnrec_spmm_pair_f32": (_INT, [_P, _P, _P, _INT, _P, _P, _P, _P, _P, _INT, _P, _P, _P, _I64,
-                                    _I64, _P, _I64, _P, _P, _I64, _I64, _INT, _INT, _P, _F32,
+                                    _I64, _P, _I64, _P, _I64, _I64, _INT, _INT, _P, _F32,
                                     _P, _I64, _P]),
     "gnnrec_gather_rows": (_INT, [_P, _I64, _P, _I64, _I64, _P, _I64, _P]),
     "gnnrec_gather_rows_batch": (_INT, [_P, _INT, _P]),

@@ -107,8 +107,6 @@ def _planned(indptr: torch.Tensor, split: int = ops.DEFAULT_SPLIT) -> torch.Tens
 # deterministic tree stays bitwise P-invariant.
 TILE_SPLIT = 512
 
-_SCRATCH = os.environ.get("GNNREC_SCRATCH", "1") != "0"  # reuse scratch tables across passes
-
 
 class GraphShard:
     """This rank's share of a heterograph for the sharded full-graph pass."""
@@ -405,8 +403,6 @@ class ShardedFullGraphPass:
         the exchange, which the owner's GEMM waits for, before the next layer's tiles write
         it; an aggregate is read by the side-stream GEMM whose output the next layer waits
         for before it reaches the same relation."""
-        if not _SCRATCH:
-            return torch.empty(shape, dtype=torch.float32, device=device)
         t = self._pool.get(key)
         if t is None or tuple(t.shape) != tuple(shape) or t.device != torch.device(device):
             t = torch.empty(shape, dtype=torch.float32, device=device)
@@ -744,8 +740,7 @@ class ShardedFullGraphPass:
                                       accumulate=True, split=TILE_SPLIT)
         out = {}
         for ce, rs, msg, weighted, reduce in rels:
-            if not multi_rank(self.ex) and self._owned_side and \
-                    os.environ.get("GNNREC_TREE_SIDE", "1") != "0":
+            if not multi_rank(self.ex) and self._owned_side:
                 # one rank, owner work on the side stream: the whole tree is folded there
                 # (_owned), off the main stream that runs the pair launch's inputs next
                 out[ce] = (parts[ce], None, reduce, 'tree_local')
@@ -760,8 +755,7 @@ class ShardedFullGraphPass:
         that gather from the same table with the same segments and no heavy tile rows run as
         one launch per tile (ops.spmm2: C5's clicks and buys); the rest alone.  Each pair's
         partials are bitwise those of separate launches."""
-        pair_ok = getattr(self.ops, 'spmm2', None) is not None and \
-            os.environ.get("GNNREC_TILE_PAIRS", "1") != "0"
+        pair_ok = getattr(self.ops, 'spmm2', None) is not None
         out, used = [], set()
         for i, a in enumerate(rels):
             if i in used:
@@ -812,11 +806,9 @@ class ShardedFullGraphPass:
             avg = (rs.global_edges / max(sh.num_nodes[T], 1)) if self.deterministic else None
             # a pre-projected low-degree relation fuses even beside a side stream: its
             # MFMA runs the self half only (C5 bought-by: 10.6 + 0.4 ms vs 7.6 ms gather +
-            # a 7 ms GEMM contending with the tiles for HBM); GNNREC_PRE_FUSE_PASS=0 keeps
-            # gather + side-stream GEMM there
+            # a 7 ms GEMM contending with the tiles for HBM)
             pre = reduce != 'lstm' and getattr(O, 'preproject_pays', None) is not None and \
-                O.preproject_pays(msg.shape[0], rs.n_rows, reduce) and \
-                os.environ.get("GNNREC_PRE_FUSE_PASS", "1") != "0"
+                O.preproject_pays(msg.shape[0], rs.n_rows, reduce)
             if reduce != 'lstm' and can_fuse is not None and can_fuse(
                     rs.indptr, msg, self_rows, mod.fc_self.weight, mod.fc_neigh.weight,
                     avg_deg=avg, gemm_overlaps=self.side is not None and not pre):
@@ -896,7 +888,7 @@ class ShardedFullGraphPass:
         source table at most half the destination count (C5: clicked-by and bought-by
         from the 1M items into the 10M users): both source tables pre-projected, then one
         spmm_project2 launch reads each user row once and writes it once (C5 user side
-        39.0 ms vs 41.0 ms for the two fused launches).  GNNREC_PAIR_FUSE=0 disables it.
+        39.0 ms vs 41.0 ms for the two fused launches).
         In deterministic mode the decision uses the global user count (same on every
         rank); the HeteroGraphConv combine runs in the kernel (sum, mean as /2, max, the
         attention softmax over the two relations)."""
@@ -959,7 +951,6 @@ class ShardedFullGraphPass:
         sh, O = self.shard, self.ops
         T = sh.ptype
         if getattr(O, 'spmm_project2', None) is None or \
-                os.environ.get("GNNREC_PAIR_FUSE", "1") == "0" or \
                 hconv.aggregate not in ('sum', 'mean', 'max', 'attention'):
             return None
         n_dec = sh.num_nodes[T] if self.deterministic else sh.n_own

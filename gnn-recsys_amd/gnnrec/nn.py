@@ -277,10 +277,8 @@ class HeteroGraphConv(nn.Module):
         """Inference, exactly two relations into one type, both pre-projectable
         (ConvLayer._pre_plan): one launch with the sum / mean / max / attention combine
         inside — ops.spmm_pair when both gather the same raw table, else ops.spmm_project2
-        over the pre-projected tables (the sharded pass's _pair does the same).
-        GNNREC_PAIR_FUSE=0 disables it."""
-        if self.aggregate not in ('sum', 'mean', 'max', 'attention') or \
-                os.environ.get("GNNREC_PAIR_FUSE", "1") == "0":
+        over the pre-projected tables (the sharded pass's _pair does the same)."""
+        if self.aggregate not in ('sum', 'mean', 'max', 'attention'):
             return False
         mods = [self.mods[ce[1]] for ce in ces]
         if bool(mods[0].norm) != bool(mods[1].norm):
@@ -692,8 +690,7 @@ class ConvModel(nn.Module):
                 h = self.embed(h)
         for i in range(start, len(blocks)):
             h = self.layers[i](blocks[i], h)
-        if isinstance(self.pred_fn, CosinePrediction) and \
-                os.environ.get("GNNREC_COS_PAIR", "1") != "0":
+        if isinstance(self.pred_fn, CosinePrediction):
             pos_score, neg_score = self.pred_fn.pair(pos_g, neg_g, h)
         else:
             pos_score = self.pred_fn(pos_g, h)

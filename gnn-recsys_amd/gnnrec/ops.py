@@ -464,14 +464,12 @@ GEMM_ROW_N = 256  # widest output row gnnrec_gemm_f32 normalises / attends in on
 def can_spmm_project(indptr, X, H, W_self, W_neigh, split: Optional[int] = DEFAULT_SPLIT,
                      avg_deg: Optional[float] = None, gemm_overlaps: bool = False) -> bool:
     """True when a fused aggregation+projection kernel applies (shapes, alignment, no
-    heavy rows, GPU tensors; GNNREC_FUSED=0 disables it).  avg_deg: edges per row to judge
+    heavy rows, GPU tensors).  avg_deg: edges per row to judge
     the degree threshold by (default: this CSR's own).  gemm_overlaps: the caller can run
     an unfused projection GEMM on a second stream under other HBM-bound work (the sharded
     pass) — then low-degree CSRs, whose fused kernel is the MFMA one, stay unfused: the
     overlapped GEMM costs less than the MFMA kernel's extra time over the bare gather
     (C5 bought-by: 13.1 ms fused vs 7.6 ms gather + a 7.1 ms GEMM on the side stream)."""
-    if os.environ.get("GNNREC_FUSED", "1") == "0":
-        return False
     D = FUSED_D
     if not ((X.is_cuda or X.is_meta) and (H.is_cuda or H.is_meta) and X.dim() == 2
             and H.dim() == 2):
@@ -514,11 +512,8 @@ def fused_variant(indptr, avg_deg: Optional[float] = None) -> str:
     the gather from FUSED_MIN_DEG edges per row up) or 'mfma' (gnnrec_spmm_project_mfma_f32:
     32-row tiles through fp32 MFMA, weights read once per 32 rows — low degrees).  avg_deg:
     the edges per row to decide by (the sharded pass passes the GLOBAL average so every
-    rank picks the same kernel); default this CSR's own.  GNNREC_FUSED_VARIANT=valu|mfma
-    forces one (tuning, tests)."""
-    forced = os.environ.get("GNNREC_FUSED_VARIANT", "auto")
-    if forced in ("valu", "mfma"):
-        return forced
+    rank picks the same kernel); default this CSR's own (spmm_project's `variant` forces
+    one)."""
     if avg_deg is None:
         n = indptr.numel() - 1
         avg_deg = _nnz(indptr) / n if n else float(FUSED_MIN_DEG)
@@ -598,34 +593,6 @@ def _packed4(Ws_a, Wn_a, Ws_b, Wn_b) -> torch.Tensor:
     if torch.compiler.is_compiling() or not Ws_a.is_cuda:
         return make()
     return _cached_on(Ws_a, "_gnnrec_wt4", tuple(_wkey(W) for W in Ws), make)
-
-
-def _packed_bf16x3(Ws_a, Wn_a, Ws_b, Wn_b) -> torch.Tensor:
-    """The four pair weights as bf16 planes [4, 3, d, d] (gnnrec_spmm_pair_f32's W3): plane 0
-    = bf16(W), 1 = bf16(W - plane 0), 2 = bf16(W - planes 0..1), round to nearest even,
-    so the planes sum to W exactly; n-major (W itself).  Cached on W_self,a like _packed4."""
-    Ws = (Ws_a, Wn_a, Ws_b, Wn_b)
-
-    def make():
-        out = []
-        for W in Ws:
-            x = W.detach().float()
-            hi = x.to(torch.bfloat16)
-            r = x - hi.float()
-            mid = r.to(torch.bfloat16)
-            out.append(torch.stack([hi, mid, (r - mid.float()).to(torch.bfloat16)]))
-        return torch.stack(out).contiguous()
-
-    if torch.compiler.is_compiling() or not Ws_a.is_cuda:
-        return make()
-    return _cached_on(Ws_a, "_gnnrec_w3", tuple(_wkey(W) for W in Ws), make)
-
-
-# Projection arithmetic of the one-table pair launch (GNNREC_PAIR_MFMA: f32 | bf16x3).  bf16x3
-# issues 2.7x fewer MFMA cycles but streams 1.5x the weight bytes per tile, and that stream,
-# not the MFMA, bounds the projection phase: C5's pair launch 38.7 ms (f32) vs 47.3 ms
-# (profiles/r04j_pair_bf16x3_ab.md)
-PAIR_MFMA = os.environ.get("GNNREC_PAIR_MFMA", "f32")
 
 
 def spmm_project(indptr, indices, X, H, W_self, W_neigh, reduce: str = "mean",
@@ -766,16 +733,13 @@ def spmm_project2(rel_a, rel_b, H, W_self_a, W_self_b, bias_a=None, bias_b=None,
 def spmm_pair(rel_a, rel_b, X, H, W_self_a, W_neigh_a, W_self_b, W_neigh_b, bias_a=None,
               bias_b=None, *, relu: bool = True, l2norm: bool = False, combine: str = "add",
               out_div: float = 0.0, out: Optional[torch.Tensor] = None,
-              attn_vec: Optional[torch.Tensor] = None,
-              mfma: Optional[str] = None) -> torch.Tensor:
+              attn_vec: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Two relations gathering from ONE source table X into one destination type, all four
     projections in the launch (gnnrec_spmm_pair_f32, MFMA epilogue): out = combine(
     epi(H W_self_aᵀ + agg_a W_neigh_aᵀ + bias_a [+ bias_nonempty_a]), epi(... b ...)) /
     out_div.  rel_r = (indptr, indices, reduce, edge_weight, bias_nonempty), reduce sum or
     mean; combine as spmm_project2.  Unlike spmm_project2 nothing is pre-projected: the
-    gathered working set is X alone.  mfma (default PAIR_MFMA): 'f32' runs the projections
-    on the fp32 MFMA, 'bf16x3' as six bf16 MFMA products of three-way split operands
-    (fp32-accurate, 2.7x fewer MFMA cycles, 1.5x the weight bytes; _packed_bf16x3)."""
+    gathered working set is X alone; the projections run on the fp32 MFMA."""
     D = FUSED_D
     n_dst = rel_a[0].numel() - 1
     args = []
@@ -820,12 +784,8 @@ def spmm_pair(rel_a, rel_b, X, H, W_self_a, W_neigh_a, W_self_b, W_neigh_b, bias
         _dev(out, "out", torch.float32)
         _rowmajor(out, "out")
     epi = (_lib.EPI_RELU if relu else 0) | (_lib.EPI_L2NORM if l2norm else 0)
-    mfma = mfma or PAIR_MFMA
-    if mfma not in ("bf16x3", "f32"):
-        raise ValueError(f"spmm_pair: mfma must be 'bf16x3' or 'f32', not {mfma!r}")
-    Ws = (W_self_a, W_neigh_a, W_self_b, W_neigh_b)
-    WT4, W3 = (None, _packed_bf16x3(*Ws)) if mfma == "bf16x3" else (_packed4(*Ws), None)
-    _T().spmm_pair(*args, X, H, WT4, W3, epi,
+    WT4 = _packed4(W_self_a, W_neigh_a, W_self_b, W_neigh_b)
+    _T().spmm_pair(*args, X, H, WT4, epi,
                    ACCUM["attn_last" if combine == "attention" else combine], attn_vec,
                    float(out_div), out)
     return out
@@ -835,10 +795,7 @@ def preproject_pays(n_src: int, n_dst: int, reduce: str) -> bool:
     """Project a low-degree relation's source rows ahead of the reduction (spmm_project
     with W_neigh=None) when the reduction is linear and the source type has at most half
     as many rows as the destination: the MFMA then runs the self half only (C5 bought-by,
-    1M items -> 10M users: fused 13.0 -> 10.6 ms + 0.38 ms for the 1M-row projection).
-    GNNREC_PREPROJECT=0 disables it."""
-    if os.environ.get("GNNREC_PREPROJECT", "1") == "0":
-        return False
+    1M items -> 10M users: fused 13.0 -> 10.6 ms + 0.38 ms for the 1M-row projection)."""
     return reduce in ("sum", "mean") and 2 * n_src <= n_dst
 
 

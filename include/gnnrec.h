@@ -289,14 +289,9 @@ int gnnrec_spmm_project2_f32(const int64_t* indptr_a, const int32_t* indices_a,
  * agg_r = sum / mean over relation r's in-edges of X[indices_r[e]] (* ew_r[e]), X [n_src, d]
  * with row stride ldx (indices_r < n_src).  WT4 is the
  * packed k-major weight array [W_self_a^T | W_neigh_a^T | W_self_b^T | W_neigh_b^T], four
- * contiguous d x d blocks (block[k][n] = W[n][k]); the projections then run on the fp32
- * MFMA.  Or (WT4 NULL) W3: the same four weights as bf16 planes [4][3][d n][d k]
- * (plane 0 = bf16_rn(W), 1 = bf16_rn(W - plane 0), 2 = bf16_rn(W - planes 0..1), so the
- * three sum to W exactly), 16-B aligned; the projections then run as six bf16 MFMA products
- * per K step on operands split the same way (hi·hi + hi·mid + mid·hi + hi·lo + mid·mid +
- * lo·hi: every dropped product is below 2^-24 |a·b|, fp32-accurate, not bitwise the fp32
- * MFMA's sums).  Exactly one of WT4 / W3.  32-row tiles; the gathered working set is the
- * one table (gnnrec_spmm_project2_f32 gathers two pre-projected ones).
+ * contiguous d x d blocks (block[k][n] = W[n][k]); the projections run on the fp32 MFMA.
+ * 32-row tiles; the gathered working set is the one table (gnnrec_spmm_project2_f32 gathers
+ * two pre-projected ones).
  * combine / attn_vec / out_div / epilogue / d /
  * alignment as gnnrec_spmm_project2_f32; bias_r NULL: none.  Each aggregate has the bits
  * of gnnrec_spmm_csr_f32's; the projection sums k in a fixed order of its own.  Replaces two
@@ -306,7 +301,7 @@ int gnnrec_spmm_pair_f32(const int64_t* indptr_a, const int32_t* indices_a, cons
                          const int64_t* indptr_b, const int32_t* indices_b, const float* ew_b,
                          int reduce_b, const float* bias_b, const float* bias_nonempty_b,
                          const float* X, int64_t n_src, int64_t ldx, const float* H,
-                         int64_t ldh, const float* WT4, const uint16_t* W3, int64_t n_dst,
+                         int64_t ldh, const float* WT4, int64_t n_dst,
                          int64_t d, int epilogue, int combine, const float* attn_vec,
                          float out_div, float* out, int64_t ldo, void* stream);
 

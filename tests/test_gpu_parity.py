@@ -955,15 +955,11 @@ def _combine_ref(rng, zs, combine):
     return zs[0] + zs[1], dict(combine="add")
 
 
-PAIR_MFMA = ("bf16x3", "f32")
-
-
-@pytest.mark.parametrize("mfma", PAIR_MFMA)
 @pytest.mark.parametrize("combine,weighted", [("sum", False), ("mean", False), ("max", True),
                                               ("attention", False), ("sum", True)])
-def test_spmm_pair_one_table_matches_oracle(combine, weighted, mfma):
+def test_spmm_pair_one_table_matches_oracle(combine, weighted):
     """gnnrec_spmm_pair_f32: two relations gathering ONE raw source table, all four
-    projections on the MFMA (fp32, or six bf16 products of split operands), against the
+    projections on the fp32 MFMA, against the
     oracle's two ConvLayers + HeteroGraphConv sum / mean / max / attention (reference
     src/model.py:143-235,384-406): mean and sum reduces, empty rows, a 700-edge row (the
     row-by-row gather past 64 edges), biases on non-empty rows only, a row count that is not
@@ -974,41 +970,14 @@ def test_spmm_pair_one_table_matches_oracle(combine, weighted, mfma):
     X, H, rels, zs, W = _pair_case(rng, 2999, 900, weighted)
     ref, kw = _combine_ref(rng, zs, combine)
     args = (rels[0], rels[1], _t(X), _t(H), W[0][0], W[0][1], W[1][0], W[1][1], W[0][2], W[1][2])
-    out = ops.spmm_pair(*args, relu=True, l2norm=True, mfma=mfma, **kw)
+    out = ops.spmm_pair(*args, relu=True, l2norm=True, **kw)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=RTOL, atol=ATOL)
-    assert torch.equal(out, ops.spmm_pair(*args, relu=True, l2norm=True, mfma=mfma, **kw))
+    assert torch.equal(out, ops.spmm_pair(*args, relu=True, l2norm=True, **kw))
     with pytest.raises(ValueError):
         ops.spmm_pair(rels[0], rels[1][:2] + ("max",) + rels[1][3:], *args[2:])
 
 
-def test_spmm_pair_bf16x3_is_fp32_accurate():
-    """The six-product bf16 form against a float64 projection of the same aggregates: its
-    error is that of an fp32 dot product (the dropped products are below 2^-24 |a·b|), no
-    larger than the fp32 MFMA form's; weights with a wide dynamic range (1e-3 .. 1e3)."""
-    from gnnrec import ops
-    rng = np.random.default_rng(21)
-    X, H, rels, _, _ = _pair_case(rng, 1500, 700, False)
-    rels = [r[:4] + (None,) for r in rels]
-    d = 128
-    Wn = [(rng.standard_normal((d, d)) * 10.0 ** rng.uniform(-3, 3, (d, d))).astype(np.float32)
-          for _ in range(4)]
-    outs = {m: ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), *[_t(w) for w in Wn],
-                             relu=False, l2norm=False, mfma=m).cpu().numpy().astype(np.float64)
-            for m in PAIR_MFMA}
-    aggs = [oracle.spmm_csr(r[0].cpu().numpy(), r[1].cpu().numpy(), X, r[2]).astype(np.float64)
-            for r in rels]
-    H64 = H.astype(np.float64)
-    ref = sum(H64 @ Wn[2 * i].T.astype(np.float64) + aggs[i] @ Wn[2 * i + 1].T.astype(np.float64)
-              for i in range(2))
-    scale = sum(np.abs(H64) @ np.abs(Wn[2 * i].T.astype(np.float64)) +
-                np.abs(aggs[i]) @ np.abs(Wn[2 * i + 1].T.astype(np.float64)) for i in range(2))
-    err = {m: float(np.max(np.abs(o - ref) / scale)) for m, o in outs.items()}
-    assert err["bf16x3"] < 3e-6 and err["f32"] < 3e-6, err
-    assert err["bf16x3"] < 4 * err["f32"] + 1e-7, err
-
-
-@pytest.mark.parametrize("mfma", PAIR_MFMA)
-def test_spmm_pair_row_queue_and_small_grids(mfma):
+def test_spmm_pair_row_queue_and_small_grids():
     """Row counts that take the static walk with fewer blocks than XCDs (40, 200 rows), the
     XCD walk (20k) and the row queue (200k rows: at least 4 tickets per block), with
     degrees around C5's 40 + 10 per row and no norm — every row written once, against the
@@ -1025,25 +994,22 @@ def test_spmm_pair_row_queue_and_small_grids(mfma):
                 b.cpu().numpy() + (np.diff(ipn) > 0)[:, None] * bne.cpu().numpy()
             zs.append(oracle.relu(z))
         out = ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), W[0][0], W[0][1], W[1][0], W[1][1],
-                            W[0][2], W[1][2], relu=True, l2norm=False, mfma=mfma)
+                            W[0][2], W[1][2], relu=True, l2norm=False)
         np.testing.assert_allclose(out.cpu().numpy(), zs[0] + zs[1], rtol=RTOL, atol=ATOL,
                                    err_msg=f"n_dst={n_dst}")
 
 
-@pytest.mark.parametrize("mfma", PAIR_MFMA)
-def test_spmm_pair_aggregates_have_the_plain_kernels_bits(mfma):
+def test_spmm_pair_aggregates_have_the_plain_kernels_bits():
     """With identity projections (W_self = 0, W_neigh = I, no bias, no ReLU/norm) the pair
     kernel's output is agg_a + agg_b: each aggregate must carry spmm_csr's bits (same
-    per-row summation order), so the sum equals the plain kernel's two outputs added (the
-    bf16x3 form too: an aggregate's three pieces sum back to it exactly)."""
+    per-row summation order), so the sum equals the plain kernel's two outputs added."""
     from gnnrec import ops
     rng = np.random.default_rng(8)
     X, H, rels, _, _ = _pair_case(rng, 777, 500, False)
     rels = [r[:4] + (None,) for r in rels]  # no non-empty bias
     I = torch.eye(128, device=DEV)
     Z = torch.zeros(128, 128, device=DEV)
-    out = ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), Z, I, Z, I, relu=False, l2norm=False,
-                        mfma=mfma)
+    out = ops.spmm_pair(rels[0], rels[1], _t(X), _t(H), Z, I, Z, I, relu=False, l2norm=False)
     a = ops.spmm(rels[0][0], rels[0][1], _t(X), rels[0][2])
     b = ops.spmm(rels[1][0], rels[1][1], _t(X), rels[1][2])
     torch.testing.assert_close(out, a + b, rtol=0, atol=0)
