@@ -81,9 +81,13 @@ __device__ __forceinline__ void gather_job(const GatherJobs& J, int j, int64_t t
   const int64_t upr = J.upr[j], total = J.n[j] * upr;
   for (int64_t t = t0; t < total; t += step) {
     const int64_t row = t / upr, u = t - row * upr;
-    const U* s = reinterpret_cast<const U*>(J.src[j] + J.idx[j][row] * J.src_ld[j]) + u;
+    const int64_t r = J.idx[j][row];
     U* d = reinterpret_cast<U*>(J.dst[j] + row * J.dst_ld[j]) + u;
-    *d = *s;
+    if (r < 0) {  // a padding slot of a static-shape block: a zero row
+      *d = U{};
+      continue;
+    }
+    *d = *(reinterpret_cast<const U*>(J.src[j] + r * J.src_ld[j]) + u);
   }
 }
 

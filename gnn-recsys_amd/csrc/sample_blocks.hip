@@ -20,6 +20,15 @@
 //   * sizes stay on the device (`sizes`): step s+1's grids are sized by capacities
 //     (seeds x fanout) and read the actual counts there, so one host read after the call
 //     sizes every block (the per-layer path read back twice per layer).
+//   * static shapes (plan.static_shapes): every block at its capacity, nothing to read back,
+//     so a training step over it can be captured into a hipGraph.  Seed slots holding -1
+//     are padding; each block gets one extra "dump" row per destination type (index
+//     seed_cap): a padding seed's row holds `fanout` padding edges, the dump row the rest of
+//     the edge capacity, every padding edge from the source type's dump node (eid -1).  New
+//     sources start after the dump row, the source list is -1 beyond them, up to node_cap
+//     + 1 entries: the last is the next block's dump row (its index there is its seed
+//     count), so a layer's output rows are the next block's source rows.  Padding only
+//     ever reaches padding rows: the real rows' blocks, local ids aside, are the exact ones.
 #include "common.hpp"
 #include "sampler.hpp"
 
@@ -46,6 +55,7 @@ struct RelArgs {
   int32_t* out_src;
   int64_t* out_eid;
   int64_t* edge_total;  // sizes entry
+  int64_t edge_cap;     // static shapes: the block's edge count (the dump row ends there)
   // exclusion flags set by begin, cleared by the last finalize
   const int64_t* excl_eids;
   int64_t n_excl;
@@ -67,6 +77,9 @@ struct TypeArgs {
   int64_t* nodes;          // this step's source node list (the next step's seeds)
   int64_t* n_nodes_out;    // sizes entry
   int64_t n_seeds_host;    // begin only: the batch's seed count
+  int64_t node_cap;        // static shapes: the source list's length
+  int64_t node_len;        // static shapes: node_cap + 1 (the next block's dump row, -1)
+  int64_t new0;            // static shapes: where the new sources start (seed_cap + 1)
 };
 
 // sections of one launch: block ranges [begin[k], begin[k+1]) run job kind[k] on index idx[k]
@@ -83,7 +96,7 @@ struct Sections {
 };
 
 struct StepArgs {
-  int n_rels, n_types, last;
+  int n_rels, n_types, last, stat;
   uint32_t stamp;
   RelArgs rel[GNNREC_SB_MAX_RELS];
   TypeArgs type[GNNREC_SB_MAX_TYPES];
@@ -92,7 +105,7 @@ struct StepArgs {
 };
 
 enum { kSecSeedPos, kSecZeroBits, kSecExclSet, kSecPick, kSecZeroNext, kSecCompact,
-       kSecNewNodes, kSecPrefix, kSecExclClear };
+       kSecNewNodes, kSecPrefix, kSecExclClear, kSecDumpEdges, kSecPadNodes };
 
 // (stamp << 32) | ~position: the atomicMax of two writes of one stamp keeps the smaller
 // position, and any write of a newer stamp beats every older entry
@@ -118,7 +131,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
   switch (A.sec.kind[k]) {
     case kSecSeedPos: {
       const TypeArgs& T = A.type[i];
-      if (t < T.n_seeds_host) set_pos(T.pos_cur, T.seeds[t], A.stamp, t);
+      if (t < T.n_seeds_host && T.seeds[t] >= 0) set_pos(T.pos_cur, T.seeds[t], A.stamp, t);
       break;
     }
     case kSecZeroBits: {
@@ -157,6 +170,10 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
   const int64_t i = (int64_t)b * (kSbBlock / G) + (threadIdx.x / G);
   if (i >= *D.n_seeds) return;  // group-uniform
   const int64_t v = D.seeds[i];
+  if (v < 0) {  // a padding seed (static shapes): its row holds `fanout` padding edges
+    if (grp.lane == 0) R.counts[i] = R.fanout;
+    return;
+  }
   const int64_t beg = R.indptr[v], end = R.indptr[v + 1], deg = end - beg;
   const uint8_t* const excluded =
       R.excl_mask && (!R.excl_rows || R.excl_rows[v]) ? R.excl_mask : nullptr;
@@ -274,14 +291,16 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
     out[n] = carry;
     if (is_rel) {
       *A.rel[seg].edge_total = carry;
+      if (A.stat) out[n + 1] = A.rel[seg].edge_cap;  // the dump row takes the rest
     } else {
       const TypeArgs& T = A.type[seg - A.n_rels];
-      *T.n_nodes_out = *T.n_seeds + carry;
+      *T.n_nodes_out = A.stat ? T.node_cap : *T.n_seeds + carry;
     }
   }
 }
 
 // ---------------------------------------------------------------- finalize (step s)
+// n_p: where the new sources start (the seed count; static shapes: after the dump row)
 __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint32_t stamp,
                                             int32_t s) {
   const unsigned long long v = T.pos_cur[s];
@@ -302,8 +321,27 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       const int64_t i = t / R.fanout, j = t - i * R.fanout;
       if (i >= *D.n_seeds || j >= R.counts[i]) return;
       const int64_t o = R.out_indptr[i] + j;
-      R.out_src[o] = (int32_t)local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
+      if (D.seeds[i] < 0) {  // a padding seed's padding edge
+        R.out_src[o] = (int32_t)S.seed_cap;
+        R.out_eid[o] = -1;
+        break;
+      }
+      R.out_src[o] = (int32_t)local_id(S, A.stat ? S.new0 : *S.n_seeds, A.stamp, R.pick_src[t]);
       R.out_eid[o] = R.pick_eid[t];
+      break;
+    }
+    case kSecDumpEdges: {  // static shapes: the edge capacity's rest -> the dump row
+      const RelArgs& R = A.rel[x];
+      const int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t;
+      if (e >= R.edge_cap) return;
+      R.out_src[e] = (int32_t)A.type[R.src_t].seed_cap;
+      R.out_eid[e] = -1;
+      break;
+    }
+    case kSecPadNodes: {  // static shapes: the dump node and the list's tail are -1
+      const TypeArgs& T = A.type[x];
+      const int64_t p = t == 0 ? T.seed_cap : T.new0 + T.word_rank[T.words] + t - 1;
+      if (p < T.node_len) T.nodes[p] = -1;
       break;
     }
     case kSecNewNodes: {  // bitmap word t -> its new nodes, ascending, after the seeds
@@ -311,7 +349,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (t >= T.words) return;
       unsigned long long word = T.bits_cur[t];
       if (!word) return;
-      int64_t p = *T.n_seeds + T.word_rank[t];
+      int64_t p = (A.stat ? T.new0 : *T.n_seeds) + T.word_rank[t];
       while (word) {
         const int64_t id = t * 64 + __builtin_ctzll(word);
         T.nodes[p] = id;
@@ -326,7 +364,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (t >= *T.n_seeds) return;
       const int64_t id = T.seeds[t];
       T.nodes[t] = id;
-      set_pos(T.pos_next, id, A.stamp + 1u, t);
+      if (id >= 0) set_pos(T.pos_next, id, A.stamp + 1u, t);
       break;
     }
     case kSecExclClear: {
@@ -336,6 +374,101 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
         R.mask_w[e] = 0;
         R.rows_w[R.coo_dst[e]] = 0;
       }
+      break;
+    }
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------- compact_ids
+struct CompactArgs {
+  int n_lists, n_types;
+  const int64_t* ids[GNNREC_COMPACT_MAX_LISTS];
+  int64_t n[GNNREC_COMPACT_MAX_LISTS];
+  int type[GNNREC_COMPACT_MAX_LISTS];
+  int64_t* local[GNNREC_COMPACT_MAX_LISTS];
+  unsigned long long* bits_cur[GNNREC_SB_MAX_TYPES];
+  unsigned long long* bits_next[GNNREC_SB_MAX_TYPES];
+  int64_t* word_rank[GNNREC_SB_MAX_TYPES];
+  int64_t words[GNNREC_SB_MAX_TYPES];
+  int64_t* nodes[GNNREC_SB_MAX_TYPES];
+  int64_t cap[GNNREC_SB_MAX_TYPES];
+  int64_t* count;
+  Sections sec;
+};
+enum { kCxMark, kCxZero, kCxLocal, kCxNodes, kCxPad };
+
+__global__ __launch_bounds__(kSbBlock) void cx_mark_kernel(CompactArgs A) {
+  const int k = A.sec.find((int)blockIdx.x);
+  const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
+  const int x = A.sec.idx[k];
+  if (A.sec.kind[k] == kCxZero) {
+    if (t < A.words[x]) A.bits_next[x][t] = 0ull;
+    return;
+  }
+  if (t >= A.n[x]) return;
+  const int64_t id = A.ids[x][t];
+  unsigned long long* w = A.bits_cur[A.type[x]] + (id >> 6);
+  const unsigned long long bit = 1ull << (id & 63);
+  if ((*w & bit) == 0ull) __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kScanThreads) void cx_scan_kernel(CompactArgs A) {
+  __shared__ int64_t wsum[kScanThreads / 64];
+  constexpr int kItems = 4;
+  const int t = (int)blockIdx.x;
+  const int64_t n = A.words[t];
+  const unsigned long long* bits = A.bits_cur[t];
+  int64_t* out = A.word_rank[t];
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kItems) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * kItems;
+    int64_t v[kItems], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      v[j] = i0 + j < n ? (int64_t)__popcll(bits[i0 + j]) : 0;
+      sum += v[j];
+    }
+    int64_t tot;
+    int64_t run = carry + block_excl_scan(sum, wsum, &tot);
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      if (i0 + j < n) out[i0 + j] = run;
+      run += v[j];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    out[n] = carry;
+    A.count[t] = carry;
+  }
+}
+
+__global__ __launch_bounds__(kSbBlock) void cx_finalize_kernel(CompactArgs A) {
+  const int k = A.sec.find((int)blockIdx.x);
+  const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
+  const int x = A.sec.idx[k];
+  switch (A.sec.kind[k]) {
+    case kCxLocal: {
+      if (t >= A.n[x]) return;
+      const int ty = A.type[x];
+      const int64_t id = A.ids[x][t], w = id >> 6;
+      A.local[x][t] = A.word_rank[ty][w] + __popcll(A.bits_cur[ty][w] & ((1ull << (id & 63)) - 1ull));
+      break;
+    }
+    case kCxNodes: {
+      if (t >= A.words[x]) return;
+      unsigned long long word = A.bits_cur[x][t];
+      int64_t p = A.word_rank[x][t];
+      while (word && p < A.cap[x]) {
+        A.nodes[x][p++] = t * 64 + __builtin_ctzll(word);
+        word &= word - 1ull;
+      }
+      break;
+    }
+    case kCxPad: {
+      const int64_t p = A.word_rank[x][A.words[x]] + t;
+      if (p < A.cap[x]) A.nodes[x][p] = -1;
       break;
     }
     default: break;
@@ -389,7 +522,8 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
       int64_t e = 0;
       for (int r = 0; r < P->n_rels; ++r)
         if (P->rel[r].src_type == t) e += C->edge[s][r];
-      C->node[s][t] = C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
+      C->node[s][t] = C->seed[s][t] + (P->static_shapes ? 1 : 0) +
+                      std::min<int64_t>(e, P->type[t].n_nodes);
       if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
     }
   }
@@ -469,6 +603,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     A.n_rels = R;
     A.n_types = T;
     A.last = s == L - 1;
+    A.stat = P->static_shapes ? 1 : 0;
     A.stamp = P->stamp + (uint32_t)s;
     A.sizes_seed_row = node_count;
     for (int t = 0; t < T; ++t) {
@@ -488,6 +623,9 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.words = W;
       a.nodes = P->nodes[s][t];
       a.n_nodes_out = node_count + (int64_t)(s + 1) * T + t;
+      a.node_cap = C.node[s][t];
+      a.node_len = C.node[s][t] + 1;
+      a.new0 = C.seed[s][t] + 1;
     }
     for (int r = 0; r < R; ++r) {
       const gnnrec_sample_rel& re = P->rel[r];
@@ -508,6 +646,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.out_src = P->out_src[s][r];
       a.out_eid = P->out_eid[s][r];
       a.edge_total = edge_count + (int64_t)s * R + r;
+      a.edge_cap = C.edge[s][r];
       a.excl_eids = re.excl_eids;
       a.n_excl = re.n_excl;
       a.coo_dst = re.coo_dst;
@@ -569,11 +708,80 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     for (int t = 0; t < T; ++t) add_sec(A.sec, kSecPrefix, t, nblocks(C.seed[s][t]));
     if (s == L - 1)
       for (int r = 0; r < R; ++r) add_sec(A.sec, kSecExclClear, r, nblocks(P->rel[r].n_excl));
+    if (P->static_shapes) {
+      for (int r = 0; r < R; ++r) add_sec(A.sec, kSecDumpEdges, r, nblocks(C.edge[s][r]));
+      for (int t = 0; t < T; ++t)
+        add_sec(A.sec, kSecPadNodes, t, nblocks(C.node[s][t] + 1 - C.seed[s][t]));
+    }
     if (A.sec.n) {
       hipLaunchKernelGGL(sb_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock),
                          0, hs, A);
       if (int st = check_launch("gnnrec_sample_blocks(finalize)")) return st;
     }
+  }
+  return GNNREC_OK;
+}
+
+extern "C" int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
+                                  const gnnrec_compact_type* types, int n_types, int parity,
+                                  int64_t* count, void* stream) {
+  GNNREC_REQUIRE(n_lists >= 0 && n_lists <= GNNREC_COMPACT_MAX_LISTS && n_types >= 1 &&
+                     n_types <= GNNREC_SB_MAX_TYPES,
+                 "gnnrec_compact_ids: %d lists (<= %d), %d types (1..%d)", n_lists,
+                 GNNREC_COMPACT_MAX_LISTS, n_types, GNNREC_SB_MAX_TYPES);
+  GNNREC_REQUIRE((parity == 0 || parity == 1) && count, "gnnrec_compact_ids: parity / count");
+  CompactArgs A{};
+  A.n_lists = n_lists;
+  A.n_types = n_types;
+  A.count = count;
+  for (int t = 0; t < n_types; ++t) {
+    const gnnrec_compact_type& ty = types[t];
+    GNNREC_REQUIRE(ty.n_nodes >= 0 && ty.cap >= 0 && ty.bits && ty.word_rank && (ty.cap == 0 || ty.nodes),
+                   "gnnrec_compact_ids: type %d: sizes / null scratch", t);
+    const int64_t W = words_of(ty.n_nodes);
+    A.bits_cur[t] = reinterpret_cast<unsigned long long*>(ty.bits) + parity * W;
+    A.bits_next[t] = reinterpret_cast<unsigned long long*>(ty.bits) + (1 - parity) * W;
+    A.word_rank[t] = ty.word_rank;
+    A.words[t] = W;
+    A.nodes[t] = ty.nodes;
+    A.cap[t] = ty.cap;
+  }
+  for (int l = 0; l < n_lists; ++l) {
+    const gnnrec_compact_list& li = lists[l];
+    GNNREC_REQUIRE(li.n >= 0 && li.type >= 0 && li.type < n_types && (li.n == 0 || (li.ids && li.local)),
+                   "gnnrec_compact_ids: list %d: size / type / null pointer", l);
+    A.ids[l] = li.ids;
+    A.n[l] = li.n;
+    A.type[l] = li.type;
+    A.local[l] = li.local;
+  }
+  auto add_sec = [](Sections& S, int kind, int idx, int blocks) {
+    if (blocks <= 0) return;
+    S.kind[S.n] = kind;
+    S.idx[S.n] = idx;
+    S.begin[S.n + 1] = S.begin[S.n] + blocks;
+    ++S.n;
+  };
+  hipStream_t hs = as_stream(stream);
+  A.sec.n = 0;
+  A.sec.begin[0] = 0;
+  for (int l = 0; l < n_lists; ++l) add_sec(A.sec, kCxMark, l, nblocks(A.n[l]));
+  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxZero, t, nblocks(A.words[t]));
+  if (A.sec.n) {
+    hipLaunchKernelGGL(cx_mark_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0, hs, A);
+    if (int st = check_launch("gnnrec_compact_ids(mark)")) return st;
+  }
+  hipLaunchKernelGGL(cx_scan_kernel, dim3((unsigned)n_types), dim3(kScanThreads), 0, hs, A);
+  if (int st = check_launch("gnnrec_compact_ids(scan)")) return st;
+  A.sec.n = 0;
+  A.sec.begin[0] = 0;
+  for (int l = 0; l < n_lists; ++l) add_sec(A.sec, kCxLocal, l, nblocks(A.n[l]));
+  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxNodes, t, nblocks(A.words[t]));
+  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxPad, t, nblocks(A.cap[t]));
+  if (A.sec.n) {
+    hipLaunchKernelGGL(cx_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0,
+                       hs, A);
+    if (int st = check_launch("gnnrec_compact_ids(finalize)")) return st;
   }
   return GNNREC_OK;
 }

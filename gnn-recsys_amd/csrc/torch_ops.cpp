@@ -837,17 +837,19 @@ Tensor row_degrees(const Tensor& indptr) {
   return (indptr.narrow(0, 1, M) - indptr.narrow(0, 0, M)).to(at::kInt).contiguous();
 }
 
-// sum gather of X over a CSR whose edge count is known on the host but whose degrees are
-// not (the transposed block): heavy rows planned on the device, as ops.spmm does
+// gather of X over a CSR whose edge count is known on the host but whose degrees are
+// not (the transposed block, a static-shape block's dump row): heavy rows planned on the
+// device, as ops.spmm does
 void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const Tensor& X,
-                    int64_t nnz, Tensor& out, bool accumulate = false) {
+                    int64_t nnz, Tensor& out, bool accumulate = false,
+                    int reduce = GNNREC_REDUCE_SUM) {
   const int64_t n = ip.numel() - 1, d = X.size(1);
   const int64_t cap_h = std::min<int64_t>(n, nnz / (kSplit + 1));
   void* s = stream_of(X);
   const int flags = accumulate ? GNNREC_SPMM_ACCUM : 0;
   if (cap_h <= 0) {
     ck(gnnrec_spmm_csr_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X), ld(X, "X"), n, d,
-                           GNNREC_REDUCE_SUM, flags, p<float>(out), ld(out, "out"), s),
+                           reduce, flags, p<float>(out), ld(out, "out"), s),
        "gnnrec_spmm_csr_f32");
     return;
   }
@@ -857,7 +859,7 @@ void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const T
      "gnnrec_spmm_plan_build");
   Tensor wsp = at::empty({cap_c, d}, X.options());
   ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),
-                                 ld(X, "X"), n, d, GNNREC_REDUCE_SUM, flags, p<float>(out),
+                                 ld(X, "X"), n, d, reduce, flags, p<float>(out),
                                  ld(out, "out"), kSplit, p<int64_t>(plan), cap_h, cap_c,
                                  p<float>(wsp), s),
      "gnnrec_spmm_csr_planned_f32");
@@ -870,7 +872,8 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                                                     const Tensor& indices,
                                                     const optional<Tensor>& ew, int64_t reduce,
                                                     bool norm, const optional<Tensor>& bias,
-                                                    const optional<Tensor>& bias_ne) {
+                                                    const optional<Tensor>& bias_ne,
+                                                    int64_t heavy_nnz) {
   const OneDevice one_device_;
   dev(m, "m", at::kFloat);
   dev(h_self, "h_self", at::kFloat);
@@ -903,10 +906,16 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
   Tensor nrm = norm ? at::empty({M}, m.options()) : at::empty({0}, m.options());
   if (meta(m)) return {z, agg, nrm};
   const c10::DeviceGuard g(m.device());
-  ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), p<float>(X),
-                         ld(X, "m"), M, X.size(1), (int)reduce, 0, p<float>(agg), ld(agg, "agg"),
-                         stream_of(m)),
-     "gnnrec_spmm_csr_f32");
+  if (heavy_nnz > 0) {  // rows of any length (a static block's dump row): planned on the device
+    TORCH_CHECK_VALUE(indices.numel() >= heavy_nnz, "sage_rel_forward: heavy_nnz > edges");
+    const Tensor w = has(ewc) ? *ewc : Tensor();
+    gather_planned(indptr, indices, w, X, heavy_nnz, agg, false, (int)reduce);
+  } else {
+    ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), p<float>(X),
+                           ld(X, "m"), M, X.size(1), (int)reduce, 0, p<float>(agg),
+                           ld(agg, "agg"), stream_of(m)),
+       "gnnrec_spmm_csr_f32");
+  }
   const Tensor deg = bnc.defined() ? row_degrees(indptr) : Tensor();
   gemm_nt(H, Wsc, &agg, &Wnc, GNNREC_EPI_RELU | (norm ? GNNREC_EPI_L2NORM : 0), z,
           norm ? &nrm : nullptr, GNNREC_ACC_STORE, bc.defined() ? p<float>(bc) : nullptr,
@@ -1519,7 +1528,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               const c10::List<optional<Tensor>>& excl_rows, at::IntArrayRef n_nodes,
               at::TensorList seeds, at::TensorList pos, at::TensorList bits,
               at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
-              int64_t steps, int64_t stamp) {
+              int64_t steps, int64_t stamp, bool static_shapes) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = n_nodes.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
@@ -1541,6 +1550,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   P.n_types = (int)NT;
   P.n_steps = (int)steps;
   P.stamp = (uint32_t)stamp;
+  P.static_shapes = static_shapes ? 1 : 0;
   for (size_t r = 0; r < R; ++r) {
     dev(indptrs[r], "indptr", at::kLong);
     dev(indices[r], "indices", at::kInt);
@@ -1614,7 +1624,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     for (size_t r = 0; r < R; ++r) {
       const int64_t sc = seed_cap[s * GNNREC_SB_MAX_TYPES + dst_type[r]];
       const int64_t ec = edge_cap[s * GNNREC_SB_MAX_RELS + r];
-      o_ip[s * R + r] = at::empty({sc + 1}, i64);
+      o_ip[s * R + r] = at::empty({sc + (static_shapes ? 2 : 1)}, i64);
       o_src[s * R + r] = at::empty({ec}, i64.dtype(at::kInt));
       o_eid[s * R + r] = at::empty({ec}, i64);
       P.out_indptr[s][r] = p<int64_t>(o_ip[s * R + r]);
@@ -1622,7 +1632,8 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
       P.out_eid[s][r] = p<int64_t>(o_eid[s * R + r]);
     }
     for (size_t t = 0; t < NT; ++t) {
-      nodes[s * NT + t] = at::empty({node_cap[s * GNNREC_SB_MAX_TYPES + t]}, i64);
+      nodes[s * NT + t] =
+          at::empty({node_cap[s * GNNREC_SB_MAX_TYPES + t] + (static_shapes ? 1 : 0)}, i64);
       P.nodes[s][t] = p<int64_t>(nodes[s * NT + t]);
     }
   }
@@ -1632,6 +1643,15 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   P.sizes = p<int64_t>(sizes);
   P.workspace = ws.data_ptr();
   ck(gnnrec_sample_blocks(&P, stream_of(pos[0])), "gnnrec_sample_blocks");
+  if (static_shapes) {  // every output at its capacity: the sizes are the capacities
+    std::vector<int64_t> caps;
+    for (size_t t = 0; t < NT; ++t) caps.push_back(seed_cap[t]);
+    for (int64_t s = 0; s < steps; ++s)
+      for (size_t t = 0; t < NT; ++t) caps.push_back(node_cap[s * GNNREC_SB_MAX_TYPES + t]);
+    for (int64_t s = 0; s < steps; ++s)
+      for (size_t r = 0; r < R; ++r) caps.push_back(edge_cap[s * GNNREC_SB_MAX_RELS + r]);
+    return {o_ip, o_src, o_eid, nodes, caps};
+  }
   const Tensor hs = sizes.to(at::kCPU);  // the call's one size readback
   const int64_t* h = hs.data_ptr<int64_t>();
   std::vector<int64_t> out_sizes(h, h + n_sizes);
@@ -1682,6 +1702,53 @@ void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList ou
   if (n == 0 || meta(src[0])) return;
   const c10::DeviceGuard g(src[0].device());
   ck(gnnrec_gather_rows_batch(jobs.data(), (int)n, stream_of(src[0])), "gnnrec_gather_rows_batch");
+}
+
+// a11: compact_graphs over id lists at static shapes (gnnrec_compact_ids): per node type the
+// sorted distinct ids of its lists in nodes[t] [caps[t]] (-1 past the count), each list
+// relabelled to local ids, the per-type counts left on the device — no host read, so a
+// loader feeding a captured step keeps every shape fixed.  bits [2 ceil(n/64)] and
+// word_rank [ceil(n/64) + 1] per type; bits zero before the first call, parity alternating.
+std::tuple<std::vector<Tensor>, std::vector<Tensor>, Tensor>
+compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
+            at::IntArrayRef caps, at::TensorList bits, at::TensorList word_rank, int64_t parity) {
+  const OneDevice one_device_;
+  const size_t L = ids.size(), NT = n_nodes.size();
+  TORCH_CHECK_VALUE(type.size() == L && L <= GNNREC_COMPACT_MAX_LISTS && NT >= 1 &&
+                        NT <= GNNREC_SB_MAX_TYPES && caps.size() == NT && bits.size() == NT &&
+                        word_rank.size() == NT,
+                    "compact_ids: at most ", GNNREC_COMPACT_MAX_LISTS, " lists (one type each) "
+                    "and 1..", GNNREC_SB_MAX_TYPES, " types (a cap and a scratch pair each)");
+  TORCH_CHECK_VALUE(parity == 0 || parity == 1, "compact_ids: parity is 0 or 1");
+  gnnrec_compact_type T[GNNREC_SB_MAX_TYPES] = {};
+  gnnrec_compact_list Ls[GNNREC_COMPACT_MAX_LISTS] = {};
+  const c10::DeviceGuard g(bits[0].device());
+  const auto i64 = bits[0].options();
+  std::vector<Tensor> nodes(NT), local(L);
+  for (size_t t = 0; t < NT; ++t) {
+    dev(bits[t], "bits", at::kLong);
+    dev(word_rank[t], "word_rank", at::kLong);
+    const int64_t W = (n_nodes[t] + 63) / 64;
+    TORCH_CHECK_VALUE(n_nodes[t] >= 0 && caps[t] >= 0 && bits[t].numel() == 2 * W &&
+                          word_rank[t].numel() == W + 1,
+                      "compact_ids: type ", t, ": scratch sized 2 ceil(n/64), ceil(n/64)+1");
+    nodes[t] = at::empty({caps[t]}, i64);
+    T[t] = gnnrec_compact_type{n_nodes[t], p<uint64_t>(bits[t]), p<int64_t>(word_rank[t]),
+                               p<int64_t>(nodes[t]), caps[t]};
+  }
+  for (size_t l = 0; l < L; ++l) {
+    dev(ids[l], "ids", at::kLong);
+    TORCH_CHECK_VALUE(type[l] >= 0 && (size_t)type[l] < NT && ids[l].is_contiguous(),
+                      "compact_ids: list ", l, ": type out of range or ids not contiguous");
+    local[l] = at::empty({ids[l].numel()}, i64);
+    Ls[l] = gnnrec_compact_list{p<int64_t>(ids[l]), ids[l].numel(), (int32_t)type[l],
+                                p<int64_t>(local[l])};
+  }
+  Tensor count = at::empty({(int64_t)NT}, i64);
+  ck(gnnrec_compact_ids(Ls, (int)L, T, (int)NT, (int)parity, p<int64_t>(count),
+                        stream_of(bits[0])),
+     "gnnrec_compact_ids");
+  return {nodes, local, count};
 }
 
 // EdgeDataLoader's batch head in one call (gnnrec/sampling.py _iter_batches): the batch's
@@ -1891,7 +1958,7 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor(a!) out) -> ()");
   m.def("sage_rel_forward(Tensor m, Tensor h_self, int n_self, Tensor W_self, Tensor W_neigh, "
         "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm, "
-        "Tensor? bias=None, Tensor? bias_nonempty=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor? bias=None, Tensor? bias_nonempty=None, int heavy_nnz=0) -> (Tensor, Tensor, Tensor)");
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
         "int reduce, int n_src, int nnz, bool norm, int need, Tensor? indptr_t=None, "
@@ -1917,9 +1984,11 @@ TORCH_LIBRARY(gnnrec, m) {
         "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
         "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
         "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
-        "int stamp) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
+        "int stamp, bool static_shapes=False) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
         "Tensor[] src_nid, int[] sizes)");
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out) -> ()");
+  m.def("compact_ids(Tensor[] ids, int[] type, int[] n_nodes, int[] caps, Tensor(a!)[] bits, "
+        "Tensor(b!)[] word_rank, int parity) -> (Tensor[] nodes, Tensor[] local, Tensor count)");
   // host-only entry points (no tensors: one catch-all kernel each)
   m.def("version() -> int", &version);
   m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);
@@ -1991,6 +2060,7 @@ TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) {
   m.impl("sample_layer", &sample_layer);  // data-dependent sizes: device only, no meta form
   m.impl("edge_batch_pairs", &edge_batch_pairs);
   m.impl("sample_blocks", &sample_blocks);
+  m.impl("compact_ids", &compact_ids);
 }
 // Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
 TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }

@@ -97,6 +97,8 @@ SIGNATURES = {
     # (plan*, seed_cap*, edge_cap*, node_cap*, workspace_bytes*) / (plan*, stream)
     "gnnrec_sample_blocks_caps": (_INT, [_P, _P, _P, _P, _P]),
     "gnnrec_sample_blocks": (_INT, [_P, _P]),
+    # (lists*, n_lists, types*, n_types, parity, count*, stream)
+    "gnnrec_compact_ids": (_INT, [_P, _INT, _P, _INT, _INT, _P, _P]),
     "gnnrec_csr_transpose_workspace_bytes": (_U64, [_I64, _I64]),
     "gnnrec_csr_transpose": (_INT, [_P, _P, _P, _I64, _I64, _I64, _INT, _P, _U64, _P, _P, _P, _P]),
     "gnnrec_csr_from_keys_workspace_bytes": (_U64, [_I64, _I64]),

@@ -177,6 +177,13 @@ class SageProjectFn(torch.autograd.Function):
         return g_self, g_agg, g_Ws, g_Wn, None, None
 
 
+def _heavy_nnz(indptr) -> int:
+    """A static-shape block's CSR (sampling, static_shapes=True) may hold rows of any length
+    (the dump row): its edge count, so the forward gather plans heavy rows on the device;
+    0 for the sampler's bounded-degree blocks."""
+    return int(getattr(indptr, "_gnnrec_heavy", 0))
+
+
 class SageRelFn(torch.autograd.Function):
     """One sum / mean ConvLayer relation of a training step — SpmmFn and SageProjectFn as
     ONE autograd node whose forward and backward are each ONE dispatcher call
@@ -192,7 +199,7 @@ class SageRelFn(torch.autograd.Function):
                 n_self: int = 0, transposed=None):
         z, agg, nrm = ops._T().sage_rel_forward(m, h_self, n_self, Ws.detach(), Wn.detach(),
                                                 indptr, indices, ew, ops.REDUCE[reduce],
-                                                bool(norm))
+                                                bool(norm), None, None, _heavy_nnz(indptr))
         ctx.save_for_backward(h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew)
         ctx.reduce, ctx.norm, ctx.n_src = reduce, bool(norm), m.shape[0]
         ctx.nnz = ops._nnz(indptr)  # sampled blocks carry it: no readback
@@ -254,7 +261,7 @@ class HeteroSageFn(torch.autograd.Function):
             z, agg, nrm = T.sage_rel_forward(
                 m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip, ix, ew, ops.REDUCE[reduce],
                 bool(norm), None if b is None else b.detach(),
-                None if bne is None else bne.detach())
+                None if bne is None else bne.detach(), _heavy_nnz(ip))
             zs.append(z)
             saved += [agg, z, nrm]
         outs = []

@@ -1,0 +1,104 @@
+"""A training step captured once into a hipGraph and replayed per batch (SURVEY §8f row f2,
+the reference's train loop src/train/run.py:104-160 — forward, max_margin_loss, backward,
+optimizer step — per EdgeDataLoader batch).
+
+The batches come from EdgeDataLoader(static_shapes=True): every full batch has the same
+shapes and nothing in the step reads a value back to the host, so the whole step — some
+hundreds of kernels, each a few microseconds, whose launches bound the eager step on the
+host — is recorded once and re-issued by one hipGraphLaunch.  Per batch the step copies the
+batch's tensors into the captured batch's buffers (one torch._foreach_copy_) and replays.
+
+    step = CapturedTrainStep(model, opt, lambda m, b: loss_of(m, b))
+    for batch in loader:            # loader = EdgeDataLoader(..., static_shapes=True)
+        loss = step(batch)          # a device scalar; read it when needed
+
+Eager steps: the first `warmup` static batches (lazy initialisation, the model's and the
+sampler's settled choices, e.g. the first-layer fold), and every batch whose structure
+differs from the captured one (a final partial batch comes in the exact, non-static form).
+The optimizer must keep its step counts on the device (Adam / AdamW with fused=True or
+capturable=True); its param groups are switched to capturable at capture.  Between steps
+the gradients live in the graph's memory: do not zero or replace them (the graph overwrites
+them every replay, as the eager step's zero_grad + backward would).
+"""
+from __future__ import annotations
+
+import torch
+
+from .sampling import _tensors
+
+
+def batch_is_static(batch) -> bool:
+    """A loader item of EdgeDataLoader(static_shapes=True) at fixed shapes."""
+    return any(getattr(x, "static", False) for x in batch[1:-1]) and \
+        all(getattr(b, "static", False) for b in batch[-1])
+
+
+def _signature(tensors):
+    return tuple((tuple(t.shape), t.dtype, t.stride(), t.device) for t in tensors)
+
+
+class CapturedTrainStep:
+    """loss_fn(model, batch) -> scalar loss: the step's forward (model + loss)."""
+
+    def __init__(self, model, optimizer, loss_fn, warmup: int = 2):
+        self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
+        self.warmup = int(warmup)
+        self.graph = None
+        self.loss = None
+        self._batch = None   # the captured batch: its tensors are the graph's inputs
+        self._inputs = None
+        self._sig = None
+        self.seen = 0
+        self.replays = 0
+        self.eager_steps = 0
+
+    def eager(self, batch):
+        """One ordinary step (the form the graph records)."""
+        self.eager_steps += 1
+        loss = self.loss_fn(self.model, batch)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss
+
+    def _capturable(self):
+        for group in self.opt.param_groups:
+            if "capturable" not in group:
+                raise TypeError(f"{type(self.opt).__name__}: no capturable mode to replay in a "
+                                "graph (use Adam / AdamW with fused=True or capturable=True)")
+            group["capturable"] = True
+            for p in group["params"]:
+                st = self.opt.state.get(p, {})
+                step = st.get("step")
+                if torch.is_tensor(step) and step.device != p.device:
+                    st["step"] = step.to(p.device)
+
+    def _capture(self, batch, inputs):
+        self._capturable()
+        # the step's own ops run at least once outside the capture on this batch's shapes
+        # (the warm-up steps), so every lazy allocation / library init has happened
+        self.opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            loss = self.loss_fn(self.model, batch)
+            loss.backward()
+            self.opt.step()
+        self.graph, self.loss = g, loss
+        self._batch, self._inputs, self._sig = batch, inputs, _signature(inputs)
+
+    def __call__(self, batch):
+        if not batch_is_static(batch):
+            return self.eager(batch)
+        self.seen += 1
+        if self.seen <= self.warmup:
+            return self.eager(batch)
+        inputs = [t for t in _tensors(batch, []) if t.is_cuda]
+        if self.graph is None:
+            self._capture(batch, inputs)  # records only: the replay below runs the step
+        elif _signature(inputs) != self._sig:
+            return self.eager(batch)
+        else:
+            torch._foreach_copy_(self._inputs, inputs)
+        self.graph.replay()
+        self.replays += 1
+        return self.loss

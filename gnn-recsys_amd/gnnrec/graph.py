@@ -332,6 +332,7 @@ class Block:
     """A sampled computation block (DGL to_block output, restated)."""
 
     is_block = True
+    static = False  # fixed-capacity block (BlockSampler static shapes): -1-padded rows
 
     def __init__(self, src_nid: Dict[str, torch.Tensor], num_dst: Dict[str, int],
                  rels: Dict[CEType, Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]):
@@ -395,6 +396,8 @@ class PairGraph:
     """pos_g / neg_g: edges over compacted seed nodes (DGL compact_graphs output)."""
 
     is_block = False
+    static = False      # node lists at a fixed capacity, -1 past the real nodes
+    node_counts = None  # static: the real node count per type (device scalars)
 
     def __init__(self, edges: Dict[CEType, Tuple[torch.Tensor, torch.Tensor]],
                  node_ids: Dict[str, torch.Tensor]):

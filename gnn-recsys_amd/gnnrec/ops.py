@@ -556,6 +556,10 @@ def _cached_on(W: torch.Tensor, attr: str, key, make):
     another stream than the one that made it, the consumer first waits for its making and
     the copy is record_stream-ed there (so replacing it never frees memory a side-stream
     kernel is still reading)."""
+    if torch.cuda.is_current_stream_capturing():
+        # inside a captured step (gnnrec.capture): the copy is made by the graph on every
+        # replay, after the captured optimizer step changed W — never a stale cached one
+        return make()
     hit = getattr(W, attr, None)
     cur = torch.cuda.current_stream(W.device)
     if hit is None or hit[0] != key:
@@ -1254,12 +1258,14 @@ class SampleScratch:
 
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
-                  fanouts, keys, stamp):
+                  fanouts, keys, stamp, static_shapes=False):
     """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
     1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
     output block); excl: per relation None or (eids, coo_dst, mask, rows).
     -> per step: ([out_indptr], [local src int32], [eids]) per relation, [src node ids] per
-    type, and the sizes (node counts rows -1..L-1 x types, then edge counts)."""
+    type, and the sizes (node counts rows -1..L-1 x types, then edge counts).
+    static_shapes: every output at its capacity, no host read (the -1-padded layout of
+    include/gnnrec.h); the sizes are then the capacities (seed caps, node caps, edge caps)."""
     steps, R = len(fanouts), len(indptrs)
     ex = [e if e is not None else (None,) * 4 for e in excl]
     o_ip, o_src, o_eid, nodes, sizes = _T().sample_blocks(
@@ -1267,13 +1273,41 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
         [e[0] for e in ex], [e[1] for e in ex], [e[2] for e in ex], [e[3] for e in ex],
         list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
         [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
-        [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp))
+        [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes))
     NT = len(n_nodes)
     out = []
     for s in range(steps):
         out.append(([o_ip[s * R + r] for r in range(R)], [o_src[s * R + r] for r in range(R)],
                     [o_eid[s * R + r] for r in range(R)], [nodes[s * NT + t] for t in range(NT)]))
     return out, sizes
+
+
+class CompactScratch:
+    """Per-node-type scratch of compact_ids: two id bitmaps used alternately (the call marks
+    one and zeroes the other) and their word ranks."""
+
+    def __init__(self, n_nodes: int, device):
+        w = (n_nodes + 63) // 64
+        self.n_nodes = n_nodes
+        self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
+        self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
+        self.parity = 0
+
+
+def compact_ids(lists, scratch, caps):
+    """a11, DGL's compact_graphs over id lists at static shapes (gnnrec::compact_ids, 3
+    launches, no host read): lists = [(ids int64, type index)]; scratch / caps per type.
+    -> ([nodes [cap] per type: ascending ids, -1 past the count], [local ids per list],
+    count [types] on the device)."""
+    for ids, _ in lists:
+        _dev(ids, "ids", torch.int64)
+    parity = scratch[0].parity
+    out = _T().compact_ids([ids.contiguous() for ids, _ in lists], [int(t) for _, t in lists],
+                           [s.n_nodes for s in scratch], [int(c) for c in caps],
+                           [s.bits for s in scratch], [s.word_rank for s in scratch], parity)
+    for s in scratch:
+        s.parity = 1 - parity
+    return out
 
 
 def gather_rows_batch(jobs):

@@ -113,9 +113,14 @@ class BlockSampler:
         return all(0 <= self._fanout(b, ce) <= ops.SB_MAX_FANOUT
                    for b in range(self.num_layers) for ce in ces)
 
-    def _sample_fused(self, g, seeds, exclude_eids, transposes):
+    def _sample_fused(self, g, seeds, exclude_eids, transposes, static=False):
         """sample_blocks through gnnrec_sample_blocks: 1 + 3L launches and one host read for
-        all L blocks (bitwise the blocks of the per-layer path, _one_block)."""
+        all L blocks (bitwise the blocks of the per-layer path, _one_block).
+
+        static: the blocks at their capacities, nothing read back (include/gnnrec.h, static
+        shapes): seeds may hold -1 padding; block s has seed_cap + 1 destination rows per
+        type (the last is the dump row) and node_cap + 1 source rows (the last is the next
+        block's dump row), so every layer's output is the next block's source table."""
         ces, nts = list(g.canonical_etypes), list(g.ntypes)
         tix = {nt: i for i, nt in enumerate(nts)}
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
@@ -149,19 +154,28 @@ class BlockSampler:
             [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
             [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
             [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
-            fans, keys, stamp)
+            fans, keys, stamp, static_shapes=static)
         NT, R = len(nts), len(ces)
         blocks = []
         for s, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
             rels = {}
             for r, ce in enumerate(ces):
                 ip = o_ip[r]
-                ip._gnnrec_nnz = int(sizes[(L + 1) * NT + s * R + r])
-                if 0 <= fans[s][r] <= ops.DEFAULT_SPLIT:
-                    ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
+                if static:  # sizes = seed caps, node caps [L x T], edge caps [L x R]
+                    ip._gnnrec_nnz = int(sizes[NT + L * NT + s * R + r])
+                    ip._gnnrec_heavy = ip._gnnrec_nnz  # the dump row: any length
+                else:
+                    ip._gnnrec_nnz = int(sizes[(L + 1) * NT + s * R + r])
+                    if 0 <= fans[s][r] <= ops.DEFAULT_SPLIT:
+                        ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
                 rels[ce] = (ip, src_loc[r], o_eid[r])
-            num_dst = {nt: int(sizes[s * NT + t]) for t, nt in enumerate(nts)}
-            blocks.insert(0, Block(dict(zip(nts, nodes)), num_dst, rels))
+            if static:
+                num_dst = {nt: int(sizes[s * NT + t]) + 1 for t, nt in enumerate(nts)}
+            else:
+                num_dst = {nt: int(sizes[s * NT + t]) for t, nt in enumerate(nts)}
+            b = Block(dict(zip(nts, nodes)), num_dst, rels)
+            b.static = static
+            blocks.insert(0, b)
         if transposes:
             for block_id, b in enumerate(blocks):
                 if block_id > 0 or self._first_transposes(b):
@@ -174,15 +188,20 @@ class BlockSampler:
 
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
                       exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
-                      transposes: bool = False) -> List[Block]:
+                      transposes: bool = False, static_shapes: bool = False) -> List[Block]:
         """transposes: also build every relation's source-major CSR (Block._t), which the
         training backward gathers over — in the sampling thread (num_workers > 0), off the
-        training thread (EdgeDataLoader, transposed_blocks=True)."""
+        training thread (EdgeDataLoader, transposed_blocks=True).
+        static_shapes: the blocks at fixed capacities with nothing read back (seeds may hold
+        -1 padding; _sample_fused) — the batches of a captured training step."""
         self._calls += 1
         seeds = {nt: torch.as_tensor(v, dtype=torch.int64, device=g.device)
                  for nt, v in seed_nodes.items()}
+        if static_shapes and not self._fused_ok(g):
+            raise ValueError("static_shapes needs the fused sampler: bounded fanouts (0..64) "
+                             "on a HIP device within its limits")
         if self._fused_ok(g):
-            blocks = self._sample_fused(g, seeds, exclude_eids, transposes)
+            blocks = self._sample_fused(g, seeds, exclude_eids, transposes, static_shapes)
             _copy_block_data(g, blocks)
             for b in blocks:
                 b._sampler = weakref.ref(self)
@@ -524,7 +543,7 @@ class EdgeDataLoader:
                  reverse_eids=None, reverse_etypes: Optional[dict] = None,
                  negative_sampler=None, batch_size: int = 1, shuffle: bool = False,
                  drop_last: bool = False, num_workers: int = 0, pin_memory: bool = False,
-                 transposed_blocks: bool = True, **kwargs):
+                 transposed_blocks: bool = True, static_shapes: bool = False, **kwargs):
         self.g = g
         self.g_sampling = g_sampling if g_sampling is not None else g
         # the training loader's blocks carry their source-major CSRs (built by the sampler,
@@ -562,10 +581,68 @@ class EdgeDataLoader:
         self.type_starts = _type_starts(ids, dev)
         self.batch_size, self.shuffle, self.drop_last = batch_size, shuffle, drop_last
         self.num_workers = num_workers
+        # static_shapes: every full batch at fixed shapes with nothing read back to the host
+        # (_head_static + the sampler's static blocks), so a training step over it can be
+        # captured once and replayed (gnnrec.capture.CapturedTrainStep); a final partial
+        # batch comes in the ordinary exact form
+        self.static_shapes = static_shapes
+        if static_shapes:
+            if len(self.types) != 1 or not self.fused_head:
+                raise ValueError("static_shapes: batches of one edge type, with "
+                                 "negative_sampler.Uniform or none, on a HIP device")
+            if not block_sampler._fused_ok(self.g_sampling):
+                raise ValueError("static_shapes needs bounded fanouts (0..64) within the fused "
+                                 "sampler's limits")
+        self._cx_scratch = None
 
     def __len__(self):
         n = self.flat_ids.numel()
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def _head_static(self, batch):
+        """_head at fixed shapes, with no host read: the same pairs, negatives (the same
+        generator draws) and compaction, each type's node list padded with -1 to its bound —
+        the batch's distinct ids, at most min(n_nodes, the positive endpoints plus the
+        negative destinations): a Uniform negative's source is a positive's source."""
+        g = self.g
+        nts = list(g.ntypes)
+        tix = {nt: i for i, nt in enumerate(nts)}
+        if self._cx_scratch is None:
+            self._cx_scratch = [ops.CompactScratch(g.num_nodes(nt), g.device) for nt in nts]
+        k = 0 if self.negative_sampler is None else self.negative_sampler.k
+        pairs = []
+        for ce, e in batch.items():
+            coo = g._coo[ce]
+            pairs.append((ce, coo[0].index_select(0, e), coo[1].index_select(0, e)))
+        negs = []
+        for ce, ps, _pd in pairs:
+            if k:
+                ns = ps.unsqueeze(1).expand(ps.numel(), k).reshape(-1)
+                nd = torch.randint(0, g.num_nodes(ce[2]), (ns.numel(),), device=g.device)
+                negs.append((ce, ns, nd))
+        lists, caps = [], [0] * len(nts)
+        for ce, ps, pd in pairs:
+            lists += [(ps, tix[ce[0]]), (pd, tix[ce[2]])]
+            caps[tix[ce[0]]] += ps.numel()
+            caps[tix[ce[2]]] += pd.numel()
+        for ce, ns, nd in negs:
+            lists += [(ns, tix[ce[0]]), (nd, tix[ce[2]])]
+            caps[tix[ce[2]]] += nd.numel()
+        caps = [min(c, g.num_nodes(nt)) for c, nt in zip(caps, nts)]
+        nodes, local, count = ops.compact_ids(lists, self._cx_scratch, caps)
+        node_ids = dict(zip(nts, nodes))
+        pos_l, neg_l, i = {}, {}, 0
+        for ce, _ps, _pd in pairs:
+            pos_l[ce] = (local[i], local[i + 1])
+            i += 2
+        for ce, _ns, _nd in negs:
+            neg_l[ce] = (local[i], local[i + 1])
+            i += 2
+        empty = torch.zeros(0, dtype=torch.int64, device=g.device)
+        pos_l = {ce: pos_l.get(ce, (empty, empty)) for ce in g.canonical_etypes}
+        if k:  # every etype, in graph order, as _head returns them
+            neg_l = {ce: neg_l.get(ce, (empty, empty)) for ce in g.canonical_etypes}
+        return node_ids, pos_l, neg_l, count
 
     def _compact(self, pos_edges, neg_edges):
         """DGL compact_graphs([pos, neg]): both pair graphs over the union of their nodes
@@ -632,7 +709,11 @@ class EdgeDataLoader:
                             self.drop_last, g.device):
             parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
             batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
-            if self.fused_head:
+            static = self.static_shapes and idx.numel() == self.batch_size
+            counts = None
+            if static:
+                node_ids, pos_l, neg_l, counts = self._head_static(batch)
+            elif self.fused_head:
                 node_ids, pos_l, neg_l = self._head(batch)
             else:  # the readable form: the same kernels, generator draws and order
                 pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch
@@ -643,6 +724,7 @@ class EdgeDataLoader:
                     neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
                 node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
             pos_g = PairGraph(pos_l, node_ids)
+            pos_g.static = static
             for ce, e in batch.items():
                 for k, v in g._edata[ce].items():
                     pos_g._edata[ce][k] = ops.gather_rows(v, e)
@@ -658,12 +740,17 @@ class EdgeDataLoader:
                 exclude = dict(batch)
             seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
             blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
-                                                transposes=self.transposed_blocks)
+                                                transposes=self.transposed_blocks,
+                                                static_shapes=static)
+            # static: the real node count per type, on the device (the node lists hold -1
+            # past it)
+            pos_g.node_counts = dict(zip(g.ntypes, counts.unbind(0))) if static else None
             input_nodes = blocks[0].srcdata[NID]
             if self.negative_sampler is None:
                 yield input_nodes, pos_g, blocks
             else:
                 neg_g = PairGraph(neg_l, node_ids)
+                neg_g.static = static
                 if type(self.negative_sampler) is _Uniform:
                     # every etype's negative sources are its positive sources repeated K times
                     # (in local ids too: one relabel maps both): CosinePrediction.pair scores

@@ -394,7 +394,20 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * `bits` (uint64 [2 * ceil(n_nodes/64)]) / `word_rank` (int64 [ceil(n_nodes/64) + 1])
  * scratch across calls; `stamp` >= 1 grows by L + 1 per call on the same `pos` arrays (the
  * caller zeroes `pos` and restarts at 1 before it would pass 2^32 - 2).  A seed listed twice
- * keeps its first position (its later copies get local ids but no edges point at them). */
+ * keeps its first position (its later copies get local ids but no edges point at them).
+ * Static shapes (static_shapes = 1): every output at its capacity and nothing to read back,
+ * so the call (and a training step over its blocks) can be captured into a hipGraph.  Seed
+ * slots holding -1 are padding (step 0's seeds: the batch padded to a fixed count).  Each
+ * destination type gets one more row, the dump row at index seed_cap: out_indptr holds
+ * seed_cap + 2 entries.  A padding seed's row holds `fanout` padding edges, the dump row the
+ * rest of the edge capacity; every padding edge comes from the source type's dump node
+ * (local id = its seed_cap) with eid -1.  New sources start at seed_cap + 1; the source list
+ * is -1 at the dump node and past the new sources.  A real seed's row is its eager row with
+ * the new sources' local ids shifted by seed_cap + 1 - n_seeds: padding reaches padding rows
+ * only.  node_cap = seed_cap + 1 + min(n_nodes, edges sourced from the type); the nodes
+ * outputs then hold node_cap + 1 entries, the last -1: the next step's dump row (its index
+ * there, seed_cap, is this step's node_cap), so one layer's output rows are exactly the
+ * source rows of the block it feeds. */
 #define GNNREC_SB_MAX_RELS 8
 #define GNNREC_SB_MAX_TYPES 4
 #define GNNREC_SB_MAX_STEPS 4
@@ -427,9 +440,10 @@ typedef struct gnnrec_sample_plan {
   int64_t fanout[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS]; /* 0..64 */
   uint64_t key[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   uint32_t stamp;
+  int static_shapes;    /* 0: exact sizes (read `sizes`), 1: capacities, -1-padded (above) */
   /* outputs, sized by gnnrec_sample_blocks_caps: per step s and relation r the block CSR
-   * (out_indptr [seed_cap + 1], out_src int32 local ids [edge_cap], out_eid [edge_cap]),
-   * per step and type the source node ids [node_cap] (seeds first) */
+   * (out_indptr [seed_cap + 1 (+1 static)], out_src int32 local ids [edge_cap], out_eid [edge_cap]),
+   * per step and type the source node ids [node_cap (+1 static)] (seeds first) */
   int64_t* out_indptr[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   int32_t* out_src[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   int64_t* out_eid[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
@@ -445,6 +459,35 @@ typedef struct gnnrec_sample_plan {
 int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
                               int64_t* edge_cap, int64_t* node_cap, int64_t* workspace_bytes);
 int gnnrec_sample_blocks(const gnnrec_sample_plan* plan, void* stream);
+
+/* compact_graphs over id lists (EdgeDataLoader's pair graphs, src/sampling.py:167-207 ->
+ * DGL compact_graphs([pos, neg])) at static shapes, for a captured training step: per node
+ * type the ids of its lists form one ascending node list, padded with -1 to `cap` (the
+ * caller's bound on the distinct ids: past it ids are left out of the list and their local ids
+ * point past cap, so the caller must rule that out), and every list
+ * element gets its position in that list.  3 launches (mark bits, scan popcounts, relabel +
+ * list), no host synchronisation; `bits` (uint64 [2 * ceil(n_nodes/64)], zero before the
+ * first call) and `word_rank` (int64 [ceil(n_nodes/64) + 1]) are the caller's scratch, and
+ * `parity` alternates 0 / 1 between calls on the same scratch.  count [n_types] (device)
+ * receives each type's number of distinct ids.  The lists' order does not matter: the node
+ * lists are those of the per-type mark / scan / compact path (gnnrec_mark_ids & co.). */
+#define GNNREC_COMPACT_MAX_LISTS 8
+typedef struct gnnrec_compact_list {
+  const int64_t* ids; /* global ids (>= 0) of node type `type` */
+  int64_t n;
+  int32_t type;
+  int64_t* local;     /* [n] out: position in the type's node list */
+} gnnrec_compact_list;
+typedef struct gnnrec_compact_type {
+  int64_t n_nodes;
+  uint64_t* bits;
+  int64_t* word_rank;
+  int64_t* nodes;     /* [cap] out */
+  int64_t cap;
+} gnnrec_compact_type;
+int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
+                       const gnnrec_compact_type* types, int n_types, int parity, int64_t* count,
+                       void* stream);
 
 /* ---- f1: recommendation top-k --------------------------------------------
  * For each row r of scores[n_rows, n_cols] (leading dimension ld): the k
@@ -600,7 +643,8 @@ int gnnrec_lstm_slots(const int64_t* indptr, const int32_t* indices, const int64
  * data into the blocks (read at src/train/run.py:112,340). */
 /* Up to GNNREC_GATHER_MAX_JOBS independent row gathers of gnnrec_gather_rows in ONE launch
  * (a sampled batch's edge data for every block and relation plus the input block's node
- * features: one launch instead of one per table). */
+ * features: one launch instead of one per table).  A negative index (a padding slot of a
+ * static-shape block, gnnrec_sample_blocks) writes a zero row. */
 #define GNNREC_GATHER_MAX_JOBS 16
 typedef struct gnnrec_gather_job {
   const void* src;

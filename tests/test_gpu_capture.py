@@ -1,0 +1,180 @@
+"""GPU tests of the static-shape minibatch path and the captured training step (row f2,
+reference src/train/run.py:104-160 per EdgeDataLoader batch).
+
+Static blocks (BlockSampler static shapes, include/gnnrec.h) must hold exactly the exact
+blocks' rows for every real node — the same edges, eids and source ids, local ids aside —
+with padding only in padding rows; the static batch head must give the exact pair graphs;
+and a step over a static batch, eager or replayed from a hipGraph, must train the model as
+the exact batch does (fp32 tolerance: the padded GEMMs sum over more rows)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_sampling import BOUGHT, BUYS, CLICKED, CLICKS, DEV, _graph, _model
+
+pytestmark = pytest.mark.gpu
+
+REV = {'buys': 'bought-by', 'bought-by': 'buys', 'clicks': 'clicked-by',
+       'clicked-by': 'clicks'}
+
+
+def _rows(block, ce):
+    """dst global id -> [(src global id, eid)] of every row, and the padding rows' edges."""
+    from gnnrec.graph import NID
+    ip, loc, eid = (t.cpu().numpy() for t in block._rels[ce])
+    src = block.srcdata[NID][ce[0]].cpu().numpy()
+    dst = block.srcdata[NID][ce[2]].cpu().numpy()[:block.number_of_dst_nodes(ce[2])]
+    real, pad = {}, []
+    for i, v in enumerate(dst.tolist()):
+        edges = [(int(src[loc[e]]), int(eid[e])) for e in range(ip[i], ip[i + 1])]
+        if v >= 0:
+            real[v] = edges
+        else:
+            pad += edges
+    return real, pad, ip
+
+
+@pytest.mark.parametrize("fanouts", [[4, 3], [{"buys": 2, "bought-by": 5, "clicks": 0,
+                                               "clicked-by": 64}, 1]])
+def test_static_blocks_hold_the_exact_rows(fanouts):
+    from gnnrec.graph import NID
+    from gnnrec.sampling import MultiLayerNeighborSampler
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    exact = MultiLayerNeighborSampler(fanouts, seed=4)
+    stat = MultiLayerNeighborSampler(fanouts, seed=4)
+    users = torch.arange(3, 300, 7, device=DEV)
+    items = torch.tensor([5, 1, 77, 9], device=DEV)
+    pad = torch.full((6,), -1, dtype=torch.int64, device=DEV)
+    excl = {BUYS: torch.arange(0, 4000, 5, device=DEV), BOUGHT: torch.arange(0, 4000, 5, device=DEV)}
+    for rep in range(2):
+        a = exact.sample_blocks(g, {"user": users, "item": items}, excl, transposes=True)
+        b = stat.sample_blocks(g, {"user": torch.cat([users, pad]), "item": torch.cat([items, pad])},
+                               excl, transposes=True, static_shapes=True)
+        assert all(x.static for x in b) and not any(x.static for x in a)
+        for ba, bb in zip(a, b):
+            for nt in bb.ntypes:
+                # source list: the exact one's ids in order (seeds, then the new sources),
+                # with -1 at the padding seeds, the dump node and past the new sources
+                sa = ba.srcdata[NID][nt].cpu().numpy()
+                sb = bb.srcdata[NID][nt].cpu().numpy()
+                assert sb[-1] == -1 and (sb[bb.number_of_dst_nodes(nt) - 1] == -1)
+                np.testing.assert_array_equal(sb[sb >= 0], sa)
+                f = bb._src[nt].get("features")
+                if f is not None:
+                    assert not f.cpu().numpy()[sb < 0].any()
+            for ce in bb.canonical_etypes:
+                ra, pa, _ = _rows(ba, ce)
+                rb, pb, ipb = _rows(bb, ce)
+                assert ra == rb, ce
+                assert not pa and all(s == -1 and e == -1 for s, e in pb), ce
+                assert ipb[-1] == bb.num_edges(ce) == bb._rels[ce][0]._gnnrec_nnz
+                occ = bb._edata[ce].get("occurrence")
+                if occ is not None:
+                    eid = bb._rels[ce][2].cpu().numpy()
+                    assert not occ.cpu().numpy()[eid < 0].any()
+            # the layer chain: every block's output rows are the next block's source rows
+        for lo, hi in zip(b[:-1], b[1:]):
+            for nt in lo.ntypes:
+                assert lo.number_of_dst_nodes(nt) == hi.number_of_src_nodes(nt)
+
+
+def _loader(g, static, K=4, batch=64, n=700, seed=5, fanouts=(4, 3), nw=0):
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    return EdgeDataLoader(g, {BUYS: torch.arange(n)}, MultiLayerNeighborSampler(list(fanouts), seed=seed),
+                          exclude='reverse_types', reverse_etypes=REV,
+                          negative_sampler=negative_sampler.Uniform(K), batch_size=batch,
+                          shuffle=True, static_shapes=static, num_workers=nw)
+
+
+def test_static_batch_head_gives_the_exact_pair_graphs():
+    from gnnrec.graph import NID
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    out = []
+    for static in (False, True):
+        torch.manual_seed(3)
+        out.append(list(_loader(g, static)))
+    assert len(out[0]) == len(out[1]) == -(-700 // 64)
+    for k, (ia, ib) in enumerate(zip(*out)):
+        (_, pa, na, ba), (_, pb, nb, bb) = ia, ib
+        last = k == len(out[0]) - 1  # 700 % 64: the partial batch is exact
+        assert pb.static == (not last) and all(x.static == (not last) for x in bb)
+        for nt in ("user", "item"):
+            ida, idb = pa.ndata[NID][nt].cpu().numpy(), pb.ndata[NID][nt].cpu().numpy()
+            np.testing.assert_array_equal(idb[:ida.size], ida)
+            assert (idb[ida.size:] == -1).all()
+            if not last:
+                assert int(pb.node_counts[nt]) == ida.size
+        for ce in g.canonical_etypes:
+            for ga, gb in ((pa, pb), (na, nb)):
+                for x, y in zip(ga.all_edges(etype=ce), gb.all_edges(etype=ce)):
+                    assert torch.equal(x, y), ce
+        assert nb.src_repeats_pos == na.src_repeats_pos == 4
+
+
+def _loss(K):
+    from gnnrec import nn as gnn
+
+    def f(model, batch):
+        _, pos_g, neg_g, blocks = batch
+        _, ps, ns = model(blocks, blocks[0].srcdata['features'], pos_g, neg_g, True)
+        return gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata['recency'])
+    return f
+
+
+def _close(a, b, what, rtol=2e-4, atol=2e-6):
+    torch.testing.assert_close(a, b, rtol=rtol, atol=atol, msg=what)
+
+
+@pytest.mark.parametrize("agg,fold", [("mean", "0"), ("mean", "1"), ("mean_nn_edge", "auto")])
+def test_static_step_trains_as_the_exact_step(monkeypatch, agg, fold):
+    """One step over the static batch and over the exact one: the same loss and gradients
+    (fp32 rounding: the weight-gradient GEMMs sum over the padding rows' zeros too)."""
+    monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    K = 4
+    batches = []
+    for static in (False, True):
+        torch.manual_seed(3)
+        batches.append(next(iter(_loader(g, static, K=K))))
+    base = _model(g, agg=agg).train()
+    grads = []
+    for batch in batches:
+        m = copy.deepcopy(base)
+        loss = _loss(K)(m, batch)
+        loss.backward()
+        grads.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()
+                                      if p.grad is not None}))
+    (la, ga), (lb, gb) = grads
+    _close(lb, la, "loss")
+    assert ga.keys() == gb.keys() and ga
+    for n in ga:
+        _close(gb[n], ga[n], n)
+
+
+@pytest.mark.parametrize("nw", [0, 2])
+def test_captured_steps_train_as_the_eager_loop(nw):
+    """CapturedTrainStep over a static loader (warm-up steps, capture, replays, the exact
+    partial batch eagerly) against the eager loop over the exact loader: per-step losses and
+    the final parameters agree."""
+    from gnnrec.capture import CapturedTrainStep
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    K = 4
+    base = _model(g, agg="mean").train()
+    runs = []
+    for captured in (False, True):
+        torch.manual_seed(7)
+        m = copy.deepcopy(base)
+        opt = torch.optim.Adam(m.parameters(), lr=0.01, fused=True)
+        step = CapturedTrainStep(m, opt, _loss(K), warmup=1)
+        losses = []
+        for _epoch in range(2):
+            for batch in _loader(g, captured, K=K, nw=nw if captured else 0):
+                losses.append(float(step(batch) if captured else step.eager(batch)))
+        runs.append((losses, m, step))
+    (la, ma, _), (lb, mb, st) = runs
+    assert st.replays >= 2 * (700 // 64) - 2 and st.eager_steps == 1 + 2
+    np.testing.assert_allclose(lb, la, rtol=1e-3, atol=1e-5)
+    for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        _close(pb.detach(), pa.detach(), n, rtol=2e-3, atol=2e-5)
