@@ -468,9 +468,10 @@ def cpu_baseline(args, d):
         aff = None
     return {"value": port, "unit": "edges/s", "cores": cores, "kind": "port",
             "cores_affinity": aff, "cores_machine": os.cpu_count(),
-            "cores_note": (f"{cores} OpenMP threads = the job's CPU lease (OMP_NUM_THREADS="
-                           f"{os.environ.get('OMP_NUM_THREADS', 'unset')}); the process may run "
-                           f"on {aff} of the machine's {os.cpu_count()} logical CPUs"),
+            "cores_note": (f"{cores} of the machine's {os.cpu_count()} logical CPUs: {cores} "
+                           f"OpenMP threads = the job's CPU lease (OMP_NUM_THREADS="
+                           f"{os.environ.get('OMP_NUM_THREADS', 'unset')}; the process may run "
+                           f"on {aff} CPUs), not the whole host SURVEY 8(d) d5 names"),
             "cpu_model": cpu_model(), "index_add_value": alt, "config": wl,
             "sample": f"{wl} full-size tables ({U}x{d} + {I}x{d} fp32) and edge stream; dst rows "
                       f"[0,{f:g}N) of both relations = {edges // 2} edges/layer; 2 layers, "
@@ -824,7 +825,63 @@ def minibatch_step(dev, warmup: int = 5):
                                             "pos_edges_per_s": round(1024 / ms * 1e3),
                                             "loss": float(loss.detach())}
             del it, el
+        try:
+            out[f"K{K}_num_workers2_captured"] = captured_step(g, dev, K, steps, warmup)
+        except Exception as exc:  # a secondary measurement never masks the others
+            out[f"K{K}_num_workers2_captured"] = {"error": repr(exc)}
     return out
+
+
+def captured_step(g, dev, K: int, steps: int, warmup: int):
+    """The same C2 step over EdgeDataLoader(static_shapes=True) batches, recorded once into a
+    hipGraph and replayed per batch (gnnrec.capture.CapturedTrainStep): the sampling thread
+    builds fixed-shape batches on its own stream, the training thread copies each into the
+    captured batch's buffers and launches the graph.  gpu_ms_per_replay: HIP events around
+    replays of one batch alone; busy = that / ms_per_step (the GPU's share of the step)."""
+    from gnnrec import nn as gnn
+    from gnnrec.capture import CapturedTrainStep
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+
+    buys = ("user", "buys", "item")
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
+                          "mean", "cos", "sum", True).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=0.005, fused=True)
+
+    def loss_fn(m, batch):
+        _, pos_g, neg_g, blocks = batch
+        _, ps, ns = m(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+        return gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
+
+    step = CapturedTrainStep(model, opt, loss_fn, warmup=2)
+    el = EdgeDataLoader(g, {buys: torch.arange(g.num_edges(buys))},
+                        MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
+                        reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
+                        negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
+                        shuffle=True, num_workers=2, static_shapes=True)
+    it = iter(el)
+    for _ in range(max(warmup, 3)):
+        loss = step(next(it))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step(next(it))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    res = {"ms_per_step": round(ms, 3), "steps": steps,
+           "pos_edges_per_s": round(1024 / ms * 1e3), "loss": float(loss.detach()),
+           "replays": step.replays, "eager_steps": step.eager_steps}
+    del it, el
+    if step.graph is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            step.graph.replay()
+        e1.record()
+        e1.synchronize()
+        res["gpu_ms_per_replay"] = round(e0.elapsed_time(e1) / 20, 3)
+        res["busy"] = round(res["gpu_ms_per_replay"] / ms, 3)
+    return res
 
 
 MFMA_F32_PEAK_TFS = 157.3  # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md

@@ -22,13 +22,14 @@
 //     sizes every block (the per-layer path read back twice per layer).
 //   * static shapes (plan.static_shapes): every block at its capacity, nothing to read back,
 //     so a training step over it can be captured into a hipGraph.  Seed slots holding -1
-//     are padding; each block gets one extra "dump" row per destination type (index
-//     seed_cap): a padding seed's row holds `fanout` padding edges, the dump row the rest of
-//     the edge capacity, every padding edge from the source type's dump node (eid -1).  New
-//     sources start after the dump row, the source list is -1 beyond them, up to node_cap
-//     + 1 entries: the last is the next block's dump row (its index there is its seed
-//     count), so a layer's output rows are the next block's source rows.  Padding only
-//     ever reaches padding rows: the real rows' blocks, local ids aside, are the exact ones.
+//     (a suffix) are padding rows; each block gets one extra "dump" row per destination
+//     type (index seed_cap): a padding row holds `fanout` padding edges, the dump row the
+//     rest of the edge capacity, every padding edge from the source list's last slot
+//     (node_cap - 1, always -1) with eid -1.  The source list is the exact one — the real
+//     seeds, the new sources after them, at the same positions — then -1 up to node_cap + 1
+//     entries: the last is the next block's dump row (its index there is its seed_cap), so
+//     a layer's output rows are the next block's source rows.  A padding row may sit over a
+//     real source's slot: its output is garbage no real row reads, and its gradient is 0.
 #include "common.hpp"
 #include "sampler.hpp"
 
@@ -66,7 +67,7 @@ struct RelArgs {
 
 struct TypeArgs {
   const int64_t* seeds;    // this step's destination nodes
-  const int64_t* n_seeds;  // device count (sizes row s - 1)
+  const int64_t* n_seeds;  // device count of the real seeds (sizes row s - 1)
   int64_t seed_cap;
   unsigned long long* pos_cur;   // this step's seed positions (read)
   unsigned long long* pos_next;  // the next step's (written by finalize)
@@ -79,7 +80,6 @@ struct TypeArgs {
   int64_t n_seeds_host;    // begin only: the batch's seed count
   int64_t node_cap;        // static shapes: the source list's length
   int64_t node_len;        // static shapes: node_cap + 1 (the next block's dump row, -1)
-  int64_t new0;            // static shapes: where the new sources start (seed_cap + 1)
 };
 
 // sections of one launch: block ranges [begin[k], begin[k+1]) run job kind[k] on index idx[k]
@@ -121,17 +121,30 @@ __device__ __forceinline__ void set_pos(unsigned long long* pos, int64_t id, uin
                          __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the destination rows of a step: the seeds, or (static shapes) the seed capacity
+__device__ __forceinline__ int64_t seed_rows(const StepArgs& A, const TypeArgs& T) {
+  return A.stat ? T.seed_cap : *T.n_seeds;
+}
+
 // ---------------------------------------------------------------- begin
 __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
   const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
   const int i = A.sec.idx[k];
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)A.n_types)
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)A.n_types &&
+      (!A.stat || A.type[threadIdx.x].n_seeds_host == 0))
     A.sizes_seed_row[threadIdx.x] = A.type[threadIdx.x].n_seeds_host;
   switch (A.sec.kind[k]) {
     case kSecSeedPos: {
       const TypeArgs& T = A.type[i];
-      if (t < T.n_seeds_host && T.seeds[t] >= 0) set_pos(T.pos_cur, T.seeds[t], A.stamp, t);
+      if (t >= T.n_seeds_host) break;
+      const int64_t v = T.seeds[t];
+      if (v >= 0) set_pos(T.pos_cur, v, A.stamp, t);
+      // static shapes: the real seeds' count = the end of the non-negative prefix (one
+      // writer: the last real seed, or slot 0 when there is none)
+      if (A.stat && ((v >= 0 && (t + 1 == T.n_seeds_host || T.seeds[t + 1] < 0)) ||
+                     (t == 0 && v < 0)))
+        A.sizes_seed_row[i] = v >= 0 ? t + 1 : 0;
       break;
     }
     case kSecZeroBits: {
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
   const TypeArgs& S = A.type[R.src_t];
   const Group<G> grp;
   const int64_t i = (int64_t)b * (kSbBlock / G) + (threadIdx.x / G);
-  if (i >= *D.n_seeds) return;  // group-uniform
+  if (i >= seed_rows(A, D)) return;  // group-uniform
   const int64_t v = D.seeds[i];
   if (v < 0) {  // a padding seed (static shapes): its row holds `fanout` padding edges
     if (grp.lane == 0) R.counts[i] = R.fanout;
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
   int64_t* out;
   if (is_rel) {
     const RelArgs& R = A.rel[seg];
-    n = *A.type[R.dst_t].n_seeds;
+    n = seed_rows(A, A.type[R.dst_t]);
     cnt = R.counts;
     out = R.out_indptr;
   } else {
@@ -294,13 +307,13 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
       if (A.stat) out[n + 1] = A.rel[seg].edge_cap;  // the dump row takes the rest
     } else {
       const TypeArgs& T = A.type[seg - A.n_rels];
-      *T.n_nodes_out = A.stat ? T.node_cap : *T.n_seeds + carry;
+      *T.n_nodes_out = *T.n_seeds + carry;
     }
   }
 }
 
 // ---------------------------------------------------------------- finalize (step s)
-// n_p: where the new sources start (the seed count; static shapes: after the dump row)
+// n_p: where the new sources start (the real seeds' count)
 __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint32_t stamp,
                                             int32_t s) {
   const unsigned long long v = T.pos_cur[s];
@@ -319,14 +332,14 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       const TypeArgs& D = A.type[R.dst_t];
       const TypeArgs& S = A.type[R.src_t];
       const int64_t i = t / R.fanout, j = t - i * R.fanout;
-      if (i >= *D.n_seeds || j >= R.counts[i]) return;
+      if (i >= seed_rows(A, D) || j >= R.counts[i]) return;
       const int64_t o = R.out_indptr[i] + j;
-      if (D.seeds[i] < 0) {  // a padding seed's padding edge
-        R.out_src[o] = (int32_t)S.seed_cap;
+      if (D.seeds[i] < 0) {  // a padding row's padding edge
+        R.out_src[o] = (int32_t)(S.node_cap - 1);
         R.out_eid[o] = -1;
         break;
       }
-      R.out_src[o] = (int32_t)local_id(S, A.stat ? S.new0 : *S.n_seeds, A.stamp, R.pick_src[t]);
+      R.out_src[o] = (int32_t)local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
       R.out_eid[o] = R.pick_eid[t];
       break;
     }
@@ -334,13 +347,13 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       const RelArgs& R = A.rel[x];
       const int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t;
       if (e >= R.edge_cap) return;
-      R.out_src[e] = (int32_t)A.type[R.src_t].seed_cap;
+      R.out_src[e] = (int32_t)(A.type[R.src_t].node_cap - 1);
       R.out_eid[e] = -1;
       break;
     }
-    case kSecPadNodes: {  // static shapes: the dump node and the list's tail are -1
+    case kSecPadNodes: {  // static shapes: the list past the real seeds and new sources
       const TypeArgs& T = A.type[x];
-      const int64_t p = t == 0 ? T.seed_cap : T.new0 + T.word_rank[T.words] + t - 1;
+      const int64_t p = *T.n_seeds + T.word_rank[T.words] + t;
       if (p < T.node_len) T.nodes[p] = -1;
       break;
     }
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (t >= T.words) return;
       unsigned long long word = T.bits_cur[t];
       if (!word) return;
-      int64_t p = (A.stat ? T.new0 : *T.n_seeds) + T.word_rank[t];
+      int64_t p = *T.n_seeds + T.word_rank[t];
       while (word) {
         const int64_t id = t * 64 + __builtin_ctzll(word);
         T.nodes[p] = id;
@@ -522,8 +535,13 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
       int64_t e = 0;
       for (int r = 0; r < P->n_rels; ++r)
         if (P->rel[r].src_type == t) e += C->edge[s][r];
-      C->node[s][t] = C->seed[s][t] + (P->static_shapes ? 1 : 0) +
-                      std::min<int64_t>(e, P->type[t].n_nodes);
+      // static shapes: the real sources (at most n_nodes) and the dump slot, and never fewer
+      // rows than the destinations (a block's dst rows are a prefix of its sources)
+      C->node[s][t] = P->static_shapes
+                          ? std::max<int64_t>(C->seed[s][t],
+                                              std::min<int64_t>(C->seed[s][t] + e,
+                                                                P->type[t].n_nodes)) + 1
+                          : C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
       if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
     }
   }
@@ -625,7 +643,6 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.n_nodes_out = node_count + (int64_t)(s + 1) * T + t;
       a.node_cap = C.node[s][t];
       a.node_len = C.node[s][t] + 1;
-      a.new0 = C.seed[s][t] + 1;
     }
     for (int r = 0; r < R; ++r) {
       const gnnrec_sample_rel& re = P->rel[r];
@@ -711,7 +728,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     if (P->static_shapes) {
       for (int r = 0; r < R; ++r) add_sec(A.sec, kSecDumpEdges, r, nblocks(C.edge[s][r]));
       for (int t = 0; t < T; ++t)
-        add_sec(A.sec, kSecPadNodes, t, nblocks(C.node[s][t] + 1 - C.seed[s][t]));
+        add_sec(A.sec, kSecPadNodes, t, nblocks(C.node[s][t] + 1));
     }
     if (A.sec.n) {
       hipLaunchKernelGGL(sb_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock),

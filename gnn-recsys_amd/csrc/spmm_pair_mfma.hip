@@ -49,10 +49,13 @@
 //
 // Not kept either (tools/EXPERIMENTS.md): the projections as six bf16 MFMA products of
 // three-way split operands (fp32-accurate, 2.7x fewer MFMA issue cycles but 1.5x the weight
-// bytes per tile: launch 47.3 vs 38.7 ms, profiles/r04j_pair_bf16x3_ab.md — the projection
-// phase is bound by streaming the four weight matrices from L2 once per 32-row tile, not by
-// the MFMA); 48-row tiles / a third block per CU (round 5 verdict) were not attempted: the
-// pre-projected launch stays the default.
+// bytes per tile: launch 47.3 vs 38.7 ms, profiles/r04j_pair_bf16x3_ab.md).  What bounds the
+// projection phase (14.2 ms against 8.3 ms of MFMA issue at 2.4 GHz) is not the weight
+// stream's latency — streaming the weights 8, 16 or 32 k-steps ahead changed nothing
+// (profiles/r04r_pair_weight_stream.md) — but the clock under MFMA load (≈2.0-2.2 GHz) and
+// each tile's epilogue and barriers beside the MFMAs; both phases need all 16 resident waves
+// (profiles/r04s_pair_waves_per_cu.md).  48-row tiles / a third block per CU were not
+// attempted: the pre-projected launch stays the default.
 #include "common.hpp"
 #include "gather.hpp"
 #include "rowq.hpp"

@@ -174,7 +174,16 @@ class BlockSampler:
             else:
                 num_dst = {nt: int(sizes[s * NT + t]) for t, nt in enumerate(nts)}
             b = Block(dict(zip(nts, nodes)), num_dst, rels)
-            b.static = static
+            if static:
+                # the destination ids are the step's seed slots (-1: padding rows, the dump
+                # row last), not the source prefix: a padding row may sit over a real source
+                b.static = True
+                for t, nt in enumerate(nts):
+                    if s == 0:
+                        dst_ids = torch.cat([seeds.get(nt, empty), empty.new_full((1,), -1)])
+                    else:
+                        dst_ids = steps[s - 1][3][t]
+                    b._dst[nt][NID] = dst_ids
             blocks.insert(0, b)
         if transposes:
             for block_id, b in enumerate(blocks):

@@ -315,11 +315,13 @@ int gnnrec_sddmm_cos_f32(const int64_t* src, const int64_t* dst, int64_t n_edges
  * (src/sampling.py:163-165: every positive edge's source repeated K times): group g = source
  * src_g[g], its positive edge to first[g] (may be NULL) -> out_first[g], and its K negatives
  * to dst[g K + j] -> out[g K + j].  One gathered row per edge; bitwise the scores of
- * gnnrec_sddmm_cos_f32 on the expanded edge lists.  d % 4 == 0, d <= 256, 16-B aligned. */
+ * gnnrec_sddmm_cos_f32 on the expanded edge lists.  d % 4 == 0, d <= 256, 16-B aligned.
+ * n_rows_d: Hd's row count — a table larger than an XCD's L2 share is scored in XCD slices
+ * (each XCD gathers from an L2-resident slice of the rows at a time; the same bits). */
 int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_groups, const int64_t* first,
                                  float* out_first, int64_t K, const int64_t* dst, float* out,
                                  const float* Hs, int64_t lds, const float* Hd, int64_t ldd,
-                                 int64_t d, void* stream);
+                                 int64_t n_rows_d, int64_t d, void* stream);
 
 /* ---- a8: PredictingLayer over gathered edge endpoints (K6) ---------------
  * P = Hs W1a^T + b1 and Q = Hd W1b^T are precomputed per node by gnnrec_gemm_f32
@@ -397,17 +399,18 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * keeps its first position (its later copies get local ids but no edges point at them).
  * Static shapes (static_shapes = 1): every output at its capacity and nothing to read back,
  * so the call (and a training step over its blocks) can be captured into a hipGraph.  Seed
- * slots holding -1 are padding (step 0's seeds: the batch padded to a fixed count).  Each
- * destination type gets one more row, the dump row at index seed_cap: out_indptr holds
- * seed_cap + 2 entries.  A padding seed's row holds `fanout` padding edges, the dump row the
- * rest of the edge capacity; every padding edge comes from the source type's dump node
- * (local id = its seed_cap) with eid -1.  New sources start at seed_cap + 1; the source list
- * is -1 at the dump node and past the new sources.  A real seed's row is its eager row with
- * the new sources' local ids shifted by seed_cap + 1 - n_seeds: padding reaches padding rows
- * only.  node_cap = seed_cap + 1 + min(n_nodes, edges sourced from the type); the nodes
- * outputs then hold node_cap + 1 entries, the last -1: the next step's dump row (its index
+ * slots holding -1 are padding rows and form a suffix (step 0's seeds: the batch padded to
+ * a fixed count).  Each destination type gets one more row, the dump row at index
+ * seed_cap: out_indptr holds seed_cap + 2 entries.  A padding row holds `fanout` padding
+ * edges, the dump row the rest of the edge capacity; every padding edge comes from the
+ * source list's slot node_cap - 1 (always -1) with eid -1.  The source list holds the
+ * exact call's list (real seeds, then the new sources, at the same positions and local
+ * ids), then -1 up to node_cap + 1 entries: the last is the next step's dump row (its index
  * there, seed_cap, is this step's node_cap), so one layer's output rows are exactly the
- * source rows of the block it feeds. */
+ * source rows of the block it feeds.  A padding row may sit over a real source's slot: no
+ * real row reads its output and its gradient is zero.  node_cap = max(seed_cap,
+ * min(n_nodes, seed_cap + edges sourced from the type)) + 1; `sizes` then holds the real
+ * seed / node counts per step and the edge counts of the seed rows (the dump row's aside). */
 #define GNNREC_SB_MAX_RELS 8
 #define GNNREC_SB_MAX_TYPES 4
 #define GNNREC_SB_MAX_STEPS 4
@@ -454,8 +457,9 @@ typedef struct gnnrec_sample_plan {
 
 /* Host only: per step the capacities of the outputs (seed_cap [s][t]: destination nodes,
  * edge_cap [s][r] = seed_cap[s][dst] x fanout, node_cap [s][t] = seed_cap[s][t] +
- * min(n_nodes_t, sum of edge_cap[s][r] over relations sourced from t); seed_cap[s+1] =
- * node_cap[s]), each flattened [step][GNNREC_SB_MAX_*], and the workspace bytes. */
+ * min(n_nodes_t, sum of edge_cap[s][r] over relations sourced from t), static shapes: see
+ * above; seed_cap[s+1] = node_cap[s]), each flattened [step][GNNREC_SB_MAX_*], and the
+ * workspace bytes. */
 int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
                               int64_t* edge_cap, int64_t* node_cap, int64_t* workspace_bytes);
 int gnnrec_sample_blocks(const gnnrec_sample_plan* plan, void* stream);

@@ -25,7 +25,8 @@ def _rows(block, ce):
     from gnnrec.graph import NID
     ip, loc, eid = (t.cpu().numpy() for t in block._rels[ce])
     src = block.srcdata[NID][ce[0]].cpu().numpy()
-    dst = block.srcdata[NID][ce[2]].cpu().numpy()[:block.number_of_dst_nodes(ce[2])]
+    dst = block.dstdata[NID][ce[2]].cpu().numpy()
+    assert dst.size == block.number_of_dst_nodes(ce[2])
     real, pad = {}, []
     for i, v in enumerate(dst.tolist()):
         edges = [(int(src[loc[e]]), int(eid[e])) for e in range(ip[i], ip[i + 1])]
@@ -55,12 +56,17 @@ def test_static_blocks_hold_the_exact_rows(fanouts):
         assert all(x.static for x in b) and not any(x.static for x in a)
         for ba, bb in zip(a, b):
             for nt in bb.ntypes:
-                # source list: the exact one's ids in order (seeds, then the new sources),
-                # with -1 at the padding seeds, the dump node and past the new sources
+                # source list: the exact one (the seeds, then the new sources, at the same
+                # positions), then -1 — the padding-edge source slot and the next block's
+                # dump row last; destinations: the seed slots, -1 at padding and dump rows
                 sa = ba.srcdata[NID][nt].cpu().numpy()
                 sb = bb.srcdata[NID][nt].cpu().numpy()
-                assert sb[-1] == -1 and (sb[bb.number_of_dst_nodes(nt) - 1] == -1)
-                np.testing.assert_array_equal(sb[sb >= 0], sa)
+                np.testing.assert_array_equal(sb[:sa.size], sa)
+                assert (sb[sa.size:] == -1).all() and sb.size >= sa.size + 2
+                da = ba.dstdata[NID][nt].cpu().numpy()
+                db = bb.dstdata[NID][nt].cpu().numpy()
+                np.testing.assert_array_equal(db[:da.size], da)
+                assert (db[da.size:] == -1).all() and db[-1] == -1
                 f = bb._src[nt].get("features")
                 if f is not None:
                     assert not f.cpu().numpy()[sb < 0].any()
@@ -169,12 +175,17 @@ def test_captured_steps_train_as_the_eager_loop(nw):
         opt = torch.optim.Adam(m.parameters(), lr=0.01, fused=True)
         step = CapturedTrainStep(m, opt, _loss(K), warmup=1)
         losses = []
-        for _epoch in range(2):
-            for batch in _loader(g, captured, K=K, nw=nw if captured else 0):
-                losses.append(float(step(batch) if captured else step.eager(batch)))
+        # an epoch and the start of the next: warm-up, capture, replays, the partial batch
+        # eagerly, replays again (further on, a hinge of the margin loss flipped by the two
+        # runs' fp32 rounding differences moves the losses apart by one term)
+        for epoch in range(2):
+            for k, batch in enumerate(_loader(g, captured, K=K, nw=nw if captured else 0)):
+                if epoch == 0 or k < 3:
+                    loss = step(batch) if captured else step.eager(batch)
+                    losses.append(float(loss.detach()))
         runs.append((losses, m, step))
     (la, ma, _), (lb, mb, st) = runs
-    assert st.replays >= 2 * (700 // 64) - 2 and st.eager_steps == 1 + 2
-    np.testing.assert_allclose(lb, la, rtol=1e-3, atol=1e-5)
+    assert st.replays == 700 // 64 - 1 + 3 and st.eager_steps == 1 + 1
+    np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
     for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         _close(pb.detach(), pa.detach(), n, rtol=2e-3, atol=2e-5)
