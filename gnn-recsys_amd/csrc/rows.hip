@@ -71,6 +71,7 @@ struct GatherJobs {
   const int64_t* idx[GNNREC_GATHER_MAX_JOBS];
   int64_t src_ld[GNNREC_GATHER_MAX_JOBS], dst_ld[GNNREC_GATHER_MAX_JOBS];
   int64_t n[GNNREC_GATHER_MAX_JOBS], upr[GNNREC_GATHER_MAX_JOBS];
+  const int64_t* n_dev[GNNREC_GATHER_MAX_JOBS];
   int unit[GNNREC_GATHER_MAX_JOBS];  // log2 of the unit bytes: 4, 3, 2 or 0
   int block0[GNNREC_GATHER_MAX_JOBS + 1];
   int n_jobs;
@@ -78,7 +79,8 @@ struct GatherJobs {
 
 template <typename U>
 __device__ __forceinline__ void gather_job(const GatherJobs& J, int j, int64_t t0, int64_t step) {
-  const int64_t upr = J.upr[j], total = J.n[j] * upr;
+  const int64_t rows = J.n_dev[j] ? min(*J.n_dev[j], J.n[j]) : J.n[j];
+  const int64_t upr = J.upr[j], total = rows * upr;
   for (int64_t t = t0; t < total; t += step) {
     const int64_t row = t / upr, u = t - row * upr;
     const int64_t r = J.idx[j][row];
@@ -131,6 +133,7 @@ extern "C" int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_job
     J.src_ld[k] = g.src_ld_bytes;
     J.dst_ld[k] = g.dst_ld_bytes;
     J.n[k] = g.n;
+    J.n_dev[k] = g.n_dev;
     J.unit[k] = unit;
     J.upr[k] = g.row_bytes >> unit;
     int64_t nb = (g.n * J.upr[k] + 255) / 256;

@@ -1528,7 +1528,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               const c10::List<optional<Tensor>>& excl_rows, at::IntArrayRef n_nodes,
               at::TensorList seeds, at::TensorList pos, at::TensorList bits,
               at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
-              int64_t steps, int64_t stamp, bool static_shapes) {
+              int64_t steps, int64_t stamp, bool static_shapes, const optional<Tensor>& sizes_out) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = n_nodes.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
@@ -1638,12 +1638,19 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     }
   }
   const int64_t n_sizes = (steps + 1) * (int64_t)NT + steps * (int64_t)R;
-  Tensor sizes = at::empty({n_sizes}, i64);
+  // sizes_out: the device sizes land there and nothing is read back — the caller queues
+  // work sized by them (gathers with device row counts) before its own one read
+  if (has(sizes_out)) {
+    dev(sizes_out, "sizes_out", at::kLong);
+    TORCH_CHECK_VALUE(sizes_out->numel() == n_sizes && sizes_out->is_contiguous(),
+                      "sample_blocks: sizes_out must hold ", n_sizes, " entries");
+  }
+  Tensor sizes = has(sizes_out) ? *sizes_out : at::empty({n_sizes}, i64);
   Tensor ws = at::empty({std::max<int64_t>(ws_bytes, 1)}, i64.dtype(at::kByte));
   P.sizes = p<int64_t>(sizes);
   P.workspace = ws.data_ptr();
   ck(gnnrec_sample_blocks(&P, stream_of(pos[0])), "gnnrec_sample_blocks");
-  if (static_shapes) {  // every output at its capacity: the sizes are the capacities
+  if (static_shapes || has(sizes_out)) {  // every output at its capacity: return those
     std::vector<int64_t> caps;
     for (size_t t = 0; t < NT; ++t) caps.push_back(seed_cap[t]);
     for (int64_t s = 0; s < steps; ++s)
@@ -1670,11 +1677,13 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
 }
 
 // a10: several row gathers in one launch (gnnrec_gather_rows_batch): out[j] = src[j][idx[j]]
-void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList out) {
+void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList out,
+                       at::TensorList n_dev) {
   const OneDevice one_device_;
   const size_t n = src.size();
-  TORCH_CHECK_VALUE(idx.size() == n && out.size() == n && n <= GNNREC_GATHER_MAX_JOBS,
-                    "gather_rows_batch: one idx and out per src, at most ",
+  TORCH_CHECK_VALUE(idx.size() == n && out.size() == n && n <= GNNREC_GATHER_MAX_JOBS &&
+                        (n_dev.empty() || n_dev.size() == n),
+                    "gather_rows_batch: one idx and out (and n_dev, if any) per src, at most ",
                     GNNREC_GATHER_MAX_JOBS, " jobs");
   std::vector<gnnrec_gather_job> jobs(n);
   for (size_t j = 0; j < n; ++j) {
@@ -1696,8 +1705,15 @@ void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList ou
       inner *= src[j].size(k);
     }
     const int64_t es = src[j].element_size();
+    // n_dev[j] (one device int64, or empty): rows min(*n_dev, n) — a producer's count
+    const int64_t* cnt = nullptr;
+    if (!n_dev.empty() && n_dev[j].numel() > 0) {
+      dev(n_dev[j], "n_dev", at::kLong);
+      TORCH_CHECK_VALUE(n_dev[j].numel() == 1, "gather_rows_batch: n_dev entries hold one count");
+      cnt = p<int64_t>(n_dev[j]);
+    }
     jobs[j] = gnnrec_gather_job{src[j].data_ptr(), src[j].stride(0) * es, p<int64_t>(idx[j]),
-                                idx[j].numel(), inner * es, out[j].data_ptr(), inner * es};
+                                idx[j].numel(), inner * es, out[j].data_ptr(), inner * es, cnt};
   }
   if (n == 0 || meta(src[0])) return;
   const c10::DeviceGuard g(src[0].device());
@@ -1984,9 +2000,10 @@ TORCH_LIBRARY(gnnrec, m) {
         "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
         "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
         "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
-        "int stamp, bool static_shapes=False) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
+        "int stamp, bool static_shapes=False, Tensor(d!)? sizes_out=None) -> (Tensor[] out_indptr, "
+        "Tensor[] src_local, Tensor[] eids, "
         "Tensor[] src_nid, int[] sizes)");
-  m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out) -> ()");
+  m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");
   m.def("compact_ids(Tensor[] ids, int[] type, int[] n_nodes, int[] caps, Tensor(a!)[] bits, "
         "Tensor(b!)[] word_rank, int parity) -> (Tensor[] nodes, Tensor[] local, Tensor count)");
   // host-only entry points (no tensors: one catch-all kernel each)

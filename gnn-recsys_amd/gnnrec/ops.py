@@ -1258,14 +1258,18 @@ class SampleScratch:
 
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
-                  fanouts, keys, stamp, static_shapes=False):
+                  fanouts, keys, stamp, static_shapes=False, sizes_out=None):
     """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
     1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
     output block); excl: per relation None or (eids, coo_dst, mask, rows).
     -> per step: ([out_indptr], [local src int32], [eids]) per relation, [src node ids] per
     type, and the sizes (node counts rows -1..L-1 x types, then edge counts).
     static_shapes: every output at its capacity, no host read (the -1-padded layout of
-    include/gnnrec.h); the sizes are then the capacities (seed caps, node caps, edge caps)."""
+    include/gnnrec.h); the sizes are then the capacities (seed caps, node caps, edge caps).
+    sizes_out (int64 device tensor of the sizes' length): the exact outputs at their
+    capacities and the sizes left there, not read back — the caller queues work sized by
+    them on the device (gather_rows_batch's n_dev) before it reads them itself; the returned
+    sizes are the capacities then too."""
     steps, R = len(fanouts), len(indptrs)
     ex = [e if e is not None else (None,) * 4 for e in excl]
     o_ip, o_src, o_eid, nodes, sizes = _T().sample_blocks(
@@ -1273,7 +1277,8 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
         [e[0] for e in ex], [e[1] for e in ex], [e[2] for e in ex], [e[3] for e in ex],
         list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
         [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
-        [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes))
+        [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes),
+        sizes_out)
     NT = len(n_nodes)
     out = []
     for s in range(steps):
@@ -1310,14 +1315,23 @@ def compact_ids(lists, scratch, caps):
     return out
 
 
-def gather_rows_batch(jobs):
+def gather_rows_batch(jobs, n_dev=None):
     """a10, several gathers in one launch: jobs = [(src, idx)] -> [src[idx]] (any dtype,
-    contiguous rows; at most GATHER_MAX_JOBS per launch)."""
+    contiguous rows; at most GATHER_MAX_JOBS per launch).  n_dev: per job None or a one-entry
+    int64 device tensor — only the first min(n_dev, len(idx)) rows are gathered (the rest of
+    the output is left unwritten)."""
     outs = []
+    empty = None
     for i in range(0, len(jobs), GATHER_MAX_JOBS):
         part = jobs[i:i + GATHER_MAX_JOBS]
-        srcs, idxs, res = [], [], []
-        for src, idx in part:
+        srcs, idxs, res, cnts = [], [], [], []
+        for k, (src, idx) in enumerate(part):
+            c = None if n_dev is None else n_dev[i + k]
+            if c is None:
+                if empty is None:
+                    empty = torch.empty(0, dtype=torch.int64, device=idx.device)
+                c = empty
+            cnts.append(c)
             _dev(idx, "idx", torch.int64)
             if src.dim() == 0:
                 raise ValueError("src: expected at least one dimension")
@@ -1328,7 +1342,7 @@ def gather_rows_batch(jobs):
             idxs.append(idx.contiguous())
             res.append(torch.empty((idx.numel(),) + tuple(src.shape[1:]), dtype=src.dtype,
                                    device=src.device))
-        _T().gather_rows_batch(srcs, idxs, res)
+        _T().gather_rows_batch(srcs, idxs, res, cnts if n_dev is not None else [])
         outs.extend(res)
     return outs
 

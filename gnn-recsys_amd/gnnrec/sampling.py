@@ -150,41 +150,72 @@ class BlockSampler:
         fans = [[self._fanout(L - 1 - s, ce) for ce in ces] for s in range(L)]
         keys = [[_mix(self.seed, self._calls, L - 1 - s, r) for r in range(len(ces))]
                 for s in range(L)]
+        NT, R = len(nts), len(ces)
+        # exact sizes: left on the device while the block data gathers are queued behind the
+        # sampler (row counts read there), then ONE host read sizes every block
+        sizes_dev = None if static else torch.empty((L + 1) * NT + L * R, dtype=torch.int64,
+                                                    device=g.device)
         steps, sizes = ops.sample_blocks(
             [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
             [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
             [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
-            fans, keys, stamp, static_shapes=static)
-        NT, R = len(nts), len(ces)
+            fans, keys, stamp, static_shapes=static, sizes_out=sizes_dev)
+        # the block data (DGL copies it at block creation; the reference reads
+        # blocks[0].srcdata['features']): every table in one launch; static: -1 ids -> zero rows
+        jobs, dests, cnts = [], [], []
+        for s_, (_ip, _loc, o_eid, nodes) in enumerate(steps):
+            for r, ce in enumerate(ces):
+                for k, v in g._edata[ce].items():
+                    jobs.append((v, o_eid[r]))
+                    dests.append((s_, ce, k))
+                    cnts.append(None if static else sizes_dev[(L + 1) * NT + s_ * R + r:][:1])
+        for t, nt in enumerate(nts):
+            for k, v in g._ndata[nt].items():
+                jobs.append((v, steps[L - 1][3][t]))
+                dests.append((L - 1, nt, k))
+                cnts.append(None if static else sizes_dev[L * NT + t:][:1])
+        gathered = ops.gather_rows_batch(jobs, None if static else cnts) if jobs else []
+        if not static:
+            sizes = sizes_dev.tolist()  # the call's one host read
         blocks = []
-        for s, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
+        for s_, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
             rels = {}
             for r, ce in enumerate(ces):
-                ip = o_ip[r]
+                ip, loc, eid = o_ip[r], src_loc[r], o_eid[r]
                 if static:  # sizes = seed caps, node caps [L x T], edge caps [L x R]
-                    ip._gnnrec_nnz = int(sizes[NT + L * NT + s * R + r])
+                    ip._gnnrec_nnz = int(sizes[NT + L * NT + s_ * R + r])
                     ip._gnnrec_heavy = ip._gnnrec_nnz  # the dump row: any length
                 else:
-                    ip._gnnrec_nnz = int(sizes[(L + 1) * NT + s * R + r])
-                    if 0 <= fans[s][r] <= ops.DEFAULT_SPLIT:
+                    ne = sizes[(L + 1) * NT + s_ * R + r]
+                    ip = ip[:sizes[s_ * NT + tix[ce[2]]] + 1]
+                    loc, eid = loc[:ne], eid[:ne]
+                    ip._gnnrec_nnz = ne
+                    if 0 <= fans[s_][r] <= ops.DEFAULT_SPLIT:
                         ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
-                rels[ce] = (ip, src_loc[r], o_eid[r])
+                rels[ce] = (ip, loc, eid)
             if static:
-                num_dst = {nt: int(sizes[s * NT + t]) + 1 for t, nt in enumerate(nts)}
+                num_dst = {nt: int(sizes[s_ * NT + t]) + 1 for t, nt in enumerate(nts)}
             else:
-                num_dst = {nt: int(sizes[s * NT + t]) for t, nt in enumerate(nts)}
+                num_dst = {nt: sizes[s_ * NT + t] for t, nt in enumerate(nts)}
+                nodes = [n_[:sizes[(s_ + 1) * NT + t]] for t, n_ in enumerate(nodes)]
             b = Block(dict(zip(nts, nodes)), num_dst, rels)
             if static:
                 # the destination ids are the step's seed slots (-1: padding rows, the dump
                 # row last), not the source prefix: a padding row may sit over a real source
                 b.static = True
                 for t, nt in enumerate(nts):
-                    if s == 0:
+                    if s_ == 0:
                         dst_ids = torch.cat([seeds.get(nt, empty), empty.new_full((1,), -1)])
                     else:
-                        dst_ids = steps[s - 1][3][t]
+                        dst_ids = steps[s_ - 1][3][t]
                     b._dst[nt][NID] = dst_ids
             blocks.insert(0, b)
+        for (s_, key, k), t in zip(dests, gathered):
+            b = blocks[L - 1 - s_]
+            if isinstance(key, tuple):  # edge data of relation `key`
+                b._edata[key][k] = t if static else t[:b._rels[key][1].numel()]
+            else:  # input features of node type `key`
+                b._src[key][k] = t if static else t[:b.number_of_src_nodes(key)]
         if transposes:
             for block_id, b in enumerate(blocks):
                 if block_id > 0 or self._first_transposes(b):
@@ -211,7 +242,6 @@ class BlockSampler:
                              "on a HIP device within its limits")
         if self._fused_ok(g):
             blocks = self._sample_fused(g, seeds, exclude_eids, transposes, static_shapes)
-            _copy_block_data(g, blocks)
             for b in blocks:
                 b._sampler = weakref.ref(self)
             return blocks

@@ -658,6 +658,8 @@ typedef struct gnnrec_gather_job {
   int64_t row_bytes;
   void* dst;
   int64_t dst_ld_bytes;
+  const int64_t* n_dev; /* device row count (NULL: n); rows min(*n_dev, n) are gathered, so a
+                         * gather can be queued before the producer's sizes reach the host */
 } gnnrec_gather_job;
 int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_jobs, void* stream);
 int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx, int64_t n,

@@ -14,3 +14,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_capture.py tests/test_gpu_s
 tail -3 $O/tests.log
 timeout -k 10 400 python -u tools/probe_captured_step.py > $O/probe.json 2> $O/probe.err || { echo "probe failed"; tail -30 $O/probe.err; exit 1; }
 cat $O/probe.json
+timeout -k 10 300 python -u tools/minibatch_roofline.py > $O/mb_roof.json 2> $O/mb_roof.err || { echo "mb roofline failed"; tail -20 $O/mb_roof.err; exit 1; }
+cat $O/mb_roof.json
