@@ -46,11 +46,11 @@ static void validation() {
                              nullptr) == GNNREC_EINVAL,
         "cos negative");
   CHECK(gnnrec_sddmm_cos_grouped_f32(nullptr, 4, nullptr, nullptr, 3, nullptr, nullptr, nullptr,
-                                     8, nullptr, 8, 100, 8, nullptr) == GNNREC_EINVAL &&
+                                     8, nullptr, 8, 8, nullptr) == GNNREC_EINVAL &&
             err_has("null pointer"),
         "cos grouped null");
   CHECK(gnnrec_sddmm_cos_grouped_f32(nullptr, 0, nullptr, nullptr, 3, nullptr, nullptr, nullptr,
-                                     8, nullptr, 8, 100, 8, nullptr) == GNNREC_OK,
+                                     8, nullptr, 8, 8, nullptr) == GNNREC_OK,
         "cos grouped empty");
   CHECK(gnnrec_sample_count(nullptr, nullptr, nullptr, nullptr, nullptr, 4, 65, 0, nullptr,
                             nullptr) == GNNREC_EINVAL && err_has("fanout"),

@@ -15,9 +15,7 @@
 //    a 32-wide dot and the sigmoid — the [E, 2d] concatenation of the
 //    reference is never built.
 #include "common.hpp"
-#include <algorithm>
 #include <cmath>
-#include <cstdlib>
 
 namespace gnnrec {
 namespace {
@@ -188,146 +186,6 @@ int launch_cos_grouped(const int64_t* src_g, int64_t G, const int64_t* first, fl
   return check_launch("gnnrec_sddmm_cos_grouped_f32");
 }
 
-// --------------------------------------------- grouped cosine, XCD slices ----
-// The same scores for a destination table too large for one XCD's L2 (C3: 100k x 512 B =
-// 51 MB, so every negative's row came from the Infinity Cache at its random-row rate).  The
-// table's rows are cut into S = 8 P slices of a size an XCD's 4 MiB L2 holds; block b (dealt
-// round-robin over the 8 XCDs, so b and b + 8 share one: MI355X_MICROARCH.md §Workgroup
-// dispatch) takes slice (b mod 8) + 8 (pass), the passes in dispatch order, and scores only
-// the negatives whose row lies in its slice: every XCD gathers from one L2-resident slice at a
-// time, and each chunk's ids are read S times instead (8 B against 4d B per negative).  A
-// wave scans a chunk of kCosXChunk negatives 64 ids at a time, queues its slice's matches in
-// LDS and scores them kCosU per lane group exactly as sddmm_cos_grouped_kernel does (same
-// fragments, same reduction tree, same expression): bitwise the same scores.  Speed only —
-// any placement gives the same results.
-constexpr int kCosXChunk = 512;
-constexpr int64_t kCosSliceBytes = int64_t(3) << 20;  // an XCD's L2 share of the table
-constexpr int kCosMaxPasses = 4;
-
-template <int LPR>
-__global__ __launch_bounds__(256) void sddmm_cos_grouped_xcd_kernel(
-    const int64_t* __restrict__ src_g, int64_t n_groups, const int64_t* __restrict__ first,
-    float* __restrict__ out_first, int64_t K, int64_t chunks, const int64_t* __restrict__ dst,
-    float* __restrict__ out, const float* __restrict__ Hs, int64_t lds,
-    const float* __restrict__ Hd, int64_t ldd, int d, int64_t slice_rows,
-    int64_t blocks_per_pass) {
-  constexpr int NPW = kWave / LPR;
-  constexpr int STEP = NPW * kCosU;  // queued negatives scored per flush (<= 64)
-  static_assert(STEP <= 64, "the queue holds one wave load of ids");
-  __shared__ int32_t q_edge[4][64];
-  __shared__ int32_t q_row[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int grp = lane / LPR;
-  const int gl = lane % LPR;
-  const int64_t pass = blockIdx.x / blocks_per_pass, r = blockIdx.x % blocks_per_pass;
-  const int64_t slice = pass * 8 + r % 8;
-  const int64_t task = (r / 8) * 4 + wv;
-  if (task >= n_groups * chunks) return;  // wave-uniform
-  const int64_t lo = slice * slice_rows, hi = lo + slice_rows;
-  const int64_t g = task / chunks, c = task - g * chunks;
-  const int col = gl * 4;
-  const bool cok = col < d;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  float su = 0.f;
-  if (cok) {
-    a = *reinterpret_cast<const float4*>(Hs + src_g[g] * lds + col);
-    su += dot4(a, a);
-  }
-#pragma unroll
-  for (int off = 1; off < LPR; off <<= 1) su += __shfl_xor(su, off);
-  const float nu = fmaxf(sqrtf(su), 1e-12f);
-  auto score = [&](const float4& b, bool ok) {
-    float dot = 0.f, sv = 0.f;
-    if (ok) {
-      dot += dot4(a, b);
-      sv += dot4(b, b);
-    }
-#pragma unroll
-    for (int off = 1; off < LPR; off <<= 1) {
-      dot += __shfl_xor(dot, off);
-      sv += __shfl_xor(sv, off);
-    }
-    const float nv = fmaxf(sqrtf(sv), 1e-12f);
-    return dot / (nu * nv);
-  };
-  if (c == 0 && first != nullptr) {
-    const int64_t v = first[g];
-    if (v >= lo && v < hi) {  // the group's positive edge, by the wave of its row's slice
-      float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cok) b = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
-      const float rr = score(b, cok);
-      if (lane == 0) out_first[g] = rr;
-    }
-  }
-  int32_t* qe = q_edge[wv];
-  int32_t* qr = q_row[wv];
-  int qlen = 0;
-  const int64_t e_grp = g * K;
-  auto flush = [&](int n) {  // score queue slots [0, n), then move the rest down
-    float4 b[kCosU];
-    int32_t eo[kCosU];
-#pragma unroll
-    for (int k = 0; k < kCosU; ++k) {
-      const int slot = k * NPW + grp;
-      const bool ok = slot < n;
-      eo[k] = ok ? qe[slot] : -1;
-      const int64_t v = ok ? (int64_t)qr[slot] : 0;
-      b[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cok && ok) b[k] = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
-    }
-#pragma unroll
-    for (int k = 0; k < kCosU; ++k) {
-      const float rr = score(b[k], cok && eo[k] >= 0);
-      if (gl == 0 && eo[k] >= 0) out[e_grp + eo[k]] = rr;
-    }
-    const int rest = qlen - n;
-    int32_t te = 0, tr = 0;
-    if (lane < rest) {
-      te = qe[lane + n];
-      tr = qr[lane + n];
-    }
-    if (lane < rest) {
-      qe[lane] = te;
-      qr[lane] = tr;
-    }
-    qlen = rest;
-  };
-  const int64_t e_beg = c * kCosXChunk, e_end = min<int64_t>(K, e_beg + kCosXChunk);
-  for (int64_t e0 = e_beg; e0 < e_end; e0 += 64) {
-    const int64_t e = e0 + lane;
-    const int64_t v = e < e_end ? dst[e_grp + e] : -1;
-    const bool m = v >= lo && v < hi;
-    const uint64_t mask = __ballot(m);
-    const int cnt = __popcll(mask);
-    if (cnt == 0) continue;
-    while (qlen + cnt > 64) flush(qlen < STEP ? qlen : STEP);
-    if (m) {
-      const int at = qlen + __popcll(mask & ((1ull << lane) - 1ull));
-      qe[at] = (int32_t)e;
-      qr[at] = (int32_t)v;
-    }
-    qlen += cnt;
-    while (qlen >= STEP) flush(STEP);
-  }
-  if (qlen > 0) flush(qlen);
-}
-
-template <int LPR>
-int launch_cos_grouped_xcd(const int64_t* src_g, int64_t G, const int64_t* first,
-                           float* out_first, int64_t K, const int64_t* dst, float* out,
-                           const float* Hs, int64_t lds, const float* Hd, int64_t ldd,
-                           int64_t n_rows, int d, int passes, hipStream_t s) {
-  const int64_t chunks = K > 0 ? (K + kCosXChunk - 1) / kCosXChunk : 1;
-  const int64_t tasks = G * chunks;
-  const int64_t slices = 8 * (int64_t)passes;
-  const int64_t slice_rows = (n_rows + slices - 1) / slices;
-  const int64_t per_pass = 8 * ((tasks + 3) / 4);
-  hipLaunchKernelGGL(sddmm_cos_grouped_xcd_kernel<LPR>, dim3((unsigned)(per_pass * passes)),
-                     dim3(256), 0, s, src_g, G, first, out_first, K, chunks, dst, out, Hs, lds,
-                     Hd, ldd, d, slice_rows, per_pass);
-  return check_launch("gnnrec_sddmm_cos_grouped_f32(xcd)");
-}
-
 // ------------------------------------------------------------- edge MLP ----
 // One wave scores 32 edges: A[i][k] = relu(P[src_i][k] + Q[dst_i][k]) (k < 128),
 // B[k][j] = W2[j][k]; lane half h consumes k in [64h, 64h+64).  Output
@@ -406,8 +264,8 @@ extern "C" int gnnrec_sddmm_cos_f32(const int64_t* src, const int64_t* dst, int6
 extern "C" int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_groups,
                                             const int64_t* first, float* out_first, int64_t K,
                                             const int64_t* dst, float* out, const float* Hs,
-                                            int64_t lds, const float* Hd, int64_t ldd,
-                                            int64_t n_rows_d, int64_t d, void* stream) {
+                                            int64_t lds, const float* Hd, int64_t ldd, int64_t d,
+                                            void* stream) {
   using namespace gnnrec;
   GNNREC_REQUIRE(n_groups >= 0 && K >= 0 && d >= 0, "gnnrec_sddmm_cos_grouped_f32: negative size");
   if (n_groups == 0 || (K == 0 && first == nullptr)) return GNNREC_OK;
@@ -420,27 +278,7 @@ extern "C" int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_grou
                  "rows (gnnrec_sddmm_cos_f32 takes the rest)");
   GNNREC_REQUIRE(n_groups * ((K + 255) / 256 + 1) < (int64_t(1) << 32),
                  "gnnrec_sddmm_cos_grouped_f32: too many groups");
-  GNNREC_REQUIRE(n_rows_d >= 0 && n_rows_d < (int64_t(1) << 31),
-                 "gnnrec_sddmm_cos_grouped_f32: destination rows out of int32 range");
   hipStream_t s = as_stream(stream);
-  // a destination table beyond what one XCD's L2 holds: XCD slices (passes of 8 slices of
-  // at most kCosSliceBytes each)
-  const int64_t table = n_rows_d * ldd * 4;
-  if (K >= kCosXChunk && table > kCosSliceBytes) {
-    int passes = (int)std::min<int64_t>(kCosMaxPasses,
-                                        (table + 8 * kCosSliceBytes - 1) / (8 * kCosSliceBytes));
-    if (const char* e = std::getenv("GNNREC_COS_XCD_PASSES")) passes = std::atoi(e);  // A/B only
-    if (passes <= 0) goto plain;
-    if (d <= 64)
-      return launch_cos_grouped_xcd<16>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds,
-                                        Hd, ldd, n_rows_d, (int)d, passes, s);
-    if (d <= 128)
-      return launch_cos_grouped_xcd<32>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds,
-                                        Hd, ldd, n_rows_d, (int)d, passes, s);
-    return launch_cos_grouped_xcd<64>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd,
-                                      ldd, n_rows_d, (int)d, passes, s);
-  }
-plain:
   if (d <= 64)
     return launch_cos_grouped<16>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd, ldd,
                                   (int)d, s);

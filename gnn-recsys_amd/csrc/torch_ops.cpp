@@ -465,7 +465,7 @@ void sddmm_cos_grouped(const Tensor& src_g, const optional<Tensor>& first, int64
   const c10::DeviceGuard g(Hs.device());
   ck(gnnrec_sddmm_cos_grouped_f32(p<int64_t>(src_g), G, p<int64_t>(first), p<float>(out_first),
                                   K, p<int64_t>(dst), p<float>(out), p<float>(Hs), lds,
-                                  p<float>(Hd), ldd, Hd.size(0), Hs.size(1), stream_of(Hs)),
+                                  p<float>(Hd), ldd, Hs.size(1), stream_of(Hs)),
      "gnnrec_sddmm_cos_grouped_f32");
 }
 

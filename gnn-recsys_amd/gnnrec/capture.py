@@ -59,7 +59,10 @@ class CapturedTrainStep:
         self.opt.zero_grad(set_to_none=True)
         loss.backward()
         self.opt.step()
-        return loss
+        # no reference to the step's autograd graph outlives it: a kept graph keeps its
+        # AccumulateGrad nodes (bound to this stream) alive into the capture, whose backward
+        # would then accumulate on the wrong stream
+        return loss.detach()
 
     def _capturable(self):
         for group in self.opt.param_groups:
@@ -78,12 +81,14 @@ class CapturedTrainStep:
         # the step's own ops run at least once outside the capture on this batch's shapes
         # (the warm-up steps), so every lazy allocation / library init has happened
         self.opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             loss = self.loss_fn(self.model, batch)
             loss.backward()
             self.opt.step()
-        self.graph, self.loss = g, loss
+        self.graph, self.loss = g, loss.detach()
+        del loss
         self._batch, self._inputs, self._sig = batch, inputs, _signature(inputs)
 
     def __call__(self, batch):

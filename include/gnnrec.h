@@ -315,13 +315,11 @@ int gnnrec_sddmm_cos_f32(const int64_t* src, const int64_t* dst, int64_t n_edges
  * (src/sampling.py:163-165: every positive edge's source repeated K times): group g = source
  * src_g[g], its positive edge to first[g] (may be NULL) -> out_first[g], and its K negatives
  * to dst[g K + j] -> out[g K + j].  One gathered row per edge; bitwise the scores of
- * gnnrec_sddmm_cos_f32 on the expanded edge lists.  d % 4 == 0, d <= 256, 16-B aligned.
- * n_rows_d: Hd's row count — a table larger than an XCD's L2 share is scored in XCD slices
- * (each XCD gathers from an L2-resident slice of the rows at a time; the same bits). */
+ * gnnrec_sddmm_cos_f32 on the expanded edge lists.  d % 4 == 0, d <= 256, 16-B aligned. */
 int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_groups, const int64_t* first,
                                  float* out_first, int64_t K, const int64_t* dst, float* out,
                                  const float* Hs, int64_t lds, const float* Hd, int64_t ldd,
-                                 int64_t n_rows_d, int64_t d, void* stream);
+                                 int64_t d, void* stream);
 
 /* ---- a8: PredictingLayer over gathered edge endpoints (K6) ---------------
  * P = Hs W1a^T + b1 and Q = Hd W1b^T are precomputed per node by gnnrec_gemm_f32

@@ -1712,33 +1712,6 @@ def test_sddmm_cos_grouped_bitwise_equals_per_edge_and_oracle(d):
         np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
 
 
-@pytest.mark.parametrize("d,n_d,passes", [(64, 40000, None), (128, 30000, None),
-                                           (64, 110000, None), (32, 20000, "3")])
-def test_sddmm_cos_grouped_xcd_slices_bitwise(monkeypatch, d, n_d, passes):
-    """Destination tables beyond an XCD's L2 share (>3 MB) are scored in XCD slices (each
-    block one slice of the rows, its chunk's ids filtered into an LDS queue): the same bits
-    as the per-edge kernel — slices of 1..3 passes, chunk tails, queue flushes of partial
-    steps, positive edges in any slice, rows at the slice bounds."""
-    from gnnrec import ops
-    if passes:
-        monkeypatch.setenv("GNNREC_COS_XCD_PASSES", passes)
-    rng = np.random.default_rng(n_d + d)
-    hs = rng.standard_normal((50, d)).astype(np.float32)
-    hd = rng.standard_normal((n_d, d)).astype(np.float32)
-    hd[n_d - 1] = 0
-    for G, K in ((7, 512), (11, 700), (3, 2500), (5, 1537)):
-        src_g = rng.integers(0, 50, G)
-        first = rng.integers(0, n_d, G)
-        first[0] = n_d - 1
-        dst = rng.integers(0, n_d, G * K)
-        dst[:64] = rng.integers(0, 64, 64)          # one slice's ids: a full queue at once
-        dst[64:70] = n_d - 1
-        pos, neg = ops.sddmm_cos_grouped(_t(src_g), _t(first), K, _t(dst), _t(hs), _t(hd))
-        src = np.concatenate([src_g, np.repeat(src_g, K)])
-        ref = ops.sddmm_cos(_t(src), _t(np.concatenate([first, dst])), _t(hs), _t(hd))
-        assert torch.equal(pos, ref[:G]) and torch.equal(neg, ref[G:]), (G, K)
-
-
 def test_cosine_pair_head_grouped_path_forward_and_gradients():
     """CosinePrediction.pair on a negative graph marked by the loader (src_repeats_pos = K)
     takes the grouped launch: the same scores and the same gradients as the unmarked graph."""
