@@ -549,11 +549,18 @@ __global__ __launch_bounds__(256) void plan_mark_kernel(const int64_t* __restric
   }
 }
 
+// the plan's two counts zeroed by a kernel, not hipMemsetAsync: the plan is rebuilt inside
+// captured training steps (gnnrec.capture), and a kernel node re-runs on every replay
+__global__ void plan_zero_kernel(int64_t* __restrict__ plan) {
+  if (threadIdx.x < 2) plan[threadIdx.x] = 0;
+}
+
 // one block: chunk_ptr = exclusive scan of ceil(deg/split) over the heavy rows, then
-// chunk_row[c] = owning heavy row
+// chunk_row[c] = owning heavy row (at most cap_c chunks: the host's bound from the edge
+// count, enforced here too so a CSR that breaks it cannot write past the plan)
 __global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __restrict__ indptr,
                                                            int64_t split, int64_t* __restrict__ plan,
-                                                           int64_t cap_h) {
+                                                           int64_t cap_h, int64_t cap_c) {
   __shared__ int64_t buf[1024];
   int64_t* heavy_rows = plan + 2;
   int64_t* chunk_ptr = heavy_rows + cap_h;
@@ -584,27 +591,34 @@ __global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __rest
     plan[1] = carry;
   }
   __syncthreads();
-  for (int64_t h = t; h < n; h += 1024)
-    for (int64_t c = chunk_ptr[h]; c < chunk_ptr[h + 1]; ++c) chunk_row[c] = h;
+  for (int64_t h = t; h < n; h += 1024) {
+    const int64_t c1 = chunk_ptr[h + 1] < cap_c ? chunk_ptr[h + 1] : cap_c;
+    for (int64_t c = chunk_ptr[h]; c < c1; ++c) chunk_row[c] = h;
+  }
+  if (t == 0) {  // counts past the capacities (a CSR breaking the bounds) are clipped
+    if (carry > cap_c) plan[1] = cap_c;
+    if (plan[0] > cap_h) plan[0] = cap_h;
+  }
 }
 
 }  // namespace
 }  // namespace gnnrec
 
 extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split,
-                                      int64_t cap_h, int64_t* plan, void* stream) {
+                                      int64_t cap_h, int64_t cap_c, int64_t* plan, void* stream) {
   using namespace gnnrec;
-  GNNREC_REQUIRE(n_dst >= 0 && split > 0 && cap_h >= 0, "gnnrec_spmm_plan_build: bad sizes");
+  GNNREC_REQUIRE(n_dst >= 0 && split > 0 && cap_h >= 0 && cap_c >= 0,
+                 "gnnrec_spmm_plan_build: bad sizes");
   GNNREC_REQUIRE(indptr && plan, "gnnrec_spmm_plan_build: null pointer");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(plan, 0, 2 * sizeof(int64_t), s) != hipSuccess)
-    return check_launch("gnnrec_spmm_plan_build");
+  hipLaunchKernelGGL(plan_zero_kernel, dim3(1), dim3(64), 0, s, plan);
   if (n_dst > 0 && cap_h > 0) {
     int64_t blocks = (n_dst + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(plan_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, s, indptr, n_dst,
                        split, cap_h, reinterpret_cast<unsigned long long*>(plan), plan + 2);
-    hipLaunchKernelGGL(plan_chunks_kernel, dim3(1), dim3(1024), 0, s, indptr, split, plan, cap_h);
+    hipLaunchKernelGGL(plan_chunks_kernel, dim3(1), dim3(1024), 0, s, indptr, split, plan, cap_h,
+                       cap_c);
   }
   return check_launch("gnnrec_spmm_plan_build");
 }

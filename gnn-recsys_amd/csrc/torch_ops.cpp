@@ -168,9 +168,11 @@ void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor&
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(plan, "plan", at::kLong);
+  const int64_t cap_c = plan.numel() - (3 + 2 * cap_h);  // plan = {2 | cap_h | cap_h+1 | cap_c}
+  TORCH_CHECK_VALUE(cap_h >= 0 && cap_c >= 0, "spmm_plan_build: plan shorter than 3 + 2 cap_h");
   if (meta(indptr)) return;
   const c10::DeviceGuard g(indptr.device());
-  ck(gnnrec_spmm_plan_build(p<int64_t>(indptr), indptr.numel() - 1, split, cap_h,
+  ck(gnnrec_spmm_plan_build(p<int64_t>(indptr), indptr.numel() - 1, split, cap_h, cap_c,
                             p<int64_t>(plan), stream_of(indptr)),
      "gnnrec_spmm_plan_build");
 }
@@ -855,7 +857,7 @@ void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const T
   }
   const int64_t cap_c = nnz / kSplit + cap_h;
   Tensor plan = at::empty({2 + cap_h + cap_h + 1 + cap_c}, ip.options());
-  ck(gnnrec_spmm_plan_build(p<int64_t>(ip), n, kSplit, cap_h, p<int64_t>(plan), s),
+  ck(gnnrec_spmm_plan_build(p<int64_t>(ip), n, kSplit, cap_h, cap_c, p<int64_t>(plan), s),
      "gnnrec_spmm_plan_build");
   Tensor wsp = at::empty({cap_c, d}, X.options());
   ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),

@@ -212,7 +212,7 @@ int run_side(const int64_t* keys, const int64_t* other, const float* g, int64_t 
   hipLaunchKernelGGL(cos_permute_kernel, dim3(flat_grid(E)), dim3(256), 0, s, perm, other, g,
                      inv_other, E, ix, w);
   if (c.cap_h > 0) {
-    rc = gnnrec_spmm_plan_build(indptr, n_rows, kCosSplit, c.cap_h, plan, s);
+    rc = gnnrec_spmm_plan_build(indptr, n_rows, kCosSplit, c.cap_h, c.cap_c, plan, s);
     if (rc != GNNREC_OK) return rc;
     rc = gnnrec_spmm_csr_planned_f32(indptr, ix, w, O, ldo, n_rows, d, GNNREC_REDUCE_SUM, 0, G,
                                      d, kCosSplit, plan, c.cap_h, c.cap_c, chunk_ws, s);

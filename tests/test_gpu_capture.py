@@ -133,17 +133,24 @@ def _close(a, b, what, rtol=2e-4, atol=2e-6):
     torch.testing.assert_close(a, b, rtol=rtol, atol=atol, msg=what)
 
 
-@pytest.mark.parametrize("agg,fold", [("mean", "0"), ("mean", "1"), ("mean_nn_edge", "auto")])
-def test_static_step_trains_as_the_exact_step(monkeypatch, agg, fold):
+@pytest.mark.parametrize("agg,fold,fanouts", [("mean", "0", (4, 3)), ("mean", "1", (4, 3)),
+                                              ("mean_nn_edge", "auto", (4, 3)),
+                                              ("mean", "0", (64, 64)), ("mean", "1", (64, 64))])
+def test_static_step_trains_as_the_exact_step(monkeypatch, agg, fold, fanouts):
     """One step over the static batch and over the exact one: the same loss and gradients
-    (fp32 rounding: the weight-gradient GEMMs sum over the padding rows' zeros too)."""
+    (fp32 rounding: the weight-gradient GEMMs sum over the padding rows' zeros too).  Fanout
+    64 on this graph leaves dump rows of more than 2048 edges: the heavy-row plans of the
+    forward gather and of the transposed backward gather are built on the device."""
     monkeypatch.setenv("GNNREC_TRAIN_FOLD", fold)
     g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
     K = 4
     batches = []
     for static in (False, True):
         torch.manual_seed(3)
-        batches.append(next(iter(_loader(g, static, K=K))))
+        batches.append(next(iter(_loader(g, static, K=K, fanouts=fanouts))))
+    heavy = [ip._gnnrec_nnz for b in batches[1][-1] for ip, _l, _e in b._rels.values()]
+    if fanouts[0] == 64:  # the dump rows need the planned gathers here
+        assert max(heavy) > 2 * 2048
     base = _model(g, agg=agg).train()
     grads = []
     for batch in batches:
@@ -159,8 +166,8 @@ def test_static_step_trains_as_the_exact_step(monkeypatch, agg, fold):
         _close(gb[n], ga[n], n)
 
 
-@pytest.mark.parametrize("nw", [0, 2])
-def test_captured_steps_train_as_the_eager_loop(nw):
+@pytest.mark.parametrize("nw,fanouts", [(0, (4, 3)), (2, (4, 3)), (0, (64, 64))])
+def test_captured_steps_train_as_the_eager_loop(nw, fanouts):
     """CapturedTrainStep over a static loader (warm-up steps, capture, replays, the exact
     partial batch eagerly) against the eager loop over the exact loader: per-step losses and
     the final parameters agree."""
@@ -179,7 +186,8 @@ def test_captured_steps_train_as_the_eager_loop(nw):
         # eagerly, replays again (further on, a hinge of the margin loss flipped by the two
         # runs' fp32 rounding differences moves the losses apart by one term)
         for epoch in range(2):
-            for k, batch in enumerate(_loader(g, captured, K=K, nw=nw if captured else 0)):
+            for k, batch in enumerate(_loader(g, captured, K=K, fanouts=fanouts,
+                                              nw=nw if captured else 0)):
                 if epoch == 0 or k < 3:
                     loss = step(batch) if captured else step.eager(batch)
                     losses.append(float(loss.detach()))
