@@ -24,8 +24,8 @@
 //     so a training step over it can be captured into a hipGraph.  Seed slots holding -1
 //     (a suffix) are padding rows; each block gets one extra "dump" row per destination
 //     type (index seed_cap): a padding row holds `fanout` padding edges, the dump row the
-//     rest of the edge capacity, every padding edge from the source list's last slot
-//     (node_cap - 1, always -1) with eid -1.  The source list is the exact one — the real
+//     rest of the edge capacity, every padding edge from one of the source list's padding
+//     slots (past the real sources; node_cap - 1 always is one) with eid -1.  The source list is the exact one — the real
 //     seeds, the new sources after them, at the same positions — then -1 up to node_cap + 1
 //     entries: the last is the next block's dump row (its index there is its seed_cap), so
 //     a layer's output rows are the next block's source rows.  A padding row may sit over a
@@ -322,6 +322,14 @@ __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint
   return n_p + T.word_rank[w] + __popcll(T.bits_cur[w] & ((1ull << (s & 63)) - 1ull));
 }
 
+// static shapes: the source slot of padding edge k — spread over the list's padding slots
+// [real sources, node_cap + 1), all -1, so the backward's transposed block has no single
+// source row holding every padding edge (a radix sort's worst case, and a heavy row)
+__device__ __forceinline__ int32_t pad_src(const TypeArgs& S, int64_t k) {
+  const int64_t real = *S.n_seeds + S.word_rank[S.words];
+  return (int32_t)(real + k % (S.node_len - real));
+}
+
 __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
   const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (i >= seed_rows(A, D) || j >= R.counts[i]) return;
       const int64_t o = R.out_indptr[i] + j;
       if (D.seeds[i] < 0) {  // a padding row's padding edge
-        R.out_src[o] = (int32_t)(S.node_cap - 1);
+        R.out_src[o] = pad_src(S, o);
         R.out_eid[o] = -1;
         break;
       }
@@ -347,7 +355,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       const RelArgs& R = A.rel[x];
       const int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t;
       if (e >= R.edge_cap) return;
-      R.out_src[e] = (int32_t)(A.type[R.src_t].node_cap - 1);
+      R.out_src[e] = pad_src(A.type[R.src_t], e);
       R.out_eid[e] = -1;
       break;
     }

@@ -15,6 +15,8 @@ batch's tensors into the captured batch's buffers (one torch._foreach_copy_) and
 Eager steps: the first `warmup` static batches (lazy initialisation, the model's and the
 sampler's settled choices, e.g. the first-layer fold), and every batch whose structure
 differs from the captured one (a final partial batch comes in the exact, non-static form).
+A new structure seen on `recapture_after` batches in a row is captured in place of the old
+(the batches a prefetching loader built before such a choice settled run eagerly).
 The optimizer must keep its step counts on the device (Adam / AdamW with fused=True or
 capturable=True); its param groups are switched to capturable at capture.  Between steps
 the gradients live in the graph's memory: do not zero or replace them (the graph overwrites
@@ -40,9 +42,12 @@ def _signature(tensors):
 class CapturedTrainStep:
     """loss_fn(model, batch) -> scalar loss: the step's forward (model + loss)."""
 
-    def __init__(self, model, optimizer, loss_fn, warmup: int = 2):
+    def __init__(self, model, optimizer, loss_fn, warmup: int = 2, recapture_after: int = 2):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.warmup = int(warmup)
+        self.recapture_after = int(recapture_after)
+        self._new_sig, self._new_seen = None, 0
+        self.captures = 0
         self.graph = None
         self.loss = None
         self._batch = None   # the captured batch: its tensors are the graph's inputs
@@ -90,6 +95,7 @@ class CapturedTrainStep:
         self.graph, self.loss = g, loss.detach()
         del loss
         self._batch, self._inputs, self._sig = batch, inputs, _signature(inputs)
+        self.captures += 1
 
     def __call__(self, batch):
         if not batch_is_static(batch):
@@ -98,10 +104,17 @@ class CapturedTrainStep:
         if self.seen <= self.warmup:
             return self.eager(batch)
         inputs = [t for t in _tensors(batch, []) if t.is_cuda]
+        sig = None if self.graph is None else _signature(inputs)
+        if self.graph is not None and sig != self._sig:
+            if sig != self._new_sig:
+                self._new_sig, self._new_seen = sig, 0
+            self._new_seen += 1
+            if self._new_seen < self.recapture_after:
+                return self.eager(batch)
+            self.graph = None  # the new structure has settled: capture it instead
+        self._new_sig, self._new_seen = None, 0
         if self.graph is None:
             self._capture(batch, inputs)  # records only: the replay below runs the step
-        elif _signature(inputs) != self._sig:
-            return self.eager(batch)
         else:
             torch._foreach_copy_(self._inputs, inputs)
         self.graph.replay()

@@ -578,6 +578,9 @@ class CosinePrediction(nn.Module):
 class ConvModel(nn.Module):
     """Embedding layers + ConvLayers + prediction head (src/model.py:330-470)."""
 
+    # None: GNNREC_TRAIN_FOLD decides ('auto' by default); '0' / '1' / 'auto' for this model
+    train_fold = None
+
     def __init__(self, g, n_layers: int, dim_dict, norm: bool = True, dropout: float = 0.0,
                  aggregator_type: str = 'mean', pred: str = 'cos',
                  aggregator_hetero: str = 'sum', embedding_layer: bool = True):
@@ -645,8 +648,9 @@ class ConvModel(nn.Module):
         per step, which a host-bound small step pays (C2 at K = 10: 2.62 → 2.92 ms without the
         sampling thread) and a GPU-bound large one recovers several times over (K = 2500:
         4.3 → 3.46 ms; profiles/r04h_train_fold_ab.md, r04l_k10_fold_ab.md); '1' always, '0'
-        never (embed, then aggregate)."""
-        mode = os.environ.get("GNNREC_TRAIN_FOLD", "auto")
+        never (embed, then aggregate).  `model.train_fold` overrides the variable for one model
+        (a captured step, whose host cost is gone, folds every block: '1')."""
+        mode = self.train_fold or os.environ.get("GNNREC_TRAIN_FOLD", "auto")
         if mode == "0" or not blocks or \
                 not getattr(blocks[0], 'is_block', False) or not isinstance(
                     self.layers[0], HeteroGraphConv) or not _grad_mode(module=self):

@@ -402,8 +402,9 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * slots holding -1 are padding rows and form a suffix (step 0's seeds: the batch padded to
  * a fixed count).  Each destination type gets one more row, the dump row at index
  * seed_cap: out_indptr holds seed_cap + 2 entries.  A padding row holds `fanout` padding
- * edges, the dump row the rest of the edge capacity; every padding edge comes from the
- * source list's slot node_cap - 1 (always -1) with eid -1.  The source list holds the
+ * edges, the dump row the rest of the edge capacity; every padding edge comes from a
+ * padding slot of the source list (past its real sources, spread evenly; node_cap - 1 always
+ * is one) with eid -1.  The source list holds the
  * exact call's list (real seeds, then the new sources, at the same positions and local
  * ids), then -1 up to node_cap + 1 entries: the last is the next step's dump row (its index
  * there, seed_cap, is this step's node_cap), so one layer's output rows are exactly the
