@@ -81,8 +81,8 @@ static void sampler_plans() {
   int64_t edge[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_RELS];
   int64_t node[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
   int64_t ws = -1;
-  CHECK(gnnrec_sample_blocks_caps(nullptr, seed, edge, node, &ws) == GNNREC_EINVAL, "null plan");
-  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL, "zero types");
+  CHECK(gnnrec_sample_blocks_caps(nullptr, seed, edge, node, nullptr, &ws) == GNNREC_EINVAL, "null plan");
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, nullptr, &ws) == GNNREC_EINVAL, "zero types");
   std::srand(5);
   for (int it = 0; it < 2000; ++it) {
     std::memset(&P, 0, sizeof(P));
@@ -98,7 +98,7 @@ static void sampler_plans() {
       P.rel[r].dst_type = std::rand() % P.n_types;
       for (int s = 0; s < P.n_steps; ++s) P.fanout[s][r] = std::rand() % 65;
     }
-    CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_OK, "plan");
+    CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, nullptr, &ws) == GNNREC_OK, "plan");
     for (int s = 0; s < P.n_steps; ++s) {
       for (int r = 0; r < P.n_rels; ++r)
         CHECK(edge[s * GNNREC_SB_MAX_RELS + r] ==
@@ -124,11 +124,11 @@ static void sampler_plans() {
   P.n_rels = 1;
   P.n_steps = 1;
   P.fanout[0][0] = 65;
-  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL && err_has("fanout"),
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, nullptr, &ws) == GNNREC_EINVAL && err_has("fanout"),
         "fanout bound");
   P.fanout[0][0] = 3;
   P.rel[0].dst_type = 2;
-  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, &ws) == GNNREC_EINVAL, "type range");
+  CHECK(gnnrec_sample_blocks_caps(&P, seed, edge, node, nullptr, &ws) == GNNREC_EINVAL, "type range");
   P.rel[0].dst_type = 0;
   P.stamp = 0;
   CHECK(gnnrec_sample_blocks(&P, nullptr) == GNNREC_EINVAL && err_has("stamp"), "stamp 0");

@@ -22,14 +22,17 @@
 //     sizes every block (the per-layer path read back twice per layer).
 //   * static shapes (plan.static_shapes): every block at its capacity, nothing to read back,
 //     so a training step over it can be captured into a hipGraph.  Seed slots holding -1
-//     (a suffix) are padding rows; each block gets one extra "dump" row per destination
-//     type (index seed_cap): a padding row holds `fanout` padding edges, the dump row the
-//     rest of the edge capacity, every padding edge from one of the source list's padding
-//     slots (past the real sources; node_cap - 1 always is one) with eid -1.  The source list is the exact one — the real
-//     seeds, the new sources after them, at the same positions — then -1 up to node_cap + 1
-//     entries: the last is the next block's dump row (its index there is its seed_cap), so
-//     a layer's output rows are the next block's source rows.  A padding row may sit over a
-//     real source's slot: its output is garbage no real row reads, and its gradient is 0.
+//     (a suffix) are padding rows; after the seed rows each block gets D "dump" rows per
+//     destination type, D = 1 + ceil(edge_cap / kDumpEdges) over the relations into it: a
+//     padding row holds `fanout` padding edges, the dump rows the rest of the edge capacity
+//     in runs of at most kDumpEdges (so no row is heavier than a heavy-row split: no plan,
+//     no serial row anywhere), every padding edge from one of the source list's padding
+//     slots (past the real sources, spread evenly; node_cap - 1 always is one) with eid -1.
+//     The source list is the exact one — the real seeds, the new sources after them, at
+//     the same positions — then -1 up to node_cap + D' entries, D' the next block's dump
+//     rows (their index there starts at its seed_cap = this node_cap), so a layer's output
+//     rows are the next block's source rows.  A padding row may sit over a real source's
+//     slot: its output is garbage no real row reads, and its gradient is 0.
 #include "common.hpp"
 #include "sampler.hpp"
 
@@ -37,6 +40,7 @@ namespace gnnrec {
 namespace {
 
 constexpr int kSbBlock = 256;
+constexpr int64_t kDumpEdges = 2048;  // a static block's dump row: at most ops.DEFAULT_SPLIT
 constexpr int kScanThreads = 1024;
 constexpr int kMaxSec = 4 * GNNREC_SB_MAX_TYPES + 2 * GNNREC_SB_MAX_RELS;
 
@@ -56,7 +60,8 @@ struct RelArgs {
   int32_t* out_src;
   int64_t* out_eid;
   int64_t* edge_total;  // sizes entry
-  int64_t edge_cap;     // static shapes: the block's edge count (the dump row ends there)
+  int64_t edge_cap;     // static shapes: the block's edge count (the dump rows end there)
+  int64_t dump_rows;    // static shapes: the destination type's dump rows
   // exclusion flags set by begin, cleared by the last finalize
   const int64_t* excl_eids;
   int64_t n_excl;
@@ -79,7 +84,7 @@ struct TypeArgs {
   int64_t* n_nodes_out;    // sizes entry
   int64_t n_seeds_host;    // begin only: the batch's seed count
   int64_t node_cap;        // static shapes: the source list's length
-  int64_t node_len;        // static shapes: node_cap + 1 (the next block's dump row, -1)
+  int64_t node_len;        // static shapes: node_cap + the next block's dump rows (all -1)
 };
 
 // sections of one launch: block ranges [begin[k], begin[k+1]) run job kind[k] on index idx[k]
@@ -300,11 +305,16 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
     }
     carry += tot;
   }
+  if (is_rel && A.stat) {  // the dump rows' bounds: runs of kDumpEdges up to the capacity
+    const RelArgs& R = A.rel[seg];
+    for (int64_t j = 1 + threadIdx.x; j < R.dump_rows; j += kScanThreads)
+      out[n + 1 + j] = min(carry + (j + 1) * kDumpEdges, R.edge_cap);
+  }
   if (threadIdx.x == 0) {
     out[n] = carry;
     if (is_rel) {
       *A.rel[seg].edge_total = carry;
-      if (A.stat) out[n + 1] = A.rel[seg].edge_cap;  // the dump row takes the rest
+      if (A.stat) out[n + 1] = min(carry + kDumpEdges, A.rel[seg].edge_cap);
     } else {
       const TypeArgs& T = A.type[seg - A.n_rels];
       *T.n_nodes_out = *T.n_seeds + carry;
@@ -351,7 +361,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       R.out_eid[o] = R.pick_eid[t];
       break;
     }
-    case kSecDumpEdges: {  // static shapes: the edge capacity's rest -> the dump row
+    case kSecDumpEdges: {  // static shapes: the edge capacity's rest -> the dump rows
       const RelArgs& R = A.rel[x];
       const int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t;
       if (e >= R.edge_cap) return;
@@ -504,6 +514,8 @@ struct Caps {
   int64_t seed[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
   int64_t edge[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   int64_t node[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
+  int64_t dump[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];  // static: dump rows per dst type
+  int64_t len[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];   // static: node list lengths
   int64_t ws_bytes;
 };
 
@@ -553,6 +565,18 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
       if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
     }
   }
+  for (int s = 0; s < P->n_steps; ++s)
+    for (int t = 0; t < P->n_types; ++t) {
+      int64_t dmax = 0;
+      for (int r = 0; r < P->n_rels; ++r)
+        if (P->rel[r].dst_type == t)
+          dmax = std::max<int64_t>(dmax, (C->edge[s][r] + kDumpEdges - 1) / kDumpEdges);
+      C->dump[s][t] = P->static_shapes ? 1 + dmax : 0;
+    }
+  for (int s = 0; s < P->n_steps; ++s)
+    for (int t = 0; t < P->n_types; ++t)
+      C->len[s][t] = C->node[s][t] +
+                     (P->static_shapes ? (s + 1 < P->n_steps ? C->dump[s + 1][t] : 1) : 0);
   C->ws_bytes = ws;
   return GNNREC_OK;
 }
@@ -564,13 +588,14 @@ using namespace gnnrec;
 
 extern "C" int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
                                          int64_t* edge_cap, int64_t* node_cap,
-                                         int64_t* workspace_bytes) {
+                                         int64_t* dump_rows, int64_t* workspace_bytes) {
   Caps C{};
   if (int st = plan_caps(plan, &C)) return st;
   for (int s = 0; s < GNNREC_SB_MAX_STEPS; ++s) {
     for (int t = 0; t < GNNREC_SB_MAX_TYPES; ++t) {
       if (seed_cap) seed_cap[s * GNNREC_SB_MAX_TYPES + t] = C.seed[s][t];
       if (node_cap) node_cap[s * GNNREC_SB_MAX_TYPES + t] = C.node[s][t];
+      if (dump_rows) dump_rows[s * GNNREC_SB_MAX_TYPES + t] = C.dump[s][t];
     }
     for (int r = 0; r < GNNREC_SB_MAX_RELS; ++r)
       if (edge_cap) edge_cap[s * GNNREC_SB_MAX_RELS + r] = C.edge[s][r];
@@ -650,7 +675,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.nodes = P->nodes[s][t];
       a.n_nodes_out = node_count + (int64_t)(s + 1) * T + t;
       a.node_cap = C.node[s][t];
-      a.node_len = C.node[s][t] + 1;
+      a.node_len = C.len[s][t];
     }
     for (int r = 0; r < R; ++r) {
       const gnnrec_sample_rel& re = P->rel[r];
@@ -672,6 +697,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.out_eid = P->out_eid[s][r];
       a.edge_total = edge_count + (int64_t)s * R + r;
       a.edge_cap = C.edge[s][r];
+      a.dump_rows = C.dump[s][re.dst_type];
       a.excl_eids = re.excl_eids;
       a.n_excl = re.n_excl;
       a.coo_dst = re.coo_dst;
@@ -736,7 +762,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     if (P->static_shapes) {
       for (int r = 0; r < R; ++r) add_sec(A.sec, kSecDumpEdges, r, nblocks(C.edge[s][r]));
       for (int t = 0; t < T; ++t)
-        add_sec(A.sec, kSecPadNodes, t, nblocks(C.node[s][t] + 1));
+        add_sec(A.sec, kSecPadNodes, t, nblocks(C.len[s][t]));
     }
     if (A.sec.n) {
       hipLaunchKernelGGL(sb_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock),

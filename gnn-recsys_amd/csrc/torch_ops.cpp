@@ -1616,9 +1616,16 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   int64_t seed_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
   int64_t edge_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_RELS];
   int64_t node_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
+  int64_t dump_rows[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
   int64_t ws_bytes = 0;
-  ck(gnnrec_sample_blocks_caps(&P, seed_cap, edge_cap, node_cap, &ws_bytes),
+  ck(gnnrec_sample_blocks_caps(&P, seed_cap, edge_cap, node_cap, dump_rows, &ws_bytes),
      "gnnrec_sample_blocks_caps");
+  // static shapes: a node list also holds the next step's dump rows (the last step: one)
+  auto node_len = [&](int64_t s, size_t t) {
+    if (!static_shapes) return node_cap[s * GNNREC_SB_MAX_TYPES + t];
+    return node_cap[s * GNNREC_SB_MAX_TYPES + t] +
+           (s + 1 < steps ? dump_rows[(s + 1) * GNNREC_SB_MAX_TYPES + t] : 1);
+  };
   const c10::DeviceGuard g(pos[0].device());
   const auto i64 = pos[0].options();
   std::vector<Tensor> o_ip(steps * R), o_src(steps * R), o_eid(steps * R), nodes(steps * NT);
@@ -1626,7 +1633,8 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     for (size_t r = 0; r < R; ++r) {
       const int64_t sc = seed_cap[s * GNNREC_SB_MAX_TYPES + dst_type[r]];
       const int64_t ec = edge_cap[s * GNNREC_SB_MAX_RELS + r];
-      o_ip[s * R + r] = at::empty({sc + (static_shapes ? 2 : 1)}, i64);
+      o_ip[s * R + r] = at::empty(
+          {sc + 1 + (static_shapes ? dump_rows[s * GNNREC_SB_MAX_TYPES + dst_type[r]] : 0)}, i64);
       o_src[s * R + r] = at::empty({ec}, i64.dtype(at::kInt));
       o_eid[s * R + r] = at::empty({ec}, i64);
       P.out_indptr[s][r] = p<int64_t>(o_ip[s * R + r]);
@@ -1634,8 +1642,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
       P.out_eid[s][r] = p<int64_t>(o_eid[s * R + r]);
     }
     for (size_t t = 0; t < NT; ++t) {
-      nodes[s * NT + t] =
-          at::empty({node_cap[s * GNNREC_SB_MAX_TYPES + t] + (static_shapes ? 1 : 0)}, i64);
+      nodes[s * NT + t] = at::empty({node_len(s, t)}, i64);
       P.nodes[s][t] = p<int64_t>(nodes[s * NT + t]);
     }
   }
@@ -1653,12 +1660,14 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   P.workspace = ws.data_ptr();
   ck(gnnrec_sample_blocks(&P, stream_of(pos[0])), "gnnrec_sample_blocks");
   if (static_shapes || has(sizes_out)) {  // every output at its capacity: return those
-    std::vector<int64_t> caps;
-    for (size_t t = 0; t < NT; ++t) caps.push_back(seed_cap[t]);
+    std::vector<int64_t> caps;  // seed caps [T], node caps [L x T], edge caps [L x R], and
+    for (size_t t = 0; t < NT; ++t) caps.push_back(seed_cap[t]);  // dump rows [L x T]
     for (int64_t s = 0; s < steps; ++s)
       for (size_t t = 0; t < NT; ++t) caps.push_back(node_cap[s * GNNREC_SB_MAX_TYPES + t]);
     for (int64_t s = 0; s < steps; ++s)
       for (size_t r = 0; r < R; ++r) caps.push_back(edge_cap[s * GNNREC_SB_MAX_RELS + r]);
+    for (int64_t s = 0; s < steps; ++s)
+      for (size_t t = 0; t < NT; ++t) caps.push_back(dump_rows[s * GNNREC_SB_MAX_TYPES + t]);
     return {o_ip, o_src, o_eid, nodes, caps};
   }
   const Tensor hs = sizes.to(at::kCPU);  // the call's one size readback

@@ -118,9 +118,10 @@ class BlockSampler:
         all L blocks (bitwise the blocks of the per-layer path, _one_block).
 
         static: the blocks at their capacities, nothing read back (include/gnnrec.h, static
-        shapes): seeds may hold -1 padding; block s has seed_cap + 1 destination rows per
-        type (the last is the dump row) and node_cap + 1 source rows (the last is the next
-        block's dump row), so every layer's output is the next block's source table."""
+        shapes): seeds may hold -1 padding; block s has seed_cap + D destination rows per
+        type (the last D are its dump rows, at most 2048 edges each) and node_cap + D'
+        source rows (the last D' are the next block's dump rows), so every layer's output is
+        the next block's source table."""
         ces, nts = list(g.canonical_etypes), list(g.ntypes)
         tix = {nt: i for i, nt in enumerate(nts)}
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
@@ -182,9 +183,10 @@ class BlockSampler:
             rels = {}
             for r, ce in enumerate(ces):
                 ip, loc, eid = o_ip[r], src_loc[r], o_eid[r]
-                if static:  # sizes = seed caps, node caps [L x T], edge caps [L x R]
+                if static:  # sizes = seed caps, node caps [L x T], edge caps [L x R], dump rows
                     ip._gnnrec_nnz = int(sizes[NT + L * NT + s_ * R + r])
-                    ip._gnnrec_heavy = ip._gnnrec_nnz  # the dump row: any length
+                    if 0 <= fans[s_][r] <= ops.DEFAULT_SPLIT:  # dump rows: <= 2048 edges
+                        ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)
                 else:
                     ne = sizes[(L + 1) * NT + s_ * R + r]
                     ip = ip[:sizes[s_ * NT + tix[ce[2]]] + 1]
@@ -194,18 +196,20 @@ class BlockSampler:
                         ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
                 rels[ce] = (ip, loc, eid)
             if static:
-                num_dst = {nt: int(sizes[s_ * NT + t]) + 1 for t, nt in enumerate(nts)}
+                dump = [int(sizes[NT + L * NT + L * R + s_ * NT + t]) for t in range(NT)]
+                num_dst = {nt: int(sizes[s_ * NT + t]) + dump[t] for t, nt in enumerate(nts)}
             else:
                 num_dst = {nt: sizes[s_ * NT + t] for t, nt in enumerate(nts)}
                 nodes = [n_[:sizes[(s_ + 1) * NT + t]] for t, n_ in enumerate(nodes)]
             b = Block(dict(zip(nts, nodes)), num_dst, rels)
             if static:
                 # the destination ids are the step's seed slots (-1: padding rows, the dump
-                # row last), not the source prefix: a padding row may sit over a real source
+                # rows last), not the source prefix: a padding row may sit over a real source
                 b.static = True
                 for t, nt in enumerate(nts):
                     if s_ == 0:
-                        dst_ids = torch.cat([seeds.get(nt, empty), empty.new_full((1,), -1)])
+                        dst_ids = torch.cat([seeds.get(nt, empty),
+                                             empty.new_full((dump[t],), -1)])
                     else:
                         dst_ids = steps[s_ - 1][3][t]
                     b._dst[nt][NID] = dst_ids

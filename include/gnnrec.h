@@ -400,18 +400,20 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * Static shapes (static_shapes = 1): every output at its capacity and nothing to read back,
  * so the call (and a training step over its blocks) can be captured into a hipGraph.  Seed
  * slots holding -1 are padding rows and form a suffix (step 0's seeds: the batch padded to
- * a fixed count).  Each destination type gets one more row, the dump row at index
- * seed_cap: out_indptr holds seed_cap + 2 entries.  A padding row holds `fanout` padding
- * edges, the dump row the rest of the edge capacity; every padding edge comes from a
- * padding slot of the source list (past its real sources, spread evenly; node_cap - 1 always
- * is one) with eid -1.  The source list holds the
- * exact call's list (real seeds, then the new sources, at the same positions and local
- * ids), then -1 up to node_cap + 1 entries: the last is the next step's dump row (its index
- * there, seed_cap, is this step's node_cap), so one layer's output rows are exactly the
- * source rows of the block it feeds.  A padding row may sit over a real source's slot: no
- * real row reads its output and its gradient is zero.  node_cap = max(seed_cap,
+ * a fixed count).  After its seed_cap seed rows every destination type gets D dump rows,
+ * D = dump_rows[s][t] = 1 + max over the relations into it of ceil(edge_cap / 2048):
+ * out_indptr holds seed_cap + 1 + D entries.  A padding row holds `fanout` padding edges;
+ * the dump rows hold the rest of the edge capacity in runs of at most 2048 edges (no row
+ * heavier than a heavy-row split, so nothing downstream needs a plan); every padding edge
+ * comes from a padding slot of the source list (past its real sources, spread evenly;
+ * node_cap - 1 always is one) with eid -1.  The source list holds the exact call's list
+ * (real seeds, then the new sources, at the same positions and local ids), then -1 up to
+ * node_cap + D' entries, D' = the next step's dump rows (1 at the last step): their index
+ * there starts at seed_cap, this step's node_cap, so one layer's output rows are exactly
+ * the source rows of the block it feeds.  A padding row may sit over a real source's slot:
+ * no real row reads its output and its gradient is zero.  node_cap = max(seed_cap,
  * min(n_nodes, seed_cap + edges sourced from the type)) + 1; `sizes` then holds the real
- * seed / node counts per step and the edge counts of the seed rows (the dump row's aside). */
+ * seed / node counts per step and the edge counts of the seed rows (the dump rows' aside). */
 #define GNNREC_SB_MAX_RELS 8
 #define GNNREC_SB_MAX_TYPES 4
 #define GNNREC_SB_MAX_STEPS 4
@@ -446,8 +448,8 @@ typedef struct gnnrec_sample_plan {
   uint32_t stamp;
   int static_shapes;    /* 0: exact sizes (read `sizes`), 1: capacities, -1-padded (above) */
   /* outputs, sized by gnnrec_sample_blocks_caps: per step s and relation r the block CSR
-   * (out_indptr [seed_cap + 1 (+1 static)], out_src int32 local ids [edge_cap], out_eid [edge_cap]),
-   * per step and type the source node ids [node_cap (+1 static)] (seeds first) */
+   * (out_indptr [seed_cap + 1 (+ D static)], out_src int32 local ids [edge_cap], out_eid
+   * [edge_cap]), per step and type the source node ids [node_cap (+ D' static)] (seeds first) */
   int64_t* out_indptr[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   int32_t* out_src[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   int64_t* out_eid[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
@@ -459,10 +461,11 @@ typedef struct gnnrec_sample_plan {
 /* Host only: per step the capacities of the outputs (seed_cap [s][t]: destination nodes,
  * edge_cap [s][r] = seed_cap[s][dst] x fanout, node_cap [s][t] = seed_cap[s][t] +
  * min(n_nodes_t, sum of edge_cap[s][r] over relations sourced from t), static shapes: see
- * above; seed_cap[s+1] = node_cap[s]), each flattened [step][GNNREC_SB_MAX_*], and the
- * workspace bytes. */
+ * above; seed_cap[s+1] = node_cap[s]) and the static dump rows (0 otherwise; nullable), each
+ * flattened [step][GNNREC_SB_MAX_*], and the workspace bytes. */
 int gnnrec_sample_blocks_caps(const gnnrec_sample_plan* plan, int64_t* seed_cap,
-                              int64_t* edge_cap, int64_t* node_cap, int64_t* workspace_bytes);
+                              int64_t* edge_cap, int64_t* node_cap, int64_t* dump_rows,
+                              int64_t* workspace_bytes);
 int gnnrec_sample_blocks(const gnnrec_sample_plan* plan, void* stream);
 
 /* compact_graphs over id lists (EdgeDataLoader's pair graphs, src/sampling.py:167-207 ->
