@@ -551,28 +551,28 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
       ws += up256(8 * C->seed[s][P->rel[r].dst_type]) + up256(4 * C->edge[s][r]) +
             up256(8 * C->edge[s][r]);
     }
-    for (int t = 0; t < P->n_types; ++t) {
-      int64_t e = 0;
-      for (int r = 0; r < P->n_rels; ++r)
-        if (P->rel[r].src_type == t) e += C->edge[s][r];
-      // static shapes: the real sources (at most n_nodes) and the dump slot, and never fewer
-      // rows than the destinations (a block's dst rows are a prefix of its sources)
-      C->node[s][t] = P->static_shapes
-                          ? std::max<int64_t>(C->seed[s][t],
-                                              std::min<int64_t>(C->seed[s][t] + e,
-                                                                P->type[t].n_nodes)) + 1
-                          : C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
-      if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
-    }
-  }
-  for (int s = 0; s < P->n_steps; ++s)
-    for (int t = 0; t < P->n_types; ++t) {
+    for (int t = 0; t < P->n_types; ++t) {  // static: dump rows per destination type
       int64_t dmax = 0;
       for (int r = 0; r < P->n_rels; ++r)
         if (P->rel[r].dst_type == t)
           dmax = std::max<int64_t>(dmax, (C->edge[s][r] + kDumpEdges - 1) / kDumpEdges);
       C->dump[s][t] = P->static_shapes ? 1 + dmax : 0;
     }
+    for (int t = 0; t < P->n_types; ++t) {
+      int64_t e = 0;
+      for (int r = 0; r < P->n_rels; ++r)
+        if (P->rel[r].src_type == t) e += C->edge[s][r];
+      // static shapes: the real sources (at most n_nodes) and one padding slot, and never
+      // fewer rows than the destinations with their dump rows (a block's dst rows are a
+      // prefix of its sources)
+      C->node[s][t] = P->static_shapes
+                          ? std::max<int64_t>(C->seed[s][t] + C->dump[s][t],
+                                              std::min<int64_t>(C->seed[s][t] + e,
+                                                                P->type[t].n_nodes) + 1)
+                          : C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
+      if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
+    }
+  }
   for (int s = 0; s < P->n_steps; ++s)
     for (int t = 0; t < P->n_types; ++t)
       C->len[s][t] = C->node[s][t] +

@@ -411,8 +411,8 @@ int gnnrec_clear_prefix_pos(const int64_t* prefix, int64_t n, int64_t* prefix_po
  * node_cap + D' entries, D' = the next step's dump rows (1 at the last step): their index
  * there starts at seed_cap, this step's node_cap, so one layer's output rows are exactly
  * the source rows of the block it feeds.  A padding row may sit over a real source's slot:
- * no real row reads its output and its gradient is zero.  node_cap = max(seed_cap,
- * min(n_nodes, seed_cap + edges sourced from the type)) + 1; `sizes` then holds the real
+ * no real row reads its output and its gradient is zero.  node_cap = max(seed_cap + D,
+ * min(n_nodes, seed_cap + edges sourced from the type) + 1); `sizes` then holds the real
  * seed / node counts per step and the edge counts of the seed rows (the dump rows' aside). */
 #define GNNREC_SB_MAX_RELS 8
 #define GNNREC_SB_MAX_TYPES 4
