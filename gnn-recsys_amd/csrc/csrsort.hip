@@ -129,17 +129,31 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
   }
 }
 
-// row_ptr[r] = first sorted position with key >= r (run boundaries, one write per row)
+// first position in keys[lo, hi) with key >= r
+__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* __restrict__ keys, int64_t lo,
+                                                   int64_t hi, int64_t r) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)keys[mid] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// row_ptr[r] = first sorted position with key >= r, one thread per row: the block finds its
+// 256 rows' key span with two searches, each row searches inside that span.  (Run boundaries
+// written by the edge after each run cost a serial loop over every empty row of a gap — a
+// static-shape block's unused padding slots: 1.3 ms for one 130k-row gap.)
 __global__ __launch_bounds__(256) void row_bounds_kernel(const uint32_t* __restrict__ keys,
                                                          int64_t E, int64_t n_rows,
                                                          int64_t* __restrict__ row_ptr) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= E; k += stride) {
-    // clamped: an out-of-range key (a caller bug) leaves wrong rows, never a wild write
-    const int64_t prev = k > 0 ? min((int64_t)keys[k - 1], n_rows) : -1;
-    const int64_t cur = k < E ? min((int64_t)keys[k], n_rows) : n_rows;
-    for (int64_t r = prev + 1; r <= cur; ++r) row_ptr[r] = k;
-  }
+  __shared__ int64_t span[2];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int64_t r1 = min(r0 + 256, n_rows + 1);
+  if (threadIdx.x < 2) span[threadIdx.x] = lower_bound_u32(keys, 0, E, threadIdx.x ? r1 : r0);
+  __syncthreads();
+  const int64_t r = r0 + threadIdx.x;
+  if (r < r1) row_ptr[r] = r == n_rows ? E : lower_bound_u32(keys, span[0], span[1], r);
 }
 
 __global__ __launch_bounds__(256) void zero_rows_kernel(int64_t* __restrict__ p, int64_t n) {
@@ -235,8 +249,8 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
     }
   }
   if (row_ptr)
-    hipLaunchKernelGGL(row_bounds_kernel, dim3(flat_grid(E + 1)), dim3(256), 0, s, keys_out, E,
-                       n_rows, row_ptr);
+    hipLaunchKernelGGL(row_bounds_kernel, dim3((unsigned)((n_rows + 1 + 255) / 256)), dim3(256), 0,
+                       s, keys_out, E, n_rows, row_ptr);
   return check_launch("radix sort");
 }
 
