@@ -2,7 +2,7 @@
 from a hipGraph), at K = 10 and the reference's K = 2500 — bench.captured_step and the
 eager loop of bench.minibatch_step without the rooflines.
 
-    python tools/probe_captured_step.py [K ...]
+    python tools/probe_captured_step.py [--captured-only] [K ...]
 """
 import json
 import os
@@ -53,11 +53,14 @@ def main():
     from gnnrec.synth import minibatch_graph
     dev = torch.device("cuda")
     g = minibatch_graph(64, dev)
-    Ks = [int(k) for k in sys.argv[1:]] or [10, 2500]
+    only = "--captured-only" in sys.argv
+    Ks = [int(k) for k in sys.argv[1:] if not k.startswith("--")] or [10, 2500]
     for K in Ks:
         steps = 100 if K <= 10 else 40
-        rec = {"K": K, "eager_num_workers2": eager(g, dev, K, steps, 5),
-               "captured_num_workers2": bench.captured_step(g, dev, K, steps, 5)}
+        rec = {"K": K}
+        if not only:
+            rec["eager_num_workers2"] = eager(g, dev, K, steps, 5)
+        rec["captured_num_workers2"] = bench.captured_step(g, dev, K, steps, 5)
         print(json.dumps(rec), flush=True)
 
 
