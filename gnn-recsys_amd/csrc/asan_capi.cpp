@@ -67,6 +67,14 @@ static void validation() {
         "gather batch null");
   jobs[0].n = 0;
   CHECK(gnnrec_gather_rows_batch(jobs, 3, nullptr) == GNNREC_OK, "gather batch empty");
+  const void* cs[2] = {nullptr, nullptr};
+  void* cd[2] = {nullptr, nullptr};
+  int64_t cb[2] = {0, 16};
+  CHECK(gnnrec_copy_batch(cs, cd, cb, GNNREC_COPY_MAX_JOBS + 1, nullptr) == GNNREC_EINVAL,
+        "copy batch n");
+  CHECK(gnnrec_copy_batch(cs, cd, cb, 2, nullptr) == GNNREC_EINVAL && err_has("null pointer"),
+        "copy batch null");
+  CHECK(gnnrec_copy_batch(cs, cd, cb, 1, nullptr) == GNNREC_OK, "copy batch empty");
   CHECK(gnnrec_lstm_step_f32(nullptr, 4, nullptr, nullptr, nullptr, 0, 1, nullptr, nullptr,
                              nullptr, 1000, nullptr, nullptr, 1000, nullptr) != GNNREC_OK &&
             err_has("hidden size"),

@@ -148,6 +148,68 @@ extern "C" int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_job
   return gnnrec::check_launch("gnnrec_gather_rows_batch");
 }
 
+// ---- many contiguous copies in one launch (a captured step's input hand-over) ----
+namespace gnnrec {
+namespace {
+
+struct CopyJobs {
+  const char* src[GNNREC_COPY_MAX_JOBS];
+  char* dst[GNNREC_COPY_MAX_JOBS];
+  int64_t units[GNNREC_COPY_MAX_JOBS];
+  int unit[GNNREC_COPY_MAX_JOBS];  // log2 of the unit bytes: 4 or 0
+  int block0[GNNREC_COPY_MAX_JOBS + 1];
+  int n;
+};
+
+template <typename U>
+__device__ __forceinline__ void copy_job(const CopyJobs& J, int j, int64_t t0, int64_t step) {
+  const U* s = reinterpret_cast<const U*>(J.src[j]);
+  U* d = reinterpret_cast<U*>(J.dst[j]);
+  for (int64_t t = t0; t < J.units[j]; t += step) d[t] = s[t];
+}
+
+__global__ __launch_bounds__(256) void copy_batch_kernel(CopyJobs J) {
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.block0[j + 1]) ++j;  // block-uniform
+  const int64_t t0 = (int64_t)((int)blockIdx.x - J.block0[j]) * 256 + threadIdx.x;
+  const int64_t step = (int64_t)(J.block0[j + 1] - J.block0[j]) * 256;
+  if (J.unit[j] == 4) copy_job<uint4>(J, j, t0, step);
+  else copy_job<uint8_t>(J, j, t0, step);
+}
+
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_copy_batch(const void* const* src, void* const* dst, const int64_t* bytes,
+                                 int n, void* stream) {
+  GNNREC_REQUIRE(n >= 0 && n <= GNNREC_COPY_MAX_JOBS, "gnnrec_copy_batch: n=%d (0..%d)", n,
+                 GNNREC_COPY_MAX_JOBS);
+  GNNREC_REQUIRE(n == 0 || (src && dst && bytes), "gnnrec_copy_batch: null arrays");
+  gnnrec::CopyJobs J{};
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    GNNREC_REQUIRE(bytes[i] >= 0, "gnnrec_copy_batch: job %d: negative size", i);
+    if (bytes[i] == 0) continue;
+    GNNREC_REQUIRE(src[i] && dst[i], "gnnrec_copy_batch: job %d: null pointer", i);
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src[i]) | reinterpret_cast<uintptr_t>(dst[i]) |
+                         (uintptr_t)bytes[i];
+    const int k = J.n++;
+    J.src[k] = static_cast<const char*>(src[i]);
+    J.dst[k] = static_cast<char*>(dst[i]);
+    J.unit[k] = (al & 15u) == 0 ? 4 : 0;
+    J.units[k] = bytes[i] >> J.unit[k];
+    int64_t nb = (J.units[k] + 255) / 256;
+    if (nb > 4096) nb = 4096;  // grid-stride beyond: 1M units in flight per job
+    J.block0[k] = blocks;
+    blocks += (int)nb;
+  }
+  if (J.n == 0) return GNNREC_OK;
+  J.block0[J.n] = blocks;
+  hipLaunchKernelGGL(gnnrec::copy_batch_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     gnnrec::as_stream(stream), J);
+  return gnnrec::check_launch("gnnrec_copy_batch");
+}
+
 // ---- partial-table add (the deterministic pass's fixed tree over source-range tiles) ----
 namespace gnnrec {
 namespace {

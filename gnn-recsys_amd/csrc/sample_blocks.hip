@@ -107,10 +107,16 @@ struct StepArgs {
   TypeArgs type[GNNREC_SB_MAX_TYPES];
   Sections sec;
   int64_t* sizes_seed_row;  // begin: sizes row -1
+  // the scan's chained tiles: per segment (relations, then types) a ticket word and one
+  // flag word per tile, scan_stride words apart (zeroed by the step's pick kernel); the
+  // scan's grid covers each segment's capacity in tiles from seg_block0
+  unsigned long long* scan_ws;
+  int64_t scan_stride, scan_words;
+  int seg_block0[GNNREC_SB_MAX_RELS + GNNREC_SB_MAX_TYPES + 1];
 };
 
 enum { kSecSeedPos, kSecZeroBits, kSecExclSet, kSecPick, kSecZeroNext, kSecCompact,
-       kSecNewNodes, kSecPrefix, kSecExclClear, kSecDumpEdges, kSecPadNodes };
+       kSecNewNodes, kSecPrefix, kSecExclClear, kSecDumpEdges, kSecPadNodes, kSecZeroScan };
 
 // (stamp << 32) | ~position: the atomicMax of two writes of one stamp keeps the smaller
 // position, and any write of a newer stamp beats every older entry
@@ -179,6 +185,11 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
     const TypeArgs& T = A.type[A.sec.idx[k]];
     const int64_t w = (int64_t)b * kSbBlock + threadIdx.x;
     if (w < T.words) T.bits_next[w] = 0ull;
+    return;
+  }
+  if (A.sec.kind[k] == kSecZeroScan) {  // the scan's tickets and tile flags, for this step
+    const int64_t w = (int64_t)b * kSbBlock + threadIdx.x;
+    if (w < A.scan_words) A.scan_ws[w] = 0ull;
     return;
   }
   const RelArgs& R = A.rel[A.sec.idx[k]];
@@ -266,10 +277,28 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t* wsum, int
   return before + v - x;
 }
 
+// Chained tiles with decoupled look-back (the library's exclusive scan, sampler.hip): every
+// segment is cut into tiles of kScanTile items, a block takes its segment's next tile by
+// ticket (so a tile only ever waits on tiles taken before it), publishes the tile's
+// aggregate, its first wave walks back over the predecessors' flags 64 at a time until an
+// inclusive prefix, and publishes its own.  The grid covers each segment's capacity; tiles
+// past the device count exit.  (One block per segment took 0.3-0.46 ms on the 1M-row
+// segments of a K = 2500 batch.)
+constexpr int kScanItems = 4;
+constexpr int64_t kScanTile = (int64_t)kScanThreads * kScanItems;
+constexpr unsigned long long kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62;
+__device__ __forceinline__ unsigned long long flag_pack(unsigned long long st, int64_t v) {
+  return st | ((unsigned long long)v & ((1ull << 62) - 1));
+}
+__device__ __forceinline__ int64_t flag_value(unsigned long long f) {
+  return (int64_t)(f << 2) >> 2;
+}
+
 __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
   __shared__ int64_t wsum[kScanThreads / 64];
-  constexpr int kItems = 4;
-  const int seg = (int)blockIdx.x;
+  __shared__ int64_t sh_tile, sh_prefix;
+  int seg = 0;
+  while (seg + 1 < A.n_rels + A.n_types && (int)blockIdx.x >= A.seg_block0[seg + 1]) ++seg;
   const bool is_rel = seg < A.n_rels;
   int64_t n;
   const int64_t* cnt = nullptr;
@@ -286,25 +315,72 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
     bits = T.bits_cur;
     out = T.word_rank;
   }
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kItems) {
-    const int64_t i0 = base + (int64_t)threadIdx.x * kItems;
-    int64_t v[kItems], s = 0;
+  unsigned long long* ticket = A.scan_ws + seg * A.scan_stride;
+  unsigned long long* flags = ticket + 1;
+  if (threadIdx.x == 0)
+    sh_tile = (int64_t)__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int64_t tile = sh_tile;
+  const int64_t n_tiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+  if (tile >= n_tiles) return;  // block-uniform: past the device count
+  const int64_t i0 = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t v[kScanItems], s = 0;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      const int64_t i = i0 + j;
-      v[j] = i < n ? (is_rel ? cnt[i] : (int64_t)__popcll(bits[i])) : 0;
-      s += v[j];
-    }
-    int64_t tot;
-    int64_t run = carry + block_excl_scan(s, wsum, &tot);
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      if (i0 + j < n) out[i0 + j] = run;
-      run += v[j];
-    }
-    carry += tot;
+  for (int j = 0; j < kScanItems; ++j) {
+    const int64_t i = i0 + j;
+    v[j] = i < n ? (is_rel ? cnt[i] : (int64_t)__popcll(bits[i])) : 0;
+    s += v[j];
   }
+  int64_t agg;
+  const int64_t ex = block_excl_scan(s, wsum, &agg);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (tile == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(flags, flag_pack(kFlagIncl, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        sh_prefix = 0;
+      }
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(flags + tile, flag_pack(kFlagAgg, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t prefix = 0;
+      for (int64_t j = tile - 1;; j -= 64) {  // window [j - 63, j], nearest first
+        const int64_t idx = j - lane;
+        unsigned long long f = kFlagIncl;  // before tile 0: an inclusive prefix of 0
+        if (idx >= 0) {
+          f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while ((f >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        const uint64_t incl = __ballot((f >> 62) == 2);
+        const int stop = incl ? __builtin_ctzll(incl) : 64;
+        int64_t x = lane <= stop ? flag_value(f) : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+        prefix += x;
+        if (incl) break;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(flags + tile, flag_pack(kFlagIncl, prefix + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        sh_prefix = prefix;
+      }
+    }
+  }
+  __syncthreads();
+  int64_t run = sh_prefix + ex;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    if (i0 + j < n) out[i0 + j] = run;
+    run += v[j];
+  }
+  if (tile != n_tiles - 1) return;  // the last tile closes the segment
+  const int64_t carry = sh_prefix + agg;
   if (is_rel && A.stat) {  // the dump rows' bounds: runs of kDumpEdges up to the capacity
     const RelArgs& R = A.rel[seg];
     for (int64_t j = 1 + threadIdx.x; j < R.dump_rows; j += kScanThreads)
@@ -516,6 +592,7 @@ struct Caps {
   int64_t node[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
   int64_t dump[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];  // static: dump rows per dst type
   int64_t len[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];   // static: node list lengths
+  int64_t scan_stride;  // words per scan segment: a ticket + the most tiles of any step
   int64_t ws_bytes;
 };
 
@@ -577,6 +654,15 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
     for (int t = 0; t < P->n_types; ++t)
       C->len[s][t] = C->node[s][t] +
                      (P->static_shapes ? (s + 1 < P->n_steps ? C->dump[s + 1][t] : 1) : 0);
+  int64_t tiles = 1;
+  for (int s = 0; s < P->n_steps; ++s) {
+    for (int r = 0; r < P->n_rels; ++r)
+      tiles = std::max<int64_t>(tiles, (C->seed[s][P->rel[r].dst_type] + kScanTile - 1) / kScanTile);
+  }
+  for (int t = 0; t < P->n_types; ++t)
+    tiles = std::max<int64_t>(tiles, (words_of(P->type[t].n_nodes) + kScanTile - 1) / kScanTile);
+  C->scan_stride = 1 + tiles;
+  ws += up256(8 * (int64_t)(P->n_rels + P->n_types) * C->scan_stride);
   C->ws_bytes = ws;
   return GNNREC_OK;
 }
@@ -646,6 +732,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       peid[s][r] = reinterpret_cast<int64_t*>(ws);
       ws += up256(8 * C.edge[s][r]);
     }
+  unsigned long long* scan_ws = reinterpret_cast<unsigned long long*>(ws);
   int64_t* node_count = P->sizes;                   // [(L + 1) x T], row -1 first
   int64_t* edge_count = P->sizes + (int64_t)(L + 1) * T;  // [L x R]
 
@@ -657,6 +744,16 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     A.stat = P->static_shapes ? 1 : 0;
     A.stamp = P->stamp + (uint32_t)s;
     A.sizes_seed_row = node_count;
+    A.scan_ws = scan_ws;
+    A.scan_stride = C.scan_stride;
+    A.scan_words = (int64_t)(R + T) * C.scan_stride;
+    A.seg_block0[0] = 0;
+    for (int r = 0; r < R; ++r)  // the scan's grid: each segment's capacity in tiles
+      A.seg_block0[r + 1] = A.seg_block0[r] +
+          (int)std::max<int64_t>(1, (C.seed[s][P->rel[r].dst_type] + kScanTile - 1) / kScanTile);
+    for (int t = 0; t < T; ++t)
+      A.seg_block0[R + t + 1] = A.seg_block0[R + t] +
+          (int)std::max<int64_t>(1, (words_of(P->type[t].n_nodes) + kScanTile - 1) / kScanTile);
     for (int t = 0; t < T; ++t) {
       const gnnrec_sample_type& ty = P->type[t];
       TypeArgs& a = A.type[t];
@@ -738,6 +835,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       add_sec(A.sec, kSecPick, r,
               (int)((C.seed[s][P->rel[r].dst_type] + kSbBlock / G - 1) / (kSbBlock / G)));
     for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroNext, t, nblocks(A.type[t].words));
+    add_sec(A.sec, kSecZeroScan, 0, nblocks(A.scan_words));
     if (A.sec.n) {
       const dim3 grid((unsigned)A.sec.begin[A.sec.n]);
       switch (G) {
@@ -748,8 +846,9 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       }
       if (int st = check_launch("gnnrec_sample_blocks(pick)")) return st;
     }
-    // scan: one block per relation and per type
-    hipLaunchKernelGGL(sb_scan_kernel, dim3((unsigned)(R + T)), dim3(kScanThreads), 0, hs, A);
+    // scan: chained tiles over every relation's counts and every type's bitmap words
+    hipLaunchKernelGGL(sb_scan_kernel, dim3((unsigned)A.seg_block0[R + T]), dim3(kScanThreads),
+                       0, hs, A);
     if (int st = check_launch("gnnrec_sample_blocks(scan)")) return st;
     // finalize
     A.sec.n = 0;

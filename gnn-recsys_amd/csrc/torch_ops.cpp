@@ -1778,6 +1778,36 @@ compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
   return {nodes, local, count};
 }
 
+// a12: many contiguous same-size copies dst[j] <- src[j] in one launch per 64
+// (gnnrec_copy_batch: a static batch into a captured step's buffers, gnnrec/capture.py)
+void copy_batch(at::TensorList src, at::TensorList dst) {
+  const OneDevice one_device_;
+  TORCH_CHECK_VALUE(src.size() == dst.size(), "copy_batch: one dst per src");
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<int64_t> nb;
+  for (size_t j = 0; j < src.size(); ++j) {
+    TORCH_CHECK_VALUE(src[j].is_cuda() && dst[j].is_cuda(),
+                      "copy_batch: device tensors (there is no CPU path)");
+    same_dev(src[j], "src");
+    same_dev(dst[j], "dst");
+    TORCH_CHECK_VALUE(src[j].scalar_type() == dst[j].scalar_type() &&
+                          src[j].sizes() == dst[j].sizes() && src[j].is_contiguous() &&
+                          dst[j].is_contiguous(),
+                      "copy_batch: job ", j, ": contiguous tensors of one dtype and shape");
+    sp.push_back(src[j].data_ptr());
+    dp.push_back(dst[j].data_ptr());
+    nb.push_back(src[j].nbytes());
+  }
+  if (src.empty()) return;
+  const c10::DeviceGuard g(src[0].device());
+  for (size_t i = 0; i < sp.size(); i += GNNREC_COPY_MAX_JOBS) {
+    const int n = (int)std::min<size_t>(GNNREC_COPY_MAX_JOBS, sp.size() - i);
+    ck(gnnrec_copy_batch(sp.data() + i, dp.data() + i, nb.data() + i, n, stream_of(src[0])),
+       "gnnrec_copy_batch");
+  }
+}
+
 // EdgeDataLoader's batch head in one call (gnnrec/sampling.py _iter_batches): the batch's
 // positive pairs (find_edges), the uniform negatives (src repeated K times, dst =
 // randint(N_dst) from the default generator — the same draws as negative_sampler.Uniform),
@@ -2015,6 +2045,7 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor[] src_local, Tensor[] eids, "
         "Tensor[] src_nid, int[] sizes)");
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");
+  m.def("copy_batch(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("compact_ids(Tensor[] ids, int[] type, int[] n_nodes, int[] caps, Tensor(a!)[] bits, "
         "Tensor(b!)[] word_rank, int parity) -> (Tensor[] nodes, Tensor[] local, Tensor count)");
   // host-only entry points (no tensors: one catch-all kernel each)
@@ -2089,6 +2120,7 @@ TORCH_LIBRARY_IMPL(gnnrec, CUDA, m) {
   m.impl("edge_batch_pairs", &edge_batch_pairs);
   m.impl("sample_blocks", &sample_blocks);
   m.impl("compact_ids", &compact_ids);
+  m.impl("copy_batch", &copy_batch);
 }
 // Meta / fake tensors (torch.compile tracing): the same functions stop after their checks.
 TORCH_LIBRARY_IMPL(gnnrec, Meta, m) { GNNREC_IMPLS(m); }

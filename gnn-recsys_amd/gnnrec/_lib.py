@@ -94,6 +94,7 @@ SIGNATURES = {
                                     _P, _I64, _P]),
     "gnnrec_gather_rows": (_INT, [_P, _I64, _P, _I64, _I64, _P, _I64, _P]),
     "gnnrec_gather_rows_batch": (_INT, [_P, _INT, _P]),
+    "gnnrec_copy_batch": (_INT, [_P, _P, _P, _INT, _P]),
     # (plan*, seed_cap*, edge_cap*, node_cap*, workspace_bytes*) / (plan*, stream)
     "gnnrec_sample_blocks_caps": (_INT, [_P, _P, _P, _P, _P, _P]),
     "gnnrec_sample_blocks": (_INT, [_P, _P]),

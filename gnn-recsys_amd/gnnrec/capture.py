@@ -6,7 +6,8 @@ The batches come from EdgeDataLoader(static_shapes=True): every full batch has t
 shapes and nothing in the step reads a value back to the host, so the whole step — some
 hundreds of kernels, each a few microseconds, whose launches bound the eager step on the
 host — is recorded once and re-issued by one hipGraphLaunch.  Per batch the step copies the
-batch's tensors into the captured batch's buffers (one torch._foreach_copy_) and replays.
+batch's tensors into the captured batch's buffers (ops.copy_batch: one launch per 64
+tensors, not one blit per tensor) and replays.
 
     step = CapturedTrainStep(model, opt, lambda m, b: loss_of(m, b))
     for batch in loader:            # loader = EdgeDataLoader(..., static_shapes=True)
@@ -26,6 +27,7 @@ from __future__ import annotations
 
 import torch
 
+from . import ops
 from .sampling import _tensors
 
 
@@ -116,7 +118,7 @@ class CapturedTrainStep:
         if self.graph is None:
             self._capture(batch, inputs)  # records only: the replay below runs the step
         else:
-            torch._foreach_copy_(self._inputs, inputs)
+            ops.copy_batch(inputs, self._inputs)  # one launch per 64 tensors
         self.graph.replay()
         self.replays += 1
         return self.loss

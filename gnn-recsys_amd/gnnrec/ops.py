@@ -1315,6 +1315,21 @@ def compact_ids(lists, scratch, caps):
     return out
 
 
+def copy_batch(src, dst) -> None:
+    """a12: dst[j].copy_(src[j]) for contiguous same-shape device tensors, 64 per launch
+    (gnnrec_copy_batch); other pairs through torch's copy."""
+    a, b = [], []
+    for s_, d_ in zip(src, dst):
+        if s_.is_contiguous() and d_.is_contiguous() and s_.dtype == d_.dtype and \
+                s_.shape == d_.shape:
+            a.append(s_)
+            b.append(d_)
+        else:
+            d_.copy_(s_)
+    if a:
+        _T().copy_batch(a, b)
+
+
 def gather_rows_batch(jobs, n_dev=None):
     """a10, several gathers in one launch: jobs = [(src, idx)] -> [src[idx]] (any dtype,
     contiguous rows; at most GATHER_MAX_JOBS per launch).  n_dev: per job None or a one-entry

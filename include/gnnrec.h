@@ -669,6 +669,13 @@ int gnnrec_gather_rows_batch(const gnnrec_gather_job* jobs, int n_jobs, void* st
 int gnnrec_gather_rows(const void* src, int64_t src_ld_bytes, const int64_t* idx, int64_t n,
                        int64_t row_bytes, void* dst, int64_t dst_ld_bytes, void* stream);
 
+/* Up to GNNREC_COPY_MAX_JOBS contiguous device copies dst[j] <- src[j] (bytes[j]) in one
+ * launch: a static-shape batch handed into the buffers a captured training step replays
+ * over (gnnrec/capture.py), instead of one copy engine / blit launch per tensor. */
+#define GNNREC_COPY_MAX_JOBS 64
+int gnnrec_copy_batch(const void* const* src, void* const* dst, const int64_t* bytes, int n,
+                      void* stream);
+
 /* ---- f2: edge-score side of the training step ----------------------------
  * max_margin_loss (src/model.py:473-533) for one etype, forward and gradient in one pass:
  *   s[e,k] = relu(((neg[e,k] + delta) - pos[e]) - mask[e,k]) / recency[e]

@@ -200,3 +200,22 @@ def test_captured_steps_train_as_the_eager_loop(nw, fanouts):
     np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
     for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         _close(pb.detach(), pa.detach(), n, rtol=2e-3, atol=2e-5)
+
+
+def test_copy_batch_equals_tensor_copies():
+    """ops.copy_batch (gnnrec_copy_batch, 64 copies per launch): every dtype and size,
+    16-B-aligned and unaligned (offset views), more than one launch's worth, empty ones."""
+    from gnnrec import ops
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(0)
+    src = []
+    for k in range(70):
+        n = int(torch.randint(0, 5000, (1,), generator=gen, device=DEV))
+        base = torch.randint(-1 << 40, 1 << 40, (n + 3,), device=DEV, generator=gen)
+        t = [base[:n], base[1:n + 1].to(torch.int32), base[3:].float(), base[:n].to(torch.uint8),
+             base[2:n + 2].double()][k % 5]
+        src.append(t.contiguous() if k % 3 else t)
+    dst = [torch.empty_like(s) for s in src]
+    ops.copy_batch(src, dst)
+    for s, d in zip(src, dst):
+        assert torch.equal(s, d)
