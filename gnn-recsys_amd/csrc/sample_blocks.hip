@@ -102,6 +102,7 @@ struct Sections {
 
 struct StepArgs {
   int n_rels, n_types, last, stat;
+  int64_t* overflow;  // static shapes with capacity hints: set when a batch does not fit
   uint32_t stamp;
   RelArgs rel[GNNREC_SB_MAX_RELS];
   TypeArgs type[GNNREC_SB_MAX_TYPES];
@@ -393,7 +394,8 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
       if (A.stat) out[n + 1] = min(carry + kDumpEdges, A.rel[seg].edge_cap);
     } else {
       const TypeArgs& T = A.type[seg - A.n_rels];
-      *T.n_nodes_out = *T.n_seeds + carry;
+      // static shapes: at most node_cap - 1 real sources (a hinted capacity may cut them)
+      *T.n_nodes_out = A.stat ? min(*T.n_seeds + carry, T.node_cap - 1) : *T.n_seeds + carry;
     }
   }
 }
@@ -412,7 +414,7 @@ __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint
 // [real sources, node_cap + 1), all -1, so the backward's transposed block has no single
 // source row holding every padding edge (a radix sort's worst case, and a heavy row)
 __device__ __forceinline__ int32_t pad_src(const TypeArgs& S, int64_t k) {
-  const int64_t real = *S.n_seeds + S.word_rank[S.words];
+  const int64_t real = min(*S.n_seeds + S.word_rank[S.words], S.node_cap - 1);
   return (int32_t)(real + k % (S.node_len - real));
 }
 
@@ -433,7 +435,12 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
         R.out_eid[o] = -1;
         break;
       }
-      R.out_src[o] = (int32_t)local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
+      int64_t loc = local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
+      if (A.stat && loc >= S.node_cap - 1) {  // past a hinted capacity: a padding slot
+        if (A.overflow) *A.overflow = 1;
+        loc = S.node_cap - 1;
+      }
+      R.out_src[o] = (int32_t)loc;
       R.out_eid[o] = R.pick_eid[t];
       break;
     }
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
     }
     case kSecPadNodes: {  // static shapes: the list past the real seeds and new sources
       const TypeArgs& T = A.type[x];
-      const int64_t p = *T.n_seeds + T.word_rank[T.words] + t;
+      const int64_t p = min(*T.n_seeds + T.word_rank[T.words], T.node_cap - 1) + t;
       if (p < T.node_len) T.nodes[p] = -1;
       break;
     }
@@ -459,6 +466,10 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       int64_t p = *T.n_seeds + T.word_rank[t];
       while (word) {
         const int64_t id = t * 64 + __builtin_ctzll(word);
+        if (A.stat && p >= T.node_cap - 1) {  // past a hinted capacity: left out
+          if (A.overflow) *A.overflow = 1;
+          break;
+        }
         T.nodes[p] = id;
         T.pos_next[id] = pack_pos(A.stamp + 1u, p);  // (new ids are distinct)
         word &= word - 1ull;
@@ -642,10 +653,11 @@ int plan_caps(const gnnrec_sample_plan* P, Caps* C) {
       // static shapes: the real sources (at most n_nodes) and one padding slot, and never
       // fewer rows than the destinations with their dump rows (a block's dst rows are a
       // prefix of its sources)
+      int64_t real_cap = std::min<int64_t>(C->seed[s][t] + e, P->type[t].n_nodes) + 1;
+      if (P->static_shapes && P->node_cap_hint[s][t] > 0)  // a caller's tighter bound
+        real_cap = std::min<int64_t>(real_cap, P->node_cap_hint[s][t]);
       C->node[s][t] = P->static_shapes
-                          ? std::max<int64_t>(C->seed[s][t] + C->dump[s][t],
-                                              std::min<int64_t>(C->seed[s][t] + e,
-                                                                P->type[t].n_nodes) + 1)
+                          ? std::max<int64_t>(C->seed[s][t] + C->dump[s][t], real_cap)
                           : C->seed[s][t] + std::min<int64_t>(e, P->type[t].n_nodes);
       if (s + 1 < P->n_steps) C->seed[s + 1][t] = C->node[s][t];
     }
@@ -742,6 +754,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     A.n_types = T;
     A.last = s == L - 1;
     A.stat = P->static_shapes ? 1 : 0;
+    A.overflow = P->overflow;
     A.stamp = P->stamp + (uint32_t)s;
     A.sizes_seed_row = node_count;
     A.scan_ws = scan_ws;

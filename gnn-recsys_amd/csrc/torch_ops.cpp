@@ -1530,7 +1530,8 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               const c10::List<optional<Tensor>>& excl_rows, at::IntArrayRef n_nodes,
               at::TensorList seeds, at::TensorList pos, at::TensorList bits,
               at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
-              int64_t steps, int64_t stamp, bool static_shapes, const optional<Tensor>& sizes_out) {
+              int64_t steps, int64_t stamp, bool static_shapes, const optional<Tensor>& sizes_out,
+              at::IntArrayRef node_cap_hint, const optional<Tensor>& overflow) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = n_nodes.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
@@ -1553,6 +1554,16 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   P.n_steps = (int)steps;
   P.stamp = (uint32_t)stamp;
   P.static_shapes = static_shapes ? 1 : 0;
+  // static capacity hints [step][type] (empty: none) and the overflow flag they may raise
+  TORCH_CHECK_VALUE(node_cap_hint.empty() || (int64_t)node_cap_hint.size() == steps * (int64_t)NT,
+                    "sample_blocks: node_cap_hint must hold steps x types entries");
+  for (int64_t s = 0; s < steps && !node_cap_hint.empty(); ++s)
+    for (size_t t = 0; t < NT; ++t) P.node_cap_hint[s][t] = node_cap_hint[s * NT + t];
+  if (has(overflow)) {
+    dev(overflow, "overflow", at::kLong);
+    TORCH_CHECK_VALUE(overflow->numel() >= 1, "sample_blocks: overflow holds one flag");
+    P.overflow = p<int64_t>(overflow);
+  }
   for (size_t r = 0; r < R; ++r) {
     dev(indptrs[r], "indptr", at::kLong);
     dev(indices[r], "indices", at::kInt);
@@ -2041,7 +2052,8 @@ TORCH_LIBRARY(gnnrec, m) {
         "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
         "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
         "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
-        "int stamp, bool static_shapes=False, Tensor(d!)? sizes_out=None) -> (Tensor[] out_indptr, "
+        "int stamp, bool static_shapes=False, Tensor(d!)? sizes_out=None, int[] node_cap_hint=[], "
+        "Tensor(e!)? overflow=None) -> (Tensor[] out_indptr, "
         "Tensor[] src_local, Tensor[] eids, "
         "Tensor[] src_nid, int[] sizes)");
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");

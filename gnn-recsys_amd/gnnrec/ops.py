@@ -1258,7 +1258,8 @@ class SampleScratch:
 
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
-                  fanouts, keys, stamp, static_shapes=False, sizes_out=None):
+                  fanouts, keys, stamp, static_shapes=False, sizes_out=None, node_cap_hint=None,
+                  overflow=None):
     """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
     1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
     output block); excl: per relation None or (eids, coo_dst, mask, rows).
@@ -1269,7 +1270,9 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
     sizes_out (int64 device tensor of the sizes' length): the exact outputs at their
     capacities and the sizes left there, not read back — the caller queues work sized by
     them on the device (gather_rows_batch's n_dev) before it reads them itself; the returned
-    sizes are the capacities then too."""
+    sizes are the capacities then too.  node_cap_hint ([step][type], static): tighter node
+    capacities than the provable ones; a batch that does not fit sets `overflow` (int64
+    device flag) and must be discarded or redone."""
     steps, R = len(fanouts), len(indptrs)
     ex = [e if e is not None else (None,) * 4 for e in excl]
     o_ip, o_src, o_eid, nodes, sizes = _T().sample_blocks(
@@ -1278,7 +1281,7 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
         list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
         [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
         [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes),
-        sizes_out)
+        sizes_out, [int(h) for hs in (node_cap_hint or []) for h in hs], overflow)
     NT = len(n_nodes)
     out = []
     for s in range(steps):

@@ -113,7 +113,8 @@ class BlockSampler:
         return all(0 <= self._fanout(b, ce) <= ops.SB_MAX_FANOUT
                    for b in range(self.num_layers) for ce in ces)
 
-    def _sample_fused(self, g, seeds, exclude_eids, transposes, static=False):
+    def _sample_fused(self, g, seeds, exclude_eids, transposes, static=False, hints=None,
+                      overflow=None):
         """sample_blocks through gnnrec_sample_blocks: 1 + 3L launches and one host read for
         all L blocks (bitwise the blocks of the per-layer path, _one_block).
 
@@ -160,7 +161,9 @@ class BlockSampler:
             [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
             [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
             [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
-            fans, keys, stamp, static_shapes=static, sizes_out=sizes_dev)
+            fans, keys, stamp, static_shapes=static, sizes_out=sizes_dev,
+            node_cap_hint=[[(hints or {}).get((s_, nt), 0) for nt in nts] for s_ in range(L)]
+            if hints else None, overflow=overflow)
         # the block data (DGL copies it at block creation; the reference reads
         # blocks[0].srcdata['features']): every table in one launch; static: -1 ids -> zero rows
         jobs, dests, cnts = [], [], []
@@ -232,12 +235,16 @@ class BlockSampler:
 
     def sample_blocks(self, g: HeteroGraph, seed_nodes: Dict[str, torch.Tensor],
                       exclude_eids: Optional[Dict[tuple, torch.Tensor]] = None,
-                      transposes: bool = False, static_shapes: bool = False) -> List[Block]:
+                      transposes: bool = False, static_shapes: bool = False,
+                      node_cap_hint=None, overflow=None) -> List[Block]:
         """transposes: also build every relation's source-major CSR (Block._t), which the
         training backward gathers over — in the sampling thread (num_workers > 0), off the
         training thread (EdgeDataLoader, transposed_blocks=True).
         static_shapes: the blocks at fixed capacities with nothing read back (seeds may hold
-        -1 padding; _sample_fused) — the batches of a captured training step."""
+        -1 padding; _sample_fused) — the batches of a captured training step.
+        node_cap_hint {(step, ntype): capacity} and overflow (an int64 device flag): tighter
+        static node capacities than the provable ones, and the flag a batch that does not fit
+        them raises (EdgeDataLoader learns them from its first exact batches)."""
         self._calls += 1
         seeds = {nt: torch.as_tensor(v, dtype=torch.int64, device=g.device)
                  for nt, v in seed_nodes.items()}
@@ -245,7 +252,8 @@ class BlockSampler:
             raise ValueError("static_shapes needs the fused sampler: bounded fanouts (0..64) "
                              "on a HIP device within its limits")
         if self._fused_ok(g):
-            blocks = self._sample_fused(g, seeds, exclude_eids, transposes, static_shapes)
+            blocks = self._sample_fused(g, seeds, exclude_eids, transposes, static_shapes,
+                                        node_cap_hint, overflow)
             for b in blocks:
                 b._sampler = weakref.ref(self)
             return blocks
@@ -586,7 +594,8 @@ class EdgeDataLoader:
                  reverse_eids=None, reverse_etypes: Optional[dict] = None,
                  negative_sampler=None, batch_size: int = 1, shuffle: bool = False,
                  drop_last: bool = False, num_workers: int = 0, pin_memory: bool = False,
-                 transposed_blocks: bool = True, static_shapes: bool = False, **kwargs):
+                 transposed_blocks: bool = True, static_shapes: bool = False,
+                 static_caps: str = "auto", **kwargs):
         self.g = g
         self.g_sampling = g_sampling if g_sampling is not None else g
         # the training loader's blocks carry their source-major CSRs (built by the sampler,
@@ -629,6 +638,20 @@ class EdgeDataLoader:
         # captured once and replayed (gnnrec.capture.CapturedTrainStep); a final partial
         # batch comes in the ordinary exact form
         self.static_shapes = static_shapes
+        # static_caps: 'provable' — the capacities no batch can exceed (a graph-sized source
+        # list where the fanout can reach most of a node type: C2 at K = 2500 pads its first
+        # block's 7.3M edges to 11M); 'auto' — the first STATIC_LEARN full batches come out
+        # exact, and their largest source lists x STATIC_MARGIN (+ a padding slot) become the
+        # node capacities: a later batch that does not fit (the sampler's overflow flag, read
+        # back in the loader's thread) is redone exactly and the capacities grow
+        if static_caps not in ("auto", "provable"):
+            raise ValueError(f"static_caps={static_caps!r}: 'auto' or 'provable'")
+        self.static_caps = static_caps
+        self._node_hint = None if static_caps == "auto" else {}
+        self._seen_nodes = {}
+        self._learned = 0
+        self._overflow = None
+        self.static_redone = 0
         if static_shapes:
             if len(self.types) != 1 or not self.fused_head:
                 raise ValueError("static_shapes: batches of one edge type, with "
@@ -641,6 +664,23 @@ class EdgeDataLoader:
     def __len__(self):
         n = self.flat_ids.numel()
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    STATIC_LEARN = 3
+    STATIC_MARGIN = 1.1
+
+    def _learn_caps(self, blocks):
+        """Record an exact batch's source-list sizes per (step, node type); after
+        STATIC_LEARN of them, fix the static node capacities."""
+        L = len(blocks)
+        for s_ in range(L):
+            b = blocks[L - 1 - s_]
+            for nt in b.ntypes:
+                n = b.number_of_src_nodes(nt)
+                self._seen_nodes[(s_, nt)] = max(self._seen_nodes.get((s_, nt), 0), n)
+        self._learned += 1
+        if self._learned >= self.STATIC_LEARN:
+            self._node_hint = {k: -(-int(v * self.STATIC_MARGIN + 2) // 1024) * 1024
+                               for k, v in self._seen_nodes.items()}
 
     def _head_static(self, batch):
         """_head at fixed shapes, with no host read: the same pairs, negatives (the same
@@ -752,7 +792,9 @@ class EdgeDataLoader:
                             self.drop_last, g.device):
             parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
             batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
-            static = self.static_shapes and idx.numel() == self.batch_size
+            static = self.static_shapes and idx.numel() == self.batch_size and \
+                self._node_hint is not None
+            learn = self.static_shapes and idx.numel() == self.batch_size and not static
             counts = None
             if static:
                 node_ids, pos_l, neg_l, counts = self._head_static(batch)
@@ -782,12 +824,38 @@ class EdgeDataLoader:
             elif self.exclude == 'self':
                 exclude = dict(batch)
             seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
+            hint = self._node_hint if static and self._node_hint else None
+            if hint is not None:
+                if self._overflow is None:
+                    self._overflow = torch.zeros(1, dtype=torch.int64, device=g.device)
+                self._overflow.zero_()
             blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
                                                 transposes=self.transposed_blocks,
-                                                static_shapes=static)
+                                                static_shapes=static, node_cap_hint=hint,
+                                                overflow=self._overflow if hint else None)
+            if hint is not None and int(self._overflow.item()):
+                # the batch outgrew the learned capacities: redo it exactly (same pairs and
+                # negatives, fresh picks) and let the capacities grow
+                self.static_redone += 1
+                self._node_hint = {k: -(-int(v * self.STATIC_MARGIN) // 1024) * 1024
+                                   for k, v in self._node_hint.items()}
+                cnt = counts.tolist()
+                node_ids = {nt: v[:c] for (nt, v), c in zip(node_ids.items(), cnt)}
+                pos_g = PairGraph(pos_l, node_ids)
+                for ce, e in batch.items():
+                    for k, v in g._edata[ce].items():
+                        pos_g._edata[ce][k] = ops.gather_rows(v, e)
+                    pos_g._edata[ce][EID] = e
+                static = False
+                seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
+                blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
+                                                    transposes=self.transposed_blocks)
+            if learn:
+                self._learn_caps(blocks)
             # static: the real node count per type, on the device (the node lists hold -1
             # past it)
             pos_g.node_counts = dict(zip(g.ntypes, counts.unbind(0))) if static else None
+            pos_g.static = static
             input_nodes = blocks[0].srcdata[NID]
             if self.negative_sampler is None:
                 yield input_nodes, pos_g, blocks

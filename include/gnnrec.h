@@ -447,6 +447,12 @@ typedef struct gnnrec_sample_plan {
   uint64_t key[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_RELS];
   uint32_t stamp;
   int static_shapes;    /* 0: exact sizes (read `sizes`), 1: capacities, -1-padded (above) */
+  /* static shapes: a tighter node capacity per step and type than the provable one (0: none;
+   * never below seed_cap + D).  A batch whose real sources do not fit sets *overflow to 1
+   * (device, nullable) and stays memory-safe — sources past the capacity are left out and
+   * their edges point at a padding slot — so the caller discards or redoes that batch. */
+  int64_t node_cap_hint[GNNREC_SB_MAX_STEPS][GNNREC_SB_MAX_TYPES];
+  int64_t* overflow;
   /* outputs, sized by gnnrec_sample_blocks_caps: per step s and relation r the block CSR
    * (out_indptr [seed_cap + 1 (+ D static)], out_src int32 local ids [edge_cap], out_eid
    * [edge_cap]), per step and type the source node ids [node_cap (+ D' static)] (seeds first) */

@@ -89,12 +89,12 @@ def test_static_blocks_hold_the_exact_rows(fanouts):
                 assert lo.number_of_dst_nodes(nt) == hi.number_of_src_nodes(nt)
 
 
-def _loader(g, static, K=4, batch=64, n=700, seed=5, fanouts=(4, 3), nw=0):
+def _loader(g, static, K=4, batch=64, n=700, seed=5, fanouts=(4, 3), nw=0, caps="provable"):
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
     return EdgeDataLoader(g, {BUYS: torch.arange(n)}, MultiLayerNeighborSampler(list(fanouts), seed=seed),
                           exclude='reverse_types', reverse_etypes=REV,
                           negative_sampler=negative_sampler.Uniform(K), batch_size=batch,
-                          shuffle=True, static_shapes=static, num_workers=nw)
+                          shuffle=True, static_shapes=static, num_workers=nw, static_caps=caps)
 
 
 def test_static_batch_head_gives_the_exact_pair_graphs():
@@ -169,8 +169,9 @@ def test_static_step_trains_as_the_exact_step(monkeypatch, agg, fold, fanouts):
         _close(gb[n], ga[n], n)
 
 
-@pytest.mark.parametrize("nw,fanouts", [(0, (4, 3)), (2, (4, 3)), (0, (64, 64))])
-def test_captured_steps_train_as_the_eager_loop(nw, fanouts):
+@pytest.mark.parametrize("nw,fanouts,caps", [(0, (4, 3), "provable"), (2, (4, 3), "provable"),
+                                             (0, (64, 64), "provable"), (2, (4, 3), "auto")])
+def test_captured_steps_train_as_the_eager_loop(nw, fanouts, caps):
     """CapturedTrainStep over a static loader (warm-up steps, capture, replays, the exact
     partial batch eagerly) against the eager loop over the exact loader: per-step losses and
     the final parameters agree."""
@@ -189,14 +190,15 @@ def test_captured_steps_train_as_the_eager_loop(nw, fanouts):
         # eagerly, replays again (further on, a hinge of the margin loss flipped by the two
         # runs' fp32 rounding differences moves the losses apart by one term)
         for epoch in range(2):
-            for k, batch in enumerate(_loader(g, captured, K=K, fanouts=fanouts,
+            for k, batch in enumerate(_loader(g, captured, K=K, fanouts=fanouts, caps=caps,
                                               nw=nw if captured else 0)):
                 if epoch == 0 or k < 3:
                     loss = step(batch) if captured else step.eager(batch)
                     losses.append(float(loss.detach()))
         runs.append((losses, m, step))
     (la, ma, _), (lb, mb, st) = runs
-    assert st.replays == 700 // 64 - 1 + 3 and st.eager_steps == 1 + 1
+    learn = 3 if caps == "auto" else 0  # exact batches that fix the learned capacities
+    assert st.replays == 700 // 64 - 1 - learn + 3 and st.eager_steps == 1 + 1 + learn
     np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
     for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         _close(pb.detach(), pa.detach(), n, rtol=2e-3, atol=2e-5)
@@ -219,3 +221,22 @@ def test_copy_batch_equals_tensor_copies():
     ops.copy_batch(src, dst)
     for s, d in zip(src, dst):
         assert torch.equal(s, d)
+
+
+def test_learned_caps_shrink_the_blocks_and_overflow_is_redone():
+    """static_caps='auto': after 3 exact batches the source lists get learned capacities,
+    below the provable ones where a fanout reaches most of a type (items here); a batch that
+    outgrows them raises the sampler's overflow flag — memory-safe — and is redone exactly."""
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    prov = [x for x in _loader(g, True, fanouts=(10, 10), caps="provable")]
+    auto_l = _loader(g, True, fanouts=(10, 10), caps="auto")
+    auto = list(auto_l)
+    assert [x[1].static for x in auto[:3]] == [False] * 3 and auto[3][1].static
+    rows = lambda item: sum(b.number_of_src_nodes(nt) for b in item[-1] for nt in b.ntypes)  # noqa: E731
+    assert rows(auto[3]) <= rows(prov[3])
+    tight = _loader(g, True, fanouts=(10, 10), caps="auto")
+    tight._node_hint = {(s_, nt): 1 for s_ in range(2) for nt in ("user", "item")}
+    item = next(iter(tight))
+    assert tight.static_redone == 1 and not item[1].static and not item[-1][0].static
+    loss = _loss(4)(_model(g, agg="mean").train(), item)
+    assert torch.isfinite(loss)
