@@ -197,8 +197,11 @@ def test_captured_steps_train_as_the_eager_loop(nw, fanouts, caps):
                     losses.append(float(loss.detach()))
         runs.append((losses, m, step))
     (la, ma, _), (lb, mb, st) = runs
-    learn = 3 if caps == "auto" else 0  # exact batches that fix the learned capacities
-    assert st.replays == 700 // 64 - 1 - learn + 3 and st.eager_steps == 1 + 1 + learn
+    full = 700 // 64
+    if caps == "auto":  # each epoch's loader first learns its capacities on 3 exact batches
+        assert st.replays == full - 3 - 1 and st.eager_steps == 3 + 1 + 1 + 3
+    else:
+        assert st.replays == full - 1 + 3 and st.eager_steps == 1 + 1
     np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
     for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         _close(pb.detach(), pa.detach(), n, rtol=2e-3, atol=2e-5)
