@@ -595,7 +595,7 @@ class EdgeDataLoader:
                  negative_sampler=None, batch_size: int = 1, shuffle: bool = False,
                  drop_last: bool = False, num_workers: int = 0, pin_memory: bool = False,
                  transposed_blocks: bool = True, static_shapes: bool = False,
-                 static_caps: str = "auto", **kwargs):
+                 static_caps: str = "provable", **kwargs):
         self.g = g
         self.g_sampling = g_sampling if g_sampling is not None else g
         # the training loader's blocks carry their source-major CSRs (built by the sampler,
@@ -638,12 +638,15 @@ class EdgeDataLoader:
         # captured once and replayed (gnnrec.capture.CapturedTrainStep); a final partial
         # batch comes in the ordinary exact form
         self.static_shapes = static_shapes
-        # static_caps: 'provable' — the capacities no batch can exceed (a graph-sized source
-        # list where the fanout can reach most of a node type: C2 at K = 2500 pads its first
-        # block's 7.3M edges to 11M); 'auto' — the first STATIC_LEARN full batches come out
-        # exact, and their largest source lists x STATIC_MARGIN (+ a padding slot) become the
-        # node capacities: a later batch that does not fit (the sampler's overflow flag, read
-        # back in the loader's thread) is redone exactly and the capacities grow
+        # static_caps: 'provable' (default) — the capacities no batch can exceed (a graph-sized
+        # source list where the fanout can reach most of a node type: C2 at K = 2500 pads its
+        # first block's 7.3M edges to 11M); 'auto' — the first STATIC_LEARN full batches come
+        # out exact, and their largest source lists x STATIC_MARGIN (+ a padding slot) become
+        # the node capacities: a later batch that does not fit (the sampler's overflow flag,
+        # read back in the loader's thread) is redone exactly and the capacities grow.  The
+        # read-back makes the loader wait for its own kernels, which then queue behind the
+        # training step's: C2 K = 2500 replays drop 3.22 -> 2.81 ms of GPU time but the step
+        # went 4.6 -> 6.6 ms (profiles/r05l_captured_step_probe_learned_caps.json)
         if static_caps not in ("auto", "provable"):
             raise ValueError(f"static_caps={static_caps!r}: 'auto' or 'provable'")
         self.static_caps = static_caps
