@@ -1521,7 +1521,7 @@ sample_layer(at::TensorList indptrs, at::TensorList indices, at::TensorList eids
 //   eids; per step and type ([s][t]): the source node ids (seeds first); the sizes (node
 //   counts rows -1..L-1 x T, then edge counts L x R).
 std::tuple<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>,
-           std::vector<int64_t>>
+           std::vector<int64_t>, std::vector<Tensor>>
 sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eids,
               at::IntArrayRef src_type, at::IntArrayRef dst_type,
               const c10::List<optional<Tensor>>& excl_eids,
@@ -1531,7 +1531,9 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               at::TensorList seeds, at::TensorList pos, at::TensorList bits,
               at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
               int64_t steps, int64_t stamp, bool static_shapes, const optional<Tensor>& sizes_out,
-              at::IntArrayRef node_cap_hint, const optional<Tensor>& overflow) {
+              at::IntArrayRef node_cap_hint, const optional<Tensor>& overflow,
+              at::TensorList edge_tables, at::IntArrayRef edge_table_rel,
+              at::TensorList node_tables, at::IntArrayRef node_table_type) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = n_nodes.size();
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
@@ -1670,6 +1672,50 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
   P.sizes = p<int64_t>(sizes);
   P.workspace = ws.data_ptr();
   ck(gnnrec_sample_blocks(&P, stream_of(pos[0])), "gnnrec_sample_blocks");
+  // the block data (a10): every step's edge data tables at its edge ids, the input block's
+  // node tables at its source ids — queued behind the sampler, row counts read on the device
+  // (static shapes: every slot; -1 ids give zero rows), ahead of the one size read below
+  TORCH_CHECK_VALUE(edge_table_rel.size() == edge_tables.size() &&
+                        node_table_type.size() == node_tables.size(),
+                    "sample_blocks: one relation / node type per data table");
+  std::vector<Tensor> gathered;
+  std::vector<gnnrec_gather_job> jobs;
+  auto add_job = [&](const Tensor& src, const Tensor& idx, int64_t n, const int64_t* n_dev) {
+    TORCH_CHECK_VALUE(src.is_cuda() && src.dim() >= 1, "sample_blocks: data tables on the device");
+    same_dev(src, "data table");
+    std::vector<int64_t> shape(src.sizes().begin(), src.sizes().end());
+    shape[0] = n;
+    int64_t inner = 1;
+    for (int64_t k = src.dim() - 1; k >= 1; --k) {
+      TORCH_CHECK_VALUE(src.size(k) <= 1 || src.stride(k) == inner,
+                        "sample_blocks: data table rows must be contiguous");
+      inner *= src.size(k);
+    }
+    Tensor out = at::empty(shape, src.options());
+    const int64_t es = src.element_size();
+    jobs.push_back(gnnrec_gather_job{src.data_ptr(), src.stride(0) * es, p<int64_t>(idx), n,
+                                     inner * es, out.data_ptr(), inner * es, n_dev});
+    gathered.push_back(out);
+  };
+  const bool exact = !static_shapes;
+  for (int64_t s = 0; s < steps; ++s)
+    for (size_t j = 0; j < edge_tables.size(); ++j) {
+      const int64_t r = edge_table_rel[j];
+      TORCH_CHECK_VALUE(r >= 0 && (size_t)r < R, "sample_blocks: edge table relation");
+      add_job(edge_tables[j], o_eid[s * R + r], edge_cap[s * GNNREC_SB_MAX_RELS + r],
+              exact ? p<int64_t>(sizes) + (steps + 1) * NT + s * R + r : nullptr);
+    }
+  for (size_t j = 0; j < node_tables.size(); ++j) {
+    const int64_t t = node_table_type[j];
+    TORCH_CHECK_VALUE(t >= 0 && (size_t)t < NT, "sample_blocks: node table type");
+    add_job(node_tables[j], nodes[(steps - 1) * NT + t], node_len(steps - 1, t),
+            exact ? p<int64_t>(sizes) + steps * NT + t : nullptr);
+  }
+  for (size_t i = 0; i < jobs.size(); i += GNNREC_GATHER_MAX_JOBS)
+    ck(gnnrec_gather_rows_batch(jobs.data() + i,
+                                (int)std::min<size_t>(GNNREC_GATHER_MAX_JOBS, jobs.size() - i),
+                                stream_of(pos[0])),
+       "gnnrec_gather_rows_batch");
   if (static_shapes || has(sizes_out)) {  // every output at its capacity: return those
     std::vector<int64_t> caps;  // seed caps [T], node caps [L x T], edge caps [L x R], and
     for (size_t t = 0; t < NT; ++t) caps.push_back(seed_cap[t]);  // dump rows [L x T]
@@ -1679,7 +1725,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
       for (size_t r = 0; r < R; ++r) caps.push_back(edge_cap[s * GNNREC_SB_MAX_RELS + r]);
     for (int64_t s = 0; s < steps; ++s)
       for (size_t t = 0; t < NT; ++t) caps.push_back(dump_rows[s * GNNREC_SB_MAX_TYPES + t]);
-    return {o_ip, o_src, o_eid, nodes, caps};
+    return {o_ip, o_src, o_eid, nodes, caps, gathered};
   }
   const Tensor hs = sizes.to(at::kCPU);  // the call's one size readback
   const int64_t* h = hs.data_ptr<int64_t>();
@@ -1695,7 +1741,13 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     for (size_t t = 0; t < NT; ++t)
       nodes[s * NT + t] = nodes[s * NT + t].narrow(0, 0, h[(s + 1) * NT + t]);
   }
-  return {o_ip, o_src, o_eid, nodes, out_sizes};
+  size_t gi = 0;
+  for (int64_t s = 0; s < steps; ++s)
+    for (size_t j = 0; j < edge_tables.size(); ++j, ++gi)
+      gathered[gi] = gathered[gi].narrow(0, 0, h[(steps + 1) * NT + s * R + edge_table_rel[j]]);
+  for (size_t j = 0; j < node_tables.size(); ++j, ++gi)
+    gathered[gi] = gathered[gi].narrow(0, 0, h[steps * NT + node_table_type[j]]);
+  return {o_ip, o_src, o_eid, nodes, out_sizes, gathered};
 }
 
 // a10: several row gathers in one launch (gnnrec_gather_rows_batch): out[j] = src[j][idx[j]]
@@ -2052,10 +2104,10 @@ TORCH_LIBRARY(gnnrec, m) {
         "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
         "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
         "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
-        "int stamp, bool static_shapes=False, Tensor(d!)? sizes_out=None, int[] node_cap_hint=[], "
-        "Tensor(e!)? overflow=None) -> (Tensor[] out_indptr, "
-        "Tensor[] src_local, Tensor[] eids, "
-        "Tensor[] src_nid, int[] sizes)");
+        "int stamp, bool static_shapes, Tensor(d!)? sizes_out, int[] node_cap_hint, "
+        "Tensor(e!)? overflow, Tensor[] edge_tables, int[] edge_table_rel, Tensor[] node_tables, "
+        "int[] node_table_type) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
+        "Tensor[] src_nid, int[] sizes, Tensor[] data)");
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");
   m.def("copy_batch(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("compact_ids(Tensor[] ids, int[] type, int[] n_nodes, int[] caps, Tensor(a!)[] bits, "

@@ -1259,7 +1259,7 @@ class SampleScratch:
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
                   fanouts, keys, stamp, static_shapes=False, sizes_out=None, node_cap_hint=None,
-                  overflow=None):
+                  overflow=None, edge_tables=(), node_tables=()):
     """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
     1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
     output block); excl: per relation None or (eids, coo_dst, mask, rows).
@@ -1272,22 +1272,28 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
     them on the device (gather_rows_batch's n_dev) before it reads them itself; the returned
     sizes are the capacities then too.  node_cap_hint ([step][type], static): tighter node
     capacities than the provable ones; a batch that does not fit sets `overflow` (int64
-    device flag) and must be discarded or redone."""
+    device flag) and must be discarded or redone.
+    edge_tables [(table, relation)] / node_tables [(table, node type)]: the block data (a10),
+    gathered inside the call — every step's edge data at its edge ids, the input block's
+    (the last step's) node rows at its source ids — returned as a third value in that order
+    (step-major for the edge tables)."""
     steps, R = len(fanouts), len(indptrs)
     ex = [e if e is not None else (None,) * 4 for e in excl]
-    o_ip, o_src, o_eid, nodes, sizes = _T().sample_blocks(
+    o_ip, o_src, o_eid, nodes, sizes, data = _T().sample_blocks(
         list(indptrs), list(indices), list(eids), list(src_type), list(dst_type),
         [e[0] for e in ex], [e[1] for e in ex], [e[2] for e in ex], [e[3] for e in ex],
         list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
         [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
         [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes),
-        sizes_out, [int(h) for hs in (node_cap_hint or []) for h in hs], overflow)
+        sizes_out, [int(h) for hs in (node_cap_hint or []) for h in hs], overflow,
+        [t for t, _ in edge_tables], [int(r) for _, r in edge_tables],
+        [t for t, _ in node_tables], [int(x) for _, x in node_tables])
     NT = len(n_nodes)
     out = []
     for s in range(steps):
         out.append(([o_ip[s * R + r] for r in range(R)], [o_src[s * R + r] for r in range(R)],
                     [o_eid[s * R + r] for r in range(R)], [nodes[s * NT + t] for t in range(NT)]))
-    return out, sizes
+    return out, sizes, data
 
 
 class CompactScratch:

@@ -153,34 +153,22 @@ class BlockSampler:
         keys = [[_mix(self.seed, self._calls, L - 1 - s, r) for r in range(len(ces))]
                 for s in range(L)]
         NT, R = len(nts), len(ces)
-        # exact sizes: left on the device while the block data gathers are queued behind the
-        # sampler (row counts read there), then ONE host read sizes every block
-        sizes_dev = None if static else torch.empty((L + 1) * NT + L * R, dtype=torch.int64,
-                                                    device=g.device)
-        steps, sizes = ops.sample_blocks(
+        # the block data (DGL copies it at block creation; the reference reads
+        # blocks[0].srcdata['features']) is gathered inside the call, behind the sampler and
+        # ahead of its one size read; static: -1 ids -> zero rows
+        etab = [(ce, k, v if v.dim() < 2 or v[0].is_contiguous() else v.contiguous())
+                for ce in ces for k, v in g._edata[ce].items()]
+        ntab = [(nt, k, v if v.dim() < 2 or v[0].is_contiguous() else v.contiguous())
+                for nt in nts for k, v in g._ndata[nt].items()]
+        steps, sizes, data = ops.sample_blocks(
             [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
             [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
             [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
-            fans, keys, stamp, static_shapes=static, sizes_out=sizes_dev,
+            fans, keys, stamp, static_shapes=static,
             node_cap_hint=[[(hints or {}).get((s_, nt), 0) for nt in nts] for s_ in range(L)]
-            if hints else None, overflow=overflow)
-        # the block data (DGL copies it at block creation; the reference reads
-        # blocks[0].srcdata['features']): every table in one launch; static: -1 ids -> zero rows
-        jobs, dests, cnts = [], [], []
-        for s_, (_ip, _loc, o_eid, nodes) in enumerate(steps):
-            for r, ce in enumerate(ces):
-                for k, v in g._edata[ce].items():
-                    jobs.append((v, o_eid[r]))
-                    dests.append((s_, ce, k))
-                    cnts.append(None if static else sizes_dev[(L + 1) * NT + s_ * R + r:][:1])
-        for t, nt in enumerate(nts):
-            for k, v in g._ndata[nt].items():
-                jobs.append((v, steps[L - 1][3][t]))
-                dests.append((L - 1, nt, k))
-                cnts.append(None if static else sizes_dev[L * NT + t:][:1])
-        gathered = ops.gather_rows_batch(jobs, None if static else cnts) if jobs else []
-        if not static:
-            sizes = sizes_dev.tolist()  # the call's one host read
+            if hints else None, overflow=overflow,
+            edge_tables=[(v, ces.index(ce)) for ce, _k, v in etab],
+            node_tables=[(v, tix[nt]) for nt, _k, v in ntab])
         blocks = []
         for s_, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
             rels = {}
@@ -191,10 +179,7 @@ class BlockSampler:
                     if 0 <= fans[s_][r] <= ops.DEFAULT_SPLIT:  # dump rows: <= 2048 edges
                         ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)
                 else:
-                    ne = sizes[(L + 1) * NT + s_ * R + r]
-                    ip = ip[:sizes[s_ * NT + tix[ce[2]]] + 1]
-                    loc, eid = loc[:ne], eid[:ne]
-                    ip._gnnrec_nnz = ne
+                    ip._gnnrec_nnz = int(sizes[(L + 1) * NT + s_ * R + r])
                     if 0 <= fans[s_][r] <= ops.DEFAULT_SPLIT:
                         ip._gnnrec_split_plan = (ops.DEFAULT_SPLIT, None)  # no heavy rows
                 rels[ce] = (ip, loc, eid)
@@ -202,8 +187,7 @@ class BlockSampler:
                 dump = [int(sizes[NT + L * NT + L * R + s_ * NT + t]) for t in range(NT)]
                 num_dst = {nt: int(sizes[s_ * NT + t]) + dump[t] for t, nt in enumerate(nts)}
             else:
-                num_dst = {nt: sizes[s_ * NT + t] for t, nt in enumerate(nts)}
-                nodes = [n_[:sizes[(s_ + 1) * NT + t]] for t, n_ in enumerate(nodes)]
+                num_dst = {nt: int(sizes[s_ * NT + t]) for t, nt in enumerate(nts)}
             b = Block(dict(zip(nts, nodes)), num_dst, rels)
             if static:
                 # the destination ids are the step's seed slots (-1: padding rows, the dump
@@ -217,12 +201,13 @@ class BlockSampler:
                         dst_ids = steps[s_ - 1][3][t]
                     b._dst[nt][NID] = dst_ids
             blocks.insert(0, b)
-        for (s_, key, k), t in zip(dests, gathered):
+        it = iter(data)
+        for s_ in range(L):
             b = blocks[L - 1 - s_]
-            if isinstance(key, tuple):  # edge data of relation `key`
-                b._edata[key][k] = t if static else t[:b._rels[key][1].numel()]
-            else:  # input features of node type `key`
-                b._src[key][k] = t if static else t[:b.number_of_src_nodes(key)]
+            for ce, k, _v in etab:
+                b._edata[ce][k] = next(it)
+        for nt, k, _v in ntab:
+            blocks[0]._src[nt][k] = next(it)
         if transposes:
             for block_id, b in enumerate(blocks):
                 if block_id > 0 or self._first_transposes(b):
