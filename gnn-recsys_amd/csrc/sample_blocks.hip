@@ -78,6 +78,8 @@ struct TypeArgs {
   unsigned long long* pos_next;  // the next step's (written by finalize)
   unsigned long long* bits_cur;
   unsigned long long* bits_next;
+  uint8_t* mark_cur;       // new-source marks, one byte per node (64 * words), alternating
+  uint8_t* mark_next;
   int64_t* word_rank;
   int64_t words;
   int64_t* nodes;          // this step's source node list (the next step's seeds)
@@ -133,6 +135,25 @@ __device__ __forceinline__ void set_pos(unsigned long long* pos, int64_t id, uin
                          __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 64 mark bytes (each 0 / 1) -> their word of the bitmap.  New sources are MARKED by plain
+// byte stores, not OR-ed into the bitmap: at C2 the 1.1M picks of a step land on 100k items,
+// ~700 atomic ORs per 64-item word, serialised at the L2 (the pick kernel's largest cost);
+// the scan builds each word from its 64 bytes instead.
+__device__ __forceinline__ unsigned long long word_of_marks(const uint8_t* __restrict__ m) {
+  unsigned long long w = 0ull;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint4 x = reinterpret_cast<const uint4*>(m)[q];
+    const uint32_t part[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        w |= (unsigned long long)((part[k] >> (8 * b)) & 1u) << (q * 16 + k * 4 + b);
+  }
+  return w;
+}
+
 // the destination rows of a step: the seeds, or (static shapes) the seed capacity
 __device__ __forceinline__ int64_t seed_rows(const StepArgs& A, const TypeArgs& T) {
   return A.stat ? T.seed_cap : *T.n_seeds;
@@ -159,9 +180,9 @@ __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
         A.sizes_seed_row[i] = v >= 0 ? t + 1 : 0;
       break;
     }
-    case kSecZeroBits: {
+    case kSecZeroBits: {  // the first step's marks (64 B per word, 16 B per thread)
       const TypeArgs& T = A.type[i];
-      if (t < T.words) T.bits_cur[t] = 0ull;
+      if (t < T.words * 4) reinterpret_cast<uint4*>(T.mark_cur)[t] = make_uint4(0, 0, 0, 0);
       break;
     }
     case kSecExclSet: {
@@ -182,10 +203,10 @@ template <int G>
 __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
   const int b = (int)blockIdx.x - A.sec.begin[k];
-  if (A.sec.kind[k] == kSecZeroNext) {
+  if (A.sec.kind[k] == kSecZeroNext) {  // the next step's marks
     const TypeArgs& T = A.type[A.sec.idx[k]];
     const int64_t w = (int64_t)b * kSbBlock + threadIdx.x;
-    if (w < T.words) T.bits_next[w] = 0ull;
+    if (w < T.words * 4) reinterpret_cast<uint4*>(T.mark_next)[w] = make_uint4(0, 0, 0, 0);
     return;
   }
   if (A.sec.kind[k] == kSecZeroScan) {  // the scan's tickets and tile flags, for this step
@@ -242,12 +263,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
     R.pick_src[q] = src;
     R.pick_eid[q] = id;
     // a source that is not one of its type's seeds at this step is a new node
-    if ((uint32_t)(S.pos_cur[src] >> 32) != A.stamp) {
-      unsigned long long* w = S.bits_cur + (src >> 6);
-      const unsigned long long bit = 1ull << (src & 63);
-      if ((*w & bit) == 0ull)
-        __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if ((uint32_t)(S.pos_cur[src] >> 32) != A.stamp) S.mark_cur[src] = 1;
   }
   if (grp.lane == 0) R.counts[i] = c;
 }
@@ -303,7 +319,8 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
   const bool is_rel = seg < A.n_rels;
   int64_t n;
   const int64_t* cnt = nullptr;
-  const unsigned long long* bits = nullptr;
+  unsigned long long* bits = nullptr;
+  const uint8_t* marks = nullptr;
   int64_t* out;
   if (is_rel) {
     const RelArgs& R = A.rel[seg];
@@ -314,6 +331,7 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
     const TypeArgs& T = A.type[seg - A.n_rels];
     n = T.words;
     bits = T.bits_cur;
+    marks = T.mark_cur;
     out = T.word_rank;
   }
   unsigned long long* ticket = A.scan_ws + seg * A.scan_stride;
@@ -330,7 +348,15 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
     const int64_t i = i0 + j;
-    v[j] = i < n ? (is_rel ? cnt[i] : (int64_t)__popcll(bits[i])) : 0;
+    if (i >= n) {
+      v[j] = 0;
+    } else if (is_rel) {
+      v[j] = cnt[i];
+    } else {  // the bitmap word from its marks (finalize ranks new sources in it)
+      const unsigned long long w = word_of_marks(marks + i * 64);
+      bits[i] = w;
+      v[j] = __popcll(w);
+    }
     s += v[j];
   }
   int64_t agg;
@@ -507,6 +533,8 @@ struct CompactArgs {
   int64_t* local[GNNREC_COMPACT_MAX_LISTS];
   unsigned long long* bits_cur[GNNREC_SB_MAX_TYPES];
   unsigned long long* bits_next[GNNREC_SB_MAX_TYPES];
+  uint8_t* mark_cur[GNNREC_SB_MAX_TYPES];
+  uint8_t* mark_next[GNNREC_SB_MAX_TYPES];
   int64_t* word_rank[GNNREC_SB_MAX_TYPES];
   int64_t words[GNNREC_SB_MAX_TYPES];
   int64_t* nodes[GNNREC_SB_MAX_TYPES];
@@ -520,15 +548,13 @@ __global__ __launch_bounds__(kSbBlock) void cx_mark_kernel(CompactArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
   const int64_t t = (int64_t)((int)blockIdx.x - A.sec.begin[k]) * kSbBlock + threadIdx.x;
   const int x = A.sec.idx[k];
-  if (A.sec.kind[k] == kCxZero) {
-    if (t < A.words[x]) A.bits_next[x][t] = 0ull;
+  if (A.sec.kind[k] == kCxZero) {  // the other parity's marks, for the next call
+    if (t < A.words[x] * 4)
+      reinterpret_cast<uint4*>(A.mark_next[x])[t] = make_uint4(0, 0, 0, 0);
     return;
   }
   if (t >= A.n[x]) return;
-  const int64_t id = A.ids[x][t];
-  unsigned long long* w = A.bits_cur[A.type[x]] + (id >> 6);
-  const unsigned long long bit = 1ull << (id & 63);
-  if ((*w & bit) == 0ull) __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  A.mark_cur[A.type[x]][A.ids[x][t]] = 1;  // plain byte stores (see word_of_marks)
 }
 
 __global__ __launch_bounds__(kScanThreads) void cx_scan_kernel(CompactArgs A) {
@@ -536,7 +562,8 @@ __global__ __launch_bounds__(kScanThreads) void cx_scan_kernel(CompactArgs A) {
   constexpr int kItems = 4;
   const int t = (int)blockIdx.x;
   const int64_t n = A.words[t];
-  const unsigned long long* bits = A.bits_cur[t];
+  unsigned long long* bits = A.bits_cur[t];
+  const uint8_t* marks = A.mark_cur[t];
   int64_t* out = A.word_rank[t];
   int64_t carry = 0;
   for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kItems) {
@@ -544,7 +571,12 @@ __global__ __launch_bounds__(kScanThreads) void cx_scan_kernel(CompactArgs A) {
     int64_t v[kItems], sum = 0;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-      v[j] = i0 + j < n ? (int64_t)__popcll(bits[i0 + j]) : 0;
+      v[j] = 0;
+      if (i0 + j < n) {
+        const unsigned long long w = word_of_marks(marks + (i0 + j) * 64);
+        bits[i0 + j] = w;
+        v[j] = __popcll(w);
+      }
       sum += v[j];
     }
     int64_t tot;
@@ -713,8 +745,10 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
   const int R = P->n_rels, T = P->n_types, L = P->n_steps;
   for (int t = 0; t < T; ++t) {
     const gnnrec_sample_type& ty = P->type[t];
-    GNNREC_REQUIRE(ty.pos && ty.bits && ty.word_rank && (ty.n_seeds == 0 || ty.seeds),
+    GNNREC_REQUIRE(ty.pos && ty.bits && ty.marks && ty.word_rank && (ty.n_seeds == 0 || ty.seeds),
                    "gnnrec_sample_blocks: type %d: null scratch or seeds", t);
+    GNNREC_REQUIRE((reinterpret_cast<uintptr_t>(ty.marks) & 15u) == 0,
+                   "gnnrec_sample_blocks: type %d: marks must be 16-byte aligned", t);
     for (int s = 0; s < L; ++s)
       GNNREC_REQUIRE(P->nodes[s][t] || C.node[s][t] == 0,
                      "gnnrec_sample_blocks: null nodes output (step %d, type %d)", s, t);
@@ -780,6 +814,8 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
           reinterpret_cast<unsigned long long*>(ty.pos) + ((A.stamp + 1u) & 1u) * ty.n_nodes;
       a.bits_cur = reinterpret_cast<unsigned long long*>(ty.bits) + (A.stamp & 1u) * W;
       a.bits_next = reinterpret_cast<unsigned long long*>(ty.bits) + ((A.stamp + 1u) & 1u) * W;
+      a.mark_cur = ty.marks + (A.stamp & 1u) * 64 * W;
+      a.mark_next = ty.marks + ((A.stamp + 1u) & 1u) * 64 * W;
       a.word_rank = ty.word_rank;
       a.words = W;
       a.nodes = P->nodes[s][t];
@@ -829,7 +865,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
   A.sec.n = 0;
   A.sec.begin[0] = 0;
   for (int t = 0; t < T; ++t) add_sec(A.sec, kSecSeedPos, t, nblocks(P->type[t].n_seeds));
-  for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroBits, t, nblocks(A.type[t].words));
+  for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroBits, t, nblocks(4 * A.type[t].words));
   for (int r = 0; r < R; ++r) add_sec(A.sec, kSecExclSet, r, nblocks(P->rel[r].n_excl));
   if (A.sec.n == 0) add_sec(A.sec, kSecSeedPos, 0, 1);  // the seed-count row still lands
   hipLaunchKernelGGL(sb_begin_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0, hs,
@@ -847,7 +883,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     for (int r = 0; r < R; ++r)
       add_sec(A.sec, kSecPick, r,
               (int)((C.seed[s][P->rel[r].dst_type] + kSbBlock / G - 1) / (kSbBlock / G)));
-    for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroNext, t, nblocks(A.type[t].words));
+    for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroNext, t, nblocks(4 * A.type[t].words));
     add_sec(A.sec, kSecZeroScan, 0, nblocks(A.scan_words));
     if (A.sec.n) {
       const dim3 grid((unsigned)A.sec.begin[A.sec.n]);
@@ -899,11 +935,14 @@ extern "C" int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
   A.count = count;
   for (int t = 0; t < n_types; ++t) {
     const gnnrec_compact_type& ty = types[t];
-    GNNREC_REQUIRE(ty.n_nodes >= 0 && ty.cap >= 0 && ty.bits && ty.word_rank && (ty.cap == 0 || ty.nodes),
-                   "gnnrec_compact_ids: type %d: sizes / null scratch", t);
+    GNNREC_REQUIRE(ty.n_nodes >= 0 && ty.cap >= 0 && ty.bits && ty.marks && ty.word_rank &&
+                       (ty.cap == 0 || ty.nodes) && (reinterpret_cast<uintptr_t>(ty.marks) & 15u) == 0,
+                   "gnnrec_compact_ids: type %d: sizes / null or unaligned scratch", t);
     const int64_t W = words_of(ty.n_nodes);
     A.bits_cur[t] = reinterpret_cast<unsigned long long*>(ty.bits) + parity * W;
     A.bits_next[t] = reinterpret_cast<unsigned long long*>(ty.bits) + (1 - parity) * W;
+    A.mark_cur[t] = ty.marks + parity * 64 * W;
+    A.mark_next[t] = ty.marks + (1 - parity) * 64 * W;
     A.word_rank[t] = ty.word_rank;
     A.words[t] = W;
     A.nodes[t] = ty.nodes;
@@ -929,7 +968,7 @@ extern "C" int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
   A.sec.n = 0;
   A.sec.begin[0] = 0;
   for (int l = 0; l < n_lists; ++l) add_sec(A.sec, kCxMark, l, nblocks(A.n[l]));
-  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxZero, t, nblocks(A.words[t]));
+  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxZero, t, nblocks(4 * A.words[t]));
   if (A.sec.n) {
     hipLaunchKernelGGL(cx_mark_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0, hs, A);
     if (int st = check_launch("gnnrec_compact_ids(mark)")) return st;

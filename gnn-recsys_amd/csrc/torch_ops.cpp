@@ -1529,8 +1529,9 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               const c10::List<optional<Tensor>>& excl_masks,
               const c10::List<optional<Tensor>>& excl_rows, at::IntArrayRef n_nodes,
               at::TensorList seeds, at::TensorList pos, at::TensorList bits,
-              at::TensorList word_rank, at::IntArrayRef fanouts, at::IntArrayRef keys,
-              int64_t steps, int64_t stamp, bool static_shapes, const optional<Tensor>& sizes_out,
+              at::TensorList word_rank, at::TensorList marks, at::IntArrayRef fanouts,
+              at::IntArrayRef keys, int64_t steps, int64_t stamp, bool static_shapes,
+              const optional<Tensor>& sizes_out,
               at::IntArrayRef node_cap_hint, const optional<Tensor>& overflow,
               at::TensorList edge_tables, at::IntArrayRef edge_table_rel,
               at::TensorList node_tables, at::IntArrayRef node_table_type) {
@@ -1541,8 +1542,8 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
                         excl_masks.size() == R && excl_rows.size() == R,
                     "sample_blocks: one entry per relation in every relation list");
   TORCH_CHECK_VALUE(seeds.size() == NT && pos.size() == NT && bits.size() == NT &&
-                        word_rank.size() == NT,
-                    "sample_blocks: one seed list and one scratch triple per node type");
+                        word_rank.size() == NT && marks.size() == NT,
+                    "sample_blocks: one seed list and one scratch set per node type");
   TORCH_CHECK_VALUE(steps >= 1 && steps <= GNNREC_SB_MAX_STEPS && R <= GNNREC_SB_MAX_RELS &&
                         NT >= 1 && NT <= GNNREC_SB_MAX_TYPES,
                     "sample_blocks: ", steps, " steps, ", R, " relations, ", NT,
@@ -1613,11 +1614,13 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     dev(pos[t], "pos", at::kLong);
     dev(bits[t], "bits", at::kLong);
     dev(word_rank[t], "word_rank", at::kLong);
+    dev(marks[t], "marks", at::kByte);
     const int64_t W = (n_nodes[t] + 63) / 64;
     TORCH_CHECK_VALUE(seeds[t].is_contiguous() && pos[t].numel() == 2 * n_nodes[t] &&
-                          bits[t].numel() == 2 * W && word_rank[t].numel() == W + 1,
+                          bits[t].numel() == 2 * W && word_rank[t].numel() == W + 1 &&
+                          marks[t].numel() == 2 * 64 * W,
                       "sample_blocks: type ", t,
-                      ": scratch sized 2n, 2 ceil(n/64), ceil(n/64)+1");
+                      ": scratch sized 2n, 2 ceil(n/64), ceil(n/64)+1, 128 ceil(n/64) bytes");
     gnnrec_sample_type& ty = P.type[t];
     ty.n_nodes = n_nodes[t];
     ty.seeds = p<int64_t>(seeds[t]);
@@ -1625,6 +1628,7 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     ty.pos = p<int64_t>(pos[t]);
     ty.bits = p<uint64_t>(bits[t]);
     ty.word_rank = p<int64_t>(word_rank[t]);
+    ty.marks = p<uint8_t>(marks[t]);
   }
   int64_t seed_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_TYPES];
   int64_t edge_cap[GNNREC_SB_MAX_STEPS * GNNREC_SB_MAX_RELS];
@@ -1801,12 +1805,13 @@ void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList ou
 // word_rank [ceil(n/64) + 1] per type; bits zero before the first call, parity alternating.
 std::tuple<std::vector<Tensor>, std::vector<Tensor>, Tensor>
 compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
-            at::IntArrayRef caps, at::TensorList bits, at::TensorList word_rank, int64_t parity) {
+            at::IntArrayRef caps, at::TensorList bits, at::TensorList word_rank,
+            at::TensorList marks, int64_t parity) {
   const OneDevice one_device_;
   const size_t L = ids.size(), NT = n_nodes.size();
   TORCH_CHECK_VALUE(type.size() == L && L <= GNNREC_COMPACT_MAX_LISTS && NT >= 1 &&
                         NT <= GNNREC_SB_MAX_TYPES && caps.size() == NT && bits.size() == NT &&
-                        word_rank.size() == NT,
+                        word_rank.size() == NT && marks.size() == NT,
                     "compact_ids: at most ", GNNREC_COMPACT_MAX_LISTS, " lists (one type each) "
                     "and 1..", GNNREC_SB_MAX_TYPES, " types (a cap and a scratch pair each)");
   TORCH_CHECK_VALUE(parity == 0 || parity == 1, "compact_ids: parity is 0 or 1");
@@ -1819,12 +1824,14 @@ compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
     dev(bits[t], "bits", at::kLong);
     dev(word_rank[t], "word_rank", at::kLong);
     const int64_t W = (n_nodes[t] + 63) / 64;
+    dev(marks[t], "marks", at::kByte);
     TORCH_CHECK_VALUE(n_nodes[t] >= 0 && caps[t] >= 0 && bits[t].numel() == 2 * W &&
-                          word_rank[t].numel() == W + 1,
-                      "compact_ids: type ", t, ": scratch sized 2 ceil(n/64), ceil(n/64)+1");
+                          word_rank[t].numel() == W + 1 && marks[t].numel() == 2 * 64 * W,
+                      "compact_ids: type ", t,
+                      ": scratch sized 2 ceil(n/64), ceil(n/64)+1, 128 ceil(n/64) bytes");
     nodes[t] = at::empty({caps[t]}, i64);
     T[t] = gnnrec_compact_type{n_nodes[t], p<uint64_t>(bits[t]), p<int64_t>(word_rank[t]),
-                               p<int64_t>(nodes[t]), caps[t]};
+                               p<int64_t>(nodes[t]), caps[t], p<uint8_t>(marks[t])};
   }
   for (size_t l = 0; l < L; ++l) {
     dev(ids[l], "ids", at::kLong);
@@ -2103,7 +2110,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("sample_blocks(Tensor[] indptrs, Tensor[] indices, Tensor[] eids, int[] src_type, "
         "int[] dst_type, Tensor?[] excl_eids, Tensor?[] coo_dst, Tensor?[] excl_masks, "
         "Tensor?[] excl_rows, int[] n_nodes, Tensor[] seeds, Tensor(a!)[] pos, "
-        "Tensor(b!)[] bits, Tensor(c!)[] word_rank, int[] fanouts, int[] keys, int steps, "
+        "Tensor(b!)[] bits, Tensor(c!)[] word_rank, Tensor(f!)[] marks, int[] fanouts, "
+        "int[] keys, int steps, "
         "int stamp, bool static_shapes, Tensor(d!)? sizes_out, int[] node_cap_hint, "
         "Tensor(e!)? overflow, Tensor[] edge_tables, int[] edge_table_rel, Tensor[] node_tables, "
         "int[] node_table_type) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
@@ -2111,7 +2119,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");
   m.def("copy_batch(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("compact_ids(Tensor[] ids, int[] type, int[] n_nodes, int[] caps, Tensor(a!)[] bits, "
-        "Tensor(b!)[] word_rank, int parity) -> (Tensor[] nodes, Tensor[] local, Tensor count)");
+        "Tensor(b!)[] word_rank, Tensor(c!)[] marks, int parity) -> (Tensor[] nodes, "
+        "Tensor[] local, Tensor count)");
   // host-only entry points (no tensors: one catch-all kernel each)
   m.def("version() -> int", &version);
   m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);

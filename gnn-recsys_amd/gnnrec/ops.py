@@ -1255,6 +1255,7 @@ class SampleScratch:
         self.pos = torch.zeros(2 * n_nodes, dtype=torch.int64, device=device)
         self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
         self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
+        self.marks = torch.zeros(2 * 64 * w, dtype=torch.uint8, device=device)
 
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
@@ -1283,7 +1284,8 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
         list(indptrs), list(indices), list(eids), list(src_type), list(dst_type),
         [e[0] for e in ex], [e[1] for e in ex], [e[2] for e in ex], [e[3] for e in ex],
         list(n_nodes), list(seeds), [s.pos for s in scratch], [s.bits for s in scratch],
-        [s.word_rank for s in scratch], [int(f) for fs in fanouts for f in fs],
+        [s.word_rank for s in scratch], [s.marks for s in scratch],
+        [int(f) for fs in fanouts for f in fs],
         [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes),
         sizes_out, [int(h) for hs in (node_cap_hint or []) for h in hs], overflow,
         [t for t, _ in edge_tables], [int(r) for _, r in edge_tables],
@@ -1305,6 +1307,7 @@ class CompactScratch:
         self.n_nodes = n_nodes
         self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
         self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
+        self.marks = torch.zeros(2 * 64 * w, dtype=torch.uint8, device=device)
         self.parity = 0
 
 
@@ -1318,7 +1321,8 @@ def compact_ids(lists, scratch, caps):
     parity = scratch[0].parity
     out = _T().compact_ids([ids.contiguous() for ids, _ in lists], [int(t) for _, t in lists],
                            [s.n_nodes for s in scratch], [int(c) for c in caps],
-                           [s.bits for s in scratch], [s.word_rank for s in scratch], parity)
+                           [s.bits for s in scratch], [s.word_rank for s in scratch],
+                           [s.marks for s in scratch], parity)
     for s in scratch:
         s.parity = 1 - parity
     return out

@@ -437,6 +437,9 @@ typedef struct gnnrec_sample_type {
   int64_t* pos;         /* scratch, see above: [2 * n_nodes] */
   uint64_t* bits;
   int64_t* word_rank;
+  uint8_t* marks;       /* scratch: [2 * 64 * ceil(n_nodes/64)] bytes, zero before the first
+                         * call, 16-byte aligned (new sources are marked by byte stores, the
+                         * scan packs them into `bits`) */
 } gnnrec_sample_type;
 
 typedef struct gnnrec_sample_plan {
@@ -498,6 +501,8 @@ typedef struct gnnrec_compact_type {
   int64_t* word_rank;
   int64_t* nodes;     /* [cap] out */
   int64_t cap;
+  uint8_t* marks;     /* [2 * 64 * ceil(n_nodes/64)] bytes, zero before the first call,
+                       * 16-byte aligned, parity halves like `bits` */
 } gnnrec_compact_type;
 int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
                        const gnnrec_compact_type* types, int n_types, int parity, int64_t* count,
