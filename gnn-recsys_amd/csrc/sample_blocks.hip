@@ -40,7 +40,7 @@ namespace gnnrec {
 namespace {
 
 constexpr int kSbBlock = 256;
-constexpr int64_t kDumpEdges = 256;  // a static block's dump row (<= ops.DEFAULT_SPLIT): short, no straggler
+constexpr int64_t kDumpEdges = 2048;  // a static block's dump row: at most ops.DEFAULT_SPLIT
 constexpr int kScanThreads = 1024;
 constexpr int kMaxSec = 4 * GNNREC_SB_MAX_TYPES + 2 * GNNREC_SB_MAX_RELS;
 
