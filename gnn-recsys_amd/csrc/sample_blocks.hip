@@ -311,6 +311,46 @@ __device__ __forceinline__ int64_t flag_value(unsigned long long f) {
   return (int64_t)(f << 2) >> 2;
 }
 
+// The first wave of a tile's block (threadIdx.x < 64): publish the tile's aggregate, walk back
+// over the predecessors' flags 64 at a time until an inclusive prefix, publish the tile's own
+// inclusive value -> the tile's exclusive prefix (every lane).  Tile 0 publishes at once.
+__device__ __forceinline__ int64_t look_back(unsigned long long* flags, int64_t tile,
+                                             int64_t agg) {
+  const int lane = threadIdx.x & 63;
+  if (tile == 0) {
+    if (lane == 0)
+      __hip_atomic_store(flags, flag_pack(kFlagIncl, agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0)
+    __hip_atomic_store(flags + tile, flag_pack(kFlagAgg, agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  int64_t prefix = 0;
+  for (int64_t j = tile - 1;; j -= 64) {  // window [j - 63, j], nearest first
+    const int64_t idx = j - lane;
+    unsigned long long f = kFlagIncl;  // before tile 0: an inclusive prefix of 0
+    if (idx >= 0) {
+      f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((f >> 62) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const uint64_t incl = __ballot((f >> 62) == 2);
+    const int stop = incl ? __builtin_ctzll(incl) : 64;
+    int64_t x = lane <= stop ? flag_value(f) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    prefix += x;
+    if (incl) break;
+  }
+  if (lane == 0)
+    __hip_atomic_store(flags + tile, flag_pack(kFlagIncl, prefix + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
+
 __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
   __shared__ int64_t wsum[kScanThreads / 64];
   __shared__ int64_t sh_tile, sh_prefix;
@@ -362,42 +402,8 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
   int64_t agg;
   const int64_t ex = block_excl_scan(s, wsum, &agg);
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    if (tile == 0) {
-      if (lane == 0) {
-        __hip_atomic_store(flags, flag_pack(kFlagIncl, agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        sh_prefix = 0;
-      }
-    } else {
-      if (lane == 0)
-        __hip_atomic_store(flags + tile, flag_pack(kFlagAgg, agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      int64_t prefix = 0;
-      for (int64_t j = tile - 1;; j -= 64) {  // window [j - 63, j], nearest first
-        const int64_t idx = j - lane;
-        unsigned long long f = kFlagIncl;  // before tile 0: an inclusive prefix of 0
-        if (idx >= 0) {
-          f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          while ((f >> 62) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            f = __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        const uint64_t incl = __ballot((f >> 62) == 2);
-        const int stop = incl ? __builtin_ctzll(incl) : 64;
-        int64_t x = lane <= stop ? flag_value(f) : 0;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        prefix += x;
-        if (incl) break;
-      }
-      if (lane == 0) {
-        __hip_atomic_store(flags + tile, flag_pack(kFlagIncl, prefix + agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        sh_prefix = prefix;
-      }
-    }
+    const int64_t pr = look_back(flags, tile, agg);
+    if (threadIdx.x == 0) sh_prefix = pr;
   }
   __syncthreads();
   int64_t run = sh_prefix + ex;
@@ -540,9 +546,15 @@ struct CompactArgs {
   int64_t* nodes[GNNREC_SB_MAX_TYPES];
   int64_t cap[GNNREC_SB_MAX_TYPES];
   int64_t* count;
+  unsigned long long* scan_ws[GNNREC_SB_MAX_TYPES];  // ticket + tile flags per type
+  int tile0[GNNREC_SB_MAX_TYPES + 1];                // first scan block of each type
   Sections sec;
 };
-enum { kCxMark, kCxZero, kCxLocal, kCxNodes, kCxPad };
+enum { kCxMark, kCxZero, kCxZeroScan, kCxLocal, kCxNodes, kCxPad };
+constexpr int64_t kCxTile = kScanThreads;  // bitmap words per scan tile (64 KiB of marks)
+__host__ __device__ inline int64_t cx_tiles(int64_t words) {
+  return words > 0 ? (words + kCxTile - 1) / kCxTile : 1;
+}
 
 __global__ __launch_bounds__(kSbBlock) void cx_mark_kernel(CompactArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
@@ -553,44 +565,49 @@ __global__ __launch_bounds__(kSbBlock) void cx_mark_kernel(CompactArgs A) {
       reinterpret_cast<uint4*>(A.mark_next[x])[t] = make_uint4(0, 0, 0, 0);
     return;
   }
+  if (A.sec.kind[k] == kCxZeroScan) {  // this call's scan ticket and tile flags
+    if (t < 1 + cx_tiles(A.words[x])) A.scan_ws[x][t] = 0ull;
+    return;
+  }
   if (t >= A.n[x]) return;
   A.mark_cur[A.type[x]][A.ids[x][t]] = 1;  // plain byte stores (see word_of_marks)
 }
 
+// Per type the bitmap words from the marks and their exclusive popcount ranks: chained tiles
+// of kCxTile words with decoupled look-back, as sb_scan_kernel (one block per type walked a
+// 1M-node type's 1 MB of marks alone: 56 us of a K = 10 batch's 445)
 __global__ __launch_bounds__(kScanThreads) void cx_scan_kernel(CompactArgs A) {
   __shared__ int64_t wsum[kScanThreads / 64];
-  constexpr int kItems = 4;
-  const int t = (int)blockIdx.x;
+  __shared__ int64_t sh_tile, sh_prefix;
+  int t = 0;
+  while (t + 1 < A.n_types && (int)blockIdx.x >= A.tile0[t + 1]) ++t;
   const int64_t n = A.words[t];
-  unsigned long long* bits = A.bits_cur[t];
-  const uint8_t* marks = A.mark_cur[t];
-  int64_t* out = A.word_rank[t];
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kItems) {
-    const int64_t i0 = base + (int64_t)threadIdx.x * kItems;
-    int64_t v[kItems], sum = 0;
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      v[j] = 0;
-      if (i0 + j < n) {
-        const unsigned long long w = word_of_marks(marks + (i0 + j) * 64);
-        bits[i0 + j] = w;
-        v[j] = __popcll(w);
-      }
-      sum += v[j];
-    }
-    int64_t tot;
-    int64_t run = carry + block_excl_scan(sum, wsum, &tot);
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      if (i0 + j < n) out[i0 + j] = run;
-      run += v[j];
-    }
-    carry += tot;
+  unsigned long long* ticket = A.scan_ws[t];
+  if (threadIdx.x == 0)
+    sh_tile = (int64_t)__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int64_t tile = sh_tile;
+  const int64_t n_tiles = cx_tiles(n);
+  if (tile >= n_tiles) return;  // block-uniform
+  const int64_t i = tile * kCxTile + threadIdx.x;
+  int64_t v = 0;
+  if (i < n) {
+    const unsigned long long w = word_of_marks(A.mark_cur[t] + i * 64);
+    A.bits_cur[t][i] = w;
+    v = __popcll(w);
   }
-  if (threadIdx.x == 0) {
-    out[n] = carry;
-    A.count[t] = carry;
+  int64_t agg;
+  const int64_t ex = block_excl_scan(v, wsum, &agg);
+  if (threadIdx.x < 64) {
+    const int64_t pr = look_back(ticket + 1, tile, agg);
+    if (threadIdx.x == 0) sh_prefix = pr;
+  }
+  __syncthreads();
+  if (i < n) A.word_rank[t][i] = sh_prefix + ex;
+  if (tile == n_tiles - 1 && threadIdx.x == 0) {
+    A.word_rank[t][n] = sh_prefix + agg;
+    A.count[t] = sh_prefix + agg;
   }
 }
 
@@ -947,7 +964,11 @@ extern "C" int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
     A.words[t] = W;
     A.nodes[t] = ty.nodes;
     A.cap[t] = ty.cap;
+    GNNREC_REQUIRE(ty.scan_ws, "gnnrec_compact_ids: type %d: null scan_ws", t);
+    A.scan_ws[t] = reinterpret_cast<unsigned long long*>(ty.scan_ws);
   }
+  A.tile0[0] = 0;
+  for (int t = 0; t < n_types; ++t) A.tile0[t + 1] = A.tile0[t] + (int)cx_tiles(A.words[t]);
   for (int l = 0; l < n_lists; ++l) {
     const gnnrec_compact_list& li = lists[l];
     GNNREC_REQUIRE(li.n >= 0 && li.type >= 0 && li.type < n_types && (li.n == 0 || (li.ids && li.local)),
@@ -969,11 +990,13 @@ extern "C" int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
   A.sec.begin[0] = 0;
   for (int l = 0; l < n_lists; ++l) add_sec(A.sec, kCxMark, l, nblocks(A.n[l]));
   for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxZero, t, nblocks(4 * A.words[t]));
-  if (A.sec.n) {
+  for (int t = 0; t < n_types; ++t) add_sec(A.sec, kCxZeroScan, t, nblocks(1 + cx_tiles(A.words[t])));
+  {
     hipLaunchKernelGGL(cx_mark_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock), 0, hs, A);
     if (int st = check_launch("gnnrec_compact_ids(mark)")) return st;
   }
-  hipLaunchKernelGGL(cx_scan_kernel, dim3((unsigned)n_types), dim3(kScanThreads), 0, hs, A);
+  hipLaunchKernelGGL(cx_scan_kernel, dim3((unsigned)A.tile0[n_types]), dim3(kScanThreads), 0, hs,
+                     A);
   if (int st = check_launch("gnnrec_compact_ids(scan)")) return st;
   A.sec.n = 0;
   A.sec.begin[0] = 0;

@@ -680,21 +680,26 @@ void topk_rows(const Tensor& scores, int64_t k, const optional<Tensor>& exclude_
 
 // ---------------------------------------------------------------- f2 training
 void gemm_tn(const Tensor& A, const Tensor& B, const optional<Tensor>& colsum, bool accumulate,
-             Tensor& out, Tensor& ws) {
+             Tensor& out, Tensor& ws, const optional<Tensor>& row_ptr) {
   const OneDevice one_device_;
   dev(A, "A", at::kFloat);
   dev(B, "B", at::kFloat);
   dev(colsum, "colsum", at::kFloat);
   dev(out, "out", at::kFloat);
+  dev(row_ptr, "row_ptr", at::kLong);
   const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
   TORCH_CHECK_VALUE(B.size(0) == K, "gemm_tn: A and B differ in K");
   TORCH_CHECK_VALUE(out.size(0) == M && out.size(1) == N, "out must be [", M, ", ", N, "]");
+  TORCH_CHECK_VALUE(!has(row_ptr) || (has(colsum) && row_ptr->numel() == K + 1 &&
+                                      row_ptr->is_contiguous()),
+                    "gemm_tn: row_ptr must be a contiguous [", K + 1, "] indptr beside colsum");
   const int64_t lda = ld(A, "A"), ldb = ld(B, "B"), ldc = ld(out, "out");
   if (meta(A)) return;
   const c10::DeviceGuard g(A.device());
-  ck(gnnrec_gemm_tn_bias_f32(p<float>(A), lda, p<float>(B), ldb, K, M, N, p<float>(out), ldc,
-                             p<float>(colsum), (int)accumulate, p<float>(ws), stream_of(A)),
-     "gnnrec_gemm_tn_bias_f32");
+  ck(gnnrec_gemm_tn_bias_rows_f32(p<float>(A), lda, p<float>(B), ldb, K, M, N, p<float>(out),
+                                  ldc, p<float>(colsum), p<int64_t>(row_ptr), (int)accumulate,
+                                  p<float>(ws), stream_of(A)),
+     "gnnrec_gemm_tn_bias_rows_f32");
 }
 
 void act_backward(const Tensor& u, const Tensor& gz, int64_t flags, Tensor& out) {
@@ -820,16 +825,20 @@ Tensor gemm_nt(const Tensor& A, const Tensor& W, const Tensor* A2, const Tensor*
   return out;
 }
 
-// guᵀ X, split-K MFMA; colsum (nullable, [M]) receives Σ_k gu[k] from the same pass
-Tensor weight_grad(const Tensor& gu, const Tensor& X, Tensor* colsum = nullptr) {
+// guᵀ X, split-K MFMA; colsum (nullable, [M]) receives Σ_k gu[k] from the same pass — over
+// the rows with row_ptr[k+1] > row_ptr[k] only, when row_ptr is given
+Tensor weight_grad(const Tensor& gu, const Tensor& X, Tensor* colsum = nullptr,
+                   const Tensor* row_ptr = nullptr) {
   const int64_t K = gu.size(0), M = gu.size(1), N = X.size(1);
   Tensor out = at::empty({M, N}, gu.options());
   const int64_t wsb = gnnrec_gemm_tn_workspace_bytes(K, M, N);
   Tensor ws = at::empty({std::max<int64_t>(wsb / 4, 1)}, gu.options());
-  ck(gnnrec_gemm_tn_bias_f32(p<float>(gu), ld(gu, "gu"), p<float>(X), ld(X, "X"), K, M, N,
-                             p<float>(out), ld(out, "out"), colsum ? p<float>(*colsum) : nullptr,
-                             0, p<float>(ws), stream_of(gu)),
-     "gnnrec_gemm_tn_bias_f32");
+  ck(gnnrec_gemm_tn_bias_rows_f32(p<float>(gu), ld(gu, "gu"), p<float>(X), ld(X, "X"), K, M, N,
+                                  p<float>(out), ld(out, "out"),
+                                  colsum ? p<float>(*colsum) : nullptr,
+                                  row_ptr ? p<int64_t>(*row_ptr) : nullptr, 0, p<float>(ws),
+                                  stream_of(gu)),
+     "gnnrec_gemm_tn_bias_rows_f32");
   return out;
 }
 
@@ -1029,8 +1038,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
   } else if (need & 16) {
     g_b = gu.sum(0);
   }
-  if (need & 8) g_Wn = weight_grad(gu, agg.contiguous());
-  if (need & 32) {  // Σ over the rows with an in-edge: the mean of an empty set carries no bias
+  // g_bne: Σ over the rows with an in-edge (the mean of an empty set carries no bias), from
+  // the W_neigh gradient's own pass over gu
+  if (need & 32) g_bne = at::empty({N}, z.options());
+  if (need & 8) {
+    const Tensor ip = indptr.contiguous();
+    g_Wn = weight_grad(gu, agg.contiguous(), (need & 32) ? &g_bne : nullptr,
+                       (need & 32) ? &ip : nullptr);
+  } else if (need & 32) {
     const Tensor ne = (row_degrees(indptr) > 0).to(gu.scalar_type()).unsqueeze(1);
     g_bne = (gu * ne).sum(0);
   }
@@ -1801,8 +1816,9 @@ void gather_rows_batch(at::TensorList src, at::TensorList idx, at::TensorList ou
 // a11: compact_graphs over id lists at static shapes (gnnrec_compact_ids): per node type the
 // sorted distinct ids of its lists in nodes[t] [caps[t]] (-1 past the count), each list
 // relabelled to local ids, the per-type counts left on the device — no host read, so a
-// loader feeding a captured step keeps every shape fixed.  bits [2 ceil(n/64)] and
-// word_rank [ceil(n/64) + 1] per type; bits zero before the first call, parity alternating.
+// loader feeding a captured step keeps every shape fixed.  bits [2 ceil(n/64) +
+// GNNREC_COMPACT_SCAN_WS(n)] and word_rank [ceil(n/64) + 1] per type; the bitmaps zero before
+// the first call, parity alternating.
 std::tuple<std::vector<Tensor>, std::vector<Tensor>, Tensor>
 compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
             at::IntArrayRef caps, at::TensorList bits, at::TensorList word_rank,
@@ -1825,13 +1841,16 @@ compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
     dev(word_rank[t], "word_rank", at::kLong);
     const int64_t W = (n_nodes[t] + 63) / 64;
     dev(marks[t], "marks", at::kByte);
-    TORCH_CHECK_VALUE(n_nodes[t] >= 0 && caps[t] >= 0 && bits[t].numel() == 2 * W &&
+    // bits: the two parity bitmaps, then the scan's workspace
+    const int64_t ws = GNNREC_COMPACT_SCAN_WS(n_nodes[t]);
+    TORCH_CHECK_VALUE(n_nodes[t] >= 0 && caps[t] >= 0 && bits[t].numel() == 2 * W + ws &&
                           word_rank[t].numel() == W + 1 && marks[t].numel() == 2 * 64 * W,
-                      "compact_ids: type ", t,
-                      ": scratch sized 2 ceil(n/64), ceil(n/64)+1, 128 ceil(n/64) bytes");
+                      "compact_ids: type ", t, ": scratch sized 2 ceil(n/64) + ", ws,
+                      ", ceil(n/64)+1, 128 ceil(n/64) bytes");
     nodes[t] = at::empty({caps[t]}, i64);
     T[t] = gnnrec_compact_type{n_nodes[t], p<uint64_t>(bits[t]), p<int64_t>(word_rank[t]),
-                               p<int64_t>(nodes[t]), caps[t], p<uint8_t>(marks[t])};
+                               p<int64_t>(nodes[t]), caps[t], p<uint8_t>(marks[t]),
+                               p<uint64_t>(bits[t]) + 2 * W};
   }
   for (size_t l = 0; l < L; ++l) {
     dev(ids[l], "ids", at::kLong);
@@ -2057,7 +2076,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("topk_rows(Tensor scores, int k, Tensor? exclude_indptr, Tensor? exclude_indices, "
         "Tensor(a!) out_vals, Tensor(b!) out_idx) -> ()");
   m.def("gemm_tn(Tensor A, Tensor B, Tensor(b!)? colsum, bool accumulate, Tensor(a!) out, "
-        "Tensor(c!) workspace) -> ()");
+        "Tensor(c!) workspace, Tensor? row_ptr=None) -> ()");
   m.def("act_backward(Tensor u, Tensor gz, int flags, Tensor(a!) out) -> ()");
   m.def("act_backward_normed(Tensor z, Tensor row_norm, Tensor gz, bool relu, "
         "Tensor(a!) out) -> ()");

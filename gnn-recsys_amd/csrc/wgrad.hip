@@ -74,7 +74,7 @@ template <bool VEC, int T, int KS>
 __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
     const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
     int64_t K, int64_t M, int64_t N, int64_t kchunk, float* __restrict__ part,
-    float* __restrict__ part_b) {
+    float* __restrict__ part_b, const int64_t* __restrict__ row_ptr) {
   constexpr int NT = T / 64, S = T + 4, LI = KS * T / 1024;
   __shared__ float As[2][KS * S];
   __shared__ float Bs[2][KS * S];
@@ -86,8 +86,18 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
   const int64_t kb = split * kchunk, ke = kb + kchunk < K ? kb + kchunk : K;
 
   // part_b: column sums of A over this split (the bias gradient Σ_k dY[k, i]); the blocks
-  // of the first N tile add up the A tiles they already hold in LDS
+  // of the first N tile add up the A tiles they already hold in LDS.  row_ptr (nullable):
+  // only rows k with row_ptr[k+1] > row_ptr[k] count (a folded NodeEmbedding's bias on the
+  // rows with an in-edge): lane r of a summing wave loads step row r's test with the step's
+  // operand prefetch, and a ballot hands the wave the step's row mask
   const bool colsum = part_b != nullptr && blockIdx.z == 0 && threadIdx.x < T;
+  const bool masked = colsum && row_ptr != nullptr;
+  const int mlane = threadIdx.x & 63;
+  auto row_ne = [&](int64_t k0, int64_t ke) {
+    const int64_t k = k0 + mlane;
+    return mlane < KS && k < ke && row_ptr[k + 1] > row_ptr[k];
+  };
+  bool ne_cur = false, ne_next = false;
   float csum = 0.f;
   f32x16 acc[NT][NT];
 #pragma unroll
@@ -101,6 +111,7 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
     float4 ra[LI], rb[LI];
     load_step<VEC, T, KS>(A, lda, M, i_base, kb, ke, ra);
     load_step<VEC, T, KS>(B, ldb, N, j_base, kb, ke, rb);
+    if (masked) ne_cur = row_ne(kb, ke);
     store_step<T, KS>(As[0], ra);
     store_step<T, KS>(Bs[0], rb);
     __syncthreads();
@@ -110,6 +121,7 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
       if (more) {
         load_step<VEC, T, KS>(A, lda, M, i_base, k0 + KS, ke, ra);
         load_step<VEC, T, KS>(B, ldb, N, j_base, k0 + KS, ke, rb);
+        if (masked) ne_next = row_ne(k0 + KS, ke);
       }
       const float* as = As[buf];
       const float* bs = Bs[buf];
@@ -129,9 +141,17 @@ __global__ __launch_bounds__(256) void gemm_tn_partial_kernel(
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
       }
       if (colsum) {
+        if (row_ptr == nullptr) {
 #pragma unroll 16
-        for (int r = 0; r < KS; ++r) csum += as[r * S + threadIdx.x];
+          for (int r = 0; r < KS; ++r) csum += as[r * S + threadIdx.x];
+        } else {  // (rows past the split test false)
+          const unsigned long long mask = __ballot(ne_cur);
+#pragma unroll 16
+          for (int r = 0; r < KS; ++r)
+            if ((mask >> r) & 1ull) csum += as[r * S + threadIdx.x];
+        }
       }
+      ne_cur = ne_next;
       if (more) {
         store_step<T, KS>(As[buf ^ 1], ra);
         store_step<T, KS>(Bs[buf ^ 1], rb);
@@ -292,10 +312,11 @@ extern "C" int64_t gnnrec_gemm_tn_workspace_bytes(int64_t K, int64_t M, int64_t 
   return tn_splits(K, M, N) * (M * N + M) * (int64_t)sizeof(float);
 }
 
-extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
-                                       int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
-                                       float* colsum, int accumulate, float* workspace,
-                                       void* stream) {
+extern "C" int gnnrec_gemm_tn_bias_rows_f32(const float* A, int64_t lda, const float* B,
+                                            int64_t ldb, int64_t K, int64_t M, int64_t N,
+                                            float* C, int64_t ldc, float* colsum,
+                                            const int64_t* row_ptr, int accumulate,
+                                            float* workspace, void* stream) {
   GNNREC_REQUIRE(K >= 0 && M >= 0 && N >= 0, "gnnrec_gemm_tn_f32: negative size");
   GNNREC_REQUIRE(lda >= M && ldb >= N && ldc >= N, "gnnrec_gemm_tn_f32: bad leading dims");
   if (M == 0 || N == 0) return GNNREC_OK;
@@ -319,21 +340,29 @@ extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float*
   if (M <= 64 && N <= 64) {  // one 64 x 64 tile, 64-row steps
     if (vec)
       hipLaunchKernelGGL((gemm_tn_partial_kernel<true, 64, 64>), grid, dim3(256), 0, s, A, lda,
-                         B, ldb, K, M, N, chunk, workspace, part_b);
+                         B, ldb, K, M, N, chunk, workspace, part_b, row_ptr);
     else
       hipLaunchKernelGGL((gemm_tn_partial_kernel<false, 64, 64>), grid, dim3(256), 0, s, A, lda,
-                         B, ldb, K, M, N, chunk, workspace, part_b);
+                         B, ldb, K, M, N, chunk, workspace, part_b, row_ptr);
   } else if (vec) {
     hipLaunchKernelGGL((gemm_tn_partial_kernel<true, kTile, kKStep>), grid, dim3(256), 0, s, A,
-                       lda, B, ldb, K, M, N, chunk, workspace, part_b);
+                       lda, B, ldb, K, M, N, chunk, workspace, part_b, row_ptr);
   } else {
     hipLaunchKernelGGL((gemm_tn_partial_kernel<false, kTile, kKStep>), grid, dim3(256), 0, s, A,
-                       lda, B, ldb, K, M, N, chunk, workspace, part_b);
+                       lda, B, ldb, K, M, N, chunk, workspace, part_b, row_ptr);
   }
   const int64_t nout = M * N + (colsum ? M : 0);
   hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)((nout + 63) / 64)), dim3(256), 0, s,
                      workspace, part_b, splits, M, N, C, ldc, colsum, accumulate);
   return check_launch("gnnrec_gemm_tn_f32");
+}
+
+extern "C" int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
+                                       int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
+                                       float* colsum, int accumulate, float* workspace,
+                                       void* stream) {
+  return gnnrec_gemm_tn_bias_rows_f32(A, lda, B, ldb, K, M, N, C, ldc, colsum, nullptr,
+                                      accumulate, workspace, stream);
 }
 
 extern "C" int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,

@@ -75,6 +75,8 @@ SIGNATURES = {
     "gnnrec_gemm_tn_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _INT, _P, _P]),
     "gnnrec_gemm_tn_bias_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _INT,
                                        _P, _P]),
+    "gnnrec_gemm_tn_bias_rows_f32": (_INT, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P,
+                                            _P, _INT, _P, _P]),
     "gnnrec_lstm_step_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _I64, _P, _P,
                                     _I64, _P]),
     "gnnrec_lstm_step_save_f32": (_INT, [_P, _I64, _P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P,

@@ -348,6 +348,47 @@ class HeteroSageFn(torch.autograd.Function):
         return (None, *g_tab, *g_per)
 
 
+class FoldFn(torch.autograd.Function):
+    """The first-layer fold's weight products for one node type (nn._fold_weights): every
+    weight W_i that the type's NodeEmbedding (W_e, b_e) feeds, stacked as A = [W_1; W_2; ..],
+    -> (W_1 W_e, W_2 W_e, .., W_1 b_e, W_2 b_e, ..), each a contiguous row block of A W_e /
+    A b_e.  As one node its backward is six launches — the two stacked gradients, dA =
+    dWF W_eᵀ + dBF b_eᵀ, dW_e = Aᵀ dWF, db_e = Aᵀ dBF — where the per-slice autograd form
+    (cat, matmul, slices) zero-fills and copies every slice's gradient and adds them
+    (≈15 launches per node type in a captured C2 step)."""
+
+    @staticmethod
+    def forward(ctx, W_e, b_e, *Ws):
+        A = torch.cat(Ws, 0) if len(Ws) > 1 else Ws[0]
+        WF = torch.mm(A, W_e)
+        BF = torch.mv(A, b_e)
+        rows = [W.shape[0] for W in Ws]
+        ctx.save_for_backward(A, W_e, b_e)
+        ctx.rows = rows
+        return (*WF.split(rows), *BF.split(rows))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        A, W_e, b_e = ctx.saved_tensors
+        rows = ctx.rows
+        n = len(rows)
+
+        def stacked(gs, shape):
+            gs = [g if g is not None else A.new_zeros(shape(r)) for g, r in zip(gs, rows)]
+            return torch.cat(gs, 0) if n > 1 else gs[0]
+        dWF = stacked(grads[:n], lambda r: (r, W_e.shape[1]))
+        dBF = stacked(grads[n:], lambda r: (r,))
+        need = ctx.needs_input_grad
+        dW_e = torch.mm(A.t(), dWF) if need[0] else None
+        db_e = torch.mv(A.t(), dBF) if need[1] else None
+        dWs = [None] * n
+        if any(need[2:]):
+            dA = torch.mm(dWF, W_e.t())
+            dA.addr_(dBF, b_e)
+            dWs = list(dA.split(rows))
+        return (dW_e, db_e, *dWs)
+
+
 def sage_rel_fusable(m, h_self, Wn, reduce: str, norm: bool) -> bool:
     """SageRelFn applies: a linear reduce, fp32 row-major tables, the row norm within one
     GEMM block (ops.GEMM_ROW_N)."""

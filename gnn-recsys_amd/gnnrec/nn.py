@@ -421,15 +421,10 @@ def _fold_weights(plan, fold):
     out = [[None] * 4 for _ in plan]
     for nt, lst in uses.items():
         W_e, b_e = fold[nt]
-        A = torch.cat([W for _r, _k, W in lst], 0) if len(lst) > 1 else lst[0][2]
-        WF = torch.matmul(A, W_e)
-        BF = torch.matmul(A, b_e)
-        o = 0
-        for r, k, W in lst:
-            n = W.shape[0]
-            out[r][k] = WF[o:o + n]
-            out[r][2 + k] = BF[o:o + n]
-            o += n
+        prods = ag.FoldFn.apply(W_e, b_e, *[W for _r, _k, W in lst])
+        for i, (r, k, _W) in enumerate(lst):
+            out[r][k] = prods[i]
+            out[r][2 + k] = prods[len(lst) + i]
     return out
 
 
@@ -545,6 +540,12 @@ class CosinePrediction(nn.Module):
                 pos[etype] = self.forward_one(h, etype, ps, pd)
                 continue
             ns, nd = neg_g.all_edges(etype=etype)
+            if ps.numel() == 0 and ns.numel() == 0:
+                # an etype the batch has no pairs of: empty scores, no launches, and no
+                # zero gradient for autograd to add into the endpoint tables
+                pos[etype] = h[etype[0]].new_zeros((0, 1))
+                neg[etype] = h[etype[0]].new_zeros((0, 1))
+                continue
             # negative_sampler.Uniform's pairs (the loader marks them): every positive's
             # source repeated K times -> the grouped launch, one gathered row per edge
             K = getattr(neg_g, 'src_repeats_pos', None)

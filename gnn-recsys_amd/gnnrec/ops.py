@@ -812,11 +812,13 @@ def preproject(X: torch.Tensor, W_neigh: torch.Tensor,
 
 
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None,
-            accumulate: bool = False, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+            accumulate: bool = False, colsum: Optional[torch.Tensor] = None,
+            row_ptr: Optional[torch.Tensor] = None) -> torch.Tensor:
     """f2 weight gradient: out [M,N] (+)= Aᵀ B for A [K,M], B [K,N] (dW = dYᵀ X); with
-    colsum [M], also colsum (+)= Σ_k A[k] (the bias gradient) from the same pass.
+    colsum [M], also colsum (+)= Σ_k A[k] (the bias gradient) from the same pass — over the
+    rows k with row_ptr[k+1] > row_ptr[k] only when row_ptr (an int64 [K+1] indptr) is given.
 
-    Deterministic split-K MFMA (gnnrec_gemm_tn_bias_f32)."""
+    Deterministic split-K MFMA (gnnrec_gemm_tn_bias_rows_f32)."""
     T = _T()
     _dev(A, "A", torch.float32)
     _dev(B, "B", torch.float32)
@@ -841,7 +843,12 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None
     _rowmajor(out, "out")
     nbytes = T.gemm_tn_workspace_bytes(K, M, N)
     ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=A.device)
-    T.gemm_tn(A, B, colsum, bool(accumulate), out, ws)
+    if row_ptr is not None:
+        _dev(row_ptr, "row_ptr", torch.int64)
+        if colsum is None or row_ptr.numel() != K + 1:
+            raise ValueError(f"row_ptr must be a [{K + 1}] indptr beside colsum")
+        row_ptr = row_ptr.contiguous()
+    T.gemm_tn(A, B, colsum, bool(accumulate), out, ws, row_ptr)
     return out
 
 
@@ -1101,7 +1108,11 @@ def margin_loss(parts, delta: float):
     [(g_pos, g_neg)]).  Gradients are d(sum of scores)/d(score); the loss is the mean."""
     T = _T()
     dev = parts[0][0].device
-    blocks = [int(T.margin_loss_blocks(p[0].numel())) for p in parts]
+    # an etype without positive edges (the pair graphs' other etypes) adds nothing: no
+    # launch and no partial for it, unless every etype is empty (the NaN mean below)
+    skip = any(p[0].numel() for p in parts)
+    blocks = [0 if skip and p[0].numel() == 0 else int(T.margin_loss_blocks(p[0].numel()))
+              for p in parts]
     partial = torch.empty(sum(blocks), dtype=torch.float32, device=dev)
     grads, off, total = [], 0, 0
     for (pos, neg, K, mask, rec), nb in zip(parts, blocks):
@@ -1123,6 +1134,9 @@ def margin_loss(parts, delta: float):
                 raise ValueError("recency must have one value per positive edge")
         g_pos = torch.empty_like(pos)
         g_neg = torch.empty_like(neg)
+        if nb == 0:
+            grads.append((g_pos, g_neg))
+            continue
         T.margin_loss(pos.contiguous(), neg.contiguous(), K, float(delta), mask, rec, g_pos,
                       g_neg, partial[off:off + nb])
         grads.append((g_pos, g_neg))
@@ -1305,7 +1319,8 @@ class CompactScratch:
     def __init__(self, n_nodes: int, device):
         w = (n_nodes + 63) // 64
         self.n_nodes = n_nodes
-        self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
+        # the two bitmaps, then the scan's ticket and tile flags (GNNREC_COMPACT_SCAN_WS)
+        self.bits = torch.zeros(2 * w + 2 + w // 1024, dtype=torch.int64, device=device)
         self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
         self.marks = torch.zeros(2 * 64 * w, dtype=torch.uint8, device=device)
         self.parity = 0

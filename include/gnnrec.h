@@ -482,8 +482,8 @@ int gnnrec_sample_blocks(const gnnrec_sample_plan* plan, void* stream);
  * type the ids of its lists form one ascending node list, padded with -1 to `cap` (the
  * caller's bound on the distinct ids: past it ids are left out of the list and their local ids
  * point past cap, so the caller must rule that out), and every list
- * element gets its position in that list.  3 launches (mark bits, scan popcounts, relabel +
- * list), no host synchronisation; `bits` (uint64 [2 * ceil(n_nodes/64)], zero before the
+ * element gets its position in that list.  3 launches (mark bits, a chained scan of the
+ * popcounts, relabel + list), no host synchronisation; `bits` (uint64 [2 * ceil(n_nodes/64)], zero before the
  * first call) and `word_rank` (int64 [ceil(n_nodes/64) + 1]) are the caller's scratch, and
  * `parity` alternates 0 / 1 between calls on the same scratch.  count [n_types] (device)
  * receives each type's number of distinct ids.  The lists' order does not matter: the node
@@ -503,7 +503,10 @@ typedef struct gnnrec_compact_type {
   int64_t cap;
   uint8_t* marks;     /* [2 * 64 * ceil(n_nodes/64)] bytes, zero before the first call,
                        * 16-byte aligned, parity halves like `bits` */
+  uint64_t* scan_ws;  /* [GNNREC_COMPACT_SCAN_WS(n_nodes)] words, any contents (the call
+                       * zeroes them): the scan's ticket and tile flags */
 } gnnrec_compact_type;
+#define GNNREC_COMPACT_SCAN_WS(n_nodes) (2 + ((n_nodes) + 63) / 64 / 1024)
 int gnnrec_compact_ids(const gnnrec_compact_list* lists, int n_lists,
                        const gnnrec_compact_type* types, int n_types, int parity, int64_t* count,
                        void* stream);
@@ -538,6 +541,14 @@ int gnnrec_gemm_tn_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
 int gnnrec_gemm_tn_bias_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t K,
                             int64_t M, int64_t N, float* C, int64_t ldc, float* colsum,
                             int accumulate, float* workspace, void* stream);
+/* Same, the column sum over only the rows k with row_ptr[k+1] > row_ptr[k] (row_ptr: the
+ * int64 indptr of a CSR over A's K rows; NULL = every row): a NodeEmbedding folded into the
+ * neighbour side adds its bias on rows with an in-edge only, so that bias's gradient sums
+ * those rows (torch_ops sage_rel_backward; replaces (dY * (deg > 0)).sum(0)). */
+int gnnrec_gemm_tn_bias_rows_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
+                                 int64_t K, int64_t M, int64_t N, float* C, int64_t ldc,
+                                 float* colsum, const int64_t* row_ptr, int accumulate,
+                                 float* workspace, void* stream);
 /* gu = d/du of z = norm?(relu?(u)) applied to gz, flags = GNNREC_EPI_RELU|GNNREC_EPI_L2NORM
  * (norm: z = a / ||a||, rows with ||a|| == 0 unchanged — the zero-guarded norm of
  * src/model.py:231-235).  u: the pre-activation rows [n_rows, d]. */

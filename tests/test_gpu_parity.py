@@ -500,6 +500,16 @@ def test_gemm_tn_matches_fp64(K, M, N):
     ops.gemm_tn(A, B, out=out2, accumulate=True, colsum=cs)
     np.testing.assert_allclose(cs.cpu().numpy(), (2 * cs0.double()).cpu().numpy(), rtol=1e-5,
                                atol=tol)
+    # the column sum over the rows with an in-edge only (a folded NodeEmbedding's bias):
+    # a CSR over A's rows with about a third of them empty
+    deg = torch.randint(0, 3, (K,), device="cuda", generator=gen)
+    row_ptr = torch.zeros(K + 1, dtype=torch.int64, device="cuda")
+    row_ptr[1:] = torch.cumsum(deg, 0)
+    csm = torch.empty(M, device="cuda")
+    out3 = ops.gemm_tn(A, B, colsum=csm, row_ptr=row_ptr)
+    assert torch.equal(out3, out)
+    ref_m = (A.double() * (deg > 0).double().unsqueeze(1)).sum(0)
+    np.testing.assert_allclose(csm.cpu().numpy(), ref_m.cpu().numpy(), rtol=1e-4, atol=tol)
 
 
 @pytest.mark.parametrize("relu,l2", [(True, False), (False, True), (True, True)])

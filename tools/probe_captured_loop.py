@@ -1,9 +1,8 @@
-"""The captured C2 training step's graph alone: after a few batches through
-CapturedTrainStep, replay the graph N times with nothing else on the GPU, so that a
-`rocprofv3 --kernel-trace --stats` of this script is the replay's own kernel budget
-(totals / N per step).
+"""The captured C2 training loop (bench.captured_step's loop: EdgeDataLoader(static_shapes,
+num_workers=2) -> CapturedTrainStep), its timed steps bracketed by torch.cuda._sleep marker
+kernels, for a kernel trace whose steady state tools/rocpd_timeline.py measures.
 
-    python tools/probe_replay.py [K] [N]
+    python tools/probe_captured_loop.py [K] [steps] [switch_interval_s]
 """
 import json
 import os
@@ -21,7 +20,9 @@ def main():
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
     from gnnrec.synth import minibatch_graph
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    N = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+    if len(sys.argv) > 3:  # the interpreter's thread switch interval (s), an A/B knob
+        sys.setswitchinterval(float(sys.argv[3]))
     dev = torch.device("cuda")
     g = minibatch_graph(64, dev)
     buys = ("user", "buys", "item")
@@ -36,26 +37,28 @@ def main():
         _, ps, ns = m(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
         return gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
 
+    step = CapturedTrainStep(model, opt, loss_fn, warmup=2)
     el = EdgeDataLoader(g, {buys: torch.arange(g.num_edges(buys))},
                         MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                         reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
-                        shuffle=True, static_shapes=True)
+                        shuffle=True, num_workers=2, static_shapes=True)
     el.sampler.first_transposes_below = 0
-    step = CapturedTrainStep(model, opt, loss_fn, warmup=2)
     it = iter(el)
     for _ in range(5):
         step(next(it))
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(N):
-        step.graph.replay()
-    host = time.perf_counter() - t
+    torch.cuda._sleep(1000)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step(next(it))
+    torch.cuda._sleep(1000)
     torch.cuda.synchronize()
-    # host time of the replay calls alone (a launch that waits for the previous replay shows
-    # here as the GPU time per replay)
-    print(json.dumps({"K": K, "replays": N, "ms_per_replay": (time.perf_counter() - t) / N * 1e3,
-                      "host_ms_per_replay_call": host / N * 1e3}))
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    print(json.dumps({"K": K, "steps": steps, "ms_per_step": round(ms, 4),
+                      "switch_interval": sys.getswitchinterval(),
+                      "replays": step.replays, "loss": float(loss)}))
+    del it, el
 
 
 if __name__ == "__main__":
