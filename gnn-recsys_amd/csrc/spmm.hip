@@ -150,7 +150,23 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
     float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq,
-    int rq_ch, int64_t group_deg) {
+    int rq_ch, int64_t group_deg, const int64_t* __restrict__ live) {
+  if (live != nullptr) {
+    // rows from the device count on (a static block's padding and dump rows): the empty
+    // row's value (0: sum / mean), no gathers; left as they are under ACCUM (+= 0)
+    const int64_t l = *live;
+    const int64_t n_rows = l < 0 ? 0 : (l < n_dst ? l : n_dst);
+    if (!(flags & GNNREC_SPMM_ACCUM) && blockIdx.y == 0) {
+      const int64_t nw = (int64_t)gridDim.x * 4;
+      for (int64_t r = n_rows + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_dst; r += nw)
+        for (int c = threadIdx.x & 63; c < d; c += 64) out[r * ldo + c] = 0.f;
+    }
+    n_dst = n_rows;
+    if (n_dst == 0) {
+      if (rq != nullptr) rq_finish(rq);
+      return;
+    }
+  }
   if constexpr (VEC == 4 && (LPR == 8 || LPR == 16)) {  // d in (16, 64]; at LPR 4 the 16
                                                         // partials cost occupancy
     // low mean degree: one lane group per row (the choice needs the CSR's edge count,
@@ -312,6 +328,7 @@ struct SpmmArgs {
   const int64_t* chunk_row; int64_t n_chunks; float* ws;
   const int64_t* counts;  // device-built plan: {n_heavy, n_chunks}; n_heavy/n_chunks above
                           // are then the plan's capacities (grid sizes)
+  const int64_t* live;    // device row count (nullable): rows from it on are empty rows
 };
 
 // Resident 256-thread blocks per CU the row kernels occupy (grid-stride beyond): every wave
@@ -344,7 +361,7 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
                      a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, kRowChunk,
-                     kGroupMaxAvgDeg);
+                     kGroupMaxAvgDeg, a.live);
   rowq_launched(ticket, s);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
@@ -489,6 +506,8 @@ int spmm_entry(SpmmArgs a, int64_t d, int reduce, void* stream) {
   GNNREC_REQUIRE(a.n_heavy == 0 || (a.split > 0 && a.heavy_rows && a.chunk_ptr && a.chunk_row &&
                                     a.ws && a.n_chunks > 0),
                  "gnnrec_spmm_csr_split_f32: incomplete heavy-row plan");
+  GNNREC_REQUIRE(a.live == nullptr || reduce != GNNREC_REDUCE_MAX,
+                 "gnnrec_spmm_csr_live_f32: a device row count needs sum or mean");
   a.d = (int)d;
   const bool vec4 = (d % 4 == 0) && (a.ldx % 4 == 0) && (a.ldo % 4 == 0) && aligned16(a.X) &&
                     aligned16(a.out) && (a.n_heavy == 0 || aligned16(a.ws));
@@ -509,7 +528,17 @@ extern "C" int gnnrec_spmm_csr_f32(const int64_t* indptr, const int32_t* indices
                                    const float* X, int64_t ldx, int64_t n_dst, int64_t d,
                                    int reduce, int flags, float* out, int64_t ldo, void* stream) {
   gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
-                     0, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr};
+                     0, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
+  return gnnrec::spmm_entry(a, d, reduce, stream);
+}
+
+extern "C" int gnnrec_spmm_csr_live_f32(const int64_t* indptr, const int32_t* indices,
+                                        const float* ew, const float* X, int64_t ldx,
+                                        int64_t n_dst, int64_t d, int reduce, int flags,
+                                        float* out, int64_t ldo, const int64_t* live,
+                                        void* stream) {
+  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
+                     0, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, live};
   return gnnrec::spmm_entry(a, d, reduce, stream);
 }
 
@@ -522,7 +551,7 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* i
                                          int64_t n_chunks, float* workspace, void* stream) {
   gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
                      split, heavy_rows, n_heavy, chunk_ptr, chunk_row, n_chunks, workspace,
-                     nullptr};
+                     nullptr, nullptr};
   return gnnrec::spmm_entry(a, d, reduce, stream);
 }
 
@@ -539,7 +568,12 @@ __global__ __launch_bounds__(256) void plan_mark_kernel(const int64_t* __restric
                                                         int64_t n_dst, int64_t split,
                                                         int64_t cap_h,
                                                         unsigned long long* __restrict__ counts,
-                                                        int64_t* __restrict__ heavy_rows) {
+                                                        int64_t* __restrict__ heavy_rows,
+                                                        const int64_t* __restrict__ live) {
+  if (live != nullptr) {  // rows past the device count are empty rows, never heavy
+    const int64_t l = *live;
+    n_dst = l < 0 ? 0 : (l < n_dst ? l : n_dst);
+  }
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n_dst; v += stride) {
     if (indptr[v + 1] - indptr[v] > split) {
@@ -604,8 +638,9 @@ __global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __rest
 }  // namespace
 }  // namespace gnnrec
 
-extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split,
-                                      int64_t cap_h, int64_t cap_c, int64_t* plan, void* stream) {
+extern "C" int gnnrec_spmm_plan_build_live(const int64_t* indptr, int64_t n_dst, int64_t split,
+                                           int64_t cap_h, int64_t cap_c, int64_t* plan,
+                                           const int64_t* live, void* stream) {
   using namespace gnnrec;
   GNNREC_REQUIRE(n_dst >= 0 && split > 0 && cap_h >= 0 && cap_c >= 0,
                  "gnnrec_spmm_plan_build: bad sizes");
@@ -616,11 +651,30 @@ extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int6
     int64_t blocks = (n_dst + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(plan_mark_kernel, dim3((unsigned)blocks), dim3(256), 0, s, indptr, n_dst,
-                       split, cap_h, reinterpret_cast<unsigned long long*>(plan), plan + 2);
+                       split, cap_h, reinterpret_cast<unsigned long long*>(plan), plan + 2, live);
     hipLaunchKernelGGL(plan_chunks_kernel, dim3(1), dim3(1024), 0, s, indptr, split, plan, cap_h,
                        cap_c);
   }
   return check_launch("gnnrec_spmm_plan_build");
+}
+
+extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split,
+                                      int64_t cap_h, int64_t cap_c, int64_t* plan, void* stream) {
+  return gnnrec_spmm_plan_build_live(indptr, n_dst, split, cap_h, cap_c, plan, nullptr, stream);
+}
+
+extern "C" int gnnrec_spmm_csr_planned_live_f32(const int64_t* indptr, const int32_t* indices,
+                                                const float* ew, const float* X, int64_t ldx,
+                                                int64_t n_dst, int64_t d, int reduce, int flags,
+                                                float* out, int64_t ldo, int64_t split,
+                                                const int64_t* plan, int64_t cap_h,
+                                                int64_t cap_c, float* workspace,
+                                                const int64_t* live, void* stream) {
+  GNNREC_REQUIRE(plan && cap_h > 0 && cap_c > 0, "gnnrec_spmm_csr_planned_f32: empty plan");
+  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
+                     split, plan + 2, cap_h, plan + 2 + cap_h, plan + 3 + 2 * cap_h, cap_c,
+                     workspace, plan, live};
+  return gnnrec::spmm_entry(a, d, reduce, stream);
 }
 
 extern "C" int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices,
@@ -629,11 +683,9 @@ extern "C" int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t*
                                            float* out, int64_t ldo, int64_t split,
                                            const int64_t* plan, int64_t cap_h, int64_t cap_c,
                                            float* workspace, void* stream) {
-  GNNREC_REQUIRE(plan && cap_h > 0 && cap_c > 0, "gnnrec_spmm_csr_planned_f32: empty plan");
-  gnnrec::SpmmArgs a{indptr, indices, ew, X, ldx, n_dst, 0, out, ldo, flags,
-                     split, plan + 2, cap_h, plan + 2 + cap_h, plan + 3 + 2 * cap_h, cap_c,
-                     workspace, plan};
-  return gnnrec::spmm_entry(a, d, reduce, stream);
+  return gnnrec_spmm_csr_planned_live_f32(indptr, indices, ew, X, ldx, n_dst, d, reduce, flags,
+                                          out, ldo, split, plan, cap_h, cap_c, workspace,
+                                          nullptr, stream);
 }
 
 // ---------------------------------------------------------------- backward --

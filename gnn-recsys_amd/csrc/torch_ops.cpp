@@ -90,8 +90,17 @@ int64_t ld(const Tensor& t, const char* name) {
 bool meta(const Tensor& t) { return t.is_meta(); }
 
 // ---------------------------------------------------------------- a1 aggregation
+// live (nullable, one device int64): rows from it on are empty rows (gnnrec_spmm_csr_live_f32)
+const int64_t* live_ptr(const optional<Tensor>& live) {
+  if (!has(live)) return nullptr;
+  dev(live, "live", at::kLong);
+  TORCH_CHECK_VALUE(live->numel() == 1, "live must hold one row count");
+  return p<int64_t>(live);
+}
+
 void spmm_csr(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
-              const Tensor& X, int64_t reduce, int64_t flags, Tensor& out) {
+              const Tensor& X, int64_t reduce, int64_t flags, Tensor& out,
+              const optional<Tensor>& live) {
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
@@ -104,8 +113,9 @@ void spmm_csr(const Tensor& indptr, const Tensor& indices, const optional<Tensor
   const int64_t ldx = ld(X, "X"), ldo = ld(out, "out");
   if (meta(X)) return;
   const c10::DeviceGuard g(X.device());
-  ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew), p<float>(X), ldx,
-                         n_dst, d, (int)reduce, (int)flags, p<float>(out), ldo, stream_of(X)),
+  ck(gnnrec_spmm_csr_live_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew), p<float>(X),
+                              ldx, n_dst, d, (int)reduce, (int)flags, p<float>(out), ldo,
+                              live_ptr(live), stream_of(X)),
      "gnnrec_spmm_csr_f32");
 }
 
@@ -164,7 +174,8 @@ void spmm_csr2(const Tensor& indptr_a, const Tensor& indices_a, const optional<T
      "gnnrec_spmm_csr2_f32");
 }
 
-void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor& plan) {
+void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor& plan,
+                     const optional<Tensor>& live) {
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(plan, "plan", at::kLong);
@@ -172,14 +183,15 @@ void spmm_plan_build(const Tensor& indptr, int64_t split, int64_t cap_h, Tensor&
   TORCH_CHECK_VALUE(cap_h >= 0 && cap_c >= 0, "spmm_plan_build: plan shorter than 3 + 2 cap_h");
   if (meta(indptr)) return;
   const c10::DeviceGuard g(indptr.device());
-  ck(gnnrec_spmm_plan_build(p<int64_t>(indptr), indptr.numel() - 1, split, cap_h, cap_c,
-                            p<int64_t>(plan), stream_of(indptr)),
+  ck(gnnrec_spmm_plan_build_live(p<int64_t>(indptr), indptr.numel() - 1, split, cap_h, cap_c,
+                                 p<int64_t>(plan), live_ptr(live), stream_of(indptr)),
      "gnnrec_spmm_plan_build");
 }
 
 void spmm_csr_planned(const Tensor& indptr, const Tensor& indices, const optional<Tensor>& ew,
                       const Tensor& X, int64_t reduce, int64_t flags, int64_t split,
-                      const Tensor& plan, int64_t cap_h, int64_t cap_c, Tensor& out, Tensor& ws) {
+                      const Tensor& plan, int64_t cap_h, int64_t cap_c, Tensor& out, Tensor& ws,
+                      const optional<Tensor>& live) {
   const OneDevice one_device_;
   dev(indptr, "indptr", at::kLong);
   dev(indices, "indices", at::kInt);
@@ -194,10 +206,10 @@ void spmm_csr_planned(const Tensor& indptr, const Tensor& indices, const optiona
   const int64_t ldx = ld(X, "X"), ldo = ld(out, "out");
   if (meta(X)) return;
   const c10::DeviceGuard g(X.device());
-  ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew),
-                                 p<float>(X), ldx, n_dst, d, (int)reduce, (int)flags,
-                                 p<float>(out), ldo, split, p<int64_t>(plan), cap_h, cap_c,
-                                 p<float>(ws), stream_of(X)),
+  ck(gnnrec_spmm_csr_planned_live_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ew),
+                                      p<float>(X), ldx, n_dst, d, (int)reduce, (int)flags,
+                                      p<float>(out), ldo, split, p<int64_t>(plan), cap_h, cap_c,
+                                      p<float>(ws), live_ptr(live), stream_of(X)),
      "gnnrec_spmm_csr_planned_f32");
 }
 
@@ -853,26 +865,27 @@ Tensor row_degrees(const Tensor& indptr) {
 // device, as ops.spmm does
 void gather_planned(const Tensor& ip, const Tensor& ix, const Tensor& w, const Tensor& X,
                     int64_t nnz, Tensor& out, bool accumulate = false,
-                    int reduce = GNNREC_REDUCE_SUM) {
+                    int reduce = GNNREC_REDUCE_SUM, const int64_t* live = nullptr) {
   const int64_t n = ip.numel() - 1, d = X.size(1);
   const int64_t cap_h = std::min<int64_t>(n, nnz / (kSplit + 1));
   void* s = stream_of(X);
   const int flags = accumulate ? GNNREC_SPMM_ACCUM : 0;
   if (cap_h <= 0) {
-    ck(gnnrec_spmm_csr_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X), ld(X, "X"), n, d,
-                           reduce, flags, p<float>(out), ld(out, "out"), s),
+    ck(gnnrec_spmm_csr_live_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X), ld(X, "X"), n,
+                                d, reduce, flags, p<float>(out), ld(out, "out"), live, s),
        "gnnrec_spmm_csr_f32");
     return;
   }
   const int64_t cap_c = nnz / kSplit + cap_h;
   Tensor plan = at::empty({2 + cap_h + cap_h + 1 + cap_c}, ip.options());
-  ck(gnnrec_spmm_plan_build(p<int64_t>(ip), n, kSplit, cap_h, cap_c, p<int64_t>(plan), s),
+  ck(gnnrec_spmm_plan_build_live(p<int64_t>(ip), n, kSplit, cap_h, cap_c, p<int64_t>(plan), live,
+                                 s),
      "gnnrec_spmm_plan_build");
   Tensor wsp = at::empty({cap_c, d}, X.options());
-  ck(gnnrec_spmm_csr_planned_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),
-                                 ld(X, "X"), n, d, reduce, flags, p<float>(out),
-                                 ld(out, "out"), kSplit, p<int64_t>(plan), cap_h, cap_c,
-                                 p<float>(wsp), s),
+  ck(gnnrec_spmm_csr_planned_live_f32(p<int64_t>(ip), p<int32_t>(ix), pw(w), p<float>(X),
+                                      ld(X, "X"), n, d, reduce, flags, p<float>(out),
+                                      ld(out, "out"), kSplit, p<int64_t>(plan), cap_h, cap_c,
+                                      p<float>(wsp), live, s),
      "gnnrec_spmm_csr_planned_f32");
 }
 }  // namespace
@@ -884,7 +897,8 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                                                     const optional<Tensor>& ew, int64_t reduce,
                                                     bool norm, const optional<Tensor>& bias,
                                                     const optional<Tensor>& bias_ne,
-                                                    int64_t heavy_nnz) {
+                                                    int64_t heavy_nnz,
+                                                    const optional<Tensor>& live) {
   const OneDevice one_device_;
   dev(m, "m", at::kFloat);
   dev(h_self, "h_self", at::kFloat);
@@ -917,14 +931,17 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
   Tensor nrm = norm ? at::empty({M}, m.options()) : at::empty({0}, m.options());
   if (meta(m)) return {z, agg, nrm};
   const c10::DeviceGuard g(m.device());
+  // live: the static block's real destination count on the device (its padding and dump
+  // rows aggregate nothing: their outputs feed no real row and get no gradient)
+  const int64_t* lv = live_ptr(live);
   if (heavy_nnz > 0) {  // rows of any length (a static block's dump row): planned on the device
     TORCH_CHECK_VALUE(indices.numel() >= heavy_nnz, "sage_rel_forward: heavy_nnz > edges");
     const Tensor w = has(ewc) ? *ewc : Tensor();
-    gather_planned(indptr, indices, w, X, heavy_nnz, agg, false, (int)reduce);
+    gather_planned(indptr, indices, w, X, heavy_nnz, agg, false, (int)reduce, lv);
   } else {
-    ck(gnnrec_spmm_csr_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc), p<float>(X),
-                           ld(X, "m"), M, X.size(1), (int)reduce, 0, p<float>(agg),
-                           ld(agg, "agg"), stream_of(m)),
+    ck(gnnrec_spmm_csr_live_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc),
+                                p<float>(X), ld(X, "m"), M, X.size(1), (int)reduce, 0,
+                                p<float>(agg), ld(agg, "agg"), lv, stream_of(m)),
        "gnnrec_spmm_csr_f32");
   }
   const Tensor deg = bnc.defined() ? row_degrees(indptr) : Tensor();
@@ -941,7 +958,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
     int64_t nnz, bool norm, int64_t need, const optional<Tensor>& indptr_t_in,
     const optional<Tensor>& indices_t_in, const optional<Tensor>& w_mean_in,
     const optional<Tensor>& g_self_out, bool g_self_acc, const optional<Tensor>& g_m_out,
-    bool g_m_acc) {
+    bool g_m_acc, const optional<Tensor>& live_src) {
   // need bits: 1 g_self, 2 g_m, 4 g_Ws, 8 g_Wn, 16 g_bias (Σ rows of the pre-activation
   // gradient), 32 g_bias_nonempty (the same over rows with an in-edge)
   const OneDevice one_device_;
@@ -1030,7 +1047,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> sage_rel_backward(
          "gnnrec_csr_transpose");
     }
     g_m = has(g_m_out) ? *g_m_out : at::empty({n_src, Wn.size(1)}, z.options());
-    gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m, has(g_m_out) && g_m_acc);
+    // live_src: the static block's real source count (its padding sources' gradient rows
+    // are zero: only padding rows, whose gradient is zero, point at them)
+    gather_planned(ip_t, ix_t, w_t, g_agg, nnz, g_m, has(g_m_out) && g_m_acc, GNNREC_REDUCE_SUM,
+                   live_ptr(live_src));
   }
   if (need & 16) g_b = at::empty({N}, z.options());
   if (need & 4) {
@@ -2021,17 +2041,18 @@ int64_t margin_loss_blocks(int64_t n_pos) { return gnnrec_margin_loss_blocks(n_p
 // writes; every launch op returns ().
 TORCH_LIBRARY(gnnrec, m) {
   m.def("spmm_csr(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, int reduce, "
-        "int flags, Tensor(a!) out) -> ()");
+        "int flags, Tensor(a!) out, Tensor? live=None) -> ()");
   m.def("spmm_csr_split(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, "
         "int reduce, int flags, int split, Tensor heavy_rows, Tensor chunk_ptr, "
         "Tensor chunk_row, int n_chunks, Tensor(a!) out, Tensor(b!) workspace) -> ()");
-  m.def("spmm_plan_build(Tensor indptr, int split, int cap_h, Tensor(a!) plan) -> ()");
+  m.def("spmm_plan_build(Tensor indptr, int split, int cap_h, Tensor(a!) plan, "
+        "Tensor? live=None) -> ()");
   m.def("spmm_csr2(Tensor indptr_a, Tensor indices_a, Tensor? ew_a, Tensor indptr_b, "
         "Tensor indices_b, Tensor? ew_b, Tensor X, int reduce, int flags, Tensor(a!) out_a, "
         "Tensor(b!) out_b) -> ()");
   m.def("spmm_csr_planned(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor X, "
         "int reduce, int flags, int split, Tensor plan, int cap_h, int cap_c, Tensor(a!) out, "
-        "Tensor(b!) workspace) -> ()");
+        "Tensor(b!) workspace, Tensor? live=None) -> ()");
   m.def("spmm_backward(Tensor indptr, Tensor indices, Tensor? edge_weight, Tensor grad_out, "
         "Tensor? X, Tensor? out, int reduce, Tensor(a!) grad_X) -> ()");
   m.def("gemm(Tensor A1, Tensor W1, Tensor? A2, Tensor? W2, Tensor? a2_deg, int a2_mode, "
@@ -2104,13 +2125,14 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor(a!) out) -> ()");
   m.def("sage_rel_forward(Tensor m, Tensor h_self, int n_self, Tensor W_self, Tensor W_neigh, "
         "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm, "
-        "Tensor? bias=None, Tensor? bias_nonempty=None, int heavy_nnz=0) -> (Tensor, Tensor, Tensor)");
+        "Tensor? bias=None, Tensor? bias_nonempty=None, int heavy_nnz=0, Tensor? live=None) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
         "int reduce, int n_src, int nnz, bool norm, int need, Tensor? indptr_t=None, "
         "Tensor? indices_t=None, Tensor? w_mean=None, Tensor(a!)? g_self_out=None, "
-        "bool g_self_acc=False, Tensor(b!)? g_m_out=None, bool g_m_acc=False) "
-        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "bool g_self_acc=False, Tensor(b!)? g_m_out=None, bool g_m_acc=False, "
+        "Tensor? live_src=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("block_transposes(Tensor[] indptrs, Tensor[] indices, int[] n_src, int[] nnz) "
         "-> (Tensor[], Tensor[], Tensor[])");
   m.def("edge_batch_pairs(Tensor[] rel_src, Tensor[] rel_dst, int[] src_type, int[] dst_type, "

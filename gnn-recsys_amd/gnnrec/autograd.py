@@ -177,6 +177,12 @@ class SageProjectFn(torch.autograd.Function):
         return g_self, g_agg, g_Ws, g_Wn, None, None
 
 
+def _live(indptr):
+    """A static-shape block's real row count on the device (sampling, static_shapes=True),
+    or None: the gathers over its CSR treat the rows past it as empty."""
+    return getattr(indptr, "_gnnrec_live", None)
+
+
 def _heavy_nnz(indptr) -> int:
     """A static-shape block's CSR (sampling, static_shapes=True) may hold rows of any length
     (the dump row): its edge count, so the forward gather plans heavy rows on the device;
@@ -199,7 +205,8 @@ class SageRelFn(torch.autograd.Function):
                 n_self: int = 0, transposed=None):
         z, agg, nrm = ops._T().sage_rel_forward(m, h_self, n_self, Ws.detach(), Wn.detach(),
                                                 indptr, indices, ew, ops.REDUCE[reduce],
-                                                bool(norm), None, None, _heavy_nnz(indptr))
+                                                bool(norm), None, None, _heavy_nnz(indptr),
+                                                _live(indptr))
         ctx.save_for_backward(h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew)
         ctx.reduce, ctx.norm, ctx.n_src = reduce, bool(norm), m.shape[0]
         ctx.nnz = ops._nnz(indptr)  # sampled blocks carry it: no readback
@@ -216,7 +223,8 @@ class SageRelFn(torch.autograd.Function):
         tr = ctx.transposed or (None, None, None)
         g_self, g_m, g_Ws, g_Wn, _gb, _gbne = ops._T().sage_rel_backward(
             gz, z, nrm, h_self, agg, Ws.detach(), Wn.detach(), indptr, indices, ew,
-            ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask, *tr)
+            ops.REDUCE[ctx.reduce], ctx.n_src, ctx.nnz, ctx.norm, mask, *tr,
+            live_src=_live(tr[0]) if tr[0] is not None else None)
         return (g_m if need[0] else None, g_self if need[1] else None,
                 g_Ws if need[2] else None, g_Wn if need[3] else None,
                 None, None, None, None, None, None, None)
@@ -261,7 +269,7 @@ class HeteroSageFn(torch.autograd.Function):
             z, agg, nrm = T.sage_rel_forward(
                 m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip, ix, ew, ops.REDUCE[reduce],
                 bool(norm), None if b is None else b.detach(),
-                None if bne is None else bne.detach(), _heavy_nnz(ip))
+                None if bne is None else bne.detach(), _heavy_nnz(ip), _live(ip))
             zs.append(z)
             saved += [agg, z, nrm]
         outs = []
@@ -322,6 +330,8 @@ class HeteroSageFn(torch.autograd.Function):
                                                 dtype=torch.float32, device=g.device)
                     kw.update(g_m_out=g_tab[si], g_m_acc=acc)
                 t3 = tr if (tr is not None and ew is None) else (None, None, None)
+                if t3[0] is not None:
+                    kw.update(live_src=_live(t3[0]))
                 _gs, g_m, g_Ws, g_Wn, g_b, g_bne = T.sage_rel_backward(
                     g, z, nrm, tables[di], agg, Ws.detach(), Wn.detach(), ip, ix, ew,
                     ops.REDUCE[reduce], ctx.n_src[r], ctx.nnz[r], bool(norm), mask, *t3, **kw)

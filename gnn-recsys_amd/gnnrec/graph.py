@@ -346,6 +346,8 @@ class Block:
         self._dst = {nt: _FrameDict({NID: src_nid[nt][: num_dst[nt]]}) for nt in self.ntypes}
         self._edata = {ce: _FrameDict({EID: rels[ce][2]}) for ce in self.canonical_etypes}
         self._t = {}  # ce -> source-major CSR of the relation (sampler, training loaders)
+        # static blocks: ('dst' | 'src', ntype) -> the real row count on the device (int64 [1])
+        self._live = {}
 
     @property
     def srcdata(self):

@@ -160,11 +160,15 @@ class BlockSampler:
                 for ce in ces for k, v in g._edata[ce].items()]
         ntab = [(nt, k, v if v.dim() < 2 or v[0].is_contiguous() else v.contiguous())
                 for nt in nts for k, v in g._ndata[nt].items()]
+        # static: the real counts stay on the device (sizes_out: [L + 1][T] node counts, the
+        # seed counts first, then [L][R] edge counts) and drive the kernels over the blocks
+        dsz = torch.empty((L + 1) * len(nts) + L * len(ces), dtype=torch.int64,
+                          device=g.device) if static else None
         steps, sizes, data = ops.sample_blocks(
             [c[0] for c in csrs], [c[1] for c in csrs], [c[2] for c in csrs],
             [tix[ce[0]] for ce in ces], [tix[ce[2]] for ce in ces], excl,
             [g.num_nodes(nt) for nt in nts], [seeds.get(nt, empty) for nt in nts], scratch,
-            fans, keys, stamp, static_shapes=static,
+            fans, keys, stamp, static_shapes=static, sizes_out=dsz,
             node_cap_hint=[[(hints or {}).get((s_, nt), 0) for nt in nts] for s_ in range(L)]
             if hints else None, overflow=overflow,
             edge_tables=[(v, ces.index(ce)) for ce, _k, v in etab],
@@ -193,6 +197,13 @@ class BlockSampler:
                 # the destination ids are the step's seed slots (-1: padding rows, the dump
                 # rows last), not the source prefix: a padding row may sit over a real source
                 b.static = True
+                # the real destination / source counts (device): the aggregation gathers the
+                # real rows only, and the backward's transposed gathers the real sources
+                for t, nt in enumerate(nts):
+                    b._live[('dst', nt)] = dsz.narrow(0, s_ * NT + t, 1)
+                    b._live[('src', nt)] = dsz.narrow(0, (s_ + 1) * NT + t, 1)
+                for ce in ces:
+                    rels[ce][0]._gnnrec_live = b._live[('dst', ce[2])]
                 for t, nt in enumerate(nts):
                     if s_ == 0:
                         dst_ids = torch.cat([seeds.get(nt, empty),
@@ -375,6 +386,9 @@ def _add_transposes(block: Block) -> None:
         [ops._nnz(block._rels[ce][0]) for ce in ces])
     for ce, ip, ix, w in zip(ces, ips, ixs, ws):
         ip._gnnrec_nnz = ops._nnz(block._rels[ce][0])
+        live = block._live.get(('src', ce[0]))
+        if live is not None:  # a static block: its real sources (rows past them are padding)
+            ip._gnnrec_live = live
         block._t[ce] = (ip, ix, w)
 
 

@@ -168,6 +168,26 @@ int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices, c
                                 const int64_t* plan, int64_t cap_h, int64_t cap_c,
                                 float* workspace, void* stream);
 
+/* The row gathers above driven by a device row count: rows >= *live (read on the device;
+ * a static-shape block's padding and dump rows, whose real count only the sampler's sizes
+ * hold) are empty rows — written as 0 (sum / mean only), left alone under
+ * GNNREC_SPMM_ACCUM — with no gathers, and the plan never marks them heavy.  Rows below it
+ * are bitwise the plain calls'.  A captured training step over static blocks (gnnrec.capture)
+ * so gathers only the batch's real edges. */
+int gnnrec_spmm_csr_live_f32(const int64_t* indptr, const int32_t* indices, const float* ew,
+                             const float* X, int64_t ldx, int64_t n_dst, int64_t d, int reduce,
+                             int flags, float* out, int64_t ldo, const int64_t* live,
+                             void* stream);
+int gnnrec_spmm_plan_build_live(const int64_t* indptr, int64_t n_dst, int64_t split,
+                                int64_t cap_h, int64_t cap_c, int64_t* plan,
+                                const int64_t* live, void* stream);
+int gnnrec_spmm_csr_planned_live_f32(const int64_t* indptr, const int32_t* indices,
+                                     const float* ew, const float* X, int64_t ldx, int64_t n_dst,
+                                     int64_t d, int reduce, int flags, float* out, int64_t ldo,
+                                     int64_t split, const int64_t* plan, int64_t cap_h,
+                                     int64_t cap_c, float* workspace, const int64_t* live,
+                                     void* stream);
+
 /* Two relations into one destination type in one launch: out_a[v] = reduce over relation
  * A's in-edges of v, out_b[v] likewise over relation B, both gathering from the same source
  * table X (C5's clicks and buys source tiles: the 12.5-edges-per-row relation runs beside

@@ -243,3 +243,55 @@ def test_learned_caps_shrink_the_blocks_and_overflow_is_redone():
     assert tight.static_redone == 1 and not item[1].static and not item[-1][0].static
     loss = _loss(4)(_model(g, agg="mean").train(), item)
     assert torch.isfinite(loss)
+
+
+@pytest.mark.parametrize("planned", [False, True])
+def test_live_row_count_gathers_only_the_real_rows(planned):
+    """gnnrec_spmm_csr_live_f32 / the planned form: rows below the device count are bitwise
+    the plain gather's, rows from it on are empty rows (0) — or left alone under ACCUM — and
+    never heavy; a static block's padding and dump rows (sampling static_shapes) so cost no
+    gathers."""
+    from gnnrec import _lib, ops
+    T = ops._T()
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(5)
+    n_dst, n_src, d = 3000, 700, 64
+    deg = torch.randint(0, 12, (n_dst,), device=DEV, generator=gen)
+    deg[2500] = 9000  # a heavy row past the live count
+    deg[100] = 5000   # and one below it
+    ip = torch.zeros(n_dst + 1, dtype=torch.int64, device=DEV)
+    ip[1:] = torch.cumsum(deg, 0)
+    nnz = int(ip[-1])
+    ix = torch.randint(0, n_src, (nnz,), device=DEV, generator=gen).int()
+    X = torch.randn(n_src, d, device=DEV, generator=gen)
+    live_n = 2200
+    live = torch.tensor([live_n], dtype=torch.int64, device=DEV)
+    ref = ops.spmm(ip, ix, X, 'mean')
+
+    def run(lv, flags=0, out=None):
+        out = torch.full((n_dst, d), 7.0, device=DEV) if out is None else out
+        if not planned:
+            T.spmm_csr(ip, ix, None, X, ops.REDUCE['mean'], flags, out, lv)
+            return out
+        split = 2048
+        cap_h = min(n_dst, nnz // (split + 1))
+        cap_c = nnz // split + cap_h
+        plan = torch.empty(3 + 2 * cap_h + cap_c, dtype=torch.int64, device=DEV)
+        T.spmm_plan_build(ip, split, cap_h, plan, lv)
+        ws = torch.empty(cap_c * d, device=DEV)
+        T.spmm_csr_planned(ip, ix, None, X, ops.REDUCE['mean'], flags, split, plan, cap_h,
+                           cap_c, out, ws, lv)
+        return out
+
+    full = run(None)
+    np.testing.assert_allclose(full.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    out = run(live)
+    assert torch.equal(out[:live_n], full[:live_n])
+    assert torch.count_nonzero(out[live_n:]) == 0
+    acc = torch.ones(n_dst, d, device=DEV)
+    run(live, _lib.SPMM_ACCUM, acc)
+    assert torch.equal(acc[live_n:], torch.ones_like(acc[live_n:]))
+    np.testing.assert_allclose(acc[:live_n].cpu().numpy(), (1 + full[:live_n]).cpu().numpy(),
+                               rtol=1e-6, atol=1e-6)
+    zero = torch.zeros(1, dtype=torch.int64, device=DEV)
+    assert torch.count_nonzero(run(zero)) == 0

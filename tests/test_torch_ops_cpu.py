@@ -21,7 +21,9 @@ NOT_OPS = {"gnnrec_last_error", "gnnrec_gemm_f32", "gnnrec_gemm_tn_f32",
            "gnnrec_spmm_project_mfma_f32",
            "gnnrec_sample_blocks_caps"}  # (sample_blocks sizes its outputs with it)
 RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_tn",
-           "gnnrec_gemm_tn_bias_rows_f32": "gemm_tn",
+           "gnnrec_gemm_tn_bias_rows_f32": "gemm_tn", "gnnrec_spmm_csr_live_f32": "spmm_csr",
+           "gnnrec_spmm_plan_build_live": "spmm_plan_build",
+           "gnnrec_spmm_csr_planned_live_f32": "spmm_csr_planned",
            "gnnrec_row_epilogue_f32": "row_epilogue", "gnnrec_add_f32": "add_",
            "gnnrec_tree_sum_f32": "tree_sum_", "gnnrec_spmm_csr_f32": "spmm_csr",
            "gnnrec_spmm_csr_split_f32": "spmm_csr_split",

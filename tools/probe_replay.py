@@ -47,10 +47,12 @@ def main():
     for _ in range(5):
         step(next(it))
     torch.cuda.synchronize()
+    torch.cuda._sleep(1000)  # trace marker (tools/rocpd_timeline.py, rocpd_sequence.py)
     t = time.perf_counter()
     for _ in range(N):
         step.graph.replay()
     host = time.perf_counter() - t
+    torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     # host time of the replay calls alone (a launch that waits for the previous replay shows
     # here as the GPU time per replay)
