@@ -40,6 +40,7 @@ struct GemmArgs {
   const float* A1; int64_t lda1; int64_t K1; const float* W1;
   const float* A2; int64_t lda2; int64_t K2; const float* W2;
   const int32_t* a2_deg; int a2_mode;
+  const int64_t* a2_ip;  // GNNREC_A2_DEG_INDPTR: the degrees as indptr differences instead
   const float* bias;
   const float* bias_ne;  // added on rows with a2_deg > 0 (a folded NodeEmbedding's W_n b_e)
   int64_t M; int64_t N;
@@ -49,6 +50,10 @@ struct GemmArgs {
   float* row_norm;  // nullable: |row| before the L2 norm (training keeps it for the backward)
   int vecA1, vecA2, vecW1, vecW2, vecO;
 };
+
+__device__ __forceinline__ int32_t a2_degree(const GemmArgs& g, int64_t row) {
+  return g.a2_ip ? (int32_t)(g.a2_ip[row + 1] - g.a2_ip[row]) : g.a2_deg[row];
+}
 
 __device__ __forceinline__ f32x4 load4(const float* base, int64_t row, int64_t ld, int64_t k,
                                         int64_t K, bool rowok, bool vec) {
@@ -120,7 +125,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[B
     bool ne = false;
     if (g.bias_ne) {
       const int64_t row = m0 + wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-      ne = row < g.M && g.a2_deg[row] > 0;
+      ne = row < g.M && a2_degree(g, row) > 0;
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(256, GEMM_WAVES_PER_SIMD) void gemm_f32_kernel(Gemm
     if (mode != GNNREC_A2_NONE) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int32_t dg = g.a2_deg[arow[i]];
+        const int32_t dg = a2_degree(g, arow[i]);
         if (mode == GNNREC_A2_DIV_DEG) rowdiv[i] = (float)(dg > 0 ? dg : 1);
         else rowzero[i] = rowzero[i] || dg == 0;
       }
@@ -509,7 +514,7 @@ __global__ __launch_bounds__(256, (BN > 128 ? 1 : GEMM_WAVES_PER_SIMD)) void gem
   float rowdiv2 = 1.f;
   bool rowzero2 = false;
   if (g.K2 > 0 && g.a2_mode != GNNREC_A2_NONE) {
-    const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
+    const int32_t dg = a2_degree(g, my_row < g.M ? my_row : g.M - 1);
     if (g.a2_mode == GNNREC_A2_DIV_DEG) rowdiv2 = (float)(dg > 0 ? dg : 1);
     else rowzero2 = dg == 0;
   }
@@ -652,7 +657,7 @@ __global__ __launch_bounds__(256, glds16_waves<S>()) void gemm_f32_glds16_kernel
   float rowinv2 = 1.f;
   bool rowzero2 = false;
   if (g.K2 > 0 && g.a2_mode != GNNREC_A2_NONE) {
-    const int32_t dg = g.a2_deg[my_row < g.M ? my_row : g.M - 1];
+    const int32_t dg = a2_degree(g, my_row < g.M ? my_row : g.M - 1);
     if (g.a2_mode == GNNREC_A2_DIV_DEG) rowinv2 = 1.f / (float)(dg > 0 ? dg : 1);
     else rowzero2 = dg == 0;
   }
@@ -780,6 +785,10 @@ extern "C" int gnnrec_gemm_rownorm_f32(const float* A1, int64_t lda1, int64_t K1
   GNNREC_REQUIRE(out != nullptr && ldo >= N, "gnnrec_gemm_f32: bad output");
   GNNREC_REQUIRE(K1 == 0 || (A1 && W1 && lda1 >= K1), "gnnrec_gemm_f32: bad A1/W1");
   GNNREC_REQUIRE(K2 == 0 || (A2 && W2 && lda2 >= K2), "gnnrec_gemm_f32: bad A2/W2");
+  // GNNREC_A2_DEG_INDPTR: a2_deg is an int64 indptr [M + 1] (a block CSR's: no degree array
+  // to build first)
+  const bool deg_ip = (a2_mode & GNNREC_A2_DEG_INDPTR) != 0;
+  a2_mode &= ~GNNREC_A2_DEG_INDPTR;
   GNNREC_REQUIRE(a2_mode == GNNREC_A2_NONE || a2_deg != nullptr,
                  "gnnrec_gemm_f32: a2_mode needs a2_deg");
   GNNREC_REQUIRE(bias_nonempty == nullptr || a2_deg != nullptr,
@@ -794,7 +803,9 @@ extern "C" int gnnrec_gemm_rownorm_f32(const float* A1, int64_t lda1, int64_t K1
   GemmArgs g;
   g.A1 = A1; g.lda1 = lda1; g.K1 = K1; g.W1 = W1;
   g.A2 = A2; g.lda2 = lda2; g.K2 = K2; g.W2 = W2;
-  g.a2_deg = a2_deg; g.a2_mode = a2_mode; g.bias = bias; g.bias_ne = bias_nonempty;
+  g.a2_deg = deg_ip ? nullptr : a2_deg;
+  g.a2_ip = deg_ip ? reinterpret_cast<const int64_t*>(a2_deg) : nullptr;
+  g.a2_mode = a2_mode; g.bias = bias; g.bias_ne = bias_nonempty;
   g.M = M; g.N = N; g.epilogue = epilogue; g.accum = accum; g.out_div = out_div;
   g.attn_vec = attn_vec; g.attn_state = attn_state;
   g.out = out; g.ldo = ldo;

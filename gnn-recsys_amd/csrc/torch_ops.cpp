@@ -825,12 +825,12 @@ float* pw(const Tensor& t) { return t.defined() ? p<float>(t) : nullptr; }
 Tensor gemm_nt(const Tensor& A, const Tensor& W, const Tensor* A2, const Tensor* W2, int epi,
                Tensor out, Tensor* row_norm, int accum = GNNREC_ACC_STORE,
                const float* bias = nullptr, const float* bias_ne = nullptr,
-               const int32_t* a2_deg = nullptr) {
+               const int32_t* a2_deg = nullptr, int a2_mode = GNNREC_A2_NONE) {
   const int64_t M = A.size(0), K1 = A.size(1), N = W.size(0);
   const int64_t K2 = A2 ? A2->size(1) : 0;
   ck(gnnrec_gemm_rownorm_f32(p<float>(A), ld(A, "A"), K1, p<float>(W), A2 ? p<float>(*A2) : nullptr,
                              A2 ? ld(*A2, "A2") : 1, K2, W2 ? p<float>(*W2) : nullptr, a2_deg,
-                             GNNREC_A2_NONE, bias, bias_ne, M, N, epi, accum, 0.f,
+                             a2_mode, bias, bias_ne, M, N, epi, accum, 0.f,
                              nullptr, nullptr, p<float>(out), ld(out, "out"),
                              row_norm ? p<float>(*row_norm) : nullptr, stream_of(A)),
      "gnnrec_gemm_f32");
@@ -944,10 +944,13 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                                 p<float>(agg), ld(agg, "agg"), lv, stream_of(m)),
        "gnnrec_spmm_csr_f32");
   }
-  const Tensor deg = bnc.defined() ? row_degrees(indptr) : Tensor();
+  // bias_ne's non-empty test reads the block CSR's indptr directly (GNNREC_A2_DEG_INDPTR)
+  const Tensor ipc = bnc.defined() ? indptr.contiguous() : Tensor();
   gemm_nt(H, Wsc, &agg, &Wnc, GNNREC_EPI_RELU | (norm ? GNNREC_EPI_L2NORM : 0), z,
           norm ? &nrm : nullptr, GNNREC_ACC_STORE, bc.defined() ? p<float>(bc) : nullptr,
-          bnc.defined() ? p<float>(bnc) : nullptr, deg.defined() ? p<int32_t>(deg) : nullptr);
+          bnc.defined() ? p<float>(bnc) : nullptr,
+          ipc.defined() ? reinterpret_cast<const int32_t*>(p<int64_t>(ipc)) : nullptr,
+          ipc.defined() ? GNNREC_A2_DEG_INDPTR : GNNREC_A2_NONE);
   return {z, agg, nrm};
 }
 
@@ -1872,11 +1875,18 @@ compact_ids(at::TensorList ids, at::IntArrayRef type, at::IntArrayRef n_nodes,
                                p<int64_t>(nodes[t]), caps[t], p<uint8_t>(marks[t]),
                                p<uint64_t>(bits[t]) + 2 * W};
   }
+  // the lists' local ids are consecutive views of one buffer (lists given one after the
+  // other, e.g. an etype's positive then negative sources, come back joined)
+  int64_t n_all = 0;
+  for (size_t l = 0; l < L; ++l) n_all += ids[l].numel();
+  const Tensor local_all = at::empty({n_all}, i64);
+  int64_t off = 0;
   for (size_t l = 0; l < L; ++l) {
     dev(ids[l], "ids", at::kLong);
     TORCH_CHECK_VALUE(type[l] >= 0 && (size_t)type[l] < NT && ids[l].is_contiguous(),
                       "compact_ids: list ", l, ": type out of range or ids not contiguous");
-    local[l] = at::empty({ids[l].numel()}, i64);
+    local[l] = local_all.narrow(0, off, ids[l].numel());
+    off += ids[l].numel();
     Ls[l] = gnnrec_compact_list{p<int64_t>(ids[l]), ids[l].numel(), (int32_t)type[l],
                                 p<int64_t>(local[l])};
   }

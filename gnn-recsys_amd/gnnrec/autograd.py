@@ -433,6 +433,17 @@ class CosineFn(torch.autograd.Function):
         return ga, gb, None, None
 
 
+def _joined(a, b):
+    """torch.cat([a, b]) of two 1-d tensors — as a view when b starts where a ends in the
+    same storage (no launch)."""
+    if a.dim() == 1 and b.dim() == 1 and a.is_contiguous() and b.is_contiguous() and \
+            a.dtype == b.dtype and a.device == b.device and \
+            a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr() and \
+            b.storage_offset() == a.storage_offset() + a.numel():
+        return a.as_strided((a.numel() + b.numel(),), (1,), a.storage_offset())
+    return torch.cat([a, b])
+
+
 class CosinePairFn(torch.autograd.Function):
     """CosineFn over the positive and the negative pair graph of one etype at once (they
     share node ids): one forward launch over both edge lists, and one backward call whose
@@ -459,14 +470,20 @@ class CosinePairFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         if not (need[0] or need[1]):
             return None, None, None, None, None, None, None
-        src, dst = torch.cat([src_p, src_n]), torch.cat([dst_p, dst_n])
+        # the positive and negative lists are usually one buffer already (the static batch
+        # head's compaction, MarginLossFn's gradient): a view then, no cat / copy launches
+        src, dst = _joined(src_p, src_n), _joined(dst_p, dst_n)
         n_pos = ctx.n_pos
-        g = torch.empty(src.numel(), dtype=torch.float32, device=src.device)
-        for part, gp in ((g[:n_pos], g_pos), (g[n_pos:], g_neg)):
-            if gp is None:
-                part.zero_()
-            else:
-                part.copy_(gp.reshape(-1))
+        g = None
+        if g_pos is not None and g_neg is not None:
+            g = _joined(g_pos.reshape(-1), g_neg.reshape(-1))
+        else:
+            g = torch.empty(src.numel(), dtype=torch.float32, device=src.device)
+            for part, gp in ((g[:n_pos], g_pos), (g[n_pos:], g_neg)):
+                if gp is None:
+                    part.zero_()
+                else:
+                    part.copy_(gp.reshape(-1))
         ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(), g,
                                         need[0], need[1])
         return ga, gb, None, None, None, None, None
@@ -482,18 +499,22 @@ class MarginLossFn(torch.autograd.Function):
         delta, meta = spec
         parts = [(scores[2 * i].reshape(-1), scores[2 * i + 1].reshape(-1), K, mask, rec)
                  for i, (K, mask, rec) in enumerate(meta)]
-        loss, total, grads = ops.margin_loss(parts, delta)
-        ctx.grads, ctx.total = grads, total
+        loss, total, grads, flat = ops.margin_loss(parts, delta, flat=True)
+        ctx.grads, ctx.total, ctx.flat = grads, total, flat
         ctx.shapes = [t.shape for t in scores]
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        scale = g / ctx.total
-        out = [None]
+        # the unscaled gradients are views of one buffer (ops.margin_loss): one scale launch
+        # for all of them, handed back as views of its result (the cosine backward then joins
+        # an etype's positive and negative parts without a copy)
+        scaled = ctx.flat * (g / ctx.total)
+        out, off = [None], 0
         for i, (gp, gn) in enumerate(ctx.grads):
-            out.append((gp * scale).view(ctx.shapes[2 * i]) if ctx.needs_input_grad[1 + 2 * i]
-                       else None)
-            out.append((gn * scale).view(ctx.shapes[2 * i + 1])
-                       if ctx.needs_input_grad[2 + 2 * i] else None)
+            for j, part in enumerate((gp, gn)):
+                n = part.numel()
+                view = scaled.narrow(0, off, n).view(ctx.shapes[2 * i + j])
+                out.append(view if ctx.needs_input_grad[1 + 2 * i + j] else None)
+                off += n
         return tuple(out)

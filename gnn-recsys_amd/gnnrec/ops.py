@@ -1102,10 +1102,12 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
     return gHs, gHd
 
 
-def margin_loss(parts, delta: float):
+def margin_loss(parts, delta: float, flat: bool = False):
     """f2: max_margin_loss forward + unscaled gradients for a list of etype parts
     [(pos [E], neg [E*K], K, mask|None, recency|None)] -> (loss 0-d tensor, N_total,
-    [(g_pos, g_neg)]).  Gradients are d(sum of scores)/d(score); the loss is the mean."""
+    [(g_pos, g_neg)]).  Gradients are d(sum of scores)/d(score); the loss is the mean.
+    They are views of one buffer, in part order (pos_0, neg_0, pos_1, ...); flat: that
+    buffer is returned as well."""
     T = _T()
     dev = parts[0][0].device
     # an etype without positive edges (the pair graphs' other etypes) adds nothing: no
@@ -1114,7 +1116,9 @@ def margin_loss(parts, delta: float):
     blocks = [0 if skip and p[0].numel() == 0 else int(T.margin_loss_blocks(p[0].numel()))
               for p in parts]
     partial = torch.empty(sum(blocks), dtype=torch.float32, device=dev)
-    grads, off, total = [], 0, 0
+    gflat = torch.empty(sum(p[0].numel() + p[1].numel() for p in parts), dtype=torch.float32,
+                        device=dev)
+    grads, off, total, goff = [], 0, 0, 0
     for (pos, neg, K, mask, rec), nb in zip(parts, blocks):
         _dev(pos, "pos_score", torch.float32)
         _dev(neg, "neg_score", torch.float32)
@@ -1132,8 +1136,9 @@ def margin_loss(parts, delta: float):
             rec = rec.contiguous()
             if rec.numel() != n_pos:
                 raise ValueError("recency must have one value per positive edge")
-        g_pos = torch.empty_like(pos)
-        g_neg = torch.empty_like(neg)
+        g_pos = gflat.narrow(0, goff, n_pos).view(pos.shape)
+        g_neg = gflat.narrow(0, goff + n_pos, neg.numel()).view(neg.shape)
+        goff += n_pos + neg.numel()
         if nb == 0:
             grads.append((g_pos, g_neg))
             continue
@@ -1144,7 +1149,7 @@ def margin_loss(parts, delta: float):
         total += neg.numel()
     loss = torch.empty((), dtype=torch.float32, device=dev)
     T.sum_scaled(partial, 1.0 / total if total else float('nan'), loss)
-    return loss, total, grads
+    return (loss, total, grads, gflat) if flat else (loss, total, grads)
 
 
 def edge_mlp(src: torch.Tensor, dst: torch.Tensor, P: torch.Tensor, Q: torch.Tensor,

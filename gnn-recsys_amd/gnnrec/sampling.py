@@ -705,24 +705,29 @@ class EdgeDataLoader:
                 ns = ps.unsqueeze(1).expand(ps.numel(), k).reshape(-1)
                 nd = torch.randint(0, g.num_nodes(ce[2]), (ns.numel(),), device=g.device)
                 negs.append((ce, ns, nd))
-        lists, caps = [], [0] * len(nts)
+        # per etype: positive sources, negative sources, positive dsts, negative dsts — the
+        # local ids come back as consecutive views of one buffer, so an etype's positive and
+        # negative endpoint lists are one list each (the cosine backward reads them joined)
+        neg_of = {ce: (ns, nd) for ce, ns, nd in negs}
+        lists, caps, slots = [], [0] * len(nts), {}
         for ce, ps, pd in pairs:
-            lists += [(ps, tix[ce[0]]), (pd, tix[ce[2]])]
-            caps[tix[ce[0]]] += ps.numel()
-            caps[tix[ce[2]]] += pd.numel()
-        for ce, ns, nd in negs:
-            lists += [(ns, tix[ce[0]]), (nd, tix[ce[2]])]
-            caps[tix[ce[2]]] += nd.numel()
+            ns, nd = neg_of.get(ce, (None, None))
+            for key, ids, nt in (('ps', ps, ce[0]), ('ns', ns, ce[0]), ('pd', pd, ce[2]),
+                                 ('nd', nd, ce[2])):
+                if ids is None:
+                    continue
+                slots[(ce, key)] = len(lists)
+                lists.append((ids, tix[nt]))
+                if key != 'ns':  # a negative's source is a positive's source
+                    caps[tix[nt]] += ids.numel()
         caps = [min(c, g.num_nodes(nt)) for c, nt in zip(caps, nts)]
         nodes, local, count = ops.compact_ids(lists, self._cx_scratch, caps)
         node_ids = dict(zip(nts, nodes))
-        pos_l, neg_l, i = {}, {}, 0
+        pos_l, neg_l = {}, {}
         for ce, _ps, _pd in pairs:
-            pos_l[ce] = (local[i], local[i + 1])
-            i += 2
-        for ce, _ns, _nd in negs:
-            neg_l[ce] = (local[i], local[i + 1])
-            i += 2
+            pos_l[ce] = (local[slots[(ce, 'ps')]], local[slots[(ce, 'pd')]])
+            if ce in neg_of:
+                neg_l[ce] = (local[slots[(ce, 'ns')]], local[slots[(ce, 'nd')]])
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
         pos_l = {ce: pos_l.get(ce, (empty, empty)) for ce in g.canonical_etypes}
         if k:  # every etype, in graph order, as _head returns them

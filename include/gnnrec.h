@@ -95,6 +95,8 @@ extern "C" {
 #define GNNREC_A2_NONE 0
 #define GNNREC_A2_DIV_DEG 1  /* row / max(deg,1)   (mean of a summed neighbourhood) */
 #define GNNREC_A2_ZERO_DEG 2 /* row := 0 where deg == 0 (max of an empty neighbourhood) */
+#define GNNREC_A2_DEG_INDPTR 16 /* or-ed in: a2_deg points at an int64 indptr [M + 1] and the
+                                 * degrees are its differences (no degree array to build) */
 
 /* ---- library ---------------------------------------------------------- */
 int gnnrec_version(void);
