@@ -345,7 +345,9 @@ def _emulation_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gnnrec.dist import AsyncEmulatedExchange
-        ex = AsyncEmulatedExchange(delay_us=30000)
+        # a long delay: the two ranks share one GPU here, and the other process's kernels
+        # can hold this one's fill back by tens of ms (30 ms flaked on a busy box)
+        ex = AsyncEmulatedExchange(delay_us=300000)
         own = torch.full((4, 8), float(rank + 1), device="cuda")
         out = torch.full((8, 8), -1.0, device="cuda")
         _, work = ex.all_gather_rows(own, out, async_op=True)

@@ -2,7 +2,8 @@
 num_workers=2) -> CapturedTrainStep), its timed steps bracketed by torch.cuda._sleep marker
 kernels, for a kernel trace whose steady state tools/rocpd_timeline.py measures.
 
-    python tools/probe_captured_loop.py [K] [steps] [switch_interval_s]
+    python tools/probe_captured_loop.py [K] [steps] [switch_interval_s | 0] [num_workers]
+        [provable | auto]
 """
 import json
 import os
@@ -21,8 +22,10 @@ def main():
     from gnnrec.synth import minibatch_graph
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-    if len(sys.argv) > 3:  # the interpreter's thread switch interval (s), an A/B knob
+    if len(sys.argv) > 3 and float(sys.argv[3]) > 0:  # the thread switch interval (s), A/B
         sys.setswitchinterval(float(sys.argv[3]))
+    nw = int(sys.argv[4]) if len(sys.argv) > 4 else 2  # the loader's sampling thread(s)
+    caps = sys.argv[5] if len(sys.argv) > 5 else "provable"  # EdgeDataLoader static_caps
     dev = torch.device("cuda")
     g = minibatch_graph(64, dev)
     buys = ("user", "buys", "item")
@@ -42,7 +45,8 @@ def main():
                         MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                         reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
-                        shuffle=True, num_workers=2, static_shapes=True)
+                        shuffle=True, num_workers=nw, static_shapes=True,
+                        static_caps=caps)
     el.sampler.first_transposes_below = 0
     it = iter(el)
     for _ in range(5):
@@ -56,7 +60,8 @@ def main():
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     print(json.dumps({"K": K, "steps": steps, "ms_per_step": round(ms, 4),
-                      "switch_interval": sys.getswitchinterval(),
+                      "switch_interval": sys.getswitchinterval(), "num_workers": nw,
+                      "static_caps": caps, "redone": el.static_redone,
                       "replays": step.replays, "loss": float(loss)}))
     del it, el
 
