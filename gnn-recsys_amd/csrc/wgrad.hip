@@ -302,6 +302,45 @@ __global__ __launch_bounds__(256) void act_backward_normed_kernel(
   }
 }
 
+// The same for d <= 64 (d % 4 == 0, 16-B aligned rows): 16 lanes per row with one float4
+// each, four rows per wave, so a wave keeps 4 rows (2 KB) of z and gz in flight instead of
+// one — the one-row-per-wave form read a 1M-row layer at 2.8 TB/s (C2 at K = 2500).  The
+// dot is summed per lane over its 4 columns, then over the 16 lanes by an xor tree.
+__global__ __launch_bounds__(256) void act_backward_normed_v4_kernel(
+    const float* __restrict__ z, int64_t ldz, const float* __restrict__ nrm,
+    const float* __restrict__ gz, int64_t ldg, int64_t n_rows, int64_t d, int relu,
+    float* __restrict__ gu, int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+  const int64_t c = (int64_t)(lane & 15) * 4;
+  const bool ok = r < n_rows && c < d;
+  float4 zz = make_float4(0.f, 0.f, 0.f, 0.f), gg = zz;
+  if (ok) {
+    zz = *reinterpret_cast<const float4*>(z + r * ldz + c);
+    gg = *reinterpret_cast<const float4*>(gz + r * ldg + c);
+  }
+  float dot = zz.x * gg.x + zz.y * gg.y + zz.z * gg.z + zz.w * gg.w;
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+  if (!ok) return;
+  const float n = nrm[r];
+  const bool scale = n != 0.f;
+  const float inv = scale ? 1.f / n : 1.f;
+  const float coef = scale ? dot : 0.f;
+  float4 o;
+  o.x = (gg.x - zz.x * coef) * inv;
+  o.y = (gg.y - zz.y * coef) * inv;
+  o.z = (gg.z - zz.z * coef) * inv;
+  o.w = (gg.w - zz.w * coef) * inv;
+  if (relu) {
+    if (!(zz.x > 0.f)) o.x = 0.f;
+    if (!(zz.y > 0.f)) o.y = 0.f;
+    if (!(zz.z > 0.f)) o.z = 0.f;
+    if (!(zz.w > 0.f)) o.w = 0.f;
+  }
+  *reinterpret_cast<float4*>(gu + r * ldo + c) = o;
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -476,6 +515,13 @@ extern "C" int gnnrec_act_backward_normed_f32(const float* z, int64_t ldz, const
                  "gnnrec_act_backward_normed_f32: bad sizes");
   if (n_rows == 0 || d == 0) return GNNREC_OK;
   GNNREC_REQUIRE(z && row_norm && gz && gu, "gnnrec_act_backward_normed_f32: null pointer");
+  if (d <= 64 && d % 4 == 0 && ldz % 4 == 0 && ldg % 4 == 0 && ldo % 4 == 0 && aligned16(z) &&
+      aligned16(gz) && aligned16(gu)) {
+    hipLaunchKernelGGL(act_backward_normed_v4_kernel, dim3((unsigned)((n_rows + 15) / 16)),
+                       dim3(256), 0, as_stream(stream), z, ldz, row_norm, gz, ldg, n_rows, d,
+                       relu, gu, ldo);
+    return check_launch("gnnrec_act_backward_normed_f32");
+  }
   hipLaunchKernelGGL(act_backward_normed_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0,
                      as_stream(stream), z, ldz, row_norm, gz, ldg, n_rows, d, relu, gu, ldo);
   return check_launch("gnnrec_act_backward_normed_f32");
