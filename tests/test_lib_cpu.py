@@ -56,6 +56,14 @@ def test_argument_validation_without_a_gpu():
     parts = (ctypes.c_void_p * 2)(16, 36)
     rc = lib.gnnrec_tree_sum_f32(parts, 2, 8, ctypes.c_void_p(16), None)
     assert rc != 0 and b"aligned" in lib.gnnrec_last_error()
+    # a device row count (static blocks) drives sum / mean gathers only
+    rc = lib.gnnrec_spmm_csr_live_f32(ctypes.c_void_p(16), ctypes.c_void_p(16), None,
+                                      ctypes.c_void_p(16), 4, 3, 4, _lib.REDUCE_MAX, 0,
+                                      ctypes.c_void_p(16), 4, ctypes.c_void_p(16), None)
+    assert rc != 0 and b"sum or mean" in lib.gnnrec_last_error()
+    rc = lib.gnnrec_gemm_tn_bias_rows_f32(None, 4, None, 4, -1, 4, 4, None, 4, None, None, 0,
+                                          None, None)
+    assert rc != 0 and b"negative size" in lib.gnnrec_last_error()
     # empty problems are no-ops that succeed without touching memory
     assert lib.gnnrec_spmm_csr_f32(None, None, None, None, 4, 0, 4, 1, 0, None, 4, None) == 0
     assert lib.gnnrec_tree_sum_f32(parts, 2, 0, None, None) == 0
