@@ -47,9 +47,11 @@ def main():
     for _ in range(5):
         step()
     torch.cuda.synchronize()
+    torch.cuda._sleep(1000)  # trace markers (tools/rocpd_timeline.py)
     t = time.perf_counter()
     for _ in range(N):
         loss = step()
+    torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     print(json.dumps({"K": K, "steps": N, "ms_per_step": (time.perf_counter() - t) / N * 1e3,
                       "loss": float(loss)}))
