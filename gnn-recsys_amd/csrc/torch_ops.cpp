@@ -483,9 +483,11 @@ void sddmm_cos_grouped(const Tensor& src_g, const optional<Tensor>& first, int64
      "gnnrec_sddmm_cos_grouped_f32");
 }
 
+// groups > 0: the grouped layout of gnnrec_sddmm_cos_backward_grouped_f32 (K negatives per
+// positive, E = groups (K + 1))
 void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, const Tensor& Hd,
                         const Tensor& grad, const optional<Tensor>& gHs,
-                        const optional<Tensor>& gHd, Tensor& ws) {
+                        const optional<Tensor>& gHd, Tensor& ws, int64_t groups, int64_t K) {
   const OneDevice one_device_;
   dev(src, "src", at::kLong);
   dev(dst, "dst", at::kLong);
@@ -497,9 +499,19 @@ void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, 
   const int64_t E = src.numel(), d = Hs.size(1);
   TORCH_CHECK_VALUE(dst.numel() == E && grad.numel() == E, "src/dst/grad length mismatch");
   TORCH_CHECK_VALUE(Hd.size(1) == d, "endpoint feature sizes differ");
+  TORCH_CHECK_VALUE(groups <= 0 || (K >= 0 && groups * (K + 1) == E),
+                    "sddmm_cos_backward: groups x (K + 1) must equal the edge count");
   const int64_t lds = ld(Hs, "Hs"), ldd = ld(Hd, "Hd");
   if (meta(Hs)) return;
   const c10::DeviceGuard g(Hs.device());
+  if (groups > 0) {
+    ck(gnnrec_sddmm_cos_backward_grouped_f32(
+           p<int64_t>(src), p<int64_t>(dst), groups, K, p<float>(Hs), lds, Hs.size(0),
+           p<float>(Hd), ldd, Hd.size(0), d, p<float>(grad), p<float>(gHs), p<float>(gHd),
+           ws.data_ptr(), ws.nbytes(), stream_of(Hs)),
+       "gnnrec_sddmm_cos_backward_grouped_f32");
+    return;
+  }
   ck(gnnrec_sddmm_cos_backward_f32(p<int64_t>(src), p<int64_t>(dst), E, p<float>(Hs), lds,
                                    Hs.size(0), p<float>(Hd), ldd, Hd.size(0), d, p<float>(grad),
                                    p<float>(gHs), p<float>(gHd), ws.data_ptr(), ws.nbytes(),
@@ -2039,7 +2051,10 @@ int64_t csr_build_workspace_bytes(int64_t E, int64_t n_dst) {
   const OneDevice one_device_;
   return (int64_t)gnnrec_csr_build_workspace_bytes(E, n_dst);
 }
-int64_t sddmm_cos_backward_workspace_bytes(int64_t E, int64_t n_src, int64_t n_dst, int64_t d) {
+int64_t sddmm_cos_backward_workspace_bytes(int64_t E, int64_t n_src, int64_t n_dst, int64_t d,
+                                           int64_t groups, int64_t K) {
+  if (groups > 0)
+    return (int64_t)gnnrec_sddmm_cos_backward_grouped_workspace_bytes(groups, K, n_src, n_dst, d);
   const OneDevice one_device_;
   return (int64_t)gnnrec_sddmm_cos_backward_workspace_bytes(E, n_src, n_dst, d);
 }
@@ -2089,7 +2104,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("sddmm_cos_grouped(Tensor src_g, Tensor? first, int K, Tensor dst, Tensor Hs, Tensor Hd, "
         "Tensor(a!) out_first, Tensor(b!) out) -> ()");
   m.def("sddmm_cos_backward(Tensor src, Tensor dst, Tensor Hs, Tensor Hd, Tensor grad, "
-        "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace) -> ()");
+        "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace, int groups=0, int K=0) -> ()");
   m.def("edge_mlp(Tensor src, Tensor dst, Tensor P, Tensor Q, Tensor W2, Tensor b2, Tensor w3, "
         "Tensor b3, Tensor(a!) out) -> ()");
   m.def("sample_count(Tensor indptr, Tensor eids, Tensor? excluded, Tensor seeds, int fanout, "
@@ -2184,8 +2199,8 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("csr_from_keys_workspace_bytes(int n_edges, int n_rows) -> int",
         &csr_from_keys_workspace_bytes);
   m.def("csr_build_workspace_bytes(int n_edges, int n_dst) -> int", &csr_build_workspace_bytes);
-  m.def("sddmm_cos_backward_workspace_bytes(int n_edges, int n_src, int n_dst, int d) -> int",
-        &sddmm_cos_backward_workspace_bytes);
+  m.def("sddmm_cos_backward_workspace_bytes(int n_edges, int n_src, int n_dst, int d, "
+        "int groups=0, int K=0) -> int", &sddmm_cos_backward_workspace_bytes);
   m.def("margin_loss_blocks(int n_pos) -> int", &margin_loss_blocks);
 }
 

@@ -228,6 +228,162 @@ int run_side(const int64_t* keys, const int64_t* other, const float* g, int64_t 
   return GNNREC_OK;
 }
 
+// ---- grouped source side (negative_sampler.Uniform's pair graphs) ----------------------
+// Edges [G positives | G x K negatives] with src[G + g K + j] = src[g] (the reference's
+// src.repeat_interleave(K), src/sampling.py:163-165): a group's K + 1 edges share their source
+// row, so the source side needs no sort of the E edges — only of the G group keys.  A wave
+// gathers one 64-edge chunk of one group (weights g_e inv_t, rows Hd[t]) into a partial
+// row; a source row then sums its groups' chunks in key-sorted group order and applies the
+// normalisation epilogue of cos_epilogue_kernel.  Every sum runs in a fixed order.
+constexpr int kCosBwdChunk = 64;
+
+template <int LPR>
+__global__ __launch_bounds__(256) void cos_bwd_chunk_kernel(
+    const int64_t* __restrict__ dst, const float* __restrict__ grad,
+    const float* __restrict__ inv_d, const float* __restrict__ Hd, int64_t ldd, int d,
+    int64_t G, int64_t K, int64_t chunks, float* __restrict__ part) {
+  constexpr int NPW = kWave / LPR;  // edges per wave-instruction
+  constexpr int U = 8;              // edges in flight per lane group
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / LPR, gl = lane % LPR;
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= G * chunks) return;  // wave-uniform
+  const int64_t g = task / chunks, c = task - g * chunks;
+  const int col = gl * 4;
+  const bool cok = col < d;
+  const int64_t q0 = c * kCosBwdChunk;
+  const int64_t q1 = q0 + kCosBwdChunk < K + 1 ? q0 + kCosBwdChunk : K + 1;
+  auto edge_of = [&](int64_t q) { return q == 0 ? g : G + g * K + (q - 1); };
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t qb = q0 + grp; qb < q1; qb += (int64_t)NPW * U) {
+    float4 v[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = qb + (int64_t)u * NPW;
+      const bool ok = q < q1;
+      const int64_t e = edge_of(ok ? q : q0);
+      const int64_t t = dst[e];
+      w[u] = ok ? grad[e] * inv_d[t] : 0.f;
+      v[u] = cok ? *reinterpret_cast<const float4*>(Hd + t * ldd + col)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (qb + (int64_t)u * NPW < q1) {
+        acc.x += w[u] * v[u].x;
+        acc.y += w[u] * v[u].y;
+        acc.z += w[u] * v[u].z;
+        acc.w += w[u] * v[u].w;
+      }
+    }
+  }
+  // the NPW lane groups' partials, combined by a fixed xor tree
+#pragma unroll
+  for (int off = LPR; off < kWave; off <<= 1) {
+    acc.x += __shfl_xor(acc.x, off);
+    acc.y += __shfl_xor(acc.y, off);
+    acc.z += __shfl_xor(acc.z, off);
+    acc.w += __shfl_xor(acc.w, off);
+  }
+  if (grp == 0 && cok) *reinterpret_cast<float4*>(part + task * d + col) = acc;
+}
+
+// one wave per source row: G_s = its groups' chunk partials in order, then
+// gHs[s] = inv (G_s - û (û . G_s)) as cos_epilogue_kernel
+__global__ __launch_bounds__(256) void cos_bwd_combine_kernel(
+    const int64_t* __restrict__ indptr_g, const int32_t* __restrict__ perm_g,
+    const float* __restrict__ part, int64_t chunks, const float* __restrict__ T, int64_t ldt,
+    int64_t n, int d, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane * 4;
+  const bool cok = col < d;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n;
+       r += (int64_t)gridDim.x * 4) {
+    float4 Gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = indptr_g[r]; i < indptr_g[r + 1]; ++i) {
+      const float* pg = part + (int64_t)perm_g[i] * chunks * d;
+      for (int64_t c = 0; c < chunks; ++c) {
+        if (cok) {
+          const float4 x = *reinterpret_cast<const float4*>(pg + c * d + col);
+          Gv.x += x.x;
+          Gv.y += x.y;
+          Gv.z += x.z;
+          Gv.w += x.w;
+        }
+      }
+    }
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cok) t = *reinterpret_cast<const float4*>(T + r * ldt + col);
+    float ss = t.x * t.x + t.y * t.y + t.z * t.z + t.w * t.w;
+    float dot = t.x * Gv.x + t.y * Gv.y + t.z * Gv.z + t.w * Gv.w;
+    ss = wave_sum(ss);
+    dot = wave_sum(dot);
+    const float nrm = sqrtf(ss);
+    const float inv = 1.f / fmaxf(nrm, 1e-12f);
+    const bool big = nrm > 1e-12f;
+    const float proj = big ? dot * inv * inv : 0.f;
+    if (cok) {
+      float4 o;
+      o.x = inv * (Gv.x - (big ? t.x * proj : 0.f));
+      o.y = inv * (Gv.y - (big ? t.y * proj : 0.f));
+      o.z = inv * (Gv.z - (big ? t.z * proj : 0.f));
+      o.w = inv * (Gv.w - (big ? t.w * proj : 0.f));
+      *reinterpret_cast<float4*>(out + r * d + col) = o;
+    }
+  }
+}
+
+inline int64_t cos_bwd_chunks(int64_t K) { return (K + 1 + kCosBwdChunk - 1) / kCosBwdChunk; }
+
+// scratch of the grouped source side: keys32 | indptr_g | perm_g | sort | partials
+size_t grouped_side_bytes(int64_t G, int64_t K, int64_t n_src, int64_t d) {
+  size_t b = 0;
+  b += align_up((size_t)G * 4);
+  b += align_up((size_t)(n_src + 1) * 8);
+  b += align_up((size_t)G * 4);
+  b += align_up(gnnrec_csr_from_keys_workspace_bytes(G, n_src));
+  b += align_up((size_t)G * cos_bwd_chunks(K) * d * 4);
+  return b;
+}
+
+int run_grouped_src_side(const int64_t* src, const int64_t* dst, const float* grad, int64_t G,
+                         int64_t K, const float* Hs, int64_t lds, int64_t n_src, const float* Hd,
+                         int64_t ldd, const float* inv_d, int64_t d, float* gHs, char* p,
+                         hipStream_t s) {
+  int32_t* k32 = reinterpret_cast<int32_t*>(p);
+  p += align_up((size_t)G * 4);
+  int64_t* indptr_g = reinterpret_cast<int64_t*>(p);
+  p += align_up((size_t)(n_src + 1) * 8);
+  int32_t* perm_g = reinterpret_cast<int32_t*>(p);
+  p += align_up((size_t)G * 4);
+  const size_t sort_bytes = gnnrec_csr_from_keys_workspace_bytes(G, n_src);
+  void* sort_ws = p;
+  p += align_up(sort_bytes);
+  float* part = reinterpret_cast<float*>(p);
+  hipLaunchKernelGGL(keys_to_i32_kernel, dim3(flat_grid(G)), dim3(256), 0, s, src, G, k32);
+  int rc = gnnrec_csr_from_keys(k32, G, n_src, sort_ws, sort_bytes, indptr_g, perm_g, s);
+  if (rc != GNNREC_OK) return rc;
+  const int64_t chunks = cos_bwd_chunks(K), tasks = G * chunks;
+  const dim3 grid((unsigned)((tasks + 3) / 4));
+  const int lanes = (int)(d / 4);
+  if (lanes <= 16)
+    hipLaunchKernelGGL(cos_bwd_chunk_kernel<16>, grid, dim3(256), 0, s, dst, grad, inv_d, Hd,
+                       ldd, (int)d, G, K, chunks, part);
+  else if (lanes <= 32)
+    hipLaunchKernelGGL(cos_bwd_chunk_kernel<32>, grid, dim3(256), 0, s, dst, grad, inv_d, Hd,
+                       ldd, (int)d, G, K, chunks, part);
+  else
+    hipLaunchKernelGGL(cos_bwd_chunk_kernel<64>, grid, dim3(256), 0, s, dst, grad, inv_d, Hd,
+                       ldd, (int)d, G, K, chunks, part);
+  int64_t blocks = (n_src + 3) / 4;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  if (blocks > 0)
+    hipLaunchKernelGGL(cos_bwd_combine_kernel, dim3((unsigned)blocks), dim3(256), 0, s, indptr_g,
+                       perm_g, part, chunks, Hs, lds, n_src, (int)d, gHs);
+  return GNNREC_OK;
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -322,4 +478,75 @@ extern "C" int gnnrec_sddmm_cos_backward_f32(const int64_t* src, const int64_t* 
     if (rc != GNNREC_OK) return rc;
   }
   return check_launch("gnnrec_sddmm_cos_backward_f32");
+}
+
+// the grouped layout (include/gnnrec.h): the source side from the group keys alone
+extern "C" size_t gnnrec_sddmm_cos_backward_grouped_workspace_bytes(int64_t n_groups, int64_t K,
+                                                                    int64_t n_src, int64_t n_dst,
+                                                                    int64_t d) {
+  using namespace gnnrec;
+  const int64_t E = n_groups * (K + 1);
+  if (E <= 0) return 0;
+  const size_t a = grouped_side_bytes(n_groups, K, n_src, d), b = side_bytes(E, n_dst, d);
+  return align_up((size_t)n_src * 4) + align_up((size_t)n_dst * 4) + (a > b ? a : b);
+}
+
+extern "C" int gnnrec_sddmm_cos_backward_grouped_f32(const int64_t* src, const int64_t* dst,
+                                                     int64_t n_groups, int64_t K, const float* Hs,
+                                                     int64_t lds, int64_t n_src, const float* Hd,
+                                                     int64_t ldd, int64_t n_dst, int64_t d,
+                                                     const float* grad, float* gHs, float* gHd,
+                                                     void* workspace, size_t workspace_bytes,
+                                                     void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_groups >= 0 && K >= 0 && n_src >= 0 && n_dst >= 0 && d > 0,
+                 "gnnrec_sddmm_cos_backward_grouped_f32: bad sizes");
+  const int64_t E = n_groups * (K + 1);
+  GNNREC_REQUIRE(E < (int64_t(1) << 31) && n_src < (int64_t(1) << 31) &&
+                     n_dst < (int64_t(1) << 31),
+                 "gnnrec_sddmm_cos_backward_grouped_f32: int32 edge / node ids");
+  GNNREC_REQUIRE(lds >= d && ldd >= d,
+                 "gnnrec_sddmm_cos_backward_grouped_f32: leading dimension < d");
+  GNNREC_REQUIRE(d % 4 == 0 && d <= 256 && lds % 4 == 0 && ldd % 4 == 0 && aligned16(Hs) &&
+                     aligned16(Hd) && (!gHs || aligned16(gHs)),
+                 "gnnrec_sddmm_cos_backward_grouped_f32: d %% 4 == 0, d <= 256, 16-B rows");
+  hipStream_t s = as_stream(stream);
+  if (E == 0) {
+    if (gHs && n_src) (void)hipMemsetAsync(gHs, 0, (size_t)n_src * d * 4, s);
+    if (gHd && n_dst) (void)hipMemsetAsync(gHd, 0, (size_t)n_dst * d * 4, s);
+    return check_launch("gnnrec_sddmm_cos_backward_grouped_f32");
+  }
+  GNNREC_REQUIRE(src && dst && Hs && Hd && grad && workspace,
+                 "gnnrec_sddmm_cos_backward_grouped_f32: null pointer");
+  const size_t need = gnnrec_sddmm_cos_backward_grouped_workspace_bytes(n_groups, K, n_src,
+                                                                        n_dst, d);
+  GNNREC_REQUIRE(workspace_bytes >= need,
+                 "gnnrec_sddmm_cos_backward_grouped_f32: workspace %zu < %zu bytes",
+                 workspace_bytes, need);
+  char* p = static_cast<char*>(workspace);
+  float* inv_s = reinterpret_cast<float*>(p);
+  p += align_up((size_t)n_src * 4);
+  float* inv_d = reinterpret_cast<float*>(p);
+  p += align_up((size_t)n_dst * 4);
+  auto norm_grid = [](int64_t n) {
+    int64_t b = (n + 3) / 4;
+    return (unsigned)(b < 1 ? 1 : (b > 256 * 16 ? 256 * 16 : b));
+  };
+  if (gHs && n_dst)
+    hipLaunchKernelGGL(row_inv_norm_kernel, dim3(norm_grid(n_dst)), dim3(256), 0, s, Hd, ldd,
+                       n_dst, d, inv_d);
+  if (gHd && n_src)
+    hipLaunchKernelGGL(row_inv_norm_kernel, dim3(norm_grid(n_src)), dim3(256), 0, s, Hs, lds,
+                       n_src, d, inv_s);
+  int rc;
+  if (gHs) {
+    rc = run_grouped_src_side(src, dst, grad, n_groups, K, Hs, lds, n_src, Hd, ldd, inv_d, d,
+                              gHs, p, s);
+    if (rc != GNNREC_OK) return rc;
+  }
+  if (gHd) {
+    rc = run_side(dst, src, grad, E, Hd, ldd, n_dst, Hs, lds, inv_s, d, gHd, p, s);
+    if (rc != GNNREC_OK) return rc;
+  }
+  return check_launch("gnnrec_sddmm_cos_backward_grouped_f32");
 }

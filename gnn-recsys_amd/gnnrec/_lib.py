@@ -133,6 +133,10 @@ SIGNATURES = {
                                       _P]),
     "gnnrec_sum_scaled_f32": (_INT, [_P, _I64, _F32, _P, _P]),
     "gnnrec_sddmm_cos_backward_workspace_bytes": (_U64, [_I64, _I64, _I64, _I64]),
+    "gnnrec_sddmm_cos_backward_grouped_workspace_bytes": (_U64, [_I64, _I64, _I64, _I64, _I64]),
+    "gnnrec_sddmm_cos_backward_grouped_f32": (_INT, [_P, _P, _I64, _I64, _P, _I64, _I64, _P,
+                                                     _I64, _I64, _I64, _P, _P, _P, _P, _U64,
+                                                     _P]),
     "gnnrec_sddmm_cos_backward_f32": (_INT, [_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64,
                                              _P, _P, _P, _P, _U64, _P]),
 }

@@ -462,6 +462,7 @@ class CosinePairFn(torch.autograd.Function):
             a, b = out[:src_p.numel()], out[src_p.numel():]
         ctx.save_for_backward(hs, hd, src_p, dst_p, src_n, dst_n)
         ctx.n_pos = src_p.numel()
+        ctx.K = K
         return a, b
 
     @staticmethod
@@ -484,8 +485,11 @@ class CosinePairFn(torch.autograd.Function):
                     part.zero_()
                 else:
                     part.copy_(gp.reshape(-1))
+        # the grouped layout (each negative's source its positive's): the source side
+        # sorts only the positives' keys
+        K = ctx.K if ctx.K is not None else 0
         ga, gb = ops.sddmm_cos_backward(src, dst, hs.contiguous(), hd.contiguous(), g,
-                                        need[0], need[1])
+                                        need[0], need[1], groups=n_pos if K else 0, K=K)
         return ga, gb, None, None, None, None, None
 
 

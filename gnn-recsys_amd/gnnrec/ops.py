@@ -1078,9 +1078,13 @@ def sddmm_cos_grouped(src_g: torch.Tensor, first: Optional[torch.Tensor], K: int
 
 
 def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, Hd: torch.Tensor,
-                       grad: torch.Tensor, need_src: bool = True, need_dst: bool = True):
+                       grad: torch.Tensor, need_src: bool = True, need_dst: bool = True,
+                       groups: int = 0, K: int = 0):
     """f2: gradients of sddmm_cos w.r.t. Hs and Hd given dL/dcos [E] -> (gHs|None, gHd|None),
-    one library call (key sort, planned weighted gather, normalisation Jacobian)."""
+    one library call (key sort, planned weighted gather, normalisation Jacobian).
+    groups > 0: the edges are [groups positives | groups x K negatives] with each negative's
+    source its positive's (negative_sampler.Uniform): the source side sorts only the group
+    keys (gnnrec_sddmm_cos_backward_grouped_f32)."""
     T = _T()
     _dev(src, "src", torch.int64)
     _dev(dst, "dst", torch.int64)
@@ -1095,10 +1099,14 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
     n_s, n_d = Hs.shape[0], Hd.shape[0]
     gHs = torch.empty((n_s, d), dtype=torch.float32, device=Hs.device) if need_src else None
     gHd = torch.empty((n_d, d), dtype=torch.float32, device=Hs.device) if need_dst else None
-    nbytes = int(T.sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d))
+    if groups and not (groups * (K + 1) == E and d % 4 == 0 and d <= 256 and
+                       Hs.stride(0) % 4 == 0 and Hd.stride(0) % 4 == 0 and
+                       Hs.data_ptr() % 16 == 0 and Hd.data_ptr() % 16 == 0):
+        groups = K = 0  # the layout or the rows do not fit the grouped form
+    nbytes = int(T.sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d, groups, K))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=Hs.device)
     T.sddmm_cos_backward(src.contiguous(), dst.contiguous(), Hs, Hd, grad.contiguous(), gHs, gHd,
-                         ws)
+                         ws, groups, K)
     return gHs, gHd
 
 

@@ -748,6 +748,22 @@ int gnnrec_sddmm_cos_backward_f32(const int64_t* src, const int64_t* dst, int64_
                                   int64_t ldd, int64_t n_dst, int64_t d, const float* grad,
                                   float* gHs, float* gHd, void* workspace,
                                   size_t workspace_bytes, void* stream);
+/* The same for negative_sampler.Uniform(K)'s pair graphs (src/sampling.py:163-165): the
+ * n_edges = n_groups (K + 1) edges are laid out [n_groups positives | n_groups x K
+ * negatives] with src[n_groups + g K + j] = src[g], so the source side sorts only the group
+ * keys: one wave per 64-edge chunk of a group gathers its weighted rows into a partial, and
+ * each source row sums its groups' chunks in key order before the normalisation epilogue
+ * (no sort of the n_edges).  The destination side is the call above's.  Sums in a fixed
+ * order; d % 4 == 0, d <= 256, 16-byte aligned rows. */
+size_t gnnrec_sddmm_cos_backward_grouped_workspace_bytes(int64_t n_groups, int64_t K,
+                                                         int64_t n_src, int64_t n_dst, int64_t d);
+int gnnrec_sddmm_cos_backward_grouped_f32(const int64_t* src, const int64_t* dst,
+                                          int64_t n_groups, int64_t K, const float* Hs,
+                                          int64_t lds, int64_t n_src, const float* Hd,
+                                          int64_t ldd, int64_t n_dst, int64_t d,
+                                          const float* grad, float* gHs, float* gHd,
+                                          void* workspace, size_t workspace_bytes,
+                                          void* stream);
 
 /* ---- synthetic graph generator (benchmark shapes; no reference analogue) --
  * For e in [e0, e0+n): u[e-e0] = h(seed, e, 0) mod n_u, i[e-e0] = item(h(seed, e, 1)),

@@ -1723,14 +1723,17 @@ def test_sddmm_cos_grouped_bitwise_equals_per_edge_and_oracle(d):
         np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
 
 
-def test_cosine_pair_head_grouped_path_forward_and_gradients():
+@pytest.mark.parametrize("K,d", [(50, 64), (200, 128), (10, 40)])
+def test_cosine_pair_head_grouped_path_forward_and_gradients(K, d):
     """CosinePrediction.pair on a negative graph marked by the loader (src_repeats_pos = K)
-    takes the grouped launch: the same scores and the same gradients as the unmarked graph."""
+    takes the grouped launch: the same scores and item gradients as the unmarked graph, and
+    user gradients from the grouped backward (only the positives' keys sorted; 64-edge
+    chunks summed per user — repeated users included) within fp32 reassociation."""
     from gnnrec.graph import PairGraph
     from gnnrec.nn import CosinePrediction
     rng = np.random.default_rng(1)
     ce = ("user", "buys", "item")
-    K, P = 50, 40
+    P = 40
     ps, pd = rng.integers(0, 30, P), rng.integers(0, 60, P)
     nd = rng.integers(0, 60, P * K)
     nodes = {"user": _t(np.arange(30)), "item": _t(np.arange(60))}
@@ -1741,14 +1744,16 @@ def test_cosine_pair_head_grouped_path_forward_and_gradients():
     head = CosinePrediction()
     res = []
     for neg_g in (neg_plain, neg_marked):
-        h = {"user": _t(np.random.default_rng(2).standard_normal((30, 64)).astype(np.float32)),
-             "item": _t(np.random.default_rng(3).standard_normal((60, 64)).astype(np.float32))}
+        h = {"user": _t(np.random.default_rng(2).standard_normal((30, d)).astype(np.float32)),
+             "item": _t(np.random.default_rng(3).standard_normal((60, d)).astype(np.float32))}
         for t in h.values():
             t.requires_grad_(True)
         a, b = head.pair(pos_g, neg_g, h)
         (a[ce].sum() * 0.3 + (b[ce] ** 2).sum()).backward()
         with torch.no_grad():
             c, e = head.pair(pos_g, neg_g, {k: v.detach() for k, v in h.items()})
-        res.append((a[ce].detach(), b[ce].detach(), c[ce], e[ce], h["user"].grad, h["item"].grad))
-    for x, y in zip(*res):
+        res.append((a[ce].detach(), b[ce].detach(), c[ce], e[ce], h["item"].grad, h["user"].grad))
+    for x, y in zip(res[0][:5], res[1][:5]):
         assert torch.equal(x, y)
+    np.testing.assert_allclose(res[1][5].cpu().numpy(), res[0][5].cpu().numpy(), rtol=1e-5,
+                               atol=1e-6)

@@ -32,6 +32,9 @@ RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_t
            "gnnrec_spmm_project_f32": "spmm_project", "gnnrec_sddmm_cos_f32": "sddmm_cos",
            "gnnrec_spmm_project2_f32": "spmm_project2", "gnnrec_spmm_pair_f32": "spmm_pair",
            "gnnrec_sddmm_cos_backward_f32": "sddmm_cos_backward",
+           "gnnrec_sddmm_cos_backward_grouped_f32": "sddmm_cos_backward",
+           "gnnrec_sddmm_cos_backward_grouped_workspace_bytes":
+               "sddmm_cos_backward_workspace_bytes",
            "gnnrec_sddmm_cos_grouped_f32": "sddmm_cos_grouped",
            "gnnrec_edge_mlp_f32": "edge_mlp", "gnnrec_act_backward_f32": "act_backward",
            "gnnrec_act_backward_normed_f32": "act_backward_normed",
