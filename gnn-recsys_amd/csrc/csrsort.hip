@@ -2,20 +2,23 @@
 //
 // Reference: create_graph / dgl.heterograph (src/builder.py:377-383) and the reverse
 // relations of src/utils_data.py:204-238, whose in-CSR DGL builds when update_all first
-// runs; the CSR keeps the edges of a row in edge-id order.  Here: per pass of 8 key bits
-// (3 passes for up to 16M rows),
+// runs; the CSR keeps the edges of a row in edge-id order.  Here: per pass of DB key bits
+// (radix_plan: the fewest passes of at most 10 bits, then the narrowest digit that many
+// passes need — 17-bit keys in 2 passes of 9, 20-bit in 2 of 10, 24-bit in 3 of 8),
 //   radix_hist    one 256-thread block per 2048-edge tile counts the tile's digits,
-//                 stored digit-major [256][tiles];
+//                 stored digit-major [2^DB][tiles];
 //   scan          exclusive scan of that table (gnnrec_exclusive_scan_i32): the first
 //                 output position of every (digit, tile);
-//   radix_scatter each wave ranks its 512 edges, 64 at a time, by digit: 8 ballots give
+//   radix_scatter each wave ranks its 512 edges, 64 at a time, by digit: DB ballots give
 //                 the lanes holding the same digit, mbcnt the rank among them, and an LDS
 //                 counter per (wave, digit) the edges of earlier rounds — so equal digits
 //                 keep their input order (stable), then writes key and value at
 //                 tile offset + earlier waves' counts + rank.
 // The final pass writes the CSR directly (indices = src[e], eids = e), and the row
 // pointers come from the sorted keys' run boundaries.  Bytes per edge per pass: 4 (hist)
-// + 8 read + 8 written (scatter); C4's 500M-edge relation sorts in 3 passes.
+// + 8 read + 8 written (scatter) + 12 · 2^DB / 2048 for the digit table and its scan;
+// C4's 500M-edge relation sorts in 3 passes.  The sorted order is unique (a stable sort by
+// key), so the digit width changes launches and bytes, never the result.
 #include "common.hpp"
 #include "csrsort.hpp"
 
@@ -25,15 +28,22 @@ namespace {
 constexpr int kRT = 256;                 // threads per tile block
 constexpr int kRRounds = 8;              // 64-edge rounds per wave
 constexpr int kRTile = kRT * kRRounds;   // edges per tile
-constexpr int kDigits = 256;
+constexpr int kMaxDigitBits = 10;
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
-inline int key_passes(int64_t n_rows) {
+struct RadixPlan {
+  int passes, bits;  // passes of `bits` key bits each
+};
+inline RadixPlan radix_plan(int64_t n_rows) {
   int b = 1;
   while (b < 32 && (int64_t(1) << b) < n_rows) ++b;
-  return (b + 7) / 8;
+  RadixPlan r;
+  r.passes = (b + kMaxDigitBits - 1) / kMaxDigitBits;
+  r.bits = (b + r.passes - 1) / r.passes;
+  if (r.bits < 8) r.bits = 8;
+  return r;
 }
 
 inline unsigned tile_grid(int64_t n_tiles) {
@@ -41,39 +51,44 @@ inline unsigned tile_grid(int64_t n_tiles) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
-template <class K>
+template <class K, int DB>
 __global__ __launch_bounds__(kRT) void radix_hist_kernel(const K* __restrict__ keys, int64_t E,
                                                          int shift, int64_t n_tiles,
                                                          int32_t* __restrict__ hist) {
-  __shared__ int cnt[kDigits];
+  constexpr int ND = 1 << DB;
+  __shared__ int cnt[ND];
   const int tid = threadIdx.x;
   for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-    cnt[tid] = 0;
+#pragma unroll
+    for (int d = tid; d < ND; d += kRT) cnt[d] = 0;
     __syncthreads();
     const int64_t base = t * kRTile;
 #pragma unroll
     for (int j = 0; j < kRRounds; ++j) {
       const int64_t i = base + j * kRT + tid;
-      if (i < E) atomicAdd(&cnt[((uint32_t)keys[i] >> shift) & (kDigits - 1)], 1);
+      if (i < E) atomicAdd(&cnt[((uint32_t)keys[i] >> shift) & (ND - 1)], 1);
     }
     __syncthreads();
-    hist[(int64_t)tid * n_tiles + t] = cnt[tid];
+#pragma unroll
+    for (int d = tid; d < ND; d += kRT) hist[(int64_t)d * n_tiles + t] = cnt[d];
     __syncthreads();
   }
 }
 
 // MODE 0: keys_out / vals_out; MODE 1: keys_out + the CSR gather (idx_out, eid_out)
-template <class K, bool VIN, int MODE>
+// (positions fit int32: E < 2^31, radix_sort_rows)
+template <class K, bool VIN, int MODE, int DB>
 __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
     const K* __restrict__ keys, const int32_t* __restrict__ vals, int64_t E, int shift,
     int64_t n_tiles, const int64_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out, const int64_t* __restrict__ src,
     int32_t* __restrict__ idx_out, int64_t* __restrict__ eid_out) {
-  __shared__ int cnt[kRT / kWave][kDigits];
-  __shared__ int64_t pos[kRT / kWave][kDigits];
+  constexpr int ND = 1 << DB;
+  // per (wave, digit): the wave's running count, then (in place) its first output position
+  __shared__ int cnt[kRT / kWave][ND];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
   for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-    for (int i = tid; i < (kRT / kWave) * kDigits; i += kRT) cnt[i / kDigits][i % kDigits] = 0;
+    for (int i = tid; i < (kRT / kWave) * ND; i += kRT) cnt[i / ND][i % ND] = 0;
     __syncthreads();
     const int64_t base = t * kRTile + (int64_t)w * (kRRounds * kWave);
     uint32_t kk[kRRounds];
@@ -86,10 +101,10 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
       const uint32_t k = act ? (uint32_t)keys[i] : 0u;
       kk[j] = k;
       vv[j] = act ? (VIN ? vals[i] : (int32_t)i) : 0;
-      const uint32_t d = (k >> shift) & (kDigits - 1);
+      const uint32_t d = (k >> shift) & (ND - 1);
       uint64_t peers = __ballot(act);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
+      for (int b = 0; b < DB; ++b) {
         const uint64_t bb = __ballot((d >> b) & 1u);
         peers &= ((d >> b) & 1u) ? bb : ~bb;
       }
@@ -102,13 +117,14 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
       dr[j] = (d << 16) | (uint32_t)(old + (int)r);
     }
     __syncthreads();
-    {  // per digit: the tile's first position, then each wave's after the earlier waves'
-      const int d = tid;
-      int64_t run = offs[(int64_t)d * n_tiles + t];
+    // per digit: the tile's first position, then each wave's after the earlier waves'
+    for (int d = tid; d < ND; d += kRT) {
+      int run = (int)offs[(int64_t)d * n_tiles + t];
 #pragma unroll
       for (int ww = 0; ww < kRT / kWave; ++ww) {
-        pos[ww][d] = run;
-        run += cnt[ww][d];
+        const int c = cnt[ww][d];
+        cnt[ww][d] = run;
+        run += c;
       }
     }
     __syncthreads();
@@ -116,7 +132,7 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
     for (int j = 0; j < kRRounds; ++j) {
       const int64_t i = base + j * kWave + lane;
       if (i >= E) continue;
-      const int64_t p = pos[w][dr[j] >> 16] + (dr[j] & 0xffff);
+      const int64_t p = (int64_t)cnt[w][dr[j] >> 16] + (dr[j] & 0xffff);
       if (keys_out) keys_out[p] = kk[j];
       if (MODE == 0) {
         vals_out[p] = vv[j];
@@ -167,20 +183,20 @@ inline unsigned flat_grid(int64_t n) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
-template <class K>
+template <class K, int DB>
 void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64_t n_tiles,
                  int32_t* hist, int64_t* offs, void* scan_ws, uint32_t* k_out, int32_t* v_out,
                  const CsrGather* g, hipStream_t s) {
   const unsigned grid = tile_grid(n_tiles);
-  hipLaunchKernelGGL(radix_hist_kernel<K>, dim3(grid), dim3(kRT), 0, s, keys, E, shift, n_tiles,
-                     hist);
-  (void)gnnrec_exclusive_scan_i32(hist, (int64_t)kDigits * n_tiles, offs, scan_ws, s);
+  hipLaunchKernelGGL((radix_hist_kernel<K, DB>), dim3(grid), dim3(kRT), 0, s, keys, E, shift,
+                     n_tiles, hist);
+  (void)gnnrec_exclusive_scan_i32(hist, ((int64_t)1 << DB) * n_tiles, offs, scan_ws, s);
   const int64_t* src = g ? g->src : nullptr;
   int32_t* idx = g ? g->idx_out : nullptr;
   int64_t* eid = g ? g->eid_out : nullptr;
-#define GNNREC_SCATTER(VIN, MODE)                                                            \
-  hipLaunchKernelGGL((radix_scatter_kernel<K, VIN, MODE>), dim3(grid), dim3(kRT), 0, s, keys, \
-                     vals, E, shift, n_tiles, offs, k_out, v_out, src, idx, eid)
+#define GNNREC_SCATTER(VIN, MODE)                                                        \
+  hipLaunchKernelGGL((radix_scatter_kernel<K, VIN, MODE, DB>), dim3(grid), dim3(kRT), 0, s, \
+                     keys, vals, E, shift, n_tiles, offs, k_out, v_out, src, idx, eid)
   if (g) {
     if (vals) GNNREC_SCATTER(true, 1);
     else GNNREC_SCATTER(false, 1);
@@ -191,13 +207,24 @@ void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64
 #undef GNNREC_SCATTER
 }
 
+template <class K>
+void launch_pass_bits(int bits, const K* keys, const int32_t* vals, int64_t E, int shift,
+                      int64_t n_tiles, int32_t* hist, int64_t* offs, void* scan_ws,
+                      uint32_t* k_out, int32_t* v_out, const CsrGather* g, hipStream_t s) {
+  if (bits == 8)
+    launch_pass<K, 8>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+  else if (bits == 9)
+    launch_pass<K, 9>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+  else
+    launch_pass<K, 10>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+}
+
 }  // namespace
 
 size_t radix_ws_bytes(int64_t E, int64_t n_rows) {
-  (void)n_rows;
   if (E <= 0) return 0;
   const int64_t n_tiles = (E + kRTile - 1) / kRTile;
-  const int64_t n_hist = kDigits * n_tiles;
+  const int64_t n_hist = ((int64_t)1 << radix_plan(n_rows).bits) * n_tiles;
   return 4 * align_up((size_t)E * 4)                            // two (key, value) buffers
          + align_up((size_t)n_hist * 4)                         // per-tile digit counts
          + align_up((size_t)(n_hist + 1) * 8)                   // their scan
@@ -220,8 +247,9 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
                  "radix sort: null pointer");
   GNNREC_REQUIRE(ws_bytes >= radix_ws_bytes(E, n_rows), "radix sort: workspace %zu < %zu bytes",
                  ws_bytes, radix_ws_bytes(E, n_rows));
+  const RadixPlan plan = radix_plan(n_rows);
   const int64_t n_tiles = (E + kRTile - 1) / kRTile;
-  const int64_t n_hist = kDigits * n_tiles;
+  const int64_t n_hist = ((int64_t)1 << plan.bits) * n_tiles;
   char* p = static_cast<char*>(ws);
   const size_t slot = align_up((size_t)E * 4);
   uint32_t* kb[2] = {reinterpret_cast<uint32_t*>(p), reinterpret_cast<uint32_t*>(p + slot)};
@@ -230,22 +258,22 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
   int32_t* hist = reinterpret_cast<int32_t*>(p + 4 * slot);
   int64_t* offs = reinterpret_cast<int64_t*>(p + 4 * slot + align_up((size_t)n_hist * 4));
   void* scan_ws = p + 4 * slot + align_up((size_t)n_hist * 4) + align_up((size_t)(n_hist + 1) * 8);
-  const int passes = key_passes(n_rows);
-  for (int ps = 0; ps < passes; ++ps) {
-    const bool last = ps == passes - 1;
+  const int bits = plan.bits;
+  for (int ps = 0; ps < plan.passes; ++ps) {
+    const bool last = ps == plan.passes - 1;
     uint32_t* k_out = last ? keys_out : kb[ps & 1];
     int32_t* v_out = last ? vals_out : vb[ps & 1];
     const CsrGather* gg = last ? g : nullptr;
     if (ps == 0) {
       if (keys64)
-        launch_pass(static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles, hist, offs,
-                    scan_ws, k_out, v_out, gg, s);
+        launch_pass_bits(bits, static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles,
+                         hist, offs, scan_ws, k_out, v_out, gg, s);
       else
-        launch_pass(static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles, hist, offs,
-                    scan_ws, k_out, v_out, gg, s);
+        launch_pass_bits(bits, static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles,
+                         hist, offs, scan_ws, k_out, v_out, gg, s);
     } else {
-      launch_pass(kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, 8 * ps, n_tiles, hist, offs, scan_ws,
-                  k_out, v_out, gg, s);
+      launch_pass_bits(bits, (const uint32_t*)kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, bits * ps,
+                       n_tiles, hist, offs, scan_ws, k_out, v_out, gg, s);
     }
   }
   if (row_ptr)

@@ -107,17 +107,22 @@ __global__ __launch_bounds__(256) void keys_to_i32_kernel(const int64_t* __restr
     k32[i] = (int32_t)k64[i];
 }
 
-// edges in row-grouped order: other endpoint (int32) and weight g_e · inv_other
+// edges in row-grouped order: other endpoint (int32) and weight g_e · inv_other.
+// gK > 0: the grouped layout [G positives | G x gK negatives] (run_grouped_src_side), where
+// edge e's other endpoint is its group's positive's, other[e < G ? e : (e - G) / gK] — a
+// read from the G-entry head of the array (cache-resident) instead of a random one over E
 __global__ __launch_bounds__(256) void cos_permute_kernel(const int32_t* __restrict__ perm,
                                                           const int64_t* __restrict__ other,
                                                           const float* __restrict__ g,
                                                           const float* __restrict__ inv_other,
-                                                          int64_t E, int32_t* __restrict__ ix,
+                                                          int64_t E, uint32_t gG, uint32_t gK,
+                                                          int32_t* __restrict__ ix,
                                                           float* __restrict__ w) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < E; k += stride) {
     const int32_t e = perm[k];
-    const int64_t o = other[e];
+    const uint32_t ue = (uint32_t)e;
+    const int64_t o = gK == 0 ? other[e] : other[ue < gG ? ue : (ue - gG) / gK];
     ix[k] = (int32_t)o;
     w[k] = g[e] * inv_other[o];
   }
@@ -179,9 +184,11 @@ size_t side_bytes(int64_t E, int64_t n_rows, int64_t d) {
   return b;
 }
 
+// gG, gK: the grouped layout's group count and negatives per group (cos_permute_kernel), or 0
 int run_side(const int64_t* keys, const int64_t* other, const float* g, int64_t E,
              const float* T, int64_t ldt, int64_t n_rows, const float* O, int64_t ldo,
-             const float* inv_other, int64_t d, float* gT, char* p, hipStream_t s) {
+             const float* inv_other, int64_t d, float* gT, char* p, hipStream_t s,
+             int64_t gG = 0, int64_t gK = 0) {
   const CosSide c = side_caps(E, n_rows);
   int32_t* k32 = reinterpret_cast<int32_t*>(p);
   p += align_up((size_t)E * 4);
@@ -210,7 +217,7 @@ int run_side(const int64_t* keys, const int64_t* other, const float* g, int64_t 
   int rc = gnnrec_csr_from_keys(k32, E, n_rows, sort_ws, sort_bytes, indptr, perm, s);
   if (rc != GNNREC_OK) return rc;
   hipLaunchKernelGGL(cos_permute_kernel, dim3(flat_grid(E)), dim3(256), 0, s, perm, other, g,
-                     inv_other, E, ix, w);
+                     inv_other, E, (uint32_t)gG, (uint32_t)gK, ix, w);
   if (c.cap_h > 0) {
     rc = gnnrec_spmm_plan_build(indptr, n_rows, kCosSplit, c.cap_h, c.cap_c, plan, s);
     if (rc != GNNREC_OK) return rc;
@@ -545,7 +552,9 @@ extern "C" int gnnrec_sddmm_cos_backward_grouped_f32(const int64_t* src, const i
     if (rc != GNNREC_OK) return rc;
   }
   if (gHd) {
-    rc = run_side(dst, src, grad, E, Hd, ldd, n_dst, Hs, lds, inv_s, d, gHd, p, s);
+    // (K == 0: every edge a positive, the per-edge read)
+    rc = run_side(dst, src, grad, E, Hd, ldd, n_dst, Hs, lds, inv_s, d, gHd, p, s, n_groups,
+                  K);
     if (rc != GNNREC_OK) return rc;
   }
   return check_launch("gnnrec_sddmm_cos_backward_grouped_f32");
