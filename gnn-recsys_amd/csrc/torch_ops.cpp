@@ -496,8 +496,11 @@ void sddmm_cos_backward(const Tensor& src, const Tensor& dst, const Tensor& Hs, 
   dev(grad, "grad", at::kFloat);
   dev(gHs, "gHs", at::kFloat);
   dev(gHd, "gHd", at::kFloat);
-  const int64_t E = src.numel(), d = Hs.size(1);
-  TORCH_CHECK_VALUE(dst.numel() == E && grad.numel() == E, "src/dst/grad length mismatch");
+  // grouped (groups > 0): src may hold only the positives' sources (the only entries read)
+  const int64_t E = dst.numel(), d = Hs.size(1);
+  TORCH_CHECK_VALUE((src.numel() == E || (groups > 0 && src.numel() == groups)) &&
+                        grad.numel() == E,
+                    "src/dst/grad length mismatch");
   TORCH_CHECK_VALUE(Hd.size(1) == d, "endpoint feature sizes differ");
   TORCH_CHECK_VALUE(groups <= 0 || (K >= 0 && groups * (K + 1) == E),
                     "sddmm_cos_backward: groups x (K + 1) must equal the edge count");

@@ -52,16 +52,32 @@ __global__ __launch_bounds__(256) void margin_loss_kernel(
                          : reinterpret_cast<const float*>(rec)[e];
     const float inv_r = 1.f / r;
     float gsum = 0.f, row = 0.f;
-    for (int64_t k = lane; k < K; k += kWave) {
-      const int64_t i = e * K + k;
-      float x = neg[i] + delta - p;  // (neg + delta) - pos, the reference's order
-      if (mask) x = x - mask[i];
-      const bool on = x > 0.f;
-      // the reference divides the ReLU output by the recency (not a multiply by 1/r)
-      row += on ? (rec ? x / r : x) : 0.f;
-      const float gi = on ? inv_r : 0.f;
-      g_neg[i] = gi;
-      gsum += gi;
+    // a lane's negatives in its own order (k = lane, lane + 64, ...), their loads requested
+    // kMlU at a time: one wave per positive leaves few waves per CU, so a load per
+    // iteration left the launch latency-bound (18 µs for C2's 1024 x 2500)
+    constexpr int kMlU = 8;
+    for (int64_t k0 = lane; k0 < K; k0 += kMlU * kWave) {
+      float nv[kMlU], mv[kMlU];
+#pragma unroll
+      for (int u = 0; u < kMlU; ++u) {
+        const int64_t k = k0 + (int64_t)u * kWave;
+        nv[u] = k < K ? neg[e * K + k] : 0.f;
+        mv[u] = mask && k < K ? mask[e * K + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kMlU; ++u) {
+        const int64_t k = k0 + (int64_t)u * kWave;
+        if (k >= K) break;
+        const int64_t i = e * K + k;
+        float x = nv[u] + delta - p;  // (neg + delta) - pos, the reference's order
+        if (mask) x = x - mv[u];
+        const bool on = x > 0.f;
+        // the reference divides the ReLU output by the recency (not a multiply by 1/r)
+        row += on ? (rec ? x / r : x) : 0.f;
+        const float gi = on ? inv_r : 0.f;
+        g_neg[i] = gi;
+        gsum += gi;
+      }
     }
     gsum = wave_sum(gsum);
     if (lane == 0) g_pos[e] = -gsum;

@@ -472,14 +472,16 @@ class CosinePairFn(torch.autograd.Function):
         if not (need[0] or need[1]):
             return None, None, None, None, None, None, None
         # the positive and negative lists are usually one buffer already (the static batch
-        # head's compaction, MarginLossFn's gradient): a view then, no cat / copy launches
-        src, dst = _joined(src_p, src_n), _joined(dst_p, dst_n)
+        # head's compaction, MarginLossFn's gradient): a view then, no cat / copy launches.
+        # The grouped backward reads only the positives' sources.
+        src = src_p if ctx.K else _joined(src_p, src_n)
+        dst = _joined(dst_p, dst_n)
         n_pos = ctx.n_pos
         g = None
         if g_pos is not None and g_neg is not None:
             g = _joined(g_pos.reshape(-1), g_neg.reshape(-1))
         else:
-            g = torch.empty(src.numel(), dtype=torch.float32, device=src.device)
+            g = torch.empty(dst.numel(), dtype=torch.float32, device=dst.device)
             for part, gp in ((g[:n_pos], g_pos), (g[n_pos:], g_neg)):
                 if gp is None:
                     part.zero_()

@@ -1084,15 +1084,16 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
     one library call (key sort, planned weighted gather, normalisation Jacobian).
     groups > 0: the edges are [groups positives | groups x K negatives] with each negative's
     source its positive's (negative_sampler.Uniform): the source side sorts only the group
-    keys (gnnrec_sddmm_cos_backward_grouped_f32)."""
+    keys (gnnrec_sddmm_cos_backward_grouped_f32), and src may be the positives' sources
+    alone (groups entries; the only ones read)."""
     T = _T()
     _dev(src, "src", torch.int64)
     _dev(dst, "dst", torch.int64)
     _dev(Hs, "Hs", torch.float32)
     _dev(Hd, "Hd", torch.float32)
     _dev(grad, "grad", torch.float32)
-    E, d = src.numel(), Hs.shape[1]
-    if dst.numel() != E or grad.numel() != E:
+    E, d = dst.numel(), Hs.shape[1]
+    if not (src.numel() == E or (groups and src.numel() == groups)) or grad.numel() != E:
         raise ValueError("sddmm_cos_backward: src/dst/grad length mismatch")
     if Hd.shape[1] != d:
         raise ValueError("endpoint feature sizes differ")
@@ -1102,6 +1103,8 @@ def sddmm_cos_backward(src: torch.Tensor, dst: torch.Tensor, Hs: torch.Tensor, H
     if groups and not (groups * (K + 1) == E and d % 4 == 0 and d <= 256 and
                        Hs.stride(0) % 4 == 0 and Hd.stride(0) % 4 == 0 and
                        Hs.data_ptr() % 16 == 0 and Hd.data_ptr() % 16 == 0):
+        if groups and src.numel() == groups and groups * (K + 1) == E:
+            src = torch.cat([src, src.repeat_interleave(K)])  # the per-edge form's full list
         groups = K = 0  # the layout or the rows do not fit the grouped form
     nbytes = int(T.sddmm_cos_backward_workspace_bytes(E, n_s, n_d, d, groups, K))
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=Hs.device)

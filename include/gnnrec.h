@@ -753,8 +753,10 @@ int gnnrec_sddmm_cos_backward_f32(const int64_t* src, const int64_t* dst, int64_
  * negatives] with src[n_groups + g K + j] = src[g], so the source side sorts only the group
  * keys: one wave per 64-edge chunk of a group gathers its weighted rows into a partial, and
  * each source row sums its groups' chunks in key order before the normalisation epilogue
- * (no sort of the n_edges).  The destination side is the call above's.  Sums in a fixed
- * order; d % 4 == 0, d <= 256, 16-byte aligned rows. */
+ * (no sort of the n_edges).  The destination side is the call above's, each edge's source
+ * taken from its group's positive.  Only src[0, n_groups) is read: the negatives' entries
+ * may be absent (src = the positives' sources alone).  Sums in a fixed order; d % 4 == 0,
+ * d <= 256, 16-byte aligned rows. */
 size_t gnnrec_sddmm_cos_backward_grouped_workspace_bytes(int64_t n_groups, int64_t K,
                                                          int64_t n_src, int64_t n_dst, int64_t d);
 int gnnrec_sddmm_cos_backward_grouped_f32(const int64_t* src, const int64_t* dst,

@@ -1757,3 +1757,27 @@ def test_cosine_pair_head_grouped_path_forward_and_gradients(K, d):
         assert torch.equal(x, y)
     np.testing.assert_allclose(res[1][5].cpu().numpy(), res[0][5].cpu().numpy(), rtol=1e-5,
                                atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,d", [(300, 64), (7, 6)])
+def test_cos_backward_grouped_reads_only_the_positives_sources(K, d):
+    """The grouped cosine backward reads src only at the positives (each negative's source is
+    its group's positive's): passing the positives' sources alone gives the bits of the full
+    list — also where the rows do not fit the grouped form (d = 6: the per-edge fallback
+    expands the list)."""
+    from gnnrec import ops
+    rng = np.random.default_rng(5)
+    G, n_s, n_d = 64, 40, 500
+    ps = _t(rng.integers(0, n_s, G))
+    dst = _t(rng.integers(0, n_d, G * (K + 1)))
+    src_full = torch.cat([ps, ps.repeat_interleave(K)])
+    hs = _t(rng.standard_normal((n_s, d)).astype(np.float32))
+    hd = _t(rng.standard_normal((n_d, d)).astype(np.float32))
+    g = _t(rng.standard_normal(G * (K + 1)).astype(np.float32))
+    a = ops.sddmm_cos_backward(src_full, dst, hs, hd, g, groups=G, K=K)
+    b = ops.sddmm_cos_backward(ps, dst, hs, hd, g, groups=G, K=K)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    with pytest.raises((ValueError, RuntimeError)):
+        ops.sddmm_cos_backward(ps, dst, hs, hd, g)  # a short src needs the grouped layout
