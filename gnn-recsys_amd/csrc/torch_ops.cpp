@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <utility>
+#include <map>
 #include <vector>
 
 #include "gnnrec.h"
@@ -1992,6 +1993,17 @@ edge_batch_pairs(at::TensorList rel_src, at::TensorList rel_dst, at::IntArrayRef
       auto& dlist = side == &ps ? pd : nd;
       lists[dst_type[r]].push_back(&dlist[r]);
     }
+  // a relation's positive and negative local ids of one side are written into one buffer
+  // [positives | negatives]: the cosine backward then joins them as a view, not a cat
+  std::map<const Tensor*, Tensor> joined_out;
+  for (size_t r = 0; r < R; ++r)
+    for (auto side : {std::make_pair(&ps[r], &ns[r]), std::make_pair(&pd[r], &nd[r])}) {
+      const int64_t a = side.first->numel(), b = side.second->numel();
+      if (a == 0 || b == 0) continue;
+      const Tensor buf = at::empty({a + b}, opt);
+      joined_out[side.first] = buf.narrow(0, 0, a);
+      joined_out[side.second] = buf.narrow(0, a, b);
+    }
   std::vector<Tensor> rank(NT);
   for (size_t t = 0; t < NT; ++t) {
     Tensor pp = prefix_pos[t], mk = marks[t];
@@ -2009,7 +2021,8 @@ edge_batch_pairs(at::TensorList rel_src, at::TensorList rel_dst, at::IntArrayRef
     nodes[t] = at::empty({nn}, opt);
     if (nn) compact_marked(mk, rank[t], nodes[t]);
     for (Tensor* ids : lists[t]) {
-      Tensor loc = at::empty({ids->numel()}, opt);
+      const auto j = joined_out.find(ids);
+      Tensor loc = j != joined_out.end() ? j->second : at::empty({ids->numel()}, opt);
       relabel_ids(*ids, pp, rank[t], 0, loc);
       *ids = loc;  // the list entry becomes its local ids
     }

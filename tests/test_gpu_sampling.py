@@ -183,6 +183,7 @@ def test_fused_batch_head_matches_readable_form(K):
     pair graphs, node ids and blocks bit for bit as find_edges + negative_sampler.Uniform +
     _compact, batch after batch (the same generator draws in the same order)."""
     from gnnrec.graph import NID
+    from gnnrec.autograd import _joined
     from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
     g, _ = _graph()
 
@@ -203,6 +204,10 @@ def test_fused_batch_head_matches_readable_form(K):
                 rec[("pos",) + ce] = [t.cpu() for t in pos_g.all_edges(etype=ce)]
                 if K:
                     rec[("neg",) + ce] = [t.cpu() for t in neg_g.all_edges(etype=ce)]
+                    if fused:  # [positives | negatives] in one buffer per side: joined as a view
+                        for pt, nt_ in zip(pos_g.all_edges(etype=ce), neg_g.all_edges(etype=ce)):
+                            if pt.numel() and nt_.numel():
+                                assert _joined(pt, nt_).data_ptr() == pt.data_ptr(), ce
             rec["b0"] = {nt: blocks[0].srcdata[NID][nt].cpu() for nt in blocks[0].ntypes}
             out.append(rec)
         return out
