@@ -25,10 +25,13 @@ def _check(src, dst, n_dst, ref=None):
 
 @pytest.mark.parametrize("E,n_dst", [(0, 1), (0, 9), (1, 1), (5, 1), (5000, 7), (5000, 300),
                                      (2049, 70_000), (100_000, 255), (100_000, 256),
-                                     (100_000, 257), (300_000, 65_536), (300_000, 20_000_000)])
+                                     (100_000, 257), (300_000, 65_536), (300_000, 20_000_000),
+                                     (100_000, 1024), (100_000, 1025), (300_000, 262_145),
+                                     (300_000, 1 << 20), (300_000, (1 << 20) + 1)])
 def test_csr_build_matches_oracle(E, n_dst):
-    """every pass count (1-4 passes of 8 bits), tile tails (E not a multiple of 2048),
-    empty rows, one row, empty relations"""
+    """every digit plan of the radix sort (csrsort.hip radix_plan: 1 pass of 8-10 bits, 2 of
+    8 / 9 / 10, 3 of 8 / 9), tile tails (E not a multiple of 2048), empty rows, one row,
+    empty relations"""
     g = torch.Generator(device=DEV)
     g.manual_seed(E + n_dst)
     src = torch.randint(0, 1 << 31, (E,), device=DEV, generator=g)
