@@ -266,7 +266,8 @@ __global__ __launch_bounds__(256) void cos_bwd_chunk_kernel(
     const float* __restrict__ inv_d, const float* __restrict__ Hd, int64_t ldd, int d,
     int64_t G, int64_t K, int64_t chunks, float* __restrict__ part) {
   constexpr int NPW = kWave / LPR;  // edges per wave-instruction
-  constexpr int U = 8;              // edges in flight per lane group
+  constexpr int U = 16;             // edges in flight per lane group
+  static_assert(kCosBwdChunk <= kWave, "a chunk's edges fit one wave load");
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPR, gl = lane % LPR;
   const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -277,23 +278,34 @@ __global__ __launch_bounds__(256) void cos_bwd_chunk_kernel(
   const int64_t q0 = c * kCosBwdChunk;
   const int64_t q1 = q0 + kCosBwdChunk < K + 1 ? q0 + kCosBwdChunk : K + 1;
   auto edge_of = [&](int64_t q) { return q == 0 ? g : G + g * K + (q - 1); };
+  // the chunk's ids and weights g_e inv_t in one load per lane (lane l: edge q0 + l), so the
+  // gathers below wait on one id load, not one per step of U edges
+  int64_t my_t = 0;
+  float my_w = 0.f;
+  if (q0 + lane < q1) {
+    const int64_t e = edge_of(q0 + lane);
+    my_t = dst[e];
+    my_w = grad[e] * inv_d[my_t];
+  }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t qb = q0 + grp; qb < q1; qb += (int64_t)NPW * U) {
+  // lane group grp sums edges q0 + grp, q0 + grp + NPW, ... in increasing order
+  for (int qo = grp; qo < kCosBwdChunk && q0 + qo - grp < q1; qo += NPW * U) {
     float4 v[U];
     float w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t q = qb + (int64_t)u * NPW;
-      const bool ok = q < q1;
-      const int64_t e = edge_of(ok ? q : q0);
-      const int64_t t = dst[e];
-      w[u] = ok ? grad[e] * inv_d[t] : 0.f;
-      v[u] = cok ? *reinterpret_cast<const float4*>(Hd + t * ldd + col)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int slot = qo + u * NPW;  // this group's edge q0 + slot (uniform per group)
+      const int src_lane = slot < kWave ? slot : 0;
+      const int64_t t = __shfl(my_t, src_lane);
+      w[u] = __shfl(my_w, src_lane);
+      const bool ok = slot < kCosBwdChunk && q0 + slot < q1;
+      v[u] = cok && ok ? *reinterpret_cast<const float4*>(Hd + t * ldd + col)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (qb + (int64_t)u * NPW < q1) {
+      const int slot = qo + u * NPW;
+      if (slot < kCosBwdChunk && q0 + slot < q1) {
         acc.x += w[u] * v[u].x;
         acc.y += w[u] * v[u].y;
         acc.z += w[u] * v[u].z;
@@ -326,13 +338,24 @@ __global__ __launch_bounds__(256) void cos_bwd_combine_kernel(
     float4 Gv = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = indptr_g[r]; i < indptr_g[r + 1]; ++i) {
       const float* pg = part + (int64_t)perm_g[i] * chunks * d;
-      for (int64_t c = 0; c < chunks; ++c) {
-        if (cok) {
-          const float4 x = *reinterpret_cast<const float4*>(pg + c * d + col);
-          Gv.x += x.x;
-          Gv.y += x.y;
-          Gv.z += x.z;
-          Gv.w += x.w;
+      // the group's chunk partials in chunk order, their loads requested 8 at a time (one
+      // per step left ~40 dependent loads per group: 65 µs for C2's K = 2500 head)
+      constexpr int CU = 8;
+      for (int64_t c0 = 0; c0 < chunks; c0 += CU) {
+        float4 x[CU];
+#pragma unroll
+        for (int u = 0; u < CU; ++u)
+          x[u] = cok && c0 + u < chunks
+                     ? *reinterpret_cast<const float4*>(pg + (c0 + u) * d + col)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < CU; ++u) {
+          if (cok && c0 + u < chunks) {
+            Gv.x += x[u].x;
+            Gv.y += x[u].y;
+            Gv.z += x[u].z;
+            Gv.w += x[u].w;
+          }
         }
       }
     }
