@@ -74,6 +74,11 @@ def parse(argv=None):
                     help="committed one-GPU output digests a P > 1 run compares its bits with")
     ap.add_argument("--record-digest", default=None, metavar="PATH",
                     help="(one GPU) add this run's output digest to the digest file PATH")
+    ap.add_argument("--allgather", choices=["auto", "rccl", "a2a"], default="auto",
+                    help="P > 1: the item tables' all-gather as RCCL's all-gather or as an "
+                         "all-to-all of the own block (GNNREC_ALLGATHER); auto: after the "
+                         "warm-up, replay the pass's all-gathers both ways and keep the faster "
+                         "(the outputs are the same bits either way)")
     ap.add_argument("--pg-timeout", type=float, default=300.0,
                     help="process-group timeout (s): a stuck collective ends the run, named")
     return ap.parse_args(argv) if argv is None else ap.parse_known_args(argv)[0]
@@ -617,6 +622,10 @@ def main():
         # (no per-collective stderr writes inside the measurement) and only the heartbeat
         # says where a stalled rank is
         runner.ex, runner.progress = ex, None
+    ag_choice = None
+    if world > 1:
+        hb.enter("all-gather form")
+        ag_choice = choose_allgather(args, runner, ex, feats, dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -745,6 +754,8 @@ def main():
         if world > 1:
             cfg["bitwise_vs_p1"] = bitwise
             cfg["bitwise_vs_p1_src"] = digest_src
+        if ag_choice is not None:
+            cfg["all_gather_choice"] = ag_choice
         if diag is not None:
             cfg.update(diag)
         rec = {
@@ -788,6 +799,12 @@ def minibatch_step(dev, warmup: int = 5):
     out["cosine_frac"] = roof.get("cosine", {}).get("frac")
     out["edge_mlp_mfma_frac"] = roof.get("edge_mlp", {}).get("mfma_frac")
     for K, steps in ((10, 100), (2500, 40)):
+        caps = "auto" if K > 100 else "provable"
+        # the eager and captured runs consume the SAME batches (same seeds, same warm-up
+        # count: the captured loader's learned-capacity batches and the step's own warm-up),
+        # so their per-step losses compare step for step
+        W = _captured_warmup(warmup, caps)
+        eager_losses = None
         for nw in (2, 0):
             torch.manual_seed(0)
             model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True,
@@ -813,27 +830,53 @@ def minibatch_step(dev, warmup: int = 5):
                 opt.step()
                 return loss
 
-            for _ in range(warmup):
+            l1 = step().detach()  # batch 1: both runs from the same initial weights
+            for _ in range(W - 1):
                 step()
             torch.cuda.synchronize()
+            losses = []
             t0 = time.perf_counter()
             for _ in range(steps):
-                loss = step()
+                losses.append(step().detach())  # device scalars: no sync in the loop
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / steps * 1e3
+            losses = torch.stack([l1] + losses).double().cpu()
             out[f"K{K}_num_workers{nw}"] = {"ms_per_step": round(ms, 3), "steps": steps,
+                                            "warmup_batches": W,
                                             "pos_edges_per_s": round(1024 / ms * 1e3),
-                                            "loss": float(loss.detach())}
+                                            "loss": float(losses[-1]),
+                                            "loss_first": float(losses[1]),
+                                            "loss_batch1": float(losses[0])}
+            if eager_losses is None:
+                eager_losses = losses
             del it, el
         try:
             # K = 2500: the provable capacities pad the first block's 7.3M sampled edges to
             # 11M (every user a potential source); capacities learned from the first batches
             # (static_caps='auto') hold them within 10 % and replay 3.8 -> 3.5 ms per step
-            out[f"K{K}_num_workers2_captured"] = captured_step(
-                g, dev, K, steps, warmup, caps="auto" if K > 100 else "provable")
+            cap = captured_step(g, dev, K, steps, warmup, caps=caps)
+            cl = cap.pop("_losses", None)
+            if cl is not None and eager_losses is not None:
+                el_ = eager_losses[[0, 1, -1]]
+                rel = (cl - el_).abs() / el_.abs().clamp_min(1e-30)
+                # the same batches, step for step: fp32 rounding apart (the captured step
+                # folds the NodeEmbedding and sums over padding rows), which training carries
+                # forward — batch 1 (same initial weights) is the tight comparison; at K = 10
+                # the eager run does not fold (below FOLD_MIN_SRC_ROWS), so its trajectory
+                # drifts from the captured one by Adam-amplified rounding
+                cap["loss_rel_diff_vs_eager"] = {"batch1": float(rel[0]), "first": float(rel[1]),
+                                                 "last": float(rel[2])}
+            out[f"K{K}_num_workers2_captured"] = cap
         except Exception as exc:  # a secondary measurement never masks the others
             out[f"K{K}_num_workers2_captured"] = {"error": repr(exc)}
     return out
+
+
+def _captured_warmup(warmup: int, caps: str) -> int:
+    """Batches a captured run consumes before its timed steps: the step's warm-up and
+    capture (at least 3) plus, with learned capacities, the loader's exact learning batches."""
+    from gnnrec.sampling import EdgeDataLoader
+    return max(warmup, 3) + (EdgeDataLoader.STATIC_LEARN if caps == "auto" else 0)
 
 
 def captured_step(g, dev, K: int, steps: int, warmup: int, caps: str = "provable"):
@@ -841,7 +884,7 @@ def captured_step(g, dev, K: int, steps: int, warmup: int, caps: str = "provable
     hipGraph and replayed per batch (gnnrec.capture.CapturedTrainStep): the sampling thread
     builds fixed-shape batches on its own stream, the training thread copies each into the
     captured batch's buffers and launches the graph.  gpu_ms_per_replay: HIP events around
-    replays of one batch alone; busy = that / ms_per_step (the GPU's share of the step).
+    replays of one batch alone (the replayed step's kernels without the loader's).
     caps: the loader's static_caps ('provable' or 'auto', learned from its first batches)."""
     from gnnrec import nn as gnn
     from gnnrec.capture import CapturedTrainStep
@@ -871,20 +914,29 @@ def captured_step(g, dev, K: int, steps: int, warmup: int, caps: str = "provable
     it = iter(el)
     # learned capacities: the first STATIC_LEARN batches come out exact (eager steps), then
     # the step's own warm-up and capture — all before the timed steps
-    for _ in range(max(warmup, 3) + (el.STATIC_LEARN if caps == "auto" else 0)):
+    W = _captured_warmup(warmup, caps)
+    l1 = step(next(it)).clone()  # batch 1: from the same initial weights as the eager run
+    for _ in range(W - 1):
         loss = step(next(it))
     torch.cuda.synchronize()
+    first = None
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for k in range(steps):
         loss = step(next(it))
+        if k == 0:  # the next replay overwrites the captured loss: keep the first one
+            first = loss.clone()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
-    res = {"ms_per_step": round(ms, 3), "steps": steps,
-           "pos_edges_per_s": round(1024 / ms * 1e3), "loss": float(loss.detach()),
+    losses = torch.stack([l1, first, loss.detach()]).double().cpu()
+    res = {"ms_per_step": round(ms, 3), "steps": steps, "warmup_batches": W,
+           "pos_edges_per_s": round(1024 / ms * 1e3), "loss": float(losses[-1]),
+           "loss_first": float(losses[1]), "loss_batch1": float(losses[0]),
            "replays": step.replays, "eager_steps": step.eager_steps,
            "captures": step.captures, "fold": model.train_fold, "static_caps": caps,
-           "redone": el.static_redone}
+           "redone": el.static_redone, "_losses": losses}
     del it, el
+    from gnnrec import ops
+    res["plan_overflows"] = ops.plan_overflows()  # heavy-row plans past their capacities
     if step.graph is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -892,8 +944,10 @@ def captured_step(g, dev, K: int, steps: int, warmup: int, caps: str = "provable
             step.graph.replay()
         e1.record()
         e1.synchronize()
+        # the replayed step's own kernels (the loader's, on the sampling thread's stream,
+        # are not in it); the GPU's occupancy of the loop is a kernel-trace measurement
+        # (union of kernel intervals, tools/rocpd_timeline.py), not a ratio of these events
         res["gpu_ms_per_replay"] = round(e0.elapsed_time(e1) / 20, 3)
-        res["busy"] = round(res["gpu_ms_per_replay"] / ms, 3)
     return res
 
 
@@ -1049,6 +1103,38 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
     return out
 
 
+def choose_allgather(args, runner, ex, feats, dev):
+    """P > 1: the form of the pass's item all-gathers (Exchange.ag_mode).  'auto' records
+    one pass's collectives, replays its all-gathers alone in both forms — RCCL's ring
+    all-gather and the all-to-all of the own block that writes every peer over its own
+    xGMI link — takes the faster by the max over ranks (every rank must choose the same),
+    and runs one more pass in it before the timed region.  Both forms deliver the same
+    table, so the output bits do not depend on the choice."""
+    from gnnrec.dist import RecordingExchange
+    if args.allgather != "auto" or os.environ.get("GNNREC_ALLGATHER"):
+        mode = os.environ.get("GNNREC_ALLGATHER") or args.allgather
+        ex.ag_mode = mode
+        return {"mode": mode, "how": "fixed (--allgather / GNNREC_ALLGATHER)"}
+    rec = RecordingExchange(ex)
+    runner.ex = rec
+    runner.run(feats, replicate_output=False)
+    torch.cuda.synchronize()
+    runner.ex = ex
+    ags = [c for c in rec.calls if c[0] == "all_gather"]
+    if not ags:
+        return {"mode": ex.ag_mode, "how": "no all-gather in the timed pass"}
+    sub = RecordingExchange(ex)
+    sub.calls = ags
+    ms = {m: ex.max_scalar(v, dev) for m, v in sub.replay_ms_by_allgather(dev).items()}
+    mode = min(ms, key=ms.get)
+    ex.ag_mode = mode
+    runner.run(feats, replicate_output=False)  # one pass in the chosen form
+    torch.cuda.synchronize()
+    return {"mode": mode, "how": "auto: the pass's all-gathers replayed alone in both forms, "
+                                 "max over ranks, faster kept",
+            "replay_ms": {m: round(v, 3) for m, v in ms.items()}, "calls_per_pass": len(ags)}
+
+
 def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev, ms_step):
     """Self-diagnosis of a P > 1 run (every rank takes part; rank 0 reports):
       rank_compute_ms  each rank's share of the pass with the same kernels and concurrency
@@ -1067,6 +1153,7 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
     torch.cuda.synchronize()
     runner.ex = ex
     comm_ms = rec.replay_ms(dev)
+    comm_both = rec.replay_ms_by_allgather(dev)
     per_kind = rec.replay_by_kind(dev)
     null = ShardedFullGraphPass(model, shard, ComputeOnlyExchange(world, ex.rk),
                                 overlap=not args.no_overlap, deterministic=det, concurrency=conc)
@@ -1102,6 +1189,8 @@ def multi_gpu_diagnostics(args, runner, ex, feats, model, shard, det, conc, dev,
             "rank_compute_ms": [round(c, 2) for c in compute], "rank_edges": edges,
             "ms_per_step_replicated_output": round(rep_ms, 3),
             "comm_ms": comm_ms, "comm_bytes_per_rank": rec.bytes_sent(),
+            # one pass's collectives replayed alone with its all-gathers in each form
+            "comm_ms_by_all_gather_mode": {k: round(v, 3) for k, v in comm_both.items()},
             "collectives_per_pass": len(rec.calls), "overlap_frac": overlap,
             # per collective kind, replayed alone: ms per call, bytes each rank sends per
             # call, and bus bandwidth = those bytes / time (nccl-tests' busbw: algbw x

@@ -276,8 +276,11 @@ extern "C" int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_grou
                      aligned16(Hd),
                  "gnnrec_sddmm_cos_grouped_f32: needs d %% 4 == 0, d <= 256 and 16-B aligned "
                  "rows (gnnrec_sddmm_cos_f32 takes the rest)");
-  GNNREC_REQUIRE(n_groups * ((K + 255) / 256 + 1) < (int64_t(1) << 32),
-                 "gnnrec_sddmm_cos_grouped_f32: too many groups");
+  // one wave per (group, kCosChunk negatives): the launch's work-items (4 waves per
+  // 256-thread block) must stay below 2^32
+  GNNREC_REQUIRE((n_groups * (K > 0 ? (K + kCosChunk - 1) / kCosChunk : 1) + 3) / 4 * 256 <
+                     (int64_t(1) << 32),
+                 "gnnrec_sddmm_cos_grouped_f32: too many groups x negatives for one launch");
   hipStream_t s = as_stream(stream);
   if (d <= 64)
     return launch_cos_grouped<16>(src_g, n_groups, first, out_first, K, dst, out, Hs, lds, Hd, ldd,

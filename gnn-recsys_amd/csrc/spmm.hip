@@ -150,7 +150,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ ew, const float* __restrict__ X, int64_t ldx, int64_t n_dst, int d,
     float* __restrict__ out, int64_t ldo, int flags, int64_t max_deg, unsigned* rq,
-    int rq_ch, int64_t group_deg, const int64_t* __restrict__ live) {
+    int rq_ch, int64_t group_deg, const int64_t* __restrict__ live,
+    const int64_t* __restrict__ plan_counts) {
+  // a device-built plan that overflowed its capacities (plan_chunks_kernel: n_heavy < 0)
+  // covers no row: every row, heavy or not, is reduced here instead
+  if (plan_counts != nullptr && plan_counts[0] < 0) max_deg = INT64_MAX;
   if (live != nullptr) {
     // rows from the device count on (a static block's padding and dump rows): the empty
     // row's value (0: sum / mean), no gathers; left as they are under ACCUM (+= 0)
@@ -260,6 +264,7 @@ __global__ __launch_bounds__(256) void spmm_chunk_kernel(
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
   if (counts) n_chunks = counts[1];  // device-built plan: the grid covers its capacity
+                                     // (0 when it overflowed)
   for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += wstride) {
     const int64_t h = chunk_row[c];
     const int64_t row = heavy_rows[h];
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
   const int lane = threadIdx.x & 63;
   const float init = (REDUCE == GNNREC_REDUCE_MAX) ? -INFINITY : 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-  if (counts) n_heavy = counts[0];
+  if (counts) n_heavy = counts[0];  // < 0: an overflowed plan (the row kernel took them)
   for (int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); h < n_heavy; h += wstride) {
     const int64_t row = heavy_rows[h];
     const int64_t deg = indptr[row + 1] - indptr[row];
@@ -361,7 +366,7 @@ int launch_all(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((spmm_csr_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
                      dim3(grid, slices), dim3(256), 0, s, a.indptr, a.indices, a.ew,
                      a.X, a.ldx, a.n_dst, a.d, a.out, a.ldo, eni, max_deg, rq, kRowChunk,
-                     kGroupMaxAvgDeg, a.live);
+                     kGroupMaxAvgDeg, a.live, a.counts);
   rowq_launched(ticket, s);
   if (a.n_heavy > 0) {
     hipLaunchKernelGGL((spmm_chunk_kernel<LPR, VEC, REDUCE, WEIGHTED, UNROLL>),
@@ -589,9 +594,17 @@ __global__ void plan_zero_kernel(int64_t* __restrict__ plan) {
   if (threadIdx.x < 2) plan[threadIdx.x] = 0;
 }
 
+// Plans whose heavy rows or chunks exceed their capacities (a CSR breaking the host's bound
+// from its edge count): counted here, read by gnnrec_spmm_plan_overflows.  Atomic adds are
+// vector-memory atomics; nothing else writes it.
+__device__ unsigned long long g_plan_overflows = 0;
+
 // one block: chunk_ptr = exclusive scan of ceil(deg/split) over the heavy rows, then
 // chunk_row[c] = owning heavy row (at most cap_c chunks: the host's bound from the edge
-// count, enforced here too so a CSR that breaks it cannot write past the plan)
+// count, enforced here too so a CSR that breaks it cannot write past the plan).  A plan
+// past either capacity is marked overflowed — plan[0] = -(heavy rows found), plan[1] = 0 —
+// and counted: its chunk and combine kernels then do nothing and the row kernel reduces
+// every row itself (exact, one wave per row), so no aggregate is ever clipped.
 __global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __restrict__ indptr,
                                                            int64_t split, int64_t* __restrict__ plan,
                                                            int64_t cap_h, int64_t cap_c) {
@@ -629,9 +642,10 @@ __global__ __launch_bounds__(1024) void plan_chunks_kernel(const int64_t* __rest
     const int64_t c1 = chunk_ptr[h + 1] < cap_c ? chunk_ptr[h + 1] : cap_c;
     for (int64_t c = chunk_ptr[h]; c < c1; ++c) chunk_row[c] = h;
   }
-  if (t == 0) {  // counts past the capacities (a CSR breaking the bounds) are clipped
-    if (carry > cap_c) plan[1] = cap_c;
-    if (plan[0] > cap_h) plan[0] = cap_h;
+  if (t == 0 && (carry > cap_c || plan[0] > cap_h)) {
+    plan[0] = -(plan[0] > 0 ? plan[0] : 1);
+    plan[1] = 0;
+    atomicAdd(&g_plan_overflows, 1ull);
   }
 }
 
@@ -656,6 +670,18 @@ extern "C" int gnnrec_spmm_plan_build_live(const int64_t* indptr, int64_t n_dst,
                        cap_c);
   }
   return check_launch("gnnrec_spmm_plan_build");
+}
+
+extern "C" int gnnrec_spmm_plan_overflows(int64_t* count) {
+  GNNREC_REQUIRE(count, "gnnrec_spmm_plan_overflows: null pointer");
+  unsigned long long v = 0;
+  hipError_t e = hipDeviceSynchronize();  // every plan build issued so far has run
+  if (e == hipSuccess)
+    e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(gnnrec::g_plan_overflows), sizeof(v), 0,
+                                     hipMemcpyDeviceToHost);
+  GNNREC_REQUIRE(e == hipSuccess, "gnnrec_spmm_plan_overflows: %s", hipGetErrorString(e));
+  *count = (int64_t)v;
+  return GNNREC_OK;
 }
 
 extern "C" int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split,

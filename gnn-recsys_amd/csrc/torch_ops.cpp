@@ -913,7 +913,6 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
                                                     const optional<Tensor>& ew, int64_t reduce,
                                                     bool norm, const optional<Tensor>& bias,
                                                     const optional<Tensor>& bias_ne,
-                                                    int64_t heavy_nnz,
                                                     const optional<Tensor>& live) {
   const OneDevice one_device_;
   dev(m, "m", at::kFloat);
@@ -949,17 +948,14 @@ std::tuple<Tensor, Tensor, Tensor> sage_rel_forward(const Tensor& m, const Tenso
   const c10::DeviceGuard g(m.device());
   // live: the static block's real destination count on the device (its padding and dump
   // rows aggregate nothing: their outputs feed no real row and get no gradient)
+  // The forward blocks' rows are bounded (fanout rows; a static block's dump rows hold at
+  // most kDumpEdges = the heavy-row split), so the gather needs no heavy-row plan; a
+  // full-neighbour block's long rows run unsplit (one wave each, the same values)
   const int64_t* lv = live_ptr(live);
-  if (heavy_nnz > 0) {  // rows of any length (a static block's dump row): planned on the device
-    TORCH_CHECK_VALUE(indices.numel() >= heavy_nnz, "sage_rel_forward: heavy_nnz > edges");
-    const Tensor w = has(ewc) ? *ewc : Tensor();
-    gather_planned(indptr, indices, w, X, heavy_nnz, agg, false, (int)reduce, lv);
-  } else {
-    ck(gnnrec_spmm_csr_live_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc),
-                                p<float>(X), ld(X, "m"), M, X.size(1), (int)reduce, 0,
-                                p<float>(agg), ld(agg, "agg"), lv, stream_of(m)),
-       "gnnrec_spmm_csr_f32");
-  }
+  ck(gnnrec_spmm_csr_live_f32(p<int64_t>(indptr), p<int32_t>(indices), p<float>(ewc),
+                              p<float>(X), ld(X, "m"), M, X.size(1), (int)reduce, 0,
+                              p<float>(agg), ld(agg, "agg"), lv, stream_of(m)),
+     "gnnrec_spmm_csr_f32");
   // bias_ne's non-empty test reads the block CSR's indptr directly (GNNREC_A2_DEG_INDPTR)
   const Tensor ipc = bnc.defined() ? indptr.contiguous() : Tensor();
   gemm_nt(H, Wsc, &agg, &Wnc, GNNREC_EPI_RELU | (norm ? GNNREC_EPI_L2NORM : 0), z,
@@ -2044,6 +2040,12 @@ std::tuple<int64_t, int64_t> get_concurrency() {
   ck(gnnrec_get_concurrency(&r, &d), "gnnrec_get_concurrency");
   return {r, d};
 }
+int64_t spmm_plan_overflows() {
+  int64_t n = 0;
+  ck(gnnrec_spmm_plan_overflows(&n), "gnnrec_spmm_plan_overflows");
+  return n;
+}
+
 std::tuple<int64_t, int64_t> rowq_stats() {
   const OneDevice one_device_;
   int64_t q = 0, b = 0;
@@ -2166,7 +2168,7 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor(a!) out) -> ()");
   m.def("sage_rel_forward(Tensor m, Tensor h_self, int n_self, Tensor W_self, Tensor W_neigh, "
         "Tensor indptr, Tensor indices, Tensor? edge_weight, int reduce, bool norm, "
-        "Tensor? bias=None, Tensor? bias_nonempty=None, int heavy_nnz=0, Tensor? live=None) "
+        "Tensor? bias=None, Tensor? bias_nonempty=None, Tensor? live=None) "
         "-> (Tensor, Tensor, Tensor)");
   m.def("sage_rel_backward(Tensor gz, Tensor z, Tensor row_norm, Tensor h_self, Tensor agg, "
         "Tensor W_self, Tensor W_neigh, Tensor indptr, Tensor indices, Tensor? edge_weight, "
@@ -2208,6 +2210,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.def("set_concurrency(int reserve_cus, bool dynamic) -> ()", &set_concurrency);
   m.def("get_concurrency() -> (int, int)", &get_concurrency);
   m.def("rowq_stats() -> (int, int)", &rowq_stats);
+  m.def("spmm_plan_overflows() -> int", &spmm_plan_overflows);
   m.def("scan_workspace_bytes(int n) -> int", &scan_workspace_bytes);
   m.def("gemm_tn_workspace_bytes(int K, int M, int N) -> int", &gemm_tn_workspace_bytes);
   m.def("csr_transpose_workspace_bytes(int n_edges, int n_src) -> int",

@@ -51,6 +51,7 @@ SIGNATURES = {
     "gnnrec_spmm_csr_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64, _P]),
     "gnnrec_spmm_csr_split_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,
                                          _I64, _P, _I64, _P, _P, _I64, _P, _P]),
+    "gnnrec_spmm_plan_overflows": (_INT, [_P]),
     "gnnrec_spmm_plan_build": (_INT, [_P, _I64, _I64, _I64, _I64, _P, _P]),
     "gnnrec_spmm_plan_build_live": (_INT, [_P, _I64, _I64, _I64, _I64, _P, _P, _P]),
     "gnnrec_spmm_csr_live_f32": (_INT, [_P, _P, _P, _P, _I64, _I64, _I64, _INT, _INT, _P, _I64,

@@ -183,13 +183,6 @@ def _live(indptr):
     return getattr(indptr, "_gnnrec_live", None)
 
 
-def _heavy_nnz(indptr) -> int:
-    """A static-shape block's CSR (sampling, static_shapes=True) may hold rows of any length
-    (the dump row): its edge count, so the forward gather plans heavy rows on the device;
-    0 for the sampler's bounded-degree blocks."""
-    return int(getattr(indptr, "_gnnrec_heavy", 0))
-
-
 class SageRelFn(torch.autograd.Function):
     """One sum / mean ConvLayer relation of a training step — SpmmFn and SageProjectFn as
     ONE autograd node whose forward and backward are each ONE dispatcher call
@@ -205,8 +198,7 @@ class SageRelFn(torch.autograd.Function):
                 n_self: int = 0, transposed=None):
         z, agg, nrm = ops._T().sage_rel_forward(m, h_self, n_self, Ws.detach(), Wn.detach(),
                                                 indptr, indices, ew, ops.REDUCE[reduce],
-                                                bool(norm), None, None, _heavy_nnz(indptr),
-                                                _live(indptr))
+                                                bool(norm), None, None, _live(indptr))
         ctx.save_for_backward(h_self, agg, Ws, Wn, z, nrm, indptr, indices, ew)
         ctx.reduce, ctx.norm, ctx.n_src = reduce, bool(norm), m.shape[0]
         ctx.nnz = ops._nnz(indptr)  # sampled blocks carry it: no readback
@@ -269,7 +261,7 @@ class HeteroSageFn(torch.autograd.Function):
             z, agg, nrm = T.sage_rel_forward(
                 m, tables[di], n_dst, Ws.detach(), Wn.detach(), ip, ix, ew, ops.REDUCE[reduce],
                 bool(norm), None if b is None else b.detach(),
-                None if bne is None else bne.detach(), _heavy_nnz(ip), _live(ip))
+                None if bne is None else bne.detach(), _live(ip))
             zs.append(z)
             saved += [agg, z, nrm]
         outs = []
@@ -362,16 +354,19 @@ class FoldFn(torch.autograd.Function):
     """The first-layer fold's weight products for one node type (nn._fold_weights): every
     weight W_i that the type's NodeEmbedding (W_e, b_e) feeds, stacked as A = [W_1; W_2; ..],
     -> (W_1 W_e, W_2 W_e, .., W_1 b_e, W_2 b_e, ..), each a contiguous row block of A W_e /
-    A b_e.  As one node its backward is six launches — the two stacked gradients, dA =
-    dWF W_eᵀ + dBF b_eᵀ, dW_e = Aᵀ dWF, db_e = Aᵀ dBF — where the per-slice autograd form
-    (cat, matmul, slices) zero-fills and copies every slice's gradient and adds them
-    (≈15 launches per node type in a captured C2 step)."""
+    A b_e.  As one node its backward is the two stacked gradients and three library GEMMs —
+    dW_e = Aᵀ dWF and db_e = (dBFᵀ A)ᵀ on the split-K weight-gradient GEMM, dA = dWF W_eᵀ +
+    dBF b_eᵀ as one two-operand GEMM — where the per-slice autograd form (cat, matmul,
+    slices) zero-filled and copied every slice's gradient and added them (≈15 launches per
+    node type in a captured C2 step).  Every product runs on the library's fp32 MFMA GEMMs
+    (ops.gemm / ops.gemm_tn), as the inference fold does (inference.py), not vendor BLAS."""
 
     @staticmethod
     def forward(ctx, W_e, b_e, *Ws):
-        A = torch.cat(Ws, 0) if len(Ws) > 1 else Ws[0]
-        WF = torch.mm(A, W_e)
-        BF = torch.mv(A, b_e)
+        A = (torch.cat(Ws, 0) if len(Ws) > 1 else Ws[0]).detach().contiguous()
+        W_e, b_e = W_e.detach().contiguous(), b_e.detach().contiguous()
+        WF = ops.gemm(A, W_e.t().contiguous())             # A W_e = linear(A, W_eᵀ)
+        BF = ops.gemm(b_e.view(1, -1), A).view(-1)         # (A b_e)ᵀ = linear(b_eᵀ, A)
         rows = [W.shape[0] for W in Ws]
         ctx.save_for_backward(A, W_e, b_e)
         ctx.rows = rows
@@ -385,16 +380,15 @@ class FoldFn(torch.autograd.Function):
 
         def stacked(gs, shape):
             gs = [g if g is not None else A.new_zeros(shape(r)) for g, r in zip(gs, rows)]
-            return torch.cat(gs, 0) if n > 1 else gs[0]
+            return (torch.cat(gs, 0) if n > 1 else gs[0]).contiguous()
         dWF = stacked(grads[:n], lambda r: (r, W_e.shape[1]))
         dBF = stacked(grads[n:], lambda r: (r,))
         need = ctx.needs_input_grad
-        dW_e = torch.mm(A.t(), dWF) if need[0] else None
-        db_e = torch.mv(A.t(), dBF) if need[1] else None
+        dW_e = ops.gemm_tn(A, dWF) if need[0] else None
+        db_e = ops.gemm_tn(dBF.view(-1, 1), A).view(-1) if need[1] else None
         dWs = [None] * n
         if any(need[2:]):
-            dA = torch.mm(dWF, W_e.t())
-            dA.addr_(dBF, b_e)
+            dA = ops.gemm(dWF, W_e, dBF.view(-1, 1), b_e.view(-1, 1))
             dWs = list(dA.split(rows))
         return (dW_e, db_e, *dWs)
 

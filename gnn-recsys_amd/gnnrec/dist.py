@@ -224,6 +224,7 @@ class AsyncEmulatedExchange(Exchange):
         self.sync_calls = 0
         self._streams = None
         self._pool = None
+        self._gate = None
         # the transport thread's collectives go through their own gloo group, so they never
         # interleave with collectives the main thread issues on the default one
         self._tgroup = dist.new_group(backend="gloo") if self.ws > 1 else None
@@ -246,24 +247,55 @@ class AsyncEmulatedExchange(Exchange):
             from . import ops
             ops.hold_cus(self.hold_blocks, self.delay_us, stream=stream)
 
+    def gate(self):
+        """Ordering by events instead of delays (tests of the emulation itself): the
+        collectives issued from now until release(event) copy their input in only after
+        `event` — recorded by the caller on its stream once it has done whatever must come
+        first — and land their output only after that copy-in, so 'the input is read late'
+        and 'the output lands late' hold by construction, whatever the box's load."""
+        import threading
+        self._gate = {"open": threading.Event(), "after": None}
+
+    def release(self, event: torch.cuda.Event):
+        g, self._gate = self._gate, None
+        g["after"] = event
+        g["open"].set()
+
     def _issue(self, src: torch.Tensor, out: torch.Tensor, transport, async_op: bool):
         """src (device) -> transport(h_in, h_out) on host copies -> out (device)."""
         dev = src.device
         self._dev_setup(dev)
         s_in, s_out = self._streams
         cur = torch.cuda.current_stream(dev)
-        s_in.wait_stream(cur)
-        with torch.cuda.stream(s_in):
-            self._delay(s_in)
-            h_in = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-            h_in.copy_(src, non_blocking=True)
-            ev_in = torch.cuda.Event()
-            ev_in.record(s_in)
+        h_in = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        gate = self._gate
+
+        def copy_in():
+            with torch.cuda.stream(s_in):
+                self._delay(s_in)
+                h_in.copy_(src, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s_in)
+            return ev
+
+        if gate is None:
+            s_in.wait_stream(cur)
+            ev_in = copy_in()
+        else:  # the copy-in is queued by the transport thread once the gate opens
+            ev_in = None
+            ev_issue = torch.cuda.Event()
+            ev_issue.record(cur)
         src.record_stream(s_in)
         out.record_stream(s_out)
         h_out = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
 
         def job():
+            nonlocal ev_in
+            if gate is not None:
+                gate["open"].wait()
+                s_in.wait_event(ev_issue)
+                s_in.wait_event(gate["after"])
+                ev_in = copy_in()
             ev_in.synchronize()
             transport(h_in, h_out)
             with torch.cuda.stream(s_out):
@@ -300,6 +332,13 @@ class AsyncEmulatedExchange(Exchange):
             return super().all_gather_rows(own, out, async_op)
         own = own.contiguous()
         if own.is_cuda:
+            if self.ag_mode == "a2a":  # as Exchange's: an all-to-all of the own block x P
+                src = own.unsqueeze(0).expand((self.ws,) + tuple(own.shape)).contiguous()
+
+                def transport(h_in, h_out):
+                    dist.all_to_all_single(h_out, h_in.view(h_out.shape), group=self._tgroup)
+                return out, self._issue(src, out, transport, async_op)
+
             def transport(h_in, h_out):
                 dist.all_gather_into_tensor(h_out, h_in, group=self._tgroup)
             return out, self._issue(own, out, transport, async_op)
@@ -540,8 +579,7 @@ class RecordingExchange:
         for kind in sorted({c[0] for c in self.calls}):
             calls = [c for c in self.calls if c[0] == kind]
             modes = [None]
-            if kind == "all_gather" and hasattr(self.inner, "ag_mode") and \
-                    type(self.inner) is Exchange:
+            if kind == "all_gather" and getattr(self.inner, "ag_mode", None) in ("rccl", "a2a"):
                 modes.append("a2a" if self.inner.ag_mode == "rccl" else "rccl")
             for mode in modes:
                 sub = RecordingExchange(self.inner)
@@ -558,6 +596,20 @@ class RecordingExchange:
                 out[kind if mode is None else f"{kind}_{mode}"] = {
                     "ms": ms, "calls": len(calls), "bytes": int(sent),
                     "busbw_GBs": sent / (ms * 1e-3) / 1e9 if ms > 0 else None}
+        return out
+
+    def replay_ms_by_allgather(self, device, reps: int = 3) -> dict:
+        """replay_ms with the pass's all-gathers in each form: {'rccl': ms, 'a2a': ms} — the
+        communication one pass would cost under either GNNREC_ALLGATHER setting."""
+        if self.ws == 1 or not self.calls or not hasattr(self.inner, "ag_mode"):
+            return {}
+        keep, out = self.inner.ag_mode, {}
+        try:
+            for mode in ("rccl", "a2a"):
+                self.inner.ag_mode = mode
+                out[mode] = self.replay_ms(device, reps)
+        finally:
+            self.inner.ag_mode = keep
         return out
 
     def _timed(self, once, device, reps):

@@ -394,6 +394,11 @@ class Block:
         return b
 
 
+def _stamp(t: torch.Tensor):
+    """Identity of a tensor's contents: storage, in-place version, size."""
+    return (t.data_ptr(), t._version, t.numel(), t.device)
+
+
 class PairGraph:
     """pos_g / neg_g: edges over compacted seed nodes (DGL compact_graphs output)."""
 
@@ -411,7 +416,28 @@ class PairGraph:
         self.nodes = _TypeAccessor(self._ndata, lambda k: k)
         # K when this is the negative graph of negative_sampler.Uniform(K): every etype's
         # sources are the positive graph's repeated K times (EdgeDataLoader sets it)
-        self.src_repeats_pos = None
+        self._repeats = None
+
+    @property
+    def src_repeats_pos(self):
+        """K when marked as negative_sampler.Uniform(K)'s negative graph, else None."""
+        return None if self._repeats is None else self._repeats[0]
+
+    @src_repeats_pos.setter
+    def src_repeats_pos(self, K):
+        """Mark (or unmark: None) the graph's CURRENT source tensors as the positives'
+        sources repeated K times.  The mark holds per etype only while that tensor is the
+        one marked, unmodified (src_repeats): a replaced or edited edge list falls back to
+        the per-edge cosine instead of trusting a stale mark."""
+        self._repeats = None if K is None else (
+            int(K), {ce: _stamp(s) for ce, (s, _d) in self._coo.items()})
+
+    def src_repeats(self, etype, src) -> Optional[int]:
+        """K if `src` is still the marked source tensor of `etype`, else None."""
+        r = self._repeats
+        if r is None or r[1].get(tuple(etype)) != _stamp(src):
+            return None
+        return r[0]
 
     @property
     def ndata(self):
@@ -445,7 +471,9 @@ class PairGraph:
         for ce, f in self._edata.items():
             for k, v in f.items():
                 p._edata[ce][k] = v.to(device)
-        p.src_repeats_pos = self.src_repeats_pos
+        if self._repeats is not None and all(
+                self.src_repeats(ce, s) is not None for ce, (s, _d) in self._coo.items()):
+            p.src_repeats_pos = self._repeats[0]  # the copies hold the same values
         return p
 
 

@@ -35,6 +35,9 @@ from . import _lib, ops
 from . import autograd as ag
 
 USER_ITEM = ("user", "item")
+# debug: check a negative graph's src_repeats_pos mark against its values before the grouped
+# cosine trusts it (one device comparison and sync per etype and step; tests switch it on)
+CHECK_GROUPED_PAIRS = False
 _PREAGG = ("pool_nn", "pool_nn_edge", "mean_nn", "mean_nn_edge")
 _KNOWN = ("mean", "mean_nn", "pool_nn", "lstm", "mean_edge", "mean_nn_edge", "pool_nn_edge",
           "lstm_edge")
@@ -548,10 +551,14 @@ class CosinePrediction(nn.Module):
                 continue
             # negative_sampler.Uniform's pairs (the loader marks them): every positive's
             # source repeated K times -> the grouped launch, one gathered row per edge
-            K = getattr(neg_g, 'src_repeats_pos', None)
+            K = neg_g.src_repeats(etype, ns) if hasattr(neg_g, 'src_repeats') else None
             if K is not None and (ns.numel() != ps.numel() * K or
                                   not ops.cos_grouped_ok(h[etype[0]], h[etype[2]])):
                 K = None
+            if K is not None and CHECK_GROUPED_PAIRS:  # debug: the mark against the values
+                if not torch.equal(ns, ps.repeat_interleave(K)):
+                    raise ValueError(f"{etype}: negative sources are not the positives' "
+                                     f"sources repeated {K} times (stale src_repeats_pos)")
             if _grad_mode(h[etype[0]], h[etype[2]]):
                 a, b = ag.CosinePairFn.apply(h[etype[0]], h[etype[2]], ps, pd, ns, nd, K)
             elif K is not None:

@@ -154,6 +154,14 @@ def _device_plan(indptr: torch.Tensor, split: int):
     return res
 
 
+def plan_overflows() -> int:
+    """Device-built heavy-row plans that overflowed their capacities since the library
+    loaded (gnnrec_spmm_plan_overflows; synchronises the device).  Such a plan's gather
+    reduced every row unsplit — exact, not clipped — but a nonzero count means a CSR whose
+    host edge count (`_gnnrec_nnz`) understated its edges: check it after a step."""
+    return int(_T().spmm_plan_overflows())
+
+
 def spmm(indptr: torch.Tensor, indices: torch.Tensor, X: torch.Tensor, reduce: str = "mean",
          edge_weight: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
          empty_neginf: bool = False, split: Optional[int] = DEFAULT_SPLIT,

@@ -157,11 +157,17 @@ int gnnrec_spmm_csr_split_f32(const int64_t* indptr, const int32_t* indices, con
  * count): plan = int64[2 + cap_h + (cap_h + 1) + cap_c] laid out {n_heavy, n_chunks,
  * heavy_rows[cap_h], chunk_ptr[cap_h+1], chunk_row[cap_c]}, with cap_h = min(n_dst,
  * n_edges / (split + 1)) and cap_c = n_edges / split + cap_h (bounds that hold for any
- * degree distribution; the build never writes past cap_c chunks, nor counts more).
+ * degree distribution; the build never writes past cap_h rows or cap_c chunks).
  * gnnrec_spmm_plan_build fills it (no host call in it but kernels: replayable inside a
  * captured graph); gnnrec_spmm_csr_planned_f32
  * reduces with workspace[cap_c, d].  Used for blocks whose edge count is known on the
- * host but whose degrees are not (sampled blocks, the backward's transposed blocks). */
+ * host but whose degrees are not (sampled blocks, the backward's transposed blocks).
+ * Overflow: a CSR that breaks those bounds (its edge count understated) gets a plan marked
+ * overflowed — n_heavy = -(heavy rows found) < 0, n_chunks = 0 — and counted in a device
+ * counter; the planned gather then reduces EVERY row in the row kernel (exact, unsplit), so
+ * no aggregate is clipped.  gnnrec_spmm_plan_overflows synchronises the device and returns
+ * how many plans have overflowed since the library loaded (0 on every well-formed CSR). */
+int gnnrec_spmm_plan_overflows(int64_t* count);
 int gnnrec_spmm_plan_build(const int64_t* indptr, int64_t n_dst, int64_t split, int64_t cap_h,
                            int64_t cap_c, int64_t* plan, void* stream);
 int gnnrec_spmm_csr_planned_f32(const int64_t* indptr, const int32_t* indices, const float* ew,

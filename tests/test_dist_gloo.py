@@ -200,6 +200,8 @@ def _ag_worker(rank, world, port, q):
         rec = RecordingExchange(ex)
         rec.all_gather_rows(own, torch.empty(6 * world, 3))
         kinds = rec.replay_by_kind(torch.device("cpu"), reps=1)
+        both = rec.replay_ms_by_allgather(torch.device("cpu"), reps=1)
+        assert ex.ag_mode == "rccl" and sorted(both) == ["a2a", "rccl"]
         q.put((rank, res, sorted(kinds)))
     finally:
         dist.destroy_process_group()

@@ -295,3 +295,46 @@ def test_live_row_count_gathers_only_the_real_rows(planned):
                                rtol=1e-6, atol=1e-6)
     zero = torch.zeros(1, dtype=torch.int64, device=DEV)
     assert torch.count_nonzero(run(zero)) == 0
+
+
+@pytest.mark.parametrize("short", ["rows", "chunks"])
+def test_overflowed_plan_is_flagged_and_reduces_every_row(short):
+    """A device-built heavy-row plan whose capacities are too short for its CSR (a host edge
+    count that understates the edges): the build marks the plan overflowed (n_heavy < 0,
+    n_chunks = 0), the library's overflow counter rises, and the planned gather reduces every
+    row in the row kernel — bitwise the unplanned gather, no row dropped or clipped."""
+    from gnnrec import ops
+    T = ops._T()
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(11)
+    n_dst, n_src, d, split = 2000, 500, 64, 2048
+    deg = torch.randint(0, 9, (n_dst,), device=DEV, generator=gen)
+    deg[[7, 901, 1999]] = torch.tensor([9000, 5000, 20000], device=DEV)  # 3 heavy rows, 18 chunks
+    ip = torch.zeros(n_dst + 1, dtype=torch.int64, device=DEV)
+    ip[1:] = torch.cumsum(deg, 0)
+    nnz = int(ip[-1])
+    ix = torch.randint(0, n_src, (nnz,), device=DEV, generator=gen).int()
+    X = torch.randn(n_src, d, device=DEV, generator=gen)
+    ref = torch.empty(n_dst, d, device=DEV)
+    T.spmm_csr(ip, ix, None, X, ops.REDUCE["mean"], 0, ref, None)  # no plan: unsplit rows
+    cap_h, cap_c = (1, 64) if short == "rows" else (8, 4)
+    plan = torch.empty(3 + 2 * cap_h + cap_c, dtype=torch.int64, device=DEV)
+    before = ops.plan_overflows()
+    T.spmm_plan_build(ip, split, cap_h, plan, None)
+    ws = torch.empty(cap_c * d, device=DEV)
+    out = torch.full((n_dst, d), 7.0, device=DEV)
+    T.spmm_csr_planned(ip, ix, None, X, ops.REDUCE["mean"], 0, split, plan, cap_h, cap_c, out,
+                       ws, None)
+    torch.cuda.synchronize()
+    assert int(plan[0]) == -3 and int(plan[1]) == 0
+    assert ops.plan_overflows() == before + 1
+    assert torch.equal(out, ref)
+    # a plan with room for its rows is not flagged, and splits the heavy rows as before
+    plan = torch.empty(3 + 2 * 8 + 64, dtype=torch.int64, device=DEV)
+    T.spmm_plan_build(ip, split, 8, plan, None)
+    ws = torch.empty(64 * d, device=DEV)
+    T.spmm_csr_planned(ip, ix, None, X, ops.REDUCE["mean"], 0, split, plan, 8, 64, out, ws, None)
+    torch.cuda.synchronize()
+    assert int(plan[0]) == 3 and int(plan[1]) == 5 + 3 + 10
+    assert ops.plan_overflows() == before + 1
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)

@@ -287,6 +287,102 @@ def test_c2_k2500_default_fold_gradients_match_unfolded(c2_graph, monkeypatch):
                                    msg=n)
 
 
+def _real_blocks(blocks):
+    """A static batch's blocks cut to their real rows for the oracle: the real destination
+    rows come first (the seeds), their edges are the CSR prefix [0, indptr[n_real]) and point
+    only at the real source rows (the sampler's static-shape contract, include/gnnrec.h)."""
+    out = []
+    for b in blocks:
+        n_dst = {nt: int(b._live[("dst", nt)]) for nt in b.ntypes}
+        rels = {}
+        for ce in b.canonical_etypes:
+            ip, loc, eid = (_np(t) for t in b._rels[ce])
+            n = n_dst[ce[2]]
+            e = int(ip[n])
+            n_src = int(b._live[("src", ce[0])])
+            assert (loc[:e] < n_src).all() and (eid[:e] >= 0).all()
+            rels[ce] = (ip[:n + 1].copy(), loc[:e].copy(), eid[:e].copy())
+        out.append(oracle.BlockGraph(rels, n_dst))
+    return out
+
+
+@pytest.mark.parametrize("K,caps", [(10, "provable"), (2500, "auto")])
+def test_c2_captured_static_steps_match_oracle(c2_graph, K, caps):
+    """The path bench.py's captured minibatch numbers run (bench.captured_step): the C2 graph,
+    EdgeDataLoader(static_shapes=True) with its sampling thread — padding rows, dump rows of
+    <= 2048 edges, learned capacities at K = 2500 — and CapturedTrainStep (hipGraph replay,
+    the first-layer fold forced on).  For three replayed steps, the step's forward embeddings
+    (real rows), positive / negative scores and loss against oracle.model_blocks +
+    cosine_prediction + max_margin_loss on the batch's real rows, with the weights the step
+    started from (reference src/train/run.py:89-138, src/sampling.py:153-165).  The fold
+    reassociates fp32 products (W_s W_e) x: rtol 1e-4, the north star's tolerance."""
+    from gnnrec import nn as gnn
+    from gnnrec import ops
+    from gnnrec.capture import CapturedTrainStep
+    from gnnrec.sampling import EdgeDataLoader, MultiLayerNeighborSampler, negative_sampler
+    g, feats = c2_graph
+    _set_feats(g, feats[64])
+    torch.manual_seed(0)
+    model = gnn.ConvModel(g, 3, {"user": 64, "item": 64, "hidden": 64, "out": 64}, True, 0.0,
+                          "mean", "cos", "sum", True).to(DEV)
+    model.train_fold = "1"
+    opt = torch.optim.Adam(model.parameters(), lr=0.005, fused=True)
+    captured = {}
+
+    def loss_fn(m, batch):
+        _, pos_g, neg_g, blocks = batch
+        h, ps, ns = m(blocks, blocks[0].srcdata["features"], pos_g, neg_g, True)
+        if torch.cuda.is_current_stream_capturing():  # the graph's own output tensors
+            captured["out"] = (h, ps, ns)
+        return gnn.max_margin_loss(ps, ns, 0.266, K, True, pos_g.edata["recency"])
+
+    step = CapturedTrainStep(model, opt, loss_fn, warmup=2)
+    el = EdgeDataLoader(g, {BUYS: torch.arange(g.num_edges(BUYS))},
+                        MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
+                        reverse_etypes=REV, negative_sampler=negative_sampler.Uniform(K),
+                        batch_size=1024, shuffle=True, num_workers=2, static_shapes=True,
+                        static_caps=caps)
+    el.sampler.first_transposes_below = 0
+    before = ops.plan_overflows()
+    checked = 0
+    for batch in el:
+        sd = _sd(model)  # the weights this step starts from
+        r0 = step.replays
+        loss = step(batch)
+        if step.replays == r0:
+            continue
+        torch.cuda.synchronize()
+        _, pos_g, neg_g, blocks = batch
+        assert pos_g.static and all(b.static for b in blocks)
+        h, ps, ns = captured["out"]
+        rb = _real_blocks(blocks)
+        n_src0 = {nt: int(blocks[0]._live[("src", nt)]) for nt in blocks[0].ntypes}
+        x = {nt: _np(v)[:n_src0[nt]] for nt, v in blocks[0].srcdata["features"].items()}
+        rh = oracle.model_blocks(rb, x, sd, "mean", "sum", True, True)
+        for nt in rh:
+            n = rh[nt].shape[0]
+            assert n == int(blocks[-1]._live[("dst", nt)])
+            np.testing.assert_allclose(_np(h[nt])[:n], rh[nt], rtol=RTOL, atol=ATOL,
+                                       err_msg=f"replay {checked}: {nt} embeddings")
+        pos = {ce: tuple(_np(t) for t in pos_g.all_edges(etype=ce)) for ce in pos_g.canonical_etypes}
+        neg = {ce: tuple(_np(t) for t in neg_g.all_edges(etype=ce)) for ce in neg_g.canonical_etypes}
+        rps, rns = oracle.cosine_prediction(pos, rh), oracle.cosine_prediction(neg, rh)
+        for ce in rps:
+            np.testing.assert_allclose(_np(ps[ce]), rps[ce], rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(_np(ns[ce]), rns[ce], rtol=RTOL, atol=ATOL)
+        rec = {ce: _np(v) for ce, v in pos_g.edata["recency"].items()}
+        rl = oracle.max_margin_loss(rps, rns, 0.266, K, use_recency=True, recency=rec)
+        np.testing.assert_allclose(float(loss), rl, rtol=RTOL, atol=ATOL)
+        print(f"  K={K} replay {checked}: loss {float(loss):.6f} (oracle {rl:.6f}), "
+              f"{sum(v.shape[0] for v in rh.values())} output rows", flush=True)
+        checked += 1
+        if checked == 3:
+            break
+    assert checked == 3 and step.captures == 1
+    assert ops.plan_overflows() == before
+    del el
+
+
 @pytest.mark.parametrize("n_layers", [3, 4])
 def test_c3_mean_nn_cosine_1024x2500_matches_oracle(c2_graph, n_layers):
     from gnnrec import nn as gnn

@@ -345,19 +345,32 @@ def _emulation_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gnnrec.dist import AsyncEmulatedExchange
-        # a long delay: the two ranks share one GPU here, and the other process's kernels
-        # can hold this one's fill back by tens of ms (30 ms flaked on a busy box)
-        ex = AsyncEmulatedExchange(delay_us=300000)
+        # ordered by events, not by a delay outrunning the other rank's kernels on the
+        # shared GPU: the gate holds the copy-in until the event recorded after the early
+        # read, and the copy-out follows the copy-in
+        ex = AsyncEmulatedExchange(delay_us=0)
         own = torch.full((4, 8), float(rank + 1), device="cuda")
         out = torch.full((8, 8), -1.0, device="cuda")
+        ex.gate()
         _, work = ex.all_gather_rows(own, out, async_op=True)
         own.fill_(7.0)  # the collective reads its input late: this write races it
         early = out.clone()  # no wait: the output has not landed yet
+        after = torch.cuda.Event()
+        after.record()
+        ex.release(after)
         work.wait()
         late = out.clone()
         full = torch.arange(16.0, device="cuda").view(8, 2) * (rank + 1)
         blocks, work = ex.all_to_all_rows(full, async_op=True)
         work.wait()
+        # the all-gather as an all-to-all of the own block x P (GNNREC_ALLGATHER=a2a)
+        ex.ag_mode = "a2a"
+        own2 = torch.full((4, 8), float(rank + 1), device="cuda")
+        out2 = torch.full((8, 8), -1.0, device="cuda")
+        _, work = ex.all_gather_rows(own2, out2, async_op=True)
+        work.wait()
+        want = torch.cat([torch.full((4, 8), float(r + 1), device="cuda") for r in range(world)])
+        assert torch.equal(out2, want)
         q.put((rank, early.cpu().numpy(), late.cpu().numpy(), blocks.cpu().numpy()))
         ex.close()
     finally:
@@ -367,7 +380,9 @@ def _emulation_worker(rank, world, port, q):
 def test_async_emulation_lands_late_and_reads_late():
     """The emulation does what makes it a test of the pass's ordering: a reader that skips
     work.wait() sees the output before it lands, and the input is read when the collective
-    runs (after its delay), not when it is issued — as under RCCL."""
+    runs, not when it is issued — as under RCCL.  Ordered by events (AsyncEmulatedExchange
+    .gate/release), so the assertions do not depend on a delay beating another process's
+    kernels."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q, port = ctx.Queue(), _port()

@@ -1723,7 +1723,7 @@ def test_sddmm_cos_grouped_bitwise_equals_per_edge_and_oracle(d):
         np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
 
 
-@pytest.mark.parametrize("K,d", [(50, 64), (200, 128), (10, 40)])
+@pytest.mark.parametrize("K,d", [(50, 64), (200, 128), (10, 40), (130, 200), (70, 256)])
 def test_cosine_pair_head_grouped_path_forward_and_gradients(K, d):
     """CosinePrediction.pair on a negative graph marked by the loader (src_repeats_pos = K)
     takes the grouped launch: the same scores and item gradients as the unmarked graph, and
@@ -1781,3 +1781,44 @@ def test_cos_backward_grouped_reads_only_the_positives_sources(K, d):
         assert torch.equal(x, y)
     with pytest.raises((ValueError, RuntimeError)):
         ops.sddmm_cos_backward(ps, dst, hs, hd, g)  # a short src needs the grouped layout
+
+
+def test_cosine_pair_head_ignores_a_stale_grouped_mark():
+    """The loader's src_repeats_pos mark binds the negative graph's source tensors as they
+    were when marked: an edge list edited in place afterwards (or replaced) is scored by the
+    per-edge kernel, never by the grouped one on a broken promise; and the debug check
+    (nn.CHECK_GROUPED_PAIRS) rejects a graph marked with sources that were never repeats."""
+    from gnnrec import nn as gnn
+    from gnnrec import ops
+    from gnnrec.graph import PairGraph
+    rng = np.random.default_rng(4)
+    ce = ("user", "buys", "item")
+    P, K, d = 16, 8, 64
+    ps, pd = _t(rng.integers(0, 30, P)), _t(rng.integers(0, 60, P))
+    nd = _t(rng.integers(0, 60, P * K))
+    nodes = {"user": _t(np.arange(30)), "item": _t(np.arange(60))}
+    h = {"user": _t(rng.standard_normal((30, d)).astype(np.float32)),
+         "item": _t(rng.standard_normal((60, d)).astype(np.float32))}
+    pos_g = PairGraph({ce: (ps, pd)}, nodes)
+    ns = ps.repeat_interleave(K)
+    neg_g = PairGraph({ce: (ns, nd)}, nodes)
+    neg_g.src_repeats_pos = K
+    assert neg_g.src_repeats(ce, ns) == K
+    other = _t(rng.integers(0, 30, P * K))
+    ns.copy_(other)  # edited after marking: the mark no longer holds
+    assert neg_g.src_repeats(ce, ns) is None
+    head = gnn.CosinePrediction()
+    with torch.no_grad():
+        _, b = head.pair(pos_g, neg_g, h)
+        want = ops.sddmm_cos(other, nd, h["user"], h["item"])
+    assert torch.equal(b[ce][:, 0], want)
+    bad = PairGraph({ce: (other.clone(), nd)}, nodes)
+    bad.src_repeats_pos = K  # marked, but not repeats
+    old = gnn.CHECK_GROUPED_PAIRS
+    gnn.CHECK_GROUPED_PAIRS = True
+    try:
+        with pytest.raises(ValueError, match="repeated"):
+            with torch.no_grad():
+                head.pair(pos_g, bad, h)
+    finally:
+        gnn.CHECK_GROUPED_PAIRS = old
