@@ -42,12 +42,15 @@ namespace {
 constexpr int kSbBlock = 256;
 constexpr int64_t kDumpEdges = 2048;  // a static block's dump row: at most ops.DEFAULT_SPLIT
 constexpr int kScanThreads = 1024;
+constexpr int kStrideBlocks = 2048;  // grid-stride sections (static padding): 8 per CU
 constexpr int kMaxSec = 4 * GNNREC_SB_MAX_TYPES + 2 * GNNREC_SB_MAX_RELS;
 
 struct RelArgs {
   const int64_t* indptr;
   const int32_t* indices;
   const int64_t* eids;
+  const uint64_t* rec;  // packed {eid << 32 | src} per CSR edge (NULL: indices / eids); the
+                        // picks then go to pick_eid packed the same way (pick_src unused)
   const uint8_t* excl_mask;  // NULL: nothing excluded in this call
   const uint8_t* excl_rows;
   int src_t, dst_t;
@@ -78,6 +81,12 @@ struct TypeArgs {
   unsigned long long* pos_next;  // the next step's (written by finalize)
   unsigned long long* bits_cur;
   unsigned long long* bits_next;
+  // this step's seeds as one byte per node (set by begin / the previous finalize, by plain
+  // byte stores like the new-source marks), the next step's written by finalize: the pick's
+  // "is this source a seed" test reads a byte of a 1 MB array (a 1M-node type), not the
+  // 8-byte stamped position of a random node (an 8 MB array)
+  uint8_t* smark_cur;
+  uint8_t* smark_next;
   uint8_t* mark_cur;       // new-source marks, one byte per node (64 * words), alternating
   uint8_t* mark_next;
   int64_t* word_rank;
@@ -119,7 +128,8 @@ struct StepArgs {
 };
 
 enum { kSecSeedPos, kSecZeroBits, kSecExclSet, kSecPick, kSecZeroNext, kSecCompact,
-       kSecNewNodes, kSecPrefix, kSecExclClear, kSecDumpEdges, kSecPadNodes, kSecZeroScan };
+       kSecNewNodes, kSecPrefix, kSecExclClear, kSecDumpEdges, kSecPadNodes, kSecZeroScan,
+       kSecSeedClear };
 
 // (stamp << 32) | ~position: the atomicMax of two writes of one stamp keeps the smaller
 // position, and any write of a newer stamp beats every older entry
@@ -172,7 +182,10 @@ __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
       const TypeArgs& T = A.type[i];
       if (t >= T.n_seeds_host) break;
       const int64_t v = T.seeds[t];
-      if (v >= 0) set_pos(T.pos_cur, v, A.stamp, t);
+      if (v >= 0) {
+        set_pos(T.pos_cur, v, A.stamp, t);
+        T.smark_cur[v] = 1;  // (zero: the previous call's last finalize cleared it)
+      }
       // static shapes: the real seeds' count = the end of the non-negative prefix (one
       // writer: the last real seed, or slot 0 when there is none)
       if (A.stat && ((v >= 0 && (t + 1 == T.n_seeds_host || T.seeds[t + 1] < 0)) ||
@@ -199,14 +212,76 @@ __global__ __launch_bounds__(kSbBlock) void sb_begin_kernel(StepArgs A) {
 }
 
 // ---------------------------------------------------------------- pick (step s)
+// A group of G lanes per seed, SPG seeds per group: each of the seed -> indptr -> record
+// chain's loads is issued for all SPG seeds before any is consumed, so a wave keeps
+// SPG x (64 / G) seeds' round trips in flight (the kernel is bound by those dependent round
+// trips: the K = 2500 first block's 0.8M seeds at one seed per group ran at 3 TB/s).  Each
+// seed's picks, slots and counts are exactly the one-seed form's.
+constexpr int kPickSpg = 2;
+
+// Floyd's fanout of one seed's row (sampler.hpp floyd_pick: the same candidates, the same
+// duplicate resolution, the same picks) with the group's candidates exchanged through LDS:
+// each lane stores its step's candidate, every lane reads the group's G candidates back with
+// G/4 broadcast ds_read_b128, and the k sequential duplicate checks run on registers and
+// ballots — where floyd_pick spent two ds_bpermute per step (64-bit __shfl), the LDS pipe
+// that bounded the pick kernel.  Positions fit 31 bits (a row holds < 2^31 edges).
 template <int G>
+__device__ __forceinline__ int floyd_pick_lds(const Group<G>& grp, uint64_t key, int64_t v,
+                                              int64_t deg, int k, int* __restrict__ sh) {
+  const int64_t jl = deg - k + grp.lane;  // this lane's step (valid for lane < k)
+  const int tl = grp.lane < k ? (int)(hash3(key, (uint64_t)v, (uint64_t)jl) % (uint64_t)(jl + 1))
+                              : -1;
+  sh[grp.lane] = tl;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  int t[G];
+#pragma unroll
+  for (int q = 0; q < G / 4; ++q) {
+    const int4 x = reinterpret_cast<const int4*>(sh)[q];
+    t[4 * q] = x.x;
+    t[4 * q + 1] = x.y;
+    t[4 * q + 2] = x.z;
+    t[4 * q + 3] = x.w;
+  }
+  int mine = -1;
+#pragma unroll
+  for (int s = 0; s < G; ++s) {
+    if (s < k) {
+      const bool dup = grp.ballot(grp.lane < s && mine == t[s]) != 0ull;
+      if (grp.lane == s) mine = dup ? (int)jl : t[s];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // sh is rewritten next
+  return mine;  // lanes >= k: -1
+}
+
+// a kept pick's slot in its row: the kept picks at smaller positions (picks are distinct),
+// from the group's positions exchanged through LDS (not kept: INT_MAX, counted by no lane)
+template <int G>
+__device__ __forceinline__ int kept_rank_lds(const Group<G>& grp, bool keep, int pos,
+                                             int* __restrict__ sh) {
+  sh[grp.lane] = keep ? pos : 0x7fffffff;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  int slot = 0;
+#pragma unroll
+  for (int q = 0; q < G / 4; ++q) {
+    const int4 x = reinterpret_cast<const int4*>(sh)[q];
+    slot += (x.x < pos) + (x.y < pos) + (x.z < pos) + (x.w < pos);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  return slot;
+}
+
+template <int G, int SPG>
 __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
   const int k = A.sec.find((int)blockIdx.x);
   const int b = (int)blockIdx.x - A.sec.begin[k];
-  if (A.sec.kind[k] == kSecZeroNext) {  // the next step's marks
+  if (A.sec.kind[k] == kSecZeroNext) {  // the next step's new-source and seed marks
     const TypeArgs& T = A.type[A.sec.idx[k]];
     const int64_t w = (int64_t)b * kSbBlock + threadIdx.x;
-    if (w < T.words * 4) reinterpret_cast<uint4*>(T.mark_next)[w] = make_uint4(0, 0, 0, 0);
+    if (w < T.words * 4) {
+      reinterpret_cast<uint4*>(T.mark_next)[w] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(T.smark_next)[w] = make_uint4(0, 0, 0, 0);
+    }
     return;
   }
   if (A.sec.kind[k] == kSecZeroScan) {  // the scan's tickets and tile flags, for this step
@@ -218,54 +293,90 @@ __global__ __launch_bounds__(kSbBlock) void sb_pick_kernel(StepArgs A) {
   const TypeArgs& D = A.type[R.dst_t];
   const TypeArgs& S = A.type[R.src_t];
   const Group<G> grp;
-  const int64_t i = (int64_t)b * (kSbBlock / G) + (threadIdx.x / G);
-  if (i >= seed_rows(A, D)) return;  // group-uniform
-  const int64_t v = D.seeds[i];
-  if (v < 0) {  // a padding seed (static shapes): its row holds `fanout` padding edges
-    if (grp.lane == 0) R.counts[i] = R.fanout;
-    return;
-  }
-  const int64_t beg = R.indptr[v], end = R.indptr[v + 1], deg = end - beg;
-  const uint8_t* const excluded =
-      R.excl_mask && (!R.excl_rows || R.excl_rows[v]) ? R.excl_mask : nullptr;
+  __shared__ int4 sh_all[kSbBlock / 4];  // G ints per group: candidates, then positions
+  int* const sh = reinterpret_cast<int*>(sh_all) + (threadIdx.x & ~(G - 1));
+  const int64_t rows = seed_rows(A, D);
+  const int64_t i0 = ((int64_t)b * (kSbBlock / G) + (threadIdx.x / G)) * SPG;
+  if (i0 >= rows) return;  // group-uniform
   const int64_t f = R.fanout;
-  bool keep;
-  int slot, c;
-  int32_t src = 0;
-  int64_t id = 0;
-  if (deg <= f) {  // the whole row (deg <= fanout <= G: one chunk), in edge order
-    const int64_t e = beg + grp.lane;
-    const bool valid = e < end;
-    id = valid ? R.eids[e] : 0;
-    src = valid ? R.indices[e] : 0;
-    keep = valid && !(excluded && excluded[id]);
-    const uint64_t m = grp.ballot(keep);
-    slot = grp.below(m);
-    c = __popcll(m);
-  } else {  // fanout of deg by Floyd's algorithm, kept picks in position order
-    const int kf = (int)f;
-    const int64_t p = floyd_pick(grp, R.key, v, deg, kf);
-    const bool valid = p >= 0;
-    const int64_t e = beg + (valid ? p : 0);
-    id = valid ? R.eids[e] : 0;
-    src = valid ? R.indices[e] : 0;
-    keep = valid && !(excluded && excluded[id]);
-    slot = 0;
-    for (int r = 0; r < kf; ++r) {
-      const int64_t pr = __shfl(p, grp.base + r);
-      const int kr = __shfl((int)keep, grp.base + r);
-      slot += (kr && pr < p) ? 1 : 0;
+  const int kf = (int)f;
+  int64_t v[SPG], beg[SPG], end[SPG];
+  const uint8_t* excluded[SPG];
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) v[u] = i0 + u < rows ? D.seeds[i0 + u] : -2;  // -2: no row
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) {
+    beg[u] = end[u] = 0;
+    excluded[u] = nullptr;
+    if (v[u] >= 0) {
+      beg[u] = R.indptr[v[u]];
+      end[u] = R.indptr[v[u] + 1];
+      excluded[u] = R.excl_mask && (!R.excl_rows || R.excl_rows[v[u]]) ? R.excl_mask : nullptr;
     }
-    c = __popcll(grp.ballot(keep));
   }
-  if (keep) {
-    const int64_t q = i * f + slot;
-    R.pick_src[q] = src;
-    R.pick_eid[q] = id;
-    // a source that is not one of its type's seeds at this step is a new node
-    if ((uint32_t)(S.pos_cur[src] >> 32) != A.stamp) S.mark_cur[src] = 1;
+  // each seed's pick position: the whole row (deg <= fanout <= G: one chunk, in edge order)
+  // or Floyd's fanout of deg (lanes >= fanout: -1)
+  int64_t pos[SPG];
+  bool whole[SPG];
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) {
+    const int64_t deg = end[u] - beg[u];
+    whole[u] = deg <= f;
+    if (v[u] < 0) pos[u] = -1;
+    else if (whole[u]) pos[u] = grp.lane < deg ? grp.lane : -1;
+    else pos[u] = floyd_pick_lds(grp, R.key, v[u], deg, kf, sh);
   }
-  if (grp.lane == 0) R.counts[i] = c;
+  // the picked edges: one packed record, or the index and the eid
+  int32_t src[SPG];
+  int64_t id[SPG];
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) {
+    src[u] = 0;
+    id[u] = 0;
+    if (pos[u] >= 0) {
+      const int64_t e = beg[u] + pos[u];
+      if (R.rec != nullptr) {
+        const uint64_t r = R.rec[e];
+        src[u] = (int32_t)(uint32_t)r;
+        id[u] = (int64_t)(r >> 32);
+      } else {
+        id[u] = R.eids[e];
+        src[u] = R.indices[e];
+      }
+    }
+  }
+  bool keep[SPG];
+  uint8_t is_seed[SPG];
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) {
+    keep[u] = pos[u] >= 0 && !(excluded[u] && excluded[u][id[u]]);
+    is_seed[u] = keep[u] ? S.smark_cur[src[u]] : 1;  // (issued for every seed first)
+  }
+#pragma unroll
+  for (int u = 0; u < SPG; ++u) {
+    const int64_t i = i0 + u;
+    if (v[u] == -2) continue;  // group-uniform
+    if (v[u] < 0) {  // a padding seed (static shapes): its row holds `fanout` padding edges
+      if (grp.lane == 0) R.counts[i] = f;
+      continue;
+    }
+    int slot;
+    const uint64_t m = grp.ballot(keep[u]);
+    if (whole[u]) slot = grp.below(m);
+    else slot = kept_rank_lds(grp, keep[u], (int)pos[u], sh);  // kept picks in position order
+    if (keep[u]) {
+      const int64_t q = i * f + slot;
+      if (R.rec != nullptr) {
+        R.pick_eid[q] = (int64_t)(((uint64_t)id[u] << 32) | (uint32_t)src[u]);
+      } else {
+        R.pick_src[q] = src[u];
+        R.pick_eid[q] = id[u];
+      }
+      // a source that is not one of its type's seeds at this step is a new node
+      if (!is_seed[u]) S.mark_cur[src[u]] = 1;
+    }
+    if (grp.lane == 0) R.counts[i] = __popcll(m);
+  }
 }
 
 // ---------------------------------------------------------------- scan (step s)
@@ -436,10 +547,13 @@ __global__ __launch_bounds__(kScanThreads) void sb_scan_kernel(StepArgs A) {
 // n_p: where the new sources start (the real seeds' count)
 __device__ __forceinline__ int64_t local_id(const TypeArgs& T, int64_t n_p, uint32_t stamp,
                                             int32_t s) {
+  // the position and the rank words requested together: one round trip, not two
+  const int64_t w = s >> 6;
   const unsigned long long v = T.pos_cur[s];
+  const int64_t rank = T.word_rank[w];
+  const unsigned long long bw = T.bits_cur[w];
   if ((uint32_t)(v >> 32) == stamp) return pos_of(v);  // one of this step's seeds
-  const int64_t w = s >> 6;                           // a new source: its rank among them
-  return n_p + T.word_rank[w] + __popcll(T.bits_cur[w] & ((1ull << (s & 63)) - 1ull));
+  return n_p + rank + __popcll(bw & ((1ull << (s & 63)) - 1ull));  // a new source: its rank
 }
 
 // static shapes: the source slot of padding edge k — spread over the list's padding slots
@@ -460,34 +574,58 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       const TypeArgs& D = A.type[R.dst_t];
       const TypeArgs& S = A.type[R.src_t];
       const int64_t i = t / R.fanout, j = t - i * R.fanout;
-      if (i >= seed_rows(A, D) || j >= R.counts[i]) return;
-      const int64_t o = R.out_indptr[i] + j;
-      if (D.seeds[i] < 0) {  // a padding row's padding edge
+      if (i >= seed_rows(A, D)) return;
+      // the slot's loads requested together before any of them is tested (the pick slot
+      // may be unwritten past the row's count: read, not used)
+      const int64_t cnt = R.counts[i];
+      const int64_t row0 = R.out_indptr[i];
+      const int64_t seed = D.seeds[i];
+      int32_t ps;
+      int64_t pe;
+      if (R.rec != nullptr) {
+        const uint64_t pk = (uint64_t)R.pick_eid[t];
+        ps = (int32_t)(uint32_t)pk;
+        pe = (int64_t)(pk >> 32);
+      } else {
+        ps = R.pick_src[t];
+        pe = R.pick_eid[t];
+      }
+      if (j >= cnt) return;
+      const int64_t o = row0 + j;
+      if (seed < 0) {  // a padding row's padding edge
         R.out_src[o] = pad_src(S, o);
         R.out_eid[o] = -1;
         break;
       }
-      int64_t loc = local_id(S, *S.n_seeds, A.stamp, R.pick_src[t]);
+      int64_t loc = local_id(S, *S.n_seeds, A.stamp, ps);
       if (A.stat && loc >= S.node_cap - 1) {  // past a hinted capacity: a padding slot
         if (A.overflow) *A.overflow = 1;
         loc = S.node_cap - 1;
       }
       R.out_src[o] = (int32_t)loc;
-      R.out_eid[o] = R.pick_eid[t];
+      R.out_eid[o] = pe;
       break;
     }
     case kSecDumpEdges: {  // static shapes: the edge capacity's rest -> the dump rows
+      // (a grid-stride section of at most kStrideBlocks blocks: the rest is known only
+      // here, and a grid covering the whole capacity was mostly idle threads)
       const RelArgs& R = A.rel[x];
-      const int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t;
-      if (e >= R.edge_cap) return;
-      R.out_src[e] = pad_src(A.type[R.src_t], e);
-      R.out_eid[e] = -1;
+      const TypeArgs& S = A.type[R.src_t];
+      const int64_t nth = (int64_t)(A.sec.begin[k + 1] - A.sec.begin[k]) * kSbBlock;
+      const int64_t real = min(*S.n_seeds + S.word_rank[S.words], S.node_cap - 1);
+      const int64_t span = S.node_len - real;  // pad_src's slots, read once
+      for (int64_t e = R.out_indptr[A.type[R.dst_t].seed_cap] + t; e < R.edge_cap; e += nth) {
+        R.out_src[e] = (int32_t)(real + e % span);
+        R.out_eid[e] = -1;
+      }
       break;
     }
     case kSecPadNodes: {  // static shapes: the list past the real seeds and new sources
       const TypeArgs& T = A.type[x];
-      const int64_t p = min(*T.n_seeds + T.word_rank[T.words], T.node_cap - 1) + t;
-      if (p < T.node_len) T.nodes[p] = -1;
+      const int64_t nth = (int64_t)(A.sec.begin[k + 1] - A.sec.begin[k]) * kSbBlock;
+      for (int64_t p = min(*T.n_seeds + T.word_rank[T.words], T.node_cap - 1) + t;
+           p < T.node_len; p += nth)
+        T.nodes[p] = -1;
       break;
     }
     case kSecNewNodes: {  // bitmap word t -> its new nodes, ascending, after the seeds
@@ -504,6 +642,7 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
         }
         T.nodes[p] = id;
         T.pos_next[id] = pack_pos(A.stamp + 1u, p);  // (new ids are distinct)
+        if (!A.last) T.smark_next[id] = 1;
         word &= word - 1ull;
         ++p;
       }
@@ -514,7 +653,15 @@ __global__ __launch_bounds__(kSbBlock) void sb_finalize_kernel(StepArgs A) {
       if (t >= *T.n_seeds) return;
       const int64_t id = T.seeds[t];
       T.nodes[t] = id;
-      if (id >= 0) set_pos(T.pos_next, id, A.stamp + 1u, t);
+      if (id >= 0) {
+        set_pos(T.pos_next, id, A.stamp + 1u, t);
+        if (!A.last) T.smark_next[id] = 1;
+      }
+      break;
+    }
+    case kSecSeedClear: {  // the last step: its seed marks are the next call's step-0 marks
+      const TypeArgs& T = A.type[x];
+      if (t < T.words * 4) reinterpret_cast<uint4*>(T.smark_cur)[t] = make_uint4(0, 0, 0, 0);
       break;
     }
     case kSecExclClear: {
@@ -772,7 +919,8 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
   }
   for (int r = 0; r < R; ++r) {
     const gnnrec_sample_rel& re = P->rel[r];
-    GNNREC_REQUIRE(re.indptr && re.indices && re.eids, "gnnrec_sample_blocks: relation %d: null CSR", r);
+    GNNREC_REQUIRE(re.indptr && ((re.indices && re.eids) || re.edge_rec),
+                   "gnnrec_sample_blocks: relation %d: null CSR", r);
     GNNREC_REQUIRE(re.n_excl == 0 || (re.excl_eids && re.coo_dst && re.excl_mask && re.excl_rows),
                    "gnnrec_sample_blocks: relation %d: exclusion needs eids, coo_dst and flags", r);
     for (int s = 0; s < L; ++s)
@@ -833,6 +981,8 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.bits_next = reinterpret_cast<unsigned long long*>(ty.bits) + ((A.stamp + 1u) & 1u) * W;
       a.mark_cur = ty.marks + (A.stamp & 1u) * 64 * W;
       a.mark_next = ty.marks + ((A.stamp + 1u) & 1u) * 64 * W;
+      a.smark_cur = ty.marks + (2 + (A.stamp & 1u)) * 64 * W;
+      a.smark_next = ty.marks + (2 + ((A.stamp + 1u) & 1u)) * 64 * W;
       a.word_rank = ty.word_rank;
       a.words = W;
       a.nodes = P->nodes[s][t];
@@ -846,6 +996,7 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
       a.indptr = re.indptr;
       a.indices = re.indices;
       a.eids = re.eids;
+      a.rec = re.edge_rec;
       a.excl_mask = re.n_excl ? re.excl_mask : nullptr;
       a.excl_rows = re.n_excl ? re.excl_rows : nullptr;
       a.src_t = re.src_type;
@@ -897,18 +1048,19 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     // pick
     A.sec.n = 0;
     A.sec.begin[0] = 0;
-    for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r)  // kPickSpg seeds per group of G lanes
       add_sec(A.sec, kSecPick, r,
-              (int)((C.seed[s][P->rel[r].dst_type] + kSbBlock / G - 1) / (kSbBlock / G)));
+              (int)((C.seed[s][P->rel[r].dst_type] + kPickSpg * (kSbBlock / G) - 1) /
+                    (kPickSpg * (kSbBlock / G))));
     for (int t = 0; t < T; ++t) add_sec(A.sec, kSecZeroNext, t, nblocks(4 * A.type[t].words));
     add_sec(A.sec, kSecZeroScan, 0, nblocks(A.scan_words));
     if (A.sec.n) {
       const dim3 grid((unsigned)A.sec.begin[A.sec.n]);
       switch (G) {
-        case 8: hipLaunchKernelGGL(sb_pick_kernel<8>, grid, dim3(kSbBlock), 0, hs, A); break;
-        case 16: hipLaunchKernelGGL(sb_pick_kernel<16>, grid, dim3(kSbBlock), 0, hs, A); break;
-        case 32: hipLaunchKernelGGL(sb_pick_kernel<32>, grid, dim3(kSbBlock), 0, hs, A); break;
-        default: hipLaunchKernelGGL(sb_pick_kernel<64>, grid, dim3(kSbBlock), 0, hs, A); break;
+        case 8: hipLaunchKernelGGL((sb_pick_kernel<8, kPickSpg>), grid, dim3(kSbBlock), 0, hs, A); break;
+        case 16: hipLaunchKernelGGL((sb_pick_kernel<16, kPickSpg>), grid, dim3(kSbBlock), 0, hs, A); break;
+        case 32: hipLaunchKernelGGL((sb_pick_kernel<32, kPickSpg>), grid, dim3(kSbBlock), 0, hs, A); break;
+        default: hipLaunchKernelGGL((sb_pick_kernel<64, kPickSpg>), grid, dim3(kSbBlock), 0, hs, A); break;
       }
       if (int st = check_launch("gnnrec_sample_blocks(pick)")) return st;
     }
@@ -923,11 +1075,14 @@ extern "C" int gnnrec_sample_blocks(const gnnrec_sample_plan* P, void* stream) {
     for (int t = 0; t < T; ++t) add_sec(A.sec, kSecNewNodes, t, nblocks(A.type[t].words));
     for (int t = 0; t < T; ++t) add_sec(A.sec, kSecPrefix, t, nblocks(C.seed[s][t]));
     if (s == L - 1)
+      for (int t = 0; t < T; ++t) add_sec(A.sec, kSecSeedClear, t, nblocks(4 * A.type[t].words));
+    if (s == L - 1)
       for (int r = 0; r < R; ++r) add_sec(A.sec, kSecExclClear, r, nblocks(P->rel[r].n_excl));
     if (P->static_shapes) {
-      for (int r = 0; r < R; ++r) add_sec(A.sec, kSecDumpEdges, r, nblocks(C.edge[s][r]));
+      for (int r = 0; r < R; ++r)
+        add_sec(A.sec, kSecDumpEdges, r, std::min(nblocks(C.edge[s][r]), kStrideBlocks));
       for (int t = 0; t < T; ++t)
-        add_sec(A.sec, kSecPadNodes, t, nblocks(C.len[s][t]));
+        add_sec(A.sec, kSecPadNodes, t, std::min(nblocks(C.len[s][t]), kStrideBlocks));
     }
     if (A.sec.n) {
       hipLaunchKernelGGL(sb_finalize_kernel, dim3((unsigned)A.sec.begin[A.sec.n]), dim3(kSbBlock),

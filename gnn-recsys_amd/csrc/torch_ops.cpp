@@ -1584,9 +1584,12 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
               const optional<Tensor>& sizes_out,
               at::IntArrayRef node_cap_hint, const optional<Tensor>& overflow,
               at::TensorList edge_tables, at::IntArrayRef edge_table_rel,
-              at::TensorList node_tables, at::IntArrayRef node_table_type) {
+              at::TensorList node_tables, at::IntArrayRef node_table_type,
+              at::TensorList edge_recs) {
   const OneDevice one_device_;
   const size_t R = indptrs.size(), NT = n_nodes.size();
+  TORCH_CHECK_VALUE(edge_recs.empty() || edge_recs.size() == R,
+                    "sample_blocks: edge_recs holds one packed record array per relation or none");
   TORCH_CHECK_VALUE(indices.size() == R && eids.size() == R && src_type.size() == R &&
                         dst_type.size() == R && excl_eids.size() == R && coo_dst.size() == R &&
                         excl_masks.size() == R && excl_rows.size() == R,
@@ -1632,6 +1635,12 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     re.indptr = p<int64_t>(indptrs[r]);
     re.indices = p<int32_t>(indices[r]);
     re.eids = p<int64_t>(eids[r]);
+    if (!edge_recs.empty()) {  // {eid << 32 | src} per CSR edge (HeteroGraph.edge_records)
+      dev(edge_recs[r], "edge_recs", at::kLong);
+      TORCH_CHECK_VALUE(edge_recs[r].is_contiguous() && edge_recs[r].numel() == eids[r].numel(),
+                        "sample_blocks: relation ", r, ": edge_recs must hold one record per edge");
+      re.edge_rec = p<uint64_t>(edge_recs[r]);
+    }
     re.src_type = (int32_t)src_type[r];
     re.dst_type = (int32_t)dst_type[r];
     const optional<Tensor> xe = excl_eids.get(r), cd = coo_dst.get(r), xm = excl_masks.get(r),
@@ -1668,9 +1677,9 @@ sample_blocks(at::TensorList indptrs, at::TensorList indices, at::TensorList eid
     const int64_t W = (n_nodes[t] + 63) / 64;
     TORCH_CHECK_VALUE(seeds[t].is_contiguous() && pos[t].numel() == 2 * n_nodes[t] &&
                           bits[t].numel() == 2 * W && word_rank[t].numel() == W + 1 &&
-                          marks[t].numel() == 2 * 64 * W,
+                          marks[t].numel() == 4 * 64 * W,
                       "sample_blocks: type ", t,
-                      ": scratch sized 2n, 2 ceil(n/64), ceil(n/64)+1, 128 ceil(n/64) bytes");
+                      ": scratch sized 2n, 2 ceil(n/64), ceil(n/64)+1, 256 ceil(n/64) bytes");
     gnnrec_sample_type& ty = P.type[t];
     ty.n_nodes = n_nodes[t];
     ty.seeds = p<int64_t>(seeds[t]);
@@ -2198,7 +2207,7 @@ TORCH_LIBRARY(gnnrec, m) {
         "int[] keys, int steps, "
         "int stamp, bool static_shapes, Tensor(d!)? sizes_out, int[] node_cap_hint, "
         "Tensor(e!)? overflow, Tensor[] edge_tables, int[] edge_table_rel, Tensor[] node_tables, "
-        "int[] node_table_type) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
+        "int[] node_table_type, Tensor[] edge_recs) -> (Tensor[] out_indptr, Tensor[] src_local, Tensor[] eids, "
         "Tensor[] src_nid, int[] sizes, Tensor[] data)");
   m.def("gather_rows_batch(Tensor[] src, Tensor[] idx, Tensor(a!)[] out, Tensor[] n_dev) -> ()");
   m.def("copy_batch(Tensor[] src, Tensor(a!)[] dst) -> ()");

@@ -180,6 +180,7 @@ class HeteroGraph:
         self._edata = {ce: _FrameDict() for ce in self.canonical_etypes}
         self._csr = {}
         self._csr_edata = {}
+        self._edge_rec = {}
         self.nodes = _TypeAccessor(self._ndata, lambda k: k)
         self.edges = _TypeAccessor(self._edata, self.to_canonical_etype)
         self.device = torch.device(device) if device is not None else (
@@ -259,6 +260,20 @@ class HeteroGraph:
         """CSR for sampling: (indptr, src global ids int32, eids) -- the cached in_csr
         arrays themselves (the sampler widens ids to int64 as it copies them)."""
         return self.in_csr(etype)
+
+    def edge_records(self, etype) -> Optional[torch.Tensor]:
+        """The in-CSR's edges as packed 8-byte records for the fused sampler, cached:
+        rec[e] = eids[e] << 32 | indices[e] (include/gnnrec.h gnnrec_sample_rel.edge_rec) —
+        a fanout pick reads one record (one cache line) instead of a line of each array.
+        None when an eid does not fit 31 bits (the sampler then reads the two arrays)."""
+        ce = self.to_canonical_etype(etype)
+        if ce not in self._edge_rec:
+            _ip, ix, eid = self.in_csr(ce)
+            rec = None
+            if eid.numel() < (1 << 31) and eid.is_cuda:
+                rec = (eid << 32) | ix.to(torch.int64)  # ids >= 0: no sign bits to mask
+            self._edge_rec[ce] = rec
+        return self._edge_rec[ce]
 
     def in_degrees(self, etype) -> torch.Tensor:
         indptr = self.in_csr(etype)[0]

@@ -1284,7 +1284,7 @@ GATHER_MAX_JOBS = 16
 class SampleScratch:
     """Per-node-type state of the fused sampler (gnnrec_sample_blocks, include/gnnrec.h):
     `pos` (two arrays of stamped seed positions, used alternately, never cleared), two
-    new-source bitmaps and their word ranks.  `stamp` advances by steps + 1 per call; before it would wrap, `pos` is zeroed
+    new-source bitmaps and their word ranks, new-source and seed byte marks (two each).  `stamp` advances by steps + 1 per call; before it would wrap, `pos` is zeroed
     and the count restarts (one memset per ~4e9 sampled layers)."""
 
     def __init__(self, n_nodes: int, device):
@@ -1293,12 +1293,13 @@ class SampleScratch:
         self.pos = torch.zeros(2 * n_nodes, dtype=torch.int64, device=device)
         self.bits = torch.zeros(2 * w, dtype=torch.int64, device=device)
         self.word_rank = torch.empty(w + 1, dtype=torch.int64, device=device)
-        self.marks = torch.zeros(2 * 64 * w, dtype=torch.uint8, device=device)
+        # two new-source mark arrays, then two seed mark arrays (each pair used alternately)
+        self.marks = torch.zeros(4 * 64 * w, dtype=torch.uint8, device=device)
 
 
 def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, seeds, scratch,
                   fanouts, keys, stamp, static_shapes=False, sizes_out=None, node_cap_hint=None,
-                  overflow=None, edge_tables=(), node_tables=()):
+                  overflow=None, edge_tables=(), node_tables=(), edge_recs=()):
     """a9, every block of one bounded-fanout sample_blocks call (gnnrec::sample_blocks,
     1 + 3L launches, one host size read).  fanouts / keys: [step][relation] (step 0 = the
     output block); excl: per relation None or (eids, coo_dst, mask, rows).
@@ -1315,7 +1316,8 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
     edge_tables [(table, relation)] / node_tables [(table, node type)]: the block data (a10),
     gathered inside the call — every step's edge data at its edge ids, the input block's
     (the last step's) node rows at its source ids — returned as a third value in that order
-    (step-major for the edge tables)."""
+    (step-major for the edge tables).  edge_recs: per relation the packed {eid << 32 | src}
+    records of its CSR (HeteroGraph.edge_records), or empty (the index / eid arrays)."""
     steps, R = len(fanouts), len(indptrs)
     ex = [e if e is not None else (None,) * 4 for e in excl]
     o_ip, o_src, o_eid, nodes, sizes, data = _T().sample_blocks(
@@ -1327,7 +1329,7 @@ def sample_blocks(indptrs, indices, eids, src_type, dst_type, excl, n_nodes, see
         [_lib.i64(k) for ks in keys for k in ks], steps, int(stamp), bool(static_shapes),
         sizes_out, [int(h) for hs in (node_cap_hint or []) for h in hs], overflow,
         [t for t, _ in edge_tables], [int(r) for _, r in edge_tables],
-        [t for t, _ in node_tables], [int(x) for _, x in node_tables])
+        [t for t, _ in node_tables], [int(x) for _, x in node_tables], list(edge_recs))
     NT = len(n_nodes)
     out = []
     for s in range(steps):

@@ -59,6 +59,10 @@ class BlockSampler:
         # bounded fanouts: every block of a call in one fused op (ops.sample_blocks); False
         # keeps the per-layer ops (the blocks are bitwise the same; tests compare the two)
         self.fused = True
+        # the fused sampler reads the CSR as packed 8-byte edge records (HeteroGraph
+        # .edge_records) when every eid fits 31 bits; False: the index and eid arrays
+        # (bitwise the same blocks; tests compare the two)
+        self.packed = True
         self._sb_scratch = {}
         self._stamp = 1
         # the first block's source-major CSRs (sample_blocks(transposes=True)) are skipped
@@ -112,6 +116,14 @@ class BlockSampler:
             return False
         return all(0 <= self._fanout(b, ce) <= ops.SB_MAX_FANOUT
                    for b in range(self.num_layers) for ce in ces)
+
+    def _edge_recs(self, g, ces):
+        """The packed edge records of every relation (HeteroGraph.edge_records), or [] —
+        the fused sampler then reads the index and eid arrays (the same picks and blocks)."""
+        if not self.packed or not hasattr(g, "edge_records"):
+            return []
+        recs = [g.edge_records(ce) for ce in ces]
+        return [] if any(r is None for r in recs) else recs
 
     def _sample_fused(self, g, seeds, exclude_eids, transposes, static=False, hints=None,
                       overflow=None):
@@ -172,7 +184,8 @@ class BlockSampler:
             node_cap_hint=[[(hints or {}).get((s_, nt), 0) for nt in nts] for s_ in range(L)]
             if hints else None, overflow=overflow,
             edge_tables=[(v, ces.index(ce)) for ce, _k, v in etab],
-            node_tables=[(v, tix[nt]) for nt, _k, v in ntab])
+            node_tables=[(v, tix[nt]) for nt, _k, v in ntab],
+            edge_recs=self._edge_recs(g, ces))
         blocks = []
         for s_, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
             rels = {}

@@ -456,6 +456,11 @@ typedef struct gnnrec_sample_rel {
   const int64_t* coo_dst; /* [E] dst of every eid (for the excluded eids' dst rows) */
   uint8_t* excl_mask;     /* [E] flags, zero between calls */
   uint8_t* excl_rows;     /* [n_dst] flags, zero between calls */
+  /* optional (NULL: read indices / eids): the CSR's edges as one 8-byte record each,
+   * rec[e] = (uint64)eids[e] << 32 | (uint32)indices[e] (every eid < 2^31) — a pick then
+   * reads ONE record, one cache line, where the two arrays cost two (a fanout pick from a
+   * long row touches a line of each per edge); the same picks and outputs either way */
+  const uint64_t* edge_rec;
 } gnnrec_sample_rel;
 
 typedef struct gnnrec_sample_type {
@@ -465,9 +470,11 @@ typedef struct gnnrec_sample_type {
   int64_t* pos;         /* scratch, see above: [2 * n_nodes] */
   uint64_t* bits;
   int64_t* word_rank;
-  uint8_t* marks;       /* scratch: [2 * 64 * ceil(n_nodes/64)] bytes, zero before the first
-                         * call, 16-byte aligned (new sources are marked by byte stores, the
-                         * scan packs them into `bits`) */
+  uint8_t* marks;       /* scratch: [4 * 64 * ceil(n_nodes/64)] bytes, zero before the first
+                         * call, 16-byte aligned: two new-source mark arrays (new sources are
+                         * marked by byte stores, the scan packs them into `bits`), then two
+                         * seed mark arrays (a step's seeds, one byte per node; each call
+                         * leaves them zero) */
 } gnnrec_sample_type;
 
 typedef struct gnnrec_sample_plan {

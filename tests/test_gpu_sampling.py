@@ -652,18 +652,23 @@ def _same_blocks(A, B):
                     assert torch.equal(x, y), ce
 
 
+@pytest.mark.parametrize("packed", [True, False])
 @pytest.mark.parametrize("fanouts", [[3, 2], [{"buys": 2, "bought-by": 4, "clicks": 0,
                                                "clicked-by": 64}, 1], [10, 10, 5], [1]])
-def test_fused_sample_blocks_equal_per_layer_path(fanouts):
+def test_fused_sample_blocks_equal_per_layer_path(fanouts, packed):
     """gnnrec_sample_blocks (every block of a call: 1 + 3L launches, one host read) builds the
     blocks of the per-layer path bit for bit — local ids, eids, node lists, edge data, input
     features and the training transposes — over consecutive calls (the stamped seed positions
     and the alternating bitmaps carried from call to call), seeds of one or both types,
     fanouts 0 / above the degree / per relation, and reverse-type exclusion, whose flags are
-    cleared again."""
+    cleared again.  packed: the CSR read as packed {eid, src} records (HeteroGraph
+    .edge_records, the default) or as the index and eid arrays."""
     from gnnrec.sampling import MultiLayerNeighborSampler
     g, edges = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
     fused = MultiLayerNeighborSampler(fanouts, seed=9)
+    fused.packed = packed
+    if packed:
+        assert len(fused._edge_recs(g, list(g.canonical_etypes))) == len(g.canonical_etypes)
     layer = MultiLayerNeighborSampler(fanouts, seed=9)
     layer.fused = False
     assert fused._fused_ok(g) and not layer._fused_ok(g)

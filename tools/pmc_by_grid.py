@@ -60,7 +60,7 @@ def main(d, pat=None):
         write = mean("WRITE_SIZE") / 1e3
         hit, miss = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
         rate = hit / (hit + miss) if hit == hit and miss == miss and hit + miss > 0 else float("nan")
-        tbs = (fetch + write) / avg / 1e3 if avg == avg and avg > 0 else float("nan")
+        tbs = (fetch + write) / avg if avg == avg and avg > 0 else float("nan")  # MB/us
         print(f"| {key[0]} | {key[1]} | {len(ts)} | {avg:.1f} | {fetch:.1f} | {write:.1f} | "
               f"{rate:.3f} | {tbs:.2f} |")
 
