@@ -33,6 +33,7 @@ from gnnrec.inference import RESERVE_CUS, ShardedFullGraphPass  # noqa: E402
 from gnnrec.synth import GraphMeta, bipartite_shard, node_features  # noqa: E402
 
 XGMI_GBS = 7 * 153.0
+LINK_FRACTIONS = (1.0, 0.5, 0.35, 0.25)  # of the links' peak an RCCL exchange may reach
 
 
 def rank_ms(P, r, split, dev, reps=3):
@@ -101,7 +102,12 @@ def main():
             "projected_ms_no_overlap": round(comp + comm_ms, 3),
             "projected_ms_full_overlap": round(max(comp, comm_ms), 3),
             # RCCL's all-to-all reaching half the links' rate, nothing overlapped
-            "projected_ms_half_rate_no_overlap": round(comp + 2 * comm_ms, 3)}
+            "projected_ms_half_rate_no_overlap": round(comp + 2 * comm_ms, 3),
+            # the exchange priced at a stated fraction of the 7 x 153 GB/s link peak, nothing
+            # overlapped (the pass overlaps the partial exchange with the item->user launch,
+            # so these are upper bounds on the pass time at that rate)
+            "projected_ms_by_link_fraction_no_overlap": {
+                str(f): round(comp + comm_ms / f, 3) for f in LINK_FRACTIONS}}
         print(json.dumps({"P": P, **{k: v for k, v in res["per_P"][str(P)].items()
                                      if k != "ranks"}}), flush=True)
     if "1" in res["per_P"]:
@@ -111,6 +117,8 @@ def main():
             v["speedup_full_overlap"] = round(base / v["projected_ms_full_overlap"], 2)
             v["speedup_half_rate_no_overlap"] = round(
                 base / v["projected_ms_half_rate_no_overlap"], 2)
+            v["speedup_by_link_fraction_no_overlap"] = {
+                f: round(base / ms, 2) for f, ms in v["projected_ms_by_link_fraction_no_overlap"].items()}
     out = json.dumps(res, indent=1)
     if a.out:
         open(a.out, "w").write(out)
