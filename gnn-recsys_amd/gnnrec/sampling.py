@@ -681,7 +681,11 @@ class EdgeDataLoader:
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     STATIC_LEARN = 3
-    STATIC_MARGIN = 1.1
+    # a batch's source-list sizes are sums of ~10^5-10^6 draws: their spread across batches
+    # is ~0.1-0.5 % (C2 K = 10 / 2500), so 3 % over the largest of the learned batches
+    # leaves ~10 standard deviations; every padded row costs the captured step's
+    # row-proportional kernels (GEMMs, weight gradients, norms, the feature gather)
+    STATIC_MARGIN = 1.03
 
     def _learn_caps(self, blocks):
         """Record an exact batch's source-list sizes per (step, node type); after
