@@ -3,7 +3,7 @@ with the sampling thread, exact shapes, fold 'auto'), N timed steps after 5 warm
 a kernel-stats difference between two N (tools/kstats_diff.py): the step's kernel budget
 loader included.
 
-    python tools/probe_eager_step.py [K] [N]
+    python tools/probe_eager_step.py [K] [N] [num_workers]
 """
 import json
 import os
@@ -21,6 +21,7 @@ def main():
     from gnnrec.synth import minibatch_graph
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 2500
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    nw = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     dev = torch.device("cuda")
     g = minibatch_graph(64, dev)
     buys = ("user", "buys", "item")
@@ -32,7 +33,7 @@ def main():
                         MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                         reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
-                        shuffle=True, num_workers=2)
+                        shuffle=True, num_workers=nw)
     it = iter(el)
 
     def step():

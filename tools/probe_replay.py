@@ -3,7 +3,7 @@ CapturedTrainStep, replay the graph N times with nothing else on the GPU, so tha
 `rocprofv3 --kernel-trace --stats` of this script is the replay's own kernel budget
 (totals / N per step).
 
-    python tools/probe_replay.py [K] [N]
+    python tools/probe_replay.py [K] [N] [caps: provable | auto]
 """
 import json
 import os
@@ -22,6 +22,7 @@ def main():
     from gnnrec.synth import minibatch_graph
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    caps = sys.argv[3] if len(sys.argv) > 3 else "provable"
     dev = torch.device("cuda")
     g = minibatch_graph(64, dev)
     buys = ("user", "buys", "item")
@@ -40,11 +41,11 @@ def main():
                         MultiLayerNeighborSampler([10, 10]), exclude="reverse_types",
                         reverse_etypes={"buys": "bought-by", "bought-by": "buys"},
                         negative_sampler=negative_sampler.Uniform(K), batch_size=1024,
-                        shuffle=True, static_shapes=True)
+                        shuffle=True, static_shapes=True, static_caps=caps)
     el.sampler.first_transposes_below = 0
     step = CapturedTrainStep(model, opt, loss_fn, warmup=2)
     it = iter(el)
-    for _ in range(5):
+    for _ in range(5 + (el.STATIC_LEARN if caps == "auto" else 0)):
         step(next(it))
     torch.cuda.synchronize()
     torch.cuda._sleep(1000)  # trace marker (tools/rocpd_timeline.py, rocpd_sequence.py)
@@ -56,7 +57,7 @@ def main():
     torch.cuda.synchronize()
     # host time of the replay calls alone (a launch that waits for the previous replay shows
     # here as the GPU time per replay)
-    print(json.dumps({"K": K, "replays": N, "ms_per_replay": (time.perf_counter() - t) / N * 1e3,
+    print(json.dumps({"K": K, "caps": caps, "replays": N, "ms_per_replay": (time.perf_counter() - t) / N * 1e3,
                       "host_ms_per_replay_call": host / N * 1e3}))
 
 
