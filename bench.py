@@ -1085,12 +1085,22 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
     ms_pq = ev_time(lambda: (ops.gemm(Hs, W1[:, :d], bias=pl.hidden_1.bias),
                              ops.gemm(Hd, W1[:, d:])))
     fl = E * (2 * 128 * 32)
-    b_alg = E * (2 * 128 * 4 + 2 * 8 + 4)
+    # bytes the launch must move: per edge the gathered Q[v] row (512 B from the 51 MB item
+    # table: Infinity-Cache resident), its two ids and the score; the P[u] rows once per run
+    # of edges sharing a source (32 edges per wave; the negatives of one positive share it:
+    # the repeated row is an L1 hit, rocprof fetches ~1.27 GB ~ the Q rows alone,
+    # profiles/r05k_minibatch_pmc_summary.md) — priced, like the cosine head, against the
+    # Infinity Cache's random-row rate
+    runs = int(torch.count_nonzero(src[1:] != src[:-1])) + 1
+    b_alg = E * (128 * 4 + 2 * 8 + 4) + runs * 128 * 4
     ref_fl = 2 * E * (2 * d * 128 + 128 * 32 + 32)
+    q_tbl = n_i * 128 * 4
+    roof_mlp = IC_GATHER_GBS if q_tbl <= IC_BYTES else HBM_PEAK_GBS
     out["edge_mlp"] = {"ms": round(ms, 4), "edges": E, "mfma_flops": fl,
                        "TFs": fl / ms / 1e9, "mfma_frac": fl / ms / 1e9 / MFMA_F32_PEAK_TFS,
                        "bytes_per_launch": b_alg, "achieved_GBs": b_alg / ms / 1e6,
-                       "hbm_frac": b_alg / ms / 1e6 / HBM_PEAK_GBS,
+                       "peak_GBs": roof_mlp, "gather_frac": b_alg / ms / 1e6 / roof_mlp,
+                       "bound_gather": "infinity-cache gather" if q_tbl <= IC_BYTES else "hbm",
                        "pq_gemms_ms": round(ms_pq, 4),
                        "head_ms": round(ms + ms_pq, 4),
                        "reference_flops": ref_fl,
