@@ -20,9 +20,13 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const char* __restrict
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = t / units_per_row, u = t - row * units_per_row;
-    const U* s = reinterpret_cast<const U*>(src + idx[row] * src_ld) + u;
+    const int64_t r = idx[row];
     U* d = reinterpret_cast<U*>(dst + row * dst_ld) + u;
-    *d = *s;
+    if (r < 0) {  // a padding slot of a static-shape block: a zero row
+      *d = U{};
+      continue;
+    }
+    *d = *(reinterpret_cast<const U*>(src + r * src_ld) + u);
   }
 }
 

@@ -32,8 +32,52 @@ EID = "_ID"
 CEType = Tuple[str, str, str]
 
 
+class LazyRows:
+    """Rows of a table at ids, gathered when first read (ops.gather_rows; a negative id gives
+    a zero row).  A static-shape batch's block data (sampling, static_shapes=True) is held
+    this way: a captured training step that reads it gathers it INSIDE its graph from the
+    batch's captured ids — so the loader neither gathers it nor hands it over, and data the
+    model never reads (a `mean` model's block edge data) is never moved."""
+
+    __slots__ = ("table", "ids")
+
+    def __init__(self, table: torch.Tensor, ids: torch.Tensor):
+        self.table, self.ids = table, ids
+
+    def get(self) -> torch.Tensor:
+        return ops.gather_rows(self.table, self.ids)
+
+
 class _FrameDict(dict):
-    """ntype/etype-keyed feature store with DGL-like access."""
+    """ntype/etype-keyed feature store with DGL-like access.  A LazyRows value is gathered
+    on first read and replaced by its tensor."""
+
+    def __getitem__(self, key):
+        v = dict.__getitem__(self, key)
+        if isinstance(v, LazyRows):
+            v = v.get()
+            dict.__setitem__(self, key, v)
+        return v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in list(self.keys())]
+
+    def values(self):
+        return [self[k] for k in list(self.keys())]
+
+    def pop(self, key, *default):
+        if key in self:
+            v = self[key]
+            dict.__delitem__(self, key)
+            return v
+        return dict.pop(self, key, *default)
+
+    def lazy_items(self):
+        """(key, value) with LazyRows values left unread."""
+        return list(dict.items(self))
 
 
 class _TypeAccessor:
@@ -389,7 +433,7 @@ class Block:
 
     def rel_graph(self, ce) -> RelGraph:
         indptr, indices, eids = self._rels[ce]
-        edata = {k: v for k, v in self._edata[ce].items() if k != EID}
+        edata = _FrameDict({k: v for k, v in self._edata[ce].lazy_items() if k != EID})
         return RelGraph(ce, indptr, indices, self.number_of_src_nodes(ce[0]), self._num_dst[ce[2]],
                         edata, eids, self._t.get(ce))
 

@@ -33,7 +33,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import ops
-from .graph import Block, EID, HeteroGraph, NID, PairGraph
+from .graph import Block, EID, HeteroGraph, LazyRows, NID, PairGraph
 
 
 def _mix(*xs) -> int:
@@ -63,6 +63,9 @@ class BlockSampler:
         # .edge_records) when every eid fits 31 bits; False: the index and eid arrays
         # (bitwise the same blocks; tests compare the two)
         self.packed = True
+        # static-shape blocks hold their block data as LazyRows (gathered when read); False:
+        # gathered by the sampler call like the exact blocks' (the same values)
+        self.lazy_static_data = True
         self._sb_scratch = {}
         self._stamp = 1
         # the first block's source-major CSRs (sample_blocks(transposes=True)) are skipped
@@ -172,6 +175,7 @@ class BlockSampler:
                 for ce in ces for k, v in g._edata[ce].items()]
         ntab = [(nt, k, v if v.dim() < 2 or v[0].is_contiguous() else v.contiguous())
                 for nt in nts for k, v in g._ndata[nt].items()]
+        lazy = static and self.lazy_static_data
         # static: the real counts stay on the device (sizes_out: [L + 1][T] node counts, the
         # seed counts first, then [L][R] edge counts) and drive the kernels over the blocks
         dsz = torch.empty((L + 1) * len(nts) + L * len(ces), dtype=torch.int64,
@@ -183,8 +187,10 @@ class BlockSampler:
             fans, keys, stamp, static_shapes=static, sizes_out=dsz,
             node_cap_hint=[[(hints or {}).get((s_, nt), 0) for nt in nts] for s_ in range(L)]
             if hints else None, overflow=overflow,
-            edge_tables=[(v, ces.index(ce)) for ce, _k, v in etab],
-            node_tables=[(v, tix[nt]) for nt, _k, v in ntab],
+            # static: the block data is left to LazyRows (gathered when read: inside a
+            # captured step's graph, from its captured ids), not gathered here
+            edge_tables=[] if lazy else [(v, ces.index(ce)) for ce, _k, v in etab],
+            node_tables=[] if lazy else [(v, tix[nt]) for nt, _k, v in ntab],
             edge_recs=self._edge_recs(g, ces))
         blocks = []
         for s_, (o_ip, src_loc, o_eid, nodes) in enumerate(steps):
@@ -225,13 +231,20 @@ class BlockSampler:
                         dst_ids = steps[s_ - 1][3][t]
                     b._dst[nt][NID] = dst_ids
             blocks.insert(0, b)
-        it = iter(data)
-        for s_ in range(L):
-            b = blocks[L - 1 - s_]
-            for ce, k, _v in etab:
-                b._edata[ce][k] = next(it)
-        for nt, k, _v in ntab:
-            blocks[0]._src[nt][k] = next(it)
+        if lazy:  # -1 ids (padding edges / source slots) read as zero rows
+            for b in blocks:
+                for ce, k, v in etab:
+                    b._edata[ce][k] = LazyRows(v, b._rels[ce][2])
+            for nt, k, v in ntab:
+                blocks[0]._src[nt][k] = LazyRows(v, blocks[0]._src[nt][NID])
+        else:
+            it = iter(data)
+            for s_ in range(L):
+                b = blocks[L - 1 - s_]
+                for ce, k, _v in etab:
+                    b._edata[ce][k] = next(it)
+            for nt, k, _v in ntab:
+                blocks[0]._src[nt][k] = next(it)
         if transposes:
             for block_id, b in enumerate(blocks):
                 if block_id > 0 or self._first_transposes(b):
@@ -451,11 +464,12 @@ def _batches(n: int, batch_size: int, shuffle: bool, drop_last: bool, device):
 
 
 def _tensors(obj, out):
-    """Every tensor reachable from a loader item (dicts, tuples, lists, blocks, graphs)."""
+    """Every tensor reachable from a loader item (dicts, tuples, lists, blocks, graphs);
+    a LazyRows value is left unread (not gathered, not listed)."""
     if isinstance(obj, torch.Tensor):
         out.append(obj)
     elif isinstance(obj, dict):
-        for v in obj.values():
+        for v in dict.values(obj):
             _tensors(v, out)
     elif isinstance(obj, (list, tuple)):
         for v in obj:

@@ -704,8 +704,8 @@ int gnnrec_lstm_slots(const int64_t* indptr, const int32_t* indices, const int64
 
 /* ---- a10: row gather (block features / edge data) -------------------------
  * dst row i (dst_ld_bytes apart) = src row idx[i] (src_ld_bytes apart), row_bytes each,
- * any dtype.  Replaces DGL's copy of node features into blocks[0].srcdata and of edge
- * data into the blocks (read at src/train/run.py:112,340). */
+ * any dtype; a negative idx[i] writes a zero row.  Replaces DGL's copy of node features into
+ * blocks[0].srcdata and of edge data into the blocks (read at src/train/run.py:112,340). */
 /* Up to GNNREC_GATHER_MAX_JOBS independent row gathers of gnnrec_gather_rows in ONE launch
  * (a sampled batch's edge data for every block and relation plus the input block's node
  * features: one launch instead of one per table).  A negative index (a padding slot of a

@@ -338,3 +338,40 @@ def test_overflowed_plan_is_flagged_and_reduces_every_row(short):
     assert int(plan[0]) == 3 and int(plan[1]) == 5 + 3 + 10
     assert ops.plan_overflows() == before + 1
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_static_block_data_is_lazy_until_read():
+    """A static batch's block data (node features of the input block, every block's edge
+    data) is held as LazyRows: walking the batch for a captured step's inputs
+    (sampling._tensors) leaves it unread and unlisted — a captured step that reads it
+    gathers it inside its graph from the captured ids — and reading it gives the rows the
+    exact gather gives, zero rows at the padding slots."""
+    from gnnrec.graph import NID, LazyRows
+    from gnnrec.sampling import _tensors
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    batch = next(iter(_loader(g, True)))
+    blocks = batch[-1]
+    assert all(b.static for b in blocks)
+    lazy = [(f, k) for f in blocks[0]._src.values() for k, v in f.lazy_items()
+            if isinstance(v, LazyRows)]
+    lazy += [(f, k) for b in blocks for f in b._edata.values() for k, v in f.lazy_items()
+             if isinstance(v, LazyRows)]
+    assert lazy
+    listed = {t.data_ptr() for t in _tensors(batch, [])}
+    assert all(isinstance(dict.__getitem__(f, k), LazyRows) for f, k in lazy)
+    for nt, f in blocks[0]._src.items():
+        for k in [k for k, v in f.lazy_items() if isinstance(v, LazyRows)]:
+            got = f[k]  # gathered now
+            assert got.data_ptr() not in listed
+            ids = f[NID]
+            table = g.nodes[nt].data[k]
+            ref = table[ids.clamp(min=0)] * (ids >= 0).reshape((-1,) + (1,) * (table.dim() - 1))
+            assert torch.equal(got, ref.to(got.dtype)), (nt, k)
+            assert not isinstance(dict.__getitem__(f, k), LazyRows)
+    for b in blocks:
+        for ce, f in b._edata.items():
+            eid = b._rels[ce][2]
+            for k in [k for k, v in f.lazy_items() if isinstance(v, LazyRows)]:
+                table = g.edges[ce].data[k]
+                ref = table[eid.clamp(min=0)] * (eid >= 0).reshape((-1,) + (1,) * (table.dim() - 1))
+                assert torch.equal(f.get(k), ref.to(table.dtype)), (ce, k)
