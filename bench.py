@@ -967,10 +967,11 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
                (the sampler reads sizes back to the host once per layer)
       cosine   (a7) C3 pair graph, 1024 pos x 2500 neg edges, d = 128, the compacted tables
                (1024 user rows, 100k item rows): 1036 B/edge; HIP-event time of the kernel
-      edge_mlp (a8) same pair graph through PredictingModule's tail kernel (relu(P[u]+Q[v])
-               -> 128x32 MFMA -> relu . w3 -> sigmoid): executed MFMA flops 2*128*32 per edge
-               over the kernel's time against the 157.3 TF fp32 MFMA peak, and its gather
-               bytes (2 x 512 + 16 + 4 B/edge) against 8 TB/s; the per-node P/Q GEMMs beside.
+      edge_mlp (a8) same pair graph through PredictingModule's tail kernel, grouped as the
+               cosine (relu(P[u]+Q[v]) -> 128x32 MFMA -> relu . w3 -> sigmoid): executed MFMA
+               flops 2*128*32 per edge over the kernel's time against the 157.3 TF fp32 MFMA
+               peak, and its gather bytes (512 + 12 B/edge, 528 B/group) against the Infinity
+               Cache's gather rate; the per-node P/Q GEMMs beside.
     Kernel times are HIP events on the stream the ops launch on (torch's current stream)."""
     from gnnrec import ops
     from gnnrec.nn import PredictingLayer
@@ -1039,7 +1040,7 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
     E = src.numel()
 
     def ev_time(fn, n=reps):
-        for _ in range(3):
+        for _ in range(n):  # (the first ~50 launches after other work run up to 10 % slow)
             fn()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -1081,18 +1082,18 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
         Q = ops.gemm(Hd, W1[:, d:])
     w2, b2 = pl.hidden_2.weight.detach(), pl.hidden_2.bias.detach()
     w3, b3 = pl.output.weight.detach().reshape(-1), pl.output.bias.detach()
-    ms = ev_time(lambda: ops.edge_mlp(src, dst, P, Q, w2, b2, w3, b3))
+    # the head as PredictingModule runs it on the loader's pair graphs: the grouped launch
+    # (group g = positive (g, pd[g]) + its K negatives, the source's P row read once per 256
+    # edges); the per-edge launch over the expanded lists beside it
+    ms = ev_time(lambda: ops.edge_mlp_grouped(ps, pd, K, nd, P, Q, w2, b2, w3, b3))
+    ms_edge = ev_time(lambda: ops.edge_mlp(src, dst, P, Q, w2, b2, w3, b3))
     ms_pq = ev_time(lambda: (ops.gemm(Hs, W1[:, :d], bias=pl.hidden_1.bias),
                              ops.gemm(Hd, W1[:, d:])))
     fl = E * (2 * 128 * 32)
     # bytes the launch must move: per edge the gathered Q[v] row (512 B from the 51 MB item
-    # table: Infinity-Cache resident), its two ids and the score; the P[u] rows once per run
-    # of edges sharing a source (32 edges per wave; the negatives of one positive share it:
-    # the repeated row is an L1 hit, rocprof fetches ~1.27 GB ~ the Q rows alone,
-    # profiles/r05k_minibatch_pmc_summary.md) — priced, like the cosine head, against the
-    # Infinity Cache's random-row rate
-    runs = int(torch.count_nonzero(src[1:] != src[:-1])) + 1
-    b_alg = E * (128 * 4 + 2 * 8 + 4) + runs * 128 * 4
+    # table: Infinity-Cache resident), its id and the score; per group the P[u] row and two
+    # ids — priced, like the cosine head, against the Infinity Cache's random-row rate
+    b_alg = E * (128 * 4 + 8 + 4) + n_u * (128 * 4 + 16)
     ref_fl = 2 * E * (2 * d * 128 + 128 * 32 + 32)
     q_tbl = n_i * 128 * 4
     roof_mlp = IC_GATHER_GBS if q_tbl <= IC_BYTES else HBM_PEAK_GBS
@@ -1103,11 +1104,14 @@ def minibatch_rooflines(dev, reps: int = 50, g=None):
                        "bound_gather": "infinity-cache gather" if q_tbl <= IC_BYTES else "hbm",
                        "pq_gemms_ms": round(ms_pq, 4),
                        "head_ms": round(ms + ms_pq, 4),
+                       "per_edge_kernel_ms": round(ms_edge, 4),
                        "reference_flops": ref_fl,
                        "reference_equivalent_TFs": ref_fl / (ms + ms_pq) / 1e9,
-                       "kernel": "edge_mlp_kernel",
+                       "kernel": "edge_mlp_lds_kernel<true> (grouped)",
                        "note": "W1[hu||hv] re-associated into per-node P, Q (two GEMMs): the "
-                               "per-edge kernel runs only the 128x32 layer on the MFMA; "
+                               "edge kernel runs only the 128x32 layer on the MFMA, over "
+                               "LDS-staged tiles of 32 edges (coalesced row loads); "
+                               "per_edge_kernel_ms = the same body on the expanded lists; "
                                "reference_equivalent_TFs prices the reference's per-edge "
                                "flops over the whole head"}
     return out

@@ -187,59 +187,211 @@ int launch_cos_grouped(const int64_t* src_g, int64_t G, const int64_t* first, fl
 }
 
 // ------------------------------------------------------------- edge MLP ----
-// One wave scores 32 edges: A[i][k] = relu(P[src_i][k] + Q[dst_i][k]) (k < 128),
-// B[k][j] = W2[j][k]; lane half h consumes k in [64h, 64h+64).  Output
-// C[i][j] (col j = lane&31) -> relu(+b2) -> dot with w3 across the 32 lanes.
-constexpr int kHid1 = 128;
+// A[i][k] = relu(P[src_i][k] + Q[dst_i][k]) (k < 128) feeds the 128x32 layer on the MFMA,
+// then relu(+b2) . w3 and the sigmoid; hidden sizes 128 and 32 (src/model.py:258-260).
 
-__global__ __launch_bounds__(256) void edge_mlp_kernel(const int64_t* __restrict__ src,
-                                                       const int64_t* __restrict__ dst,
-                                                       int64_t n_edges,
-                                                       const float* __restrict__ P,
-                                                       const float* __restrict__ Q,
-                                                       const float* __restrict__ W2,
-                                                       const float* __restrict__ b2,
-                                                       const float* __restrict__ w3,
-                                                       const float* __restrict__ b3,
-                                                       float* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const float b2r = b2[r];
-  const float w3r = w3[r];
-  const float b3v = b3[0];
-  const int64_t gstride = (int64_t)gridDim.x * 4 * 32;
-  for (int64_t e0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32; e0 < n_edges;
-       e0 += gstride) {
-    const int64_t e = e0 + r;
-    const bool eok = e < n_edges;
-    const float* pp = P + (eok ? src[e] : 0) * kHid1 + h * 64;
-    const float* pq = Q + (eok ? dst[e] : 0) * kHid1 + h * 64;
-    const float* pw = W2 + r * kHid1 + h * 64;
-    f32x16 acc;
+// One wave scores tiles of 32 edges: the tile's hidden-1 activations
+// A[i][k] = relu(P[u_i][k] + Q[v_i][k]) are built from coalesced row loads (two 512-B rows
+// of P and of Q per wave-instruction, each row's 32 16-B chunks in one lane half) and
+// stored to the wave's LDS image with row i's chunk j at position j ^ (i & 15), so that the
+// MFMA-layout reads (lane r reads row r) meet 16 distinct 4-bank groups per lane group.
+// (Per-lane row loads in the MFMA layout — lane r reading its own edge's rows — touch 32
+// rows per wave-instruction and each row's 128-B lines again from eight instructions:
+// 0.37 ms against 0.27 ms at 2.56M edges, tools/micro/edge_mlp_ab.py.)  The 128x32 layer runs transposed, C^T = W2 A^T: W2 as the A operand
+// (lane r holds hidden-2 unit r's row, in registers for the wave's life) and the staged A
+// as the B operand (lane r = edge r), so lane (r, h) ends with 16 of edge r's 32 hidden-2
+// units: the output dot is an in-register sum and one add across the lane halves.
+// GROUPED: the edges are n_groups runs of one source (negative_sampler.Uniform's negatives:
+// group g = optionally its positive (g, first[g]) then its K negatives (g, dst[g K + j])).
+constexpr int kMlpTile = 32;        // edges per MFMA tile
+constexpr int kMlpChunkTiles = 8;   // tiles per work item, at most
+constexpr int kMlpWaves = 4;        // waves per 256-thread block, each with its own image
+constexpr int kMlpResidentWaves = 2 * 256 * kMlpWaves;  // two blocks per CU (registers)
+
+struct EdgeMlpArgs {
+  const int64_t* src;    // per edge; GROUPED: per group
+  const int64_t* dst;    // per edge; GROUPED: [n_groups x K] negatives
+  const int64_t* first;  // GROUPED: per-group positive destination, or null
+  float* out_first;
+  float* out;
+  const float* P;
+  const float* Q;
+  const float* W2;
+  const float* b2;
+  const float* w3;
+  const float* b3;
+  int64_t n_edges;       // ungrouped edge count
+  int64_t K;             // GROUPED: negatives per group
+  int64_t per_group;     // GROUPED: K + (first != null)
+  int64_t chunks;        // GROUPED: work items per group
+  int64_t n_items;
+  int64_t chunk_tiles;   // tiles per work item
+};
+
+// A tile's 32 edges: lane r's destination row (and source row, per-edge form); -1 past the
+// end.  Both lane halves hold the same ids.
+template <bool GROUPED>
+__device__ __forceinline__ void mlp_tile_ids(const EdgeMlpArgs& a, int64_t g, int64_t e,
+                                             int64_t e_end, int64_t lead, int& v, int& u) {
+  v = -1;
+  if (e >= e_end) return;
+  if constexpr (GROUPED) {
+    v = (int)(e < lead ? a.first[g] : a.dst[g * a.K + e - lead]);
+  } else {
+    v = (int)a.dst[e];
+    u = (int)a.src[e];
+  }
+}
+
+// Row loads of a tile, wave-instruction i = rows 2 i + h (lane half h), chunk r ^ (row & 15):
+// GROUPED the Q chunks of rows i in [i0, i0 + N); per edge the (Q, P) chunk pairs.
+template <bool GROUPED, int N>
+__device__ __forceinline__ void mlp_load(const float4* __restrict__ Q4,
+                                         const float4* __restrict__ P4, int v, int u, int r,
+                                         int h, int i0, float4 (&q)[N], float4 (&p)[N]) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      f32x4 a = *reinterpret_cast<const f32x4*>(pp + c * 4) +
-                *reinterpret_cast<const f32x4*>(pq + c * 4);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(pw + c * 4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float av = eok ? fmaxf(a[s], 0.f) : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[s], acc, 0, 0, 0);
-      }
-    }
-    // acc[v] = hidden2 pre-activation of edge row (v&3)+8(v>>2)+4h, unit r
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      float y = fmaxf(acc[v] + b2r, 0.f) * w3r;
-#pragma unroll
-      for (int off = 1; off < 32; off <<= 1) y += __shfl_xor(y, off);
-      const int64_t er = e0 + (v & 3) + 8 * (v >> 2) + 4 * h;
-      if (r == 0 && er < n_edges) out[er] = 1.f / (1.f + expf(-(y + b3v)));
+  for (int i = 0; i < N; ++i) {
+    const int row = 2 * (i0 + i) + h;
+    const int vr = __shfl(v, row);
+    const int ur = GROUPED ? 0 : __shfl(u, row);  // (outside the branch: every lane shuffles)
+    const int j = r ^ (row & 15);
+    q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (!GROUPED) p[i] = q[i];
+    if (vr >= 0) {
+      q[i] = Q4[(int64_t)vr * 32 + j];
+      if constexpr (!GROUPED) p[i] = P4[(int64_t)ur * 32 + j];
     }
   }
+}
+
+__device__ __forceinline__ float4 relu_add4(const float4& p, const float4& q) {
+  return make_float4(fmaxf(p.x + q.x, 0.f), fmaxf(p.y + q.y, 0.f), fmaxf(p.z + q.z, 0.f),
+                     fmaxf(p.w + q.w, 0.f));
+}
+
+// The 128x32 layer of one staged tile (C^T = W2 A^T) and the output: sigmoid(w3 . relu(. + b2)
+// + b3) of edge r, stored by lane r of the first half.  RELU_P: the image holds Q rows only,
+// A = relu(P + Q) formed here with the source's P chunks pc (16 h + c).
+template <bool RELU_P>
+__device__ __forceinline__ float mlp_tile_score(const EdgeMlpArgs& a, const float4* S,
+                                                const float4 (&w)[16], const float4* pc, int r,
+                                                int h, float b3v) {
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    float4 x = S[r * 32 + ((16 * h + c) ^ (r & 15))];
+    if constexpr (RELU_P) x = relu_add4(pc[c], x);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[c].x, x.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[c].y, x.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[c].z, x.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w[c].w, x.w, acc, 0, 0, 0);
+  }
+  // acc[q]: hidden-2 unit 8 (q >> 2) + 4 h + (q & 3) of edge r
+  float y = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int jj = 8 * (q >> 2) + 4 * h + (q & 3);
+    y = fmaf(fmaxf(acc[q] + a.b2[jj], 0.f), a.w3[jj], y);
+  }
+  y += __shfl_xor(y, 32);
+  return 1.f / (1.f + expf(-(y + b3v)));
+}
+
+__device__ __forceinline__ void mlp_store(const EdgeMlpArgs& a, bool grouped, int64_t g,
+                                          int64_t e, int64_t lead, float sc) {
+  if (!grouped) a.out[e] = sc;
+  else if (e < lead) a.out_first[g] = sc;
+  else a.out[g * a.K + e - lead] = sc;
+}
+
+__device__ __forceinline__ void mlp_load_w2(const EdgeMlpArgs& a, int r, int h, float4 (&w)[16]) {
+  const float4* W4 = reinterpret_cast<const float4*>(a.W2) + r * 32 + 16 * h;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) w[c] = W4[c];  // W2 row r, chunks 16 h + c: k = 64 h + 4 c + s
+}
+
+// work item -> (group, tiles [t0, t1), edge end)
+template <bool GROUPED>
+__device__ __forceinline__ void mlp_item(const EdgeMlpArgs& a, int64_t item, int64_t tiles_pg,
+                                         int64_t& g, int64_t& t0, int64_t& t1, int64_t& e_end) {
+  if constexpr (GROUPED) {
+    g = item / a.chunks;
+    t0 = (item - g * a.chunks) * a.chunk_tiles;
+    t1 = t0 + a.chunk_tiles < tiles_pg ? t0 + a.chunk_tiles : tiles_pg;
+    e_end = a.per_group;
+  } else {
+    g = 0;
+    t0 = item * a.chunk_tiles;
+    t1 = t0 + a.chunk_tiles;
+    e_end = a.n_edges;
+  }
+}
+
+template <bool GROUPED>
+__global__ __launch_bounds__(256, 2) void edge_mlp_lds_kernel(EdgeMlpArgs a) {
+  __shared__ float4 image[kMlpWaves][kMlpTile * 32];  // 16 KB per wave
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  float4* S = image[wv];
+  const float4* P4 = reinterpret_cast<const float4*>(a.P);
+  const float4* Q4 = reinterpret_cast<const float4*>(a.Q);
+  float4 w[16];
+  mlp_load_w2(a, r, h, w);
+  const float b3v = a.b3[0];
+  const int64_t tiles_pg = GROUPED ? (a.per_group + kMlpTile - 1) / kMlpTile : 0;
+  const int64_t lead = (GROUPED && a.first) ? 1 : 0;
+  for (int64_t item = (int64_t)blockIdx.x * kMlpWaves + wv; item < a.n_items;
+       item += (int64_t)gridDim.x * kMlpWaves) {
+    int64_t g, t0, t1, e_end;
+    mlp_item<GROUPED>(a, item, tiles_pg, g, t0, t1, e_end);
+    const int u_g = GROUPED ? (int)a.src[g] : 0;
+    // GROUPED: the source's P chunks this lane adds, r ^ (row & 15) for the 16 row
+    // residues of one lane half (rows 2 i + h, i < 8, then the same residues again)
+    float4 pg[8];
+    if constexpr (GROUPED) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pg[i] = P4[(int64_t)u_g * 32 + (r ^ ((2 * i + h) & 15))];
+    }
+    for (int64_t t = t0; t < t1; ++t) {
+      const int64_t e = t * kMlpTile + r;  // this lane's edge (both halves)
+      int v, u = u_g;
+      mlp_tile_ids<GROUPED>(a, g, e, e_end, lead, v, u);
+      // stage, eight row pairs at a time
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float4 q[8], p[8];
+        mlp_load<GROUPED, 8>(Q4, P4, v, u, r, h, 8 * half, q, p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          S[(2 * (8 * half + i) + h) * 32 + r] = relu_add4(GROUPED ? pg[i] : p[i], q[i]);
+      }
+      // (the wave's own LDS writes precede its reads in issue order)
+      const float sc = mlp_tile_score<false>(a, S, w, nullptr, r, h, b3v);
+      if (h == 0 && e < e_end) mlp_store(a, GROUPED, g, e, lead, sc);
+    }
+  }
+}
+
+// tiles per work item: up to kMlpChunkTiles (the wave's W2 / P registers reused), fewer when
+// the launch would otherwise leave resident waves idle
+int64_t mlp_chunk_tiles(int64_t tiles) {
+  int64_t c = (tiles + kMlpResidentWaves - 1) / kMlpResidentWaves;
+  return c < 1 ? 1 : (c > kMlpChunkTiles ? kMlpChunkTiles : c);
+}
+
+int launch_edge_mlp_lds(bool grouped, EdgeMlpArgs& a, hipStream_t s) {
+  if (a.n_items <= 0) return GNNREC_OK;
+  int64_t blocks = (a.n_items + kMlpWaves - 1) / kMlpWaves;
+  if (blocks > kMlpResidentWaves / kMlpWaves) blocks = kMlpResidentWaves / kMlpWaves;
+  if (grouped)
+    hipLaunchKernelGGL(edge_mlp_lds_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(edge_mlp_lds_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return check_launch(grouped ? "gnnrec_edge_mlp_grouped_f32" : "gnnrec_edge_mlp_f32");
 }
 
 }  // namespace
@@ -303,9 +455,31 @@ extern "C" int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64
                  "gnnrec_edge_mlp_f32: null pointer");
   GNNREC_REQUIRE(aligned16(P) && aligned16(Q) && aligned16(W2),
                  "gnnrec_edge_mlp_f32: P/Q/W2 must be 16-byte aligned");
-  int64_t blocks = (n_edges + 127) / 128;
-  if (blocks > 256 * 32) blocks = 256 * 32;
-  hipLaunchKernelGGL(edge_mlp_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
-                     src, dst, n_edges, P, Q, W2, b2, w3, b3, out);
-  return check_launch("gnnrec_edge_mlp_f32");
+  const int64_t tiles = (n_edges + kMlpTile - 1) / kMlpTile;
+  const int64_t ct = mlp_chunk_tiles(tiles);
+  EdgeMlpArgs a{src, dst, nullptr, nullptr, out, P, Q, W2, b2, w3, b3, n_edges, 0, 0, 0,
+                (tiles + ct - 1) / ct, ct};
+  return launch_edge_mlp_lds(false, a, as_stream(stream));
+}
+
+extern "C" int gnnrec_edge_mlp_grouped_f32(const int64_t* src_g, int64_t n_groups,
+                                           const int64_t* first, float* out_first, int64_t K,
+                                           const int64_t* dst, float* out, const float* P,
+                                           const float* Q, const float* W2, const float* b2,
+                                           const float* w3, const float* b3, void* stream) {
+  using namespace gnnrec;
+  GNNREC_REQUIRE(n_groups >= 0 && K >= 0, "gnnrec_edge_mlp_grouped_f32: negative size");
+  if (n_groups == 0 || (K == 0 && first == nullptr)) return GNNREC_OK;
+  GNNREC_REQUIRE(src_g && P && Q && W2 && b2 && w3 && b3 && (K == 0 || (dst && out)) &&
+                     (!first || out_first),
+                 "gnnrec_edge_mlp_grouped_f32: null pointer");
+  GNNREC_REQUIRE(aligned16(P) && aligned16(Q) && aligned16(W2),
+                 "gnnrec_edge_mlp_grouped_f32: P/Q/W2 must be 16-byte aligned");
+  const int64_t per_group = K + (first ? 1 : 0);
+  const int64_t tiles = (per_group + kMlpTile - 1) / kMlpTile;
+  const int64_t ct = mlp_chunk_tiles(n_groups * tiles);
+  const int64_t chunks = (tiles + ct - 1) / ct;
+  EdgeMlpArgs a{src_g, dst, first, out_first, out, P, Q, W2, b2, w3, b3, 0, K, per_group, chunks,
+                n_groups * chunks, ct};
+  return launch_edge_mlp_lds(true, a, as_stream(stream));
 }

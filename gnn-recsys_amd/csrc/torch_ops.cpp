@@ -13,6 +13,7 @@
 //   spmm_csr*, spmm_project, gemm   <- ConvLayer.forward src/model.py:143-208,226-235
 //   sddmm_cos                       <- CosinePrediction.forward src/model.py:317-327
 //   edge_mlp                        <- PredictingModule.forward src/model.py:290-305
+//   edge_mlp_grouped                <- the same over negative_sampler.Uniform's pair graphs
 //   sample_*, scan, relabel ops     <- dgl samplers / to_block, src/sampling.py:153-161
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
@@ -543,6 +544,39 @@ void edge_mlp(const Tensor& src, const Tensor& dst, const Tensor& P, const Tenso
                          p<float>(W2), p<float>(b2), p<float>(w3), p<float>(b3), p<float>(out),
                          stream_of(P)),
      "gnnrec_edge_mlp_f32");
+}
+
+void edge_mlp_grouped(const Tensor& src_g, const optional<Tensor>& first, int64_t K,
+                      const Tensor& dst, const Tensor& P, const Tensor& Q, const Tensor& W2,
+                      const Tensor& b2, const Tensor& w3, const Tensor& b3, Tensor& out_first,
+                      Tensor& out) {
+  const OneDevice one_device_;
+  dev(src_g, "src_g", at::kLong);
+  dev(first, "first", at::kLong);
+  dev(dst, "dst", at::kLong);
+  for (auto* t : {&P, &Q, &W2, &b2, &w3, &b3}) dev(*t, "edge_mlp operand", at::kFloat);
+  dev(out_first, "out_first", at::kFloat);
+  dev(out, "out", at::kFloat);
+  TORCH_CHECK_VALUE(P.size(1) == 128 && Q.size(1) == 128 && W2.size(0) == 32 && W2.size(1) == 128,
+                    "edge_mlp expects the reference's 128/32 hidden sizes");
+  TORCH_CHECK_VALUE(P.is_contiguous() && Q.is_contiguous() && W2.is_contiguous(),
+                    "edge_mlp operands must be contiguous");
+  const int64_t G = src_g.numel();
+  TORCH_CHECK_VALUE(K >= 0 && dst.numel() == G * K && out.numel() == G * K,
+                    "edge_mlp_grouped: dst and out must hold n_groups x K entries");
+  TORCH_CHECK_VALUE(!has(first) || (first->numel() == G && out_first.numel() == G),
+                    "edge_mlp_grouped: first and out_first must hold n_groups entries");
+  TORCH_CHECK_VALUE(src_g.is_contiguous() && dst.is_contiguous() &&
+                        (!has(first) || first->is_contiguous()) && out.is_contiguous() &&
+                        out_first.is_contiguous(),
+                    "edge_mlp_grouped: contiguous ids and outputs");
+  if (meta(P)) return;
+  const c10::DeviceGuard g(P.device());
+  ck(gnnrec_edge_mlp_grouped_f32(p<int64_t>(src_g), G, p<int64_t>(first), p<float>(out_first), K,
+                                 p<int64_t>(dst), p<float>(out), p<float>(P), p<float>(Q),
+                                 p<float>(W2), p<float>(b2), p<float>(w3), p<float>(b3),
+                                 stream_of(P)),
+     "gnnrec_edge_mlp_grouped_f32");
 }
 
 // ---------------------------------------------------------------- a9 sampler / relabel
@@ -2134,6 +2168,8 @@ TORCH_LIBRARY(gnnrec, m) {
         "Tensor(a!)? gHs, Tensor(b!)? gHd, Tensor(c!) workspace, int groups=0, int K=0) -> ()");
   m.def("edge_mlp(Tensor src, Tensor dst, Tensor P, Tensor Q, Tensor W2, Tensor b2, Tensor w3, "
         "Tensor b3, Tensor(a!) out) -> ()");
+  m.def("edge_mlp_grouped(Tensor src_g, Tensor? first, int K, Tensor dst, Tensor P, Tensor Q, "
+        "Tensor W2, Tensor b2, Tensor w3, Tensor b3, Tensor(a!) out_first, Tensor(b!) out) -> ()");
   m.def("sample_count(Tensor indptr, Tensor eids, Tensor? excluded, Tensor seeds, int fanout, "
         "int seed_key, Tensor(a!) counts, Tensor? excluded_rows=None) -> ()");
   m.def("sample_fill(Tensor indptr, Tensor indices, Tensor eids, Tensor? excluded, Tensor seeds, "
@@ -2248,6 +2284,7 @@ TORCH_LIBRARY(gnnrec, m) {
   m.impl("sddmm_cos_grouped", &sddmm_cos_grouped);       \
   m.impl("sddmm_cos_backward", &sddmm_cos_backward);     \
   m.impl("edge_mlp", &edge_mlp);                         \
+  m.impl("edge_mlp_grouped", &edge_mlp_grouped);         \
   m.impl("sample_count", &sample_count);                 \
   m.impl("sample_fill", &sample_fill);                   \
   m.impl("exclusive_scan", &exclusive_scan);             \

@@ -74,6 +74,8 @@ SIGNATURES = {
     "gnnrec_sddmm_cos_grouped_f32": (_INT, [_P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _I64,
                                             _I64, _P]),
     "gnnrec_edge_mlp_f32": (_INT, [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gnnrec_edge_mlp_grouped_f32": (_INT, [_P, _I64, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P,
+                                            _P, _P]),
     "gnnrec_sample_count": (_INT, [_P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P]),
     "gnnrec_sample_fill": (_INT, [_P, _P, _P, _P, _P, _P, _I64, _I64, _U64, _P, _P, _P, _P]),
     "gnnrec_scan_workspace_bytes": (_I64, [_I64]),

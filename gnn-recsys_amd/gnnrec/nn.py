@@ -472,10 +472,20 @@ class PredictingLayer(nn.Module):
         x = ops.gemm(x, self.hidden_2.weight, bias=self.hidden_2.bias, relu=True)
         return ops.gemm(x, self.output.weight, bias=self.output.bias, sigmoid=True)
 
-    def score_edges(self, h_src, h_dst, src, dst):
-        """Edge scores without materialising [E, 2d]: W1[hu‖hv] = (W1a hu + b1) + W1b hv."""
+    def score_edges(self, h_src, h_dst, src, dst, K=None):
+        """Edge scores without materialising [E, 2d]: W1[hu‖hv] = (W1a hu + b1) + W1b hv.
+        K: `src` is runs of K repeats of one source (negative_sampler.Uniform's negatives:
+        the grouped launch, one P row per run)."""
         d = h_src.shape[1]
         W1 = self.hidden_1.weight
+        if K is not None and K >= 32 and src.numel() == (src.numel() // K) * K and \
+                src.numel() >= h_src.shape[0] + h_dst.shape[0]:
+            P = ops.gemm(h_src, W1[:, :d], bias=self.hidden_1.bias)
+            Q = ops.gemm(h_dst, W1[:, d:])
+            _, out = ops.edge_mlp_grouped(src[::K].contiguous(), None, K, dst, P, Q,
+                                          self.hidden_2.weight, self.hidden_2.bias,
+                                          self.output.weight.reshape(-1), self.output.bias)
+            return out
         if src.numel() < h_src.shape[0] + h_dst.shape[0]:
             # fewer edges than table rows: score the gathered rows
             hu, hv = h_src.index_select(0, src), h_dst.index_select(0, dst)
@@ -505,7 +515,11 @@ class PredictingModule(nn.Module):
                     cat_embed = torch.cat((h[utype][src_nid], h[vtype][dst_nid]), 1)
                     ratings = self.layer_nn(cat_embed)
                 else:
-                    ratings = self.layer_nn.score_edges(h[utype], h[vtype], src_nid, dst_nid)
+                    # negative_sampler.Uniform's negative graph (the loader marks it): the
+                    # grouped launch
+                    K = graph.src_repeats(etype, src_nid) if hasattr(graph, 'src_repeats') \
+                        else None
+                    ratings = self.layer_nn.score_edges(h[utype], h[vtype], src_nid, dst_nid, K)
                 ratings_dict[etype] = torch.flatten(ratings)
         return {k: torch.unsqueeze(v, 1) for k, v in ratings_dict.items()}
 

@@ -1188,6 +1188,31 @@ def edge_mlp(src: torch.Tensor, dst: torch.Tensor, P: torch.Tensor, Q: torch.Ten
     return out
 
 
+def edge_mlp_grouped(src_g: torch.Tensor, first: Optional[torch.Tensor], K: int,
+                     dst: torch.Tensor, P: torch.Tensor, Q: torch.Tensor, W2: torch.Tensor,
+                     b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor):
+    """a8 tail for the pair graphs of negative_sampler.Uniform(K), grouped as
+    sddmm_cos_grouped: group g's positive edge (src_g[g], first[g]) and its K negatives
+    (src_g[g], dst[g K + j]) -> (positive scores [G] (None without `first`), negative scores
+    [G K]); edge_mlp's scores of the expanded lists."""
+    for t, n in ((P, "P"), (Q, "Q"), (W2, "W2"), (b2, "b2"), (w3, "w3"), (b3, "b3")):
+        _dev(t, n, torch.float32)
+    for t, n in ((src_g, "src_g"), (dst, "dst")):
+        _dev(t, n, torch.int64)
+    if first is not None:
+        _dev(first, "first", torch.int64)
+    if P.shape[1] != 128 or Q.shape[1] != 128 or tuple(W2.shape) != (32, 128):
+        raise ValueError("edge_mlp expects the reference's 128/32 hidden sizes")
+    P, Q, W2 = P.contiguous(), Q.contiguous(), W2.detach().contiguous()
+    G = src_g.numel()
+    out_first = torch.empty(G if first is not None else 0, dtype=torch.float32, device=P.device)
+    out = torch.empty(G * int(K), dtype=torch.float32, device=P.device)
+    _T().edge_mlp_grouped(src_g.contiguous(), None if first is None else first.contiguous(),
+                          int(K), dst.contiguous(), P, Q, W2, b2.detach().contiguous(),
+                          w3.detach().contiguous(), b3.detach().contiguous(), out_first, out)
+    return (out_first if first is not None else None), out
+
+
 def synth_edges(seed: int, e0: int, n: int, n_u: int, n_i: int, device,
                 zipf_cdf: Optional[torch.Tensor] = None):
     """Counter-hash bipartite edges [e0, e0+n) -> (u int32 [n], i int32 [n])."""

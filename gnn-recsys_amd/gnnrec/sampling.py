@@ -486,10 +486,15 @@ class _Prefetch:
     recycle it under work the consumer queued)."""
 
     _END = object()
+    # the producer stream's priority (torch.cuda.Stream: lower is higher; 0 = normal)
+    priority = 0
 
-    def __init__(self, make_iter, depth: int, device):
+    def __init__(self, make_iter, depth: int, device, take_handoff=None):
         self.device = device
-        self.stream = torch.cuda.Stream(device=device)
+        # take_handoff() -> the event to hand the item just produced over with (recorded
+        # right after its own work), or None: an event recorded when it comes out
+        self.take_handoff = take_handoff
+        self.stream = torch.cuda.Stream(device=device, priority=self.priority)
         # the producer starts after everything the consumer has queued, which includes the
         # tail of any earlier loader's producer (its __iter__ ends with the consumer stream
         # waiting on it): a sampler shared by several loaders (reference sampling.py:153-241
@@ -513,8 +518,10 @@ class _Prefetch:
         try:
             with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
                 for item in make_iter():
-                    ev = torch.cuda.Event()
-                    ev.record(self.stream)
+                    ev = self.take_handoff() if self.take_handoff else None
+                    if ev is None:
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
                     if not self._put((item, ev)):
                         return
             self._put(self._END)
@@ -548,7 +555,7 @@ def _maybe_prefetch(loader, make_iter):
     n = int(getattr(loader, "num_workers", 0) or 0)
     dev = loader.g.device
     if n > 0 and dev.type == "cuda":
-        return iter(_Prefetch(make_iter, n, dev))
+        return iter(_Prefetch(make_iter, n, dev, getattr(loader, "_take_handoff", None)))
     return make_iter()
 
 
@@ -670,9 +677,9 @@ class EdgeDataLoader:
         # out exact, and their largest source lists x STATIC_MARGIN (+ a padding slot) become
         # the node capacities: a later batch that does not fit (the sampler's overflow flag,
         # read back in the loader's thread) is redone exactly and the capacities grow.  The
-        # read-back makes the loader wait for its own kernels, which then queue behind the
-        # training step's: C2 K = 2500 replays drop 3.22 -> 2.81 ms of GPU time but the step
-        # went 4.6 -> 6.6 ms (profiles/r05l_captured_step_probe_learned_caps.json)
+        # flag is read once the next batch's kernels are queued (_iter_batches): read at
+        # once, it made the loader wait for its own kernels, queued behind the training
+        # step's (profiles/r05l_captured_step_probe_learned_caps.json)
         if static_caps not in ("auto", "provable"):
             raise ValueError(f"static_caps={static_caps!r}: 'auto' or 'provable'")
         self.static_caps = static_caps
@@ -680,6 +687,7 @@ class EdgeDataLoader:
         self._seen_nodes = {}
         self._learned = 0
         self._overflow = None
+        self._handoff = None  # the next item's hand-off event (_iter_batches)
         self.static_redone = 0
         if static_shapes:
             if len(self.types) != 1 or not self.fused_head:
@@ -824,85 +832,137 @@ class EdgeDataLoader:
         return _maybe_prefetch(self, self._iter_batches)
 
     def _iter_batches(self):
+        """The batches in order.  A static batch's overflow flag (learned capacities) is
+        read only once the NEXT batch's kernels are queued — copied to the host behind an
+        event of its own — so the loader's host work for batch N + 1 overlaps batch N's
+        kernels instead of waiting for them (which, in a sampling thread, queue behind the
+        training step's).  Each batch is handed over with an event recorded right after
+        its own work (_Prefetch takes it from _take_handoff)."""
+        pending = None
+        for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
+                            self.drop_last, self.g.device):
+            rec = self._make_batch(idx)
+            if pending is not None:
+                yield self._settle(pending)
+                pending = None
+            if rec["flag"] is None:
+                yield self._settle(rec)
+            else:
+                pending = rec
+        if pending is not None:
+            yield self._settle(pending)
+
+    def _take_handoff(self):
+        ev, self._handoff = self._handoff, None
+        return ev
+
+    def _make_batch(self, idx):
+        """One batch's pairs, negatives and blocks, queued; static: its overflow flag on its
+        way to the host (rec['flag'], read by _settle)."""
         g = self.g
         empty = torch.zeros(0, dtype=torch.int64, device=g.device)
-        for idx in _batches(self.flat_ids.numel(), self.batch_size, self.shuffle,
-                            self.drop_last, g.device):
-            parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
-            batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
-            static = self.static_shapes and idx.numel() == self.batch_size and \
-                self._node_hint is not None
-            learn = self.static_shapes and idx.numel() == self.batch_size and not static
-            counts = None
-            if static:
-                node_ids, pos_l, neg_l, counts = self._head_static(batch)
-            elif self.fused_head:
-                node_ids, pos_l, neg_l = self._head(batch)
-            else:  # the readable form: the same kernels, generator draws and order
-                pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch
-                             else (empty, empty) for ce in g.canonical_etypes}
-                neg_edges = {}
-                if self.negative_sampler is not None:
-                    neg = self.negative_sampler(g, batch)
-                    neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
-                node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
-            pos_g = PairGraph(pos_l, node_ids)
-            pos_g.static = static
+        parts = _split_by_type(idx, self.flat_ids, self.type_starts, len(self.types))
+        batch = {ce: v for ce, v in zip(self.types, parts) if v.numel() > 0}
+        static = self.static_shapes and idx.numel() == self.batch_size and \
+            self._node_hint is not None
+        learn = self.static_shapes and idx.numel() == self.batch_size and not static
+        counts = None
+        if static:
+            node_ids, pos_l, neg_l, counts = self._head_static(batch)
+        elif self.fused_head:
+            node_ids, pos_l, neg_l = self._head(batch)
+        else:  # the readable form: the same kernels, generator draws and order
+            pos_edges = {ce: g.find_edges(batch[ce], etype=ce) if ce in batch
+                         else (empty, empty) for ce in g.canonical_etypes}
+            neg_edges = {}
+            if self.negative_sampler is not None:
+                neg = self.negative_sampler(g, batch)
+                neg_edges = {ce: neg.get(ce, (empty, empty)) for ce in g.canonical_etypes}
+            node_ids, pos_l, neg_l = self._compact(pos_edges, neg_edges)
+        exclude = None
+        if self.exclude == 'reverse_types':
+            exclude = {}
             for ce, e in batch.items():
-                for k, v in g._edata[ce].items():
-                    pos_g._edata[ce][k] = ops.gather_rows(v, e)
-                pos_g._edata[ce][EID] = e
-            exclude = None
-            if self.exclude == 'reverse_types':
-                exclude = {}
-                for ce, e in batch.items():
-                    exclude[ce] = e
-                    if ce in self.reverse_etypes:
-                        exclude[self.reverse_etypes[ce]] = e
-            elif self.exclude == 'self':
-                exclude = dict(batch)
-            seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
-            hint = self._node_hint if static and self._node_hint else None
-            if hint is not None:
-                if self._overflow is None:
-                    self._overflow = torch.zeros(1, dtype=torch.int64, device=g.device)
-                self._overflow.zero_()
-            blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
-                                                transposes=self.transposed_blocks,
-                                                static_shapes=static, node_cap_hint=hint,
-                                                overflow=self._overflow if hint else None)
-            if hint is not None and int(self._overflow.item()):
-                # the batch outgrew the learned capacities: redo it exactly (same pairs and
-                # negatives, fresh picks) and let the capacities grow
+                exclude[ce] = e
+                if ce in self.reverse_etypes:
+                    exclude[self.reverse_etypes[ce]] = e
+        elif self.exclude == 'self':
+            exclude = dict(batch)
+        hint = self._node_hint if static and self._node_hint else None
+        flag = None
+        if hint is not None:
+            if self._overflow is None:  # two flags (and host copies): batch N's is read
+                # after batch N + 1 has zeroed and set its own
+                self._overflow = [torch.zeros(1, dtype=torch.int64, device=g.device)
+                                  for _ in range(2)]
+                self._overflow_host = [torch.zeros(1, dtype=torch.int64).pin_memory()
+                                       for _ in range(2)]
+                self._overflow_i = 0
+            i = self._overflow_i
+            self._overflow_i = 1 - i
+            self._overflow[i].zero_()
+        pos_g = self._pair_graph(batch, pos_l, node_ids, static)
+        seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
+        blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
+                                            transposes=self.transposed_blocks,
+                                            static_shapes=static, node_cap_hint=hint,
+                                            overflow=self._overflow[i] if hint else None)
+        if hint is not None:
+            self._overflow_host[i].copy_(self._overflow[i], non_blocking=True)
+            flag = (self._overflow_host[i], torch.cuda.Event())
+            flag[1].record()
+        if learn:
+            self._learn_caps(blocks)
+        ready = None
+        if flag is not None:  # the hand-off event of a batch settled after the next one's
+            ready = torch.cuda.Event()  # kernels are queued: this batch's work only
+            ready.record()
+        return {"batch": batch, "pos_l": pos_l, "neg_l": neg_l, "node_ids": node_ids,
+                "counts": counts, "static": static, "exclude": exclude, "pos_g": pos_g,
+                "blocks": blocks, "flag": flag, "ready": ready}
+
+    def _pair_graph(self, batch, pos_l, node_ids, static):
+        pos_g = PairGraph(pos_l, node_ids)
+        pos_g.static = static
+        for ce, e in batch.items():
+            for k, v in self.g._edata[ce].items():
+                pos_g._edata[ce][k] = ops.gather_rows(v, e)
+            pos_g._edata[ce][EID] = e
+        return pos_g
+
+    def _settle(self, rec):
+        """The loader item of a made batch; a static batch that outgrew the learned
+        capacities is redone exactly (same pairs and negatives, fresh picks) and the
+        capacities grow."""
+        static, pos_g, blocks, node_ids = rec["static"], rec["pos_g"], rec["blocks"], rec["node_ids"]
+        self._handoff = rec["ready"]
+        if rec["flag"] is not None:
+            host, ev = rec["flag"]
+            ev.synchronize()
+            if int(host[0]):
                 self.static_redone += 1
                 self._node_hint = {k: -(-int(v * self.STATIC_MARGIN) // 1024) * 1024
                                    for k, v in self._node_hint.items()}
-                cnt = counts.tolist()
+                cnt = rec["counts"].tolist()
                 node_ids = {nt: v[:c] for (nt, v), c in zip(node_ids.items(), cnt)}
-                pos_g = PairGraph(pos_l, node_ids)
-                for ce, e in batch.items():
-                    for k, v in g._edata[ce].items():
-                        pos_g._edata[ce][k] = ops.gather_rows(v, e)
-                    pos_g._edata[ce][EID] = e
                 static = False
+                pos_g = self._pair_graph(rec["batch"], rec["pos_l"], node_ids, False)
                 seeds = {nt: v for nt, v in node_ids.items() if v.numel() > 0}
-                blocks = self.sampler.sample_blocks(self.g_sampling, seeds, exclude,
+                blocks = self.sampler.sample_blocks(self.g_sampling, seeds, rec["exclude"],
                                                     transposes=self.transposed_blocks)
-            if learn:
-                self._learn_caps(blocks)
-            # static: the real node count per type, on the device (the node lists hold -1
-            # past it)
-            pos_g.node_counts = dict(zip(g.ntypes, counts.unbind(0))) if static else None
-            pos_g.static = static
-            input_nodes = blocks[0].srcdata[NID]
-            if self.negative_sampler is None:
-                yield input_nodes, pos_g, blocks
-            else:
-                neg_g = PairGraph(neg_l, node_ids)
-                neg_g.static = static
-                if type(self.negative_sampler) is _Uniform:
-                    # every etype's negative sources are its positive sources repeated K times
-                    # (in local ids too: one relabel maps both): CosinePrediction.pair scores
-                    # them with the grouped launch
-                    neg_g.src_repeats_pos = self.negative_sampler.k
-                yield input_nodes, pos_g, neg_g, blocks
+                self._handoff = None  # the redo's work is the last queued
+        # static: the real node count per type, on the device (the node lists hold -1
+        # past it)
+        pos_g.node_counts = dict(zip(self.g.ntypes, rec["counts"].unbind(0))) if static else None
+        pos_g.static = static
+        input_nodes = blocks[0].srcdata[NID]
+        if self.negative_sampler is None:
+            return input_nodes, pos_g, blocks
+        neg_g = PairGraph(rec["neg_l"], node_ids)
+        neg_g.static = static
+        if type(self.negative_sampler) is _Uniform:
+            # every etype's negative sources are its positive sources repeated K times
+            # (in local ids too: one relabel maps both): CosinePrediction.pair scores
+            # them with the grouped launch
+            neg_g.src_repeats_pos = self.negative_sampler.k
+        return input_nodes, pos_g, neg_g, blocks

@@ -32,6 +32,7 @@
  *                                 apply_edges(fn.u_dot_v) src/model.py:317-327
  *                                 (DGL gsddmm -> _CAPI_DGLKernelSDDMM)
  *   - gnnrec_edge_mlp_f32      <- PredictingModule.forward src/model.py:290-305
+ *   - gnnrec_edge_mlp_grouped_f32 <- the same over negative_sampler.Uniform's pair graphs
  *   - gnnrec_sample_*          <- dgl.dataloading.MultiLayer{Full,}Neighbor-
  *                                 Sampler / to_block, src/sampling.py:153-161
  *                                 (_CAPI_DGLSampleNeighbors, _CAPI_DGLToBlock)
@@ -359,6 +360,15 @@ int gnnrec_sddmm_cos_grouped_f32(const int64_t* src_g, int64_t n_groups, const i
 int gnnrec_edge_mlp_f32(const int64_t* src, const int64_t* dst, int64_t n_edges,
                         const float* P, const float* Q, const float* W2, const float* b2,
                         const float* w3, const float* b3, float* out, void* stream);
+/* The same scores for negative_sampler.Uniform(K)'s pair graphs (src/sampling.py:163-165),
+ * grouped as gnnrec_sddmm_cos_grouped_f32: group g = source src_g[g], its positive edge to
+ * first[g] (may be NULL) -> out_first[g], and its K negatives to dst[g K + j] -> out[g K + j];
+ * the source's P row is read once per 256 edges.  The scores equal gnnrec_edge_mlp_f32's on
+ * the expanded edge lists (the same kernel body). */
+int gnnrec_edge_mlp_grouped_f32(const int64_t* src_g, int64_t n_groups, const int64_t* first,
+                                float* out_first, int64_t K, const int64_t* dst, float* out,
+                                const float* P, const float* Q, const float* W2, const float* b2,
+                                const float* w3, const float* b3, void* stream);
 
 /* ---- a9: block sampler (K8) ----------------------------------------------
  * Per relation, for each seed (dst) v: collect its in-edges from the global

@@ -1723,6 +1723,81 @@ def test_sddmm_cos_grouped_bitwise_equals_per_edge_and_oracle(d):
         np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
 
 
+def _mlp_tables(rng, n_s, n_d, d=64):
+    from gnnrec import ops
+    from gnnrec.nn import PredictingLayer
+    torch.manual_seed(1)
+    pl = PredictingLayer(d)
+    params = {k: v.numpy() for k, v in pl.state_dict().items()}
+    pl = pl.to(DEV).eval()
+    hs = rng.standard_normal((n_s, d)).astype(np.float32)
+    hd = rng.standard_normal((n_d, d)).astype(np.float32)
+    W1 = pl.hidden_1.weight.detach()
+    with torch.no_grad():
+        P = ops.gemm(_t(hs), W1[:, :d], bias=pl.hidden_1.bias)
+        Q = ops.gemm(_t(hd), W1[:, d:])
+    tail = (pl.hidden_2.weight.detach(), pl.hidden_2.bias.detach(),
+            pl.output.weight.detach().reshape(-1), pl.output.bias.detach())
+    return pl, params, hs, hd, P, Q, tail
+
+
+def test_edge_mlp_grouped_bitwise_equals_per_edge_and_oracle():
+    """a8 for negative_sampler.Uniform's pair graphs: the grouped launch (one P row per run
+    of 256 edges of one source) scores bitwise what the per-edge launch scores on the
+    expanded lists — the same LDS-staged body — and both match the oracle's
+    PredictingModule (src/model.py:290-305) on the concatenation form; K = 0 / 1 / tile
+    and work-item boundaries (32, 256 edges) / the reference's 2500, with and without the
+    positive edges."""
+    from gnnrec import ops
+    rng = np.random.default_rng(11)
+    pl, params, hs, hd, P, Q, tail = _mlp_tables(rng, 70, 900)
+    for G, K in ((13, 0), (13, 1), (9, 31), (9, 32), (9, 33), (5, 255), (5, 256), (3, 2500)):
+        src_g = rng.integers(0, 70, G)
+        first = rng.integers(0, 900, G)
+        dst = rng.integers(0, 900, G * K)
+        pos, neg = ops.edge_mlp_grouped(_t(src_g), _t(first), K, _t(dst), P, Q, *tail)
+        _, neg2 = ops.edge_mlp_grouped(_t(src_g), None, K, _t(dst), P, Q, *tail)
+        src = np.concatenate([src_g, np.repeat(src_g, K)])
+        dd = np.concatenate([first, dst])
+        ref = ops.edge_mlp(_t(src), _t(dd), P, Q, *tail)
+        assert torch.equal(pos, ref[:G]) and torch.equal(neg, ref[G:]), (G, K)
+        assert torch.equal(neg2, neg)
+        ora = oracle.predicting_module({("user", "buys", "item"): (src, dd)},
+                                       {"user": hs, "item": hd}, params)[("user", "buys", "item")]
+        np.testing.assert_allclose(torch.cat([pos, neg]).cpu().numpy(), ora[:, 0], rtol=RTOL,
+                                   atol=ATOL)
+
+
+@pytest.mark.parametrize("K", [40, 300, 8])
+def test_predicting_module_takes_the_grouped_launch_on_a_marked_negative_graph(K):
+    """PredictingModule.forward (no grad) on the loader's marked negative graph
+    (src_repeats_pos = K) scores with the grouped launch — the bits of the unmarked graph's
+    per-edge launch — and K < 32 (a partly filled 32-edge tile per run) stays per-edge."""
+    from gnnrec.graph import PairGraph
+    from gnnrec.nn import PredictingLayer, PredictingModule
+    rng = np.random.default_rng(12)
+    ce = ("user", "buys", "item")
+    n_u, n_i, G, d = 30, 60, 20, 64
+    ps = rng.integers(0, n_u, G)
+    nd = rng.integers(0, n_i, G * K)
+    nodes = {"user": _t(np.arange(n_u)), "item": _t(np.arange(n_i))}
+    torch.manual_seed(2)
+    mod = PredictingModule(PredictingLayer, d).to(DEV).eval()
+    h = {"user": _t(rng.standard_normal((n_u, d)).astype(np.float32)),
+         "item": _t(rng.standard_normal((n_i, d)).astype(np.float32))}
+    plain = PairGraph({ce: (_t(np.repeat(ps, K)), _t(nd))}, nodes)
+    marked = PairGraph({ce: (_t(np.repeat(ps, K)), _t(nd))}, nodes)
+    marked.src_repeats_pos = K
+    with torch.no_grad():
+        a = mod(plain, h)[ce]
+        b = mod(marked, h)[ce]
+    assert torch.equal(a, b)
+    params = {k[len("layer_nn."):]: v.cpu().numpy() for k, v in mod.state_dict().items()}
+    ora = oracle.predicting_module({ce: (np.repeat(ps, K), nd)},
+                                   {k: v.cpu().numpy() for k, v in h.items()}, params)[ce]
+    np.testing.assert_allclose(b.cpu().numpy(), ora, rtol=RTOL, atol=ATOL)
+
+
 @pytest.mark.parametrize("K,d", [(50, 64), (200, 128), (10, 40), (130, 200), (70, 256)])
 def test_cosine_pair_head_grouped_path_forward_and_gradients(K, d):
     """CosinePrediction.pair on a negative graph marked by the loader (src_repeats_pos = K)

@@ -36,7 +36,8 @@ RENAMED = {"gnnrec_gemm_rownorm_f32": "gemm", "gnnrec_gemm_tn_bias_f32": "gemm_t
            "gnnrec_sddmm_cos_backward_grouped_workspace_bytes":
                "sddmm_cos_backward_workspace_bytes",
            "gnnrec_sddmm_cos_grouped_f32": "sddmm_cos_grouped",
-           "gnnrec_edge_mlp_f32": "edge_mlp", "gnnrec_act_backward_f32": "act_backward",
+           "gnnrec_edge_mlp_f32": "edge_mlp", "gnnrec_edge_mlp_grouped_f32": "edge_mlp_grouped",
+           "gnnrec_act_backward_f32": "act_backward",
            "gnnrec_act_backward_normed_f32": "act_backward_normed",
            "gnnrec_lstm_step_f32": "lstm_step", "gnnrec_topk_rows_f32": "topk_rows",
            "gnnrec_lstm_step_save_f32": "lstm_step_save",
