@@ -20,3 +20,4 @@ void set_error(const char* fmt, ...) {
 extern "C" int gnnrec_version(void) { return 1; }
 
 extern "C" const char* gnnrec_last_error(void) { return gnnrec::g_err; }
+

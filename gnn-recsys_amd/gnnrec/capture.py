@@ -28,7 +28,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
-from .sampling import _tensors
+from .sampling import RNG_LOCK, _tensors
 
 
 def batch_is_static(batch) -> bool:
@@ -90,7 +90,9 @@ class CapturedTrainStep:
         self.opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        # a loader's sampling thread draws no negatives while the capture is under way
+        # (sampling.RNG_LOCK)
+        with RNG_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
             loss = self.loss_fn(self.model, batch)
             loss.backward()
             self.opt.step()

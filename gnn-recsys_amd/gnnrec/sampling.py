@@ -35,6 +35,12 @@ import torch
 from . import ops
 from .graph import Block, EID, HeteroGraph, LazyRows, NID, PairGraph
 
+# The loaders' draws from torch's default CUDA generator (negatives, an epoch's shuffle) and a
+# hipGraph capture (capture.CapturedTrainStep) exclude each other: while a capture is under
+# way torch refuses a draw from any stream that is not capturing ("Offset increment outside
+# graph capture"), and a sampling thread's draws are exactly that.
+RNG_LOCK = threading.RLock()
+
 
 def _mix(*xs) -> int:
     h = 0x9E3779B97F4A7C15
@@ -444,7 +450,8 @@ class _Uniform:
             ce = g.to_canonical_etype(ce)
             src, _ = g.find_edges(e, etype=ce)
             src = src.repeat_interleave(self.k)
-            dst = torch.randint(0, g.num_nodes(ce[2]), (src.numel(),), device=src.device)
+            with RNG_LOCK:
+                dst = torch.randint(0, g.num_nodes(ce[2]), (src.numel(),), device=src.device)
             out[ce] = (src, dst)
         return out
 
@@ -457,7 +464,8 @@ negative_sampler = _NegNS
 
 
 def _batches(n: int, batch_size: int, shuffle: bool, drop_last: bool, device):
-    order = torch.randperm(n, device=device) if shuffle else torch.arange(n, device=device)
+    with RNG_LOCK:
+        order = torch.randperm(n, device=device) if shuffle else torch.arange(n, device=device)
     stop = (n // batch_size) * batch_size if drop_last else n
     for i in range(0, stop, batch_size):
         yield order[i:i + batch_size]
@@ -742,7 +750,8 @@ class EdgeDataLoader:
         for ce, ps, _pd in pairs:
             if k:
                 ns = ps.unsqueeze(1).expand(ps.numel(), k).reshape(-1)
-                nd = torch.randint(0, g.num_nodes(ce[2]), (ns.numel(),), device=g.device)
+                with RNG_LOCK:
+                    nd = torch.randint(0, g.num_nodes(ce[2]), (ns.numel(),), device=g.device)
                 negs.append((ce, ns, nd))
         # per etype: positive sources, negative sources, positive dsts, negative dsts — the
         # local ids come back as consecutive views of one buffer, so an etype's positive and
@@ -818,11 +827,12 @@ class EdgeDataLoader:
         coo = [g._coo[ce] for ce in ces]
         rel = [self.sampler._relabeler(g, nt) for nt in nts]
         k = 0 if self.negative_sampler is None else self.negative_sampler.k
-        nodes, ps, pd, ns, nd = ops.edge_batch_pairs(
-            [c[0] for c in coo], [c[1] for c in coo], [tix[ce[0]] for ce in ces],
-            [tix[ce[2]] for ce in ces], [batch.get(ce, empty) for ce in ces],
-            [ces.index(ce) for ce in batch], k, [g.num_nodes(nt) for nt in nts],
-            [r.prefix_pos for r in rel], [r.mark for r in rel])
+        with RNG_LOCK:  # (its negatives: randint on the default generator)
+            nodes, ps, pd, ns, nd = ops.edge_batch_pairs(
+                [c[0] for c in coo], [c[1] for c in coo], [tix[ce[0]] for ce in ces],
+                [tix[ce[2]] for ce in ces], [batch.get(ce, empty) for ce in ces],
+                [ces.index(ce) for ce in batch], k, [g.num_nodes(nt) for nt in nts],
+                [r.prefix_pos for r in rel], [r.mark for r in rel])
         node_ids = dict(zip(nts, nodes))
         pos_l = {ce: (ps[i], pd[i]) for i, ce in enumerate(ces)}
         neg_l = {} if k == 0 else {ce: (ns[i], nd[i]) for i, ce in enumerate(ces)}

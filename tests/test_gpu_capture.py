@@ -375,3 +375,44 @@ def test_static_block_data_is_lazy_until_read():
                 table = g.edges[ce].data[k]
                 ref = table[eid.clamp(min=0)] * (eid >= 0).reshape((-1,) + (1,) * (table.dim() - 1))
                 assert torch.equal(f.get(k), ref.to(table.dtype)), (ce, k)
+
+
+def test_capture_beside_a_sampling_thread_drawing_negatives():
+    """A sampling thread drawing negatives from torch's default CUDA generator while the
+    training thread captures its step: torch refuses a draw from a non-capturing stream
+    during a capture ("Offset increment outside graph capture"), so the capture holds
+    sampling.RNG_LOCK and the loaders draw under it — no draw lands in the window."""
+    import threading
+    from gnnrec.capture import CapturedTrainStep
+    from gnnrec.sampling import negative_sampler
+    g, _ = _graph(n_u=300, n_i=120, e_b=4000, e_c=3000, min_deg=False)
+    batches = [b for b in _loader(g, True)][:3]
+    stop, errors, draws = threading.Event(), [], [0]
+
+    def draw():
+        neg = negative_sampler.Uniform(4)
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                while not stop.is_set():
+                    neg(g, {BUYS: torch.arange(64, device=DEV)})
+                    draws[0] += 1
+        except Exception as e:  # noqa: BLE001 — surfaced below
+            errors.append(e)
+
+    t = threading.Thread(target=draw, daemon=True)
+    t.start()
+    try:
+        for _ in range(3):
+            m = _model(g, agg="mean").train()
+            opt = torch.optim.Adam(m.parameters(), lr=0.01, fused=True)
+            step = CapturedTrainStep(m, opt, _loss(4), warmup=1)
+            for b in batches:
+                step(b)
+            assert step.captures == 1 and step.replays >= 1, \
+                (step.captures, step.replays, step.eager_steps)
+    finally:
+        stop.set()
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    assert draws[0] > 0
