@@ -27,6 +27,25 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // CDNA4 wavefront is 64 lanes.
 constexpr int kWave = 64;
 
+// Lane group g (of NPW groups of kWave / NPW consecutive lanes) receives lane (base + g)'s x,
+// base wave-uniform: NPW v_readlane (VALU -> SGPR) and selects, where __shfl is one
+// ds_bpermute through the LDS pipe per call.  Lane indices wrap at 64 (a group whose lane
+// is past the data ignores the value).
+template <int NPW>
+__device__ __forceinline__ int bcast_groups(int x, int base, int grp) {
+  int r = __builtin_amdgcn_readlane(x, base & 63);
+#pragma unroll
+  for (int g = 1; g < NPW; ++g) {
+    const int y = __builtin_amdgcn_readlane(x, (base + g) & 63);
+    r = grp == g ? y : r;
+  }
+  return r;
+}
+template <int NPW>
+__device__ __forceinline__ float bcast_groups(float x, int base, int grp) {
+  return __builtin_bit_cast(float, bcast_groups<NPW>(__builtin_bit_cast(int, x), base, grp));
+}
+
 // 64-bit counter hash (splitmix64 finaliser): the synthetic generator and the
 // Philox-free fanout sampler both key on it; oracle/oracle.c restates it.
 __host__ __device__ inline uint64_t mix64(uint64_t z) {

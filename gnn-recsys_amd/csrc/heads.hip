@@ -31,6 +31,30 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
 }
 
+// Sum over a lane group of LPR (16, 32 or 64) lanes by DPP adds — VALU only, where a
+// __shfl_xor tree is one ds_bpermute per level — valid in the group's LAST lane.  Each level
+// adds the same two partial sums the xor tree adds (quad_perm [1,0,3,2] / [2,3,0,1] pair the
+// xor-1 / xor-2 partners; after them a quad's lanes agree, so row_half_mirror and row_mirror
+// add the xor-4 / xor-8 partner's value; row_bcast15 / 31 add the lower row's / half's sum
+// to the upper one): the bits of the xor tree, which the u-norm reductions still use.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_add(float x) {
+  const int y = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROWS, 0xF, false);
+  return x + __builtin_bit_cast(float, y);
+}
+
+template <int LPR>
+__device__ __forceinline__ float group_sum_last(float x) {
+  static_assert(LPR == 16 || LPR == 32 || LPR == 64, "lane groups of 16, 32 or 64");
+  x = dpp_add<0xB1, 0xF>(x);   // quad_perm [1,0,3,2]
+  x = dpp_add<0x4E, 0xF>(x);   // quad_perm [2,3,0,1]
+  x = dpp_add<0x141, 0xF>(x);  // row_half_mirror
+  x = dpp_add<0x140, 0xF>(x);  // row_mirror
+  if constexpr (LPR >= 32) x = dpp_add<0x142, 0xA>(x);  // row_bcast15 into rows 1 and 3
+  if constexpr (LPR >= 64) x = dpp_add<0x143, 0xC>(x);  // row_bcast31 into rows 2 and 3
+  return x;
+}
+
 template <int LPR, int VEC>
 __global__ __launch_bounds__(256) void sddmm_cos_kernel(const int64_t* __restrict__ src,
                                                         const int64_t* __restrict__ dst,
@@ -66,13 +90,10 @@ __global__ __launch_bounds__(256) void sddmm_cos_kernel(const int64_t* __restric
         }
       }
     }
-#pragma unroll
-    for (int off = 1; off < LPR; off <<= 1) {
-      dot += __shfl_xor(dot, off);
-      su += __shfl_xor(su, off);
-      sv += __shfl_xor(sv, off);
-    }
-    if (eok && gl == 0) {
+    dot = group_sum_last<LPR>(dot);
+    su = group_sum_last<LPR>(su);
+    sv = group_sum_last<LPR>(sv);
+    if (eok && gl == LPR - 1) {
       const float nu = fmaxf(sqrtf(su), 1e-12f);
       const float nv = fmaxf(sqrtf(sv), 1e-12f);
       out[e] = dot / (nu * nv);
@@ -99,7 +120,7 @@ int launch_cos(const int64_t* src, const int64_t* dst, int64_t n, const float* H
 // chunk of one group's negatives and keeps h_u — its fragment in registers, its norm
 // reduced once — so every edge reads one gathered row (4d B) and its dst id, not two rows and
 // two ids, and the u norm is not recomputed K times.  Each value is formed exactly as
-// sddmm_cos_kernel forms it (same lane fragments, same xor tree, same final expression):
+// sddmm_cos_kernel forms it (same lane fragments, same reduction tree, same final expression):
 // the scores are bitwise those of the per-edge kernel.
 constexpr int kCosU = 16;      // edges in flight per lane group
 constexpr int kCosChunk = 64;  // negatives per wave (40 waves per group at K = 2500: the
@@ -137,32 +158,29 @@ __global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
       dot += dot4(a, b);
       sv += dot4(b, b);
     }
-#pragma unroll
-    for (int off = 1; off < LPR; off <<= 1) {
-      dot += __shfl_xor(dot, off);
-      sv += __shfl_xor(sv, off);
-    }
+    dot = group_sum_last<LPR>(dot);
+    sv = group_sum_last<LPR>(sv);
     const float nv = fmaxf(sqrtf(sv), 1e-12f);
-    return dot / (nu * nv);
+    return dot / (nu * nv);  // (valid in the group's last lane)
   };
   if (c == 0 && first != nullptr) {  // the group's positive edge
     const int64_t v = first[g];
     float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
     if (cok) b = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
     const float r = score(b, cok);
-    if (lane == 0) out_first[g] = r;
+    if (lane == LPR - 1) out_first[g] = r;
   }
   const int64_t e_beg = g * K + c * kCosChunk;
   const int64_t e_end = g * K + min<int64_t>(K, (c + 1) * kCosChunk);
-  // the chunk's ids in one coalesced load (lane l: the chunk's l-th edge)
-  const int64_t all_ids = e_beg + lane < e_end ? dst[e_beg + lane] : 0;
+  // the chunk's ids in one coalesced load (lane l: the chunk's l-th edge; row ids < 2^31)
+  const int all_ids = e_beg + lane < e_end ? (int)dst[e_beg + lane] : 0;
   for (int64_t e0 = e_beg; e0 < e_end; e0 += STEP) {
-    const int64_t id = STEP == kCosChunk ? all_ids : __shfl(all_ids, (int)(e0 - e_beg) + lane);
+    const int id = STEP == kCosChunk ? all_ids : __shfl(all_ids, (int)(e0 - e_beg) + lane);
     float4 b[kCosU];
 #pragma unroll
     for (int k = 0; k < kCosU; ++k) {
       const int slot = k * NPW + grp;
-      const int64_t v = __shfl(id, slot);
+      const int64_t v = bcast_groups<NPW>(id, k * NPW, grp);
       b[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (cok && e0 + slot < e_end) b[k] = *reinterpret_cast<const float4*>(Hd + v * ldd + col);
     }
@@ -170,7 +188,7 @@ __global__ __launch_bounds__(256) void sddmm_cos_grouped_kernel(
     for (int k = 0; k < kCosU; ++k) {
       const int64_t e = e0 + k * NPW + grp;
       const float r = score(b[k], cok && e < e_end);
-      if (gl == 0 && e < e_end) out[e] = r;
+      if (gl == LPR - 1 && e < e_end) out[e] = r;
     }
   }
 }
@@ -252,8 +270,8 @@ __device__ __forceinline__ void mlp_load(const float4* __restrict__ Q4,
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int row = 2 * (i0 + i) + h;
-    const int vr = __shfl(v, row);
-    const int ur = GROUPED ? 0 : __shfl(u, row);  // (outside the branch: every lane shuffles)
+    const int vr = bcast_groups<2>(v, 2 * (i0 + i), h);
+    const int ur = GROUPED ? 0 : bcast_groups<2>(u, 2 * (i0 + i), h);
     const int j = r ^ (row & 15);
     q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (!GROUPED) p[i] = q[i];

@@ -280,24 +280,24 @@ __global__ __launch_bounds__(256) void cos_bwd_chunk_kernel(
   auto edge_of = [&](int64_t q) { return q == 0 ? g : G + g * K + (q - 1); };
   // the chunk's ids and weights g_e inv_t in one load per lane (lane l: edge q0 + l), so the
   // gathers below wait on one id load, not one per step of U edges
-  int64_t my_t = 0;
+  int my_t = 0;  // (row ids < 2^31)
   float my_w = 0.f;
   if (q0 + lane < q1) {
     const int64_t e = edge_of(q0 + lane);
-    my_t = dst[e];
+    my_t = (int)dst[e];
     my_w = grad[e] * inv_d[my_t];
   }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   // lane group grp sums edges q0 + grp, q0 + grp + NPW, ... in increasing order
-  for (int qo = grp; qo < kCosBwdChunk && q0 + qo - grp < q1; qo += NPW * U) {
+  for (int qb = 0; qb < kCosBwdChunk && q0 + qb < q1; qb += NPW * U) {
+    const int qo = qb + grp;
     float4 v[U];
     float w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int slot = qo + u * NPW;  // this group's edge q0 + slot (uniform per group)
-      const int src_lane = slot < kWave ? slot : 0;
-      const int64_t t = __shfl(my_t, src_lane);
-      w[u] = __shfl(my_w, src_lane);
+      const int64_t t = bcast_groups<NPW>(my_t, qb + u * NPW, grp);
+      w[u] = bcast_groups<NPW>(my_w, qb + u * NPW, grp);
       const bool ok = slot < kCosBwdChunk && q0 + slot < q1;
       v[u] = cok && ok ? *reinterpret_cast<const float4*>(Hd + t * ldd + col)
                        : make_float4(0.f, 0.f, 0.f, 0.f);
