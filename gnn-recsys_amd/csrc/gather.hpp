@@ -50,6 +50,15 @@ __device__ __forceinline__ void store_frag(float* p, const Frag<VEC>& f) {
   }
 }
 
+// A gather step's per-edge source index (and weight) to each lane group: lane group grp
+// takes the range's edge base + grp, held by that lane of the index load.
+// (readlane + select: at C4 the same pass time as __shfl's ds_bpermute, 142.56 ms both,
+// with the LDS pipe left free; profiles/r06ad_c4_gather_readlane_ab.txt)
+template <int NPI, typename T>
+__device__ __forceinline__ T edge_bcast(T x, int base, int grp) {
+  return bcast_groups<NPI>(x, base, grp);
+}
+
 template <int REDUCE>
 __device__ __forceinline__ float combine(float a, float b) {
   return REDUCE == GNNREC_REDUCE_MAX ? fmaxf(a, b) : a + b;
@@ -80,7 +89,7 @@ __device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
       for (int u = 0; u < UNROLL; ++u) {
         const int k = j + u * NPI + grp;
         ok[u] = (k < cnt) && colok;
-        const int src = __shfl(myidx, k & 63);
+        const int src = edge_bcast<NPI>(myidx, j + u * NPI, grp);
         if (ok[u]) {
           load_frag<VEC>(val[u], X + (int64_t)src * ldx + col);
         } else {
@@ -91,7 +100,7 @@ __device__ __forceinline__ void gather_range(int64_t beg, int64_t end,
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         float w = 1.f;
-        if constexpr (WEIGHTED) w = __shfl(myw, (j + u * NPI + grp) & 63);
+        if constexpr (WEIGHTED) w = edge_bcast<NPI>(myw, j + u * NPI, grp);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           const float m = WEIGHTED ? val[u].v[v] * w : val[u].v[v];

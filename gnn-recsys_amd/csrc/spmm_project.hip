@@ -395,7 +395,7 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
             for (int u = 0; u < U; ++u) {
               const int k = j + u * NPI + grp;
               ok[r][u] = k < dg[r];
-              const int src = __shfl(ridx[r], k & 63);
+              const int src = edge_bcast<NPI>(ridx[r], j + u * NPI, grp);
               if (ok[r][u]) {
                 load_frag<VEC>(val[r][u], X + (int64_t)src * ldx + col);
               } else {
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kMWaves * 64, 4) void spmm_project_mfma_kernel(
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               float w = 1.f;
-              if constexpr (WEIGHTED) w = __shfl(rwt[r], (j + u * NPI + grp) & 63);
+              if constexpr (WEIGHTED) w = edge_bcast<NPI>(rwt[r], j + u * NPI, grp);
 #pragma unroll
               for (int v = 0; v < VEC; ++v) {
                 const float m = WEIGHTED ? val[r][u].v[v] * w : val[r][u].v[v];
@@ -858,7 +858,7 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
         for (int u = 0; u < U; ++u) {
           const int k = j + u * NPI + grp;
           ok[u] = k < cnt;
-          const int src = __shfl(myidx, k & 63);
+          const int src = edge_bcast<NPI>(myidx, j + u * NPI, grp);
           if (ok[u]) {
             if constexpr (NTR) {
               const float4 t = ld_stream4(r.Y + (int64_t)src * r.ldy + col);
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(kP2Waves * 64) void spmm_project2_pipe_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           float w = 1.f;
-          if constexpr (W) w = __shfl(myw, (j + u * NPI + grp) & 63);
+          if constexpr (W) w = edge_bcast<NPI>(myw, j + u * NPI, grp);
 #pragma unroll
           for (int v = 0; v < VEC; ++v) acc.v[v] += W ? val[u].v[v] * w : val[u].v[v];
         }

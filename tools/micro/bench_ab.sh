@@ -9,6 +9,6 @@ for rep in 1 2 3; do
       timeout -k 10 200 python bench.py --cpu-baseline off "$@" 2>/dev/null
     else
       GNNREC_LIB=$lib timeout -k 10 200 python bench.py --cpu-baseline off "$@" 2>/dev/null
-    fi | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(round(d['ms_per_step'],2), round(r['launch_ms'],3), round(r.get('launch_ms_spmm_project') or 0,3), round(r.get('launch_ms_spmm') or 0, 3))" || exit 1
+    fi | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(round(d['ms_per_step'],2), round(r.get('launch_ms_spmm_tile') or 0,3), round(r.get('launch_ms_spmm_project') or 0,3))" || exit 1
   done
 done
