@@ -5,15 +5,16 @@
 // runs; the CSR keeps the edges of a row in edge-id order.  Here: per pass of DB key bits
 // (radix_plan: the fewest passes of at most 10 bits, then the narrowest digit that many
 // passes need — 17-bit keys in 2 passes of 9, 20-bit in 2 of 10, 24-bit in 3 of 8),
-//   radix_hist    one 256-thread block per 2048-edge tile counts the tile's digits,
+//   radix_hist    one 256-thread block per tile (4096 edges, 2048 below 512 such tiles) counts
+//                 the tile's digits,
 //                 stored digit-major [2^DB][tiles];
 //   scan          exclusive scan of that table (gnnrec_exclusive_scan_i32): the first
 //                 output position of every (digit, tile);
-//   radix_scatter each wave ranks its 512 edges, 64 at a time, by digit: DB ballots give
-//                 the lanes holding the same digit, mbcnt the rank among them, and an LDS
-//                 counter per (wave, digit) the edges of earlier rounds — so equal digits
-//                 keep their input order (stable), then writes key and value at
-//                 tile offset + earlier waves' counts + rank.
+//   radix_scatter each wave ranks its quarter of the tile, 64 edges at a time, by digit: DB
+//                 ballots give the lanes holding the same digit, mbcnt the rank among them,
+//                 and an LDS counter per (wave, digit) the edges of earlier rounds — so
+//                 equal digits keep their input order (stable); the tile is placed in LDS
+//                 in output order and written out by consecutive threads (runs of a digit).
 // The final pass writes the CSR directly (indices = src[e], eids = e), and the row
 // pointers come from the sorted keys' run boundaries.  Bytes per edge per pass: 4 (hist)
 // + 8 read + 8 written (scatter) + 12 · 2^DB / 2048 for the digit table and its scan;
@@ -26,8 +27,13 @@ namespace gnnrec {
 namespace {
 
 constexpr int kRT = 256;                 // threads per tile block
-constexpr int kRRounds = 8;              // 64-edge rounds per wave
-constexpr int kRTile = kRT * kRRounds;   // edges per tile
+// 64-edge rounds per wave: 16 (4096-edge tiles: the scatter writes longer runs) when that
+// still gives at least 512 tiles, else 8 (2048-edge tiles: enough blocks for the chip)
+inline int radix_rounds(int64_t E) { return (E + kRT * 16 - 1) / (kRT * 16) >= 512 ? 16 : 8; }
+inline int64_t radix_tiles(int64_t E) {
+  const int64_t tile = (int64_t)kRT * radix_rounds(E);
+  return (E + tile - 1) / tile;
+}
 constexpr int kMaxDigitBits = 10;
 
 constexpr size_t kAlign = 256;
@@ -51,7 +57,7 @@ inline unsigned tile_grid(int64_t n_tiles) {
   return (unsigned)(g < 1 ? 1 : g);
 }
 
-template <class K, int DB>
+template <class K, int DB, int RR>
 __global__ __launch_bounds__(kRT) void radix_hist_kernel(const K* __restrict__ keys, int64_t E,
                                                          int shift, int64_t n_tiles,
                                                          int32_t* __restrict__ hist) {
@@ -62,9 +68,9 @@ __global__ __launch_bounds__(kRT) void radix_hist_kernel(const K* __restrict__ k
 #pragma unroll
     for (int d = tid; d < ND; d += kRT) cnt[d] = 0;
     __syncthreads();
-    const int64_t base = t * kRTile;
+    const int64_t base = t * (kRT * RR);
 #pragma unroll
-    for (int j = 0; j < kRRounds; ++j) {
+    for (int j = 0; j < RR; ++j) {
       const int64_t i = base + j * kRT + tid;
       if (i < E) atomicAdd(&cnt[((uint32_t)keys[i] >> shift) & (ND - 1)], 1);
     }
@@ -76,26 +82,37 @@ __global__ __launch_bounds__(kRT) void radix_hist_kernel(const K* __restrict__ k
 }
 
 // MODE 0: keys_out / vals_out; MODE 1: keys_out + the CSR gather (idx_out, eid_out)
-// (positions fit int32: E < 2^31, radix_sort_rows)
-template <class K, bool VIN, int MODE, int DB>
+// (positions fit int32: E < 2^31, radix_sort_rows).  The tile's edges are first placed in
+// LDS in their output order (digit-major, stable), then written out by consecutive threads:
+// a digit's edges of the tile land in consecutive lanes, so a wave-instruction writes runs
+// of the output instead of one 4-B store per digit region per lane.
+template <class K, bool VIN, int MODE, int DB, int RR>
 __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
     const K* __restrict__ keys, const int32_t* __restrict__ vals, int64_t E, int shift,
     int64_t n_tiles, const int64_t* __restrict__ offs, uint32_t* __restrict__ keys_out,
     int32_t* __restrict__ vals_out, const int64_t* __restrict__ src,
     int32_t* __restrict__ idx_out, int64_t* __restrict__ eid_out) {
   constexpr int ND = 1 << DB;
-  // per (wave, digit): the wave's running count, then (in place) its first output position
-  __shared__ int cnt[kRT / kWave][ND];
+  constexpr int NW = kRT / kWave;
+  constexpr int PER = ND / kRT;  // digits per thread in the tile's digit scan (DB >= 8)
+  static_assert(PER >= 1 && ND % kRT == 0, "at least one digit per thread");
+  // per (wave, digit): the wave's running count, then (in place) its first tile position
+  __shared__ int cnt[NW][ND];
+  __shared__ int gbase[ND];        // a digit's first output position minus its first tile position
+  constexpr int kRTile = kRT * RR;  // edges per tile
+  __shared__ uint32_t skey[kRTile];
+  __shared__ int32_t sval[kRTile];
+  __shared__ int wtot[NW];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
   for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-    for (int i = tid; i < (kRT / kWave) * ND; i += kRT) cnt[i / ND][i % ND] = 0;
+    for (int i = tid; i < NW * ND; i += kRT) cnt[i / ND][i % ND] = 0;
     __syncthreads();
-    const int64_t base = t * kRTile + (int64_t)w * (kRRounds * kWave);
-    uint32_t kk[kRRounds];
-    int32_t vv[kRRounds];
-    uint32_t dr[kRRounds];  // digit << 16 | rank among the wave's edges of that digit
+    const int64_t base = t * kRTile + (int64_t)w * (RR * kWave);
+    uint32_t kk[RR];
+    int32_t vv[RR];
+    uint32_t dr[RR];  // digit << 16 | rank among the wave's edges of that digit
 #pragma unroll
-    for (int j = 0; j < kRRounds; ++j) {
+    for (int j = 0; j < RR; ++j) {
       const int64_t i = base + j * kWave + lane;
       const bool act = i < E;
       const uint32_t k = act ? (uint32_t)keys[i] : 0u;
@@ -117,11 +134,29 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
       dr[j] = (d << 16) | (uint32_t)(old + (int)r);
     }
     __syncthreads();
-    // per digit: the tile's first position, then each wave's after the earlier waves'
-    for (int d = tid; d < ND; d += kRT) {
-      int run = (int)offs[(int64_t)d * n_tiles + t];
+    // the tile's digit starts: thread tid owns digits [tid PER, tid PER + PER); an exclusive
+    // scan of the owners' totals over the block gives each its first tile position
+    int own = 0;
 #pragma unroll
-      for (int ww = 0; ww < kRT / kWave; ++ww) {
+    for (int k = 0; k < PER; ++k)
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) own += cnt[ww][tid * PER + k];
+    int inc = own;  // inclusive scan within the wave
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    if (lane == kWave - 1) wtot[w] = inc;
+    __syncthreads();
+    int run = inc - own;
+    for (int ww = 0; ww < w; ++ww) run += wtot[ww];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int d = tid * PER + k;
+      gbase[d] = (int)offs[(int64_t)d * n_tiles + t] - run;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) {
         const int c = cnt[ww][d];
         cnt[ww][d] = run;
         run += c;
@@ -129,16 +164,26 @@ __global__ __launch_bounds__(kRT) void radix_scatter_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kRRounds; ++j) {
+    for (int j = 0; j < RR; ++j) {
       const int64_t i = base + j * kWave + lane;
       if (i >= E) continue;
-      const int64_t p = (int64_t)cnt[w][dr[j] >> 16] + (dr[j] & 0xffff);
-      if (keys_out) keys_out[p] = kk[j];
+      const int q = cnt[w][dr[j] >> 16] + (int)(dr[j] & 0xffff);
+      skey[q] = kk[j];
+      sval[q] = vv[j];
+    }
+    __syncthreads();
+    const int64_t rem = E - t * kRTile;
+    const int n_here = rem < kRTile ? (int)rem : kRTile;
+    for (int q = tid; q < n_here; q += kRT) {
+      const uint32_t k = skey[q];
+      const int32_t v = sval[q];
+      const int64_t p = (int64_t)gbase[(k >> shift) & (ND - 1)] + q;
+      if (keys_out) keys_out[p] = k;
       if (MODE == 0) {
-        vals_out[p] = vv[j];
+        vals_out[p] = v;
       } else {
-        idx_out[p] = (int32_t)src[vv[j]];
-        eid_out[p] = vv[j];
+        idx_out[p] = (int32_t)src[v];
+        eid_out[p] = v;
       }
     }
     __syncthreads();
@@ -183,19 +228,19 @@ inline unsigned flat_grid(int64_t n) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
-template <class K, int DB>
+template <class K, int DB, int RR>
 void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64_t n_tiles,
                  int32_t* hist, int64_t* offs, void* scan_ws, uint32_t* k_out, int32_t* v_out,
                  const CsrGather* g, hipStream_t s) {
   const unsigned grid = tile_grid(n_tiles);
-  hipLaunchKernelGGL((radix_hist_kernel<K, DB>), dim3(grid), dim3(kRT), 0, s, keys, E, shift,
+  hipLaunchKernelGGL((radix_hist_kernel<K, DB, RR>), dim3(grid), dim3(kRT), 0, s, keys, E, shift,
                      n_tiles, hist);
   (void)gnnrec_exclusive_scan_i32(hist, ((int64_t)1 << DB) * n_tiles, offs, scan_ws, s);
   const int64_t* src = g ? g->src : nullptr;
   int32_t* idx = g ? g->idx_out : nullptr;
   int64_t* eid = g ? g->eid_out : nullptr;
 #define GNNREC_SCATTER(VIN, MODE)                                                        \
-  hipLaunchKernelGGL((radix_scatter_kernel<K, VIN, MODE, DB>), dim3(grid), dim3(kRT), 0, s, \
+  hipLaunchKernelGGL((radix_scatter_kernel<K, VIN, MODE, DB, RR>), dim3(grid), dim3(kRT), 0, s, \
                      keys, vals, E, shift, n_tiles, offs, k_out, v_out, src, idx, eid)
   if (g) {
     if (vals) GNNREC_SCATTER(true, 1);
@@ -207,23 +252,35 @@ void launch_pass(const K* keys, const int32_t* vals, int64_t E, int shift, int64
 #undef GNNREC_SCATTER
 }
 
-template <class K>
+template <class K, int RR>
 void launch_pass_bits(int bits, const K* keys, const int32_t* vals, int64_t E, int shift,
                       int64_t n_tiles, int32_t* hist, int64_t* offs, void* scan_ws,
                       uint32_t* k_out, int32_t* v_out, const CsrGather* g, hipStream_t s) {
   if (bits == 8)
-    launch_pass<K, 8>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+    launch_pass<K, 8, RR>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
   else if (bits == 9)
-    launch_pass<K, 9>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+    launch_pass<K, 9, RR>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
   else
-    launch_pass<K, 10>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+    launch_pass<K, 10, RR>(keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out, v_out, g, s);
+}
+
+template <class K>
+void launch_pass_tiles(int bits, const K* keys, const int32_t* vals, int64_t E, int shift,
+                       int64_t n_tiles, int32_t* hist, int64_t* offs, void* scan_ws,
+                       uint32_t* k_out, int32_t* v_out, const CsrGather* g, hipStream_t s) {
+  if (radix_rounds(E) == 16)
+    launch_pass_bits<K, 16>(bits, keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out,
+                            v_out, g, s);
+  else
+    launch_pass_bits<K, 8>(bits, keys, vals, E, shift, n_tiles, hist, offs, scan_ws, k_out,
+                           v_out, g, s);
 }
 
 }  // namespace
 
 size_t radix_ws_bytes(int64_t E, int64_t n_rows) {
   if (E <= 0) return 0;
-  const int64_t n_tiles = (E + kRTile - 1) / kRTile;
+  const int64_t n_tiles = radix_tiles(E);
   const int64_t n_hist = ((int64_t)1 << radix_plan(n_rows).bits) * n_tiles;
   return 4 * align_up((size_t)E * 4)                            // two (key, value) buffers
          + align_up((size_t)n_hist * 4)                         // per-tile digit counts
@@ -248,7 +305,7 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
   GNNREC_REQUIRE(ws_bytes >= radix_ws_bytes(E, n_rows), "radix sort: workspace %zu < %zu bytes",
                  ws_bytes, radix_ws_bytes(E, n_rows));
   const RadixPlan plan = radix_plan(n_rows);
-  const int64_t n_tiles = (E + kRTile - 1) / kRTile;
+  const int64_t n_tiles = radix_tiles(E);
   const int64_t n_hist = ((int64_t)1 << plan.bits) * n_tiles;
   char* p = static_cast<char*>(ws);
   const size_t slot = align_up((size_t)E * 4);
@@ -266,14 +323,14 @@ int radix_sort_rows(const void* keys_in, bool keys64, const int32_t* vals_in, in
     const CsrGather* gg = last ? g : nullptr;
     if (ps == 0) {
       if (keys64)
-        launch_pass_bits(bits, static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles,
-                         hist, offs, scan_ws, k_out, v_out, gg, s);
+        launch_pass_tiles(bits, static_cast<const int64_t*>(keys_in), vals_in, E, 0, n_tiles,
+                          hist, offs, scan_ws, k_out, v_out, gg, s);
       else
-        launch_pass_bits(bits, static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles,
-                         hist, offs, scan_ws, k_out, v_out, gg, s);
+        launch_pass_tiles(bits, static_cast<const int32_t*>(keys_in), vals_in, E, 0, n_tiles,
+                          hist, offs, scan_ws, k_out, v_out, gg, s);
     } else {
-      launch_pass_bits(bits, (const uint32_t*)kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, bits * ps,
-                       n_tiles, hist, offs, scan_ws, k_out, v_out, gg, s);
+      launch_pass_tiles(bits, (const uint32_t*)kb[(ps - 1) & 1], vb[(ps - 1) & 1], E, bits * ps,
+                        n_tiles, hist, offs, scan_ws, k_out, v_out, gg, s);
     }
   }
   if (row_ptr)
