@@ -2,7 +2,7 @@
 # round 6 final tree (a): the GPU suite, smoke, and the default bench line with the C4
 # one-GPU digest recorded into a copy of the committed digest file
 set -o pipefail
-O=gpurun_out/r06fin
+O=gpurun_out/${TAG:-r06fin}
 mkdir -p $O
 cp profiles/p1_output_digests.json $O/p1_digests.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || { echo "gpu tests failed"; tail -60 $O/gputest.log; exit 1; }

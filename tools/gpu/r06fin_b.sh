@@ -3,7 +3,7 @@
 # gpurun_out/r06fin/p1_digests.json), the driver's 8-GPU command rehearsed with 8 gloo ranks
 # on this GPU against them, and every rank's compute share of C4 at P = 1/2/4/8
 set -o pipefail
-O=gpurun_out/r06fin
+O=gpurun_out/${TAG:-r06fin}
 mkdir -p $O
 SMALL="--users 1000000 --items 100000 --edges 50000000"
 timeout -k 10 300 python -u bench.py $SMALL --steps 3 --warmup 1 --minibatch off --cpu-baseline off \
