@@ -39,6 +39,18 @@ def test_csr_build_matches_oracle(E, n_dst):
     _check(src, dst, n_dst)
 
 
+@pytest.mark.parametrize("E,n_dst", [(2_097_151, 100_000), (2_097_152, 100_000),
+                                     (2_097_153, 1_100_000)])
+def test_csr_build_across_the_tile_size_switch(E, n_dst):
+    """The scatter's tile grows from 2048 to 4096 edges at 512 tiles of 4096 (E = 2^21): both
+    sides of the switch build the oracle's CSR, bit for bit (9- and 10/11-bit digits)."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(E)
+    src = torch.randint(0, 1 << 20, (E,), device=DEV, generator=g)
+    dst = torch.randint(0, n_dst, (E,), device=DEV, generator=g)
+    _check(src, dst, n_dst)
+
+
 def test_csr_build_skewed_and_sorted_inputs():
     """one heavy row (half of all edges), already-sorted and reverse-sorted dst ids"""
     n, E = 50_000, 1_000_000
